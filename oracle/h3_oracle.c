@@ -1,0 +1,504 @@
+/*
+ * ORACLE -- test infrastructure only. Never linked into, loaded by or called from the product path
+ * (real-time-mobility-heatmap_amd/). Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+ *
+ * CPU restatement of the H3 v4 cell-indexing path the reference runs per row:
+ *   reference heatmap_stream.py:65-75  to_h3(lat, lon) -> h3.latlng_to_cell(lat, lon, H3_RES)   (h3-py 4.x)
+ *   h3-py _cy/latlng.pyx latlng_to_cell -> deg2coord (degsToRads) -> H3 C latLngToCell
+ * Upstream H3 C v4 (third-party, unpinned by the reference: README.md:95; absent from this image) is
+ * restated function by function below, names kept: degsToRads, _geoToVec3d, _pointSquareDist,
+ * _geoToClosestFace, _geoAzimuthRads, _posAngleRads, _geoToHex2d, _hex2dToCoordIJK, _ijkNormalize,
+ * _upAp7/_upAp7r, _downAp7/_downAp7r, _unitIjkToDigit, _faceIjkToH3, _h3Rotate60ccw/cw,
+ * _h3RotatePent60ccw.  Upstream's `long double` constants (…L literals) are kept as long double so gcc on
+ * x86-64 evaluates them in x87 extended precision exactly like the compiled h3 library does.
+ * Compile with -O2 -ffp-contract=off (no FMA contraction; x86-64 SSE2 doubles), link glibc libm.
+ *
+ * Also restates the inverse (cellToLatLng: _h3ToFaceIjk, _adjustOverageClassII, _faceIjkToGeo) used ONLY
+ * to validate the tables by round trip (latLngToCell(cellToLatLng(c)) == c).
+ *
+ * Parity status: UNPINNED against h3-py (not importable here; the reference ships no fixtures).  Anchors:
+ * three public known-answer vectors from upstream READMEs, round-trip and table self-consistency checks.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#define H3T_CONST static const
+#include "../real-time-mobility-heatmap_amd/csrc/h3_tables.inc"
+
+/* upstream constants.h / coordijk.h (v4) */
+#define M_PI_180 0.0174532925199432957692369076848861271111L
+#define M_180_PI 57.29577951308232087679815481410517033240547L
+#define M_2PI 6.28318530717958647692528676655900576839433L
+#define EPSILON 0.0000000000000001L
+#define M_SQRT3_2 0.8660254037844386467637231707529361834714L
+#define M_AP7_ROT_RADS 0.333473172251832115336090755351601070065900389L
+#define RES0_U_GNOMONIC 0.38196601125010500003
+#define INV_RES0_U_GNOMONIC 2.61803398874989588842
+#define M_SQRT7 2.6457513110645905905016157536392604257102L
+#define M_RSQRT7 0.37796447300922722721451653623418006081576L
+#define M_RSIN60 1.1547005383792515290182975610039149112953L
+#define M_ONESEVENTH 0.14285714285714285714285714285714285L
+#define M_ONETHIRD 0.333333333333333333333333333333333333333L
+#define MAX_H3_RES 15
+#define MAX_FACE_COORD 2
+#define H3_INIT UINT64_C(0x00001fffffffffff)
+
+typedef struct { double lat, lng; } LatLng;
+typedef struct { double x, y, z; } Vec3d;
+typedef struct { double x, y; } Vec2d;
+typedef struct { int i, j, k; } CoordIJK;
+typedef struct { int face; CoordIJK coord; } FaceIJK;
+
+enum { CENTER_DIGIT = 0, K_AXES_DIGIT = 1, J_AXES_DIGIT = 2, JK_AXES_DIGIT = 3, I_AXES_DIGIT = 4,
+       IK_AXES_DIGIT = 5, IJ_AXES_DIGIT = 6, INVALID_DIGIT = 7 };
+
+#define GET_RES(h) ((int)(((h) >> 52) & 0xf))
+#define GET_BC(h) ((int)(((h) >> 45) & 0x7f))
+#define GET_DIGIT(h, r) ((int)(((h) >> ((MAX_H3_RES - (r)) * 3)) & 7))
+#define SET_DIGIT(h, r, d) \
+    (h) = (((h) & ~(UINT64_C(7) << ((MAX_H3_RES - (r)) * 3))) | ((uint64_t)(d) << ((MAX_H3_RES - (r)) * 3)))
+
+static double degsToRads(double degrees) { return degrees * M_PI_180; }
+static double radsToDegs(double radians) { return radians * M_180_PI; }
+
+static double _posAngleRads(double rads) {
+    double tmp = ((rads < 0.0L) ? rads + M_2PI : rads);
+    if (rads >= M_2PI) tmp -= M_2PI;
+    return tmp;
+}
+
+static void _geoToVec3d(const LatLng *geo, Vec3d *v) {
+    double r = cos(geo->lat);
+    v->z = sin(geo->lat);
+    v->x = cos(geo->lng) * r;
+    v->y = sin(geo->lng) * r;
+}
+
+static double _square(double x) { return x * x; }
+
+static double _pointSquareDist(const Vec3d *v1, const Vec3d *v2) {
+    return _square(v1->x - v2->x) + _square(v1->y - v2->y) + _square(v1->z - v2->z);
+}
+
+static void _geoToClosestFace(const LatLng *g, int *face, double *sqd) {
+    Vec3d v3d;
+    _geoToVec3d(g, &v3d);
+    *face = 0;
+    *sqd = 5.0;
+    for (int f = 0; f < H3T_NUM_FACES; ++f) {
+        Vec3d c = {H3T_faceCenterPoint[f][0], H3T_faceCenterPoint[f][1], H3T_faceCenterPoint[f][2]};
+        double sqdT = _pointSquareDist(&c, &v3d);
+        if (sqdT < *sqd) {
+            *face = f;
+            *sqd = sqdT;
+        }
+    }
+}
+
+static double _geoAzimuthRads(const LatLng *p1, const LatLng *p2) {
+    return atan2(cos(p2->lat) * sin(p2->lng - p1->lng),
+                 cos(p1->lat) * sin(p2->lat) - sin(p1->lat) * cos(p2->lat) * cos(p2->lng - p1->lng));
+}
+
+static int isResolutionClassIII(int r) { return r % 2; }
+
+static void _geoToHex2d(const LatLng *g, int res, int *face, Vec2d *v) {
+    double sqd;
+    _geoToClosestFace(g, face, &sqd);
+    double r = acos(1 - sqd / 2);
+    if (r < EPSILON) {
+        v->x = v->y = 0.0;
+        return;
+    }
+    LatLng fc = {H3T_faceCenterGeo[*face][0], H3T_faceCenterGeo[*face][1]};
+    double theta = _posAngleRads(H3T_faceAxesAzRadsCII[*face][0] - _posAngleRads(_geoAzimuthRads(&fc, g)));
+    if (isResolutionClassIII(res)) theta = _posAngleRads(theta - M_AP7_ROT_RADS);
+    r = tan(r);
+    r *= INV_RES0_U_GNOMONIC;
+    for (int i = 0; i < res; i++) r *= M_SQRT7;
+    v->x = r * cos(theta);
+    v->y = r * sin(theta);
+}
+
+static void _ijkNormalize(CoordIJK *c) {
+    if (c->i < 0) { c->j -= c->i; c->k -= c->i; c->i = 0; }
+    if (c->j < 0) { c->i -= c->j; c->k -= c->j; c->j = 0; }
+    if (c->k < 0) { c->i -= c->k; c->j -= c->k; c->k = 0; }
+    int min = c->i;
+    if (c->j < min) min = c->j;
+    if (c->k < min) min = c->k;
+    if (min > 0) { c->i -= min; c->j -= min; c->k -= min; }
+}
+
+static void _hex2dToCoordIJK(const Vec2d *v, CoordIJK *h) {
+    double a1, a2, x1, x2, r1, r2;
+    int m1, m2;
+    h->k = 0;
+    a1 = fabsl(v->x);
+    a2 = fabsl(v->y);
+    x2 = a2 * M_RSIN60;
+    x1 = a1 + x2 / 2.0;
+    m1 = x1;
+    m2 = x2;
+    r1 = x1 - m1;
+    r2 = x2 - m2;
+    if (r1 < 0.5) {
+        if (r1 < 1.0 / 3.0) {
+            if (r2 < (1.0 + r1) / 2.0) { h->i = m1; h->j = m2; }
+            else { h->i = m1; h->j = m2 + 1; }
+        } else {
+            if (r2 < (1.0 - r1)) h->j = m2; else h->j = m2 + 1;
+            if ((1.0 - r1) <= r2 && r2 < (2.0 * r1)) h->i = m1 + 1; else h->i = m1;
+        }
+    } else {
+        if (r1 < 2.0 / 3.0) {
+            if (r2 < (1.0 - r1)) h->j = m2; else h->j = m2 + 1;
+            if ((2.0 * r1 - 1.0) < r2 && r2 < (1.0 - r1)) h->i = m1; else h->i = m1 + 1;
+        } else {
+            if (r2 < (r1 / 2.0)) { h->i = m1 + 1; h->j = m2; }
+            else { h->i = m1 + 1; h->j = m2 + 1; }
+        }
+    }
+    if (v->x < 0.0) {
+        if ((h->j % 2) == 0) {
+            long long int axisi = h->j / 2;
+            long long int diff = h->i - axisi;
+            h->i = h->i - 2.0 * diff;
+        } else {
+            long long int axisi = (h->j + 1) / 2;
+            long long int diff = h->i - axisi;
+            h->i = h->i - (2.0 * diff + 1);
+        }
+    }
+    if (v->y < 0.0) {
+        h->i = h->i - (2 * h->j + 1) / 2;
+        h->j = -1 * h->j;
+    }
+    _ijkNormalize(h);
+}
+
+static void _upAp7(CoordIJK *ijk) {
+    int i = ijk->i - ijk->k, j = ijk->j - ijk->k;
+    ijk->i = (int)lround((3 * i - j) * M_ONESEVENTH);
+    ijk->j = (int)lround((i + 2 * j) * M_ONESEVENTH);
+    ijk->k = 0;
+    _ijkNormalize(ijk);
+}
+static void _upAp7r(CoordIJK *ijk) {
+    int i = ijk->i - ijk->k, j = ijk->j - ijk->k;
+    ijk->i = (int)lround((2 * i + j) * M_ONESEVENTH);
+    ijk->j = (int)lround((3 * j - i) * M_ONESEVENTH);
+    ijk->k = 0;
+    _ijkNormalize(ijk);
+}
+static void _ijkScaleAdd(CoordIJK *acc, const int v[3], int s) {
+    acc->i += v[0] * s; acc->j += v[1] * s; acc->k += v[2] * s;
+}
+static void _downAp7(CoordIJK *ijk) {
+    static const int iv[3] = {3, 0, 1}, jv[3] = {1, 3, 0}, kv[3] = {0, 1, 3};
+    CoordIJK r = {0, 0, 0};
+    _ijkScaleAdd(&r, iv, ijk->i); _ijkScaleAdd(&r, jv, ijk->j); _ijkScaleAdd(&r, kv, ijk->k);
+    *ijk = r;
+    _ijkNormalize(ijk);
+}
+static void _downAp7r(CoordIJK *ijk) {
+    static const int iv[3] = {3, 1, 0}, jv[3] = {0, 3, 1}, kv[3] = {1, 0, 3};
+    CoordIJK r = {0, 0, 0};
+    _ijkScaleAdd(&r, iv, ijk->i); _ijkScaleAdd(&r, jv, ijk->j); _ijkScaleAdd(&r, kv, ijk->k);
+    *ijk = r;
+    _ijkNormalize(ijk);
+}
+static const int UNIT_VECS[7][3] = {{0, 0, 0}, {0, 0, 1}, {0, 1, 0}, {0, 1, 1}, {1, 0, 0}, {1, 0, 1}, {1, 1, 0}};
+static int _unitIjkToDigit(const CoordIJK *ijk) {
+    CoordIJK c = *ijk;
+    _ijkNormalize(&c);
+    for (int d = CENTER_DIGIT; d < 7; d++)
+        if (c.i == UNIT_VECS[d][0] && c.j == UNIT_VECS[d][1] && c.k == UNIT_VECS[d][2]) return d;
+    return INVALID_DIGIT;
+}
+static int _rotate60ccw(int d) {
+    static const int t[8] = {0, 5, 3, 1, 6, 4, 2, 7};
+    return t[d];
+}
+static int _rotate60cw(int d) {
+    static const int t[8] = {0, 3, 6, 2, 5, 1, 4, 7};
+    return t[d];
+}
+static int _h3LeadingNonZeroDigit(uint64_t h) {
+    for (int r = 1; r <= GET_RES(h); r++)
+        if (GET_DIGIT(h, r)) return GET_DIGIT(h, r);
+    return CENTER_DIGIT;
+}
+static uint64_t _h3Rotate60ccw(uint64_t h) {
+    for (int r = 1, res = GET_RES(h); r <= res; r++) SET_DIGIT(h, r, _rotate60ccw(GET_DIGIT(h, r)));
+    return h;
+}
+static uint64_t _h3Rotate60cw(uint64_t h) {
+    for (int r = 1, res = GET_RES(h); r <= res; r++) SET_DIGIT(h, r, _rotate60cw(GET_DIGIT(h, r)));
+    return h;
+}
+static uint64_t _h3RotatePent60ccw(uint64_t h) {
+    int foundFirstNonZeroDigit = 0;
+    for (int r = 1, res = GET_RES(h); r <= res; r++) {
+        SET_DIGIT(h, r, _rotate60ccw(GET_DIGIT(h, r)));
+        if (!foundFirstNonZeroDigit && GET_DIGIT(h, r) != 0) {
+            foundFirstNonZeroDigit = 1;
+            if (_h3LeadingNonZeroDigit(h) == K_AXES_DIGIT) h = _h3Rotate60ccw(h);
+        }
+    }
+    return h;
+}
+static uint64_t _h3RotatePent60cw(uint64_t h) {
+    int foundFirstNonZeroDigit = 0;
+    for (int r = 1, res = GET_RES(h); r <= res; r++) {
+        SET_DIGIT(h, r, _rotate60cw(GET_DIGIT(h, r)));
+        if (!foundFirstNonZeroDigit && GET_DIGIT(h, r) != 0) {
+            foundFirstNonZeroDigit = 1;
+            if (_h3LeadingNonZeroDigit(h) == K_AXES_DIGIT) h = _h3Rotate60cw(h);
+        }
+    }
+    return h;
+}
+
+static uint64_t _faceIjkToH3(const FaceIJK *fijk, int res) {
+    uint64_t h = H3_INIT;
+    h |= UINT64_C(1) << 59;           /* mode = cell */
+    h |= (uint64_t)res << 52;
+    if (res == 0) {
+        if (fijk->coord.i > MAX_FACE_COORD || fijk->coord.j > MAX_FACE_COORD || fijk->coord.k > MAX_FACE_COORD)
+            return 0;
+        h |= (uint64_t)H3T_faceIjkBaseCells[fijk->face][fijk->coord.i][fijk->coord.j][fijk->coord.k][0] << 45;
+        return h;
+    }
+    FaceIJK fijkBC = *fijk;
+    CoordIJK *ijk = &fijkBC.coord;
+    for (int r = res - 1; r >= 0; r--) {
+        CoordIJK lastIJK = *ijk, lastCenter;
+        if (isResolutionClassIII(r + 1)) {
+            _upAp7(ijk);
+            lastCenter = *ijk;
+            _downAp7(&lastCenter);
+        } else {
+            _upAp7r(ijk);
+            lastCenter = *ijk;
+            _downAp7r(&lastCenter);
+        }
+        CoordIJK diff = {lastIJK.i - lastCenter.i, lastIJK.j - lastCenter.j, lastIJK.k - lastCenter.k};
+        _ijkNormalize(&diff);
+        SET_DIGIT(h, r + 1, _unitIjkToDigit(&diff));
+    }
+    if (fijkBC.coord.i > MAX_FACE_COORD || fijkBC.coord.j > MAX_FACE_COORD || fijkBC.coord.k > MAX_FACE_COORD)
+        return 0;
+    const int *bcr = H3T_faceIjkBaseCells[fijkBC.face][fijkBC.coord.i][fijkBC.coord.j][fijkBC.coord.k];
+    int baseCell = bcr[0];
+    h |= (uint64_t)baseCell << 45;
+    int numRots = bcr[1];
+    if (H3T_baseCellData[baseCell][4]) {
+        if (_h3LeadingNonZeroDigit(h) == K_AXES_DIGIT) {
+            if (H3T_baseCellData[baseCell][5] == fijkBC.face || H3T_baseCellData[baseCell][6] == fijkBC.face)
+                h = _h3Rotate60cw(h);
+            else
+                h = _h3Rotate60ccw(h);
+        }
+        for (int i = 0; i < numRots; i++) h = _h3RotatePent60ccw(h);
+    } else {
+        for (int i = 0; i < numRots; i++) h = _h3Rotate60ccw(h);
+    }
+    return h;
+}
+
+/* upstream latLngToCell (h3Index.c) with h3-py's deg2coord in front: degrees in, 0 (H3_NULL) on error. */
+uint64_t oracle_latlng_to_cell(double lat_deg, double lng_deg, int res) {
+    if (res < 0 || res > MAX_H3_RES) return 0;
+    LatLng g = {degsToRads(lat_deg), degsToRads(lng_deg)};
+    if (!isfinite(g.lat) || !isfinite(g.lng)) return 0;
+    FaceIJK fijk;
+    Vec2d v;
+    _geoToHex2d(&g, res, &fijk.face, &v);
+    _hex2dToCoordIJK(&v, &fijk.coord);
+    return _faceIjkToH3(&fijk, res);
+}
+
+void oracle_latlng_to_cell_batch(const double *lat, const double *lng, int64_t n, int res, uint64_t *out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) out[i] = oracle_latlng_to_cell(lat[i], lng[i], res);
+}
+
+/* ---------------- inverse, validation only: cellToLatLng ---------------- */
+static const int maxDimByCIIres[] = {2, -1, 14, -1, 98, -1, 686, -1, 4802, -1, 33614, -1, 235298, -1, 1647086, -1, 11529602};
+static const int unitScaleByCIIres[] = {1, -1, 7, -1, 49, -1, 343, -1, 2401, -1, 16807, -1, 117649, -1, 823543, -1, 5764801};
+
+static void _neighbor(CoordIJK *ijk, int digit) {
+    if (digit > CENTER_DIGIT && digit < 7) {
+        ijk->i += UNIT_VECS[digit][0]; ijk->j += UNIT_VECS[digit][1]; ijk->k += UNIT_VECS[digit][2];
+        _ijkNormalize(ijk);
+    }
+}
+static void _ijkRotate60ccw(CoordIJK *ijk) {
+    CoordIJK r = {0, 0, 0};
+    static const int iv[3] = {1, 1, 0}, jv[3] = {0, 1, 1}, kv[3] = {1, 0, 1};
+    _ijkScaleAdd(&r, iv, ijk->i); _ijkScaleAdd(&r, jv, ijk->j); _ijkScaleAdd(&r, kv, ijk->k);
+    *ijk = r;
+    _ijkNormalize(ijk);
+}
+static void _ijkRotate60cw(CoordIJK *ijk) {
+    CoordIJK r = {0, 0, 0};
+    static const int iv[3] = {1, 0, 1}, jv[3] = {1, 1, 0}, kv[3] = {0, 1, 1};
+    _ijkScaleAdd(&r, iv, ijk->i); _ijkScaleAdd(&r, jv, ijk->j); _ijkScaleAdd(&r, kv, ijk->k);
+    *ijk = r;
+    _ijkNormalize(ijk);
+}
+enum { NO_OVERAGE = 0, FACE_EDGE = 1, NEW_FACE = 2 };
+static int _adjustOverageClassII(FaceIJK *fijk, int res, int pentLeading4, int substrate) {
+    int overage = NO_OVERAGE;
+    CoordIJK *ijk = &fijk->coord;
+    int maxDim = maxDimByCIIres[res];
+    if (substrate) maxDim *= 3;
+    if (substrate && ijk->i + ijk->j + ijk->k == maxDim) {
+        overage = FACE_EDGE;
+    } else if (ijk->i + ijk->j + ijk->k > maxDim) {
+        overage = NEW_FACE;
+        const int *o;
+        if (ijk->k > 0) {
+            if (ijk->j > 0) {
+                o = H3T_faceNeighbors[fijk->face][3];
+            } else {
+                o = H3T_faceNeighbors[fijk->face][2];
+                if (pentLeading4) {
+                    CoordIJK tmp = {ijk->i - maxDim, ijk->j, ijk->k};
+                    _ijkRotate60cw(&tmp);
+                    ijk->i = tmp.i + maxDim; ijk->j = tmp.j; ijk->k = tmp.k;
+                }
+            }
+        } else {
+            o = H3T_faceNeighbors[fijk->face][1];
+        }
+        fijk->face = o[0];
+        for (int i = 0; i < o[4]; i++) _ijkRotate60ccw(ijk);
+        int unitScale = unitScaleByCIIres[res];
+        if (substrate) unitScale *= 3;
+        ijk->i += o[1] * unitScale; ijk->j += o[2] * unitScale; ijk->k += o[3] * unitScale;
+        _ijkNormalize(ijk);
+        if (substrate && ijk->i + ijk->j + ijk->k == maxDim) overage = FACE_EDGE;
+    }
+    return overage;
+}
+static int _h3ToFaceIjkWithInitializedFijk(uint64_t h, FaceIJK *fijk) {
+    CoordIJK *ijk = &fijk->coord;
+    int res = GET_RES(h);
+    int possibleOverage = 1;
+    if (!H3T_baseCellData[GET_BC(h)][4] && (res == 0 || (ijk->i == 0 && ijk->j == 0 && ijk->k == 0)))
+        possibleOverage = 0;
+    for (int r = 1; r <= res; r++) {
+        if (isResolutionClassIII(r)) _downAp7(ijk); else _downAp7r(ijk);
+        _neighbor(ijk, GET_DIGIT(h, r));
+    }
+    return possibleOverage;
+}
+static void _h3ToFaceIjk(uint64_t h, FaceIJK *fijk) {
+    int baseCell = GET_BC(h);
+    if (H3T_baseCellData[baseCell][4] && _h3LeadingNonZeroDigit(h) == IK_AXES_DIGIT) h = _h3Rotate60cw(h);
+    fijk->face = H3T_baseCellData[baseCell][0];
+    fijk->coord.i = H3T_baseCellData[baseCell][1];
+    fijk->coord.j = H3T_baseCellData[baseCell][2];
+    fijk->coord.k = H3T_baseCellData[baseCell][3];
+    if (!_h3ToFaceIjkWithInitializedFijk(h, fijk)) return;
+    CoordIJK origIJK = fijk->coord;
+    int res = GET_RES(h);
+    if (isResolutionClassIII(res)) {
+        _downAp7r(&fijk->coord);
+        res++;
+    }
+    int pentLeading4 = (H3T_baseCellData[baseCell][4] && _h3LeadingNonZeroDigit(h) == I_AXES_DIGIT);
+    if (_adjustOverageClassII(fijk, res, pentLeading4, 0) != NO_OVERAGE) {
+        if (H3T_baseCellData[baseCell][4])
+            while (_adjustOverageClassII(fijk, res, 0, 0) != NO_OVERAGE) continue;
+        if (res != GET_RES(h)) _upAp7r(&fijk->coord);
+    } else if (res != GET_RES(h)) {
+        fijk->coord = origIJK;
+    }
+}
+static void _geoAzDistanceRads(const LatLng *p1, double az, double distance, LatLng *p2) {
+    if (distance < EPSILON) { *p2 = *p1; return; }
+    double sinlat, sinlng, coslng;
+    az = _posAngleRads(az);
+    if (az < EPSILON || fabs(az - M_PI) < EPSILON) {
+        p2->lat = (az < EPSILON) ? p1->lat + distance : p1->lat - distance;
+        if (fabs(p2->lat - M_PI_2) < EPSILON) { p2->lat = M_PI_2; p2->lng = 0.0; }
+        else if (fabs(p2->lat + M_PI_2) < EPSILON) { p2->lat = -M_PI_2; p2->lng = 0.0; }
+        else p2->lng = p1->lng;
+    } else {
+        sinlat = sin(p1->lat) * cos(distance) + cos(p1->lat) * sin(distance) * cos(az);
+        if (sinlat > 1.0) sinlat = 1.0;
+        if (sinlat < -1.0) sinlat = -1.0;
+        p2->lat = asin(sinlat);
+        if (fabs(p2->lat - M_PI_2) < EPSILON) { p2->lat = M_PI_2; p2->lng = 0.0; }
+        else if (fabs(p2->lat + M_PI_2) < EPSILON) { p2->lat = -M_PI_2; p2->lng = 0.0; }
+        else {
+            double invcosp2lat = 1.0 / cos(p2->lat);
+            sinlng = sin(az) * sin(distance) * invcosp2lat;
+            coslng = (cos(distance) - sin(p1->lat) * sin(p2->lat)) / cos(p1->lat) * invcosp2lat;
+            if (sinlng > 1.0) sinlng = 1.0;
+            if (sinlng < -1.0) sinlng = -1.0;
+            if (coslng > 1.0) coslng = 1.0;
+            if (coslng < -1.0) coslng = -1.0;
+            p2->lng = p1->lng + atan2(sinlng, coslng);
+        }
+    }
+    /* constrainLng */
+    while (p2->lng > M_PI) p2->lng = p2->lng - (2 * M_PI);
+    while (p2->lng < -M_PI) p2->lng = p2->lng + (2 * M_PI);
+}
+int oracle_cell_to_latlng(uint64_t h, double *lat_deg, double *lng_deg) {
+    if (((h >> 59) & 0xf) != 1 || GET_RES(h) > MAX_H3_RES || GET_BC(h) >= H3T_NUM_BASE_CELLS) return -1;
+    FaceIJK fijk;
+    _h3ToFaceIjk(h, &fijk);
+    int res = GET_RES(h);
+    /* _ijkToHex2d + _hex2dToGeo (substrate = 0) */
+    int i = fijk.coord.i - fijk.coord.k, j = fijk.coord.j - fijk.coord.k;
+    Vec2d v = {i - 0.5 * j, j * M_SQRT3_2};
+    LatLng g;
+    LatLng fc = {H3T_faceCenterGeo[fijk.face][0], H3T_faceCenterGeo[fijk.face][1]};
+    double r = sqrt(v.x * v.x + v.y * v.y);
+    if (r < EPSILON) {
+        g = fc;
+    } else {
+        double theta = atan2(v.y, v.x);
+        for (int q = 0; q < res; q++) r *= M_RSQRT7;
+        r *= RES0_U_GNOMONIC;
+        r = atan(r);
+        if (isResolutionClassIII(res)) theta = _posAngleRads(theta + M_AP7_ROT_RADS);
+        theta = _posAngleRads(H3T_faceAxesAzRadsCII[fijk.face][0] - theta);
+        _geoAzDistanceRads(&fc, theta, r, &g);
+    }
+    *lat_deg = radsToDegs(g.lat);
+    *lng_deg = radsToDegs(g.lng);
+    return 0;
+}
+
+void oracle_cell_to_latlng_batch(const uint64_t *cells, int64_t n, double *lat, double *lng) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        if (oracle_cell_to_latlng(cells[i], &lat[i], &lng[i])) lat[i] = lng[i] = NAN;
+    }
+}
+
+/* Host x87 reference for the device code's extended-precision emulation (see csrc/h3_device.h):
+ * op 0: (double)(a * M_PI_180); 1: (double)(a * M_SQRT7); 2: (double)(a * M_RSIN60);
+ * 3: (double)(a + M_2PI); 4: (double)(a - M_2PI); 5: (double)(a - M_AP7_ROT_RADS); 6: (double)(a + M_AP7_ROT_RADS) */
+void oracle_ld_ops(const double *a, int64_t n, int op, double *out) {
+    for (int64_t i = 0; i < n; i++) {
+        long double x = a[i];
+        switch (op) {
+            case 0: out[i] = (double)(x * M_PI_180); break;
+            case 1: out[i] = (double)(x * M_SQRT7); break;
+            case 2: out[i] = (double)(x * M_RSIN60); break;
+            case 3: out[i] = (double)(x + M_2PI); break;
+            case 4: out[i] = (double)(x - M_2PI); break;
+            case 5: out[i] = (double)(x - M_AP7_ROT_RADS); break;
+            case 6: out[i] = (double)(x + M_AP7_ROT_RADS); break;
+            default: out[i] = NAN;
+        }
+    }
+}
