@@ -1,0 +1,173 @@
+/*
+ * mobheat -- MI355X-native drop-in for the per-micro-batch hot path of
+ * panosporf99/real-time-mobility-heatmap (reference heatmap_stream.py).
+ *
+ * C ABI only: plain pointers and sizes, no C++ or torch types. Every function returns 0 on success or a
+ * negative HM_E_* code; hm_last_error() returns the message. The ctypes host binding raises RuntimeError
+ * on a negative code, which keeps the reference's "exception fails the micro-batch" behaviour
+ * (reference heatmap_stream.py:192,196,231,235 have no try/except; the query dies in awaitTermination, :249).
+ *
+ * What each entry point replaces (reference file:line):
+ *   hm_create / hm_destroy       -- the Spark session + stateful query plan (heatmap_stream.py:41-47,241-249):
+ *                                   config H3_RES (:26), TILE_MINUTES (:29), withWatermark 10 min (:107).
+ *   hm_process_batch             -- everything between from_json (:88-93) and the Mongo writes for one
+ *                                   micro-batch: the sanity filter (:96-104), the to_h3 UDF (:65-75,105-106),
+ *                                   the watermark (:107), window(eventTs, TILE) x cellId count/avg aggregation
+ *                                   in update mode (:111-133,243), and the in-batch latest-position dedup
+ *                                   groupBy(provider,vehicleId).max(eventTs) + join back (:198-207).
+ *   hm_latlng_to_cell            -- the per-row UDF alone: h3.latlng_to_cell(lat, lon, H3_RES) (:73).
+ *   hm_stage_* (multi-GPU)       -- the same batch split into local pre-aggregation, an owner-partitioned
+ *                                   exchange (the caller moves the records with RCCL all-to-all), and the
+ *                                   owner-side merge; replaces Spark's shuffle (spark.sql.shuffle.partitions, :44).
+ */
+#ifndef MOBHEAT_H
+#define MOBHEAT_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HM_ABI_VERSION 1
+
+/* error codes */
+#define HM_OK 0
+#define HM_E_INVALID (-1)   /* bad argument */
+#define HM_E_HIP (-2)       /* HIP runtime error */
+#define HM_E_NOMEM (-3)     /* device or host allocation failed */
+#define HM_E_OVERFLOW (-4)  /* a device hash table overflowed its probe bound */
+#define HM_E_STATE (-5)     /* call out of order (stage API) */
+
+/* memory kinds for batch pointers */
+#define HM_MEM_HOST 0
+#define HM_MEM_DEVICE 1
+
+typedef struct hm_config {
+    int32_t abi_version;            /* must be HM_ABI_VERSION */
+    int32_t h3_res;                 /* H3_RES, 0..15 (reference default 8, heatmap_stream.py:26) */
+    int32_t device;                 /* HIP device ordinal */
+    int32_t late_uses_prev_watermark; /* 1 = Spark 3.5 default: late rows filtered by the previous batch's
+                                         watermark, state evicted by the current one; 0 = both current */
+    int64_t tile_us;                /* window length in microseconds: TILE_MINUTES*60e6 (default 5 min) */
+    int64_t watermark_delay_ms;     /* withWatermark delay (reference: 10 minutes = 600000) */
+    int64_t state_capacity_hint;    /* initial slots of the persistent tile state (0 = default) */
+    int64_t batch_capacity_hint;    /* expected max events per batch (0 = grow on demand) */
+} hm_config;
+
+/* One micro-batch of raw events, structure of arrays. All arrays have n entries.
+ * row_valid: 1 iff provider, vehicleId and eventTs are all non-null (NULL pointer = all 1).
+ * lat/lon: degrees; a null lat/lon is passed as NaN (it then fails the range filter, like Spark's between).
+ * ts_us: eventTs as Spark TimestampType, microseconds since the epoch, UTC.
+ * speed/speed_valid: speedKmh and its non-null flag (speed_valid NULL = all non-null; speed NULL = all null).
+ * vkey: identity of (provider, vehicleId); equal pairs must give equal keys, distinct pairs distinct keys.
+ *       UINT64_MAX is reserved. */
+typedef struct hm_batch_in {
+    int64_t n;
+    int32_t memory;        /* HM_MEM_HOST or HM_MEM_DEVICE */
+    int32_t reserved;
+    const double *lat;
+    const double *lon;
+    const int64_t *ts_us;
+    const double *speed;
+    const uint8_t *speed_valid;
+    const uint64_t *vkey;
+    const uint8_t *row_valid;
+} hm_batch_in;
+
+/* Per-batch results. Arrays are library-owned and stay valid until the next call on this context
+ * (or hm_destroy). With out_memory == HM_MEM_DEVICE they are device pointers.
+ * Tiles (update mode: every (cell, window) changed by this batch, with cumulative aggregates):
+ *   cell, window_start_us, count, avg_speed (0.0 when speed_null), speed_null, avg_lon, avg_lat.
+ *   window end = window_start_us + tile_us.
+ * Latest positions: row indices (into this batch's input) of every row whose eventTs equals the max
+ *   eventTs of its (provider, vehicleId) among this batch's valid rows; ties give several rows. Sorted. */
+typedef struct hm_batch_out {
+    int64_t n_tiles;
+    const uint64_t *cell;
+    const int64_t *window_start_us;
+    const int64_t *count;
+    const double *avg_speed;
+    const uint8_t *speed_null;
+    const double *avg_lon;
+    const double *avg_lat;
+    int64_t n_latest;
+    const int64_t *latest_row;
+    /* batch statistics */
+    int64_t n_in;                 /* input rows */
+    int64_t n_valid;              /* rows passing the filter (heatmap_stream.py:98-106) */
+    int64_t n_late;               /* valid rows dropped by the watermark */
+    int64_t n_state;              /* live keys in the persistent tile state after the batch */
+    int64_t batch_max_event_ms;   /* max(eventTs/1000) over valid rows, INT64_MIN if none */
+    int64_t watermark_ms;         /* watermark used for eviction in this batch */
+    int64_t late_watermark_ms;    /* watermark used to drop late rows in this batch */
+} hm_batch_out;
+
+typedef struct hm_ctx hm_ctx;
+
+int hm_create(const hm_config *cfg, hm_ctx **out);
+void hm_destroy(hm_ctx *ctx);
+const char *hm_last_error(const hm_ctx *ctx);   /* ctx may be NULL: last error of hm_create */
+
+/* Single-GPU hot path for one micro-batch. epoch_id is recorded (Spark's batch id); batches must be
+ * passed in order, including empty (no-data) batches. out_memory selects host or device result arrays. */
+int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t out_memory,
+                     hm_batch_out *out);
+
+/* Per-row UDF: cells for n points (degrees) at resolution res; 0 for rows the UDF maps to None.
+ * Pointers are in `memory` space (host pointers are copied). Runs on device `device`. */
+int hm_latlng_to_cell(const double *lat, const double *lon, int64_t n, int32_t res, int32_t memory,
+                      int32_t device, uint64_t *out);
+
+/* ---- multi-GPU stage API (one context per GPU/rank; the caller performs the exchanges) ----
+ * Record layouts (little endian, packed):
+ *   tile partial  (56 B): u64 cell, i64 window_start_us, i64 count, i64 n_speed, f64 sum_speed,
+ *                         f64 sum_lat, f64 sum_lon
+ *   latest cand.  (32 B): u64 vkey, i64 ts_us, i64 row, i64 origin_rank
+ * All exchange buffers are caller-owned device memory (e.g. torch tensors handed to RCCL), sized in records.
+ * 1. hm_stage_local: snap + filter + window + local pre-aggregation + local latest candidates; both record
+ *    kinds are written grouped by owner rank = hash(key) % nranks into the caller's send buffers (capacity
+ *    >= in->n records each is always enough) with per-destination counts (host arrays of nranks entries).
+ * 2. caller: exchange counts and records (all_to_all), allreduce(max) of batch_max_event_ms.
+ * 3. hm_stage_merge: merges the received tile partials into this rank's persistent state, emits the tiles
+ *    this rank owns, reduces the received candidates to winners, and writes the winners' row indices grouped
+ *    by origin rank into winner_send_buf (capacity >= n_cand_recv) with per-origin counts.
+ * 4. caller: exchange winners back; hm_stage_finish takes the received winners (rows of this rank). */
+#define HM_TILE_REC_BYTES 56
+#define HM_CAND_REC_BYTES 32
+typedef struct hm_stage_sizes {
+    int64_t n_tile_partials;      /* total tile partial records produced locally */
+    int64_t n_cands;              /* total latest candidates produced locally */
+    int64_t batch_max_event_ms;   /* local max, to be allreduced by the caller */
+    int64_t n_valid, n_late;
+} hm_stage_sizes;
+
+int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t nranks, int32_t rank,
+                   void *tile_send_buf, int64_t tile_send_cap, int64_t *tile_send_counts,
+                   void *cand_send_buf, int64_t cand_send_cap, int64_t *cand_send_counts, hm_stage_sizes *sizes);
+int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, const void *cand_recv_dev,
+                   int64_t n_cand_recv, int64_t global_batch_max_event_ms, int32_t out_memory,
+                   hm_batch_out *out, void *winner_send_buf, int64_t winner_send_cap, int64_t *winner_send_counts);
+int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_recv, int32_t out_memory,
+                    hm_batch_out *out);
+
+/* device helpers for the caller's exchange buffers */
+int hm_device_alloc(int32_t device, int64_t bytes, void **ptr);
+int hm_device_free(int32_t device, void *ptr);
+int hm_memcpy(void *dst, const void *src, int64_t bytes, int32_t kind); /* 0 H2D 1 D2H 2 D2D */
+
+/* Self-test entry (host-side execution of the device numerics; no GPU needed): evaluates the
+ * extended-precision emulation used by the kernels, op codes as oracle_ld_ops(). */
+int hm_selftest_ld_ops(const double *a, int64_t n, int32_t op, double *out);
+/* Host-side execution of the device latLngToCell code path (for debugging without a GPU; uses host libm
+ * for the transcendental functions, so it is NOT the device numerics). */
+int hm_selftest_latlng_to_cell_host(const double *lat, const double *lon, int64_t n, int32_t res,
+                                    uint64_t *out);
+
+/* Timing of the last hm_process_batch / stage call on the library's stream (HIP events), milliseconds
+ * per kernel: index 0 snap, 1 local aggregate, 2 merge, 3 emit, 4 dedup, 5 total. */
+int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

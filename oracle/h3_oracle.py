@@ -1,0 +1,66 @@
+"""ORACLE -- test infrastructure only (never imported by the product path).
+
+ctypes wrapper of oracle/libh3oracle.so, the C restatement of H3 v4 latLngToCell / cellToLatLng
+(see h3_oracle.c for provenance).  Builds the library with `make -C oracle` when it is missing.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libh3oracle.so")
+_lib = None
+
+
+def build(force=False):
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "h3_oracle.c")):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+def load():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB)
+        P = ctypes.c_void_p
+        L.oracle_latlng_to_cell.restype = ctypes.c_uint64
+        L.oracle_latlng_to_cell.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int]
+        L.oracle_latlng_to_cell_batch.restype = None
+        L.oracle_latlng_to_cell_batch.argtypes = [P, P, ctypes.c_int64, ctypes.c_int, P]
+        L.oracle_cell_to_latlng_batch.restype = None
+        L.oracle_cell_to_latlng_batch.argtypes = [P, ctypes.c_int64, P, P]
+        L.oracle_ld_ops.restype = None
+        L.oracle_ld_ops.argtypes = [P, ctypes.c_int64, ctypes.c_int, P]
+        _lib = L
+    return _lib
+
+
+def latlng_to_cell(lat, lon, res):
+    """h3.latlng_to_cell for arrays (degrees); 0 where h3 would fail (non-finite / bad res)."""
+    L = load()
+    lat = np.ascontiguousarray(lat, dtype=np.float64)
+    lon = np.ascontiguousarray(lon, dtype=np.float64)
+    out = np.empty(lat.size, dtype=np.uint64)
+    L.oracle_latlng_to_cell_batch(lat.ctypes.data, lon.ctypes.data, lat.size, int(res), out.ctypes.data)
+    return out
+
+
+def cell_to_latlng(cells):
+    L = load()
+    cells = np.ascontiguousarray(cells, dtype=np.uint64)
+    la = np.empty(cells.size)
+    lo = np.empty(cells.size)
+    L.oracle_cell_to_latlng_batch(cells.ctypes.data, cells.size, la.ctypes.data, lo.ctypes.data)
+    return la, lo
+
+
+def ld_ops(a, op):
+    """x87 long-double reference for the kernels' emulation (op codes as hm_selftest_ld_ops)."""
+    L = load()
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    out = np.empty_like(a)
+    L.oracle_ld_ops(a.ctypes.data, a.size, int(op), out.ctypes.data)
+    return out

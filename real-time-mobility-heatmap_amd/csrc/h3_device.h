@@ -1,0 +1,377 @@
+// latLngToCell for CDNA4 (gfx950): one lane per event, fp64 VALU.
+//
+// Restates upstream H3 v4 latLngToCell (h3Index.c) -> _geoToFaceIjk -> _geoToHex2d (faceijk.c) ->
+// _hex2dToCoordIJK (coordijk.c) -> _faceIjkToH3 (faceijk.c), i.e. what the reference's UDF calls per row
+// (reference heatmap_stream.py:65-75 -> h3.latlng_to_cell, h3-py 4.x).
+//
+// Bit-exactness notes:
+//  * upstream declares several constants as `long double` (M_PI_180, M_2PI, M_AP7_ROT_RADS, M_SQRT7,
+//    M_RSIN60, EPSILON); compiled on x86-64 those expressions run in x87 80-bit (64-bit mantissa, round to
+//    nearest even) and are rounded again to double on assignment.  hm::xld_* reproduce that double rounding
+//    exactly with 128-bit integer arithmetic (selftest: hm_selftest_ld_ops vs the x87 oracle).
+//  * every fp64 expression keeps upstream's operation order and is compiled with -ffp-contract=off
+//    (no v_fma_f64 contraction: x86-64 h3 builds have none).
+//  * sin/cos of the face-centre latitudes are precomputed on the host with the same libm the reference
+//    uses (glibc) and uploaded; the per-event sin/cos/acos/atan2/tan use the device math library.
+//
+// Functions are __host__ __device__ so the same code can be executed on the CPU by the self-test entry
+// points (where the transcendental calls resolve to the host libm).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HM_HD __host__ __device__ __forceinline__
+
+namespace hm {
+
+typedef unsigned __int128 u128;
+
+// ---- x87 long double constants of upstream constants.h (exact 64-bit mantissa, value = M * 2^E) ----
+#define HM_LD_PI_180_M UINT64_C(0x8efa351294e9c8ae)
+#define HM_LD_PI_180_E (-69)
+#define HM_LD_2PI_M UINT64_C(0xc90fdaa22168c235)
+#define HM_LD_2PI_E (-61)
+#define HM_LD_AP7_ROT_M UINT64_C(0xaabcfee1d47a0aea)
+#define HM_LD_AP7_ROT_E (-65)
+#define HM_LD_SQRT7_M UINT64_C(0xa953fd4e97c74dbc)
+#define HM_LD_SQRT7_E (-62)
+#define HM_LD_RSIN60_M UINT64_C(0x93cd3a2c8198e269)
+#define HM_LD_RSIN60_E (-63)
+#define HM_LD_EPSILON_M UINT64_C(0xe69594bec44de15b)
+#define HM_LD_EPSILON_E (-117)
+// double constants (no L suffix upstream)
+#define HM_INV_RES0_U_GNOMONIC 2.61803398874989588842
+
+HM_HD int clz128(u128 x) {
+    uint64_t hi = (uint64_t)(x >> 64), lo = (uint64_t)x;
+    return hi ? __builtin_clzll(hi) : 64 + __builtin_clzll(lo);
+}
+
+// Round P * 2^E (P != 0; `sticky` = nonzero bits below P's LSB) first to a 64-bit mantissa (x87 extended,
+// round-to-nearest-even), then to double (round-to-nearest-even), as x87 arithmetic + store does.
+HM_HD double round_x87_then_double(u128 P, int E, bool sticky, bool neg) {
+    int L = 127 - clz128(P);
+    uint64_t keep;
+    if (L >= 64) {
+        int sh = L - 63;
+        keep = (uint64_t)(P >> sh);
+        u128 rem = P & ((((u128)1) << sh) - 1);
+        u128 half = ((u128)1) << (sh - 1);
+        bool up = rem > half || (rem == half && (sticky || (keep & 1)));
+        E += sh;
+        if (up) {
+            keep += 1;
+            if (keep == 0) { keep = UINT64_C(1) << 63; E += 1; }
+        }
+    } else {
+        keep = (uint64_t)P << (63 - L);
+        E -= (63 - L);
+    }
+    // keep in [2^63, 2^64): value = keep * 2^E; now round to double
+    int lead = 63 + E;
+    int lsb = lead - 52;
+    if (lsb < -1074) lsb = -1074;
+    int drop = lsb - E;  // >= 11
+    uint64_t m;
+    if (drop >= 65) {
+        m = 0;
+    } else if (drop == 64) {
+        m = (keep > (UINT64_C(1) << 63)) ? 1 : 0;  // tie (== 2^63) rounds to even 0
+    } else {
+        m = keep >> drop;
+        uint64_t rem = keep & ((UINT64_C(1) << drop) - 1);
+        uint64_t half = UINT64_C(1) << (drop - 1);
+        if (rem > half || (rem == half && (m & 1))) m += 1;
+    }
+    double r = ldexp((double)m, lsb);
+    return neg ? -r : r;
+}
+
+HM_HD void split_double(double a, uint64_t &m, int &e, bool &neg) {
+    uint64_t b = __builtin_bit_cast(uint64_t, a);
+    neg = (b >> 63) != 0;
+    int ex = (int)((b >> 52) & 0x7ff);
+    uint64_t fr = b & ((UINT64_C(1) << 52) - 1);
+    if (ex == 0) { m = fr; e = -1074; }
+    else { m = fr | (UINT64_C(1) << 52); e = ex - 1075; }
+}
+
+// (double)((long double)a * C)
+HM_HD double xld_mul(double a, uint64_t cm, int ce) {
+    if (a == 0.0 || !__builtin_isfinite(a)) return a * ldexp((double)cm, ce);
+    uint64_t ma; int ea; bool neg;
+    split_double(a, ma, ea, neg);
+    u128 P = (u128)ma * (u128)cm;
+    return round_x87_then_double(P, ea + ce, false, neg);
+}
+
+// (double)((long double)a + (negc ? -C : C))
+HM_HD double xld_add(double a, bool negc, uint64_t cm, int ce) {
+    if (!__builtin_isfinite(a)) return a;
+    uint64_t ma = 0; int ea = 0; bool na = false;
+    if (a != 0.0) split_double(a, ma, ea, na);
+    int lc = ce + 63;
+    int la = ma ? ea + (63 - __builtin_clzll(ma)) : -100000;
+    int top = la > lc ? la : lc;
+    int B = top - 125;
+    bool sticky = false;
+    u128 xa = 0, xc = 0;
+    if (ma) {
+        int s = ea - B;
+        if (s >= 0) xa = ((u128)ma) << s;
+        else if (s > -128) { xa = ((u128)ma) >> (-s); sticky = ((((u128)ma) << (128 + s)) != 0); }
+        else { xa = 0; sticky = true; }
+    }
+    {
+        int s = ce - B;
+        if (s >= 0) xc = ((u128)cm) << s;
+        else if (s > -128) { xc = ((u128)cm) >> (-s); sticky = ((((u128)cm) << (128 + s)) != 0); }
+        else { xc = 0; sticky = true; }
+    }
+    u128 R;
+    bool neg;
+    if (na == negc) {
+        R = xa + xc;
+        neg = na;
+    } else {
+        // magnitudes: the operand that lost bits (if any) is the smaller one
+        if (xa >= xc) { R = xa - xc; neg = na; if (sticky && la < lc) { /* a was the smaller: impossible */ } }
+        else { R = xc - xa; neg = negc; }
+        if (sticky) { R -= 1; }   // true value lies strictly between R-1 and R (smaller operand truncated)
+    }
+    if (R == 0 && !sticky) return 0.0;
+    return round_x87_then_double(R, B, sticky, neg);
+}
+
+// a >= C (C > 0, long double), exactly
+HM_HD bool xld_ge(double a, uint64_t cm, int ce) {
+    if (!(a > 0.0)) return false;
+    if (!__builtin_isfinite(a)) return true;
+    uint64_t ma; int ea; bool neg;
+    split_double(a, ma, ea, neg);
+    int la = ea + (63 - __builtin_clzll(ma));
+    int lc = ce + 63;
+    if (la != lc) return la > lc;
+    uint64_t an = ma << (__builtin_clzll(ma));  // normalise to 64-bit with top bit set
+    return an >= cm;
+}
+HM_HD bool xld_lt(double a, uint64_t cm, int ce) { return !xld_ge(a, cm, ce); }
+
+// ---- upstream helpers ----
+HM_HD double posAngleRads(double rads) {
+    // double tmp = ((rads < 0.0L) ? rads + M_2PI : rads); if (rads >= M_2PI) tmp -= M_2PI;
+    double tmp = (rads < 0.0) ? xld_add(rads, false, HM_LD_2PI_M, HM_LD_2PI_E) : rads;
+    if (xld_ge(rads, HM_LD_2PI_M, HM_LD_2PI_E)) tmp = xld_add(tmp, true, HM_LD_2PI_M, HM_LD_2PI_E);
+    return tmp;
+}
+
+struct IJK { int i, j, k; };
+
+HM_HD void ijkNormalize(IJK &c) {
+    if (c.i < 0) { c.j -= c.i; c.k -= c.i; c.i = 0; }
+    if (c.j < 0) { c.i -= c.j; c.k -= c.j; c.j = 0; }
+    if (c.k < 0) { c.i -= c.k; c.j -= c.k; c.k = 0; }
+    int mn = c.i;
+    if (c.j < mn) mn = c.j;
+    if (c.k < mn) mn = c.k;
+    if (mn > 0) { c.i -= mn; c.j -= mn; c.k -= mn; }
+}
+
+// lround(n * M_ONESEVENTH): n/7 is never within 1/14 of a half-integer, so round-half-away-from-zero of
+// the exact quotient, in integers.
+HM_HD int round_div7(int n) { return n >= 0 ? (n + 3) / 7 : -((-n + 3) / 7); }
+
+// _hex2dToCoordIJK (coordijk.c)
+HM_HD IJK hex2dToCoordIJK(double vx, double vy) {
+    IJK h;
+    h.k = 0;
+    double a1 = __builtin_fabs(vx);
+    double a2 = __builtin_fabs(vy);
+    double x2 = xld_mul(a2, HM_LD_RSIN60_M, HM_LD_RSIN60_E);
+    double x1 = a1 + x2 / 2.0;
+    int m1 = (int)x1;
+    int m2 = (int)x2;
+    double r1 = x1 - m1;
+    double r2 = x2 - m2;
+    if (r1 < 0.5) {
+        if (r1 < 1.0 / 3.0) {
+            if (r2 < (1.0 + r1) / 2.0) { h.i = m1; h.j = m2; }
+            else { h.i = m1; h.j = m2 + 1; }
+        } else {
+            h.j = (r2 < (1.0 - r1)) ? m2 : m2 + 1;
+            h.i = ((1.0 - r1) <= r2 && r2 < (2.0 * r1)) ? m1 + 1 : m1;
+        }
+    } else {
+        if (r1 < 2.0 / 3.0) {
+            h.j = (r2 < (1.0 - r1)) ? m2 : m2 + 1;
+            h.i = ((2.0 * r1 - 1.0) < r2 && r2 < (1.0 - r1)) ? m1 : m1 + 1;
+        } else {
+            if (r2 < (r1 / 2.0)) { h.i = m1 + 1; h.j = m2; }
+            else { h.i = m1 + 1; h.j = m2 + 1; }
+        }
+    }
+    if (vx < 0.0) {
+        // upstream: h->i = h->i - 2.0 * diff (exact small integers)
+        if ((h.j % 2) == 0) {
+            long long axisi = h.j / 2;
+            long long diff = h.i - axisi;
+            h.i = (int)(h.i - 2 * diff);
+        } else {
+            long long axisi = (h.j + 1) / 2;
+            long long diff = h.i - axisi;
+            h.i = (int)(h.i - (2 * diff + 1));
+        }
+    }
+    if (vy < 0.0) {
+        h.i = h.i - (2 * h.j + 1) / 2;
+        h.j = -1 * h.j;
+    }
+    ijkNormalize(h);
+    return h;
+}
+
+// digit rotation tables (Direction enum: 0 center, 1 K, 2 J, 3 JK, 4 I, 5 IK, 6 IJ)
+HM_HD int rot60ccw(int d) { return (int)((UINT64_C(0x72461350) >> (4 * d)) & 0xf); }  // {0,5,3,1,6,4,2,7}
+HM_HD int rot60cw(int d) { return (int)((UINT64_C(0x74152630) >> (4 * d)) & 0xf); }   // {0,3,6,2,5,1,4,7}
+
+HM_HD int getDigit(uint64_t h, int r) { return (int)((h >> ((15 - r) * 3)) & 7); }
+HM_HD void setDigit(uint64_t &h, int r, int d) {
+    int s = (15 - r) * 3;
+    h = (h & ~(UINT64_C(7) << s)) | ((uint64_t)d << s);
+}
+HM_HD int leadingNonZeroDigit(uint64_t h, int res) {
+    for (int r = 1; r <= res; r++) {
+        int d = getDigit(h, r);
+        if (d) return d;
+    }
+    return 0;
+}
+HM_HD uint64_t rotate60ccw(uint64_t h, int res) {
+    for (int r = 1; r <= res; r++) setDigit(h, r, rot60ccw(getDigit(h, r)));
+    return h;
+}
+HM_HD uint64_t rotate60cw(uint64_t h, int res) {
+    for (int r = 1; r <= res; r++) setDigit(h, r, rot60cw(getDigit(h, r)));
+    return h;
+}
+HM_HD uint64_t rotatePent60ccw(uint64_t h, int res) {
+    bool found = false;
+    for (int r = 1; r <= res; r++) {
+        setDigit(h, r, rot60ccw(getDigit(h, r)));
+        if (!found && getDigit(h, r) != 0) {
+            found = true;
+            if (leadingNonZeroDigit(h, res) == 1) h = rotate60ccw(h, res);
+        }
+    }
+    return h;
+}
+
+// Tables the kernels read (device: __constant__ copies; host self-test: static copies).
+struct H3Tables {
+    double faceCenterGeo[20][2];
+    double faceCenterPoint[20][3];
+    double faceAxesAz0[20];
+    double faceCosLat[20];   // cos(faceCenterGeo[f].lat), host libm
+    double faceSinLat[20];   // sin(faceCenterGeo[f].lat), host libm
+    int faceIjkBaseCells[20][3][3][3][2];
+    int baseCellData[122][7];
+};
+
+// _faceIjkToH3 (faceijk.c), res >= 1
+HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const H3Tables &T) {
+    uint64_t h = UINT64_C(0x00001fffffffffff) | (UINT64_C(1) << 59) | ((uint64_t)res << 52);
+    if (res == 0) {
+        if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
+        return h | ((uint64_t)T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][0] << 45);
+    }
+    for (int r = res - 1; r >= 0; r--) {
+        IJK last = ijk, center;
+        int i = ijk.i - ijk.k, j = ijk.j - ijk.k;
+        if ((r + 1) & 1) {  // Class III: _upAp7 then _downAp7
+            ijk.i = round_div7(3 * i - j);
+            ijk.j = round_div7(i + 2 * j);
+            ijk.k = 0;
+            ijkNormalize(ijk);
+            center.i = 3 * ijk.i + 1 * ijk.j + 0 * ijk.k;
+            center.j = 0 * ijk.i + 3 * ijk.j + 1 * ijk.k;
+            center.k = 1 * ijk.i + 0 * ijk.j + 3 * ijk.k;
+        } else {            // Class II: _upAp7r then _downAp7r
+            ijk.i = round_div7(2 * i + j);
+            ijk.j = round_div7(3 * j - i);
+            ijk.k = 0;
+            ijkNormalize(ijk);
+            center.i = 3 * ijk.i + 0 * ijk.j + 1 * ijk.k;
+            center.j = 1 * ijk.i + 3 * ijk.j + 0 * ijk.k;
+            center.k = 0 * ijk.i + 1 * ijk.j + 3 * ijk.k;
+        }
+        ijkNormalize(center);
+        IJK diff = {last.i - center.i, last.j - center.j, last.k - center.k};
+        ijkNormalize(diff);
+        int digit = 7;
+        if (diff.i <= 1 && diff.j <= 1 && diff.k <= 1) digit = diff.i * 4 + diff.j * 2 + diff.k;
+        setDigit(h, r + 1, digit);
+    }
+    if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
+    int baseCell = T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][0];
+    int numRots = T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][1];
+    h |= (uint64_t)baseCell << 45;
+    if (T.baseCellData[baseCell][4]) {
+        if (leadingNonZeroDigit(h, res) == 1) {
+            if (T.baseCellData[baseCell][5] == face || T.baseCellData[baseCell][6] == face) h = rotate60cw(h, res);
+            else h = rotate60ccw(h, res);
+        }
+        for (int i = 0; i < numRots; i++) h = rotatePent60ccw(h, res);
+    } else {
+        for (int i = 0; i < numRots; i++) h = rotate60ccw(h, res);
+    }
+    return h;
+}
+
+// latLngToCell with h3-py's deg2coord: degrees in; returns 0 where the reference UDF returns None
+// (the range guard of heatmap_stream.py:66-69; NaN fails it).
+HM_HD uint64_t latLngToCellDeg(double lat_deg, double lng_deg, int res, const H3Tables &T) {
+    if (!(lat_deg >= -90.0 && lat_deg <= 90.0 && lng_deg >= -180.0 && lng_deg <= 180.0)) return 0;
+    double glat = xld_mul(lat_deg, HM_LD_PI_180_M, HM_LD_PI_180_E);
+    double glng = xld_mul(lng_deg, HM_LD_PI_180_M, HM_LD_PI_180_E);
+    // _geoToVec3d
+    double clat = cos(glat), slat = sin(glat);
+    double vz = slat;
+    double vx = cos(glng) * clat;
+    double vy = sin(glng) * clat;
+    // _geoToClosestFace
+    int face = 0;
+    double sqd = 5.0;
+    for (int f = 0; f < 20; ++f) {
+        double dx = T.faceCenterPoint[f][0] - vx;
+        double dy = T.faceCenterPoint[f][1] - vy;
+        double dz = T.faceCenterPoint[f][2] - vz;
+        double s = dx * dx + dy * dy;
+        s = s + dz * dz;
+        if (s < sqd) { face = f; sqd = s; }
+    }
+    // _geoToHex2d
+    double r = acos(1 - sqd / 2);
+    double hx, hy;
+    if (xld_lt(r, HM_LD_EPSILON_M, HM_LD_EPSILON_E)) {
+        hx = hy = 0.0;
+    } else {
+        double dlng = glng - T.faceCenterGeo[face][1];
+        double sd = sin(dlng), cd = cos(dlng);
+        double num = clat * sd;
+        double t1 = T.faceCosLat[face] * slat;
+        double t2 = T.faceSinLat[face] * clat;
+        t2 = t2 * cd;
+        double az = atan2(num, t1 - t2);
+        double theta = posAngleRads(T.faceAxesAz0[face] - posAngleRads(az));
+        if (res & 1) theta = posAngleRads(xld_add(theta, true, HM_LD_AP7_ROT_M, HM_LD_AP7_ROT_E));
+        r = tan(r);
+        r *= HM_INV_RES0_U_GNOMONIC;
+        for (int i = 0; i < res; i++) r = xld_mul(r, HM_LD_SQRT7_M, HM_LD_SQRT7_E);
+        hx = r * cos(theta);
+        hy = r * sin(theta);
+    }
+    IJK ijk = hex2dToCoordIJK(hx, hy);
+    return faceIjkToH3(face, ijk, res, T);
+}
+
+}  // namespace hm

@@ -1,0 +1,1388 @@
+// mobheat: MI355X-native per-micro-batch hot path of the reference's streaming job.
+//
+// Pipeline per batch (one HIP stream per context; every arithmetic step runs on the GPU):
+//   k_snap        filter (heatmap_stream.py:96-104) + H3 latLngToCell UDF (:65-75,105) + tumbling window
+//                 (:115) + late-row test against the watermark (:107); batch max event time (ms)
+//   k_local_agg   LDS hash pre-aggregation of (cell, windowStart) -> count, n_speed, sum speed/lat/lon
+//                 into 56-B partial records (Spark's partial HashAggregate, :112-123)
+//   [multi-GPU: partials partitioned by owner rank, exchanged by the caller with RCCL all-to-all]
+//   k_merge       owner-side merge of partials into the persistent device state table (update mode,
+//                 :243; Spark's StateStoreRestore/Save), marking touched keys
+//   k_emit        touched keys -> output rows with cumulative count/avg (:124-132)
+//   k_rehash      state eviction by the watermark (window end <= watermark) and table growth
+//   k_dedup_*     latest position per (provider, vehicleId): max(eventTs) + rows equal to it (:200-207)
+//
+// Semantics follow SURVEY.md App. A (Spark 3.5.1): see DESIGN.md for the rules and their provenance.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mobheat.h"
+#include "kernels.h"
+
+#define H3T_CONST static const
+#include "h3_tables.inc"
+
+using namespace hm;
+
+__constant__ H3Tables c_tab;
+
+static H3Tables make_tables() {
+    H3Tables T;
+    for (int f = 0; f < 20; f++) {
+        T.faceCenterGeo[f][0] = H3T_faceCenterGeo[f][0];
+        T.faceCenterGeo[f][1] = H3T_faceCenterGeo[f][1];
+        for (int c = 0; c < 3; c++) T.faceCenterPoint[f][c] = H3T_faceCenterPoint[f][c];
+        T.faceAxesAz0[f] = H3T_faceAxesAzRadsCII[f][0];
+        // upstream evaluates cos/sin(p1->lat) per call with the host libm; identical values
+        volatile double lat = H3T_faceCenterGeo[f][0];
+        T.faceCosLat[f] = std::cos(lat);
+        T.faceSinLat[f] = std::sin(lat);
+    }
+    memcpy(T.faceIjkBaseCells, H3T_faceIjkBaseCells, sizeof(T.faceIjkBaseCells));
+    memcpy(T.baseCellData, H3T_baseCellData, sizeof(T.baseCellData));
+    return T;
+}
+
+// =====================================================================================================
+// wave helpers
+// =====================================================================================================
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ long long wave_max(long long v) {
+    for (int o = 32; o > 0; o >>= 1) { long long w = __shfl_xor(v, o, 64); v = w > v ? w : v; }
+    return v;
+}
+__device__ __forceinline__ long long wave_min(long long v) {
+    for (int o = 32; o > 0; o >>= 1) { long long w = __shfl_xor(v, o, 64); v = w < v ? w : v; }
+    return v;
+}
+// Wave-aggregated append: returns this lane's slot index (valid only where pred), one atomic per wave.
+__device__ __forceinline__ unsigned long long wave_append(bool pred, unsigned long long *counter) {
+    unsigned long long m = __ballot(pred);
+    unsigned long long base = 0;
+    if (m) {
+        int leader = __ffsll((long long)m) - 1;
+        if (lane_id() == leader) base = atomicAdd(counter, (unsigned long long)__popcll(m));
+        base = __shfl(base, leader, 64);
+    }
+    unsigned long long below = m & ((UINT64_C(1) << lane_id()) - 1);
+    return base + __popcll(below);
+}
+
+// =====================================================================================================
+// K1: filter + latLngToCell + window + late test
+// =====================================================================================================
+__global__ __launch_bounds__(256) void k_snap(const double *__restrict__ lat, const double *__restrict__ lon,
+                                              const int64_t *__restrict__ ts, const uint8_t *__restrict__ row_valid,
+                                              int64_t n, int res, int64_t tile_us, int64_t late_end_us,
+                                              uint64_t *__restrict__ cell_out, int64_t *__restrict__ wstart_out,
+                                              uint8_t *__restrict__ flags_out, DevStats *st) {
+    unsigned long long nvalid = 0, nlate = 0;
+    long long mx = INT64_MIN;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        double la = lat[i], lo = lon[i];
+        int64_t t = ts[i];
+        bool ok = (row_valid ? row_valid[i] != 0 : true) && la >= -90.0 && la <= 90.0 && lo >= -180.0 && lo <= 180.0 &&
+                  t > INT64_MIN + 2 * tile_us && t < INT64_MAX - 2 * tile_us;
+        uint8_t fl = 0;
+        uint64_t cell = EMPTY_CELL;
+        int64_t ws = EMPTY_WIN;
+        if (ok) {
+            int64_t rem = t % tile_us;
+            if (rem < 0) rem += tile_us;
+            ws = t - rem;
+            bool late = (ws + tile_us) <= late_end_us;
+            fl = late ? (F_VALID | F_LATE) : (F_VALID | F_AGG);
+            nvalid++;
+            nlate += late;
+            long long ms = (long long)(t / 1000);
+            mx = ms > mx ? ms : mx;
+            if (!late) cell = latLngToCellDeg(la, lo, res, c_tab);
+        }
+        cell_out[i] = cell;
+        wstart_out[i] = ws;
+        flags_out[i] = fl;
+    }
+    nvalid = wave_sum(nvalid);
+    nlate = wave_sum(nlate);
+    mx = wave_max(mx);
+    if (lane_id() == 0) {
+        if (nvalid) atomicAdd(&st->n_valid, nvalid);
+        if (nlate) atomicAdd(&st->n_late, nlate);
+        if (mx != INT64_MIN) atomicMax(&st->max_ts_ms, mx);
+    }
+}
+
+// standalone UDF: cells only (hm_latlng_to_cell)
+__global__ __launch_bounds__(256) void k_cells(const double *__restrict__ lat, const double *__restrict__ lon, int64_t n,
+                                               int res, uint64_t *__restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = latLngToCellDeg(lat[i], lon[i], res, c_tab);
+}
+
+// =====================================================================================================
+// K2: LDS pre-aggregation into partial records (persistent blocks, flush when the table fills)
+// =====================================================================================================
+constexpr int LA_THREADS = 256;
+constexpr int LA_SLOTS = 1024;
+constexpr int LA_CHUNK = 512;          // events inserted between occupancy checks
+constexpr int LA_FLUSH_AT = LA_SLOTS - 2 * LA_CHUNK + 256;   // occupancy bound before a chunk: <= 768 after
+
+struct LaShared {
+    unsigned long long cell[LA_SLOTS];
+    long long w[LA_SLOTS];
+    unsigned long long cnt[LA_SLOTS];   // low 32: count, high 32: n_speed
+    double ssp[LA_SLOTS];
+    double slat[LA_SLOTS];
+    double slon[LA_SLOTS];
+    unsigned int occ;
+    unsigned int scan[LA_THREADS / 64];
+    unsigned long long base;
+};
+
+__device__ void la_flush(LaShared &S, TilePartial *out, DevStats *st) {
+    __syncthreads();
+    const int per = LA_SLOTS / LA_THREADS;  // 4
+    int t = threadIdx.x;
+    unsigned c = 0;
+    for (int q = 0; q < per; q++) c += S.cell[t * per + q] != EMPTY_CELL;
+    // block exclusive scan of c
+    unsigned incl = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        unsigned v = __shfl_up(incl, o, 64);
+        if (lane_id() >= o) incl += v;
+    }
+    int wv = t >> 6;
+    if (lane_id() == 63) S.scan[wv] = incl;
+    __syncthreads();
+    unsigned wave_off = 0, total = 0;
+    for (int q = 0; q < LA_THREADS / 64; q++) {
+        if (q < wv) wave_off += S.scan[q];
+        total += S.scan[q];
+    }
+    if (t == 0) S.base = total ? atomicAdd(&st->n_partials, (unsigned long long)total) : 0;
+    __syncthreads();
+    unsigned long long pos = S.base + wave_off + incl - c;
+    for (int q = 0; q < per; q++) {
+        int s = t * per + q;
+        if (S.cell[s] != EMPTY_CELL) {
+            TilePartial p;
+            p.cell = S.cell[s];
+            p.wstart = S.w[s];
+            p.count = (int64_t)(S.cnt[s] & 0xffffffffull);
+            p.nspeed = (int64_t)(S.cnt[s] >> 32);
+            p.sspeed = S.ssp[s];
+            p.slat = S.slat[s];
+            p.slon = S.slon[s];
+            out[pos++] = p;
+        }
+        S.cell[s] = EMPTY_CELL;
+        S.w[s] = EMPTY_WIN;
+        S.cnt[s] = 0;
+        S.ssp[s] = 0.0;
+        S.slat[s] = 0.0;
+        S.slon[s] = 0.0;
+    }
+    if (t == 0) S.occ = 0;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(LA_THREADS) void k_local_agg(const uint64_t *__restrict__ cell, const int64_t *__restrict__ wstart,
+                                                          const uint8_t *__restrict__ flags, const double *__restrict__ speed,
+                                                          const uint8_t *__restrict__ speed_valid, const double *__restrict__ lat,
+                                                          const double *__restrict__ lon, int64_t n, TilePartial *__restrict__ out,
+                                                          DevStats *st) {
+    __shared__ LaShared S;
+    for (int s = threadIdx.x; s < LA_SLOTS; s += LA_THREADS) {
+        S.cell[s] = EMPTY_CELL;
+        S.w[s] = EMPTY_WIN;
+        S.cnt[s] = 0;
+        S.ssp[s] = 0.0;
+        S.slat[s] = 0.0;
+        S.slon[s] = 0.0;
+    }
+    if (threadIdx.x == 0) S.occ = 0;
+    __syncthreads();
+    const int64_t nchunks = (n + LA_CHUNK - 1) / LA_CHUNK;
+    for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+        for (int q = 0; q < LA_CHUNK / LA_THREADS; q++) {
+            int64_t i = ch * LA_CHUNK + q * LA_THREADS + threadIdx.x;
+            if (i < n && (flags[i] & F_AGG)) {
+                uint64_t c = cell[i];
+                long long w = wstart[i];
+                bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
+                double sp = sv ? speed[i] : 0.0;
+                double la = lat[i], lo = lon[i];
+                unsigned h = (unsigned)(tile_hash(c, w) & (LA_SLOTS - 1));
+                for (int probe = 0; probe < LA_SLOTS; probe++) {
+                    unsigned long long old = atomicCAS(&S.cell[h], (unsigned long long)EMPTY_CELL, (unsigned long long)c);
+                    if (old == EMPTY_CELL) atomicAdd(&S.occ, 1u);
+                    if (old == EMPTY_CELL || old == c) {
+                        long long ow = (long long)atomicCAS((unsigned long long *)&S.w[h], (unsigned long long)EMPTY_WIN,
+                                                            (unsigned long long)w);
+                        if (ow == EMPTY_WIN || ow == w) break;
+                    }
+                    h = (h + 1) & (LA_SLOTS - 1);
+                }
+                atomicAdd(&S.cnt[h], 1ull | ((unsigned long long)sv << 32));
+                if (sv) atomicAdd(&S.ssp[h], sp);
+                atomicAdd(&S.slat[h], la);
+                atomicAdd(&S.slon[h], lo);
+            }
+        }
+        __syncthreads();
+        if (S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, out, st);
+    }
+    if (S.occ > 0) la_flush(S, out, st);
+}
+
+// =====================================================================================================
+// K3: merge partials into the persistent state table
+// =====================================================================================================
+__device__ __forceinline__ long long find_or_claim_tile(TileSlot *tab, unsigned long long mask, uint64_t c, int64_t w,
+                                                        bool &created) {
+    unsigned long long h = tile_hash(c, w) & mask;
+    created = false;
+    for (unsigned long long probe = 0; probe <= mask; probe++) {
+        TileSlot *s = &tab[h];
+        unsigned long long cur = __hip_atomic_load(&s->cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == EMPTY_CELL) cur = atomicCAS((unsigned long long *)&s->cell, (unsigned long long)EMPTY_CELL, (unsigned long long)c);
+        if (cur == EMPTY_CELL || cur == c) {
+            long long cw = __hip_atomic_load((long long *)&s->wstart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cw == EMPTY_WIN) {
+                cw = (long long)atomicCAS((unsigned long long *)&s->wstart, (unsigned long long)EMPTY_WIN, (unsigned long long)w);
+                if (cw == EMPTY_WIN) { created = true; return (long long)h; }
+            }
+            if (cw == w) return (long long)h;
+        }
+        h = (h + 1) & mask;
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(256) void k_merge(const TilePartial *__restrict__ parts, const unsigned long long *n_parts_dev,
+                                               int64_t n_parts_host, TileSlot *tab, unsigned long long mask,
+                                               unsigned long long seq, unsigned int *touched, DevStats *st) {
+    const int64_t n = n_parts_dev ? (int64_t)*n_parts_dev : n_parts_host;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    long long mn = INT64_MAX;
+    unsigned long long created_cnt = 0;
+    bool overflow = false;
+    // uniform trip count per wave so the ballot in wave_append sees every lane
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+        int64_t i = base + threadIdx.x;
+        bool first = false;
+        long long h = -1;
+        if (i < n) {
+            TilePartial p = parts[i];
+            bool created;
+            h = find_or_claim_tile(tab, mask, p.cell, p.wstart, created);
+            if (h < 0) {
+                overflow = true;
+            } else {
+                TileSlot *s = &tab[h];
+                atomicAdd(&s->count, (unsigned long long)p.count);
+                if (p.nspeed) {
+                    atomicAdd(&s->nspeed, (unsigned long long)p.nspeed);
+                    unsafeAtomicAdd(&s->sspeed, p.sspeed);
+                }
+                unsafeAtomicAdd(&s->slat, p.slat);
+                unsafeAtomicAdd(&s->slon, p.slon);
+                unsigned long long old = atomicMax(&s->touched, seq);
+                first = old < seq;
+                created_cnt += created;
+                mn = p.wstart < mn ? p.wstart : mn;
+            }
+        }
+        unsigned long long pos = wave_append(first, &st->n_touched);
+        if (first) touched[pos] = (unsigned int)h;
+    }
+    created_cnt = wave_sum(created_cnt);
+    mn = wave_min(mn);
+    unsigned long long ov = __ballot(overflow);
+    if (lane_id() == 0) {
+        if (created_cnt) atomicAdd(&st->n_state_new, created_cnt);
+        if (mn != INT64_MAX) atomicMin(&st->min_wstart, mn);
+        if (ov) atomicAdd(&st->overflow, 1ull);
+    }
+}
+
+// =====================================================================================================
+// K4: emit touched keys (update-mode output rows, cumulative aggregates)
+// =====================================================================================================
+__global__ __launch_bounds__(256) void k_emit(const TileSlot *__restrict__ tab, const unsigned int *__restrict__ touched,
+                                              const unsigned long long *n_touched, uint64_t *o_cell, int64_t *o_ws,
+                                              int64_t *o_cnt, double *o_sp, uint8_t *o_spnull, double *o_lon, double *o_lat) {
+    const int64_t n = (int64_t)*n_touched;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
+        const TileSlot s = tab[touched[t]];
+        o_cell[t] = s.cell;
+        o_ws[t] = s.wstart;
+        o_cnt[t] = (int64_t)s.count;
+        // Spark Average: sum / count (count of non-null inputs) as double; null when that count is 0
+        bool null_sp = s.nspeed == 0;
+        o_sp[t] = null_sp ? 0.0 : s.sspeed / (double)s.nspeed;
+        o_spnull[t] = null_sp;
+        o_lon[t] = s.slon / (double)s.count;
+        o_lat[t] = s.slat / (double)s.count;
+    }
+}
+
+// =====================================================================================================
+// state maintenance: rehash (grow) + evict (window end <= watermark)
+// =====================================================================================================
+__global__ __launch_bounds__(256) void k_init_tiles(TileSlot *tab, unsigned long long cap) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)cap; i += stride) {
+        TileSlot s;
+        s.cell = EMPTY_CELL;
+        s.wstart = EMPTY_WIN;
+        s.count = 0;
+        s.nspeed = 0;
+        s.sspeed = 0.0;
+        s.slat = 0.0;
+        s.slon = 0.0;
+        s.touched = 0;
+        tab[i] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_rehash(const TileSlot *__restrict__ old, unsigned long long old_cap, TileSlot *nt,
+                                                unsigned long long new_mask, int64_t tile_us, int64_t evict_end_us,
+                                                DevStats *st) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    long long mn = INT64_MAX;
+    unsigned long long kept = 0;
+    bool overflow = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)old_cap; i += stride) {
+        TileSlot s = old[i];
+        if (s.cell == EMPTY_CELL || s.wstart == EMPTY_WIN) continue;
+        if (s.wstart + tile_us <= evict_end_us) continue;  // evicted: window end <= watermark
+        bool created;
+        long long h = find_or_claim_tile(nt, new_mask, s.cell, s.wstart, created);
+        if (h < 0) { overflow = true; continue; }
+        s.touched = 0;
+        nt[h] = s;
+        kept++;
+        mn = s.wstart < mn ? s.wstart : mn;
+    }
+    kept = wave_sum(kept);
+    mn = wave_min(mn);
+    unsigned long long ov = __ballot(overflow);
+    if (lane_id() == 0) {
+        if (kept) atomicAdd(&st->n_state_new, kept);
+        if (mn != INT64_MAX) atomicMin(&st->min_wstart, mn);
+        if (ov) atomicAdd(&st->overflow, 1ull);
+    }
+}
+
+// =====================================================================================================
+// K5: latest position per (provider, vehicleId)
+// =====================================================================================================
+__device__ __forceinline__ long long find_or_claim_vkey(DedupSlot *tab, unsigned long long mask, unsigned long long v,
+                                                        bool &claimed) {
+    unsigned long long h = vkey_hash(v) & mask;
+    claimed = false;
+    for (unsigned long long probe = 0; probe <= mask; probe++) {
+        unsigned long long cur = __hip_atomic_load(&tab[h].vkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == EMPTY_VKEY) {
+            cur = atomicCAS(&tab[h].vkey, EMPTY_VKEY, v);
+            if (cur == EMPTY_VKEY) { claimed = true; return (long long)h; }
+        }
+        if (cur == v) return (long long)h;
+        h = (h + 1) & mask;
+    }
+    return -1;
+}
+__device__ __forceinline__ long long find_vkey(const DedupSlot *tab, unsigned long long mask, unsigned long long v) {
+    unsigned long long h = vkey_hash(v) & mask;
+    for (unsigned long long probe = 0; probe <= mask; probe++) {
+        unsigned long long cur = tab[h].vkey;
+        if (cur == v) return (long long)h;
+        if (cur == EMPTY_VKEY) return -1;
+        h = (h + 1) & mask;
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(256) void k_init_dedup(DedupSlot *tab, unsigned long long cap) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)cap; i += stride) {
+        tab[i].vkey = EMPTY_VKEY;
+        tab[i].maxts = INT64_MIN;
+    }
+}
+__global__ __launch_bounds__(256) void k_clear_dedup(DedupSlot *tab, const unsigned int *used, const unsigned long long *n_used) {
+    const int64_t n = (int64_t)*n_used;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        tab[used[i]].vkey = EMPTY_VKEY;
+        tab[used[i]].maxts = INT64_MIN;
+    }
+}
+
+// rows (or candidates) -> per-vkey max ts
+__global__ __launch_bounds__(256) void k_dedup_max(const uint64_t *__restrict__ vkey, const int64_t *__restrict__ ts,
+                                                   const uint8_t *__restrict__ flags, const Cand *__restrict__ cands, int64_t n,
+                                                   DedupSlot *tab, unsigned long long mask, unsigned int *used,
+                                                   unsigned long long *n_used, DevStats *st) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    bool overflow = false;
+    unsigned long long bad = 0;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+        int64_t i = base + threadIdx.x;
+        bool claimed = false;
+        long long h = -1;
+        if (i < n) {
+            bool take;
+            unsigned long long v;
+            long long t;
+            if (cands) { take = true; v = cands[i].vkey; t = cands[i].ts; }
+            else { take = (flags[i] & F_VALID) != 0; v = take ? vkey[i] : 0; t = take ? ts[i] : 0; }
+            if (take && v == EMPTY_VKEY) { bad++; take = false; }
+            if (take) {
+                h = find_or_claim_vkey(tab, mask, v, claimed);
+                if (h < 0) overflow = true;
+                else atomicMax(&tab[h].maxts, t);
+            }
+        }
+        unsigned long long pos = wave_append(claimed, n_used);
+        if (claimed) used[pos] = (unsigned int)h;
+    }
+    bad = wave_sum(bad);
+    unsigned long long ov = __ballot(overflow);
+    if (lane_id() == 0) {
+        if (ov) atomicAdd(&st->overflow, 1ull);
+        if (bad) atomicAdd(&st->bad_vkey, bad);
+    }
+}
+
+// winner flag per row (or candidate): ts == max ts of its vkey
+__global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__ vkey, const int64_t *__restrict__ ts,
+                                                    const uint8_t *__restrict__ flags, const Cand *__restrict__ cands, int64_t n,
+                                                    const DedupSlot *__restrict__ tab, unsigned long long mask,
+                                                    uint8_t *__restrict__ win) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        bool take;
+        unsigned long long v;
+        long long t;
+        if (cands) { take = true; v = cands[i].vkey; t = cands[i].ts; }
+        else { take = (flags[i] & F_VALID) != 0; v = take ? vkey[i] : 0; t = take ? ts[i] : 0; }
+        uint8_t w = 0;
+        if (take && v != EMPTY_VKEY) {
+            long long h = find_vkey(tab, mask, v);
+            w = (h >= 0 && tab[h].maxts == t) ? 1 : 0;
+        }
+        win[i] = w;
+    }
+}
+
+// =====================================================================================================
+// ordered compaction of a 0/1 byte array -> indices (deterministic, ascending)
+// =====================================================================================================
+constexpr int CP_THREADS = 256;
+constexpr int CP_PER = 16;
+constexpr int CP_TILE = CP_THREADS * CP_PER;
+
+__device__ __forceinline__ unsigned block_excl_scan(unsigned v, unsigned &total, unsigned *sh) {
+    unsigned incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        unsigned u = __shfl_up(incl, o, 64);
+        if (lane_id() >= o) incl += u;
+    }
+    int wv = threadIdx.x >> 6;
+    if (lane_id() == 63) sh[wv] = incl;
+    __syncthreads();
+    unsigned off = 0;
+    total = 0;
+    for (int q = 0; q < CP_THREADS / 64; q++) {
+        if (q < wv) off += sh[q];
+        total += sh[q];
+    }
+    __syncthreads();
+    return off + incl - v;
+}
+
+__global__ __launch_bounds__(CP_THREADS) void k_cp_count(const uint8_t *__restrict__ f, int64_t n, unsigned *__restrict__ bc) {
+    __shared__ unsigned sh[CP_THREADS / 64];
+    int64_t b0 = (int64_t)blockIdx.x * CP_TILE + (int64_t)threadIdx.x * CP_PER;
+    unsigned c = 0;
+    for (int q = 0; q < CP_PER; q++) {
+        int64_t i = b0 + q;
+        c += (i < n) ? (f[i] != 0) : 0;
+    }
+    unsigned total;
+    block_excl_scan(c, total, sh);
+    if (threadIdx.x == 0) bc[blockIdx.x] = total;
+}
+// single block: exclusive scan of nb block counts (64-bit offsets), total -> *tot
+__global__ __launch_bounds__(1024) void k_cp_scan(const unsigned *__restrict__ bc, int64_t nb, unsigned long long *__restrict__ off,
+                                                  unsigned long long *tot) {
+    __shared__ unsigned long long sh[1024];
+    int64_t per = (nb + 1023) / 1024;
+    int64_t s0 = (int64_t)threadIdx.x * per;
+    unsigned long long sum = 0;
+    for (int64_t q = 0; q < per; q++) if (s0 + q < nb) sum += bc[s0 + q];
+    sh[threadIdx.x] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        unsigned long long v = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
+        __syncthreads();
+        sh[threadIdx.x] += v;
+        __syncthreads();
+    }
+    unsigned long long run = sh[threadIdx.x] - sum;
+    for (int64_t q = 0; q < per; q++)
+        if (s0 + q < nb) { off[s0 + q] = run; run += bc[s0 + q]; }
+    if (threadIdx.x == 1023) *tot = sh[1023];
+}
+__global__ __launch_bounds__(CP_THREADS) void k_cp_write(const uint8_t *__restrict__ f, int64_t n,
+                                                         const unsigned long long *__restrict__ off, int64_t *__restrict__ out) {
+    __shared__ unsigned sh[CP_THREADS / 64];
+    int64_t b0 = (int64_t)blockIdx.x * CP_TILE + (int64_t)threadIdx.x * CP_PER;
+    unsigned c = 0;
+    uint8_t v[CP_PER];
+    for (int q = 0; q < CP_PER; q++) {
+        int64_t i = b0 + q;
+        v[q] = (i < n) ? f[i] : 0;
+        c += v[q] != 0;
+    }
+    unsigned total;
+    unsigned ex = block_excl_scan(c, total, sh);
+    unsigned long long pos = off[blockIdx.x] + ex;
+    for (int q = 0; q < CP_PER; q++)
+        if (v[q]) out[pos++] = b0 + q;
+}
+
+// =====================================================================================================
+// owner partitioning of records for the multi-GPU exchange (counts, then ordered scatter)
+// =====================================================================================================
+template <typename Rec>
+__device__ __forceinline__ int rec_owner(const Rec &r, int nranks);
+template <>
+__device__ __forceinline__ int rec_owner<TilePartial>(const TilePartial &r, int nranks) {
+    return owner_of(tile_hash(r.cell, r.wstart), nranks);
+}
+template <>
+__device__ __forceinline__ int rec_owner<Cand>(const Cand &r, int nranks) {
+    return owner_of(vkey_hash(r.vkey), nranks);
+}
+
+template <typename Rec>
+__global__ __launch_bounds__(256) void k_part_count(const Rec *__restrict__ recs, const unsigned long long *n_dev, int nranks,
+                                                    unsigned long long *counts) {
+    __shared__ unsigned long long sc[64];
+    for (int r = threadIdx.x; r < nranks; r += blockDim.x) sc[r] = 0;
+    __syncthreads();
+    const int64_t n = (int64_t)*n_dev;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        atomicAdd(&sc[rec_owner(recs[i], nranks)], 1ull);
+    __syncthreads();
+    for (int r = threadIdx.x; r < nranks; r += blockDim.x)
+        if (sc[r]) atomicAdd(&counts[r], sc[r]);
+}
+// scatter with per-owner cursors (order within an owner's segment is unspecified)
+template <typename Rec>
+__global__ __launch_bounds__(256) void k_part_scatter(const Rec *__restrict__ recs, const unsigned long long *n_dev, int nranks,
+                                                      unsigned long long *cursor, Rec *__restrict__ out) {
+    const int64_t n = (int64_t)*n_dev;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        Rec r = recs[i];
+        unsigned long long p = atomicAdd(&cursor[rec_owner(r, nranks)], 1ull);
+        out[p] = r;
+    }
+}
+
+// rows flagged as local winners -> candidate records
+__global__ __launch_bounds__(256) void k_make_cands(const int64_t *__restrict__ rows, const unsigned long long *n_dev,
+                                                    const uint64_t *__restrict__ vkey, const int64_t *__restrict__ ts, int rank,
+                                                    Cand *__restrict__ out) {
+    const int64_t n = (int64_t)*n_dev;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        int64_t r = rows[i];
+        Cand c;
+        c.vkey = vkey[r];
+        c.ts = ts[r];
+        c.row = r;
+        c.origin = rank;
+        out[i] = c;
+    }
+}
+// owner-side winners: candidates with win flag -> (origin, row) records grouped by origin
+__global__ __launch_bounds__(256) void k_winner_route(const Cand *__restrict__ cands, const int64_t *__restrict__ widx,
+                                                      const unsigned long long *n_dev, int nranks, unsigned long long *counts_or_cursor,
+                                                      int64_t *__restrict__ out, int pass) {
+    const int64_t n = (int64_t)*n_dev;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const Cand c = cands[widx[i]];
+        int o = (int)c.origin;
+        if (o < 0 || o >= nranks) continue;
+        unsigned long long p = atomicAdd(&counts_or_cursor[o], 1ull);
+        if (pass == 1) out[p] = c.row;
+    }
+}
+
+// =====================================================================================================
+// host side
+// =====================================================================================================
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+struct hm_ctx {
+    hm_config cfg;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    hipEvent_t ev[8] = {};
+    double timings[6] = {0, 0, 0, 0, 0, 0};
+    // per-event
+    DevBuf in_lat, in_lon, in_ts, in_speed, in_sv, in_vkey, in_rv;
+    DevBuf cell, wstart, flags, win, rows, block_counts, block_offs;
+    DevBuf partials, cands;
+    // persistent tile state
+    TileSlot *tab = nullptr;
+    unsigned long long cap = 0;
+    int64_t state_size = 0;
+    int64_t state_min_wstart = INT64_MAX;
+    DevBuf touched;
+    unsigned long long seq = 0;
+    // dedup table (persistent, cleared through its used list)
+    DedupSlot *dtab = nullptr;
+    unsigned long long dcap = 0;
+    DevBuf dused;
+    bool dedup_dirty = false;
+    // outputs (device + pinned host)
+    DevBuf o_cell, o_ws, o_cnt, o_sp, o_spn, o_lon, o_lat;
+    void *h_cell = nullptr, *h_ws = nullptr, *h_cnt = nullptr, *h_sp = nullptr, *h_spn = nullptr, *h_lon = nullptr,
+         *h_lat = nullptr, *h_rows = nullptr;
+    size_t h_tiles_cap = 0, h_rows_cap = 0;
+    // stats
+    DevStats *d_st = nullptr;
+    DevStats *h_st = nullptr;
+    unsigned long long *d_scratch = nullptr;   // 256 words: partition counts/cursors, totals
+    unsigned long long *h_scratch = nullptr;
+    // watermark (ms)
+    int64_t wm_prev = 0, wm_cur = 0;
+    int64_t epoch = -1;
+    // stage API state
+    int stage = 0;
+    int nranks = 1, rank = 0;
+    int64_t stage_n_in = 0;
+    hm_stage_sizes stage_sizes{};
+};
+
+static std::string g_create_err;
+// d_scratch word layout: [0,64) tile partition counts/cursors, [64,128) candidate counts/cursors,
+// DUSED_WORD: used-slot count of the persistent dedup table (survives until the table is cleared),
+// 255: result count of the last ordered compaction
+constexpr int DUSED_WORD = 253;
+
+#define HIPCHK(ctx, expr)                                                                             \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess) {                                                                       \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                           \
+            return HM_E_HIP;                                                                          \
+        }                                                                                             \
+    } while (0)
+
+static int set_err(hm_ctx *ctx, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    ctx->err = buf;
+    return code;
+}
+
+static int ensure(hm_ctx *ctx, DevBuf &b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return HM_OK;
+    if (b.p) {
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, hipFree(b.p));
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    size_t want = std::max<size_t>(bytes, 256);
+    want = (want + 4095) & ~(size_t)4095;
+    if (hipMalloc(&b.p, want) != hipSuccess) {
+        (void)hipGetLastError();
+        return set_err(ctx, HM_E_NOMEM, "hipMalloc(%zu) failed", want);
+    }
+    b.bytes = want;
+    return HM_OK;
+}
+
+static int grid_for(int64_t n, int threads, int max_blocks = 256 * 16) {
+    int64_t b = (n + threads - 1) / threads;
+    if (b < 1) b = 1;
+    if (b > max_blocks) b = max_blocks;
+    return (int)b;
+}
+
+static uint64_t next_pow2(uint64_t v) {
+    uint64_t p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+static int alloc_tiles(hm_ctx *ctx, unsigned long long cap, TileSlot **out) {
+    TileSlot *t = nullptr;
+    if (hipMalloc(&t, cap * sizeof(TileSlot)) != hipSuccess) {
+        (void)hipGetLastError();
+        return set_err(ctx, HM_E_NOMEM, "state table alloc of %llu slots failed", cap);
+    }
+    hipLaunchKernelGGL(k_init_tiles, dim3(grid_for(cap, 256)), dim3(256), 0, ctx->stream, t, cap);
+    HIPCHK(ctx, hipGetLastError());
+    *out = t;
+    return HM_OK;
+}
+
+// evict keys with window end <= wm (ms) and/or grow the table to hold `need` keys at load <= 1/2
+static int state_maintain(hm_ctx *ctx, int64_t evict_wm_ms, int64_t need_keys) {
+    int64_t evict_end_us = evict_wm_ms * 1000;
+    bool evict = ctx->state_size > 0 && ctx->state_min_wstart != INT64_MAX &&
+                 ctx->state_min_wstart + ctx->cfg.tile_us <= evict_end_us;
+    unsigned long long want = ctx->cap;
+    while ((unsigned long long)need_keys * 2 > want) want <<= 1;
+    if (!evict && want == ctx->cap) return HM_OK;
+    TileSlot *nt = nullptr;
+    int rc = alloc_tiles(ctx, want, &nt);
+    if (rc) return rc;
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_st, 0, sizeof(DevStats), ctx->stream));
+    long long init_min = INT64_MAX;
+    HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->min_wstart, &init_min, sizeof(init_min), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_rehash, dim3(grid_for(ctx->cap, 256)), dim3(256), 0, ctx->stream, ctx->tab, ctx->cap, nt, want - 1,
+                       ctx->cfg.tile_us, evict ? evict_end_us : INT64_MIN, ctx->d_st);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "state rehash overflow");
+    HIPCHK(ctx, hipFree(ctx->tab));
+    ctx->tab = nt;
+    ctx->cap = want;
+    ctx->state_size = (int64_t)ctx->h_st->n_state_new;
+    ctx->state_min_wstart = ctx->h_st->min_wstart;
+    return ensure(ctx, ctx->touched, want * sizeof(unsigned int));
+}
+
+static int dedup_prepare(hm_ctx *ctx, int64_t n_upper) {
+    if (ctx->dedup_dirty) {
+        hipLaunchKernelGGL(k_clear_dedup, dim3(grid_for(ctx->dcap, 256)), dim3(256), 0, ctx->stream, ctx->dtab,
+                           (const unsigned int *)ctx->dused.p, ctx->d_scratch + DUSED_WORD);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + DUSED_WORD, 0, 8, ctx->stream));
+        ctx->dedup_dirty = false;
+    }
+    unsigned long long want = next_pow2((unsigned long long)std::max<int64_t>(2 * n_upper, 1024));
+    if (ctx->dtab && ctx->dcap >= want) return HM_OK;
+    if (ctx->dtab) {
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, hipFree(ctx->dtab));
+        ctx->dtab = nullptr;
+    }
+    if (hipMalloc(&ctx->dtab, want * sizeof(DedupSlot)) != hipSuccess) {
+        (void)hipGetLastError();
+        return set_err(ctx, HM_E_NOMEM, "dedup table alloc failed");
+    }
+    ctx->dcap = want;
+    hipLaunchKernelGGL(k_init_dedup, dim3(grid_for(want, 256)), dim3(256), 0, ctx->stream, ctx->dtab, want);
+    HIPCHK(ctx, hipGetLastError());
+    return ensure(ctx, ctx->dused, want * sizeof(unsigned int));
+}
+
+// ordered compaction of byte flags -> int64 indices into ctx->rows; count into d_scratch[255]
+static int compact_flags(hm_ctx *ctx, const uint8_t *f, int64_t n, int64_t *out) {
+    int64_t nb = (n + CP_TILE - 1) / CP_TILE;
+    if (nb < 1) nb = 1;
+    int rc;
+    if ((rc = ensure(ctx, ctx->block_counts, nb * sizeof(unsigned)))) return rc;
+    if ((rc = ensure(ctx, ctx->block_offs, nb * sizeof(unsigned long long)))) return rc;
+    hipLaunchKernelGGL(k_cp_count, dim3(nb), dim3(CP_THREADS), 0, ctx->stream, f, n, (unsigned *)ctx->block_counts.p);
+    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->block_counts.p, nb,
+                       (unsigned long long *)ctx->block_offs.p, ctx->d_scratch + 255);
+    hipLaunchKernelGGL(k_cp_write, dim3(nb), dim3(CP_THREADS), 0, ctx->stream, f, n,
+                       (const unsigned long long *)ctx->block_offs.p, out);
+    HIPCHK(ctx, hipGetLastError());
+    return HM_OK;
+}
+
+static int stage_inputs(hm_ctx *ctx, const hm_batch_in *in, const double **lat, const double **lon, const int64_t **ts,
+                        const double **sp, const uint8_t **sv, const uint64_t **vk, const uint8_t **rv) {
+    int64_t n = in->n;
+    if (in->memory == HM_MEM_DEVICE || n == 0) {
+        *lat = in->lat; *lon = in->lon; *ts = in->ts_us; *sp = in->speed; *sv = in->speed_valid; *vk = in->vkey;
+        *rv = in->row_valid;
+        return HM_OK;
+    }
+    struct { DevBuf *b; const void *src; size_t el; const void **dst; } items[] = {
+        {&ctx->in_lat, in->lat, 8, (const void **)lat},     {&ctx->in_lon, in->lon, 8, (const void **)lon},
+        {&ctx->in_ts, in->ts_us, 8, (const void **)ts},     {&ctx->in_speed, in->speed, 8, (const void **)sp},
+        {&ctx->in_sv, in->speed_valid, 1, (const void **)sv}, {&ctx->in_vkey, in->vkey, 8, (const void **)vk},
+        {&ctx->in_rv, in->row_valid, 1, (const void **)rv},
+    };
+    for (auto &it : items) {
+        if (!it.src) { *it.dst = nullptr; continue; }
+        int rc = ensure(ctx, *it.b, n * it.el);
+        if (rc) return rc;
+        HIPCHK(ctx, hipMemcpyAsync(it.b->p, it.src, n * it.el, hipMemcpyHostToDevice, ctx->stream));
+        *it.dst = it.b->p;
+    }
+    return HM_OK;
+}
+
+static int ensure_host(hm_ctx *ctx, void **p, size_t &cap_el, size_t want_el, size_t el) {
+    (void)cap_el;
+    if (*p) HIPCHK(ctx, hipHostFree(*p));
+    *p = nullptr;
+    HIPCHK(ctx, hipHostMalloc(p, std::max<size_t>(want_el, 1) * el, hipHostMallocDefault));
+    return HM_OK;
+}
+
+// ---- batch phases shared by the single-GPU and stage paths ----
+struct Inputs {
+    const double *lat, *lon, *sp;
+    const int64_t *ts;
+    const uint8_t *sv, *rv;
+    const uint64_t *vk;
+    int64_t n;
+};
+
+static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
+    int64_t n = I.n;
+    int rc;
+    if ((rc = ensure(ctx, ctx->cell, n * 8)) || (rc = ensure(ctx, ctx->wstart, n * 8)) || (rc = ensure(ctx, ctx->flags, n)) ||
+        (rc = ensure(ctx, ctx->win, n)) || (rc = ensure(ctx, ctx->rows, n * 8)) ||
+        (rc = ensure(ctx, ctx->partials, n * sizeof(TilePartial))))
+        return rc;
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_st, 0, sizeof(DevStats), ctx->stream));
+    long long init[2] = {INT64_MIN, INT64_MAX};
+    HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->max_ts_ms, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    if (n > 0) {
+        int64_t late_end_us = late_wm_ms * 1000;
+        hipLaunchKernelGGL(k_snap, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, n,
+                           ctx->cfg.h3_res, ctx->cfg.tile_us, late_end_us, (uint64_t *)ctx->cell.p, (int64_t *)ctx->wstart.p,
+                           (uint8_t *)ctx->flags.p, ctx->d_st);
+        HIPCHK(ctx, hipGetLastError());
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+    if (n > 0) {
+        int64_t nchunks = (n + LA_CHUNK - 1) / LA_CHUNK;
+        int blocks = (int)std::min<int64_t>(nchunks, 256 * 3);
+        hipLaunchKernelGGL(k_local_agg, dim3(blocks), dim3(LA_THREADS), 0, ctx->stream, (const uint64_t *)ctx->cell.p,
+                           (const int64_t *)ctx->wstart.p, (const uint8_t *)ctx->flags.p, I.sp, I.sv, I.lat, I.lon, n,
+                           (TilePartial *)ctx->partials.p, ctx->d_st);
+        HIPCHK(ctx, hipGetLastError());
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    return HM_OK;
+}
+
+// dedup over rows (cands == nullptr) or candidates; result: ctx->rows indices, count in d_scratch[255]
+static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t n) {
+    int rc;
+    if ((rc = dedup_prepare(ctx, n))) return rc;
+    if ((rc = ensure(ctx, ctx->win, std::max<int64_t>(n, 1))) || (rc = ensure(ctx, ctx->rows, std::max<int64_t>(n, 1) * 8)))
+        return rc;
+    if (n > 0) {
+        hipLaunchKernelGGL(k_dedup_max, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, I ? I->vk : nullptr,
+                           I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, ctx->dtab, ctx->dcap - 1,
+                           (unsigned int *)ctx->dused.p, ctx->d_scratch + DUSED_WORD, ctx->d_st);
+        hipLaunchKernelGGL(k_dedup_flag, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, I ? I->vk : nullptr,
+                           I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, ctx->dtab, ctx->dcap - 1,
+                           (uint8_t *)ctx->win.p);
+        HIPCHK(ctx, hipGetLastError());
+        ctx->dedup_dirty = true;
+        if ((rc = compact_flags(ctx, (const uint8_t *)ctx->win.p, n, (int64_t *)ctx->rows.p))) return rc;
+    } else {
+        HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + 255, 0, 8, ctx->stream));
+    }
+    return HM_OK;
+}
+
+static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts, const unsigned long long *n_parts_dev,
+                            int64_t evict_wm_ms) {
+    int rc;
+    // grow (and evict with the previous batch's watermark, already applied) before inserting
+    if ((rc = state_maintain(ctx, INT64_MIN / 1000, ctx->state_size + n_parts))) return rc;
+    (void)evict_wm_ms;
+    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_touched, 0, 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_state_new, 0, 8, ctx->stream));
+    long long init_min = ctx->state_min_wstart;
+    HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->min_wstart, &init_min, sizeof(init_min), hipMemcpyHostToDevice, ctx->stream));
+    ctx->seq++;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    if (n_parts > 0) {
+        hipLaunchKernelGGL(k_merge, dim3(grid_for(n_parts, 256)), dim3(256), 0, ctx->stream, parts, n_parts_dev, n_parts,
+                           ctx->tab, ctx->cap - 1, ctx->seq, (unsigned int *)ctx->touched.p, ctx->d_st);
+        HIPCHK(ctx, hipGetLastError());
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+    if ((rc = ensure(ctx, ctx->o_cell, std::max<int64_t>(n_parts, 1) * 8)) || (rc = ensure(ctx, ctx->o_ws, std::max<int64_t>(n_parts, 1) * 8)) ||
+        (rc = ensure(ctx, ctx->o_cnt, std::max<int64_t>(n_parts, 1) * 8)) || (rc = ensure(ctx, ctx->o_sp, std::max<int64_t>(n_parts, 1) * 8)) ||
+        (rc = ensure(ctx, ctx->o_spn, std::max<int64_t>(n_parts, 1))) || (rc = ensure(ctx, ctx->o_lon, std::max<int64_t>(n_parts, 1) * 8)) ||
+        (rc = ensure(ctx, ctx->o_lat, std::max<int64_t>(n_parts, 1) * 8)))
+        return rc;
+    if (n_parts > 0) {
+        hipLaunchKernelGGL(k_emit, dim3(grid_for(n_parts, 256)), dim3(256), 0, ctx->stream, ctx->tab,
+                           (const unsigned int *)ctx->touched.p, &ctx->d_st->n_touched, (uint64_t *)ctx->o_cell.p,
+                           (int64_t *)ctx->o_ws.p, (int64_t *)ctx->o_cnt.p, (double *)ctx->o_sp.p, (uint8_t *)ctx->o_spn.p,
+                           (double *)ctx->o_lon.p, (double *)ctx->o_lat.p);
+        HIPCHK(ctx, hipGetLastError());
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+    return HM_OK;
+}
+
+static int finish_outputs(hm_ctx *ctx, int64_t n_tiles, int64_t n_rows, const int64_t *rows_dev, int32_t out_memory,
+                          hm_batch_out *out) {
+    out->n_tiles = n_tiles;
+    out->n_latest = n_rows;
+    if (out_memory == HM_MEM_DEVICE) {
+        out->cell = (const uint64_t *)ctx->o_cell.p;
+        out->window_start_us = (const int64_t *)ctx->o_ws.p;
+        out->count = (const int64_t *)ctx->o_cnt.p;
+        out->avg_speed = (const double *)ctx->o_sp.p;
+        out->speed_null = (const uint8_t *)ctx->o_spn.p;
+        out->avg_lon = (const double *)ctx->o_lon.p;
+        out->avg_lat = (const double *)ctx->o_lat.p;
+        out->latest_row = rows_dev;
+        return HM_OK;
+    }
+    int rc;
+    if ((size_t)n_tiles > ctx->h_tiles_cap || !ctx->h_cell) {
+        size_t want = std::max<size_t>((size_t)n_tiles, 1024);
+        size_t dummy = 0;
+        if ((rc = ensure_host(ctx, &ctx->h_cell, dummy, want, 8)) || (rc = ensure_host(ctx, &ctx->h_ws, dummy, want, 8)) ||
+            (rc = ensure_host(ctx, &ctx->h_cnt, dummy, want, 8)) || (rc = ensure_host(ctx, &ctx->h_sp, dummy, want, 8)) ||
+            (rc = ensure_host(ctx, &ctx->h_spn, dummy, want, 1)) || (rc = ensure_host(ctx, &ctx->h_lon, dummy, want, 8)) ||
+            (rc = ensure_host(ctx, &ctx->h_lat, dummy, want, 8)))
+            return rc;
+        ctx->h_tiles_cap = want;
+    }
+    if ((size_t)n_rows > ctx->h_rows_cap || !ctx->h_rows) {
+        size_t want = std::max<size_t>((size_t)n_rows, 1024), dummy = 0;
+        if ((rc = ensure_host(ctx, &ctx->h_rows, dummy, want, 8))) return rc;
+        ctx->h_rows_cap = want;
+    }
+    if (n_tiles > 0) {
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_cell, ctx->o_cell.p, n_tiles * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_ws, ctx->o_ws.p, n_tiles * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_cnt, ctx->o_cnt.p, n_tiles * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_sp, ctx->o_sp.p, n_tiles * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_spn, ctx->o_spn.p, n_tiles, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_lon, ctx->o_lon.p, n_tiles * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_lat, ctx->o_lat.p, n_tiles * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    if (n_rows > 0) HIPCHK(ctx, hipMemcpyAsync(ctx->h_rows, rows_dev, n_rows * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    out->cell = (const uint64_t *)ctx->h_cell;
+    out->window_start_us = (const int64_t *)ctx->h_ws;
+    out->count = (const int64_t *)ctx->h_cnt;
+    out->avg_speed = (const double *)ctx->h_sp;
+    out->speed_null = (const uint8_t *)ctx->h_spn;
+    out->avg_lon = (const double *)ctx->h_lon;
+    out->avg_lat = (const double *)ctx->h_lat;
+    out->latest_row = (const int64_t *)ctx->h_rows;
+    return HM_OK;
+}
+
+static void advance_watermark(hm_ctx *ctx, int64_t batch_max_ms) {
+    // Spark WatermarkTracker: global = max(global, batch max event time - delay); starts at 0
+    int64_t next = ctx->wm_cur;
+    if (batch_max_ms != INT64_MIN) {
+        int64_t cand = batch_max_ms - ctx->cfg.watermark_delay_ms;
+        if (cand > next) next = cand;
+    }
+    ctx->wm_prev = ctx->wm_cur;
+    ctx->wm_cur = next;
+}
+
+static void fill_stats(hm_ctx *ctx, hm_batch_out *out, int64_t n_in, const DevStats &s, int64_t late_wm) {
+    out->n_in = n_in;
+    out->n_valid = (int64_t)s.n_valid;
+    out->n_late = (int64_t)s.n_late;
+    out->n_state = ctx->state_size;
+    out->batch_max_event_ms = s.max_ts_ms;
+    out->watermark_ms = ctx->wm_cur;
+    out->late_watermark_ms = late_wm;
+}
+
+static void record_timings(hm_ctx *ctx) {
+    float t;
+    auto el = [&](int a, int b) -> double { return hipEventElapsedTime(&t, ctx->ev[a], ctx->ev[b]) == hipSuccess ? t : -1.0; };
+    ctx->timings[0] = el(0, 1);
+    ctx->timings[1] = el(1, 2);
+    ctx->timings[2] = el(3, 4);
+    ctx->timings[3] = el(4, 5);
+    ctx->timings[4] = el(5, 6);
+    ctx->timings[5] = el(0, 6);
+}
+
+extern "C" {
+
+int hm_create(const hm_config *cfg, hm_ctx **out) {
+    g_create_err.clear();
+    if (!cfg || !out) { g_create_err = "null argument"; return HM_E_INVALID; }
+    if (cfg->abi_version != HM_ABI_VERSION) { g_create_err = "ABI version mismatch"; return HM_E_INVALID; }
+    if (cfg->h3_res < 0 || cfg->h3_res > 15) { g_create_err = "h3_res out of range"; return HM_E_INVALID; }
+    if (cfg->tile_us <= 0 || cfg->watermark_delay_ms < 0) { g_create_err = "bad tile/watermark"; return HM_E_INVALID; }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        g_create_err = "no HIP device available (the mobheat hot path requires an MI355X GPU)";
+        return HM_E_HIP;
+    }
+    if (cfg->device < 0 || cfg->device >= ndev) { g_create_err = "device ordinal out of range"; return HM_E_INVALID; }
+    hm_ctx *ctx = new hm_ctx();
+    ctx->cfg = *cfg;
+    ctx->device = cfg->device;
+    auto fail = [&](const char *what) {
+        g_create_err = std::string(what) + ": " + ctx->err;
+        hm_destroy(ctx);
+        return HM_E_HIP;
+    };
+    if (hipSetDevice(ctx->device) != hipSuccess) { ctx->err = "hipSetDevice"; return fail("create"); }
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { ctx->err = "stream"; return fail("create"); }
+    for (auto &e : ctx->ev)
+        if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
+    H3Tables T = make_tables();
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &T, sizeof(T)) != hipSuccess) { ctx->err = "tables"; return fail("create"); }
+    if (hipMalloc(&ctx->d_st, sizeof(DevStats)) != hipSuccess || hipHostMalloc(&ctx->h_st, sizeof(DevStats)) != hipSuccess ||
+        hipMalloc(&ctx->d_scratch, 256 * 8) != hipSuccess || hipHostMalloc(&ctx->h_scratch, 256 * 8) != hipSuccess) {
+        ctx->err = "stats alloc";
+        return fail("create");
+    }
+    if (hipMemset(ctx->d_scratch, 0, 256 * 8) != hipSuccess) { ctx->err = "scratch init"; return fail("create"); }
+    unsigned long long cap = next_pow2((unsigned long long)std::max<int64_t>(cfg->state_capacity_hint, 1 << 16));
+    if (alloc_tiles(ctx, cap, &ctx->tab)) return fail("create");
+    ctx->cap = cap;
+    if (ensure(ctx, ctx->touched, cap * sizeof(unsigned int))) return fail("create");
+    if (cfg->batch_capacity_hint > 0) {
+        if (dedup_prepare(ctx, cfg->batch_capacity_hint)) return fail("create");
+    }
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) { ctx->err = "sync"; return fail("create"); }
+    *out = ctx;
+    return HM_OK;
+}
+
+void hm_destroy(hm_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    DevBuf *bufs[] = {&ctx->in_lat, &ctx->in_lon, &ctx->in_ts, &ctx->in_speed, &ctx->in_sv, &ctx->in_vkey, &ctx->in_rv,
+                      &ctx->cell, &ctx->wstart, &ctx->flags, &ctx->win, &ctx->rows, &ctx->block_counts, &ctx->block_offs,
+                      &ctx->partials, &ctx->cands,
+                      &ctx->touched, &ctx->dused, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
+                      &ctx->o_lon, &ctx->o_lat};
+    for (DevBuf *b : bufs)
+        if (b->p) (void)hipFree(b->p);
+    if (ctx->tab) (void)hipFree(ctx->tab);
+    if (ctx->dtab) (void)hipFree(ctx->dtab);
+    void *hbufs[] = {ctx->h_cell, ctx->h_ws, ctx->h_cnt, ctx->h_sp, ctx->h_spn, ctx->h_lon, ctx->h_lat, ctx->h_rows};
+    for (void *p : hbufs)
+        if (p) (void)hipHostFree(p);
+    if (ctx->d_st) (void)hipFree(ctx->d_st);
+    if (ctx->h_st) (void)hipHostFree(ctx->h_st);
+    if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    if (ctx->h_scratch) (void)hipHostFree(ctx->h_scratch);
+    for (auto &e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *hm_last_error(const hm_ctx *ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
+
+int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n) {
+    if (!ctx || !ms) return HM_E_INVALID;
+    for (int i = 0; i < n && i < 6; i++) ms[i] = ctx->timings[i];
+    return HM_OK;
+}
+
+int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t out_memory, hm_batch_out *out) {
+    if (!ctx || !in || !out || in->n < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (in->n > 0 && (!in->lat || !in->lon || !in->ts_us || !in->vkey))
+        return set_err(ctx, HM_E_INVALID, "lat, lon, ts_us and vkey are required");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    memset(out, 0, sizeof(*out));
+    ctx->epoch = epoch_id;
+    int rc;
+    // 1. evict with this batch's eviction watermark happened at the end of the previous batch (see below)
+    int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
+    Inputs I;
+    I.n = in->n;
+    if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
+    // 2. snap + local pre-aggregation
+    if ((rc = phase_local(ctx, I, late_wm))) return rc;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    DevStats s1 = *ctx->h_st;
+    // 3. merge into state + emit
+    if ((rc = phase_merge_emit(ctx, (const TilePartial *)ctx->partials.p, (int64_t)s1.n_partials, nullptr, ctx->wm_cur))) return rc;
+    // 4. dedup over the batch's valid rows
+    if ((rc = phase_dedup(ctx, &I, nullptr, I.n))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch + 255, ctx->d_scratch + 255, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    DevStats s2 = *ctx->h_st;
+    if (s2.overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
+    if (s2.bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved (%llu rows)", s2.bad_vkey);
+    ctx->state_size += (int64_t)s2.n_state_new;
+    ctx->state_min_wstart = s2.min_wstart;
+    int64_t n_rows = (int64_t)ctx->h_scratch[255];
+    record_timings(ctx);
+    if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, n_rows, (const int64_t *)ctx->rows.p, out_memory, out))) return rc;
+    DevStats sf = s1;
+    fill_stats(ctx, out, in->n, sf, late_wm);
+    // 5. eviction of this batch (window end <= this batch's watermark) after emission, then advance
+    int64_t evict_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_cur : ctx->wm_cur;
+    if ((rc = state_maintain(ctx, evict_wm, ctx->state_size))) return rc;
+    out->n_state = ctx->state_size;
+    advance_watermark(ctx, s1.max_ts_ms);
+    return HM_OK;
+}
+
+int hm_latlng_to_cell(const double *lat, const double *lon, int64_t n, int32_t res, int32_t memory, int32_t device,
+                      uint64_t *out) {
+    if (n < 0 || res < 0 || res > 15) return HM_E_INVALID;
+    if (n == 0) return HM_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device) return HM_E_HIP;
+    if (hipSetDevice(device) != hipSuccess) return HM_E_HIP;
+    static bool tables_loaded[64] = {};
+    if (!tables_loaded[device]) {
+        H3Tables T = make_tables();
+        if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &T, sizeof(T)) != hipSuccess) return HM_E_HIP;
+        tables_loaded[device] = true;
+    }
+    const double *dlat = lat, *dlon = lon;
+    uint64_t *dout = out;
+    void *a = nullptr, *b = nullptr, *c = nullptr;
+    if (memory == HM_MEM_HOST) {
+        if (hipMalloc(&a, n * 8) || hipMalloc(&b, n * 8) || hipMalloc(&c, n * 8)) return HM_E_NOMEM;
+        if (hipMemcpy(a, lat, n * 8, hipMemcpyHostToDevice) || hipMemcpy(b, lon, n * 8, hipMemcpyHostToDevice)) return HM_E_HIP;
+        dlat = (const double *)a;
+        dlon = (const double *)b;
+        dout = (uint64_t *)c;
+    }
+    hipLaunchKernelGGL(k_cells, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, 0, dlat, dlon, n, res, dout);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess && memory == HM_MEM_HOST) e = hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost);
+    if (a) (void)hipFree(a);
+    if (b) (void)hipFree(b);
+    if (c) (void)hipFree(c);
+    return e == hipSuccess ? HM_OK : HM_E_HIP;
+}
+
+// ---- multi-GPU stage API ----
+int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t nranks, int32_t rank, void *tile_send_buf,
+                   int64_t tile_send_cap, int64_t *tile_send_counts, void *cand_send_buf, int64_t cand_send_cap,
+                   int64_t *cand_send_counts, hm_stage_sizes *sizes) {
+    if (!ctx || !in || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks || !tile_send_counts || !cand_send_counts ||
+        (in->n > 0 && (!tile_send_buf || !cand_send_buf)))
+        return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (in->n > 0 && (!in->lat || !in->lon || !in->ts_us || !in->vkey))
+        return set_err(ctx, HM_E_INVALID, "lat, lon, ts_us and vkey are required");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc;
+    ctx->epoch = epoch_id;
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
+    Inputs I;
+    I.n = in->n;
+    if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
+    if ((rc = phase_local(ctx, I, late_wm))) return rc;
+    // local dedup over rows -> local winners -> candidates
+    if ((rc = phase_dedup(ctx, &I, nullptr, I.n))) return rc;
+    if ((rc = ensure(ctx, ctx->cands, std::max<int64_t>(I.n, 1) * sizeof(Cand)))) return rc;
+    hipLaunchKernelGGL(k_make_cands, dim3(grid_for(std::max<int64_t>(I.n, 1), 256)), dim3(256), 0, ctx->stream,
+                       (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, I.vk, I.ts, rank, (Cand *)ctx->cands.p);
+    HIPCHK(ctx, hipGetLastError());
+    // partition both record kinds by owner rank
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch, 0, 128 * 8, ctx->stream));
+    int gb = grid_for(std::max<int64_t>(I.n, 1), 256);
+    hipLaunchKernelGGL(k_part_count<TilePartial>, dim3(gb), dim3(256), 0, ctx->stream, (const TilePartial *)ctx->partials.p,
+                       &ctx->d_st->n_partials, nranks, ctx->d_scratch);
+    hipLaunchKernelGGL(k_part_count<Cand>, dim3(gb), dim3(256), 0, ctx->stream, (const Cand *)ctx->cands.p, ctx->d_scratch + 255,
+                       nranks, ctx->d_scratch + 64);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 256 * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
+    if (ctx->h_st->bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved");
+    if ((int64_t)ctx->h_st->n_partials > tile_send_cap || (int64_t)ctx->h_scratch[255] > cand_send_cap)
+        return set_err(ctx, HM_E_INVALID, "send buffer too small (%llu tiles, %llu candidates)", ctx->h_st->n_partials,
+                       ctx->h_scratch[255]);
+    // exclusive offsets -> cursors
+    unsigned long long cur[128];
+    unsigned long long acc = 0;
+    for (int r = 0; r < nranks; r++) { cur[r] = acc; tile_send_counts[r] = (int64_t)ctx->h_scratch[r]; acc += ctx->h_scratch[r]; }
+    acc = 0;
+    for (int r = 0; r < nranks; r++) { cur[64 + r] = acc; cand_send_counts[r] = (int64_t)ctx->h_scratch[64 + r]; acc += ctx->h_scratch[64 + r]; }
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_scratch, cur, 128 * 8, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_part_scatter<TilePartial>, dim3(gb), dim3(256), 0, ctx->stream, (const TilePartial *)ctx->partials.p,
+                       &ctx->d_st->n_partials, nranks, ctx->d_scratch, (TilePartial *)tile_send_buf);
+    hipLaunchKernelGGL(k_part_scatter<Cand>, dim3(gb), dim3(256), 0, ctx->stream, (const Cand *)ctx->cands.p, ctx->d_scratch + 255,
+                       nranks, ctx->d_scratch + 64, (Cand *)cand_send_buf);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (sizes) {
+        sizes->n_tile_partials = (int64_t)ctx->h_st->n_partials;
+        sizes->n_cands = 0;
+        for (int r = 0; r < nranks; r++) sizes->n_cands += cand_send_counts[r];
+        sizes->batch_max_event_ms = ctx->h_st->max_ts_ms;
+        sizes->n_valid = (int64_t)ctx->h_st->n_valid;
+        sizes->n_late = (int64_t)ctx->h_st->n_late;
+        ctx->stage_sizes = *sizes;
+    }
+    ctx->stage_n_in = I.n;
+    ctx->stage = 1;
+    return HM_OK;
+}
+
+int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, const void *cand_recv_dev, int64_t n_cand_recv,
+                   int64_t global_batch_max_event_ms, int32_t out_memory, hm_batch_out *out, void *winner_send_buf,
+                   int64_t winner_send_cap, int64_t *winner_send_counts) {
+    if (!ctx || !out || !winner_send_counts || n_tile_recv < 0 || n_cand_recv < 0 || winner_send_cap < n_cand_recv ||
+        (n_cand_recv > 0 && !winner_send_buf))
+        return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->stage != 1) return set_err(ctx, HM_E_STATE, "hm_stage_merge before hm_stage_local");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc;
+    memset(out, 0, sizeof(*out));
+    int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
+    if ((rc = phase_merge_emit(ctx, (const TilePartial *)tile_recv_dev, n_tile_recv, nullptr, ctx->wm_cur))) return rc;
+    // owner-side dedup over received candidates
+    if ((rc = phase_dedup(ctx, nullptr, (const Cand *)cand_recv_dev, n_cand_recv))) return rc;
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch, 0, 128 * 8, ctx->stream));
+    if (n_cand_recv > 0) {
+        hipLaunchKernelGGL(k_winner_route, dim3(grid_for(n_cand_recv, 256)), dim3(256), 0, ctx->stream, (const Cand *)cand_recv_dev,
+                           (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, ctx->nranks, ctx->d_scratch, (int64_t *)nullptr, 0);
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 256 * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    DevStats s2 = *ctx->h_st;
+    if (s2.overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
+    unsigned long long cur[64];
+    unsigned long long acc = 0;
+    for (int r = 0; r < ctx->nranks; r++) { cur[r] = acc; winner_send_counts[r] = (int64_t)ctx->h_scratch[r]; acc += ctx->h_scratch[r]; }
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_scratch, cur, 64 * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (n_cand_recv > 0) {
+        hipLaunchKernelGGL(k_winner_route, dim3(grid_for(n_cand_recv, 256)), dim3(256), 0, ctx->stream, (const Cand *)cand_recv_dev,
+                           (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, ctx->nranks, ctx->d_scratch,
+                           (int64_t *)winner_send_buf, 1);
+        HIPCHK(ctx, hipGetLastError());
+    }
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->state_size += (int64_t)s2.n_state_new;
+    ctx->state_min_wstart = s2.min_wstart;
+    record_timings(ctx);
+    if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, 0, nullptr, out_memory, out))) return rc;
+    DevStats sf{};
+    sf.n_valid = ctx->stage_sizes.n_valid;
+    sf.n_late = ctx->stage_sizes.n_late;
+    sf.max_ts_ms = global_batch_max_event_ms;
+    fill_stats(ctx, out, ctx->stage_n_in, sf, late_wm);
+    if ((rc = state_maintain(ctx, ctx->wm_cur, ctx->state_size))) return rc;
+    out->n_state = ctx->state_size;
+    advance_watermark(ctx, global_batch_max_event_ms);
+    ctx->stage = 2;
+    return HM_OK;
+}
+
+int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_recv, int32_t out_memory, hm_batch_out *out) {
+    if (!ctx || !out || n_winner_recv < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->stage != 2) return set_err(ctx, HM_E_STATE, "hm_stage_finish before hm_stage_merge");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc;
+    out->n_latest = n_winner_recv;
+    if (out_memory == HM_MEM_DEVICE) {
+        out->latest_row = (const int64_t *)winner_recv_dev;
+    } else {
+        if ((size_t)n_winner_recv > ctx->h_rows_cap || !ctx->h_rows) {
+            size_t want = std::max<size_t>((size_t)n_winner_recv, 1024), dummy = 0;
+            if ((rc = ensure_host(ctx, &ctx->h_rows, dummy, want, 8))) return rc;
+            ctx->h_rows_cap = want;
+        }
+        if (n_winner_recv > 0)
+            HIPCHK(ctx, hipMemcpyAsync(ctx->h_rows, winner_recv_dev, n_winner_recv * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        std::sort((int64_t *)ctx->h_rows, (int64_t *)ctx->h_rows + n_winner_recv);
+        out->latest_row = (const int64_t *)ctx->h_rows;
+    }
+    ctx->stage = 0;
+    return HM_OK;
+}
+
+int hm_device_alloc(int32_t device, int64_t bytes, void **ptr) {
+    if (!ptr || bytes < 0) return HM_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return HM_E_HIP;
+    return hipMalloc(ptr, std::max<int64_t>(bytes, 16)) == hipSuccess ? HM_OK : HM_E_NOMEM;
+}
+int hm_device_free(int32_t device, void *ptr) {
+    if (hipSetDevice(device) != hipSuccess) return HM_E_HIP;
+    return hipFree(ptr) == hipSuccess ? HM_OK : HM_E_HIP;
+}
+int hm_memcpy(void *dst, const void *src, int64_t bytes, int32_t kind) {
+    hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    return hipMemcpy(dst, src, bytes, k) == hipSuccess ? HM_OK : HM_E_HIP;
+}
+
+int hm_selftest_ld_ops(const double *a, int64_t n, int32_t op, double *out) {
+    if (!a || !out || n < 0) return HM_E_INVALID;
+    for (int64_t i = 0; i < n; i++) {
+        double x = a[i], r;
+        switch (op) {
+            case 0: r = xld_mul(x, HM_LD_PI_180_M, HM_LD_PI_180_E); break;
+            case 1: r = xld_mul(x, HM_LD_SQRT7_M, HM_LD_SQRT7_E); break;
+            case 2: r = xld_mul(x, HM_LD_RSIN60_M, HM_LD_RSIN60_E); break;
+            case 3: r = xld_add(x, false, HM_LD_2PI_M, HM_LD_2PI_E); break;
+            case 4: r = xld_add(x, true, HM_LD_2PI_M, HM_LD_2PI_E); break;
+            case 5: r = xld_add(x, true, HM_LD_AP7_ROT_M, HM_LD_AP7_ROT_E); break;
+            case 6: r = xld_add(x, false, HM_LD_AP7_ROT_M, HM_LD_AP7_ROT_E); break;
+            default: return HM_E_INVALID;
+        }
+        out[i] = r;
+    }
+    return HM_OK;
+}
+
+int hm_selftest_latlng_to_cell_host(const double *lat, const double *lon, int64_t n, int32_t res, uint64_t *out) {
+    if (!lat || !lon || !out || n < 0 || res < 0 || res > 15) return HM_E_INVALID;
+    static const H3Tables T = make_tables();
+    for (int64_t i = 0; i < n; i++) out[i] = latLngToCellDeg(lat[i], lon[i], res, T);
+    return HM_OK;
+}
+
+}  // extern "C"

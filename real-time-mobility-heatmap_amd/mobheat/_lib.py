@@ -1,0 +1,127 @@
+"""ctypes binding of libmobheat.so (C ABI declared in include/mobheat.h).
+
+The library is built in-tree (``real-time-mobility-heatmap_amd/csrc/libmobheat.so``); there is no CPU fallback:
+if it cannot be loaded, every entry point raises.  Negative return codes raise ``RuntimeError`` with the
+library's message, which keeps the reference's fail-the-batch behaviour (reference heatmap_stream.py:192-235
+has no try/except around the writes; any exception kills the streaming query at :249).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
+
+HM_ABI_VERSION = 1
+HM_MEM_HOST = 0
+HM_MEM_DEVICE = 1
+HM_TILE_REC_BYTES = 56
+HM_CAND_REC_BYTES = 32
+
+c_i32, c_i64, c_u64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double, ctypes.c_void_p
+
+
+class HmConfig(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", c_i32), ("h3_res", c_i32), ("device", c_i32), ("late_uses_prev_watermark", c_i32),
+        ("tile_us", c_i64), ("watermark_delay_ms", c_i64), ("state_capacity_hint", c_i64),
+        ("batch_capacity_hint", c_i64),
+    ]
+
+
+class HmBatchIn(ctypes.Structure):
+    _fields_ = [
+        ("n", c_i64), ("memory", c_i32), ("reserved", c_i32),
+        ("lat", c_vp), ("lon", c_vp), ("ts_us", c_vp), ("speed", c_vp), ("speed_valid", c_vp),
+        ("vkey", c_vp), ("row_valid", c_vp),
+    ]
+
+
+class HmBatchOut(ctypes.Structure):
+    _fields_ = [
+        ("n_tiles", c_i64), ("cell", c_vp), ("window_start_us", c_vp), ("count", c_vp), ("avg_speed", c_vp),
+        ("speed_null", c_vp), ("avg_lon", c_vp), ("avg_lat", c_vp),
+        ("n_latest", c_i64), ("latest_row", c_vp),
+        ("n_in", c_i64), ("n_valid", c_i64), ("n_late", c_i64), ("n_state", c_i64),
+        ("batch_max_event_ms", c_i64), ("watermark_ms", c_i64), ("late_watermark_ms", c_i64),
+    ]
+
+
+class HmStageSizes(ctypes.Structure):
+    _fields_ = [("n_tile_partials", c_i64), ("n_cands", c_i64), ("batch_max_event_ms", c_i64),
+                ("n_valid", c_i64), ("n_late", c_i64)]
+
+
+_P = ctypes.POINTER
+# name -> (restype, argtypes); must match include/mobheat.h (tests/test_abi.py checks the symbol set)
+SIGNATURES = {
+    "hm_create": (c_i32, [_P(HmConfig), _P(c_vp)]),
+    "hm_destroy": (None, [c_vp]),
+    "hm_last_error": (ctypes.c_char_p, [c_vp]),
+    "hm_process_batch": (c_i32, [c_vp, c_i64, _P(HmBatchIn), c_i32, _P(HmBatchOut)]),
+    "hm_latlng_to_cell": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp]),
+    "hm_stage_local": (c_i32, [c_vp, c_i64, _P(HmBatchIn), c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
+                               _P(HmStageSizes)]),
+    "hm_stage_merge": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, _P(HmBatchOut), c_vp, c_i64, c_vp]),
+    "hm_stage_finish": (c_i32, [c_vp, c_vp, c_i64, c_i32, _P(HmBatchOut)]),
+    "hm_device_alloc": (c_i32, [c_i32, c_i64, _P(c_vp)]),
+    "hm_device_free": (c_i32, [c_i32, c_vp]),
+    "hm_memcpy": (c_i32, [c_vp, c_vp, c_i64, c_i32]),
+    "hm_selftest_ld_ops": (c_i32, [c_vp, c_i64, c_i32, c_vp]),
+    "hm_selftest_latlng_to_cell_host": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp]),
+    "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libmobheat.so (raises if it is missing: the product path never falls back to the CPU)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libmobheat.so not built at {LIB_PATH}; run __graft_entry__.build() (or make -C csrc)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, ctx=None, what="mobheat"):
+    if rc < 0:
+        lib = load()
+        msg = lib.hm_last_error(ctx)
+        raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+    return rc
+
+
+def ptr(a):
+    """Address of a contiguous numpy array (or None)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays must be contiguous"
+    return a.ctypes.data
+
+
+def ld_ops_selftest(a, op):
+    """Host execution of the kernels' x87 emulation (see hm_selftest_ld_ops)."""
+    lib = load()
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    out = np.empty_like(a)
+    check(lib.hm_selftest_ld_ops(ptr(a), a.size, op, ptr(out)))
+    return out
+
+
+def latlng_to_cell_host_selftest(lat, lon, res):
+    """Host execution of the device latLngToCell code (host libm transcendentals) -- debugging aid only."""
+    lib = load()
+    lat = np.ascontiguousarray(lat, dtype=np.float64)
+    lon = np.ascontiguousarray(lon, dtype=np.float64)
+    out = np.empty(lat.size, dtype=np.uint64)
+    check(lib.hm_selftest_latlng_to_cell_host(ptr(lat), ptr(lon), lat.size, res, ptr(out)))
+    return out

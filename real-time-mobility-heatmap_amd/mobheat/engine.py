@@ -1,0 +1,137 @@
+"""HeatmapEngine: one device context running the per-micro-batch hot path on one GPU.
+
+Wraps hm_create / hm_process_batch / hm_destroy (include/mobheat.h).  The engine owns the persistent
+tile state (Spark's state store for the window aggregation, reference heatmap_stream.py:111-133 in
+update mode, :243) and the watermark bookkeeping (withWatermark 10 minutes, :107).
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import HM_MEM_DEVICE, HM_MEM_HOST, HmBatchIn, HmBatchOut, HmConfig, check, ptr
+
+
+@dataclass
+class TileRows:
+    """Update-mode output of the tiles aggregation (reference heatmap_stream.py:124-132)."""
+    cell: np.ndarray            # uint64 H3 index (cellId = format(cell, 'x'))
+    window_start_us: np.ndarray  # int64
+    window_end_us: np.ndarray    # int64
+    count: np.ndarray            # int64
+    avg_speed: np.ndarray        # float64 (0.0 where speed_null)
+    speed_null: np.ndarray       # bool: avg(speedKmh) is null (no non-null speed in the group)
+    avg_lon: np.ndarray          # float64
+    avg_lat: np.ndarray          # float64
+
+    def __len__(self):
+        return int(self.cell.size)
+
+
+@dataclass
+class BatchResult:
+    tiles: TileRows
+    latest_rows: np.ndarray     # int64 row indices of the in-batch latest positions (ties included)
+    n_in: int
+    n_valid: int
+    n_late: int
+    n_state: int
+    batch_max_event_ms: int
+    watermark_ms: int
+    late_watermark_ms: int
+
+
+def _u8(a, n):
+    if a is None:
+        return None
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.bool_:
+        a = a.view(np.uint8)
+    assert a.dtype == np.uint8 and a.size == n
+    return a
+
+
+class HeatmapEngine:
+    def __init__(self, h3_res=8, tile_minutes=5, watermark_delay_ms=600_000, device=0,
+                 late_uses_prev_watermark=True, state_capacity_hint=0, batch_capacity_hint=0):
+        self._lib = _lib.load()
+        self.h3_res = int(h3_res)
+        self.tile_us = int(tile_minutes) * 60 * 1_000_000
+        self.device = int(device)
+        cfg = HmConfig(abi_version=_lib.HM_ABI_VERSION, h3_res=self.h3_res, device=self.device,
+                       late_uses_prev_watermark=1 if late_uses_prev_watermark else 0, tile_us=self.tile_us,
+                       watermark_delay_ms=int(watermark_delay_ms), state_capacity_hint=int(state_capacity_hint),
+                       batch_capacity_hint=int(batch_capacity_hint))
+        h = ctypes.c_void_p()
+        check(self._lib.hm_create(ctypes.byref(cfg), ctypes.byref(h)), None, "hm_create")
+        self._ctx = h
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.hm_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- host-memory batch (the foreach_batch_func path) ----
+    def process_batch(self, epoch_id, lat, lon, ts_us, speed=None, speed_valid=None, vkey=None, row_valid=None):
+        n = int(np.asarray(lat).size)
+        lat = np.ascontiguousarray(lat, dtype=np.float64)
+        lon = np.ascontiguousarray(lon, dtype=np.float64)
+        ts_us = np.ascontiguousarray(ts_us, dtype=np.int64)
+        assert lon.size == n and ts_us.size == n
+        speed = None if speed is None else np.ascontiguousarray(speed, dtype=np.float64)
+        vkey = np.zeros(n, np.uint64) if vkey is None else np.ascontiguousarray(vkey, dtype=np.uint64)
+        b = HmBatchIn(n=n, memory=HM_MEM_HOST, lat=ptr(lat), lon=ptr(lon), ts_us=ptr(ts_us), speed=ptr(speed),
+                      speed_valid=ptr(_u8(speed_valid, n)), vkey=ptr(vkey), row_valid=ptr(_u8(row_valid, n)))
+        out = HmBatchOut()
+        check(self._lib.hm_process_batch(self._ctx, int(epoch_id), ctypes.byref(b), HM_MEM_HOST, ctypes.byref(out)),
+              self._ctx, "hm_process_batch")
+        return self._result_from_host(out)
+
+    # ---- device-resident batch (bench / multi-GPU): raw device pointers, results stay on the device ----
+    def process_batch_device(self, epoch_id, n, lat, lon, ts_us, speed, speed_valid, vkey, row_valid):
+        b = HmBatchIn(n=int(n), memory=HM_MEM_DEVICE, lat=lat, lon=lon, ts_us=ts_us, speed=speed,
+                      speed_valid=speed_valid, vkey=vkey, row_valid=row_valid)
+        out = HmBatchOut()
+        check(self._lib.hm_process_batch(self._ctx, int(epoch_id), ctypes.byref(b), HM_MEM_DEVICE,
+                                         ctypes.byref(out)), self._ctx, "hm_process_batch")
+        return out
+
+    def last_timings(self):
+        ms = (ctypes.c_double * 6)()
+        check(self._lib.hm_last_timings(self._ctx, ms, 6), self._ctx)
+        return {"snap": ms[0], "local_agg": ms[1], "merge": ms[2], "emit": ms[3], "dedup": ms[4], "total": ms[5]}
+
+    def _result_from_host(self, out):
+        def arr(p, n, dt):
+            if n == 0 or not p:
+                return np.zeros(0, dt)
+            return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                         shape=(n,)).copy()
+        nt = int(out.n_tiles)
+        ws = arr(out.window_start_us, nt, np.int64)
+        tiles = TileRows(cell=arr(out.cell, nt, np.uint64), window_start_us=ws, window_end_us=ws + self.tile_us,
+                         count=arr(out.count, nt, np.int64), avg_speed=arr(out.avg_speed, nt, np.float64),
+                         speed_null=arr(out.speed_null, nt, np.uint8).astype(bool),
+                         avg_lon=arr(out.avg_lon, nt, np.float64), avg_lat=arr(out.avg_lat, nt, np.float64))
+        return BatchResult(tiles=tiles, latest_rows=arr(out.latest_row, int(out.n_latest), np.int64),
+                           n_in=int(out.n_in), n_valid=int(out.n_valid), n_late=int(out.n_late),
+                           n_state=int(out.n_state), batch_max_event_ms=int(out.batch_max_event_ms),
+                           watermark_ms=int(out.watermark_ms), late_watermark_ms=int(out.late_watermark_ms))
+
+
+def latlng_to_cell(lat, lon, res, device=0):
+    """The reference UDF's arithmetic (h3.latlng_to_cell) for arrays, on the GPU. 0 = None."""
+    lib = _lib.load()
+    lat = np.ascontiguousarray(lat, dtype=np.float64)
+    lon = np.ascontiguousarray(lon, dtype=np.float64)
+    out = np.empty(lat.size, dtype=np.uint64)
+    check(lib.hm_latlng_to_cell(ptr(lat), ptr(lon), lat.size, int(res), HM_MEM_HOST, int(device), ptr(out)),
+          None, "hm_latlng_to_cell")
+    return out

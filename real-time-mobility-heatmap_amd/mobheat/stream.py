@@ -1,0 +1,231 @@
+"""Host-side mirror of the reference job's batch writer (reference heatmap_stream.py).
+
+Keeps the reference's interface for this path:
+  * module-level configuration from the same environment variables (heatmap_stream.py:21-37):
+    MONGO_URI, MONGO_DB, CITY, H3_RES, TILE_MINUTES, TTL_MINUTES
+  * ``foreach_batch_func(df, epoch_id)`` with the same signature (:150), called once per micro-batch, in order;
+  * the MongoDB ``tiles`` and ``positions_latest`` documents built exactly as :164-188 and :211-228, written
+    with ``UpdateOne(..., upsert=True)`` in unordered bulks of 1000 (:191-196, :230-235), tiles first;
+  * a MongoClient opened and closed per batch (:156, :237); any exception propagates and fails the batch.
+
+What changes underneath: ``df`` carries the raw events of the micro-batch (columns provider,
+vehicleId, lat, lon, speedKmh and eventTs -- or the raw ISO ``ts`` string, parsed like to_timestamp, :92) instead
+of the union of Spark's pre-aggregated tiles and the latest_raw projection (:136-146).  The sanity filter,
+the to_h3 UDF, the watermark, the window aggregation with its persistent state and the in-batch dedup all run
+on the GPU inside ``HeatmapEngine.process_batch`` (libmobheat.so).  There is no CPU fallback.
+"""
+import datetime
+import os
+from datetime import timedelta
+
+import numpy as np
+
+from .engine import HeatmapEngine
+
+# ------------------ Configuration via environment (reference heatmap_stream.py:21-37) ------------------
+MONGO_URI = os.getenv("MONGO_URI", "mongodb://127.0.0.1:27017")
+MONGO_DB = os.getenv("MONGO_DB", "mobility")
+CITY = os.getenv("CITY", "ath")
+H3_RES = int(os.getenv("H3_RES", "8"))
+TILE_MIN = int(os.getenv("TILE_MINUTES", "5"))
+TTL_MIN = int(os.getenv("TTL_MINUTES", "45"))
+WATERMARK_DELAY_MS = 10 * 60 * 1000          # withWatermark("eventTs", "10 minutes"), :107
+BULK_CHUNK = 1000                              # :191, :230
+DEVICE = int(os.getenv("MOBHEAT_DEVICE", os.getenv("LOCAL_RANK", "0")))
+
+_ENGINE = None
+
+
+def get_engine():
+    global _ENGINE
+    if _ENGINE is None:
+        _ENGINE = HeatmapEngine(h3_res=H3_RES, tile_minutes=TILE_MIN, watermark_delay_ms=WATERMARK_DELAY_MS,
+                                device=DEVICE)
+    return _ENGINE
+
+
+def reset_engine():
+    """Drop the persistent state (a new streaming query)."""
+    global _ENGINE
+    if _ENGINE is not None:
+        _ENGINE.close()
+    _ENGINE = None
+
+
+# ------------------ sinks ------------------
+class MongoSink:
+    """Per-batch MongoClient, like the reference (:156-157, :237)."""
+
+    def __init__(self, uri=None, db=None):
+        from pymongo import MongoClient
+        self._client = MongoClient(uri or MONGO_URI)
+        self._db = self._client[db or MONGO_DB]
+
+    def bulk_write(self, collection, ops):
+        self._db[collection].bulk_write(ops, ordered=False)
+
+    def close(self):
+        self._client.close()
+
+
+SINK_FACTORY = MongoSink   # tests replace this with an in-memory capture sink
+
+
+# ------------------ batch columns ------------------
+def _to_arrow(df):
+    import pyarrow as pa
+    if isinstance(df, pa.Table):
+        return df
+    if isinstance(df, pa.RecordBatch):
+        return pa.Table.from_batches([df])
+    try:
+        import pandas as pd
+        if isinstance(df, pd.DataFrame):
+            return pa.Table.from_pandas(df, preserve_index=False)
+    except ImportError:
+        pass
+    if hasattr(df, "toArrow"):           # pyspark >= 4
+        return df.toArrow()
+    if hasattr(df, "toPandas"):          # pyspark 3.x (Arrow-enabled conversion)
+        return pa.Table.from_pandas(df.toPandas(), preserve_index=False)
+    raise TypeError(f"unsupported batch type {type(df)!r}")
+
+
+def _event_ts_us(t):
+    """eventTs as int64 microseconds (Spark TimestampType) + validity mask."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    if "eventTs" in t.column_names:
+        col = t.column("eventTs")
+        if pa.types.is_timestamp(col.type):
+            us = pc.cast(col, pa.timestamp("us", tz=col.type.tz), safe=False)
+            arr = us.combine_chunks() if isinstance(us, pa.ChunkedArray) else us
+            valid = ~np.asarray(arr.is_null().to_numpy(zero_copy_only=False), dtype=bool)
+            vals = np.asarray(pc.fill_null(arr.cast(pa.int64()), 0).to_numpy(zero_copy_only=False), dtype=np.int64)
+            return vals, valid
+        col = col.combine_chunks() if isinstance(col, pa.ChunkedArray) else col
+        valid = ~np.asarray(col.is_null().to_numpy(zero_copy_only=False), dtype=bool)
+        vals = np.asarray(pc.fill_null(col.cast(pa.int64()), 0).to_numpy(zero_copy_only=False), dtype=np.int64)
+        return vals, valid
+    # raw ISO-8601 strings: to_timestamp(col("ts")) (reference :92); malformed -> null
+    import pandas as pd
+    s = pd.to_datetime(t.column("ts").to_pandas(), utc=True, errors="coerce", format="ISO8601")
+    valid = ~s.isna().to_numpy()
+    vals = np.where(valid, s.astype("int64", copy=False).to_numpy() // 1000 if len(s) else np.zeros(0, np.int64), 0)
+    return vals.astype(np.int64), valid
+
+
+def batch_columns(df):
+    """Extract the SoA buffers the C ABI takes (hm_batch_in) from a micro-batch frame."""
+    import pandas as pd
+    import pyarrow.compute as pc
+    t = _to_arrow(df)
+    n = t.num_rows
+
+    def f64(name):
+        if name not in t.column_names:
+            return np.full(n, np.nan), np.zeros(n, bool)
+        c = t.column(name).combine_chunks() if t.num_rows else t.column(name)
+        nulls = np.asarray(c.is_null().to_numpy(zero_copy_only=False), dtype=bool) if n else np.zeros(0, bool)
+        vals = np.asarray(pc.fill_null(c.cast("double"), float("nan")).to_numpy(zero_copy_only=False),
+                          dtype=np.float64) if n else np.zeros(0)
+        return vals, ~nulls
+
+    lat, _ = f64("lat")           # null lat/lon -> NaN: fails between(), like Spark (:101-102)
+    lon, _ = f64("lon")
+    speed, speed_valid = f64("speedKmh")
+    ts_us, ts_valid = _event_ts_us(t)
+    prov = t.column("provider").to_pandas() if n else pd.Series([], dtype=object)
+    vid = t.column("vehicleId").to_pandas() if n else pd.Series([], dtype=object)
+    pc_codes, p_uni = pd.factorize(prov)
+    vc_codes, v_uni = pd.factorize(vid)
+    row_valid = (pc_codes >= 0) & (vc_codes >= 0) & ts_valid        # provider/vehicleId/eventTs non-null (:99-103)
+    vkey = np.where(row_valid, pc_codes.astype(np.int64) * max(len(v_uni), 1) + vc_codes, 0).astype(np.uint64)
+    return dict(n=n, lat=lat, lon=lon, ts_us=ts_us, speed=speed, speed_valid=speed_valid, vkey=vkey,
+                row_valid=row_valid, provider=prov, vehicleId=vid)
+
+
+# ------------------ document builders (reference :164-188 and :211-228) ------------------
+def _spark_datetime(us):
+    # pyspark TimestampType.fromInternal: naive local time; the reference's '...Z' ids assume a UTC driver
+    us = int(us)
+    return datetime.datetime.fromtimestamp(us // 1000000).replace(microsecond=us % 1000000)
+
+
+def tile_ops(tiles, city=None, h3_res=None, ttl_min=None):
+    from pymongo import UpdateOne
+    city = CITY if city is None else city
+    h3_res = H3_RES if h3_res is None else h3_res
+    ttl_min = TTL_MIN if ttl_min is None else ttl_min
+    ops = []
+    for k in range(len(tiles)):
+        windowStart = _spark_datetime(tiles.window_start_us[k])
+        windowEnd = _spark_datetime(tiles.window_end_us[k])
+        cellId = format(int(tiles.cell[k]), "x")                       # h3-py's str form of the UDF output
+        count_val = int(int(tiles.count[k]) or 0)
+        avg_speed = float((None if tiles.speed_null[k] else float(tiles.avg_speed[k])) or 0.0)
+        avg_lat = float(float(tiles.avg_lat[k]) or 0.0)
+        avg_lon = float(float(tiles.avg_lon[k]) or 0.0)
+        _id = f"{city}|h3r{h3_res}|{cellId}|{windowStart.strftime('%Y-%m-%dT%H:%M:%SZ')}"
+        staleAt = windowEnd + timedelta(minutes=ttl_min)
+        doc = {
+            "_id": _id,
+            "city": city,
+            "grid": f"h3r{h3_res}",
+            "cellId": cellId,
+            "windowStart": windowStart,
+            "windowEnd": windowEnd,
+            "count": count_val,
+            "avgSpeedKmh": avg_speed,
+            "centroid": {"type": "Point", "coordinates": [avg_lon, avg_lat]},
+            "staleAt": staleAt,
+        }
+        ops.append(UpdateOne({"_id": _id}, {"$set": doc}, upsert=True))
+    return ops
+
+
+def position_ops(cols, rows):
+    from pymongo import UpdateOne
+    ops = []
+    prov, vid = cols["provider"], cols["vehicleId"]
+    for r in rows:
+        r = int(r)
+        provider = prov.iloc[r]
+        vehicleId = vid.iloc[r]
+        ts = _spark_datetime(cols["ts_us"][r])
+        lat = float(cols["lat"][r])
+        lon = float(cols["lon"][r])
+        filt = {"_id": f"{provider}|{vehicleId}"}
+        ops.append(UpdateOne(
+            {**filt, "$or": [{"ts": {"$exists": False}}, {"ts": {"$lt": ts}}]},
+            {"$set": {
+                "provider": provider,
+                "vehicleId": vehicleId,
+                "ts": ts,
+                "loc": {"type": "Point", "coordinates": [lon, lat]},
+            }},
+            upsert=True,
+        ))
+    return ops
+
+
+def _flush(sink, collection, ops):
+    for i in range(0, len(ops), BULK_CHUNK):
+        sink.bulk_write(collection, ops[i:i + BULK_CHUNK])
+
+
+# ------------------ the drop-in boundary ------------------
+def foreach_batch_func(df, epoch_id: int):
+    """Runs on each micro-batch (reference heatmap_stream.py:150): tiles + latest positions -> MongoDB."""
+    cols = batch_columns(df)
+    res = get_engine().process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"],
+                                     cols["speed_valid"], cols["vkey"], cols["row_valid"])
+    sink = SINK_FACTORY()
+    try:
+        # ---- 1) Upsert tiles (TTL via staleAt) ----
+        _flush(sink, "tiles", tile_ops(res.tiles))
+        # ---- 2) latest per (provider, vehicleId) within this micro-batch ----
+        _flush(sink, "positions_latest", position_ops(cols, res.latest_rows))
+    finally:
+        sink.close()
+    return res

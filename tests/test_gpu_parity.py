@@ -1,0 +1,274 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on identical seeded inputs.
+
+Bar (BASELINE.json north_star): cell ids, counts, window starts and latest-position rows bit-exact;
+averages within 1e-9 relative (fp64 sums in a different order than Spark's), centroid with an absolute
+floor of 1e-12 degrees for groups whose coordinates cancel around 0.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REL = 1e-9
+ABS_DEG = 1e-12
+
+
+def _tiles_dict_gpu(t):
+    return {(int(t.cell[k]), int(t.window_start_us[k])):
+            (int(t.count[k]), None if t.speed_null[k] else float(t.avg_speed[k]), float(t.avg_lon[k]),
+             float(t.avg_lat[k])) for k in range(len(t))}
+
+
+def _tiles_dict_oracle(tiles):
+    return {(x["cell"], x["window_start_us"]): (x["count"], x["avg_speed"], x["avg_lon"], x["avg_lat"]) for x in tiles}
+
+
+def _close(a, b):
+    if a is None or b is None:
+        return a is None and b is None
+    if np.isnan(a) or np.isnan(b):
+        return bool(np.isnan(a) and np.isnan(b))
+    return abs(a - b) <= max(REL * max(abs(a), abs(b)), ABS_DEG)
+
+
+def assert_batch_equal(res, exp):
+    g = _tiles_dict_gpu(res.tiles)
+    o = _tiles_dict_oracle(exp["tiles"])
+    assert len(g) == len(res.tiles), "duplicate keys emitted"
+    assert set(g) == set(o), f"key sets differ: gpu-only {len(set(g) - set(o))}, oracle-only {len(set(o) - set(g))}"
+    bad = [k for k in g if g[k][0] != o[k][0] or not all(_close(g[k][i], o[k][i]) for i in (1, 2, 3))]
+    assert not bad, f"{len(bad)} tiles differ, e.g. {bad[0]}: gpu {g[bad[0]]} oracle {o[bad[0]]}"
+    np.testing.assert_array_equal(np.sort(res.latest_rows), exp["latest_rows"])
+    assert res.n_valid == exp["n_valid"] and res.n_late == exp["n_late"]
+    assert res.n_state == exp["n_state"]
+    assert res.batch_max_event_ms == exp["batch_max_event_ms"]
+    assert res.watermark_ms == exp["watermark_ms"] and res.late_watermark_ms == exp["late_watermark_ms"]
+
+
+# ---------------------------------------------------------------------------------------------------------
+# the UDF: h3.latlng_to_cell
+# ---------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("res", range(16))
+def test_latlng_to_cell_random_and_edges(oracle_h3, res):
+    import mobheat
+    from mobheat import synth
+    rng = np.random.default_rng(500 + res)
+    n = 1_000_000
+    el, eo = synth.edge_points()
+    lat = np.r_[np.degrees(np.arcsin(rng.uniform(-1, 1, n))), el]
+    lon = np.r_[rng.uniform(-180, 180, n), eo]
+    got = mobheat.latlng_to_cell(lat, lon, res)
+    exp = oracle_h3.latlng_to_cell(lat, lon, res)
+    with np.errstate(invalid="ignore"):
+        exp = np.where((lat >= -90) & (lat <= 90) & (lon >= -180) & (lon <= 180), exp, 0)
+    bad = got != exp
+    assert not bad.any(), f"res {res}: {bad.sum()} / {lat.size} mismatches, e.g. {lat[bad][:3]}, {lon[bad][:3]}"
+
+
+def test_latlng_to_cell_golden():
+    import mobheat
+    g = np.load(os.path.join(ROOT, "tests", "golden", "h3_cells.npz"))
+    with np.errstate(invalid="ignore"):
+        ok = (g["lat"] >= -90) & (g["lat"] <= 90) & (g["lon"] >= -180) & (g["lon"] <= 180)
+    for res in range(16):
+        np.testing.assert_array_equal(mobheat.latlng_to_cell(g["lat"], g["lon"], res), np.where(ok, g[f"cells_r{res}"], 0))
+
+
+@pytest.mark.parametrize("res", [7, 8])
+def test_latlng_to_cell_c2_scale_sample(oracle_h3, res):
+    """10M uniform-sphere points (a C2-sized sample) bit-exact."""
+    import mobheat
+    rng = np.random.default_rng(77 + res)
+    n = 10_000_000
+    lat = np.degrees(np.arcsin(rng.uniform(-1, 1, n)))
+    lon = rng.uniform(-180, 180, n)
+    got = mobheat.latlng_to_cell(lat, lon, res)
+    exp = oracle_h3.latlng_to_cell(lat, lon, res)
+    assert np.count_nonzero(got != exp) == 0
+
+
+# ---------------------------------------------------------------------------------------------------------
+# the whole micro-batch
+# ---------------------------------------------------------------------------------------------------------
+def _run(engine, oracle, batch, epoch):
+    res = engine.process_batch(epoch, **batch)
+    exp = oracle.process_batch(**batch)
+    return res, exp
+
+
+def test_c1_boston_batch():
+    from mobheat import HeatmapEngine, synth
+    from oracle.spark_oracle import SparkHeatmapOracle
+    b = synth.c1_boston()
+    eng = HeatmapEngine(h3_res=8)
+    res, exp = _run(eng, SparkHeatmapOracle(h3_res=8), b, 0)
+    assert_batch_equal(res, exp)
+    assert len(res.tiles) > 100 and len(set(res.tiles.window_start_us.tolist())) == 2
+    # against the committed golden fixture too
+    g = np.load(os.path.join(ROOT, "tests", "golden", "c1_batch.npz"))
+    assert set(zip(g["t_cell"].tolist(), g["t_ws"].tolist())) == set(
+        zip(res.tiles.cell.tolist(), res.tiles.window_start_us.tolist()))
+    np.testing.assert_array_equal(np.sort(res.latest_rows), g["latest"])
+    eng.close()
+
+
+def test_multi_batch_watermark_and_eviction():
+    """Several batches: cumulative update-mode aggregates, late rows dropped with the previous batch's
+    watermark, eviction after emission, an empty (no-data) batch, out-of-order and tied timestamps."""
+    from mobheat import HeatmapEngine
+    from oracle.spark_oracle import SparkHeatmapOracle
+    rng = np.random.default_rng(11)
+    eng = HeatmapEngine(h3_res=9)
+    ora = SparkHeatmapOracle(h3_res=9)
+    t0 = 1_759_572_000_000_000
+    minute = 60_000_000
+    for epoch, (start_min, span_min, n) in enumerate([(0, 7, 20000), (5, 6, 20000), (0, 0, 0), (14, 9, 30000),
+                                                      (1, 30, 30000), (40, 3, 5000), (0, 0, 0), (55, 2, 5000)]):
+        lat = rng.uniform(37.90, 38.05, n)
+        lon = rng.uniform(23.60, 23.85, n)
+        ts = t0 + start_min * minute + rng.integers(0, max(span_min, 1) * minute, n)
+        ts[: n // 50] = ts[n // 50: 2 * (n // 50)]               # ties within vehicles below
+        speed = rng.uniform(0, 90, n)
+        sv = rng.random(n) > 0.2
+        vkey = rng.integers(0, 500, n).astype(np.uint64)
+        rv = rng.random(n) > 0.01
+        b = dict(lat=lat, lon=lon, ts_us=ts, speed=speed, speed_valid=sv, vkey=vkey, row_valid=rv)
+        res, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res, exp)
+    eng.close()
+
+
+def test_edge_semantics_batch():
+    """Filter edges (+-90/+-180 inclusive, NaN, inf, null rows), window boundaries, negative timestamps,
+    null and NaN speeds, duplicate vehicles with tied maxima."""
+    from mobheat import HeatmapEngine
+    from oracle.spark_oracle import SparkHeatmapOracle
+    tile = 300_000_000
+    t0 = 1_759_572_000_000_000
+    lat = np.array([90.0, -90.0, 0.0, 45.0, np.nan, 10.0, 10.0, 10.0, 10.0, 10.0, 10.0, 10.0, np.inf, 10.0, 10.0])
+    lon = np.array([180.0, -180.0, 0.0, 45.0, 0.0, 180.0000001, 20.0, 20.0, 20.0, 20.0, 20.0, 20.0, 0.0, -np.inf, 20.0])
+    ts = np.array([t0, t0 + tile - 1, t0 + tile, t0 - 1, t0, t0, t0 + 5, t0 + 5, t0 + 5, t0 + 7, t0 + 7, -1, t0, t0,
+                   -tile - 3], dtype=np.int64)
+    speed = np.array([1.0, 2.0, 3.0, np.nan, 5.0, 6.0, 7.0, 8.0, 9.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0])
+    sv = np.array([1, 1, 1, 1, 1, 1, 0, 0, 0, 1, 1, 1, 1, 1, 1], bool)
+    vkey = np.array([1, 1, 2, 3, 4, 5, 6, 6, 6, 7, 7, 8, 9, 10, 11], np.uint64)
+    rv = np.array([1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 1, 1, 1, 1], bool)
+    b = dict(lat=lat, lon=lon, ts_us=ts, speed=speed, speed_valid=sv, vkey=vkey, row_valid=rv)
+    for late_prev in (True, False):
+        eng = HeatmapEngine(h3_res=5, late_uses_prev_watermark=late_prev)
+        res, exp = _run(eng, SparkHeatmapOracle(h3_res=5, late_uses_prev_watermark=late_prev), b, 0)
+        assert_batch_equal(res, exp)
+        eng.close()
+
+
+def test_dedup_ties_c5_sample():
+    from mobheat import HeatmapEngine, synth
+    from oracle.spark_oracle import SparkHeatmapOracle
+    b = synth.c5_dedup(n_vehicles=200_000, updates=10)
+    eng = HeatmapEngine(h3_res=8)
+    res, exp = _run(eng, SparkHeatmapOracle(h3_res=8), b, 0)
+    assert_batch_equal(res, exp)
+    assert len(res.latest_rows) > 200_000          # the tie subset adds rows
+    eng.close()
+
+
+def test_high_cardinality_res12_two_batches():
+    from mobheat import HeatmapEngine, synth
+    from oracle.spark_oracle import SparkHeatmapOracle
+    b1, b2 = synth.c4_high_cardinality(n=2_000_000)
+    eng = HeatmapEngine(h3_res=12)
+    ora = SparkHeatmapOracle(h3_res=12)
+    # Spark runs a no-data batch after batch 1 because the watermark advanced (MicroBatchExecution's
+    # shouldRunAnotherBatch); the late filter of batch 3 then uses that batch's watermark.
+    empty = {k: v[:0] for k, v in b1.items()}
+    for e, b in enumerate((b1, empty, b2)):
+        res, exp = _run(eng, ora, b, e)
+        assert_batch_equal(res, exp)
+    assert res.n_late > 0
+    eng.close()
+
+
+def test_clustered_city_res9():
+    from mobheat import HeatmapEngine, synth
+    from oracle.spark_oracle import SparkHeatmapOracle
+    b = synth.c3_city(n=3_000_000, n_vehicles=5000)
+    eng = HeatmapEngine(h3_res=9)
+    res, exp = _run(eng, SparkHeatmapOracle(h3_res=9), b, 0)
+    assert_batch_equal(res, exp)
+    eng.close()
+
+
+def test_full_size_properties_c2():
+    """C2 size (1e8 events, res 8) through the device path: size-independent properties only."""
+    import mobheat
+    from mobheat import HeatmapEngine, synth
+    b = synth.c2_global(n=100_000_000)
+    eng = HeatmapEngine(h3_res=8)
+    res = eng.process_batch(0, **b)
+    t = res.tiles
+    assert res.n_valid == b["lat"].size and res.n_late == 0
+    assert int(t.count.sum()) == res.n_valid                       # every valid row lands in exactly one tile
+    keys = t.cell.astype(np.uint64) ^ (t.window_start_us.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15))
+    assert np.unique(keys).size == len(t)                           # no key emitted twice
+    assert set(np.unique(t.window_start_us).tolist()) <= {synth.T0 + k * 300_000_000 for k in range(3)}
+    # every latest row is a valid row and carries the max ts of its vehicle
+    lr = res.latest_rows
+    assert np.all(np.diff(lr) > 0)
+    vk, ts = b["vkey"][lr], b["ts_us"][lr]
+    order = np.lexsort((b["ts_us"], b["vkey"]))
+    last = np.r_[b["vkey"][order][1:] != b["vkey"][order][:-1], True]
+    vmax = dict(zip(b["vkey"][order][last].tolist(), b["ts_us"][order][last].tolist()))
+    assert all(vmax[int(v)] == int(x) for v, x in zip(vk[:100000], ts[:100000]))
+    assert len(set(vk.tolist())) == len(vmax)
+    # sample parity of cells against the UDF
+    idx = np.random.default_rng(0).choice(b["lat"].size, 200_000, replace=False)
+    from oracle import h3_oracle
+    c = h3_oracle.latlng_to_cell(b["lat"][idx], b["lon"][idx], 8)
+    assert np.array_equal(c, mobheat.latlng_to_cell(b["lat"][idx], b["lon"][idx], 8))
+    eng.close()
+
+
+def test_foreach_batch_func_capture_sink():
+    """The drop-in boundary end to end: a micro-batch frame in, the reference's UpdateOne ops out."""
+    import pandas as pd
+    from mobheat import stream, synth
+    from oracle.spark_oracle import SparkHeatmapOracle
+
+    class Capture:
+        ops = {}
+
+        def bulk_write(self, coll, ops):
+            assert len(ops) <= 1000
+            Capture.ops.setdefault(coll, []).extend(ops)
+
+        def close(self):
+            pass
+
+    b = synth.c1_boston(n=3000)
+    df = pd.DataFrame({
+        "provider": ["mbta"] * len(b["lat"]),
+        "vehicleId": [None if not v else f"v{i:05d}" for i, v in enumerate(b["row_valid"])],
+        "lat": b["lat"], "lon": b["lon"],
+        "speedKmh": np.where(b["speed_valid"], b["speed"], np.nan),
+        "eventTs": pd.to_datetime(b["ts_us"], unit="us"),
+    })
+    stream.reset_engine()
+    stream.SINK_FACTORY = Capture
+    try:
+        stream.foreach_batch_func(df, 0)
+    finally:
+        stream.SINK_FACTORY = stream.MongoSink
+        stream.reset_engine()
+    exp = SparkHeatmapOracle(h3_res=stream.H3_RES).process_batch(**b)
+    tiles = {op._filter["_id"]: op._doc["$set"] for op in Capture.ops["tiles"]}
+    assert len(tiles) == len(exp["tiles"])
+    for x in exp["tiles"]:
+        ws = stream._spark_datetime(x["window_start_us"])
+        _id = f"{stream.CITY}|h3r{stream.H3_RES}|{x['cell']:x}|{ws.strftime('%Y-%m-%dT%H:%M:%SZ')}"
+        d = tiles[_id]
+        assert d["count"] == x["count"] and d["cellId"] == format(x["cell"], "x")
+        assert _close(d["avgSpeedKmh"], x["avg_speed"] or 0.0)
+    pos = Capture.ops["positions_latest"]
+    assert sorted(op._filter["_id"] for op in pos) == sorted(f"mbta|v{r:05d}" for r in exp["latest_rows"])
