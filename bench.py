@@ -1,0 +1,170 @@
+#!/usr/bin/env python3
+"""Benchmark of the per-micro-batch hot path (BASELINE.json metric: events/s H3-snapped + window-aggregated).
+
+Workload (N=1 and per rank for N>1, weak scaling): BASELINE.json configs[1] shape -- a synthetic
+OpenSky-like global batch of 1e8 events uniform on the sphere, 50k vehicle ids, 15 minutes of event time
+(3 five-minute windows), 10% null speeds -- at the metric's H3 resolution 8 (configs[1] quotes res 7;
+--res 7 runs that).  One step = one micro-batch through the whole hot path on device-resident inputs:
+filter + latLngToCell + window + late test (k_snap), LDS pre-aggregation (k_local_agg), merge into the
+persistent update-mode state (k_merge), emission (k_emit), eviction/growth, and the latest-position dedup.
+Every step is a NEW micro-batch: its timestamps are the previous step's + 15 min (precomputed before the
+timed region), so the stream advances, windows close and are evicted, and no row is late.
+For N>1 each rank runs the sharded path (mobheat.distributed: RCCL all-to-all of partials by owner).
+
+Prints ONE JSON line (rank 0).  See DESIGN.md for the roofline's algorithmic-byte accounting.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "real-time-mobility-heatmap_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+T0 = 1759572000 * 1_000_000
+SPAN_US = 15 * 60 * 1_000_000
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+# algorithmic bytes: per event for k_snap/k_local_agg/dedup, per record otherwise
+BYTES = {
+    "snap": 42,        # read lat 8 + lon 8 + ts 8 + row_valid 1; write cell 8 + windowStart 8 + flags 1
+    "local_agg": 42,   # read cell 8 + windowStart 8 + flags 1 + speed 8 + speed_valid 1 + lat 8 + lon 8 (+56 B/partial written)
+    "merge": 188,      # per partial: read 56 B record + 64 B state line read + 64 B written + 4 B touched index
+    "emit": 117,       # per emitted tile: 64 B state line + 4 B index read, 49 B row written
+    "dedup": 38,       # per event: 2 x (vkey 8 + ts 8 + flags 1) + win flag 1 + 2 x 1 B compaction reads
+}
+
+
+def gen_batch(n, steps, seed, dev):
+    """C2-shaped batch generated on the device (inputs resident in HBM before timing)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    lat = torch.rad2deg(torch.asin(torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 2 - 1))
+    lon = torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 360.0 - 180.0
+    base = T0 + torch.randint(0, SPAN_US, (n,), generator=g, device=dev, dtype=torch.int64)
+    ts = [base + s * SPAN_US for s in range(steps)]
+    speed = torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 80.0
+    sv = (torch.rand(n, generator=g, device=dev) >= 0.10).to(torch.uint8)
+    vkey = torch.randint(0, 50_000, (n,), generator=g, device=dev, dtype=torch.int64)
+    rv = torch.ones(n, dtype=torch.uint8, device=dev)
+    return dict(lat=lat, lon=lon, ts=ts, speed=speed, sv=sv, vkey=vkey, rv=rv)
+
+
+def cpu_baseline(sample, res):
+    """The oracle port (oracle/: H3 restatement in C with OpenMP + Spark semantics in numpy) timed on this
+    host on a bounded sample of the same workload."""
+    from mobheat import synth
+    from oracle import h3_oracle
+    from oracle.spark_oracle import SparkHeatmapOracle
+    h3_oracle.load()
+    b = synth.c2_global(seed=11, n=sample)
+    o = SparkHeatmapOracle(h3_res=res)
+    t = time.perf_counter()
+    o.process_batch(**b)
+    dt = time.perf_counter() - t
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": sample / dt, "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": f"{sample:,} C2-shaped events (seed 11, res {res}) through oracle/spark_oracle.py; "
+                      f"H3 in C on {threads} OpenMP threads, aggregation/watermark/dedup in numpy on 1 thread; "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--events", type=int, default=100_000_000, help="events per step per GPU")
+    ap.add_argument("--res", type=int, default=8)
+    ap.add_argument("--cpu-sample", type=int, default=3_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import mobheat
+    from mobheat.distributed import LibStages, ShardedHeatmap
+    n = args.events
+    total_steps = args.warmup + args.steps
+    data = gen_batch(n, total_steps, seed=1 + 7919 * rank, dev=dev)
+    eng = mobheat.HeatmapEngine(h3_res=args.res, device=local, state_capacity_hint=1 << 30, batch_capacity_hint=n)
+    sharded = ShardedHeatmap(LibStages(eng), dev) if world > 1 else None
+
+    def step(s):
+        ptrs = dict(n=n, lat=data["lat"].data_ptr(), lon=data["lon"].data_ptr(), ts_us=data["ts"][s].data_ptr(),
+                    speed=data["speed"].data_ptr(), speed_valid=data["sv"].data_ptr(), vkey=data["vkey"].data_ptr(),
+                    row_valid=data["rv"].data_ptr())
+        if sharded is None:
+            return eng.process_batch_device(s, **ptrs)
+        return sharded.process_batch(s, ptrs)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kt = {k: 0.0 for k in BYTES}
+    recs = {"merge": 0, "emit": 0}
+    t0 = time.perf_counter()
+    last = None
+    for s in range(args.warmup, total_steps):
+        last = step(s)
+        tm = eng.last_timings()
+        for k in ("snap", "local_agg", "merge", "emit", "dedup"):
+            kt[k] += tm[k]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    K = args.steps
+    avg_ms = {k: v / K for k, v in kt.items()}
+    n_tiles = int(last.n_tiles) if last is not None else 0
+    units = {"snap": n, "local_agg": n, "dedup": n, "merge": n_tiles, "emit": n_tiles}
+    dom = max(("snap", "local_agg", "merge", "emit", "dedup"), key=lambda k: avg_ms[k])
+    achieved = BYTES[dom] * units[dom] / (avg_ms[dom] * 1e-3) / 1e9 if avg_ms[dom] > 0 else 0.0
+    value = world * n * K / elapsed
+    out = {
+        "metric": METRIC, "value": value, "unit": "events/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
+        "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"C2-shaped global batch: {n:,} events/step/GPU uniform on the sphere, 50k vehicles, "
+                               f"15 min of event time (3 windows) per step, advancing 15 min per step; H3 res {args.res}",
+                   "events_per_step_per_gpu": n, "h3_res": args.res, "parallelism": f"dp{world}",
+                   "tiles_emitted_last_step": n_tiles},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel_ms": {k: round(v, 3) for k, v in avg_ms.items()},
+                     "algorithmic_bytes_per_unit": BYTES[dom], "units_per_launch": units[dom]},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.res)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -14,10 +14,11 @@ constexpr int WAVE = 64;
 
 enum : uint8_t { F_VALID = 1, F_AGG = 2, F_LATE = 4 };
 
-// one persistent tile-state slot = one 64-B line
+// one persistent tile-state slot = one 64-B line. An all-zero slot is empty (tables are cleared with a
+// memset): the window word holds wenc = windowStart ^ 2^63, and windowStart = INT64_MIN is never valid.
 struct alignas(64) TileSlot {
     uint64_t cell;
-    int64_t wstart;
+    unsigned long long wenc;
     unsigned long long count;
     unsigned long long nspeed;
     double sspeed;
@@ -47,6 +48,17 @@ struct Cand {
     int64_t origin;
 };
 static_assert(sizeof(Cand) == 32, "Cand is 32 B");
+
+HM_HD unsigned long long wenc_of(int64_t w) { return (unsigned long long)w ^ (UINT64_C(1) << 63); }
+HM_HD int64_t wdec(unsigned long long e) { return (int64_t)(e ^ (UINT64_C(1) << 63)); }
+
+// live-key count per window (lazy eviction: dead keys stay in the table until the next compaction, so
+// the number of live keys is the sum over windows whose end is after the watermark)
+constexpr int WMAP_SLOTS = 4096;
+struct WinCount {
+    unsigned long long wenc;   // 0 = empty
+    unsigned long long count;
+};
 
 struct alignas(16) DedupSlot {
     unsigned long long vkey;

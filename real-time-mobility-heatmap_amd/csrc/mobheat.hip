@@ -255,6 +255,7 @@ __global__ __launch_bounds__(LA_THREADS) void k_local_agg(const uint64_t *__rest
 // =====================================================================================================
 __device__ __forceinline__ long long find_or_claim_tile(TileSlot *tab, unsigned long long mask, uint64_t c, int64_t w,
                                                         bool &created) {
+    const unsigned long long we = wenc_of(w);
     unsigned long long h = tile_hash(c, w) & mask;
     created = false;
     for (unsigned long long probe = 0; probe <= mask; probe++) {
@@ -262,34 +263,63 @@ __device__ __forceinline__ long long find_or_claim_tile(TileSlot *tab, unsigned 
         unsigned long long cur = __hip_atomic_load(&s->cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (cur == EMPTY_CELL) cur = atomicCAS((unsigned long long *)&s->cell, (unsigned long long)EMPTY_CELL, (unsigned long long)c);
         if (cur == EMPTY_CELL || cur == c) {
-            long long cw = __hip_atomic_load((long long *)&s->wstart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cw == EMPTY_WIN) {
-                cw = (long long)atomicCAS((unsigned long long *)&s->wstart, (unsigned long long)EMPTY_WIN, (unsigned long long)w);
-                if (cw == EMPTY_WIN) { created = true; return (long long)h; }
+            unsigned long long cw = __hip_atomic_load(&s->wenc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cw == 0) {
+                cw = atomicCAS(&s->wenc, 0ull, we);
+                if (cw == 0) { created = true; return (long long)h; }
             }
-            if (cw == w) return (long long)h;
+            if (cw == we) return (long long)h;
         }
         h = (h + 1) & mask;
     }
     return -1;
 }
 
-__global__ __launch_bounds__(256) void k_merge(const TilePartial *__restrict__ parts, const unsigned long long *n_parts_dev,
-                                               int64_t n_parts_host, TileSlot *tab, unsigned long long mask,
-                                               unsigned long long seq, unsigned int *touched, DevStats *st) {
-    const int64_t n = n_parts_dev ? (int64_t)*n_parts_dev : n_parts_host;
+// add `cnt` live keys to window `we` in the window map (one atomic per distinct window per wave)
+__device__ __forceinline__ bool wmap_add(WinCount *m, unsigned long long we, unsigned long long cnt) {
+    unsigned h = (unsigned)(mix64(we) & (WMAP_SLOTS - 1));
+    for (int probe = 0; probe < WMAP_SLOTS; probe++) {
+        unsigned long long cur = __hip_atomic_load(&m[h].wenc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == 0) cur = atomicCAS(&m[h].wenc, 0ull, we);
+        if (cur == 0 || cur == we) {
+            atomicAdd(&m[h].count, cnt);
+            return true;
+        }
+        h = (h + 1) & (WMAP_SLOTS - 1);
+    }
+    return false;
+}
+// wave-cooperative: lanes with `pred` add one key each to their window's count
+__device__ __forceinline__ bool wave_count_windows(bool pred, unsigned long long we, WinCount *m) {
+    bool ok = true;
+    while (true) {
+        unsigned long long pend = __ballot(pred);
+        if (!pend) break;
+        int leader = __ffsll((long long)pend) - 1;
+        unsigned long long wl = __shfl(we, leader, 64);
+        bool match = pred && we == wl;
+        unsigned long long mm = __ballot(match);
+        if (lane_id() == leader) ok = wmap_add(m, wl, (unsigned long long)__popcll(mm));
+        pred = pred && !match;
+    }
+    return ok;
+}
+
+__global__ __launch_bounds__(256) void k_merge(const TilePartial *__restrict__ parts, int64_t n, TileSlot *tab,
+                                               unsigned long long mask, unsigned long long seq, unsigned int *touched,
+                                               WinCount *wmap, DevStats *st) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    long long mn = INT64_MAX;
     unsigned long long created_cnt = 0;
     bool overflow = false;
-    // uniform trip count per wave so the ballot in wave_append sees every lane
+    // uniform trip count per wave so the ballots in wave_append / wave_count_windows see every lane
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
         int64_t i = base + threadIdx.x;
-        bool first = false;
+        bool first = false, created = false;
         long long h = -1;
+        int64_t w = 0;
         if (i < n) {
             TilePartial p = parts[i];
-            bool created;
+            w = p.wstart;
             h = find_or_claim_tile(tab, mask, p.cell, p.wstart, created);
             if (h < 0) {
                 overflow = true;
@@ -305,18 +335,16 @@ __global__ __launch_bounds__(256) void k_merge(const TilePartial *__restrict__ p
                 unsigned long long old = atomicMax(&s->touched, seq);
                 first = old < seq;
                 created_cnt += created;
-                mn = p.wstart < mn ? p.wstart : mn;
             }
         }
+        if (!wave_count_windows(created, wenc_of(w), wmap)) overflow = true;
         unsigned long long pos = wave_append(first, &st->n_touched);
         if (first) touched[pos] = (unsigned int)h;
     }
     created_cnt = wave_sum(created_cnt);
-    mn = wave_min(mn);
     unsigned long long ov = __ballot(overflow);
     if (lane_id() == 0) {
         if (created_cnt) atomicAdd(&st->n_state_new, created_cnt);
-        if (mn != INT64_MAX) atomicMin(&st->min_wstart, mn);
         if (ov) atomicAdd(&st->overflow, 1ull);
     }
 }
@@ -332,7 +360,7 @@ __global__ __launch_bounds__(256) void k_emit(const TileSlot *__restrict__ tab, 
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
         const TileSlot s = tab[touched[t]];
         o_cell[t] = s.cell;
-        o_ws[t] = s.wstart;
+        o_ws[t] = wdec(s.wenc);
         o_cnt[t] = (int64_t)s.count;
         // Spark Average: sum / count (count of non-null inputs) as double; null when that count is 0
         bool null_sp = s.nspeed == 0;
@@ -346,47 +374,40 @@ __global__ __launch_bounds__(256) void k_emit(const TileSlot *__restrict__ tab, 
 // =====================================================================================================
 // state maintenance: rehash (grow) + evict (window end <= watermark)
 // =====================================================================================================
-__global__ __launch_bounds__(256) void k_init_tiles(TileSlot *tab, unsigned long long cap) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)cap; i += stride) {
-        TileSlot s;
-        s.cell = EMPTY_CELL;
-        s.wstart = EMPTY_WIN;
-        s.count = 0;
-        s.nspeed = 0;
-        s.sspeed = 0.0;
-        s.slat = 0.0;
-        s.slon = 0.0;
-        s.touched = 0;
-        tab[i] = s;
-    }
-}
-
+// compaction into a cleared table: keep keys whose window end is after keep_end_us (dead keys -- evicted by an
+// earlier batch's watermark -- are dropped) and rebuild the window map
 __global__ __launch_bounds__(256) void k_rehash(const TileSlot *__restrict__ old, unsigned long long old_cap, TileSlot *nt,
-                                                unsigned long long new_mask, int64_t tile_us, int64_t evict_end_us,
-                                                DevStats *st) {
+                                                unsigned long long new_mask, int64_t tile_us, int64_t keep_end_us,
+                                                WinCount *wmap, DevStats *st) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    long long mn = INT64_MAX;
     unsigned long long kept = 0;
     bool overflow = false;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)old_cap; i += stride) {
-        TileSlot s = old[i];
-        if (s.cell == EMPTY_CELL || s.wstart == EMPTY_WIN) continue;
-        if (s.wstart + tile_us <= evict_end_us) continue;  // evicted: window end <= watermark
-        bool created;
-        long long h = find_or_claim_tile(nt, new_mask, s.cell, s.wstart, created);
-        if (h < 0) { overflow = true; continue; }
-        s.touched = 0;
-        nt[h] = s;
-        kept++;
-        mn = s.wstart < mn ? s.wstart : mn;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < (int64_t)old_cap; base += stride) {
+        int64_t i = base + threadIdx.x;
+        bool keep = false;
+        unsigned long long we = 0;
+        if (i < (int64_t)old_cap) {
+            TileSlot s = old[i];
+            we = s.wenc;
+            if (s.cell != EMPTY_CELL && we != 0 && wdec(we) + tile_us > keep_end_us) {
+                bool created;
+                long long h = find_or_claim_tile(nt, new_mask, s.cell, wdec(we), created);
+                if (h < 0) {
+                    overflow = true;
+                } else {
+                    s.touched = 0;
+                    nt[h] = s;
+                    keep = true;
+                    kept++;
+                }
+            }
+        }
+        if (!wave_count_windows(keep, we, wmap)) overflow = true;
     }
     kept = wave_sum(kept);
-    mn = wave_min(mn);
     unsigned long long ov = __ballot(overflow);
     if (lane_id() == 0) {
         if (kept) atomicAdd(&st->n_state_new, kept);
-        if (mn != INT64_MAX) atomicMin(&st->min_wstart, mn);
         if (ov) atomicAdd(&st->overflow, 1ull);
     }
 }
@@ -661,11 +682,17 @@ struct hm_ctx {
     DevBuf in_lat, in_lon, in_ts, in_speed, in_sv, in_vkey, in_rv;
     DevBuf cell, wstart, flags, win, rows, block_counts, block_offs;
     DevBuf partials, cands;
-    // persistent tile state
-    TileSlot *tab = nullptr;
+    // persistent tile state: open-addressing table + an equally sized compaction target (double buffer).
+    // Eviction is lazy: a key whose window end <= the eviction watermark can never be updated again (every
+    // later row of its window is dropped as late), so it stays in place, is excluded from n_state through the
+    // per-window live counts, and is dropped when the table is next compacted.
+    TileSlot *tab = nullptr, *tab_alt = nullptr;
     unsigned long long cap = 0;
-    int64_t state_size = 0;
-    int64_t state_min_wstart = INT64_MAX;
+    int64_t occ = 0;                  // non-empty slots (live + dead) since the last compaction
+    int64_t state_size = 0;           // live keys after the last batch
+    int64_t dead_end_us = INT64_MIN;  // keys with window end <= this are dead
+    WinCount *wmap = nullptr, *h_wmap = nullptr;
+    int wmap_used = 0;
     DevBuf touched;
     unsigned long long seq = 0;
     // dedup table (persistent, cleared through its used list)
@@ -749,44 +776,74 @@ static uint64_t next_pow2(uint64_t v) {
     return p;
 }
 
-static int alloc_tiles(hm_ctx *ctx, unsigned long long cap, TileSlot **out) {
+static int alloc_table(hm_ctx *ctx, unsigned long long cap, TileSlot **out) {
     TileSlot *t = nullptr;
     if (hipMalloc(&t, cap * sizeof(TileSlot)) != hipSuccess) {
         (void)hipGetLastError();
         return set_err(ctx, HM_E_NOMEM, "state table alloc of %llu slots failed", cap);
     }
-    hipLaunchKernelGGL(k_init_tiles, dim3(grid_for(cap, 256)), dim3(256), 0, ctx->stream, t, cap);
-    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemsetAsync(t, 0, cap * sizeof(TileSlot), ctx->stream));
     *out = t;
     return HM_OK;
 }
 
-// evict keys with window end <= wm (ms) and/or grow the table to hold `need` keys at load <= 1/2
-static int state_maintain(hm_ctx *ctx, int64_t evict_wm_ms, int64_t need_keys) {
-    int64_t evict_end_us = evict_wm_ms * 1000;
-    bool evict = ctx->state_size > 0 && ctx->state_min_wstart != INT64_MAX &&
-                 ctx->state_min_wstart + ctx->cfg.tile_us <= evict_end_us;
+// Make room for `incoming` new keys: compact (drop dead keys) into the alternate table when occupancy would
+// exceed 1/2 or the window map is filling up; grow both tables when the live keys alone would not fit.
+static int state_reserve(hm_ctx *ctx, int64_t incoming) {
+    bool wmap_full = ctx->wmap_used > WMAP_SLOTS * 3 / 4;
+    if (ctx->occ + incoming <= (int64_t)(ctx->cap / 2) && !wmap_full) return HM_OK;
     unsigned long long want = ctx->cap;
-    while ((unsigned long long)need_keys * 2 > want) want <<= 1;
-    if (!evict && want == ctx->cap) return HM_OK;
-    TileSlot *nt = nullptr;
-    int rc = alloc_tiles(ctx, want, &nt);
-    if (rc) return rc;
+    while ((unsigned long long)(ctx->state_size + incoming) * 2 > want) want <<= 1;
+    TileSlot *dst = nullptr;
+    int rc;
+    if (want == ctx->cap) {
+        dst = ctx->tab_alt;
+        HIPCHK(ctx, hipMemsetAsync(dst, 0, want * sizeof(TileSlot), ctx->stream));
+    } else if ((rc = alloc_table(ctx, want, &dst))) {
+        return rc;
+    }
+    HIPCHK(ctx, hipMemsetAsync(ctx->wmap, 0, WMAP_SLOTS * sizeof(WinCount), ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->d_st, 0, sizeof(DevStats), ctx->stream));
-    long long init_min = INT64_MAX;
-    HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->min_wstart, &init_min, sizeof(init_min), hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_rehash, dim3(grid_for(ctx->cap, 256)), dim3(256), 0, ctx->stream, ctx->tab, ctx->cap, nt, want - 1,
-                       ctx->cfg.tile_us, evict ? evict_end_us : INT64_MIN, ctx->d_st);
+    hipLaunchKernelGGL(k_rehash, dim3(grid_for(ctx->cap, 256, 256 * 32)), dim3(256), 0, ctx->stream, ctx->tab, ctx->cap, dst,
+                       want - 1, ctx->cfg.tile_us, ctx->dead_end_us, ctx->wmap, ctx->d_st);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "state rehash overflow");
-    HIPCHK(ctx, hipFree(ctx->tab));
-    ctx->tab = nt;
-    ctx->cap = want;
-    ctx->state_size = (int64_t)ctx->h_st->n_state_new;
-    ctx->state_min_wstart = ctx->h_st->min_wstart;
-    return ensure(ctx, ctx->touched, want * sizeof(unsigned int));
+    if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "state compaction overflow");
+    if (want == ctx->cap) {
+        std::swap(ctx->tab, ctx->tab_alt);
+    } else {
+        HIPCHK(ctx, hipFree(ctx->tab));
+        HIPCHK(ctx, hipFree(ctx->tab_alt));
+        ctx->tab = dst;
+        ctx->tab_alt = nullptr;
+        if (hipMalloc(&ctx->tab_alt, want * sizeof(TileSlot)) != hipSuccess) {
+            (void)hipGetLastError();
+            return set_err(ctx, HM_E_NOMEM, "state table alloc of %llu slots failed", want);
+        }
+        ctx->cap = want;
+        if ((rc = ensure(ctx, ctx->touched, want * sizeof(unsigned int)))) return rc;
+    }
+    ctx->occ = (int64_t)ctx->h_st->n_state_new;
+    ctx->wmap_used = 0;   // refreshed after the next merge
+    return HM_OK;
+}
+
+// After a batch: keys with window end <= the eviction watermark are dead from now on; n_state = live keys.
+static int state_account(hm_ctx *ctx, int64_t evict_wm_ms) {
+    ctx->dead_end_us = evict_wm_ms * 1000;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_wmap, ctx->wmap, WMAP_SLOTS * sizeof(WinCount), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    int64_t live = 0;
+    int used = 0;
+    for (int i = 0; i < WMAP_SLOTS; i++) {
+        if (!ctx->h_wmap[i].wenc) continue;
+        used++;
+        if (wdec(ctx->h_wmap[i].wenc) + ctx->cfg.tile_us > ctx->dead_end_us) live += (int64_t)ctx->h_wmap[i].count;
+    }
+    ctx->state_size = live;
+    ctx->wmap_used = used;
+    return HM_OK;
 }
 
 static int dedup_prepare(hm_ctx *ctx, int64_t n_upper) {
@@ -924,28 +981,24 @@ static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t 
     return HM_OK;
 }
 
-static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts, const unsigned long long *n_parts_dev,
-                            int64_t evict_wm_ms) {
+static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts) {
     int rc;
-    // grow (and evict with the previous batch's watermark, already applied) before inserting
-    if ((rc = state_maintain(ctx, INT64_MIN / 1000, ctx->state_size + n_parts))) return rc;
-    (void)evict_wm_ms;
+    if ((rc = state_reserve(ctx, n_parts))) return rc;
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_touched, 0, 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_state_new, 0, 8, ctx->stream));
-    long long init_min = ctx->state_min_wstart;
-    HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->min_wstart, &init_min, sizeof(init_min), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
     ctx->seq++;
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
     if (n_parts > 0) {
-        hipLaunchKernelGGL(k_merge, dim3(grid_for(n_parts, 256)), dim3(256), 0, ctx->stream, parts, n_parts_dev, n_parts,
-                           ctx->tab, ctx->cap - 1, ctx->seq, (unsigned int *)ctx->touched.p, ctx->d_st);
+        hipLaunchKernelGGL(k_merge, dim3(grid_for(n_parts, 256)), dim3(256), 0, ctx->stream, parts, n_parts, ctx->tab,
+                           ctx->cap - 1, ctx->seq, (unsigned int *)ctx->touched.p, ctx->wmap, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
-    if ((rc = ensure(ctx, ctx->o_cell, std::max<int64_t>(n_parts, 1) * 8)) || (rc = ensure(ctx, ctx->o_ws, std::max<int64_t>(n_parts, 1) * 8)) ||
-        (rc = ensure(ctx, ctx->o_cnt, std::max<int64_t>(n_parts, 1) * 8)) || (rc = ensure(ctx, ctx->o_sp, std::max<int64_t>(n_parts, 1) * 8)) ||
-        (rc = ensure(ctx, ctx->o_spn, std::max<int64_t>(n_parts, 1))) || (rc = ensure(ctx, ctx->o_lon, std::max<int64_t>(n_parts, 1) * 8)) ||
-        (rc = ensure(ctx, ctx->o_lat, std::max<int64_t>(n_parts, 1) * 8)))
+    int64_t m = std::max<int64_t>(n_parts, 1);
+    if ((rc = ensure(ctx, ctx->o_cell, m * 8)) || (rc = ensure(ctx, ctx->o_ws, m * 8)) || (rc = ensure(ctx, ctx->o_cnt, m * 8)) ||
+        (rc = ensure(ctx, ctx->o_sp, m * 8)) || (rc = ensure(ctx, ctx->o_spn, m)) || (rc = ensure(ctx, ctx->o_lon, m * 8)) ||
+        (rc = ensure(ctx, ctx->o_lat, m * 8)))
         return rc;
     if (n_parts > 0) {
         hipLaunchKernelGGL(k_emit, dim3(grid_for(n_parts, 256)), dim3(256), 0, ctx->stream, ctx->tab,
@@ -1079,8 +1132,17 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     }
     if (hipMemset(ctx->d_scratch, 0, 256 * 8) != hipSuccess) { ctx->err = "scratch init"; return fail("create"); }
     unsigned long long cap = next_pow2((unsigned long long)std::max<int64_t>(cfg->state_capacity_hint, 1 << 16));
-    if (alloc_tiles(ctx, cap, &ctx->tab)) return fail("create");
+    if (alloc_table(ctx, cap, &ctx->tab) || hipMalloc(&ctx->tab_alt, cap * sizeof(TileSlot)) != hipSuccess) {
+        if (ctx->err.empty()) ctx->err = "state table alloc";
+        return fail("create");
+    }
     ctx->cap = cap;
+    if (hipMalloc(&ctx->wmap, WMAP_SLOTS * sizeof(WinCount)) != hipSuccess ||
+        hipHostMalloc(&ctx->h_wmap, WMAP_SLOTS * sizeof(WinCount), hipHostMallocDefault) != hipSuccess ||
+        hipMemset(ctx->wmap, 0, WMAP_SLOTS * sizeof(WinCount)) != hipSuccess) {
+        ctx->err = "window map alloc";
+        return fail("create");
+    }
     if (ensure(ctx, ctx->touched, cap * sizeof(unsigned int))) return fail("create");
     if (cfg->batch_capacity_hint > 0) {
         if (dedup_prepare(ctx, cfg->batch_capacity_hint)) return fail("create");
@@ -1102,6 +1164,9 @@ void hm_destroy(hm_ctx *ctx) {
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (ctx->tab) (void)hipFree(ctx->tab);
+    if (ctx->tab_alt) (void)hipFree(ctx->tab_alt);
+    if (ctx->wmap) (void)hipFree(ctx->wmap);
+    if (ctx->h_wmap) (void)hipHostFree(ctx->h_wmap);
     if (ctx->dtab) (void)hipFree(ctx->dtab);
     void *hbufs[] = {ctx->h_cell, ctx->h_ws, ctx->h_cnt, ctx->h_sp, ctx->h_spn, ctx->h_lon, ctx->h_lat, ctx->h_rows};
     for (void *p : hbufs)
@@ -1143,7 +1208,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     DevStats s1 = *ctx->h_st;
     // 3. merge into state + emit
-    if ((rc = phase_merge_emit(ctx, (const TilePartial *)ctx->partials.p, (int64_t)s1.n_partials, nullptr, ctx->wm_cur))) return rc;
+    if ((rc = phase_merge_emit(ctx, (const TilePartial *)ctx->partials.p, (int64_t)s1.n_partials))) return rc;
     // 4. dedup over the batch's valid rows
     if ((rc = phase_dedup(ctx, &I, nullptr, I.n))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
@@ -1153,17 +1218,13 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     DevStats s2 = *ctx->h_st;
     if (s2.overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     if (s2.bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved (%llu rows)", s2.bad_vkey);
-    ctx->state_size += (int64_t)s2.n_state_new;
-    ctx->state_min_wstart = s2.min_wstart;
+    ctx->occ += (int64_t)s2.n_state_new;
     int64_t n_rows = (int64_t)ctx->h_scratch[255];
     record_timings(ctx);
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, n_rows, (const int64_t *)ctx->rows.p, out_memory, out))) return rc;
-    DevStats sf = s1;
-    fill_stats(ctx, out, in->n, sf, late_wm);
-    // 5. eviction of this batch (window end <= this batch's watermark) after emission, then advance
-    int64_t evict_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_cur : ctx->wm_cur;
-    if ((rc = state_maintain(ctx, evict_wm, ctx->state_size))) return rc;
-    out->n_state = ctx->state_size;
+    // 5. eviction after emission with this batch's watermark (lazy: see hm_ctx), then advance the watermark
+    if ((rc = state_account(ctx, ctx->wm_cur))) return rc;
+    fill_stats(ctx, out, in->n, s1, late_wm);
     advance_watermark(ctx, s1.max_ts_ms);
     return HM_OK;
 }
@@ -1280,7 +1341,7 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, 
     int rc;
     memset(out, 0, sizeof(*out));
     int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
-    if ((rc = phase_merge_emit(ctx, (const TilePartial *)tile_recv_dev, n_tile_recv, nullptr, ctx->wm_cur))) return rc;
+    if ((rc = phase_merge_emit(ctx, (const TilePartial *)tile_recv_dev, n_tile_recv))) return rc;
     // owner-side dedup over received candidates
     if ((rc = phase_dedup(ctx, nullptr, (const Cand *)cand_recv_dev, n_cand_recv))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch, 0, 128 * 8, ctx->stream));
@@ -1305,17 +1366,15 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, 
         HIPCHK(ctx, hipGetLastError());
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    ctx->state_size += (int64_t)s2.n_state_new;
-    ctx->state_min_wstart = s2.min_wstart;
+    ctx->occ += (int64_t)s2.n_state_new;
     record_timings(ctx);
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, 0, nullptr, out_memory, out))) return rc;
+    if ((rc = state_account(ctx, ctx->wm_cur))) return rc;
     DevStats sf{};
     sf.n_valid = ctx->stage_sizes.n_valid;
     sf.n_late = ctx->stage_sizes.n_late;
     sf.max_ts_ms = global_batch_max_event_ms;
     fill_stats(ctx, out, ctx->stage_n_in, sf, late_wm);
-    if ((rc = state_maintain(ctx, ctx->wm_cur, ctx->state_size))) return rc;
-    out->n_state = ctx->state_size;
     advance_watermark(ctx, global_batch_max_event_ms);
     ctx->stage = 2;
     return HM_OK;
