@@ -35,6 +35,7 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 BYTES = {
     "snap": 42,        # read lat 8 + lon 8 + ts 8 + row_valid 1; write cell 8 + windowStart 8 + flags 1
     "local_agg": 42,   # read cell 8 + windowStart 8 + flags 1 + speed 8 + speed_valid 1 + lat 8 + lon 8 (+56 B/partial written)
+    "partition": 168,  # per partial: histogram read 56 B + scatter read 56 B + write 56 B
     "merge": 188,      # per partial: read 56 B record + 64 B state line read + 64 B written + 4 B touched index
     "emit": 117,       # per emitted tile: 64 B state line + 4 B index read, 49 B row written
     "dedup": 38,       # per event: 2 x (vkey 8 + ts 8 + flags 1) + win flag 1 + 2 x 1 B compaction reads
@@ -119,13 +120,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     kt = {k: 0.0 for k in BYTES}
-    recs = {"merge": 0, "emit": 0}
     t0 = time.perf_counter()
     last = None
     for s in range(args.warmup, total_steps):
         last = step(s)
         tm = eng.last_timings()
-        for k in ("snap", "local_agg", "merge", "emit", "dedup"):
+        for k in BYTES:
             kt[k] += tm[k]
     torch.cuda.synchronize()
     if world > 1:
@@ -140,8 +140,8 @@ def main():
     K = args.steps
     avg_ms = {k: v / K for k, v in kt.items()}
     n_tiles = int(last.n_tiles) if last is not None else 0
-    units = {"snap": n, "local_agg": n, "dedup": n, "merge": n_tiles, "emit": n_tiles}
-    dom = max(("snap", "local_agg", "merge", "emit", "dedup"), key=lambda k: avg_ms[k])
+    units = {"snap": n, "local_agg": n, "dedup": n, "partition": n_tiles, "merge": n_tiles, "emit": n_tiles}
+    dom = max(BYTES, key=lambda k: avg_ms[k])
     achieved = BYTES[dom] * units[dom] / (avg_ms[dom] * 1e-3) / 1e9 if avg_ms[dom] > 0 else 0.0
     value = world * n * K / elapsed
     out = {

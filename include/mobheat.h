@@ -164,7 +164,7 @@ int hm_selftest_latlng_to_cell_host(const double *lat, const double *lon, int64_
                                     uint64_t *out);
 
 /* Timing of the last hm_process_batch / stage call on the library's stream (HIP events), milliseconds
- * per kernel: index 0 snap, 1 local aggregate, 2 merge, 3 emit, 4 dedup, 5 total. */
+ * per kernel: index 0 snap, 1 local aggregate, 2 merge, 3 emit, 4 dedup, 5 total, 6 region partition. */
 int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n);
 
 #ifdef __cplusplus

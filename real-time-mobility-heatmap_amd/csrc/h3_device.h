@@ -39,6 +39,17 @@ typedef unsigned __int128 u128;
 #define HM_LD_RSIN60_E (-63)
 #define HM_LD_EPSILON_M UINT64_C(0xe69594bec44de15b)
 #define HM_LD_EPSILON_E (-117)
+// exact split of each constant: C = HI + LO, HI = RN53(C), LO exactly representable (<= 11 bits)
+#define HM_LD_PI_180_HI 0x1.1df46a2529d39p-6
+#define HM_LD_PI_180_LO 0x1.5c00000000000p-62
+#define HM_LD_2PI_HI 0x1.921fb54442d18p+2
+#define HM_LD_2PI_LO 0x1.1a80000000000p-52
+#define HM_LD_AP7_ROT_HI 0x1.5579fdc3a8f41p-2
+#define HM_LD_AP7_ROT_LO 0x1.7500000000000p-56
+#define HM_LD_SQRT7_HI 0x1.52a7fa9d2f8eap+1
+#define HM_LD_SQRT7_LO -0x1.2200000000000p-53
+#define HM_LD_RSIN60_HI 0x1.279a74590331cp+0
+#define HM_LD_RSIN60_LO 0x1.3480000000000p-54
 // double constants (no L suffix upstream)
 #define HM_INV_RES0_U_GNOMONIC 2.61803398874989588842
 
@@ -143,6 +154,40 @@ HM_HD double xld_add(double a, bool negc, uint64_t cm, int ce) {
     return round_x87_then_double(R, B, sticky, neg);
 }
 
+// ---- fast paths: fp64 error-free transformations, exact integer path only near a rounding midpoint ----
+// E = exact result.  With p (or s) the fp64 head and t the fp64 tail, E = p + t + d, |d| <= 2^-53 ulp(p).
+// Rounding E to 64 bits and then to 53 bits can differ from RN53(E) = RN53(p + t) only when E lies within
+// 2^-12 ulp(p) of a 53-bit midpoint; lanes within 2^-10 ulp (and binade edges, zeros, non-finite values)
+// take the exact path.
+HM_HD bool xld_fast_ok(double head, double tail) {
+    uint64_t b = __builtin_bit_cast(uint64_t, head);
+    int ex = (int)((b >> 52) & 0x7ff);
+    uint64_t fr = b & ((UINT64_C(1) << 52) - 1);
+    if (ex == 0 || ex >= 0x7fe || fr < 4 || fr > (UINT64_C(1) << 52) - 4) return false;
+    double f = ldexp(tail, 1075 - ex);         // tail in units of ulp(head), exact scaling
+    if (!(__builtin_fabs(f) <= 1.0)) return false;
+    double fr2 = f - floor(f);
+    return __builtin_fabs(fr2 - 0.5) > 0x1p-10;
+}
+HM_HD double xmul(double a, uint64_t cm, int ce, double chi, double clo) {
+    double p = a * chi;
+    double e = fma(a, chi, -p);
+    double t = fma(a, clo, e);
+    if (xld_fast_ok(p, t)) return p + t;
+    return xld_mul(a, cm, ce);
+}
+HM_HD double xadd(double a, bool negc, uint64_t cm, int ce, double chi, double clo) {
+    double ch = negc ? -chi : chi, cl = negc ? -clo : clo;
+    double s = a + ch;
+    double bb = s - a;
+    double e = (a - (s - bb)) + (ch - bb);      // TwoSum: a + ch == s + e exactly
+    double t = e + cl;
+    if (xld_fast_ok(s, t)) return s + t;
+    return xld_add(a, negc, cm, ce);
+}
+#define XMUL(a, K) xmul((a), HM_LD_##K##_M, HM_LD_##K##_E, HM_LD_##K##_HI, HM_LD_##K##_LO)
+#define XADD(a, neg, K) xadd((a), (neg), HM_LD_##K##_M, HM_LD_##K##_E, HM_LD_##K##_HI, HM_LD_##K##_LO)
+
 // a >= C (C > 0, long double), exactly
 HM_HD bool xld_ge(double a, uint64_t cm, int ce) {
     if (!(a > 0.0)) return false;
@@ -160,8 +205,8 @@ HM_HD bool xld_lt(double a, uint64_t cm, int ce) { return !xld_ge(a, cm, ce); }
 // ---- upstream helpers ----
 HM_HD double posAngleRads(double rads) {
     // double tmp = ((rads < 0.0L) ? rads + M_2PI : rads); if (rads >= M_2PI) tmp -= M_2PI;
-    double tmp = (rads < 0.0) ? xld_add(rads, false, HM_LD_2PI_M, HM_LD_2PI_E) : rads;
-    if (xld_ge(rads, HM_LD_2PI_M, HM_LD_2PI_E)) tmp = xld_add(tmp, true, HM_LD_2PI_M, HM_LD_2PI_E);
+    double tmp = (rads < 0.0) ? XADD(rads, false, 2PI) : rads;
+    if (xld_ge(rads, HM_LD_2PI_M, HM_LD_2PI_E)) tmp = XADD(tmp, true, 2PI);
     return tmp;
 }
 
@@ -187,7 +232,7 @@ HM_HD IJK hex2dToCoordIJK(double vx, double vy) {
     h.k = 0;
     double a1 = __builtin_fabs(vx);
     double a2 = __builtin_fabs(vy);
-    double x2 = xld_mul(a2, HM_LD_RSIN60_M, HM_LD_RSIN60_E);
+    double x2 = XMUL(a2, RSIN60);
     double x1 = a1 + x2 / 2.0;
     int m1 = (int)x1;
     int m2 = (int)x2;
@@ -331,8 +376,8 @@ HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const H3Tables &T) {
 // (the range guard of heatmap_stream.py:66-69; NaN fails it).
 HM_HD uint64_t latLngToCellDeg(double lat_deg, double lng_deg, int res, const H3Tables &T) {
     if (!(lat_deg >= -90.0 && lat_deg <= 90.0 && lng_deg >= -180.0 && lng_deg <= 180.0)) return 0;
-    double glat = xld_mul(lat_deg, HM_LD_PI_180_M, HM_LD_PI_180_E);
-    double glng = xld_mul(lng_deg, HM_LD_PI_180_M, HM_LD_PI_180_E);
+    double glat = XMUL(lat_deg, PI_180);
+    double glng = XMUL(lng_deg, PI_180);
     // _geoToVec3d
     double clat = cos(glat), slat = sin(glat);
     double vz = slat;
@@ -363,10 +408,10 @@ HM_HD uint64_t latLngToCellDeg(double lat_deg, double lng_deg, int res, const H3
         t2 = t2 * cd;
         double az = atan2(num, t1 - t2);
         double theta = posAngleRads(T.faceAxesAz0[face] - posAngleRads(az));
-        if (res & 1) theta = posAngleRads(xld_add(theta, true, HM_LD_AP7_ROT_M, HM_LD_AP7_ROT_E));
+        if (res & 1) theta = posAngleRads(XADD(theta, true, AP7_ROT));
         r = tan(r);
         r *= HM_INV_RES0_U_GNOMONIC;
-        for (int i = 0; i < res; i++) r = xld_mul(r, HM_LD_SQRT7_M, HM_LD_SQRT7_E);
+        for (int i = 0; i < res; i++) r = XMUL(r, SQRT7);
         hx = r * cos(theta);
         hy = r * sin(theta);
     }

@@ -253,12 +253,18 @@ __global__ __launch_bounds__(LA_THREADS) void k_local_agg(const uint64_t *__rest
 // =====================================================================================================
 // K3: merge partials into the persistent state table
 // =====================================================================================================
-__device__ __forceinline__ long long find_or_claim_tile(TileSlot *tab, unsigned long long mask, uint64_t c, int64_t w,
-                                                        bool &created) {
+// Table geometry: slot index = hash & mask; the table is split into regions of (rmask + 1) slots and linear
+// probing wraps inside the key's region, so a region can be owned by one workgroup (k_merge_owned).
+__device__ __forceinline__ unsigned long long next_slot(unsigned long long h, unsigned long long rmask) {
+    return (h & ~rmask) | ((h + 1) & rmask);
+}
+
+__device__ __forceinline__ long long find_or_claim_tile(TileSlot *tab, unsigned long long mask, unsigned long long rmask,
+                                                        uint64_t c, int64_t w, bool &created) {
     const unsigned long long we = wenc_of(w);
     unsigned long long h = tile_hash(c, w) & mask;
     created = false;
-    for (unsigned long long probe = 0; probe <= mask; probe++) {
+    for (unsigned long long probe = 0; probe <= rmask; probe++) {
         TileSlot *s = &tab[h];
         unsigned long long cur = __hip_atomic_load(&s->cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (cur == EMPTY_CELL) cur = atomicCAS((unsigned long long *)&s->cell, (unsigned long long)EMPTY_CELL, (unsigned long long)c);
@@ -270,7 +276,7 @@ __device__ __forceinline__ long long find_or_claim_tile(TileSlot *tab, unsigned 
             }
             if (cw == we) return (long long)h;
         }
-        h = (h + 1) & mask;
+        h = next_slot(h, rmask);
     }
     return -1;
 }
@@ -289,8 +295,34 @@ __device__ __forceinline__ bool wmap_add(WinCount *m, unsigned long long we, uns
     }
     return false;
 }
-// wave-cooperative: lanes with `pred` add one key each to their window's count
-__device__ __forceinline__ bool wave_count_windows(bool pred, unsigned long long we, WinCount *m) {
+// Per-workgroup window counts in LDS, flushed to the global map once per workgroup: a batch touches only a
+// few windows, so per-wave global adds would all hit the same few counters.
+constexpr int WL_SLOTS = 32;
+struct WinLds {
+    unsigned long long key[WL_SLOTS];
+    unsigned long long cnt[WL_SLOTS];
+};
+__device__ __forceinline__ void wl_init(WinLds &L) {
+    for (int q = threadIdx.x; q < WL_SLOTS; q += blockDim.x) { L.key[q] = 0; L.cnt[q] = 0; }
+}
+__device__ __forceinline__ bool wl_add(WinLds &L, WinCount *g, unsigned long long we, unsigned long long c) {
+    unsigned h = (unsigned)(mix64(we) & (WL_SLOTS - 1));
+    for (int probe = 0; probe < WL_SLOTS; probe++) {
+        unsigned long long o = atomicCAS(&L.key[h], 0ull, we);
+        if (o == 0 || o == we) { atomicAdd(&L.cnt[h], c); return true; }
+        h = (h + 1) & (WL_SLOTS - 1);
+    }
+    return wmap_add(g, we, c);   // more distinct windows than LDS slots: straight to the global map
+}
+// after a __syncthreads(): one lane per LDS slot adds its count to the global map
+__device__ __forceinline__ bool wl_flush(WinLds &L, WinCount *g) {
+    bool ok = true;
+    for (int q = threadIdx.x; q < WL_SLOTS; q += blockDim.x)
+        if (L.key[q]) ok &= wmap_add(g, L.key[q], L.cnt[q]);
+    return ok;
+}
+// wave-cooperative: lanes with `pred` add one key each to their window's count (one LDS add per window per wave)
+__device__ __forceinline__ bool wave_count_windows(bool pred, unsigned long long we, WinLds &L, WinCount *g) {
     bool ok = true;
     while (true) {
         unsigned long long pend = __ballot(pred);
@@ -299,15 +331,18 @@ __device__ __forceinline__ bool wave_count_windows(bool pred, unsigned long long
         unsigned long long wl = __shfl(we, leader, 64);
         bool match = pred && we == wl;
         unsigned long long mm = __ballot(match);
-        if (lane_id() == leader) ok = wmap_add(m, wl, (unsigned long long)__popcll(mm));
+        if (lane_id() == leader) ok = wl_add(L, g, wl, (unsigned long long)__popcll(mm));
         pred = pred && !match;
     }
     return ok;
 }
 
 __global__ __launch_bounds__(256) void k_merge(const TilePartial *__restrict__ parts, int64_t n, TileSlot *tab,
-                                               unsigned long long mask, unsigned long long seq, unsigned int *touched,
-                                               WinCount *wmap, DevStats *st) {
+                                               unsigned long long mask, unsigned long long rmask, unsigned long long seq,
+                                               unsigned int *touched, WinCount *wmap, DevStats *st) {
+    __shared__ WinLds WL;
+    wl_init(WL);
+    __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     unsigned long long created_cnt = 0;
     bool overflow = false;
@@ -320,7 +355,7 @@ __global__ __launch_bounds__(256) void k_merge(const TilePartial *__restrict__ p
         if (i < n) {
             TilePartial p = parts[i];
             w = p.wstart;
-            h = find_or_claim_tile(tab, mask, p.cell, p.wstart, created);
+            h = find_or_claim_tile(tab, mask, rmask, p.cell, p.wstart, created);
             if (h < 0) {
                 overflow = true;
             } else {
@@ -337,10 +372,243 @@ __global__ __launch_bounds__(256) void k_merge(const TilePartial *__restrict__ p
                 created_cnt += created;
             }
         }
-        if (!wave_count_windows(created, wenc_of(w), wmap)) overflow = true;
+        if (!wave_count_windows(created, wenc_of(w), WL, wmap)) overflow = true;
         unsigned long long pos = wave_append(first, &st->n_touched);
         if (first) touched[pos] = (unsigned int)h;
     }
+    __syncthreads();
+    if (!wl_flush(WL, wmap)) overflow = true;
+    created_cnt = wave_sum(created_cnt);
+    unsigned long long ov = __ballot(overflow);
+    if (lane_id() == 0) {
+        if (created_cnt) atomicAdd(&st->n_state_new, created_cnt);
+        if (ov) atomicAdd(&st->overflow, 1ull);
+    }
+}
+
+// =====================================================================================================
+// K2b: radix partition of the partials by state-table region (top RP_BITS bits of the slot index), so that
+// k_merge's concurrently running waves work inside a few MB of the table instead of all of it.
+// tile histogram (LDS) -> digit-major exclusive scan -> LDS-cursor scatter.
+// =====================================================================================================
+constexpr int RP_BITS = 12;
+constexpr int RP_BINS = 1 << RP_BITS;
+constexpr int RP_TILE = 65536;         // partials per tile (one workgroup)
+constexpr int RP_THREADS = 256;
+
+__device__ __forceinline__ unsigned rp_digit(const TilePartial &p, unsigned long long mask, int shift) {
+    return (unsigned)((tile_hash(p.cell, p.wstart) & mask) >> shift);
+}
+
+__global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const TilePartial *__restrict__ parts, int64_t n,
+                                                       unsigned long long mask, int shift, unsigned *__restrict__ H,
+                                                       int64_t ntiles) {
+    __shared__ unsigned h[RP_BINS];
+    for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) h[d] = 0;
+    __syncthreads();
+    int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
+    int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
+    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) atomicAdd(&h[rp_digit(parts[i], mask, shift)], 1u);
+    __syncthreads();
+    for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) H[(int64_t)d * ntiles + blockIdx.x] = h[d];
+}
+
+// exclusive scan of m u32 entries into u64 offsets, 3 phases; block size 1024, 4096 entries per block
+constexpr int SC_PER = 4096;
+__global__ __launch_bounds__(1024) void k_scan_blocks(const unsigned *__restrict__ in, int64_t m, unsigned long long *__restrict__ out,
+                                                      unsigned *__restrict__ block_tot) {
+    __shared__ unsigned long long sh[1024];
+    int64_t b0 = (int64_t)blockIdx.x * SC_PER + (int64_t)threadIdx.x * 4;
+    unsigned v[4];
+    unsigned long long sum = 0;
+    for (int q = 0; q < 4; q++) { v[q] = (b0 + q < m) ? in[b0 + q] : 0u; sum += v[q]; }
+    sh[threadIdx.x] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        unsigned long long x = threadIdx.x >= (unsigned)o ? sh[threadIdx.x - o] : 0;
+        __syncthreads();
+        sh[threadIdx.x] += x;
+        __syncthreads();
+    }
+    unsigned long long run = sh[threadIdx.x] - sum;
+    for (int q = 0; q < 4; q++) {
+        if (b0 + q < m) out[b0 + q] = run;
+        run += v[q];
+    }
+    if (threadIdx.x == 1023) block_tot[blockIdx.x] = (unsigned)sh[1023];
+}
+__global__ __launch_bounds__(256) void k_scan_add(unsigned long long *__restrict__ out, int64_t m,
+                                                  const unsigned long long *__restrict__ block_off) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) out[i] += block_off[i / SC_PER];
+}
+
+__global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const TilePartial *__restrict__ parts, int64_t n,
+                                                          unsigned long long mask, int shift,
+                                                          const unsigned long long *__restrict__ O, int64_t ntiles,
+                                                          TilePartial *__restrict__ dst) {
+    __shared__ unsigned long long cur[RP_BINS];
+    for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) cur[d] = O[(int64_t)d * ntiles + blockIdx.x];
+    __syncthreads();
+    int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
+    int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
+    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) {
+        TilePartial p = parts[i];
+        unsigned long long pos = atomicAdd(&cur[rp_digit(p, mask, shift)], 1ull);
+        dst[pos] = p;
+    }
+}
+
+// =====================================================================================================
+// K3': owner merge. One workgroup owns one table region (the partition's bins), so the state is updated with
+// plain loads/stores instead of device-scope atomics. Within a workgroup, each chunk of 256 partials is first
+// de-duplicated in LDS; empty global slots are claimed through an LDS claim set, so two keys of a chunk never
+// take the same slot; chunks are applied in order.
+// =====================================================================================================
+constexpr int MO_THREADS = 256;
+constexpr int MO_LSLOTS = 512;
+constexpr int MO_CLAIM = 1024;
+
+struct MoShared {
+    unsigned long long kc[MO_LSLOTS];
+    unsigned long long kw[MO_LSLOTS];
+    unsigned long long cnt[MO_LSLOTS];
+    unsigned long long nsp[MO_LSLOTS];
+    double ssp[MO_LSLOTS];
+    double slat[MO_LSLOTS];
+    double slon[MO_LSLOTS];
+    unsigned long long claim[MO_CLAIM];   // claimed global slot index + 1, 0 = free
+    unsigned short uniq[MO_THREADS];
+    unsigned n_uniq;
+};
+
+template <typename T>
+__device__ __forceinline__ T ld_l2(const T *p) {   // bypass the CU's L1 (chunks of one workgroup re-read slots)
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *__restrict__ parts, int64_t n,
+                                                            const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
+                                                            TileSlot *tab, unsigned long long mask, unsigned long long rmask,
+                                                            unsigned long long seq, unsigned int *touched, WinCount *wmap,
+                                                            DevStats *st) {
+    __shared__ MoShared S;
+    __shared__ WinLds WL;
+    wl_init(WL);
+    const int t = threadIdx.x;
+    unsigned long long created_cnt = 0;
+    bool overflow = false;
+    for (int q = t; q < MO_LSLOTS; q += MO_THREADS) { S.kc[q] = 0; S.kw[q] = 0; S.cnt[q] = 0; S.nsp[q] = 0;
+        S.ssp[q] = 0.0; S.slat[q] = 0.0; S.slon[q] = 0.0; }
+    for (int q = t; q < MO_CLAIM; q += MO_THREADS) S.claim[q] = 0;
+    if (t == 0) S.n_uniq = 0;
+    __syncthreads();
+    for (int bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
+        const int64_t b0 = (int64_t)O[(int64_t)bin * ntiles];
+        const int64_t b1 = bin + 1 < nbins ? (int64_t)O[(int64_t)(bin + 1) * ntiles] : n;
+        for (int64_t c0 = b0; c0 < b1; c0 += MO_THREADS) {
+            // 1. de-duplicate the chunk in LDS
+            const int64_t i = c0 + t;
+            if (i < b1) {
+                const TilePartial p = parts[i];
+                const unsigned long long we = wenc_of(p.wstart);
+                unsigned h = (unsigned)(mix64(tile_hash(p.cell, p.wstart)) & (MO_LSLOTS - 1));
+                for (int probe = 0; probe < MO_LSLOTS; probe++) {
+                    unsigned long long oc = atomicCAS(&S.kc[h], 0ull, (unsigned long long)p.cell);
+                    if (oc == 0 || oc == p.cell) {
+                        unsigned long long ow = atomicCAS(&S.kw[h], 0ull, we);
+                        if (ow == 0) { unsigned k = atomicAdd(&S.n_uniq, 1u); S.uniq[k] = (unsigned short)h; }
+                        if (ow == 0 || ow == we) break;
+                    }
+                    h = (h + 1) & (MO_LSLOTS - 1);
+                }
+                atomicAdd(&S.cnt[h], (unsigned long long)p.count);
+                atomicAdd(&S.nsp[h], (unsigned long long)p.nspeed);
+                atomicAdd(&S.ssp[h], p.sspeed);
+                atomicAdd(&S.slat[h], p.slat);
+                atomicAdd(&S.slon[h], p.slon);
+            }
+            __syncthreads();
+            // 2. one lane per unique key: find its slot or claim an empty one (LDS claim set)
+            const unsigned nu = S.n_uniq;
+            const bool active = (unsigned)t < nu;
+            long long gslot = -1;
+            bool created = false;
+            int ls = 0;
+            unsigned long long c = 0, we = 0;
+            if (active) {
+                ls = S.uniq[t];
+                c = S.kc[ls];
+                we = S.kw[ls];
+                const int64_t w = wdec(we);
+                unsigned long long h = tile_hash(c, w) & mask;
+                for (unsigned long long probe = 0; probe <= rmask; probe++) {
+                    const unsigned long long cc = ld_l2(&tab[h].cell);
+                    if (cc == EMPTY_CELL) {
+                        unsigned ch = (unsigned)(mix64(h) & (MO_CLAIM - 1));
+                        bool mine = false, taken = false;
+                        for (int k = 0; k < MO_CLAIM; k++) {
+                            unsigned long long o = atomicCAS(&S.claim[ch], 0ull, h + 1);
+                            if (o == 0) { mine = true; break; }
+                            if (o == h + 1) { taken = true; break; }
+                            ch = (ch + 1) & (MO_CLAIM - 1);
+                        }
+                        if (mine) { gslot = (long long)h; created = true; break; }
+                        (void)taken;
+                    } else if (cc == c && ld_l2(&tab[h].wenc) == we) {
+                        gslot = (long long)h;
+                        break;
+                    }
+                    h = next_slot(h, rmask);
+                }
+                if (gslot < 0) overflow = true;
+            }
+            // 3. apply (this workgroup is the only writer of the region)
+            bool first = false;
+            if (gslot >= 0) {
+                TileSlot *sl = &tab[gslot];
+                if (created) {
+                    TileSlot v;
+                    v.cell = c;
+                    v.wenc = we;
+                    v.count = S.cnt[ls];
+                    v.nspeed = S.nsp[ls];
+                    v.sspeed = S.ssp[ls];
+                    v.slat = S.slat[ls];
+                    v.slon = S.slon[ls];
+                    v.touched = seq;
+                    *sl = v;
+                    first = true;
+                    created_cnt++;
+                } else {
+                    const unsigned long long tc = ld_l2(&sl->touched);
+                    first = tc != seq;
+                    sl->count = ld_l2(&sl->count) + S.cnt[ls];
+                    if (S.nsp[ls]) {
+                        sl->nspeed = ld_l2(&sl->nspeed) + S.nsp[ls];
+                        sl->sspeed = ld_l2(&sl->sspeed) + S.ssp[ls];
+                    }
+                    sl->slat = ld_l2(&sl->slat) + S.slat[ls];
+                    sl->slon = ld_l2(&sl->slon) + S.slon[ls];
+                    if (first) sl->touched = seq;
+                }
+            }
+            if (!wave_count_windows(created, we, WL, wmap)) overflow = true;
+            unsigned long long pos = wave_append(first, &st->n_touched);
+            if (first) touched[pos] = (unsigned int)gslot;
+            // 4. make this chunk's stores visible to the next chunk's probes, reset the LDS tables
+            __threadfence_block();
+            __syncthreads();
+            if (active) {
+                S.kc[ls] = 0; S.kw[ls] = 0; S.cnt[ls] = 0; S.nsp[ls] = 0;
+                S.ssp[ls] = 0.0; S.slat[ls] = 0.0; S.slon[ls] = 0.0;
+            }
+            for (int q = t; q < MO_CLAIM; q += MO_THREADS) S.claim[q] = 0;
+            if (t == 0) S.n_uniq = 0;
+            __syncthreads();
+        }
+    }
+    if (!wl_flush(WL, wmap)) overflow = true;
     created_cnt = wave_sum(created_cnt);
     unsigned long long ov = __ballot(overflow);
     if (lane_id() == 0) {
@@ -377,8 +645,11 @@ __global__ __launch_bounds__(256) void k_emit(const TileSlot *__restrict__ tab, 
 // compaction into a cleared table: keep keys whose window end is after keep_end_us (dead keys -- evicted by an
 // earlier batch's watermark -- are dropped) and rebuild the window map
 __global__ __launch_bounds__(256) void k_rehash(const TileSlot *__restrict__ old, unsigned long long old_cap, TileSlot *nt,
-                                                unsigned long long new_mask, int64_t tile_us, int64_t keep_end_us,
-                                                WinCount *wmap, DevStats *st) {
+                                                unsigned long long new_mask, unsigned long long new_rmask, int64_t tile_us,
+                                                int64_t keep_end_us, WinCount *wmap, DevStats *st) {
+    __shared__ WinLds WL;
+    wl_init(WL);
+    __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     unsigned long long kept = 0;
     bool overflow = false;
@@ -391,7 +662,7 @@ __global__ __launch_bounds__(256) void k_rehash(const TileSlot *__restrict__ old
             we = s.wenc;
             if (s.cell != EMPTY_CELL && we != 0 && wdec(we) + tile_us > keep_end_us) {
                 bool created;
-                long long h = find_or_claim_tile(nt, new_mask, s.cell, wdec(we), created);
+                long long h = find_or_claim_tile(nt, new_mask, new_rmask, s.cell, wdec(we), created);
                 if (h < 0) {
                     overflow = true;
                 } else {
@@ -402,8 +673,10 @@ __global__ __launch_bounds__(256) void k_rehash(const TileSlot *__restrict__ old
                 }
             }
         }
-        if (!wave_count_windows(keep, we, wmap)) overflow = true;
+        if (!wave_count_windows(keep, we, WL, wmap)) overflow = true;
     }
+    __syncthreads();
+    if (!wl_flush(WL, wmap)) overflow = true;
     kept = wave_sum(kept);
     unsigned long long ov = __ballot(overflow);
     if (lane_id() == 0) {
@@ -478,8 +751,13 @@ __global__ __launch_bounds__(256) void k_dedup_max(const uint64_t *__restrict__ 
             if (take && v == EMPTY_VKEY) { bad++; take = false; }
             if (take) {
                 h = find_or_claim_vkey(tab, mask, v, claimed);
-                if (h < 0) overflow = true;
-                else atomicMax(&tab[h].maxts, t);
+                if (h < 0) {
+                    overflow = true;
+                } else {
+                    // a stale relaxed read is <= the true max: it can only cost an extra atomic
+                    long long cur = __hip_atomic_load(&tab[h].maxts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (t > cur) atomicMax(&tab[h].maxts, t);
+                }
             }
         }
         unsigned long long pos = wave_append(claimed, n_used);
@@ -677,11 +955,11 @@ struct hm_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     hipEvent_t ev[8] = {};
-    double timings[6] = {0, 0, 0, 0, 0, 0};
+    double timings[7] = {0, 0, 0, 0, 0, 0, 0};
     // per-event
     DevBuf in_lat, in_lon, in_ts, in_speed, in_sv, in_vkey, in_rv;
     DevBuf cell, wstart, flags, win, rows, block_counts, block_offs;
-    DevBuf partials, cands;
+    DevBuf partials, cands, parts_sorted, rp_H, rp_O, rp_btot, rp_boff;
     // persistent tile state: open-addressing table + an equally sized compaction target (double buffer).
     // Eviction is lazy: a key whose window end <= the eviction watermark can never be updated again (every
     // later row of its window is dropped as late), so it stays in place, is excluded from n_state through the
@@ -776,6 +1054,16 @@ static uint64_t next_pow2(uint64_t v) {
     return p;
 }
 
+// Region geometry of a table of `cap` slots: RP_BINS owned regions (the partition's bins) once every region
+// has >= 2^MIN_REGION_BITS slots (at load <= 1/2 the fullest of 4096 regions then stays far below full);
+// smaller tables are one region (atomic merge path only).
+constexpr int MIN_REGION_BITS = 10;
+static bool regioned(unsigned long long cap) { return (63 - __builtin_clzll(cap)) >= RP_BITS + MIN_REGION_BITS; }
+static unsigned long long region_mask(unsigned long long cap) {
+    int log2cap = 63 - __builtin_clzll(cap);
+    return regioned(cap) ? (UINT64_C(1) << (log2cap - RP_BITS)) - 1 : cap - 1;
+}
+
 static int alloc_table(hm_ctx *ctx, unsigned long long cap, TileSlot **out) {
     TileSlot *t = nullptr;
     if (hipMalloc(&t, cap * sizeof(TileSlot)) != hipSuccess) {
@@ -805,7 +1093,7 @@ static int state_reserve(hm_ctx *ctx, int64_t incoming) {
     HIPCHK(ctx, hipMemsetAsync(ctx->wmap, 0, WMAP_SLOTS * sizeof(WinCount), ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->d_st, 0, sizeof(DevStats), ctx->stream));
     hipLaunchKernelGGL(k_rehash, dim3(grid_for(ctx->cap, 256, 256 * 32)), dim3(256), 0, ctx->stream, ctx->tab, ctx->cap, dst,
-                       want - 1, ctx->cfg.tile_us, ctx->dead_end_us, ctx->wmap, ctx->d_st);
+                       want - 1, region_mask(want), ctx->cfg.tile_us, ctx->dead_end_us, ctx->wmap, ctx->d_st);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -989,10 +1277,42 @@ static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_par
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
     ctx->seq++;
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
-    if (n_parts > 0) {
-        hipLaunchKernelGGL(k_merge, dim3(grid_for(n_parts, 256)), dim3(256), 0, ctx->stream, parts, n_parts, ctx->tab,
-                           ctx->cap - 1, ctx->seq, (unsigned int *)ctx->touched.p, ctx->wmap, ctx->d_st);
+    // group the partials by table region so the merge works region by region
+    int log2cap = 63 - __builtin_clzll(ctx->cap);
+    if (n_parts >= (int64_t)RP_TILE && regioned(ctx->cap)) {
+        int64_t ntiles = (n_parts + RP_TILE - 1) / RP_TILE;
+        int64_t m = (int64_t)RP_BINS * ntiles;
+        int64_t nb = (m + SC_PER - 1) / SC_PER;
+        if ((rc = ensure(ctx, ctx->parts_sorted, n_parts * sizeof(TilePartial))) || (rc = ensure(ctx, ctx->rp_H, m * 4)) ||
+            (rc = ensure(ctx, ctx->rp_O, m * 8)) || (rc = ensure(ctx, ctx->rp_btot, nb * 4)) || (rc = ensure(ctx, ctx->rp_boff, nb * 8)))
+            return rc;
+        int shift = log2cap - RP_BITS;
+        unsigned long long mask = ctx->cap - 1;
+        hipLaunchKernelGGL(k_rp_hist, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n_parts, mask, shift,
+                           (unsigned *)ctx->rp_H.p, ntiles);
+        hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_H.p, m,
+                           (unsigned long long *)ctx->rp_O.p, (unsigned *)ctx->rp_btot.p);
+        hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_btot.p, nb,
+                           (unsigned long long *)ctx->rp_boff.p, ctx->d_scratch + 254);
+        hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, (unsigned long long *)ctx->rp_O.p, m,
+                           (const unsigned long long *)ctx->rp_boff.p);
+        hipLaunchKernelGGL(k_rp_scatter, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n_parts, mask, shift,
+                           (const unsigned long long *)ctx->rp_O.p, ntiles, (TilePartial *)ctx->parts_sorted.p);
         HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
+        hipLaunchKernelGGL(k_merge_owned, dim3(RP_BINS), dim3(MO_THREADS), 0, ctx->stream,
+                           (const TilePartial *)ctx->parts_sorted.p, n_parts, (const unsigned long long *)ctx->rp_O.p, ntiles,
+                           RP_BINS, ctx->tab, mask, region_mask(ctx->cap), ctx->seq, (unsigned int *)ctx->touched.p, ctx->wmap,
+                           ctx->d_st);
+        HIPCHK(ctx, hipGetLastError());
+    } else {
+        HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
+        if (n_parts > 0) {
+            hipLaunchKernelGGL(k_merge, dim3(grid_for(n_parts, 256)), dim3(256), 0, ctx->stream, parts, n_parts, ctx->tab,
+                               ctx->cap - 1, region_mask(ctx->cap), ctx->seq, (unsigned int *)ctx->touched.p, ctx->wmap,
+                               ctx->d_st);
+            HIPCHK(ctx, hipGetLastError());
+        }
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
     int64_t m = std::max<int64_t>(n_parts, 1);
@@ -1094,6 +1414,8 @@ static void record_timings(hm_ctx *ctx) {
     ctx->timings[3] = el(4, 5);
     ctx->timings[4] = el(5, 6);
     ctx->timings[5] = el(0, 6);
+    ctx->timings[2] = el(7, 4);   // merge proper
+    ctx->timings[6] = el(3, 7);   // partition by table region
 }
 
 extern "C" {
@@ -1185,7 +1507,7 @@ const char *hm_last_error(const hm_ctx *ctx) { return ctx ? ctx->err.c_str() : g
 
 int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n) {
     if (!ctx || !ms) return HM_E_INVALID;
-    for (int i = 0; i < n && i < 6; i++) ms[i] = ctx->timings[i];
+    for (int i = 0; i < n && i < 7; i++) ms[i] = ctx->timings[i];
     return HM_OK;
 }
 
@@ -1423,13 +1745,20 @@ int hm_selftest_ld_ops(const double *a, int64_t n, int32_t op, double *out) {
     for (int64_t i = 0; i < n; i++) {
         double x = a[i], r;
         switch (op) {
-            case 0: r = xld_mul(x, HM_LD_PI_180_M, HM_LD_PI_180_E); break;
-            case 1: r = xld_mul(x, HM_LD_SQRT7_M, HM_LD_SQRT7_E); break;
-            case 2: r = xld_mul(x, HM_LD_RSIN60_M, HM_LD_RSIN60_E); break;
-            case 3: r = xld_add(x, false, HM_LD_2PI_M, HM_LD_2PI_E); break;
-            case 4: r = xld_add(x, true, HM_LD_2PI_M, HM_LD_2PI_E); break;
-            case 5: r = xld_add(x, true, HM_LD_AP7_ROT_M, HM_LD_AP7_ROT_E); break;
-            case 6: r = xld_add(x, false, HM_LD_AP7_ROT_M, HM_LD_AP7_ROT_E); break;
+            case 0: r = XMUL(x, PI_180); break;
+            case 1: r = XMUL(x, SQRT7); break;
+            case 2: r = XMUL(x, RSIN60); break;
+            case 3: r = XADD(x, false, 2PI); break;
+            case 4: r = XADD(x, true, 2PI); break;
+            case 5: r = XADD(x, true, AP7_ROT); break;
+            case 6: r = XADD(x, false, AP7_ROT); break;
+            case 10: r = xld_mul(x, HM_LD_PI_180_M, HM_LD_PI_180_E); break;
+            case 11: r = xld_mul(x, HM_LD_SQRT7_M, HM_LD_SQRT7_E); break;
+            case 12: r = xld_mul(x, HM_LD_RSIN60_M, HM_LD_RSIN60_E); break;
+            case 13: r = xld_add(x, false, HM_LD_2PI_M, HM_LD_2PI_E); break;
+            case 14: r = xld_add(x, true, HM_LD_2PI_M, HM_LD_2PI_E); break;
+            case 15: r = xld_add(x, true, HM_LD_AP7_ROT_M, HM_LD_AP7_ROT_E); break;
+            case 16: r = xld_add(x, false, HM_LD_AP7_ROT_M, HM_LD_AP7_ROT_E); break;
             default: return HM_E_INVALID;
         }
         out[i] = r;

@@ -27,11 +27,13 @@ def _inputs(op):
     return np.r_[special, r, np.nextafter(r[:1000], np.inf)]
 
 
+@pytest.mark.parametrize("path", ["fast", "exact"])
 @pytest.mark.parametrize("op", sorted(OPS))
-def test_x87_emulation_bit_exact(oracle_h3, mobheat_lib, op):
+def test_x87_emulation_bit_exact(oracle_h3, mobheat_lib, op, path):
+    """fast = fp64 error-free path with exact fallback (what the kernels run); exact = 128-bit integer path."""
     from mobheat import _lib
     a = _inputs(op)
-    got = _lib.ld_ops_selftest(a, op)
+    got = _lib.ld_ops_selftest(a, op + (10 if path == "exact" else 0))
     exp = oracle_h3.ld_ops(a, op)
     same = (got.view(np.uint64) == exp.view(np.uint64)) | (np.isnan(got) & np.isnan(exp))
     assert same.all(), f"{OPS[op]}: {np.count_nonzero(~same)} mismatches, e.g. a={a[~same][:3]!r}"

@@ -1,0 +1,115 @@
+"""CPU: the host side of the drop-in boundary (mobheat/stream.py) against the reference's document formats.
+
+Expected documents are written out literally from reference heatmap_stream.py:164-188 (tiles) and :211-228
+(positions_latest); BSON encoding uses the real pymongo/bson to pin datetime handling (naive datetimes are
+encoded as UTC milliseconds, sub-millisecond digits dropped -- SURVEY.md App. A.7).
+"""
+import datetime
+
+import bson
+import numpy as np
+import pandas as pd
+import pyarrow as pa
+import pytest
+
+from mobheat import stream
+from mobheat.engine import TileRows
+
+
+def _tiles(**kw):
+    n = len(kw["cell"])
+    base = dict(cell=np.array(kw["cell"], np.uint64), window_start_us=np.array(kw["ws"], np.int64))
+    base["window_end_us"] = base["window_start_us"] + 300_000_000
+    base["count"] = np.array(kw.get("count", [1] * n), np.int64)
+    base["avg_speed"] = np.array(kw.get("avg_speed", [0.0] * n), np.float64)
+    base["speed_null"] = np.array(kw.get("speed_null", [False] * n), bool)
+    base["avg_lon"] = np.array(kw.get("avg_lon", [0.0] * n), np.float64)
+    base["avg_lat"] = np.array(kw.get("avg_lat", [0.0] * n), np.float64)
+    return TileRows(**base)
+
+
+def test_tile_document_matches_reference_format():
+    ws = 1759573200 * 1_000_000          # 2025-10-04T10:20:00Z
+    t = _tiles(cell=[0x882A1072B5FFFFF], ws=[ws], count=[7], avg_speed=[21.5], avg_lon=[-71.06], avg_lat=[42.355])
+    ops = stream.tile_ops(t, city="ath", h3_res=8, ttl_min=45)
+    assert len(ops) == 1
+    op = ops[0]
+    _id = "ath|h3r8|882a1072b5fffff|2025-10-04T10:20:00Z"
+    start = datetime.datetime(2025, 10, 4, 10, 20)
+    end = datetime.datetime(2025, 10, 4, 10, 25)
+    assert op._filter == {"_id": _id}
+    assert op._upsert is True
+    assert op._doc == {"$set": {
+        "_id": _id, "city": "ath", "grid": "h3r8", "cellId": "882a1072b5fffff",
+        "windowStart": start, "windowEnd": end, "count": 7, "avgSpeedKmh": 21.5,
+        "centroid": {"type": "Point", "coordinates": [-71.06, 42.355]},
+        "staleAt": end + datetime.timedelta(minutes=45)}}
+    # key order of the $set document is the reference's (:176-187)
+    assert list(op._doc["$set"]) == ["_id", "city", "grid", "cellId", "windowStart", "windowEnd", "count",
+                                     "avgSpeedKmh", "centroid", "staleAt"]
+
+
+def test_tile_null_coercions_follow_reference():
+    # count or 0; avg or 0.0 (null -> 0.0, NaN stays NaN because NaN is truthy; -0.0 -> 0.0 because falsy)
+    t = _tiles(cell=[1, 2], ws=[0, 0], avg_speed=[0.0, float("nan")], speed_null=[True, False],
+               avg_lat=[-0.0, 1.0], avg_lon=[2.0, -0.0])
+    d0, d1 = (op._doc["$set"] for op in stream.tile_ops(t, "ath", 8, 45))
+    assert d0["avgSpeedKmh"] == 0.0 and np.isnan(d1["avgSpeedKmh"])
+    assert str(d0["centroid"]["coordinates"][1]) == "0.0" and str(d1["centroid"]["coordinates"][0]) == "0.0"
+
+
+def test_position_document_matches_reference_format():
+    cols = dict(provider=pd.Series(["mbta", "mbta"]), vehicleId=pd.Series(["y1", "BUS_1432"]),
+                ts_us=np.array([0, 1759573325 * 1_000_000 + 123456]), lat=np.array([0.0, 42.355]),
+                lon=np.array([0.0, -71.06]))
+    (op,) = stream.position_ops(cols, [1])
+    ts = datetime.datetime(2025, 10, 4, 10, 22, 5, 123456)
+    assert op._filter == {"_id": "mbta|BUS_1432", "$or": [{"ts": {"$exists": False}}, {"ts": {"$lt": ts}}]}
+    assert op._doc == {"$set": {"provider": "mbta", "vehicleId": "BUS_1432", "ts": ts,
+                                "loc": {"type": "Point", "coordinates": [-71.06, 42.355]}}}
+    assert op._upsert is True
+    # BSON datetimes are UTC milliseconds: the microseconds are floored (bson/datetime_ms.py)
+    enc = bson.decode(bson.encode({"ts": ts}))
+    assert enc["ts"] == datetime.datetime(2025, 10, 4, 10, 22, 5, 123000)
+
+
+def test_bulk_chunks_of_1000_tiles_first():
+    calls = []
+
+    class Sink:
+        def bulk_write(self, coll, ops):
+            calls.append((coll, len(ops)))
+
+    t = _tiles(cell=list(range(1, 2501)), ws=[0] * 2500)
+    stream._flush(Sink(), "tiles", stream.tile_ops(t, "ath", 8, 45))
+    assert calls == [("tiles", 1000), ("tiles", 1000), ("tiles", 500)]
+
+
+@pytest.mark.parametrize("kind", ["pandas", "arrow"])
+def test_batch_columns_nulls_and_keys(kind):
+    df = pd.DataFrame({
+        "provider": ["mbta", "mbta", None, "opensky", "mbta"],
+        "vehicleId": ["a", "b", "a", "a", None],
+        "lat": [42.3, None, 42.3, 10.0, 42.3],
+        "lon": [-71.0, -71.0, -71.0, 20.0, -71.0],
+        "speedKmh": [10.0, None, 3.0, float("nan"), 1.0],
+        "eventTs": pd.to_datetime(["2025-10-04T10:22:05Z", "2025-10-04T10:22:06Z", None, "2025-10-04T10:22:07.500Z",
+                                   "2025-10-04T10:22:08Z"], utc=True, format="ISO8601"),
+    })
+    src = df if kind == "pandas" else pa.Table.from_pandas(df, preserve_index=False)
+    c = stream.batch_columns(src)
+    assert c["n"] == 5
+    assert c["row_valid"].tolist() == [True, True, False, True, False]
+    assert np.isnan(c["lat"][1])
+    assert c["speed_valid"].tolist()[:2] == [True, False]
+    assert c["ts_us"][3] == 1759573327_500000
+    k = c["vkey"]
+    assert k[0] != k[1] and k[0] != k[3]       # (mbta,a) vs (mbta,b) vs (opensky,a)
+
+
+def test_iso_ts_strings_parse_like_to_timestamp():
+    df = pd.DataFrame({"provider": ["p", "p"], "vehicleId": ["v", "w"], "lat": [1.0, 2.0], "lon": [1.0, 2.0],
+                       "speedKmh": [1.0, 2.0], "ts": ["2025-09-26T12:45:10Z", "not a time"]})
+    c = stream.batch_columns(df)
+    assert c["ts_us"][0] == 1758890710 * 1_000_000
+    assert c["row_valid"].tolist() == [True, False]
