@@ -84,7 +84,15 @@ __device__ __forceinline__ unsigned long long wave_append(bool pred, unsigned lo
 // =====================================================================================================
 // K1: filter + latLngToCell + window + late test
 // =====================================================================================================
-__global__ __launch_bounds__(256) void k_snap(const double *__restrict__ lat, const double *__restrict__ lon,
+#ifndef HM_SNAP_WAVES
+#define HM_SNAP_WAVES 0
+#endif
+#if HM_SNAP_WAVES > 0
+#define HM_SNAP_ATTR __attribute__((amdgpu_waves_per_eu(HM_SNAP_WAVES)))
+#else
+#define HM_SNAP_ATTR
+#endif
+__global__ __launch_bounds__(256) HM_SNAP_ATTR void k_snap(const double *__restrict__ lat, const double *__restrict__ lon,
                                               const int64_t *__restrict__ ts, const uint8_t *__restrict__ row_valid,
                                               int64_t n, int res, int64_t tile_us, int64_t late_end_us,
                                               uint64_t *__restrict__ cell_out, int64_t *__restrict__ wstart_out,
@@ -480,6 +488,7 @@ struct MoShared {
     unsigned long long claim[MO_CLAIM];   // claimed global slot index + 1, 0 = free
     unsigned short uniq[MO_THREADS];
     unsigned n_uniq;
+    unsigned n_touched;                   // keys of the current bin touched for the first time this batch
 };
 
 template <typename T>
@@ -490,8 +499,8 @@ __device__ __forceinline__ T ld_l2(const T *p) {   // bypass the CU's L1 (chunks
 __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *__restrict__ parts, int64_t n,
                                                             const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
                                                             TileSlot *tab, unsigned long long mask, unsigned long long rmask,
-                                                            unsigned long long seq, unsigned int *touched, WinCount *wmap,
-                                                            DevStats *st) {
+                                                            unsigned long long seq, unsigned int *touched, unsigned *bin_cnt,
+                                                            WinCount *wmap, DevStats *st) {
     __shared__ MoShared S;
     __shared__ WinLds WL;
     wl_init(WL);
@@ -501,7 +510,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
     for (int q = t; q < MO_LSLOTS; q += MO_THREADS) { S.kc[q] = 0; S.kw[q] = 0; S.cnt[q] = 0; S.nsp[q] = 0;
         S.ssp[q] = 0.0; S.slat[q] = 0.0; S.slon[q] = 0.0; }
     for (int q = t; q < MO_CLAIM; q += MO_THREADS) S.claim[q] = 0;
-    if (t == 0) S.n_uniq = 0;
+    if (t == 0) { S.n_uniq = 0; S.n_touched = 0; }
     __syncthreads();
     for (int bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
         const int64_t b0 = (int64_t)O[(int64_t)bin * ntiles];
@@ -594,8 +603,12 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
                 }
             }
             if (!wave_count_windows(created, we, WL, wmap)) overflow = true;
-            unsigned long long pos = wave_append(first, &st->n_touched);
-            if (first) touched[pos] = (unsigned int)gslot;
+            // the bin's touched keys go to its own segment [b0, b0 + n) of the list (an LDS counter, no global atomic)
+            const unsigned long long fb = __ballot(first);
+            unsigned tbase = 0;
+            if (lane_id() == 0 && fb) tbase = atomicAdd(&S.n_touched, (unsigned)__popcll(fb));
+            tbase = __shfl(tbase, 0, 64);
+            if (first) touched[b0 + tbase + (unsigned)__popcll(fb & ((1ull << lane_id()) - 1))] = (unsigned int)gslot;
             // 4. make this chunk's stores visible to the next chunk's probes, reset the LDS tables
             __threadfence_block();
             __syncthreads();
@@ -607,6 +620,8 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
             if (t == 0) S.n_uniq = 0;
             __syncthreads();
         }
+        if (t == 0) { bin_cnt[bin] = S.n_touched; S.n_touched = 0; }
+        __syncthreads();
     }
     if (!wl_flush(WL, wmap)) overflow = true;
     created_cnt = wave_sum(created_cnt);
@@ -619,6 +634,33 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
 
 // =====================================================================================================
 // K4: emit touched keys (update-mode output rows, cumulative aggregates)
+// Spark Average: sum / count (count of non-null inputs) as double; null when that count is 0
+__device__ __forceinline__ void emit_row(const TileSlot &s, int64_t t, uint64_t *o_cell, int64_t *o_ws, int64_t *o_cnt,
+                                         double *o_sp, uint8_t *o_spnull, double *o_lon, double *o_lat) {
+    o_cell[t] = s.cell;
+    o_ws[t] = wdec(s.wenc);
+    o_cnt[t] = (int64_t)s.count;
+    bool null_sp = s.nspeed == 0;
+    o_sp[t] = null_sp ? 0.0 : s.sspeed / (double)s.nspeed;
+    o_spnull[t] = null_sp;
+    o_lon[t] = s.slon / (double)s.count;
+    o_lat[t] = s.slat / (double)s.count;
+}
+// after k_merge_owned: bin b's touched keys are touched[seg0(b), seg0(b) + cnt[b]), its rows go to off[b]...
+__global__ __launch_bounds__(256) void k_emit_bins(const TileSlot *__restrict__ tab, const unsigned int *__restrict__ touched,
+                                                   const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
+                                                   const unsigned *__restrict__ cnt, const unsigned long long *__restrict__ off,
+                                                   uint64_t *o_cell, int64_t *o_ws, int64_t *o_cnt, double *o_sp,
+                                                   uint8_t *o_spnull, double *o_lon, double *o_lat) {
+    for (int bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
+        const int64_t seg = (int64_t)O[(int64_t)bin * ntiles];
+        const int64_t o = (int64_t)off[bin];
+        const unsigned c = cnt[bin];
+        for (unsigned k = threadIdx.x; k < c; k += blockDim.x)
+            emit_row(tab[touched[seg + k]], o + k, o_cell, o_ws, o_cnt, o_sp, o_spnull, o_lon, o_lat);
+    }
+}
+
 // =====================================================================================================
 __global__ __launch_bounds__(256) void k_emit(const TileSlot *__restrict__ tab, const unsigned int *__restrict__ touched,
                                               const unsigned long long *n_touched, uint64_t *o_cell, int64_t *o_ws,
@@ -626,16 +668,7 @@ __global__ __launch_bounds__(256) void k_emit(const TileSlot *__restrict__ tab, 
     const int64_t n = (int64_t)*n_touched;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
-        const TileSlot s = tab[touched[t]];
-        o_cell[t] = s.cell;
-        o_ws[t] = wdec(s.wenc);
-        o_cnt[t] = (int64_t)s.count;
-        // Spark Average: sum / count (count of non-null inputs) as double; null when that count is 0
-        bool null_sp = s.nspeed == 0;
-        o_sp[t] = null_sp ? 0.0 : s.sspeed / (double)s.nspeed;
-        o_spnull[t] = null_sp;
-        o_lon[t] = s.slon / (double)s.count;
-        o_lat[t] = s.slat / (double)s.count;
+        emit_row(tab[touched[t]], t, o_cell, o_ws, o_cnt, o_sp, o_spnull, o_lon, o_lat);
     }
 }
 
@@ -972,6 +1005,7 @@ struct hm_ctx {
     WinCount *wmap = nullptr, *h_wmap = nullptr;
     int wmap_used = 0;
     DevBuf touched;
+    DevBuf bin_cnt, bin_off;   // k_merge_owned: touched keys per table region, their output offsets
     unsigned long long seq = 0;
     // dedup table (persistent, cleared through its used list)
     DedupSlot *dtab = nullptr;
@@ -1269,6 +1303,16 @@ static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t 
     return HM_OK;
 }
 
+static int ensure_outputs(hm_ctx *ctx, int64_t n_rows) {
+    int rc;
+    int64_t m = std::max<int64_t>(n_rows, 1);
+    if ((rc = ensure(ctx, ctx->o_cell, m * 8)) || (rc = ensure(ctx, ctx->o_ws, m * 8)) || (rc = ensure(ctx, ctx->o_cnt, m * 8)) ||
+        (rc = ensure(ctx, ctx->o_sp, m * 8)) || (rc = ensure(ctx, ctx->o_spn, m)) || (rc = ensure(ctx, ctx->o_lon, m * 8)) ||
+        (rc = ensure(ctx, ctx->o_lat, m * 8)))
+        return rc;
+    return HM_OK;
+}
+
 static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts) {
     int rc;
     if ((rc = state_reserve(ctx, n_parts))) return rc;
@@ -1300,11 +1344,24 @@ static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_par
                            (const unsigned long long *)ctx->rp_O.p, ntiles, (TilePartial *)ctx->parts_sorted.p);
         HIPCHK(ctx, hipGetLastError());
         HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
+        if ((rc = ensure(ctx, ctx->bin_cnt, RP_BINS * 4)) || (rc = ensure(ctx, ctx->bin_off, RP_BINS * 8))) return rc;
         hipLaunchKernelGGL(k_merge_owned, dim3(RP_BINS), dim3(MO_THREADS), 0, ctx->stream,
                            (const TilePartial *)ctx->parts_sorted.p, n_parts, (const unsigned long long *)ctx->rp_O.p, ntiles,
-                           RP_BINS, ctx->tab, mask, region_mask(ctx->cap), ctx->seq, (unsigned int *)ctx->touched.p, ctx->wmap,
-                           ctx->d_st);
+                           RP_BINS, ctx->tab, mask, region_mask(ctx->cap), ctx->seq, (unsigned int *)ctx->touched.p,
+                           (unsigned *)ctx->bin_cnt.p, ctx->wmap, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+        hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->bin_cnt.p, (int64_t)RP_BINS,
+                           (unsigned long long *)ctx->bin_off.p, &ctx->d_st->n_touched);
+        if ((rc = ensure_outputs(ctx, n_parts))) return rc;
+        hipLaunchKernelGGL(k_emit_bins, dim3(RP_BINS), dim3(256), 0, ctx->stream, ctx->tab, (const unsigned int *)ctx->touched.p,
+                           (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, (const unsigned *)ctx->bin_cnt.p,
+                           (const unsigned long long *)ctx->bin_off.p, (uint64_t *)ctx->o_cell.p, (int64_t *)ctx->o_ws.p,
+                           (int64_t *)ctx->o_cnt.p, (double *)ctx->o_sp.p, (uint8_t *)ctx->o_spn.p, (double *)ctx->o_lon.p,
+                           (double *)ctx->o_lat.p);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+        return HM_OK;
     } else {
         HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
         if (n_parts > 0) {
@@ -1315,11 +1372,7 @@ static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_par
         }
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
-    int64_t m = std::max<int64_t>(n_parts, 1);
-    if ((rc = ensure(ctx, ctx->o_cell, m * 8)) || (rc = ensure(ctx, ctx->o_ws, m * 8)) || (rc = ensure(ctx, ctx->o_cnt, m * 8)) ||
-        (rc = ensure(ctx, ctx->o_sp, m * 8)) || (rc = ensure(ctx, ctx->o_spn, m)) || (rc = ensure(ctx, ctx->o_lon, m * 8)) ||
-        (rc = ensure(ctx, ctx->o_lat, m * 8)))
-        return rc;
+    if ((rc = ensure_outputs(ctx, n_parts))) return rc;
     if (n_parts > 0) {
         hipLaunchKernelGGL(k_emit, dim3(grid_for(n_parts, 256)), dim3(256), 0, ctx->stream, ctx->tab,
                            (const unsigned int *)ctx->touched.p, &ctx->d_st->n_touched, (uint64_t *)ctx->o_cell.p,
@@ -1481,7 +1534,7 @@ void hm_destroy(hm_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->in_lat, &ctx->in_lon, &ctx->in_ts, &ctx->in_speed, &ctx->in_sv, &ctx->in_vkey, &ctx->in_rv,
                       &ctx->cell, &ctx->wstart, &ctx->flags, &ctx->win, &ctx->rows, &ctx->block_counts, &ctx->block_offs,
                       &ctx->partials, &ctx->cands,
-                      &ctx->touched, &ctx->dused, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
+                      &ctx->touched, &ctx->bin_cnt, &ctx->bin_off, &ctx->dused, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
                       &ctx->o_lon, &ctx->o_lat};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);

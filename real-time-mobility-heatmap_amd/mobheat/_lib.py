@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
+# MOBHEAT_LIB: load another build of the same ABI (kernel variants under csrc/variants/ for tuning runs)
+LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
 
 HM_ABI_VERSION = 1
 HM_MEM_HOST = 0
