@@ -159,21 +159,30 @@ HM_HD double xld_add(double a, bool negc, uint64_t cm, int ce) {
 // Rounding E to 64 bits and then to 53 bits can differ from RN53(E) = RN53(p + t) only when E lies within
 // 2^-12 ulp(p) of a 53-bit midpoint; lanes within 2^-10 ulp (and binade edges, zeros, non-finite values)
 // take the exact path.
-HM_HD bool xld_fast_ok(double head, double tail) {
+// Fast exact path for the x87 ops: with head + tail == a op C up to ~2^-52 ulp(head) (tail from an FMA
+// product or TwoSum), x87 first rounds the exact value to a 64-bit mantissa -- a grid of 2^-11 ulp(head)
+// while the result stays in head's binade -- and the store rounds that to double (RNE).  So round the tail
+// to the 2^-11 grid (exact unless it sits within ~2^-38 of a grid midpoint, where the 128-bit path takes
+// over) and let one double add do the second rounding.  Returns false when the slow path is needed.
+HM_HD bool xld_fast_round(double head, double tail, double &out) {
     uint64_t b = __builtin_bit_cast(uint64_t, head);
     int ex = (int)((b >> 52) & 0x7ff);
     uint64_t fr = b & ((UINT64_C(1) << 52) - 1);
     if (ex == 0 || ex >= 0x7fe || fr < 4 || fr > (UINT64_C(1) << 52) - 4) return false;
-    double f = ldexp(tail, 1075 - ex);         // tail in units of ulp(head), exact scaling
-    if (!(__builtin_fabs(f) <= 1.0)) return false;
-    double fr2 = f - floor(f);
-    return __builtin_fabs(fr2 - 0.5) > 0x1p-10;
+    double g = ldexp(tail, 1075 + 11 - ex);    // tail in units of 2^-11 ulp(head), exact scaling
+    if (!(__builtin_fabs(g) <= 4096.0)) return false;
+    double fl = floor(g);
+    if (__builtin_fabs((g - fl) - 0.5) < 0x1p-38) return false;
+    double gr = (g - fl) < 0.5 ? fl : fl + 1.0;
+    out = head + ldexp(gr, ex - 1075 - 11);    // exact 64-bit-mantissa value, rounded to double (RNE)
+    return true;
 }
 HM_HD double xmul(double a, uint64_t cm, int ce, double chi, double clo) {
     double p = a * chi;
     double e = fma(a, chi, -p);
     double t = fma(a, clo, e);
-    if (xld_fast_ok(p, t)) return p + t;
+    double r;
+    if (xld_fast_round(p, t, r)) return r;
     return xld_mul(a, cm, ce);
 }
 HM_HD double xadd(double a, bool negc, uint64_t cm, int ce, double chi, double clo) {
@@ -182,7 +191,8 @@ HM_HD double xadd(double a, bool negc, uint64_t cm, int ce, double chi, double c
     double bb = s - a;
     double e = (a - (s - bb)) + (ch - bb);      // TwoSum: a + ch == s + e exactly
     double t = e + cl;
-    if (xld_fast_ok(s, t)) return s + t;
+    double r;
+    if (xld_fast_round(s, t, r)) return r;
     return xld_add(a, negc, cm, ce);
 }
 #define XMUL(a, K) xmul((a), HM_LD_##K##_M, HM_LD_##K##_E, HM_LD_##K##_HI, HM_LD_##K##_LO)
@@ -379,10 +389,13 @@ HM_HD uint64_t latLngToCellDeg(double lat_deg, double lng_deg, int res, const H3
     double glat = XMUL(lat_deg, PI_180);
     double glng = XMUL(lng_deg, PI_180);
     // _geoToVec3d
-    double clat = cos(glat), slat = sin(glat);
+    // sincos: the same reduction and polynomials as separate sin and cos (device math library and glibc)
+    double clat, slat, clng, slng;
+    sincos(glat, &slat, &clat);
+    sincos(glng, &slng, &clng);
     double vz = slat;
-    double vx = cos(glng) * clat;
-    double vy = sin(glng) * clat;
+    double vx = clng * clat;
+    double vy = slng * clat;
     // _geoToClosestFace
     int face = 0;
     double sqd = 5.0;
@@ -401,7 +414,8 @@ HM_HD uint64_t latLngToCellDeg(double lat_deg, double lng_deg, int res, const H3
         hx = hy = 0.0;
     } else {
         double dlng = glng - T.faceCenterGeo[face][1];
-        double sd = sin(dlng), cd = cos(dlng);
+        double sd, cd;
+        sincos(dlng, &sd, &cd);
         double num = clat * sd;
         double t1 = T.faceCosLat[face] * slat;
         double t2 = T.faceSinLat[face] * clat;
@@ -412,8 +426,10 @@ HM_HD uint64_t latLngToCellDeg(double lat_deg, double lng_deg, int res, const H3
         r = tan(r);
         r *= HM_INV_RES0_U_GNOMONIC;
         for (int i = 0; i < res; i++) r = XMUL(r, SQRT7);
-        hx = r * cos(theta);
-        hy = r * sin(theta);
+        double st, ct;
+        sincos(theta, &st, &ct);
+        hx = r * ct;
+        hy = r * st;
     }
     IJK ijk = hex2dToCoordIJK(hx, hy);
     return faceIjkToH3(face, ijk, res, T);

@@ -84,8 +84,9 @@ __device__ __forceinline__ unsigned long long wave_append(bool pred, unsigned lo
 // =====================================================================================================
 // K1: filter + latLngToCell + window + late test
 // =====================================================================================================
+// waves per SIMD for k_snap: 3 caps it at 168 VGPRs without spills (measured best of 2..5 on MI355X)
 #ifndef HM_SNAP_WAVES
-#define HM_SNAP_WAVES 0
+#define HM_SNAP_WAVES 3
 #endif
 #if HM_SNAP_WAVES > 0
 #define HM_SNAP_ATTR __attribute__((amdgpu_waves_per_eu(HM_SNAP_WAVES)))
@@ -345,11 +346,29 @@ __device__ __forceinline__ bool wave_count_windows(bool pred, unsigned long long
     return ok;
 }
 
+constexpr unsigned KM_TBUF = 4096;
+// block-uniform: move the block's buffered touched slots to the global list with one atomic
+__device__ __forceinline__ void km_flush_touched(unsigned *tbuf, unsigned &tcnt, unsigned long long &tbase,
+                                                 unsigned int *touched, DevStats *st) {
+    const unsigned c = tcnt;
+    if (c == 0) return;
+    if (threadIdx.x == 0) tbase = atomicAdd(&st->n_touched, (unsigned long long)c);
+    __syncthreads();
+    for (unsigned q = threadIdx.x; q < c; q += blockDim.x) touched[tbase + q] = tbuf[q];
+    __syncthreads();
+    if (threadIdx.x == 0) tcnt = 0;
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void k_merge(const TilePartial *__restrict__ parts, int64_t n, TileSlot *tab,
                                                unsigned long long mask, unsigned long long rmask, unsigned long long seq,
                                                unsigned int *touched, WinCount *wmap, DevStats *st) {
     __shared__ WinLds WL;
+    __shared__ unsigned tbuf[KM_TBUF];     // touched slots, flushed to the global list in blocks
+    __shared__ unsigned tcnt;
+    __shared__ unsigned long long tbase;
     wl_init(WL);
+    if (threadIdx.x == 0) tcnt = 0;
     __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     unsigned long long created_cnt = 0;
@@ -381,10 +400,16 @@ __global__ __launch_bounds__(256) void k_merge(const TilePartial *__restrict__ p
             }
         }
         if (!wave_count_windows(created, wenc_of(w), WL, wmap)) overflow = true;
-        unsigned long long pos = wave_append(first, &st->n_touched);
-        if (first) touched[pos] = (unsigned int)h;
+        const unsigned long long fb = __ballot(first);
+        unsigned off = 0;
+        if (lane_id() == 0 && fb) off = atomicAdd(&tcnt, (unsigned)__popcll(fb));
+        off = __shfl(off, 0, 64);
+        if (first) tbuf[off + (unsigned)__popcll(fb & ((1ull << lane_id()) - 1))] = (unsigned)h;
+        __syncthreads();
+        if (tcnt > KM_TBUF - 256) km_flush_touched(tbuf, tcnt, tbase, touched, st);
     }
     __syncthreads();
+    km_flush_touched(tbuf, tcnt, tbase, touched, st);
     if (!wl_flush(WL, wmap)) overflow = true;
     created_cnt = wave_sum(created_cnt);
     unsigned long long ov = __ballot(overflow);
@@ -989,6 +1014,7 @@ struct hm_ctx {
     std::string err;
     hipEvent_t ev[8] = {};
     double timings[7] = {0, 0, 0, 0, 0, 0, 0};
+    bool force_atomic_merge = false;   // MOBHEAT_MERGE=atomic (tuning / tests): skip partition + owned merge
     // per-event
     DevBuf in_lat, in_lon, in_ts, in_speed, in_sv, in_vkey, in_rv;
     DevBuf cell, wstart, flags, win, rows, block_counts, block_offs;
@@ -1323,7 +1349,7 @@ static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_par
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
     // group the partials by table region so the merge works region by region
     int log2cap = 63 - __builtin_clzll(ctx->cap);
-    if (n_parts >= (int64_t)RP_TILE && regioned(ctx->cap)) {
+    if (n_parts >= (int64_t)RP_TILE && regioned(ctx->cap) && !ctx->force_atomic_merge) {
         int64_t ntiles = (n_parts + RP_TILE - 1) / RP_TILE;
         int64_t m = (int64_t)RP_BINS * ntiles;
         int64_t nb = (m + SC_PER - 1) / SC_PER;
@@ -1489,6 +1515,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     hm_ctx *ctx = new hm_ctx();
     ctx->cfg = *cfg;
     ctx->device = cfg->device;
+    if (const char *mm = getenv("MOBHEAT_MERGE")) ctx->force_atomic_merge = strcmp(mm, "atomic") == 0;
     auto fail = [&](const char *what) {
         g_create_err = std::string(what) + ": " + ctx->err;
         hm_destroy(ctx);

@@ -274,13 +274,17 @@ def test_foreach_batch_func_capture_sink():
     assert sorted(op._filter["_id"] for op in pos) == sorted(f"mbta|v{r:05d}" for r in exp["latest_rows"])
 
 
-def test_owned_and_atomic_merge_paths_agree():
-    """The region-owned merge (regioned table, >= 64k partials) and the atomic merge (small table) must give
-    the oracle's result on duplicate-heavy clustered data, over batches that update existing keys."""
+def test_owned_and_atomic_merge_paths_agree(monkeypatch):
+    """The region-owned merge (regioned table, >= 64k partials) and the atomic merge (small table, and forced
+    on a regioned table) must give the oracle's result on duplicate-heavy clustered data, over batches that
+    update existing keys."""
     from mobheat import HeatmapEngine, synth
     from oracle.spark_oracle import SparkHeatmapOracle
     rng = np.random.default_rng(21)
     engines = [HeatmapEngine(h3_res=10, state_capacity_hint=1 << 16), HeatmapEngine(h3_res=10, state_capacity_hint=1 << 23)]
+    monkeypatch.setenv("MOBHEAT_MERGE", "atomic")
+    engines.append(HeatmapEngine(h3_res=10, state_capacity_hint=1 << 23))
+    monkeypatch.delenv("MOBHEAT_MERGE")
     oracles = [SparkHeatmapOracle(h3_res=10) for _ in engines]
     for epoch, start in enumerate((0, 4, 8)):
         b = synth.c3_city(seed=30 + epoch, n=2_000_000, hotspots=500, n_vehicles=3000)
