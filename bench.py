@@ -5,8 +5,10 @@ Workload (N=1 and per rank for N>1, weak scaling): BASELINE.json configs[1] shap
 OpenSky-like global batch of 1e8 events uniform on the sphere, 50k vehicle ids, 15 minutes of event time
 (3 five-minute windows), 10% null speeds -- at the metric's H3 resolution 8 (configs[1] quotes res 7;
 --res 7 runs that).  One step = one micro-batch through the whole hot path on device-resident inputs:
-filter + latLngToCell + window + late test (k_snap), LDS pre-aggregation (k_local_agg), merge into the
-persistent update-mode state (k_merge), emission (k_emit), eviction/growth, and the latest-position dedup.
+one fused pass over the events (k_ingest: filter + latLngToCell + window + late test + LDS pre-aggregation +
+per-vehicle max ts), radix partition of the partials by state-table region, the region-owned merge into the
+persistent update-mode state (k_merge_owned), emission (k_emit_bins), eviction/compaction, and the
+latest-position flags + compaction.
 Every step is a NEW micro-batch: its timestamps are the previous step's + 15 min (precomputed before the
 timed region), so the stream advances, windows close and are evicted, and no row is late.
 For N>1 each rank runs the sharded path (mobheat.distributed: RCCL all-to-all of partials by owner).
@@ -30,16 +32,28 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 T0 = 1759572000 * 1_000_000
 SPAN_US = 15 * 60 * 1_000_000
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector peak: 256 CUs x 64 FMA lanes x 2 x 2.4 GHz
 
-# algorithmic bytes: per event for k_snap/k_local_agg/dedup, per record otherwise
+# algorithmic HBM bytes per unit: per event (ingest, dedup), per partial record (partition,
+# merge), per emitted tile (emit).  ingest also writes 56 B per partial (added below).
 BYTES = {
-    "snap": 42,        # read lat 8 + lon 8 + ts 8 + row_valid 1; write cell 8 + windowStart 8 + flags 1
-    "local_agg": 42,   # read cell 8 + windowStart 8 + flags 1 + speed 8 + speed_valid 1 + lat 8 + lon 8 (+56 B/partial written)
+    "ingest": 43,      # read lat 8 + lon 8 + ts 8 + speed 8 + speed_valid 1 + vkey 8 + row_valid 1; write flags 1
     "partition": 168,  # per partial: histogram read 56 B + scatter read 56 B + write 56 B
     "merge": 188,      # per partial: read 56 B record + 64 B state line read + 64 B written + 4 B touched index
     "emit": 117,       # per emitted tile: 64 B state line + 4 B index read, 49 B row written
-    "dedup": 38,       # per event: 2 x (vkey 8 + ts 8 + flags 1) + win flag 1 + 2 x 1 B compaction reads
+    "dedup": 20,       # per event: vkey 8 + ts 8 + flags 1 read, win flag 1 written, 2 x 1 B compaction reads
 }
+# k_ingest is fp64-VALU bound: its roofline is fp64 FLOP/s.  FLOPs and HBM bytes per event of this workload
+# were counted by rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r1/ingest_pmc.json).
+PMC_FILE = os.path.join(ROOT, "profiles", "r1", "ingest_pmc.json")
+
+
+def ingest_pmc(res):
+    try:
+        d = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None
+    return d if d.get("h3_res") == res else None
 
 
 def gen_batch(n, steps, seed, dev):
@@ -140,9 +154,25 @@ def main():
     K = args.steps
     avg_ms = {k: v / K for k, v in kt.items()}
     n_tiles = int(last.n_tiles) if last is not None else 0
-    units = {"snap": n, "local_agg": n, "dedup": n, "partition": n_tiles, "merge": n_tiles, "emit": n_tiles}
+    n_parts = int(last.n_partials) if last is not None else 0
+    units = {"ingest": n, "dedup": n, "partition": n_parts, "merge": n_parts, "emit": n_tiles}
+    launch_bytes = {k: BYTES[k] * units[k] for k in BYTES}
+    launch_bytes["ingest"] += 56 * n_parts
     dom = max(BYTES, key=lambda k: avg_ms[k])
-    achieved = BYTES[dom] * units[dom] / (avg_ms[dom] * 1e-3) / 1e9 if avg_ms[dom] > 0 else 0.0
+    gbs = launch_bytes[dom] / (avg_ms[dom] * 1e-3) / 1e9 if avg_ms[dom] > 0 else 0.0
+    pmc = ingest_pmc(args.res) if dom == "ingest" else None
+    if pmc is not None:
+        flops = pmc["fp64_flops_per_event"] * n
+        tf = flops / (avg_ms[dom] * 1e-3) / 1e12
+        roof = {"bound": "valu-fp64", "kernel": "k_ingest", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": tf / FP64_PEAK_TFLOPS, "traffic": pmc["hbm_bytes_per_event"] * n,
+                "fp64_flops_per_event": pmc["fp64_flops_per_event"], "pmc": os.path.relpath(PMC_FILE, ROOT),
+                "hbm_achieved_gbs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS}
+    else:
+        roof = {"bound": "hbm", "kernel": dom, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": gbs / HBM_PEAK_GBS, "traffic": None}
+    roof.update({"kernel_ms": {k: round(v, 3) for k, v in avg_ms.items()}, "algorithmic_bytes_per_launch": launch_bytes[dom],
+                 "units_per_launch": units[dom]})
     value = world * n * K / elapsed
     out = {
         "metric": METRIC, "value": value, "unit": "events/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
@@ -151,11 +181,8 @@ def main():
         "config": {"workload": f"C2-shaped global batch: {n:,} events/step/GPU uniform on the sphere, 50k vehicles, "
                                f"15 min of event time (3 windows) per step, advancing 15 min per step; H3 res {args.res}",
                    "events_per_step_per_gpu": n, "h3_res": args.res, "parallelism": f"dp{world}",
-                   "tiles_emitted_last_step": n_tiles},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel_ms": {k: round(v, 3) for k, v in avg_ms.items()},
-                     "algorithmic_bytes_per_unit": BYTES[dom], "units_per_launch": units[dom]},
+                   "tiles_emitted_last_step": n_tiles, "partials_last_step": n_parts},
+        "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.res)

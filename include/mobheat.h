@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 1
+#define HM_ABI_VERSION 2
 
 /* error codes */
 #define HM_OK 0
@@ -100,6 +100,7 @@ typedef struct hm_batch_out {
     int64_t batch_max_event_ms;   /* max(eventTs/1000) over valid rows, INT64_MIN if none */
     int64_t watermark_ms;         /* watermark used for eviction in this batch */
     int64_t late_watermark_ms;    /* watermark used to drop late rows in this batch */
+    int64_t n_partials;           /* partial records merged (after the in-batch LDS pre-aggregation) */
 } hm_batch_out;
 
 typedef struct hm_ctx hm_ctx;
@@ -164,8 +165,12 @@ int hm_selftest_latlng_to_cell_host(const double *lat, const double *lon, int64_
                                     uint64_t *out);
 
 /* Timing of the last hm_process_batch / stage call on the library's stream (HIP events), milliseconds
- * per kernel: index 0 snap, 1 local aggregate, 2 merge, 3 emit, 4 dedup, 5 total, 6 region partition. */
+ * per phase: index 0 ingest (k_ingest: filter + cells + windows + pre-aggregation + dedup max), 1 reserved
+ * (0), 2 merge, 3 emit, 4 dedup (flag + compaction), 5 total, 6 region partition. */
 int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n);
+
+/* HM_ABI_VERSION the library was built with (callers check it before hm_create). */
+int32_t hm_abi_version(void);
 
 #ifdef __cplusplus
 }

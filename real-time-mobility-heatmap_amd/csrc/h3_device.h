@@ -234,7 +234,9 @@ HM_HD void ijkNormalize(IJK &c) {
 
 // lround(n * M_ONESEVENTH): n/7 is never within 1/14 of a half-integer, so round-half-away-from-zero of
 // the exact quotient, in integers.
-HM_HD int round_div7(int n) { return n >= 0 ? (n + 3) / 7 : -((-n + 3) / 7); }
+// Equivalently floor((n + 3) / 7), done as one unsigned division by the constant (|n| < 2^28 here: the
+// coordinates of a res-15 point on its face stay below 2^24).
+HM_HD int round_div7(int n) { return (int)((unsigned)(n + 3 + 7 * (1 << 27)) / 7u) - (1 << 27); }
 
 // _hex2dToCoordIJK (coordijk.c)
 HM_HD IJK hex2dToCoordIJK(double vx, double vy) {
@@ -286,38 +288,37 @@ HM_HD IJK hex2dToCoordIJK(double vx, double vy) {
 }
 
 // digit rotation tables (Direction enum: 0 center, 1 K, 2 J, 3 JK, 4 I, 5 IK, 6 IJ)
-HM_HD int rot60ccw(int d) { return (int)((UINT64_C(0x72461350) >> (4 * d)) & 0xf); }  // {0,5,3,1,6,4,2,7}
-HM_HD int rot60cw(int d) { return (int)((UINT64_C(0x74152630) >> (4 * d)) & 0xf); }   // {0,3,6,2,5,1,4,7}
-
 HM_HD int getDigit(uint64_t h, int r) { return (int)((h >> ((15 - r) * 3)) & 7); }
 HM_HD void setDigit(uint64_t &h, int r, int d) {
     int s = (15 - r) * 3;
     h = (h & ~(UINT64_C(7) << s)) | ((uint64_t)d << s);
 }
+
+// Digit rotations, bit-parallel over all 15 digits. A digit is a unit IJK vector (i, j, k bits); 60 deg ccw
+// maps 1->5->4->6->2->3->1 (0 and 7 fixed): i' = ~j&(i|k) | ijk, j' = ~k&(i|j) | ijk, k' = ~i&(j|k) | ijk,
+// and cw assigns the same three terms to the planes shifted by one.  Digits past the resolution are 7, which
+// is fixed, so rotating all 15 equals upstream's loop over digits 1..res (_h3Rotate60ccw/_h3Rotate60cw).
+constexpr uint64_t HM_DIG_LO = UINT64_C(0x49249249249);          // bit 0 of each digit
+constexpr uint64_t HM_DIG_MASK = (UINT64_C(1) << 45) - 1;
+HM_HD uint64_t rotate60(uint64_t h, bool cw) {
+    const uint64_t k = h & HM_DIG_LO, j = (h >> 1) & HM_DIG_LO, i = (h >> 2) & HM_DIG_LO;
+    const uint64_t all = i & j & k;
+    const uint64_t a = (~j & (i | k)) | all, b = (~k & (i | j)) | all, c = (~i & (j | k)) | all;
+    const uint64_t ni = cw ? b : a, nj = cw ? c : b, nk = cw ? a : c;
+    return (h & ~HM_DIG_MASK) | (ni << 2) | (nj << 1) | nk;
+}
+// first non-zero digit among 1..res, 0 if none (_h3LeadingNonZeroDigit)
 HM_HD int leadingNonZeroDigit(uint64_t h, int res) {
-    for (int r = 1; r <= res; r++) {
-        int d = getDigit(h, r);
-        if (d) return d;
-    }
-    return 0;
+    uint64_t nz = (h | (h >> 1) | (h >> 2)) & HM_DIG_LO;
+    nz &= ~((UINT64_C(1) << (3 * (15 - res))) - 1);   // digit r's low bit is bit 3 * (15 - r)
+    if (!nz) return 0;
+    return (int)((h >> (63 - __builtin_clzll(nz))) & 7);
 }
-HM_HD uint64_t rotate60ccw(uint64_t h, int res) {
-    for (int r = 1; r <= res; r++) setDigit(h, r, rot60ccw(getDigit(h, r)));
-    return h;
-}
-HM_HD uint64_t rotate60cw(uint64_t h, int res) {
-    for (int r = 1; r <= res; r++) setDigit(h, r, rot60cw(getDigit(h, r)));
-    return h;
-}
+// _h3RotatePent60ccw: rotate; when the new leading digit is K (the deleted K-axes subsequence of a pentagon),
+// rotate once more (upstream does it as soon as the loop meets the first non-zero digit, which is the same)
 HM_HD uint64_t rotatePent60ccw(uint64_t h, int res) {
-    bool found = false;
-    for (int r = 1; r <= res; r++) {
-        setDigit(h, r, rot60ccw(getDigit(h, r)));
-        if (!found && getDigit(h, r) != 0) {
-            found = true;
-            if (leadingNonZeroDigit(h, res) == 1) h = rotate60ccw(h, res);
-        }
-    }
+    h = rotate60(h, false);
+    if (leadingNonZeroDigit(h, res) == 1) h = rotate60(h, false);
     return h;
 }
 
@@ -328,6 +329,7 @@ struct H3Tables {
     double faceAxesAz0[20];
     double faceCosLat[20];   // cos(faceCenterGeo[f].lat), host libm
     double faceSinLat[20];   // sin(faceCenterGeo[f].lat), host libm
+    float faceCenterPointF[20][3];   // (float)faceCenterPoint: the closest-face prefilter
     int faceIjkBaseCells[20][3][3][3][2];
     int baseCellData[122][7];
 };
@@ -339,47 +341,72 @@ HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const H3Tables &T) {
         if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
         return h | ((uint64_t)T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][0] << 45);
     }
+    // Digits from the finest resolution up, in axial coordinates (x, y) = (i - k, j - k): _upAp7/_upAp7r read
+    // only these, _downAp7/_downAp7r are linear and keep the (1,1,1) direction, so the parent and the centre
+    // child need no normalisation; the digit is the normalised unit IJK of (last - centre), a lookup on
+    // (dx, dy) in {-1,0,1}^2 (7 when it is not a unit vector; cf. _unitIjkToDigit).
+    int x = ijk.i - ijk.k, y = ijk.j - ijk.k;
+    uint64_t digits = 0;
     for (int r = res - 1; r >= 0; r--) {
-        IJK last = ijk, center;
-        int i = ijk.i - ijk.k, j = ijk.j - ijk.k;
-        if ((r + 1) & 1) {  // Class III: _upAp7 then _downAp7
-            ijk.i = round_div7(3 * i - j);
-            ijk.j = round_div7(i + 2 * j);
-            ijk.k = 0;
-            ijkNormalize(ijk);
-            center.i = 3 * ijk.i + 1 * ijk.j + 0 * ijk.k;
-            center.j = 0 * ijk.i + 3 * ijk.j + 1 * ijk.k;
-            center.k = 1 * ijk.i + 0 * ijk.j + 3 * ijk.k;
-        } else {            // Class II: _upAp7r then _downAp7r
-            ijk.i = round_div7(2 * i + j);
-            ijk.j = round_div7(3 * j - i);
-            ijk.k = 0;
-            ijkNormalize(ijk);
-            center.i = 3 * ijk.i + 0 * ijk.j + 1 * ijk.k;
-            center.j = 1 * ijk.i + 3 * ijk.j + 0 * ijk.k;
-            center.k = 0 * ijk.i + 1 * ijk.j + 3 * ijk.k;
+        int px, py, cx, cy;
+        if ((r + 1) & 1) {  // Class III: _upAp7, centre child by _downAp7 (i -> (3,0,1), j -> (1,3,0))
+            px = round_div7(3 * x - y);
+            py = round_div7(x + 2 * y);
+            cx = 2 * px + py;
+            cy = 3 * py - px;
+        } else {            // Class II: _upAp7r, centre child by _downAp7r (i -> (3,1,0), j -> (0,3,1))
+            px = round_div7(2 * x + y);
+            py = round_div7(3 * y - x);
+            cx = 3 * px - py;
+            cy = px + 2 * py;
         }
-        ijkNormalize(center);
-        IJK diff = {last.i - center.i, last.j - center.j, last.k - center.k};
-        ijkNormalize(diff);
-        int digit = 7;
-        if (diff.i <= 1 && diff.j <= 1 && diff.k <= 1) digit = diff.i * 4 + diff.j * 2 + diff.k;
-        setDigit(h, r + 1, digit);
+        const int dx = x - cx, dy = y - cy;
+        uint64_t digit = 7;
+        if ((unsigned)(dx + 1) <= 2u && (unsigned)(dy + 1) <= 2u)
+            digit = (0x69d0bd9u >> (3 * ((dx + 1) * 3 + (dy + 1)))) & 7u;
+        digits |= digit << ((14 - r) * 3);   // resolution r + 1
+        x = px;
+        y = py;
     }
+    h = (h & ~(HM_DIG_MASK & ~((UINT64_C(1) << (3 * (15 - res))) - 1))) | digits;
+    ijk.i = x;
+    ijk.j = y;
+    ijk.k = 0;
+    ijkNormalize(ijk);
     if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
     int baseCell = T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][0];
     int numRots = T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][1];
     h |= (uint64_t)baseCell << 45;
     if (T.baseCellData[baseCell][4]) {
-        if (leadingNonZeroDigit(h, res) == 1) {
-            if (T.baseCellData[baseCell][5] == face || T.baseCellData[baseCell][6] == face) h = rotate60cw(h, res);
-            else h = rotate60ccw(h, res);
-        }
+        if (leadingNonZeroDigit(h, res) == 1)
+            h = rotate60(h, T.baseCellData[baseCell][5] == face || T.baseCellData[baseCell][6] == face);
         for (int i = 0; i < numRots; i++) h = rotatePent60ccw(h, res);
     } else {
-        for (int i = 0; i < numRots; i++) h = rotate60ccw(h, res);
+        // numRots ccw rotations of a hexagon's digits: the same as 6 - numRots cw ones; take the shorter way
+        const bool cw = numRots > 3;
+        const int k = cw ? 6 - numRots : numRots;
+        for (int i = 0; i < k; i++) h = rotate60(h, cw);
     }
     return h;
+}
+
+// squared distance from face f's centre, upstream's operation order (_geoToClosestFace)
+HM_HD double faceSqDist(const H3Tables &T, int f, double vx, double vy, double vz) {
+    double dx = T.faceCenterPoint[f][0] - vx;
+    double dy = T.faceCenterPoint[f][1] - vy;
+    double dz = T.faceCenterPoint[f][2] - vz;
+    double s = dx * dx + dy * dy;
+    return s + dz * dz;
+}
+// upstream's loop: first face with the smallest squared distance
+// (out of line: the near-tie path is rare, and inlined its 60 constants would occupy registers)
+__host__ __device__ __attribute__((noinline)) inline void closestFaceExact(const H3Tables &T, double vx, double vy, double vz, int &face, double &sqd) {
+    face = 0;
+    sqd = 5.0;
+    for (int f = 0; f < 20; ++f) {
+        double s = faceSqDist(T, f, vx, vy, vz);
+        if (s < sqd) { face = f; sqd = s; }
+    }
 }
 
 // latLngToCell with h3-py's deg2coord: degrees in; returns 0 where the reference UDF returns None
@@ -396,16 +423,27 @@ HM_HD uint64_t latLngToCellDeg(double lat_deg, double lng_deg, int res, const H3
     double vz = slat;
     double vx = clng * clat;
     double vy = slng * clat;
-    // _geoToClosestFace
-    int face = 0;
-    double sqd = 5.0;
-    for (int f = 0; f < 20; ++f) {
-        double dx = T.faceCenterPoint[f][0] - vx;
-        double dy = T.faceCenterPoint[f][1] - vy;
-        double dz = T.faceCenterPoint[f][2] - vz;
-        double s = dx * dx + dy * dy;
-        s = s + dz * dz;
-        if (s < sqd) { face = f; sqd = s; }
+    // _geoToClosestFace.  Prefilter in fp32: sqd = 2 - 2 (c . v) for unit vectors, and the fp32 dot products
+    // are within ~1e-6 of the exact ones, so when the best face leads the runner-up by more than 1e-5 it is
+    // upstream's fp64 argmin (no tie possible) and only its fp64 distance is computed; otherwise the full
+    // upstream loop runs.
+    int face;
+    double sqd;
+    {
+        const float fx = (float)vx, fy = (float)vy, fz = (float)vz;
+        float best = -4.0f, second = -4.0f;
+        int bf = 0;
+        for (int f = 0; f < 20; ++f) {
+            const float d = T.faceCenterPointF[f][0] * fx + T.faceCenterPointF[f][1] * fy + T.faceCenterPointF[f][2] * fz;
+            if (d > best) { second = best; best = d; bf = f; }
+            else if (d > second) second = d;
+        }
+        if (best - second > 1e-5f) {
+            face = bf;
+            sqd = faceSqDist(T, bf, vx, vy, vz);
+        } else {
+            closestFaceExact(T, vx, vy, vz, face, sqd);
+        }
     }
     // _geoToHex2d
     double r = acos(1 - sqd / 2);

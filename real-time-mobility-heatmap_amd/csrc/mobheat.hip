@@ -1,16 +1,19 @@
 // mobheat: MI355X-native per-micro-batch hot path of the reference's streaming job.
 //
 // Pipeline per batch (one HIP stream per context; every arithmetic step runs on the GPU):
-//   k_snap        filter (heatmap_stream.py:96-104) + H3 latLngToCell UDF (:65-75,105) + tumbling window
-//                 (:115) + late-row test against the watermark (:107); batch max event time (ms)
-//   k_local_agg   LDS hash pre-aggregation of (cell, windowStart) -> count, n_speed, sum speed/lat/lon
-//                 into 56-B partial records (Spark's partial HashAggregate, :112-123)
+//   k_ingest      one pass over the events: filter (heatmap_stream.py:96-104) + H3 latLngToCell UDF
+//                 (:65-75,105) + tumbling window (:115) + late-row test against the watermark (:107) + batch
+//                 max event time; per-vkey max ts for the dedup (:200-203); LDS hash pre-aggregation of
+//                 (cell, windowStart) -> count, n_speed, sum speed/lat/lon into 56-B partial records
+//                 (Spark's partial HashAggregate, :112-123)
 //   [multi-GPU: partials partitioned by owner rank, exchanged by the caller with RCCL all-to-all]
-//   k_merge       owner-side merge of partials into the persistent device state table (update mode,
-//                 :243; Spark's StateStoreRestore/Save), marking touched keys
-//   k_emit        touched keys -> output rows with cumulative count/avg (:124-132)
-//   k_rehash      state eviction by the watermark (window end <= watermark) and table growth
-//   k_dedup_*     latest position per (provider, vehicleId): max(eventTs) + rows equal to it (:200-207)
+//   k_rp_*        radix partition of the partials by state-table region
+//   k_merge_owned one workgroup per region merges its partials into the persistent device state table
+//                 (update mode, :243; Spark's StateStoreRestore/Save), marking touched keys
+//                 (k_merge: the device-atomic variant for small tables / batches)
+//   k_emit_bins   touched keys -> output rows with cumulative count/avg (:124-132)
+//   k_rehash      compaction: drops keys evicted by the watermark (window end <= watermark), grows the table
+//   k_dedup_flag  latest position per (provider, vehicleId): rows whose ts equals the max (:204-207)
 //
 // Semantics follow SURVEY.md App. A (Spark 3.5.1): see DESIGN.md for the rules and their provenance.
 #include <hip/hip_runtime.h>
@@ -38,7 +41,10 @@ static H3Tables make_tables() {
     for (int f = 0; f < 20; f++) {
         T.faceCenterGeo[f][0] = H3T_faceCenterGeo[f][0];
         T.faceCenterGeo[f][1] = H3T_faceCenterGeo[f][1];
-        for (int c = 0; c < 3; c++) T.faceCenterPoint[f][c] = H3T_faceCenterPoint[f][c];
+        for (int c = 0; c < 3; c++) {
+            T.faceCenterPoint[f][c] = H3T_faceCenterPoint[f][c];
+            T.faceCenterPointF[f][c] = (float)H3T_faceCenterPoint[f][c];
+        }
         T.faceAxesAz0[f] = H3T_faceAxesAzRadsCII[f][0];
         // upstream evaluates cos/sin(p1->lat) per call with the host libm; identical values
         volatile double lat = H3T_faceCenterGeo[f][0];
@@ -84,7 +90,7 @@ __device__ __forceinline__ unsigned long long wave_append(bool pred, unsigned lo
 // =====================================================================================================
 // K1: filter + latLngToCell + window + late test
 // =====================================================================================================
-// waves per SIMD for k_snap: 3 caps it at 168 VGPRs without spills (measured best of 2..5 on MI355X)
+// waves per SIMD for k_ingest: 3 caps it at 168 VGPRs without spills (measured best of 2..5 on MI355X)
 #ifndef HM_SNAP_WAVES
 #define HM_SNAP_WAVES 3
 #endif
@@ -93,48 +99,6 @@ __device__ __forceinline__ unsigned long long wave_append(bool pred, unsigned lo
 #else
 #define HM_SNAP_ATTR
 #endif
-__global__ __launch_bounds__(256) HM_SNAP_ATTR void k_snap(const double *__restrict__ lat, const double *__restrict__ lon,
-                                              const int64_t *__restrict__ ts, const uint8_t *__restrict__ row_valid,
-                                              int64_t n, int res, int64_t tile_us, int64_t late_end_us,
-                                              uint64_t *__restrict__ cell_out, int64_t *__restrict__ wstart_out,
-                                              uint8_t *__restrict__ flags_out, DevStats *st) {
-    unsigned long long nvalid = 0, nlate = 0;
-    long long mx = INT64_MIN;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        double la = lat[i], lo = lon[i];
-        int64_t t = ts[i];
-        bool ok = (row_valid ? row_valid[i] != 0 : true) && la >= -90.0 && la <= 90.0 && lo >= -180.0 && lo <= 180.0 &&
-                  t > INT64_MIN + 2 * tile_us && t < INT64_MAX - 2 * tile_us;
-        uint8_t fl = 0;
-        uint64_t cell = EMPTY_CELL;
-        int64_t ws = EMPTY_WIN;
-        if (ok) {
-            int64_t rem = t % tile_us;
-            if (rem < 0) rem += tile_us;
-            ws = t - rem;
-            bool late = (ws + tile_us) <= late_end_us;
-            fl = late ? (F_VALID | F_LATE) : (F_VALID | F_AGG);
-            nvalid++;
-            nlate += late;
-            long long ms = (long long)(t / 1000);
-            mx = ms > mx ? ms : mx;
-            if (!late) cell = latLngToCellDeg(la, lo, res, c_tab);
-        }
-        cell_out[i] = cell;
-        wstart_out[i] = ws;
-        flags_out[i] = fl;
-    }
-    nvalid = wave_sum(nvalid);
-    nlate = wave_sum(nlate);
-    mx = wave_max(mx);
-    if (lane_id() == 0) {
-        if (nvalid) atomicAdd(&st->n_valid, nvalid);
-        if (nlate) atomicAdd(&st->n_late, nlate);
-        if (mx != INT64_MIN) atomicMax(&st->max_ts_ms, mx);
-    }
-}
-
 // standalone UDF: cells only (hm_latlng_to_cell)
 __global__ __launch_bounds__(256) void k_cells(const double *__restrict__ lat, const double *__restrict__ lon, int64_t n,
                                                int res, uint64_t *__restrict__ out) {
@@ -208,55 +172,6 @@ __device__ void la_flush(LaShared &S, TilePartial *out, DevStats *st) {
     }
     if (t == 0) S.occ = 0;
     __syncthreads();
-}
-
-__global__ __launch_bounds__(LA_THREADS) void k_local_agg(const uint64_t *__restrict__ cell, const int64_t *__restrict__ wstart,
-                                                          const uint8_t *__restrict__ flags, const double *__restrict__ speed,
-                                                          const uint8_t *__restrict__ speed_valid, const double *__restrict__ lat,
-                                                          const double *__restrict__ lon, int64_t n, TilePartial *__restrict__ out,
-                                                          DevStats *st) {
-    __shared__ LaShared S;
-    for (int s = threadIdx.x; s < LA_SLOTS; s += LA_THREADS) {
-        S.cell[s] = EMPTY_CELL;
-        S.w[s] = EMPTY_WIN;
-        S.cnt[s] = 0;
-        S.ssp[s] = 0.0;
-        S.slat[s] = 0.0;
-        S.slon[s] = 0.0;
-    }
-    if (threadIdx.x == 0) S.occ = 0;
-    __syncthreads();
-    const int64_t nchunks = (n + LA_CHUNK - 1) / LA_CHUNK;
-    for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-        for (int q = 0; q < LA_CHUNK / LA_THREADS; q++) {
-            int64_t i = ch * LA_CHUNK + q * LA_THREADS + threadIdx.x;
-            if (i < n && (flags[i] & F_AGG)) {
-                uint64_t c = cell[i];
-                long long w = wstart[i];
-                bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
-                double sp = sv ? speed[i] : 0.0;
-                double la = lat[i], lo = lon[i];
-                unsigned h = (unsigned)(tile_hash(c, w) & (LA_SLOTS - 1));
-                for (int probe = 0; probe < LA_SLOTS; probe++) {
-                    unsigned long long old = atomicCAS(&S.cell[h], (unsigned long long)EMPTY_CELL, (unsigned long long)c);
-                    if (old == EMPTY_CELL) atomicAdd(&S.occ, 1u);
-                    if (old == EMPTY_CELL || old == c) {
-                        long long ow = (long long)atomicCAS((unsigned long long *)&S.w[h], (unsigned long long)EMPTY_WIN,
-                                                            (unsigned long long)w);
-                        if (ow == EMPTY_WIN || ow == w) break;
-                    }
-                    h = (h + 1) & (LA_SLOTS - 1);
-                }
-                atomicAdd(&S.cnt[h], 1ull | ((unsigned long long)sv << 32));
-                if (sv) atomicAdd(&S.ssp[h], sp);
-                atomicAdd(&S.slat[h], la);
-                atomicAdd(&S.slon[h], lo);
-            }
-        }
-        __syncthreads();
-        if (S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, out, st);
-    }
-    if (S.occ > 0) la_flush(S, out, st);
 }
 
 // =====================================================================================================
@@ -747,10 +662,10 @@ __global__ __launch_bounds__(256) void k_rehash(const TileSlot *__restrict__ old
 // K5: latest position per (provider, vehicleId)
 // =====================================================================================================
 __device__ __forceinline__ long long find_or_claim_vkey(DedupSlot *tab, unsigned long long mask, unsigned long long v,
-                                                        bool &claimed) {
+                                                        bool &claimed, unsigned long long max_probe) {
     unsigned long long h = vkey_hash(v) & mask;
     claimed = false;
-    for (unsigned long long probe = 0; probe <= mask; probe++) {
+    for (unsigned long long probe = 0; probe < max_probe; probe++) {
         unsigned long long cur = __hip_atomic_load(&tab[h].vkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (cur == EMPTY_VKEY) {
             cur = atomicCAS(&tab[h].vkey, EMPTY_VKEY, v);
@@ -808,7 +723,7 @@ __global__ __launch_bounds__(256) void k_dedup_max(const uint64_t *__restrict__ 
             else { take = (flags[i] & F_VALID) != 0; v = take ? vkey[i] : 0; t = take ? ts[i] : 0; }
             if (take && v == EMPTY_VKEY) { bad++; take = false; }
             if (take) {
-                h = find_or_claim_vkey(tab, mask, v, claimed);
+                h = find_or_claim_vkey(tab, mask, v, claimed, mask + 1);
                 if (h < 0) {
                     overflow = true;
                 } else {
@@ -847,6 +762,124 @@ __global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__
             w = (h >= 0 && tab[h].maxts == t) ? 1 : 0;
         }
         win[i] = w;
+    }
+}
+
+// =====================================================================================================
+// K1: ingest. One pass over the events: the filter (heatmap_stream.py:96-104), latLngToCell (the UDF,
+// :65-75), the tumbling window and late test (:107,115), the per-vkey max ts of the dedup (:200-203), and
+// LDS pre-aggregation of (cell, windowStart) into partial records (:112-123). The fp64 cell computation
+// dominates; the aggregation's LDS atomics and the dedup's table atomics overlap with it.
+// =====================================================================================================
+constexpr unsigned long long DEDUP_FUSED_PROBES = 256;
+
+__global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
+    const double *__restrict__ lat, const double *__restrict__ lon, const int64_t *__restrict__ ts,
+    const uint8_t *__restrict__ row_valid, const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
+    const uint64_t *__restrict__ vkey, int64_t n, int res, int64_t tile_us, int64_t late_end_us,
+    uint8_t *__restrict__ flags_out, TilePartial *__restrict__ out, DedupSlot *dtab, unsigned long long dmask,
+    unsigned int *dused, unsigned long long *n_dused, DevStats *st) {
+    __shared__ LaShared S;
+    for (int s = threadIdx.x; s < LA_SLOTS; s += LA_THREADS) {
+        S.cell[s] = EMPTY_CELL;
+        S.w[s] = EMPTY_WIN;
+        S.cnt[s] = 0;
+        S.ssp[s] = 0.0;
+        S.slat[s] = 0.0;
+        S.slon[s] = 0.0;
+    }
+    if (threadIdx.x == 0) S.occ = 0;
+    __syncthreads();
+    unsigned long long nvalid = 0, nlate = 0, bad = 0;
+    long long mx = INT64_MIN;
+    bool dretry = false;
+    const int64_t nchunks = (n + LA_CHUNK - 1) / LA_CHUNK;
+    for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+        for (int q = 0; q < LA_CHUNK / LA_THREADS; q++) {
+            const int64_t i = ch * LA_CHUNK + q * LA_THREADS + threadIdx.x;
+            const bool in = i < n;
+            double la = 0.0, lo = 0.0;
+            int64_t t = 0;
+            bool rv = true;
+            if (in) {
+                la = lat[i];
+                lo = lon[i];
+                t = ts[i];
+                if (row_valid) rv = row_valid[i] != 0;
+            }
+            const bool ok = in && rv && la >= -90.0 && la <= 90.0 && lo >= -180.0 && lo <= 180.0 &&
+                            t > INT64_MIN + 2 * tile_us && t < INT64_MAX - 2 * tile_us;
+            uint8_t fl = 0;
+            uint64_t cell = EMPTY_CELL;
+            int64_t ws = EMPTY_WIN;
+            if (ok) {
+                int64_t rem = t % tile_us;
+                if (rem < 0) rem += tile_us;
+                ws = t - rem;
+                const bool late = (ws + tile_us) <= late_end_us;
+                fl = late ? (F_VALID | F_LATE) : (F_VALID | F_AGG);
+                nvalid++;
+                nlate += late;
+                const long long ms = (long long)(t / 1000);
+                mx = ms > mx ? ms : mx;
+                if (!late) cell = latLngToCellDeg(la, lo, res, c_tab);
+            }
+            if (in) flags_out[i] = fl;
+            // dedup: per-vkey max ts over the valid rows (late rows included, as in the reference's batch frame)
+            bool claimed = false;
+            long long dh = -1;
+            if (ok) {
+                const unsigned long long v = vkey[i];
+                if (v == EMPTY_VKEY) {
+                    bad++;
+                } else {
+                    dh = find_or_claim_vkey(dtab, dmask, v, claimed, DEDUP_FUSED_PROBES);
+                    if (dh < 0) {
+                        dretry = true;
+                    } else {
+                        const long long cur = __hip_atomic_load(&dtab[dh].maxts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (t > cur) atomicMax(&dtab[dh].maxts, (long long)t);
+                    }
+                }
+            }
+            const unsigned long long pos = wave_append(claimed, n_dused);
+            if (claimed) dused[pos] = (unsigned int)dh;
+            // LDS pre-aggregation of the window's rows
+            if (fl & F_AGG) {
+                const bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
+                const double sp = sv ? speed[i] : 0.0;
+                unsigned h = (unsigned)(tile_hash(cell, ws) & (LA_SLOTS - 1));
+                for (int probe = 0; probe < LA_SLOTS; probe++) {
+                    unsigned long long old = atomicCAS(&S.cell[h], (unsigned long long)EMPTY_CELL, (unsigned long long)cell);
+                    if (old == EMPTY_CELL) atomicAdd(&S.occ, 1u);
+                    if (old == EMPTY_CELL || old == cell) {
+                        long long ow = (long long)atomicCAS((unsigned long long *)&S.w[h], (unsigned long long)EMPTY_WIN,
+                                                            (unsigned long long)ws);
+                        if (ow == EMPTY_WIN || ow == ws) break;
+                    }
+                    h = (h + 1) & (LA_SLOTS - 1);
+                }
+                atomicAdd(&S.cnt[h], 1ull | ((unsigned long long)sv << 32));
+                if (sv) atomicAdd(&S.ssp[h], sp);
+                atomicAdd(&S.slat[h], la);
+                atomicAdd(&S.slon[h], lo);
+            }
+        }
+        __syncthreads();
+        if (S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, out, st);
+    }
+    if (S.occ > 0) la_flush(S, out, st);
+    nvalid = wave_sum(nvalid);
+    nlate = wave_sum(nlate);
+    bad = wave_sum(bad);
+    mx = wave_max(mx);
+    const unsigned long long rt = __ballot(dretry);
+    if (lane_id() == 0) {
+        if (nvalid) atomicAdd(&st->n_valid, nvalid);
+        if (nlate) atomicAdd(&st->n_late, nlate);
+        if (mx != INT64_MIN) atomicMax(&st->max_ts_ms, mx);
+        if (bad) atomicAdd(&st->bad_vkey, bad);
+        if (rt) atomicAdd(&st->dedup_retry, 1ull);
     }
 }
 
@@ -1038,6 +1071,9 @@ struct hm_ctx {
     unsigned long long dcap = 0;
     DevBuf dused;
     bool dedup_dirty = false;
+    int64_t dedup_seen = 0;
+    int64_t n_partials_merged = 0;   // partial records of the last merge (hm_batch_out.n_partials)
+    int ingest_grid = 0;             // k_ingest's persistent grid: resident workgroups per CU x CUs     // distinct vkeys of the last batch (sizes k_ingest's fused dedup table)
     // outputs (device + pinned host)
     DevBuf o_cell, o_ws, o_cnt, o_sp, o_spn, o_lon, o_lat;
     void *h_cell = nullptr, *h_ws = nullptr, *h_cnt = nullptr, *h_sp = nullptr, *h_spn = nullptr, *h_lon = nullptr,
@@ -1194,7 +1230,8 @@ static int state_account(hm_ctx *ctx, int64_t evict_wm_ms) {
     return HM_OK;
 }
 
-static int dedup_prepare(hm_ctx *ctx, int64_t n_upper) {
+// Clear the dedup table through the last batch's used list and make sure it holds `n_keys` keys at <= 1/2 load.
+static int dedup_prepare(hm_ctx *ctx, int64_t n_keys) {
     if (ctx->dedup_dirty) {
         hipLaunchKernelGGL(k_clear_dedup, dim3(grid_for(ctx->dcap, 256)), dim3(256), 0, ctx->stream, ctx->dtab,
                            (const unsigned int *)ctx->dused.p, ctx->d_scratch + DUSED_WORD);
@@ -1202,8 +1239,9 @@ static int dedup_prepare(hm_ctx *ctx, int64_t n_upper) {
         HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + DUSED_WORD, 0, 8, ctx->stream));
         ctx->dedup_dirty = false;
     }
-    unsigned long long want = next_pow2((unsigned long long)std::max<int64_t>(2 * n_upper, 1024));
-    if (ctx->dtab && ctx->dcap >= want) return HM_OK;
+    unsigned long long want = next_pow2((unsigned long long)std::max<int64_t>(2 * n_keys, 1024));
+    // keep the table when it fits and is not far larger than needed (a cache-resident table is the point)
+    if (ctx->dtab && ctx->dcap >= want && ctx->dcap <= 8 * want) return HM_OK;
     if (ctx->dtab) {
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         HIPCHK(ctx, hipFree(ctx->dtab));
@@ -1217,6 +1255,11 @@ static int dedup_prepare(hm_ctx *ctx, int64_t n_upper) {
     hipLaunchKernelGGL(k_init_dedup, dim3(grid_for(want, 256)), dim3(256), 0, ctx->stream, ctx->dtab, want);
     HIPCHK(ctx, hipGetLastError());
     return ensure(ctx, ctx->dused, want * sizeof(unsigned int));
+}
+// k_ingest's table: sized from the last batch's distinct vkeys (small and cache-resident), not from n; a batch
+// with many more keys makes the fused probes give up and phase_dedup reruns the max pass on a full-size table.
+static int64_t dedup_fused_keys(const hm_ctx *ctx, int64_t n) {
+    return std::min<int64_t>(n, std::max<int64_t>(int64_t(1) << 15, ctx->dedup_seen + ctx->dedup_seen / 4));
 }
 
 // ordered compaction of byte flags -> int64 indices into ctx->rows; count into d_scratch[255]
@@ -1279,44 +1322,46 @@ struct Inputs {
 static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
     int64_t n = I.n;
     int rc;
-    if ((rc = ensure(ctx, ctx->cell, n * 8)) || (rc = ensure(ctx, ctx->wstart, n * 8)) || (rc = ensure(ctx, ctx->flags, n)) ||
-        (rc = ensure(ctx, ctx->win, n)) || (rc = ensure(ctx, ctx->rows, n * 8)) ||
+    if ((rc = ensure(ctx, ctx->flags, n)) || (rc = ensure(ctx, ctx->win, n)) || (rc = ensure(ctx, ctx->rows, n * 8)) ||
         (rc = ensure(ctx, ctx->partials, n * sizeof(TilePartial))))
         return rc;
+    if ((rc = dedup_prepare(ctx, dedup_fused_keys(ctx, n)))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_st, 0, sizeof(DevStats), ctx->stream));
     long long init[2] = {INT64_MIN, INT64_MAX};
     HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->max_ts_ms, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
     if (n > 0) {
-        int64_t late_end_us = late_wm_ms * 1000;
-        hipLaunchKernelGGL(k_snap, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, n,
-                           ctx->cfg.h3_res, ctx->cfg.tile_us, late_end_us, (uint64_t *)ctx->cell.p, (int64_t *)ctx->wstart.p,
-                           (uint8_t *)ctx->flags.p, ctx->d_st);
+        int64_t nchunks = (n + LA_CHUNK - 1) / LA_CHUNK;
+        int blocks = (int)std::min<int64_t>(nchunks, ctx->ingest_grid);
+        hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(LA_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.sp, I.sv, I.vk,
+                           n, ctx->cfg.h3_res, ctx->cfg.tile_us, late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
+                           (TilePartial *)ctx->partials.p, ctx->dtab, ctx->dcap - 1, (unsigned int *)ctx->dused.p,
+                           ctx->d_scratch + DUSED_WORD, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
+        ctx->dedup_dirty = true;
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
-    if (n > 0) {
-        int64_t nchunks = (n + LA_CHUNK - 1) / LA_CHUNK;
-        int blocks = (int)std::min<int64_t>(nchunks, 256 * 3);
-        hipLaunchKernelGGL(k_local_agg, dim3(blocks), dim3(LA_THREADS), 0, ctx->stream, (const uint64_t *)ctx->cell.p,
-                           (const int64_t *)ctx->wstart.p, (const uint8_t *)ctx->flags.p, I.sp, I.sv, I.lat, I.lon, n,
-                           (TilePartial *)ctx->partials.p, ctx->d_st);
-        HIPCHK(ctx, hipGetLastError());
-    }
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     return HM_OK;
 }
 
-// dedup over rows (cands == nullptr) or candidates; result: ctx->rows indices, count in d_scratch[255]
-static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t n) {
+// Dedup over the batch's rows (I != nullptr; the per-vkey max came from k_ingest unless its probes gave up:
+// `rerun_max`) or over received candidates; result: ctx->rows indices, count in d_scratch[255].
+static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t n, bool rerun_max) {
     int rc;
-    if ((rc = dedup_prepare(ctx, n))) return rc;
+    const bool need_max = cands != nullptr || rerun_max;
+    if (need_max) {
+        if (I) ctx->dedup_dirty = true;   // rows: k_ingest's partial table is cleared through its used list
+        if ((rc = dedup_prepare(ctx, n))) return rc;
+    }
     if ((rc = ensure(ctx, ctx->win, std::max<int64_t>(n, 1))) || (rc = ensure(ctx, ctx->rows, std::max<int64_t>(n, 1) * 8)))
         return rc;
     if (n > 0) {
-        hipLaunchKernelGGL(k_dedup_max, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, I ? I->vk : nullptr,
-                           I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, ctx->dtab, ctx->dcap - 1,
-                           (unsigned int *)ctx->dused.p, ctx->d_scratch + DUSED_WORD, ctx->d_st);
+        if (need_max) {
+            hipLaunchKernelGGL(k_dedup_max, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, I ? I->vk : nullptr,
+                               I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, ctx->dtab, ctx->dcap - 1,
+                               (unsigned int *)ctx->dused.p, ctx->d_scratch + DUSED_WORD, ctx->d_st);
+        }
         hipLaunchKernelGGL(k_dedup_flag, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, I ? I->vk : nullptr,
                            I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, ctx->dtab, ctx->dcap - 1,
                            (uint8_t *)ctx->win.p);
@@ -1341,6 +1386,7 @@ static int ensure_outputs(hm_ctx *ctx, int64_t n_rows) {
 
 static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts) {
     int rc;
+    ctx->n_partials_merged = n_parts;
     if ((rc = state_reserve(ctx, n_parts))) return rc;
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_touched, 0, 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_state_new, 0, 8, ctx->stream));
@@ -1482,6 +1528,7 @@ static void fill_stats(hm_ctx *ctx, hm_batch_out *out, int64_t n_in, const DevSt
     out->batch_max_event_ms = s.max_ts_ms;
     out->watermark_ms = ctx->wm_cur;
     out->late_watermark_ms = late_wm;
+    out->n_partials = ctx->n_partials_merged;
 }
 
 static void record_timings(hm_ctx *ctx) {
@@ -1498,6 +1545,8 @@ static void record_timings(hm_ctx *ctx) {
 }
 
 extern "C" {
+
+int32_t hm_abi_version(void) { return HM_ABI_VERSION; }
 
 int hm_create(const hm_config *cfg, hm_ctx **out) {
     g_create_err.clear();
@@ -1527,6 +1576,15 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     H3Tables T = make_tables();
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &T, sizeof(T)) != hipSuccess) { ctx->err = "tables"; return fail("create"); }
+    {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_ingest, LA_THREADS, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) {
+            ctx->err = "occupancy query";
+            return fail("create");
+        }
+        ctx->ingest_grid = std::max(1, per_cu) * std::max(1, cus);
+    }
     if (hipMalloc(&ctx->d_st, sizeof(DevStats)) != hipSuccess || hipHostMalloc(&ctx->h_st, sizeof(DevStats)) != hipSuccess ||
         hipMalloc(&ctx->d_scratch, 256 * 8) != hipSuccess || hipHostMalloc(&ctx->h_scratch, 256 * 8) != hipSuccess) {
         ctx->err = "stats alloc";
@@ -1612,11 +1670,13 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     // 3. merge into state + emit
     if ((rc = phase_merge_emit(ctx, (const TilePartial *)ctx->partials.p, (int64_t)s1.n_partials))) return rc;
     // 4. dedup over the batch's valid rows
-    if ((rc = phase_dedup(ctx, &I, nullptr, I.n))) return rc;
+    if ((rc = phase_dedup(ctx, &I, nullptr, I.n, s1.dedup_retry != 0))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch + 255, ctx->d_scratch + 255, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch + DUSED_WORD, ctx->d_scratch + DUSED_WORD, 3 * 8, hipMemcpyDeviceToHost,
+                               ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->dedup_seen = (int64_t)ctx->h_scratch[DUSED_WORD];
     DevStats s2 = *ctx->h_st;
     if (s2.overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     if (s2.bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved (%llu rows)", s2.bad_vkey);
@@ -1683,8 +1743,10 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     I.n = in->n;
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
     if ((rc = phase_local(ctx, I, late_wm))) return rc;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     // local dedup over rows -> local winners -> candidates
-    if ((rc = phase_dedup(ctx, &I, nullptr, I.n))) return rc;
+    if ((rc = phase_dedup(ctx, &I, nullptr, I.n, ctx->h_st->dedup_retry != 0))) return rc;
     if ((rc = ensure(ctx, ctx->cands, std::max<int64_t>(I.n, 1) * sizeof(Cand)))) return rc;
     hipLaunchKernelGGL(k_make_cands, dim3(grid_for(std::max<int64_t>(I.n, 1), 256)), dim3(256), 0, ctx->stream,
                        (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, I.vk, I.ts, rank, (Cand *)ctx->cands.p);
@@ -1702,6 +1764,7 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     if (ctx->h_st->bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved");
+    ctx->dedup_seen = (int64_t)ctx->h_scratch[DUSED_WORD];
     if ((int64_t)ctx->h_st->n_partials > tile_send_cap || (int64_t)ctx->h_scratch[255] > cand_send_cap)
         return set_err(ctx, HM_E_INVALID, "send buffer too small (%llu tiles, %llu candidates)", ctx->h_st->n_partials,
                        ctx->h_scratch[255]);
@@ -1745,7 +1808,7 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, 
     int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
     if ((rc = phase_merge_emit(ctx, (const TilePartial *)tile_recv_dev, n_tile_recv))) return rc;
     // owner-side dedup over received candidates
-    if ((rc = phase_dedup(ctx, nullptr, (const Cand *)cand_recv_dev, n_cand_recv))) return rc;
+    if ((rc = phase_dedup(ctx, nullptr, (const Cand *)cand_recv_dev, n_cand_recv, true))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch, 0, 128 * 8, ctx->stream));
     if (n_cand_recv > 0) {
         hipLaunchKernelGGL(k_winner_route, dim3(grid_for(n_cand_recv, 256)), dim3(256), 0, ctx->stream, (const Cand *)cand_recv_dev,

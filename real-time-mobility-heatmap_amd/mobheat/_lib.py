@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MOBHEAT_LIB: load another build of the same ABI (kernel variants under csrc/variants/ for tuning runs)
 LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
 
-HM_ABI_VERSION = 1
+HM_ABI_VERSION = 2
 HM_MEM_HOST = 0
 HM_MEM_DEVICE = 1
 HM_TILE_REC_BYTES = 56
@@ -45,7 +45,7 @@ class HmBatchOut(ctypes.Structure):
         ("speed_null", c_vp), ("avg_lon", c_vp), ("avg_lat", c_vp),
         ("n_latest", c_i64), ("latest_row", c_vp),
         ("n_in", c_i64), ("n_valid", c_i64), ("n_late", c_i64), ("n_state", c_i64),
-        ("batch_max_event_ms", c_i64), ("watermark_ms", c_i64), ("late_watermark_ms", c_i64),
+        ("batch_max_event_ms", c_i64), ("watermark_ms", c_i64), ("late_watermark_ms", c_i64), ("n_partials", c_i64),
     ]
 
 
@@ -72,6 +72,7 @@ SIGNATURES = {
     "hm_selftest_ld_ops": (c_i32, [c_vp, c_i64, c_i32, c_vp]),
     "hm_selftest_latlng_to_cell_host": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp]),
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
+    "hm_abi_version": (c_i32, []),
 }
 
 _lib = None
@@ -89,6 +90,9 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.hm_abi_version() != HM_ABI_VERSION:
+        raise RuntimeError(f"{LIB_PATH} was built for ABI {lib.hm_abi_version()}, this binding is ABI {HM_ABI_VERSION}: "
+                           "rebuild it (__graft_entry__.build())")
     _lib = lib
     return lib
 

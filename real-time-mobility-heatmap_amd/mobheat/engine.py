@@ -106,8 +106,7 @@ class HeatmapEngine:
     def last_timings(self):
         ms = (ctypes.c_double * 7)()
         check(self._lib.hm_last_timings(self._ctx, ms, 7), self._ctx)
-        return {"snap": ms[0], "local_agg": ms[1], "merge": ms[2], "emit": ms[3], "dedup": ms[4], "total": ms[5],
-                "partition": ms[6]}
+        return {"ingest": ms[0], "merge": ms[2], "emit": ms[3], "dedup": ms[4], "total": ms[5], "partition": ms[6]}
 
     def _result_from_host(self, out):
         def arr(p, n, dt):

@@ -37,3 +37,15 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
         assert "not built" in str(e)
     else:
         raise AssertionError("load() must raise when the HIP library is missing")
+
+
+def test_abi_version_matches_header_and_binding(mobheat_lib):
+    from mobheat import _lib
+    hdr = re.search(r"#define HM_ABI_VERSION (\d+)", open(os.path.join(ROOT, "include", "mobheat.h")).read())
+    assert int(hdr.group(1)) == _lib.HM_ABI_VERSION == mobheat_lib.hm_abi_version()
+    # hm_batch_out: every field is 8 bytes wide (int64 or pointer), so the declared field count fixes its size
+    import ctypes
+    body = re.search(r"typedef struct hm_batch_out \{(.*?)\} hm_batch_out;", open(os.path.join(ROOT, "include", "mobheat.h")).read(),
+                     re.S).group(1)
+    n_fields = len(re.findall(r";", re.sub(r"/\*.*?\*/", "", body, flags=re.S)))
+    assert ctypes.sizeof(_lib.HmBatchOut) == 8 * n_fields

@@ -174,6 +174,23 @@ def test_dedup_ties_c5_sample():
     eng.close()
 
 
+def test_dedup_more_vehicles_than_fused_table():
+    """k_ingest's fused dedup table is sized from the previous batch's distinct vehicles (>= 2^18 keys); a
+    first batch with 1.2M vehicles overflows its bounded probes, so the max pass reruns on a full-size table.
+    The second batch (sized from the first) takes the fused path. Both must equal the oracle."""
+    from mobheat import HeatmapEngine, synth
+    from oracle.spark_oracle import SparkHeatmapOracle
+    eng = HeatmapEngine(h3_res=8)
+    ora = SparkHeatmapOracle(h3_res=8)
+    for epoch in range(2):
+        b = synth.c5_dedup(seed=40 + epoch, n_vehicles=1_200_000, updates=2)
+        b["ts_us"] = b["ts_us"] + epoch * 600_000_000
+        res, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res, exp)
+        assert len(res.latest_rows) >= 1_200_000
+    eng.close()
+
+
 def test_high_cardinality_res12_two_batches():
     from mobheat import HeatmapEngine, synth
     from oracle.spark_oracle import SparkHeatmapOracle
