@@ -32,7 +32,8 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 T0 = 1759572000 * 1_000_000
 SPAN_US = 15 * 60 * 1_000_000
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
-FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector peak: 256 CUs x 64 FMA lanes x 2 x 2.4 GHz
+FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector peak: 1024 SIMDs x 16 FMA lanes x 2 x 2.4 GHz
+SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 # algorithmic HBM bytes per unit: per event (ingest, dedup), per partial record (partition,
 # merge), per emitted tile (emit).  ingest also writes 56 B per partial (added below).
@@ -43,8 +44,8 @@ BYTES = {
     "emit": 117,       # per emitted tile: 64 B state line + 4 B index read, 49 B row written
     "dedup": 20,       # per event: vkey 8 + ts 8 + flags 1 read, win flag 1 written, 2 x 1 B compaction reads
 }
-# k_ingest is fp64-VALU bound: its roofline is fp64 FLOP/s.  FLOPs and HBM bytes per event of this workload
-# were counted by rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r1/ingest_pmc.json).
+# k_ingest's HBM traffic and VALU instruction mix per event of this workload were counted by rocprofv3 PMC
+# passes of this same command (tools/ingest_pmc.py -> profiles/r1/ingest_pmc.json).
 PMC_FILE = os.path.join(ROOT, "profiles", "r1", "ingest_pmc.json")
 
 
@@ -160,17 +161,23 @@ def main():
     launch_bytes["ingest"] += 56 * n_parts
     dom = max(BYTES, key=lambda k: avg_ms[k])
     gbs = launch_bytes[dom] / (avg_ms[dom] * 1e-3) / 1e9 if avg_ms[dom] > 0 else 0.0
+    # Roofline of the dominant kernel, priced on HBM (the metric's "% HBM peak").  For k_ingest the PMC file
+    # (rocprofv3 passes of this same command, tools/ingest_pmc.py) adds the measured HBM traffic and the VALU
+    # side: k_ingest is VALU/latency bound, so the HBM fraction alone understates how busy it is.
+    roof = {"bound": "hbm", "kernel": dom, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": gbs / HBM_PEAK_GBS, "traffic": None}
     pmc = ingest_pmc(args.res) if dom == "ingest" else None
     if pmc is not None:
-        flops = pmc["fp64_flops_per_event"] * n
-        tf = flops / (avg_ms[dom] * 1e-3) / 1e12
-        roof = {"bound": "valu-fp64", "kernel": "k_ingest", "achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": tf / FP64_PEAK_TFLOPS, "traffic": pmc["hbm_bytes_per_event"] * n,
-                "fp64_flops_per_event": pmc["fp64_flops_per_event"], "pmc": os.path.relpath(PMC_FILE, ROOT),
-                "hbm_achieved_gbs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS}
-    else:
-        roof = {"bound": "hbm", "kernel": dom, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": gbs / HBM_PEAK_GBS, "traffic": None}
+        sec = avg_ms[dom] * 1e-3
+        roof["traffic"] = pmc["hbm_bytes_per_event"] * n
+        roof["traffic_source"] = os.path.relpath(PMC_FILE, ROOT)
+        tf = pmc["fp64_flops_per_event"] * n / sec / 1e12
+        # VALU issue: SIMD-32 pipes, 2 cycles per wave64 32-bit op, 4 per fp64 op (MI355X_MICROARCH.md)
+        simd_cycles = (pmc["valu_f64_insts_per_event"] * 4 + pmc["valu_other_insts_per_event"] * 2) * n / 64
+        roof["valu"] = {"fp64_tflops": tf, "fp64_peak_tflops": FP64_PEAK_TFLOPS, "fp64_frac": tf / FP64_PEAK_TFLOPS,
+                        "issue_frac": simd_cycles / (SIMDS * CLOCK_HZ * sec),
+                        "valu_insts_per_event": pmc["valu_insts_per_event"],
+                        "fp64_flops_per_event": pmc["fp64_flops_per_event"]}
     roof.update({"kernel_ms": {k: round(v, 3) for k, v in avg_ms.items()}, "algorithmic_bytes_per_launch": launch_bytes[dom],
                  "units_per_launch": units[dom]})
     value = world * n * K / elapsed
