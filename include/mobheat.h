@@ -163,6 +163,11 @@ int hm_selftest_ld_ops(const double *a, int64_t n, int32_t op, double *out);
  * for the transcendental functions, so it is NOT the device numerics). */
 int hm_selftest_latlng_to_cell_host(const double *lat, const double *lon, int64_t n, int32_t res,
                                     uint64_t *out);
+/* Host-side execution of the kernels' fast path (latLngToCellFast: direct gnomonic projection with a margin
+ * test) with the exact path as fallback, as k_ingest + k_ingest_exact run it; fell_back[i] = 1 where the
+ * exact path was taken (may be NULL). */
+int hm_selftest_latlng_to_cell_fast_host(const double *lat, const double *lon, int64_t n, int32_t res,
+                                         uint64_t *out, uint8_t *fell_back);
 
 /* Timing of the last hm_process_batch / stage call on the library's stream (HIP events), milliseconds
  * per phase: index 0 ingest (k_ingest: filter + cells + windows + pre-aggregation + dedup max), 1 reserved

@@ -330,6 +330,10 @@ struct H3Tables {
     double faceCosLat[20];   // cos(faceCenterGeo[f].lat), host libm
     double faceSinLat[20];   // sin(faceCenterGeo[f].lat), host libm
     float faceCenterPointF[20][3];   // (float)faceCenterPoint: the closest-face prefilter
+    // fast path (latLngToCellFast): per face the gnomonic axes u = (ux, uy) with hex2d = S_res (p.u) / (p.c),
+    // [0] Class II, [1] Class III (rotated by -M_AP7_ROT_RADS); S_res = (1/RES0_U_GNOMONIC) sqrt(7)^res
+    double fastU[2][20][2][3];
+    double fastScale[16];
     int faceIjkBaseCells[20][3][3][3][2];
     int baseCellData[122][7];
 };
@@ -471,6 +475,136 @@ HM_HD uint64_t latLngToCellDeg(double lat_deg, double lng_deg, int res, const H3
     }
     IJK ijk = hex2dToCoordIJK(hx, hy);
     return faceIjkToH3(face, ijk, res, T);
+}
+
+
+// =====================================================================================================
+// Fast path with exact fallback.
+// latLngToCellDeg above follows upstream's operation sequence bit for bit, which costs ~2.7k VALU
+// instructions and ~170 VGPRs per event (five device-library transcendentals, x87 emulation).  The cell is a
+// discrete function of the hex2d coordinates, so any evaluation accurate to within tau gives upstream's cell
+// whenever every decision upstream takes (closest face, the lattice truncations, the comparisons of
+// _hex2dToCoordIJK, the two sign folds) has a margin above tau in our evaluation.  The fast path evaluates
+// the gnomonic projection directly as a ratio of dot products -- no acos/atan2/tan/sincos(theta) -- and
+// returns false (caller runs latLngToCellDeg, out of line) when a margin is below tau:
+//   tan(r) (cos az, sin az) = (p.n, p.e) / (p.c)   (n, e = north/east at the face centre, upstream's azimuth)
+//   hex2d = S_res tan(r) (cos(az0 - az), sin(az0 - az)) = S_res (p.ux, p.uy) / (p.c)
+//   ux = cos(az0) n + sin(az0) e,  uy = sin(az0) n - cos(az0) e   (Class III: rotated by -M_AP7_ROT_RADS)
+// tau bounds |our hex2d - upstream's hex2d| from both sides' rounding: upstream's acos(1 - sqd/2) loses
+// ~2^-53/sqd relative near a face centre, the rest is O(res) ulps of |hex2d| plus O(1) ulps of S_res.
+// =====================================================================================================
+// sin and cos of |x| <= pi + 1e-9 (absolute error < 4e-16): Cody-Waite reduction by pi/2 and fdlibm's
+// kernel polynomials; no large-argument path, so a few registers.
+HM_HD void sincos_small(double x, double &s, double &c) {
+    const double q = rint(x * 0.63661977236758134308);   // 2/pi; |q| <= 2
+    double y = fma(-q, 1.57079632673412561417e+00, x);   // pi/2 head (33 bits): q * head exact
+    y = fma(-q, 6.07710050650619224932e-11, y);          // pi/2 tail
+    const double z = y * y;
+    double ps = fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08);
+    ps = fma(z, ps, 2.75573137070700676789e-06);
+    ps = fma(z, ps, -1.98412698298579493134e-04);
+    ps = fma(z, ps, 8.33333333332248946124e-03);
+    ps = fma(z, ps, -1.66666666666666324348e-01);
+    const double sy = fma(y * z, ps, y);
+    double pc = fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09);
+    pc = fma(z, pc, -2.75573143513906633035e-07);
+    pc = fma(z, pc, 2.48015872894767294178e-05);
+    pc = fma(z, pc, -1.38888888888741095749e-03);
+    pc = fma(z, pc, 4.16666666666666019037e-02);
+    const double cy = fma(z * z, pc, fma(-0.5, z, 1.0));
+    const int k = (int)q & 3;
+    const double a = (k & 1) ? cy : sy, b = (k & 1) ? sy : cy;
+    s = (k & 2) ? -a : a;
+    c = ((k + 1) & 2) ? -b : b;
+}
+
+HM_HD double dmin(double a, double b) { return a < b ? a : b; }
+
+// The fast path.  Returns false when the caller must use latLngToCellDeg; otherwise `out` is upstream's cell
+// (0 where the reference's UDF returns None).
+HM_HD bool latLngToCellFast(double lat_deg, double lng_deg, int res, const H3Tables &T, uint64_t &out) {
+    out = 0;
+    if (!(lat_deg >= -90.0 && lat_deg <= 90.0 && lng_deg >= -180.0 && lng_deg <= 180.0)) return true;
+    double sl, cl, sg, cg;
+    sincos_small(lat_deg * 0.017453292519943295, sl, cl);
+    sincos_small(lng_deg * 0.017453292519943295, sg, cg);
+    const double px = cg * cl, py = sg * cl, pz = sl;
+    // closest face: fp32 dot products (within ~1e-6 of upstream's fp64 argmin); a lead below 1e-5 -> exact path
+    int face = 0;
+    {
+        const float fx = (float)px, fy = (float)py, fz = (float)pz;
+        float best = -4.0f, second = -4.0f;
+        for (int f = 0; f < 20; ++f) {
+            const float d = T.faceCenterPointF[f][0] * fx + T.faceCenterPointF[f][1] * fy + T.faceCenterPointF[f][2] * fz;
+            if (d > best) { second = best; best = d; face = f; }
+            else if (d > second) second = d;
+        }
+        if (!(best - second > 1e-5f)) return false;
+    }
+    const double *c = T.faceCenterPoint[face];
+    const double pc = fma(px, c[0], fma(py, c[1], pz * c[2]));
+    const double sqd = 2.0 - 2.0 * pc;
+    if (!(sqd > 1e-12)) return false;                     // within ~6 m of a face centre: exact path
+    const double(*u)[3] = T.fastU[res & 1][face];
+    const double S = T.fastScale[res];
+    const double inv = S / pc;
+    const double vx = fma(px, u[0][0], fma(py, u[0][1], pz * u[0][2])) * inv;
+    const double vy = fma(px, u[1][0], fma(py, u[1][1], pz * u[1][2])) * inv;
+    const double a1 = __builtin_fabs(vx), a2 = __builtin_fabs(vy);
+    const double M = a1 + a2;
+    const double eps = 0x1p-52;
+    const double tau0 = M * ((4.0 / sqd + 2.0) + res + 128.0) * eps + S * 32.0 * eps;
+#ifndef HM_FAST_TAU_SCALE
+#define HM_FAST_TAU_SCALE 8.0
+#endif
+    const double tau = HM_FAST_TAU_SCALE * tau0;
+    // _hex2dToCoordIJK with the margin of every comparison it makes
+    const double x2 = a2 * 1.15470053837925152902;        // M_RSIN60
+    const double x1 = a1 + x2 / 2.0;
+    const int m1 = (int)x1, m2 = (int)x2;
+    const double r1 = x1 - m1, r2 = x2 - m2;
+    double d = dmin(a1, a2);
+    d = dmin(d, dmin(r1, 1.0 - r1));
+    d = dmin(d, dmin(r2, 1.0 - r2));
+    d = dmin(d, __builtin_fabs(r1 - 1.0 / 3.0));
+    d = dmin(d, __builtin_fabs(r1 - 0.5));
+    d = dmin(d, __builtin_fabs(r1 - 2.0 / 3.0));
+    d = dmin(d, __builtin_fabs(r2 - (1.0 + r1) / 2.0));
+    d = dmin(d, __builtin_fabs(r2 - (1.0 - r1)));
+    d = dmin(d, __builtin_fabs(r2 - 2.0 * r1));
+    d = dmin(d, __builtin_fabs(r2 - (2.0 * r1 - 1.0)));
+    d = dmin(d, __builtin_fabs(r2 - r1 / 2.0));
+    if (!(d > tau) || !(x1 < 1e9)) return false;
+    IJK h;
+    h.k = 0;
+    if (r1 < 0.5) {
+        if (r1 < 1.0 / 3.0) {
+            h.i = m1;
+            h.j = (r2 < (1.0 + r1) / 2.0) ? m2 : m2 + 1;
+        } else {
+            h.j = (r2 < (1.0 - r1)) ? m2 : m2 + 1;
+            h.i = ((1.0 - r1) <= r2 && r2 < (2.0 * r1)) ? m1 + 1 : m1;
+        }
+    } else {
+        if (r1 < 2.0 / 3.0) {
+            h.j = (r2 < (1.0 - r1)) ? m2 : m2 + 1;
+            h.i = ((2.0 * r1 - 1.0) < r2 && r2 < (1.0 - r1)) ? m1 : m1 + 1;
+        } else {
+            h.i = m1 + 1;
+            h.j = (r2 < (r1 / 2.0)) ? m2 : m2 + 1;
+        }
+    }
+    if (vx < 0.0) {
+        if ((h.j % 2) == 0) h.i = h.i - 2 * (h.i - h.j / 2);
+        else h.i = h.i - (2 * (h.i - (h.j + 1) / 2) + 1);
+    }
+    if (vy < 0.0) {
+        h.i = h.i - (2 * h.j + 1) / 2;
+        h.j = -1 * h.j;
+    }
+    ijkNormalize(h);
+    out = faceIjkToH3(face, h, res, T);
+    return true;
 }
 
 }  // namespace hm

@@ -1,0 +1,43 @@
+// Host construction of hm::H3Tables from the generated tables (h3_tables.inc must be included first).
+#pragma once
+#include <cmath>
+#include <cstring>
+
+#include "h3_device.h"
+
+static hm::H3Tables hm_make_tables() {
+    hm::H3Tables T;
+    const long double ap7 = 0.333473172251832115336090755351601070065900389L;   // M_AP7_ROT_RADS
+    for (int f = 0; f < 20; f++) {
+        T.faceCenterGeo[f][0] = H3T_faceCenterGeo[f][0];
+        T.faceCenterGeo[f][1] = H3T_faceCenterGeo[f][1];
+        for (int c = 0; c < 3; c++) {
+            T.faceCenterPoint[f][c] = H3T_faceCenterPoint[f][c];
+            T.faceCenterPointF[f][c] = (float)H3T_faceCenterPoint[f][c];
+        }
+        T.faceAxesAz0[f] = H3T_faceAxesAzRadsCII[f][0];
+        // upstream evaluates cos/sin(p1->lat) per call with the host libm; identical values
+        volatile double lat = H3T_faceCenterGeo[f][0];
+        T.faceCosLat[f] = std::cos(lat);
+        T.faceSinLat[f] = std::sin(lat);
+        // fast-path gnomonic axes (h3_device.h, latLngToCellFast), in x87 extended precision
+        const long double phi = H3T_faceCenterGeo[f][0], lam = H3T_faceCenterGeo[f][1], az0 = H3T_faceAxesAzRadsCII[f][0];
+        const long double n[3] = {-sinl(phi) * cosl(lam), -sinl(phi) * sinl(lam), cosl(phi)};
+        const long double e[3] = {-sinl(lam), cosl(lam), 0.0L};
+        long double ux[3], uy[3];
+        for (int k = 0; k < 3; k++) {
+            ux[k] = cosl(az0) * n[k] + sinl(az0) * e[k];
+            uy[k] = sinl(az0) * n[k] - cosl(az0) * e[k];
+        }
+        for (int k = 0; k < 3; k++) {
+            T.fastU[0][f][0][k] = (double)ux[k];
+            T.fastU[0][f][1][k] = (double)uy[k];
+            T.fastU[1][f][0][k] = (double)(cosl(ap7) * ux[k] + sinl(ap7) * uy[k]);
+            T.fastU[1][f][1][k] = (double)(cosl(ap7) * uy[k] - sinl(ap7) * ux[k]);
+        }
+    }
+    for (int r = 0; r < 16; r++) T.fastScale[r] = (double)((long double)HM_INV_RES0_U_GNOMONIC * powl(sqrtl(7.0L), r));
+    memcpy(T.faceIjkBaseCells, H3T_faceIjkBaseCells, sizeof(T.faceIjkBaseCells));
+    memcpy(T.baseCellData, H3T_baseCellData, sizeof(T.baseCellData));
+    return T;
+}

@@ -36,25 +36,8 @@ using namespace hm;
 
 __constant__ H3Tables c_tab;
 
-static H3Tables make_tables() {
-    H3Tables T;
-    for (int f = 0; f < 20; f++) {
-        T.faceCenterGeo[f][0] = H3T_faceCenterGeo[f][0];
-        T.faceCenterGeo[f][1] = H3T_faceCenterGeo[f][1];
-        for (int c = 0; c < 3; c++) {
-            T.faceCenterPoint[f][c] = H3T_faceCenterPoint[f][c];
-            T.faceCenterPointF[f][c] = (float)H3T_faceCenterPoint[f][c];
-        }
-        T.faceAxesAz0[f] = H3T_faceAxesAzRadsCII[f][0];
-        // upstream evaluates cos/sin(p1->lat) per call with the host libm; identical values
-        volatile double lat = H3T_faceCenterGeo[f][0];
-        T.faceCosLat[f] = std::cos(lat);
-        T.faceSinLat[f] = std::sin(lat);
-    }
-    memcpy(T.faceIjkBaseCells, H3T_faceIjkBaseCells, sizeof(T.faceIjkBaseCells));
-    memcpy(T.baseCellData, H3T_baseCellData, sizeof(T.baseCellData));
-    return T;
-}
+#include "h3_tables_host.h"
+static H3Tables make_tables() { return hm_make_tables(); }
 
 // =====================================================================================================
 // wave helpers
@@ -88,32 +71,58 @@ __device__ __forceinline__ unsigned long long wave_append(bool pred, unsigned lo
 }
 
 // =====================================================================================================
-// K1: filter + latLngToCell + window + late test
+// K1: latLngToCell.  The per-event kernels run latLngToCellFast (h3_device.h: direct gnomonic projection,
+// ~60 VGPRs) and append the rare events whose decision margins are below the error bound to an exception
+// list; a second kernel runs upstream's exact sequence (latLngToCellDeg, ~170 VGPRs) on that list only, so
+// the register footprint of the exact path never limits the occupancy of the streaming kernel.
 // =====================================================================================================
-// waves per SIMD for k_ingest: 3 caps it at 168 VGPRs without spills (measured best of 2..5 on MI355X)
+// waves per SIMD for k_ingest: 6 (<= 80 VGPRs, no spills; the 512-slot LDS table allows 6 workgroups per CU)
 #ifndef HM_SNAP_WAVES
-#define HM_SNAP_WAVES 3
+#define HM_SNAP_WAVES 6
 #endif
 #if HM_SNAP_WAVES > 0
 #define HM_SNAP_ATTR __attribute__((amdgpu_waves_per_eu(HM_SNAP_WAVES)))
 #else
 #define HM_SNAP_ATTR
 #endif
-// standalone UDF: cells only (hm_latlng_to_cell)
+// standalone UDF: cells only (hm_latlng_to_cell); exceptions -> slow[]
 __global__ __launch_bounds__(256) void k_cells(const double *__restrict__ lat, const double *__restrict__ lon, int64_t n,
-                                               int res, uint64_t *__restrict__ out) {
+                                               int res, uint64_t *__restrict__ out, unsigned int *__restrict__ slow,
+                                               unsigned long long *n_slow) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+        const int64_t i = base + threadIdx.x;
+        bool exc = false;
+        if (i < n) {
+            uint64_t c;
+            exc = !latLngToCellFast(lat[i], lon[i], res, c_tab, c);
+            out[i] = c;
+        }
+        const unsigned long long pos = wave_append(exc, n_slow);
+        if (exc) slow[pos] = (unsigned int)i;
+    }
+}
+__global__ __launch_bounds__(256) void k_cells_exact(const double *__restrict__ lat, const double *__restrict__ lon,
+                                                     int res, uint64_t *__restrict__ out, const unsigned int *__restrict__ slow,
+                                                     const unsigned long long *n_slow) {
+    const int64_t m = (int64_t)*n_slow;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned i = slow[q];
         out[i] = latLngToCellDeg(lat[i], lon[i], res, c_tab);
+    }
 }
 
 // =====================================================================================================
 // K2: LDS pre-aggregation into partial records (persistent blocks, flush when the table fills)
 // =====================================================================================================
 constexpr int LA_THREADS = 256;
-constexpr int LA_SLOTS = 1024;
-constexpr int LA_CHUNK = 512;          // events inserted between occupancy checks
-constexpr int LA_FLUSH_AT = LA_SLOTS - 2 * LA_CHUNK + 256;   // occupancy bound before a chunk: <= 768 after
+#ifndef HM_LA_SLOTS
+#define HM_LA_SLOTS 512
+#endif
+constexpr int LA_SLOTS = HM_LA_SLOTS;  // LDS hash slots per workgroup (48 B each)
+constexpr int LA_CHUNK = LA_SLOTS / 2; // events inserted between occupancy checks
+constexpr int LA_FLUSH_AT = LA_SLOTS * 3 / 4 - LA_CHUNK;    // occupancy bound before a chunk: <= 3/4 full after
+static_assert(LA_CHUNK % LA_THREADS == 0 && LA_SLOTS % LA_THREADS == 0, "LDS table geometry");
 
 struct LaShared {
     unsigned long long cell[LA_SLOTS];
@@ -778,7 +787,8 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     const uint8_t *__restrict__ row_valid, const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
     const uint64_t *__restrict__ vkey, int64_t n, int res, int64_t tile_us, int64_t late_end_us,
     uint8_t *__restrict__ flags_out, TilePartial *__restrict__ out, DedupSlot *dtab, unsigned long long dmask,
-    unsigned int *dused, unsigned long long *n_dused, DevStats *st) {
+    unsigned int *dused, unsigned long long *n_dused, unsigned int *__restrict__ slow, unsigned long long *n_slow,
+    DevStats *st) {
     __shared__ LaShared S;
     for (int s = threadIdx.x; s < LA_SLOTS; s += LA_THREADS) {
         S.cell[s] = EMPTY_CELL;
@@ -822,7 +832,13 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
                 nlate += late;
                 const long long ms = (long long)(t / 1000);
                 mx = ms > mx ? ms : mx;
-                if (!late) cell = latLngToCellDeg(la, lo, res, c_tab);
+            }
+            // cell of the aggregated rows; margin exceptions go to k_ingest_exact (exact path, own partial record)
+            bool exc = false;
+            if (fl & F_AGG) exc = !latLngToCellFast(la, lo, res, c_tab, cell);
+            {
+                const unsigned long long pos = wave_append(exc, n_slow);
+                if (exc) slow[pos] = (unsigned int)i;
             }
             if (in) flags_out[i] = fl;
             // dedup: per-vkey max ts over the valid rows (late rows included, as in the reference's batch frame)
@@ -845,7 +861,7 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
             const unsigned long long pos = wave_append(claimed, n_dused);
             if (claimed) dused[pos] = (unsigned int)dh;
             // LDS pre-aggregation of the window's rows
-            if (fl & F_AGG) {
+            if ((fl & F_AGG) && !exc) {
                 const bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
                 const double sp = sv ? speed[i] : 0.0;
                 unsigned h = (unsigned)(tile_hash(cell, ws) & (LA_SLOTS - 1));
@@ -880,6 +896,37 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
         if (mx != INT64_MIN) atomicMax(&st->max_ts_ms, mx);
         if (bad) atomicAdd(&st->bad_vkey, bad);
         if (rt) atomicAdd(&st->dedup_retry, 1ull);
+    }
+}
+
+// exceptions of k_ingest's fast path: upstream's exact sequence, one partial record per event
+__global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__ lat, const double *__restrict__ lon,
+                                                      const int64_t *__restrict__ ts, const double *__restrict__ speed,
+                                                      const uint8_t *__restrict__ speed_valid, int res, int64_t tile_us,
+                                                      const unsigned int *__restrict__ slow, const unsigned long long *n_slow,
+                                                      TilePartial *__restrict__ out, DevStats *st) {
+    const int64_t m = (int64_t)*n_slow;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < m; base += stride) {
+        const int64_t q = base + threadIdx.x;
+        const bool in = q < m;
+        TilePartial p;
+        if (in) {
+            const unsigned i = slow[q];
+            const int64_t t = ts[i];
+            int64_t rem = t % tile_us;
+            if (rem < 0) rem += tile_us;
+            const bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
+            p.cell = latLngToCellDeg(lat[i], lon[i], res, c_tab);
+            p.wstart = t - rem;
+            p.count = 1;
+            p.nspeed = sv;
+            p.sspeed = sv ? speed[i] : 0.0;
+            p.slat = lat[i];
+            p.slon = lon[i];
+        }
+        const unsigned long long pos = wave_append(in, &st->n_partials);
+        if (in) out[pos] = p;
     }
 }
 
@@ -1052,6 +1099,7 @@ struct hm_ctx {
     DevBuf in_lat, in_lon, in_ts, in_speed, in_sv, in_vkey, in_rv;
     DevBuf cell, wstart, flags, win, rows, block_counts, block_offs;
     DevBuf partials, cands, parts_sorted, rp_H, rp_O, rp_btot, rp_boff;
+    DevBuf slow;   // k_ingest's fast-path exceptions (event indices) for k_ingest_exact
     // persistent tile state: open-addressing table + an equally sized compaction target (double buffer).
     // Eviction is lazy: a key whose window end <= the eviction watermark can never be updated again (every
     // later row of its window is dropped as late), so it stays in place, is excluded from n_state through the
@@ -1099,6 +1147,7 @@ static std::string g_create_err;
 // DUSED_WORD: used-slot count of the persistent dedup table (survives until the table is cleared),
 // 255: result count of the last ordered compaction
 constexpr int DUSED_WORD = 253;
+constexpr int SLOW_WORD = 252;   // number of k_ingest fast-path exceptions of the current batch
 
 #define HIPCHK(ctx, expr)                                                                             \
     do {                                                                                              \
@@ -1323,10 +1372,11 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
     int64_t n = I.n;
     int rc;
     if ((rc = ensure(ctx, ctx->flags, n)) || (rc = ensure(ctx, ctx->win, n)) || (rc = ensure(ctx, ctx->rows, n * 8)) ||
-        (rc = ensure(ctx, ctx->partials, n * sizeof(TilePartial))))
+        (rc = ensure(ctx, ctx->partials, n * sizeof(TilePartial))) || (rc = ensure(ctx, ctx->slow, n * sizeof(unsigned int))))
         return rc;
     if ((rc = dedup_prepare(ctx, dedup_fused_keys(ctx, n)))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_st, 0, sizeof(DevStats), ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + SLOW_WORD, 0, 8, ctx->stream));
     long long init[2] = {INT64_MIN, INT64_MAX};
     HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->max_ts_ms, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
@@ -1336,7 +1386,10 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
         hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(LA_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.sp, I.sv, I.vk,
                            n, ctx->cfg.h3_res, ctx->cfg.tile_us, late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
                            (TilePartial *)ctx->partials.p, ctx->dtab, ctx->dcap - 1, (unsigned int *)ctx->dused.p,
-                           ctx->d_scratch + DUSED_WORD, ctx->d_st);
+                           ctx->d_scratch + DUSED_WORD, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, ctx->d_st);
+        hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, I.ts, I.sp, I.sv,
+                           ctx->cfg.h3_res, ctx->cfg.tile_us, (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
+                           (TilePartial *)ctx->partials.p, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
         ctx->dedup_dirty = true;
     }
@@ -1618,7 +1671,7 @@ void hm_destroy(hm_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     DevBuf *bufs[] = {&ctx->in_lat, &ctx->in_lon, &ctx->in_ts, &ctx->in_speed, &ctx->in_sv, &ctx->in_vkey, &ctx->in_rv,
                       &ctx->cell, &ctx->wstart, &ctx->flags, &ctx->win, &ctx->rows, &ctx->block_counts, &ctx->block_offs,
-                      &ctx->partials, &ctx->cands,
+                      &ctx->partials, &ctx->cands, &ctx->slow,
                       &ctx->touched, &ctx->bin_cnt, &ctx->bin_off, &ctx->dused, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
                       &ctx->o_lon, &ctx->o_lat};
     for (DevBuf *b : bufs)
@@ -1651,6 +1704,7 @@ int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n) {
 
 int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t out_memory, hm_batch_out *out) {
     if (!ctx || !in || !out || in->n < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (in->n > (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds 2^32-1", (long long)in->n);
     if (in->n > 0 && (!in->lat || !in->lon || !in->ts_us || !in->vkey))
         return set_err(ctx, HM_E_INVALID, "lat, lon, ts_us and vkey are required");
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -1693,7 +1747,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
 
 int hm_latlng_to_cell(const double *lat, const double *lon, int64_t n, int32_t res, int32_t memory, int32_t device,
                       uint64_t *out) {
-    if (n < 0 || res < 0 || res > 15) return HM_E_INVALID;
+    if (n < 0 || n > (int64_t)UINT32_MAX || res < 0 || res > 15) return HM_E_INVALID;
     if (n == 0) return HM_OK;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device) return HM_E_HIP;
@@ -1706,21 +1760,32 @@ int hm_latlng_to_cell(const double *lat, const double *lon, int64_t n, int32_t r
     }
     const double *dlat = lat, *dlon = lon;
     uint64_t *dout = out;
-    void *a = nullptr, *b = nullptr, *c = nullptr;
+    void *a = nullptr, *b = nullptr, *c = nullptr, *sl = nullptr;
+    auto cleanup = [&]() {
+        for (void *p : {a, b, c, sl})
+            if (p) (void)hipFree(p);
+    };
+    // exception list + its count (last 8 bytes)
+    if (hipMalloc(&sl, n * 4 + 16) != hipSuccess) { cleanup(); return HM_E_NOMEM; }
+    unsigned long long *n_slow = (unsigned long long *)((char *)sl + ((n * 4 + 7) & ~int64_t(7)));
     if (memory == HM_MEM_HOST) {
-        if (hipMalloc(&a, n * 8) || hipMalloc(&b, n * 8) || hipMalloc(&c, n * 8)) return HM_E_NOMEM;
-        if (hipMemcpy(a, lat, n * 8, hipMemcpyHostToDevice) || hipMemcpy(b, lon, n * 8, hipMemcpyHostToDevice)) return HM_E_HIP;
+        if (hipMalloc(&a, n * 8) || hipMalloc(&b, n * 8) || hipMalloc(&c, n * 8)) { cleanup(); return HM_E_NOMEM; }
+        if (hipMemcpy(a, lat, n * 8, hipMemcpyHostToDevice) || hipMemcpy(b, lon, n * 8, hipMemcpyHostToDevice)) { cleanup(); return HM_E_HIP; }
         dlat = (const double *)a;
         dlon = (const double *)b;
         dout = (uint64_t *)c;
     }
-    hipLaunchKernelGGL(k_cells, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, 0, dlat, dlon, n, res, dout);
-    hipError_t e = hipGetLastError();
+    hipError_t e = hipMemset(n_slow, 0, 8);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_cells, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, 0, dlat, dlon, n, res, dout,
+                           (unsigned int *)sl, n_slow);
+        hipLaunchKernelGGL(k_cells_exact, dim3(256), dim3(256), 0, 0, dlat, dlon, res, dout, (const unsigned int *)sl,
+                           (const unsigned long long *)n_slow);
+        e = hipGetLastError();
+    }
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess && memory == HM_MEM_HOST) e = hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost);
-    if (a) (void)hipFree(a);
-    if (b) (void)hipFree(b);
-    if (c) (void)hipFree(c);
+    cleanup();
     return e == hipSuccess ? HM_OK : HM_E_HIP;
 }
 
@@ -1731,6 +1796,7 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     if (!ctx || !in || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks || !tile_send_counts || !cand_send_counts ||
         (in->n > 0 && (!tile_send_buf || !cand_send_buf)))
         return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (in->n > (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds 2^32-1", (long long)in->n);
     if (in->n > 0 && (!in->lat || !in->lon || !in->ts_us || !in->vkey))
         return set_err(ctx, HM_E_INVALID, "lat, lon, ts_us and vkey are required");
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -1913,6 +1979,18 @@ int hm_selftest_latlng_to_cell_host(const double *lat, const double *lon, int64_
     if (!lat || !lon || !out || n < 0 || res < 0 || res > 15) return HM_E_INVALID;
     static const H3Tables T = make_tables();
     for (int64_t i = 0; i < n; i++) out[i] = latLngToCellDeg(lat[i], lon[i], res, T);
+    return HM_OK;
+}
+
+int hm_selftest_latlng_to_cell_fast_host(const double *lat, const double *lon, int64_t n, int32_t res, uint64_t *out,
+                                         uint8_t *fell_back) {
+    if (!lat || !lon || !out || n < 0 || res < 0 || res > 15) return HM_E_INVALID;
+    static const H3Tables T = make_tables();
+    for (int64_t i = 0; i < n; i++) {
+        const bool ok = latLngToCellFast(lat[i], lon[i], res, T, out[i]);
+        if (!ok) out[i] = latLngToCellDeg(lat[i], lon[i], res, T);
+        if (fell_back) fell_back[i] = !ok;
+    }
     return HM_OK;
 }
 

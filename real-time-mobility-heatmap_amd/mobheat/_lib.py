@@ -71,6 +71,7 @@ SIGNATURES = {
     "hm_memcpy": (c_i32, [c_vp, c_vp, c_i64, c_i32]),
     "hm_selftest_ld_ops": (c_i32, [c_vp, c_i64, c_i32, c_vp]),
     "hm_selftest_latlng_to_cell_host": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp]),
+    "hm_selftest_latlng_to_cell_fast_host": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_abi_version": (c_i32, []),
 }
@@ -130,3 +131,14 @@ def latlng_to_cell_host_selftest(lat, lon, res):
     out = np.empty(lat.size, dtype=np.uint64)
     check(lib.hm_selftest_latlng_to_cell_host(ptr(lat), ptr(lon), lat.size, res, ptr(out)))
     return out
+
+
+def latlng_to_cell_fast_host_selftest(lat, lon, res):
+    """Host execution of the kernels' fast path + exact fallback; returns (cells, fell_back mask)."""
+    lib = load()
+    lat = np.ascontiguousarray(lat, dtype=np.float64)
+    lon = np.ascontiguousarray(lon, dtype=np.float64)
+    out = np.empty(lat.size, dtype=np.uint64)
+    fb = np.empty(lat.size, dtype=np.uint8)
+    check(lib.hm_selftest_latlng_to_cell_fast_host(ptr(lat), ptr(lon), lat.size, res, ptr(out), ptr(fb)))
+    return out, fb.astype(bool)

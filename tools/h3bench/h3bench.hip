@@ -10,15 +10,19 @@
 #include "kernels.h"
 #define H3T_CONST static const
 #include "h3_tables.inc"
+#include "h3_tables_host.h"
 using namespace hm;
 
 #ifndef VARIANT
 #define VARIANT "base"
 #endif
+#ifndef H3B_WAVES
+#define H3B_WAVES 3
+#endif
 
 __constant__ H3Tables c_tab;
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_cells(const double *lat, const double *lon,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H3B_WAVES))) void k_cells(const double *lat, const double *lon,
                                                                                        long n, int res, uint64_t *out) {
     for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
         out[i] = latLngToCellDeg(lat[i], lon[i], res, c_tab);
@@ -44,19 +48,7 @@ int main(int argc, char **argv) {
     long n = argc > 1 ? atol(argv[1]) : 100000000L;
     int res = argc > 2 ? atoi(argv[2]) : 8;
     int reps = argc > 3 ? atoi(argv[3]) : 5;
-    H3Tables T;
-    for (int f = 0; f < 20; f++) {
-        for (int q = 0; q < 2; q++) T.faceCenterGeo[f][q] = H3T_faceCenterGeo[f][q];
-        for (int q = 0; q < 3; q++) {
-            T.faceCenterPoint[f][q] = H3T_faceCenterPoint[f][q];
-            T.faceCenterPointF[f][q] = (float)H3T_faceCenterPoint[f][q];
-        }
-        T.faceAxesAz0[f] = H3T_faceAxesAzRadsCII[f][0];
-        T.faceCosLat[f] = cos(H3T_faceCenterGeo[f][0]);
-        T.faceSinLat[f] = sin(H3T_faceCenterGeo[f][0]);
-    }
-    memcpy(T.baseCellData, H3T_baseCellData, sizeof(T.baseCellData));
-    memcpy(T.faceIjkBaseCells, H3T_faceIjkBaseCells, sizeof(T.faceIjkBaseCells));
+    H3Tables T = hm_make_tables();
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &T, sizeof(T)) != hipSuccess) return 2;
     double *lat, *lon;
     uint64_t *out;
@@ -69,7 +61,7 @@ int main(int argc, char **argv) {
     float best = 1e30f;
     for (int r = 0; r < reps; r++) {
         hipEventRecord(e0, 0);
-        hipLaunchKernelGGL(k_cells, dim3(256 * 3 * 8), dim3(256), 0, 0, lat, lon, n, res, out);
+        hipLaunchKernelGGL(k_cells, dim3(256 * H3B_WAVES * 8), dim3(256), 0, 0, lat, lon, n, res, out);
         hipEventRecord(e1, 0);
         if (hipEventSynchronize(e1) != hipSuccess) return 4;
         float ms;

@@ -33,12 +33,15 @@ VARIANTS = {
     "no_digits": [("    for (int r = res - 1; r >= 0; r--) {", "    for (int r = -1; r >= 0; r--) {")],
     "x87_plain+trig_cheap": X87_PLAIN + TRIG_CHEAP,
 }
+# occupancy variants of the unmodified header: waves per SIMD (amdgpu_waves_per_eu) of the cells kernel
+WAVES = {"base": 3, "base_w4": 4, "base_w5": 5, "base_w6": 6, "base_w8": 8}
 
 
 def main():
     os.makedirs(BUILD, exist_ok=True)
     src = open(os.path.join(CSRC, "h3_device.h")).read()
-    for name, patches in VARIANTS.items():
+    for name in list(WAVES) + [v for v in VARIANTS if v != "base"]:
+        patches = VARIANTS.get(name, [])
         s = src
         for a, b in patches:
             if a not in s:
@@ -47,14 +50,14 @@ def main():
         d = os.path.join(BUILD, name.replace("+", "_"))
         os.makedirs(d, exist_ok=True)
         open(os.path.join(d, "h3_device.h"), "w").write(s)
-        for f in ("kernels.h", "h3_tables.inc"):
+        for f in ("kernels.h", "h3_tables.inc", "h3_tables_host.h"):
             dst = os.path.join(d, f)
             if os.path.exists(dst):
                 os.remove(dst)
             os.symlink(os.path.abspath(os.path.join(CSRC, f)), dst)
         out = os.path.join(BUILD, "h3bench_" + name.replace("+", "_"))
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-               f'-DVARIANT="{name}"', "-I", d, "-o", out, os.path.join(HERE, "h3bench.hip")]
+               f'-DVARIANT="{name}"', f"-DH3B_WAVES={WAVES.get(name, 3)}", "-I", d, "-o", out, os.path.join(HERE, "h3bench.hip")]
         subprocess.run(cmd, check=True)
         print("built", out)
 
