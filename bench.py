@@ -6,9 +6,9 @@ OpenSky-like global batch of 1e8 events uniform on the sphere, 50k vehicle ids, 
 (3 five-minute windows), 10% null speeds -- at the metric's H3 resolution 8 (configs[1] quotes res 7;
 --res 7 runs that).  One step = one micro-batch through the whole hot path on device-resident inputs:
 one fused pass over the events (k_ingest: filter + latLngToCell + window + late test + LDS pre-aggregation +
-per-vehicle max ts), radix partition of the partials by state-table region, the region-owned merge into the
-persistent update-mode state (k_merge_owned), emission (k_emit_bins), eviction/compaction, and the
-latest-position flags + compaction.
+per-vehicle max ts), census of the partials per window (sizes the per-window state tables), radix partition into
+(window, region) bins, the region-owned merge into the persistent update-mode state (k_merge_owned), emission
+(k_emit_bins), eviction (whole window tables released), and the latest-position flags + compaction.
 Every step is a NEW micro-batch: its timestamps are the previous step's + 15 min (precomputed before the
 timed region), so the stream advances, windows close and are evicted, and no row is late.
 For N>1 each rank runs the sharded path (mobheat.distributed: RCCL all-to-all of partials by owner).
@@ -36,12 +36,12 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector peak: 1024 SIMDs x 16 FMA lanes x
 SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 # algorithmic HBM bytes per unit: per event (ingest, dedup), per partial record (partition,
-# merge), per emitted tile (emit).  ingest also writes 56 B per partial (added below).
+# merge), per emitted tile (emit).  ingest also writes 64 B per partial (added below).
 BYTES = {
     "ingest": 43,      # read lat 8 + lon 8 + ts 8 + speed 8 + speed_valid 1 + vkey 8 + row_valid 1; write flags 1
-    "partition": 168,  # per partial: histogram read 56 B + scatter read 56 B + write 56 B
-    "merge": 188,      # per partial: read 56 B record + 64 B state line read + 64 B written + 4 B touched index
-    "emit": 117,       # per emitted tile: 64 B state line + 4 B index read, 49 B row written
+    "partition": 256,  # per 64-B partial: census read + histogram read + scatter read + write
+    "merge": 200,      # per partial: read 64 B record + 64 B state line read + 64 B written + 8 B touched address
+    "emit": 121,       # per emitted tile: 64 B state line + 8 B address read, 49 B row written
     "dedup": 20,       # per event: vkey 8 + ts 8 + flags 1 read, win flag 1 written, 2 x 1 B compaction reads
 }
 # k_ingest's HBM traffic and VALU instruction mix per event of this workload were counted by rocprofv3 PMC
@@ -117,7 +117,7 @@ def main():
     n = args.events
     total_steps = args.warmup + args.steps
     data = gen_batch(n, total_steps, seed=1 + 7919 * rank, dev=dev)
-    eng = mobheat.HeatmapEngine(h3_res=args.res, device=local, state_capacity_hint=1 << 30, batch_capacity_hint=n)
+    eng = mobheat.HeatmapEngine(h3_res=args.res, device=local, batch_capacity_hint=n)
     sharded = ShardedHeatmap(LibStages(eng), dev) if world > 1 else None
 
     def step(s):
@@ -137,8 +137,11 @@ def main():
     kt = {k: 0.0 for k in BYTES}
     t0 = time.perf_counter()
     last = None
+    step_ms = []
     for s in range(args.warmup, total_steps):
+        ts0 = time.perf_counter()
         last = step(s)
+        step_ms.append((time.perf_counter() - ts0) * 1e3)
         tm = eng.last_timings()
         for k in BYTES:
             kt[k] += tm[k]
@@ -158,7 +161,7 @@ def main():
     n_parts = int(last.n_partials) if last is not None else 0
     units = {"ingest": n, "dedup": n, "partition": n_parts, "merge": n_parts, "emit": n_tiles}
     launch_bytes = {k: BYTES[k] * units[k] for k in BYTES}
-    launch_bytes["ingest"] += 56 * n_parts
+    launch_bytes["ingest"] += 64 * n_parts
     dom = max(BYTES, key=lambda k: avg_ms[k])
     gbs = launch_bytes[dom] / (avg_ms[dom] * 1e-3) / 1e9 if avg_ms[dom] > 0 else 0.0
     # Roofline of the dominant kernel, priced on HBM (the metric's "% HBM peak").  For k_ingest the PMC file
@@ -194,6 +197,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.res)
     if rank == 0:
+        print("per-step ms (host wall, rank 0): " + " ".join(f"{x:.1f}" for x in step_ms), file=sys.stderr, flush=True)
         print(json.dumps(out), flush=True)
     eng.close()
     if world > 1:

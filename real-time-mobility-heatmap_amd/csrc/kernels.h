@@ -28,8 +28,9 @@ struct alignas(64) TileSlot {
 };
 static_assert(sizeof(TileSlot) == 64, "TileSlot must be one 64-B line");
 
-// tile partial record exchanged between stages / ranks (HM_TILE_REC_BYTES = 56)
-struct TilePartial {
+// tile partial record exchanged between stages / ranks (HM_TILE_REC_BYTES = 64): one 64-B line, so the
+// radix scatter's randomly placed records are whole-line writes (no read-modify-write of partial lines)
+struct alignas(64) TilePartial {
     uint64_t cell;
     int64_t wstart;
     int64_t count;
@@ -37,8 +38,9 @@ struct TilePartial {
     double sspeed;
     double slat;
     double slon;
+    uint64_t reserved;
 };
-static_assert(sizeof(TilePartial) == 56, "TilePartial is 56 B");
+static_assert(sizeof(TilePartial) == 64, "TilePartial is 64 B");
 
 // latest-position candidate (HM_CAND_REC_BYTES = 32)
 struct Cand {
@@ -52,9 +54,29 @@ static_assert(sizeof(Cand) == 32, "Cand is 32 B");
 HM_HD unsigned long long wenc_of(int64_t w) { return (unsigned long long)w ^ (UINT64_C(1) << 63); }
 HM_HD int64_t wdec(unsigned long long e) { return (int64_t)(e ^ (UINT64_C(1) << 63)); }
 
-// live-key count per window (lazy eviction: dead keys stay in the table until the next compaction, so
-// the number of live keys is the sum over windows whose end is after the watermark)
-constexpr int WMAP_SLOTS = 4096;
+// Per-window state tables ("generations").  Every live window (windowStart) has its own open-addressing table
+// of TileSlots; a window's keys never outlive it, so eviction releases the whole table (O(1), no compaction)
+// and a released table is reused for a later window WITHOUT clearing: a slot belongs to window w iff its wenc
+// is w's.  (Safe because a window never returns once evicted -- its rows are late from then on -- and a
+// growing window only moves to larger tables, never back into one that still holds its stale keys.)
+// A table of 2^L slots is split into 2^rbits regions of >= 256 slots; a key's region is taken from hash bits
+// [20, 32) and its slot from the low bits, linear probing wraps inside the region.  The radix partition
+// sends all partials of (window, region) to ONE bin = (region << (12 - rbits)) | (window salt), so the merge
+// workgroup of a bin is the only writer of the regions it receives.
+constexpr int GMAP_SLOTS = 4096;        // live windows per context (open addressing by wenc)
+constexpr int REGION_MIN_BITS = 8;      // >= 256 slots per region (overflow-free at load <= 1/2)
+struct GenDesc {
+    unsigned long long wenc;   // 0 = empty map slot
+    TileSlot *tab;
+    unsigned long long rmask;  // slots per region - 1
+    unsigned int rshift;       // log2(slots per region)
+    unsigned int rbits;        // log2(regions), <= 12
+    unsigned long long count;  // keys of this window in its table (the merge adds created keys)
+    unsigned long long pad;
+};
+static_assert(sizeof(GenDesc) == 48, "GenDesc is 48 B");
+
+// partial count per window of a batch (the census that sizes the tables)
 struct WinCount {
     unsigned long long wenc;   // 0 = empty
     unsigned long long count;
@@ -73,7 +95,7 @@ struct DevStats {
     long long min_wstart;          // min window start inserted into the state since the last rebuild
     unsigned long long n_partials;
     unsigned long long n_touched;
-    unsigned long long n_state_new; // keys created in the state table
+    unsigned long long n_state_new; // keys created in the state tables
     unsigned long long n_dedup_used;
     unsigned long long n_cands;
     unsigned long long overflow;    // nonzero: a hash table probe bound was exceeded
@@ -94,5 +116,8 @@ HM_HD uint64_t tile_hash(uint64_t cell, int64_t w) { return mix64(cell ^ mix64((
 HM_HD uint64_t vkey_hash(uint64_t v) { return mix64(v ^ UINT64_C(0x2545f4914f6cdd1d)); }
 // owner rank of a key: taken from high hash bits so it is independent of the table index bits
 HM_HD int owner_of(uint64_t h, int nranks) { return (int)(((h >> 32) * (uint64_t)nranks) >> 32); }
+// a key's 12-bit region field (independent of the table size and of the owner bits)
+HM_HD unsigned region_field(uint64_t h) { return (unsigned)(h >> 20) & 4095u; }
+HM_HD unsigned window_salt(unsigned long long we) { return (unsigned)mix64(we ^ UINT64_C(0x51ed270b27e5b3c1)); }
 
 }  // namespace hm

@@ -4,15 +4,15 @@
 //   k_ingest      one pass over the events: filter (heatmap_stream.py:96-104) + H3 latLngToCell UDF
 //                 (:65-75,105) + tumbling window (:115) + late-row test against the watermark (:107) + batch
 //                 max event time; per-vkey max ts for the dedup (:200-203); LDS hash pre-aggregation of
-//                 (cell, windowStart) -> count, n_speed, sum speed/lat/lon into 56-B partial records
+//                 (cell, windowStart) -> count, n_speed, sum speed/lat/lon into 64-B partial records
 //                 (Spark's partial HashAggregate, :112-123)
 //   [multi-GPU: partials partitioned by owner rank, exchanged by the caller with RCCL all-to-all]
-//   k_rp_*        radix partition of the partials by state-table region
-//   k_merge_owned one workgroup per region merges its partials into the persistent device state table
+//   k_census      partials per window -> sizes each window's state table (kernels.h: GenDesc)
+//   k_rp_*        radix partition of the partials into one bin per (window, table region)
+//   k_merge_owned one workgroup per bin merges its partials into the persistent per-window state tables
 //                 (update mode, :243; Spark's StateStoreRestore/Save), marking touched keys
-//                 (k_merge: the device-atomic variant for small tables / batches)
 //   k_emit_bins   touched keys -> output rows with cumulative count/avg (:124-132)
-//   k_rehash      compaction: drops keys evicted by the watermark (window end <= watermark), grows the table
+//   eviction      (watermark, :107) releases a window's whole table; k_dump_gen + a rehash merge grow one
 //   k_dedup_flag  latest position per (provider, vehicleId): rows whose ts equals the max (:204-207)
 //
 // Semantics follow SURVEY.md App. A (Spark 3.5.1): see DESIGN.md for the rules and their provenance.
@@ -68,6 +68,138 @@ __device__ __forceinline__ unsigned long long wave_append(bool pred, unsigned lo
     }
     unsigned long long below = m & ((UINT64_C(1) << lane_id()) - 1);
     return base + __popcll(below);
+}
+
+// =====================================================================================================
+// K3: per-window state tables (kernels.h: GenDesc) -- lookup, census, growth dump
+// =====================================================================================================
+__device__ __forceinline__ int gmap_find(const GenDesc *gm, unsigned long long we) {
+    unsigned h = (unsigned)(mix64(we) & (GMAP_SLOTS - 1));
+    for (int probe = 0; probe < GMAP_SLOTS; probe++) {
+        const unsigned long long w = gm[h].wenc;
+        if (w == we) return (int)h;
+        if (w == 0) return -1;
+        h = (h + 1) & (GMAP_SLOTS - 1);
+    }
+    return -1;
+}
+__device__ __forceinline__ unsigned long long home_slot(const GenDesc &g, uint64_t h) {
+    return ((unsigned long long)(region_field(h) >> (12 - g.rbits)) << g.rshift) | (h & g.rmask);
+}
+// linear probing wraps inside the key's region
+__device__ __forceinline__ unsigned long long next_slot(unsigned long long s, unsigned long long rmask) {
+    return (s & ~rmask) | ((s + 1) & rmask);
+}
+
+// LDS copy of the live windows' table descriptors (a batch touches a few windows; the global map is the
+// fallback when there are more than GC_MAX)
+constexpr int GC_MAX = 32;
+struct GenCache {
+    GenDesc e[GC_MAX];
+    int n;   // -1: use the global map
+};
+__device__ __forceinline__ void gc_load(GenCache &C, const GenDesc *glist, int n) {
+    if (threadIdx.x == 0) C.n = n <= GC_MAX ? n : -1;
+    if (n <= GC_MAX)
+        for (int q = threadIdx.x; q < n; q += blockDim.x) C.e[q] = glist[q];
+}
+__device__ __forceinline__ const GenDesc *gen_lookup(const GenCache &C, const GenDesc *gm, unsigned long long we) {
+    if (C.n >= 0) {
+        for (int q = 0; q < C.n; q++)
+            if (C.e[q].wenc == we) return &C.e[q];
+        return nullptr;
+    }
+    const int g = gmap_find(gm, we);
+    return g < 0 ? nullptr : &gm[g];
+}
+// radix bin of a key: every partial of one (window, region) lands in one bin; -1 if the window has no table
+__device__ __forceinline__ int bin_of_c(const GenCache &C, const GenDesc *gm, uint64_t cell, int64_t w) {
+    const unsigned long long we = wenc_of(w);
+    const GenDesc *g = gen_lookup(C, gm, we);
+    if (!g) return -1;
+    const unsigned rb = g->rbits;
+    const unsigned reg = region_field(tile_hash(cell, w)) >> (12 - rb);
+    return (int)((reg << (12 - rb)) | (window_salt(we) & ((1u << (12 - rb)) - 1)));
+}
+
+// census map: partial count per window (open addressing; counts added by one atomic per window per workgroup)
+__device__ __forceinline__ bool wmap_add(WinCount *m, unsigned long long we, unsigned long long cnt) {
+    unsigned h = (unsigned)(mix64(we) & (GMAP_SLOTS - 1));
+    for (int probe = 0; probe < GMAP_SLOTS; probe++) {
+        unsigned long long cur = __hip_atomic_load(&m[h].wenc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == 0) cur = atomicCAS(&m[h].wenc, 0ull, we);
+        if (cur == 0 || cur == we) {
+            atomicAdd(&m[h].count, cnt);
+            return true;
+        }
+        h = (h + 1) & (GMAP_SLOTS - 1);
+    }
+    return false;
+}
+// created keys -> the window's table key count
+__device__ __forceinline__ bool gmap_add(GenDesc *gm, unsigned long long we, unsigned long long cnt) {
+    const int g = gmap_find(gm, we);
+    if (g < 0) return false;
+    atomicAdd(&gm[g].count, cnt);
+    return true;
+}
+struct CensusSink {
+    WinCount *m;
+    __device__ bool add(unsigned long long we, unsigned long long c) const { return wmap_add(m, we, c); }
+};
+struct GenSink {
+    GenDesc *m;
+    __device__ bool add(unsigned long long we, unsigned long long c) const { return gmap_add(m, we, c); }
+};
+// Per-workgroup window counts in LDS, flushed to the global map once per workgroup: a batch touches only a
+// few windows, so per-wave global adds would all hit the same few counters.
+constexpr int WL_SLOTS = 32;
+struct WinLds {
+    unsigned long long key[WL_SLOTS];
+    unsigned long long cnt[WL_SLOTS];
+};
+__device__ __forceinline__ void wl_init(WinLds &L) {
+    for (int q = threadIdx.x; q < WL_SLOTS; q += blockDim.x) { L.key[q] = 0; L.cnt[q] = 0; }
+}
+template <class Sink>
+__device__ __forceinline__ bool wl_add(WinLds &L, const Sink &g, unsigned long long we, unsigned long long c) {
+    unsigned h = (unsigned)(mix64(we) & (WL_SLOTS - 1));
+    for (int probe = 0; probe < WL_SLOTS; probe++) {
+        unsigned long long o = atomicCAS(&L.key[h], 0ull, we);
+        if (o == 0 || o == we) { atomicAdd(&L.cnt[h], c); return true; }
+        h = (h + 1) & (WL_SLOTS - 1);
+    }
+    return g.add(we, c);   // more distinct windows than LDS slots: straight to the global map
+}
+// after a __syncthreads(): one lane per LDS slot adds its count to the global map
+template <class Sink>
+__device__ __forceinline__ bool wl_flush(WinLds &L, const Sink &g) {
+    bool ok = true;
+    for (int q = threadIdx.x; q < WL_SLOTS; q += blockDim.x)
+        if (L.key[q]) ok &= g.add(L.key[q], L.cnt[q]);
+    return ok;
+}
+// wave-cooperative: lanes with `pred` add `c` each to their window's count (one LDS add per window per wave)
+template <class Sink>
+__device__ __forceinline__ bool wave_count_windows(bool pred, unsigned long long we, unsigned long long c, WinLds &L,
+                                                   const Sink &g) {
+    bool ok = true;
+    while (true) {
+        unsigned long long pend = __ballot(pred);
+        if (!pend) break;
+        int leader = __ffsll((long long)pend) - 1;
+        unsigned long long wl = __shfl(we, leader, 64);
+        bool match = pred && we == wl;
+        unsigned long long sum = 0;
+        {
+            unsigned long long v = match ? c : 0;
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            sum = v;
+        }
+        if (lane_id() == leader) ok = wl_add(L, g, wl, sum);
+        pred = pred && !match;
+    }
+    return ok;
 }
 
 // =====================================================================================================
@@ -136,7 +268,7 @@ struct LaShared {
     unsigned long long base;
 };
 
-__device__ void la_flush(LaShared &S, TilePartial *out, DevStats *st) {
+__device__ void la_flush(LaShared &S, TilePartial *out, DevStats *st, WinLds &WL, const CensusSink &census, bool &ok) {
     __syncthreads();
     const int per = LA_SLOTS / LA_THREADS;  // 4
     int t = threadIdx.x;
@@ -161,8 +293,11 @@ __device__ void la_flush(LaShared &S, TilePartial *out, DevStats *st) {
     unsigned long long pos = S.base + wave_off + incl - c;
     for (int q = 0; q < per; q++) {
         int s = t * per + q;
-        if (S.cell[s] != EMPTY_CELL) {
+        const bool present = S.cell[s] != EMPTY_CELL;
+        ok &= wave_count_windows(present, wenc_of(S.w[s]), 1ull, WL, census);   // census for the merge
+        if (present) {
             TilePartial p;
+            p.reserved = 0;
             p.cell = S.cell[s];
             p.wstart = S.w[s];
             p.count = (int64_t)(S.cnt[s] & 0xffffffffull);
@@ -183,191 +318,82 @@ __device__ void la_flush(LaShared &S, TilePartial *out, DevStats *st) {
     __syncthreads();
 }
 
-// =====================================================================================================
-// K3: merge partials into the persistent state table
-// =====================================================================================================
-// Table geometry: slot index = hash & mask; the table is split into regions of (rmask + 1) slots and linear
-// probing wraps inside the key's region, so a region can be owned by one workgroup (k_merge_owned).
-__device__ __forceinline__ unsigned long long next_slot(unsigned long long h, unsigned long long rmask) {
-    return (h & ~rmask) | ((h + 1) & rmask);
-}
-
-__device__ __forceinline__ long long find_or_claim_tile(TileSlot *tab, unsigned long long mask, unsigned long long rmask,
-                                                        uint64_t c, int64_t w, bool &created) {
-    const unsigned long long we = wenc_of(w);
-    unsigned long long h = tile_hash(c, w) & mask;
-    created = false;
-    for (unsigned long long probe = 0; probe <= rmask; probe++) {
-        TileSlot *s = &tab[h];
-        unsigned long long cur = __hip_atomic_load(&s->cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == EMPTY_CELL) cur = atomicCAS((unsigned long long *)&s->cell, (unsigned long long)EMPTY_CELL, (unsigned long long)c);
-        if (cur == EMPTY_CELL || cur == c) {
-            unsigned long long cw = __hip_atomic_load(&s->wenc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cw == 0) {
-                cw = atomicCAS(&s->wenc, 0ull, we);
-                if (cw == 0) { created = true; return (long long)h; }
-            }
-            if (cw == we) return (long long)h;
-        }
-        h = next_slot(h, rmask);
-    }
-    return -1;
-}
-
-// add `cnt` live keys to window `we` in the window map (one atomic per distinct window per wave)
-__device__ __forceinline__ bool wmap_add(WinCount *m, unsigned long long we, unsigned long long cnt) {
-    unsigned h = (unsigned)(mix64(we) & (WMAP_SLOTS - 1));
-    for (int probe = 0; probe < WMAP_SLOTS; probe++) {
-        unsigned long long cur = __hip_atomic_load(&m[h].wenc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == 0) cur = atomicCAS(&m[h].wenc, 0ull, we);
-        if (cur == 0 || cur == we) {
-            atomicAdd(&m[h].count, cnt);
-            return true;
-        }
-        h = (h + 1) & (WMAP_SLOTS - 1);
-    }
-    return false;
-}
-// Per-workgroup window counts in LDS, flushed to the global map once per workgroup: a batch touches only a
-// few windows, so per-wave global adds would all hit the same few counters.
-constexpr int WL_SLOTS = 32;
-struct WinLds {
-    unsigned long long key[WL_SLOTS];
-    unsigned long long cnt[WL_SLOTS];
-};
-__device__ __forceinline__ void wl_init(WinLds &L) {
-    for (int q = threadIdx.x; q < WL_SLOTS; q += blockDim.x) { L.key[q] = 0; L.cnt[q] = 0; }
-}
-__device__ __forceinline__ bool wl_add(WinLds &L, WinCount *g, unsigned long long we, unsigned long long c) {
-    unsigned h = (unsigned)(mix64(we) & (WL_SLOTS - 1));
-    for (int probe = 0; probe < WL_SLOTS; probe++) {
-        unsigned long long o = atomicCAS(&L.key[h], 0ull, we);
-        if (o == 0 || o == we) { atomicAdd(&L.cnt[h], c); return true; }
-        h = (h + 1) & (WL_SLOTS - 1);
-    }
-    return wmap_add(g, we, c);   // more distinct windows than LDS slots: straight to the global map
-}
-// after a __syncthreads(): one lane per LDS slot adds its count to the global map
-__device__ __forceinline__ bool wl_flush(WinLds &L, WinCount *g) {
-    bool ok = true;
-    for (int q = threadIdx.x; q < WL_SLOTS; q += blockDim.x)
-        if (L.key[q]) ok &= wmap_add(g, L.key[q], L.cnt[q]);
-    return ok;
-}
-// wave-cooperative: lanes with `pred` add one key each to their window's count (one LDS add per window per wave)
-__device__ __forceinline__ bool wave_count_windows(bool pred, unsigned long long we, WinLds &L, WinCount *g) {
-    bool ok = true;
-    while (true) {
-        unsigned long long pend = __ballot(pred);
-        if (!pend) break;
-        int leader = __ffsll((long long)pend) - 1;
-        unsigned long long wl = __shfl(we, leader, 64);
-        bool match = pred && we == wl;
-        unsigned long long mm = __ballot(match);
-        if (lane_id() == leader) ok = wl_add(L, g, wl, (unsigned long long)__popcll(mm));
-        pred = pred && !match;
-    }
-    return ok;
-}
-
-constexpr unsigned KM_TBUF = 4096;
-// block-uniform: move the block's buffered touched slots to the global list with one atomic
-__device__ __forceinline__ void km_flush_touched(unsigned *tbuf, unsigned &tcnt, unsigned long long &tbase,
-                                                 unsigned int *touched, DevStats *st) {
-    const unsigned c = tcnt;
-    if (c == 0) return;
-    if (threadIdx.x == 0) tbase = atomicAdd(&st->n_touched, (unsigned long long)c);
-    __syncthreads();
-    for (unsigned q = threadIdx.x; q < c; q += blockDim.x) touched[tbase + q] = tbuf[q];
-    __syncthreads();
-    if (threadIdx.x == 0) tcnt = 0;
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(256) void k_merge(const TilePartial *__restrict__ parts, int64_t n, TileSlot *tab,
-                                               unsigned long long mask, unsigned long long rmask, unsigned long long seq,
-                                               unsigned int *touched, WinCount *wmap, DevStats *st) {
+// census of a batch's partials per window (sizes the window tables before the merge)
+__global__ __launch_bounds__(256) void k_census(const TilePartial *__restrict__ parts, int64_t n, WinCount *cmap, DevStats *st) {
     __shared__ WinLds WL;
-    __shared__ unsigned tbuf[KM_TBUF];     // touched slots, flushed to the global list in blocks
-    __shared__ unsigned tcnt;
-    __shared__ unsigned long long tbase;
     wl_init(WL);
-    if (threadIdx.x == 0) tcnt = 0;
     __syncthreads();
+    const CensusSink sink{cmap};
+    bool ok = true;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    unsigned long long created_cnt = 0;
-    bool overflow = false;
-    // uniform trip count per wave so the ballots in wave_append / wave_count_windows see every lane
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
-        int64_t i = base + threadIdx.x;
-        bool first = false, created = false;
-        long long h = -1;
-        int64_t w = 0;
-        if (i < n) {
-            TilePartial p = parts[i];
-            w = p.wstart;
-            h = find_or_claim_tile(tab, mask, rmask, p.cell, p.wstart, created);
-            if (h < 0) {
-                overflow = true;
-            } else {
-                TileSlot *s = &tab[h];
-                atomicAdd(&s->count, (unsigned long long)p.count);
-                if (p.nspeed) {
-                    atomicAdd(&s->nspeed, (unsigned long long)p.nspeed);
-                    unsafeAtomicAdd(&s->sspeed, p.sspeed);
-                }
-                unsafeAtomicAdd(&s->slat, p.slat);
-                unsafeAtomicAdd(&s->slon, p.slon);
-                unsigned long long old = atomicMax(&s->touched, seq);
-                first = old < seq;
-                created_cnt += created;
-            }
-        }
-        if (!wave_count_windows(created, wenc_of(w), WL, wmap)) overflow = true;
-        const unsigned long long fb = __ballot(first);
-        unsigned off = 0;
-        if (lane_id() == 0 && fb) off = atomicAdd(&tcnt, (unsigned)__popcll(fb));
-        off = __shfl(off, 0, 64);
-        if (first) tbuf[off + (unsigned)__popcll(fb & ((1ull << lane_id()) - 1))] = (unsigned)h;
-        __syncthreads();
-        if (tcnt > KM_TBUF - 256) km_flush_touched(tbuf, tcnt, tbase, touched, st);
+        const int64_t i = base + threadIdx.x;
+        const bool in = i < n;
+        const unsigned long long we = in ? wenc_of(parts[i].wstart) : 0;
+        ok &= wave_count_windows(in, we, 1ull, WL, sink);
     }
     __syncthreads();
-    km_flush_touched(tbuf, tcnt, tbase, touched, st);
-    if (!wl_flush(WL, wmap)) overflow = true;
-    created_cnt = wave_sum(created_cnt);
-    unsigned long long ov = __ballot(overflow);
-    if (lane_id() == 0) {
-        if (created_cnt) atomicAdd(&st->n_state_new, created_cnt);
-        if (ov) atomicAdd(&st->overflow, 1ull);
+    ok &= wl_flush(WL, sink);
+    if (__ballot(!ok) && lane_id() == 0) atomicAdd(&st->overflow, 1ull);
+}
+
+// growth: the live keys of one window's old table as partial records (reserved = the key's touched seq), to be
+// merged into its new table by k_merge_owned in rehash mode
+__global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, TilePartial *__restrict__ out, unsigned long long *n_out) {
+    const unsigned long long cap = (g.rmask + 1) << g.rbits;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < (int64_t)cap; base += stride) {
+        const int64_t i = base + threadIdx.x;
+        bool live = false;
+        TilePartial p;
+        if (i < (int64_t)cap) {
+            const TileSlot sl = g.tab[i];
+            live = sl.wenc == g.wenc;
+            p.cell = sl.cell;
+            p.wstart = wdec(sl.wenc);
+            p.count = (int64_t)sl.count;
+            p.nspeed = (int64_t)sl.nspeed;
+            p.sspeed = sl.sspeed;
+            p.slat = sl.slat;
+            p.slon = sl.slon;
+            p.reserved = sl.touched;
+        }
+        const unsigned long long pos = wave_append(live, n_out);
+        if (live) out[pos] = p;
     }
 }
 
 // =====================================================================================================
-// K2b: radix partition of the partials by state-table region (top RP_BITS bits of the slot index), so that
-// k_merge's concurrently running waves work inside a few MB of the table instead of all of it.
-// tile histogram (LDS) -> digit-major exclusive scan -> LDS-cursor scatter.
+// K2b: radix partition of the partials into RP_BINS bins (kernels.h: one bin per (window, region)), so that
+// one merge workgroup owns each region: tile histogram (LDS) -> digit-major exclusive scan -> LDS-cursor
+// scatter.  Records are one 64-B line each, so the scattered writes are whole lines.
 // =====================================================================================================
 constexpr int RP_BITS = 12;
 constexpr int RP_BINS = 1 << RP_BITS;
 constexpr int RP_TILE = 65536;         // partials per tile (one workgroup)
 constexpr int RP_THREADS = 256;
 
-__device__ __forceinline__ unsigned rp_digit(const TilePartial &p, unsigned long long mask, int shift) {
-    return (unsigned)((tile_hash(p.cell, p.wstart) & mask) >> shift);
+__device__ __forceinline__ unsigned rp_digit(const TilePartial &p, const GenCache &C, const GenDesc *gm, bool &bad) {
+    const int b = bin_of_c(C, gm, p.cell, p.wstart);
+    bad |= b < 0;
+    return b < 0 ? 0u : (unsigned)b;
 }
 
-__global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const TilePartial *__restrict__ parts, int64_t n,
-                                                       unsigned long long mask, int shift, unsigned *__restrict__ H,
-                                                       int64_t ntiles) {
+__global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const TilePartial *__restrict__ parts, int64_t n, const GenDesc *gm,
+                                                       const GenDesc *glist, int n_glist, unsigned *__restrict__ H,
+                                                       int64_t ntiles, DevStats *st) {
     __shared__ unsigned h[RP_BINS];
+    __shared__ GenCache C;
+    gc_load(C, glist, n_glist);
     for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) h[d] = 0;
     __syncthreads();
     int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
     int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
-    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) atomicAdd(&h[rp_digit(parts[i], mask, shift)], 1u);
+    bool bad = false;
+    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) atomicAdd(&h[rp_digit(parts[i], C, gm, bad)], 1u);
     __syncthreads();
     for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) H[(int64_t)d * ntiles + blockIdx.x] = h[d];
+    if (__ballot(bad) && lane_id() == 0) atomicAdd(&st->overflow, 1ull);
 }
 
 // exclusive scan of m u32 entries into u64 offsets, 3 phases; block size 1024, 4096 entries per block
@@ -401,26 +427,31 @@ __global__ __launch_bounds__(256) void k_scan_add(unsigned long long *__restrict
 }
 
 __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const TilePartial *__restrict__ parts, int64_t n,
-                                                          unsigned long long mask, int shift,
+                                                          const GenDesc *gm, const GenDesc *glist, int n_glist,
                                                           const unsigned long long *__restrict__ O, int64_t ntiles,
                                                           TilePartial *__restrict__ dst) {
     __shared__ unsigned long long cur[RP_BINS];
+    __shared__ GenCache C;
+    gc_load(C, glist, n_glist);
     for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) cur[d] = O[(int64_t)d * ntiles + blockIdx.x];
     __syncthreads();
     int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
     int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
     for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) {
         TilePartial p = parts[i];
-        unsigned long long pos = atomicAdd(&cur[rp_digit(p, mask, shift)], 1ull);
+        bool bad = false;
+        unsigned long long pos = atomicAdd(&cur[rp_digit(p, C, gm, bad)], 1ull);
         dst[pos] = p;
     }
 }
 
 // =====================================================================================================
-// K3': owner merge. One workgroup owns one table region (the partition's bins), so the state is updated with
-// plain loads/stores instead of device-scope atomics. Within a workgroup, each chunk of 256 partials is first
-// de-duplicated in LDS; empty global slots are claimed through an LDS claim set, so two keys of a chunk never
-// take the same slot; chunks are applied in order.
+// K3': owner merge. The workgroup of a bin is the only writer of the (window, region)s the partition sent it,
+// so the state is updated with plain loads/stores instead of device-scope atomics. Within a workgroup, each
+// chunk of 256 partials is first de-duplicated in LDS; free slots are claimed through an LDS claim set (keyed
+// by slot address), so two keys of a chunk never take the same slot; chunks are applied in order.
+// rehash != 0: growth (k_dump_gen records into the window's new table): created slots keep the record's
+// touched seq, nothing is marked touched for emission.
 // =====================================================================================================
 constexpr int MO_THREADS = 256;
 constexpr int MO_LSLOTS = 512;
@@ -434,7 +465,8 @@ struct MoShared {
     double ssp[MO_LSLOTS];
     double slat[MO_LSLOTS];
     double slon[MO_LSLOTS];
-    unsigned long long claim[MO_CLAIM];   // claimed global slot index + 1, 0 = free
+    unsigned long long tsq[MO_LSLOTS];    // rehash mode: the key's touched seq
+    unsigned long long claim[MO_CLAIM];   // claimed slot address, 0 = free
     unsigned short uniq[MO_THREADS];
     unsigned n_uniq;
     unsigned n_touched;                   // keys of the current bin touched for the first time this batch
@@ -447,28 +479,35 @@ __device__ __forceinline__ T ld_l2(const T *p) {   // bypass the CU's L1 (chunks
 
 __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *__restrict__ parts, int64_t n,
                                                             const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
-                                                            TileSlot *tab, unsigned long long mask, unsigned long long rmask,
-                                                            unsigned long long seq, unsigned int *touched, unsigned *bin_cnt,
-                                                            WinCount *wmap, DevStats *st) {
+                                                            GenDesc *gm, const GenDesc *glist, int n_glist,
+                                                            unsigned long long seq, int rehash, unsigned long long *touched,
+                                                            unsigned *bin_cnt, DevStats *st) {
     __shared__ MoShared S;
     __shared__ WinLds WL;
+    __shared__ GenCache C;
     wl_init(WL);
+    gc_load(C, glist, n_glist);
+    const GenSink sink{gm};
     const int t = threadIdx.x;
     unsigned long long created_cnt = 0;
     bool overflow = false;
     for (int q = t; q < MO_LSLOTS; q += MO_THREADS) { S.kc[q] = 0; S.kw[q] = 0; S.cnt[q] = 0; S.nsp[q] = 0;
-        S.ssp[q] = 0.0; S.slat[q] = 0.0; S.slon[q] = 0.0; }
+        S.ssp[q] = 0.0; S.slat[q] = 0.0; S.slon[q] = 0.0; S.tsq[q] = 0; }
     for (int q = t; q < MO_CLAIM; q += MO_THREADS) S.claim[q] = 0;
     if (t == 0) { S.n_uniq = 0; S.n_touched = 0; }
     __syncthreads();
     for (int bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
         const int64_t b0 = (int64_t)O[(int64_t)bin * ntiles];
         const int64_t b1 = bin + 1 < nbins ? (int64_t)O[(int64_t)(bin + 1) * ntiles] : n;
+        // software pipeline: the next chunk's record is loaded while this chunk is merged
+        TilePartial nxt;
+        if (b0 + t < b1) nxt = parts[b0 + t];
         for (int64_t c0 = b0; c0 < b1; c0 += MO_THREADS) {
             // 1. de-duplicate the chunk in LDS
             const int64_t i = c0 + t;
+            const TilePartial p = nxt;
+            if (i + MO_THREADS < b1) nxt = parts[i + MO_THREADS];
             if (i < b1) {
-                const TilePartial p = parts[i];
                 const unsigned long long we = wenc_of(p.wstart);
                 unsigned h = (unsigned)(mix64(tile_hash(p.cell, p.wstart)) & (MO_LSLOTS - 1));
                 for (int probe = 0; probe < MO_LSLOTS; probe++) {
@@ -485,12 +524,13 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
                 atomicAdd(&S.ssp[h], p.sspeed);
                 atomicAdd(&S.slat[h], p.slat);
                 atomicAdd(&S.slon[h], p.slon);
+                if (rehash) atomicMax(&S.tsq[h], (unsigned long long)p.reserved);
             }
             __syncthreads();
-            // 2. one lane per unique key: find its slot or claim an empty one (LDS claim set)
+            // 2. one lane per unique key: find its slot in its window's table, or claim a free one (LDS claim set)
             const unsigned nu = S.n_uniq;
             const bool active = (unsigned)t < nu;
-            long long gslot = -1;
+            TileSlot *gslot = nullptr;
             bool created = false;
             int ls = 0;
             unsigned long long c = 0, we = 0;
@@ -498,33 +538,36 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
                 ls = S.uniq[t];
                 c = S.kc[ls];
                 we = S.kw[ls];
-                const int64_t w = wdec(we);
-                unsigned long long h = tile_hash(c, w) & mask;
-                for (unsigned long long probe = 0; probe <= rmask; probe++) {
-                    const unsigned long long cc = ld_l2(&tab[h].cell);
-                    if (cc == EMPTY_CELL) {
-                        unsigned ch = (unsigned)(mix64(h) & (MO_CLAIM - 1));
-                        bool mine = false, taken = false;
-                        for (int k = 0; k < MO_CLAIM; k++) {
-                            unsigned long long o = atomicCAS(&S.claim[ch], 0ull, h + 1);
-                            if (o == 0) { mine = true; break; }
-                            if (o == h + 1) { taken = true; break; }
-                            ch = (ch + 1) & (MO_CLAIM - 1);
+                const GenDesc *g = gen_lookup(C, gm, we);
+                if (g) {
+                    TileSlot *const tab = g->tab;
+                    const unsigned long long rmask = g->rmask;
+                    unsigned long long sidx = home_slot(*g, tile_hash(c, wdec(we)));
+                    for (unsigned long long probe = 0; probe <= rmask; probe++) {
+                        TileSlot *sl = &tab[sidx];
+                        if (ld_l2(&sl->wenc) != we) {   // free for this window (never used, or an evicted window's key)
+                            const unsigned long long key = (unsigned long long)sl;
+                            unsigned ch = (unsigned)(mix64(key) & (MO_CLAIM - 1));
+                            bool mine = false;
+                            for (int k = 0; k < MO_CLAIM; k++) {
+                                unsigned long long o = atomicCAS(&S.claim[ch], 0ull, key);
+                                if (o == 0) { mine = true; break; }
+                                if (o == key) break;
+                                ch = (ch + 1) & (MO_CLAIM - 1);
+                            }
+                            if (mine) { gslot = sl; created = true; break; }
+                        } else if (ld_l2(&sl->cell) == c) {
+                            gslot = sl;
+                            break;
                         }
-                        if (mine) { gslot = (long long)h; created = true; break; }
-                        (void)taken;
-                    } else if (cc == c && ld_l2(&tab[h].wenc) == we) {
-                        gslot = (long long)h;
-                        break;
+                        sidx = next_slot(sidx, rmask);
                     }
-                    h = next_slot(h, rmask);
                 }
-                if (gslot < 0) overflow = true;
+                if (!gslot) overflow = true;
             }
-            // 3. apply (this workgroup is the only writer of the region)
+            // 3. apply (this workgroup is the only writer of these regions)
             bool first = false;
-            if (gslot >= 0) {
-                TileSlot *sl = &tab[gslot];
+            if (gslot) {
                 if (created) {
                     TileSlot v;
                     v.cell = c;
@@ -534,36 +577,37 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
                     v.sspeed = S.ssp[ls];
                     v.slat = S.slat[ls];
                     v.slon = S.slon[ls];
-                    v.touched = seq;
-                    *sl = v;
-                    first = true;
+                    v.touched = rehash ? S.tsq[ls] : seq;
+                    *gslot = v;
+                    first = !rehash;
                     created_cnt++;
                 } else {
-                    const unsigned long long tc = ld_l2(&sl->touched);
-                    first = tc != seq;
-                    sl->count = ld_l2(&sl->count) + S.cnt[ls];
+                    const unsigned long long tc = ld_l2(&gslot->touched);
+                    first = !rehash && tc != seq;
+                    gslot->count = ld_l2(&gslot->count) + S.cnt[ls];
                     if (S.nsp[ls]) {
-                        sl->nspeed = ld_l2(&sl->nspeed) + S.nsp[ls];
-                        sl->sspeed = ld_l2(&sl->sspeed) + S.ssp[ls];
+                        gslot->nspeed = ld_l2(&gslot->nspeed) + S.nsp[ls];
+                        gslot->sspeed = ld_l2(&gslot->sspeed) + S.ssp[ls];
                     }
-                    sl->slat = ld_l2(&sl->slat) + S.slat[ls];
-                    sl->slon = ld_l2(&sl->slon) + S.slon[ls];
-                    if (first) sl->touched = seq;
+                    gslot->slat = ld_l2(&gslot->slat) + S.slat[ls];
+                    gslot->slon = ld_l2(&gslot->slon) + S.slon[ls];
+                    if (first) gslot->touched = seq;
                 }
             }
-            if (!wave_count_windows(created, we, WL, wmap)) overflow = true;
+            // created keys count for their window (rehash: the host already carries the moved keys)
+            if (!wave_count_windows(created && !rehash, we, 1ull, WL, sink)) overflow = true;
             // the bin's touched keys go to its own segment [b0, b0 + n) of the list (an LDS counter, no global atomic)
             const unsigned long long fb = __ballot(first);
             unsigned tbase = 0;
             if (lane_id() == 0 && fb) tbase = atomicAdd(&S.n_touched, (unsigned)__popcll(fb));
             tbase = __shfl(tbase, 0, 64);
-            if (first) touched[b0 + tbase + (unsigned)__popcll(fb & ((1ull << lane_id()) - 1))] = (unsigned int)gslot;
+            if (first) touched[b0 + tbase + (unsigned)__popcll(fb & ((1ull << lane_id()) - 1))] = (unsigned long long)gslot;
             // 4. make this chunk's stores visible to the next chunk's probes, reset the LDS tables
             __threadfence_block();
             __syncthreads();
             if (active) {
                 S.kc[ls] = 0; S.kw[ls] = 0; S.cnt[ls] = 0; S.nsp[ls] = 0;
-                S.ssp[ls] = 0.0; S.slat[ls] = 0.0; S.slon[ls] = 0.0;
+                S.ssp[ls] = 0.0; S.slat[ls] = 0.0; S.slon[ls] = 0.0; S.tsq[ls] = 0;
             }
             for (int q = t; q < MO_CLAIM; q += MO_THREADS) S.claim[q] = 0;
             if (t == 0) S.n_uniq = 0;
@@ -572,7 +616,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
         if (t == 0) { bin_cnt[bin] = S.n_touched; S.n_touched = 0; }
         __syncthreads();
     }
-    if (!wl_flush(WL, wmap)) overflow = true;
+    if (!wl_flush(WL, sink)) overflow = true;
     created_cnt = wave_sum(created_cnt);
     unsigned long long ov = __ballot(overflow);
     if (lane_id() == 0) {
@@ -595,8 +639,9 @@ __device__ __forceinline__ void emit_row(const TileSlot &s, int64_t t, uint64_t 
     o_lon[t] = s.slon / (double)s.count;
     o_lat[t] = s.slat / (double)s.count;
 }
-// after k_merge_owned: bin b's touched keys are touched[seg0(b), seg0(b) + cnt[b]), its rows go to off[b]...
-__global__ __launch_bounds__(256) void k_emit_bins(const TileSlot *__restrict__ tab, const unsigned int *__restrict__ touched,
+// after k_merge_owned: bin b's touched keys (slot addresses) are touched[seg0(b), seg0(b) + cnt[b]), its rows go
+// to off[b]...
+__global__ __launch_bounds__(256) void k_emit_bins(const unsigned long long *__restrict__ touched,
                                                    const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
                                                    const unsigned *__restrict__ cnt, const unsigned long long *__restrict__ off,
                                                    uint64_t *o_cell, int64_t *o_ws, int64_t *o_cnt, double *o_sp,
@@ -606,64 +651,7 @@ __global__ __launch_bounds__(256) void k_emit_bins(const TileSlot *__restrict__ 
         const int64_t o = (int64_t)off[bin];
         const unsigned c = cnt[bin];
         for (unsigned k = threadIdx.x; k < c; k += blockDim.x)
-            emit_row(tab[touched[seg + k]], o + k, o_cell, o_ws, o_cnt, o_sp, o_spnull, o_lon, o_lat);
-    }
-}
-
-// =====================================================================================================
-__global__ __launch_bounds__(256) void k_emit(const TileSlot *__restrict__ tab, const unsigned int *__restrict__ touched,
-                                              const unsigned long long *n_touched, uint64_t *o_cell, int64_t *o_ws,
-                                              int64_t *o_cnt, double *o_sp, uint8_t *o_spnull, double *o_lon, double *o_lat) {
-    const int64_t n = (int64_t)*n_touched;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += stride) {
-        emit_row(tab[touched[t]], t, o_cell, o_ws, o_cnt, o_sp, o_spnull, o_lon, o_lat);
-    }
-}
-
-// =====================================================================================================
-// state maintenance: rehash (grow) + evict (window end <= watermark)
-// =====================================================================================================
-// compaction into a cleared table: keep keys whose window end is after keep_end_us (dead keys -- evicted by an
-// earlier batch's watermark -- are dropped) and rebuild the window map
-__global__ __launch_bounds__(256) void k_rehash(const TileSlot *__restrict__ old, unsigned long long old_cap, TileSlot *nt,
-                                                unsigned long long new_mask, unsigned long long new_rmask, int64_t tile_us,
-                                                int64_t keep_end_us, WinCount *wmap, DevStats *st) {
-    __shared__ WinLds WL;
-    wl_init(WL);
-    __syncthreads();
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    unsigned long long kept = 0;
-    bool overflow = false;
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < (int64_t)old_cap; base += stride) {
-        int64_t i = base + threadIdx.x;
-        bool keep = false;
-        unsigned long long we = 0;
-        if (i < (int64_t)old_cap) {
-            TileSlot s = old[i];
-            we = s.wenc;
-            if (s.cell != EMPTY_CELL && we != 0 && wdec(we) + tile_us > keep_end_us) {
-                bool created;
-                long long h = find_or_claim_tile(nt, new_mask, new_rmask, s.cell, wdec(we), created);
-                if (h < 0) {
-                    overflow = true;
-                } else {
-                    s.touched = 0;
-                    nt[h] = s;
-                    keep = true;
-                    kept++;
-                }
-            }
-        }
-        if (!wave_count_windows(keep, we, WL, wmap)) overflow = true;
-    }
-    __syncthreads();
-    if (!wl_flush(WL, wmap)) overflow = true;
-    kept = wave_sum(kept);
-    unsigned long long ov = __ballot(overflow);
-    if (lane_id() == 0) {
-        if (kept) atomicAdd(&st->n_state_new, kept);
-        if (ov) atomicAdd(&st->overflow, 1ull);
+            emit_row(*(const TileSlot *)touched[seg + k], o + k, o_cell, o_ws, o_cnt, o_sp, o_spnull, o_lon, o_lat);
     }
 }
 
@@ -788,8 +776,12 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     const uint64_t *__restrict__ vkey, int64_t n, int res, int64_t tile_us, int64_t late_end_us,
     uint8_t *__restrict__ flags_out, TilePartial *__restrict__ out, DedupSlot *dtab, unsigned long long dmask,
     unsigned int *dused, unsigned long long *n_dused, unsigned int *__restrict__ slow, unsigned long long *n_slow,
-    DevStats *st) {
+    WinCount *cmap, DevStats *st) {
     __shared__ LaShared S;
+    __shared__ WinLds WL;
+    wl_init(WL);
+    const CensusSink census{cmap};
+    bool census_ok = true;
     for (int s = threadIdx.x; s < LA_SLOTS; s += LA_THREADS) {
         S.cell[s] = EMPTY_CELL;
         S.w[s] = EMPTY_WIN;
@@ -803,6 +795,9 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     unsigned long long nvalid = 0, nlate = 0, bad = 0;
     long long mx = INT64_MIN;
     bool dretry = false;
+#ifdef HM_ABL_NOAGG
+    unsigned long long abl_sink = 0;
+#endif
     const int64_t nchunks = (n + LA_CHUNK - 1) / LA_CHUNK;
     for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
         for (int q = 0; q < LA_CHUNK / LA_THREADS; q++) {
@@ -835,7 +830,11 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
             }
             // cell of the aggregated rows; margin exceptions go to k_ingest_exact (exact path, own partial record)
             bool exc = false;
+#ifdef HM_ABL_NOCELL   // ablation builds (tools/ablate_ingest.sh): a hash stands in for the cell
+            if (fl & F_AGG) cell = (mix64(__builtin_bit_cast(uint64_t, la) ^ mix64(__builtin_bit_cast(uint64_t, lo))) & ~(UINT64_C(0xffff) << 48)) | (UINT64_C(1) << 59);
+#else
             if (fl & F_AGG) exc = !latLngToCellFast(la, lo, res, c_tab, cell);
+#endif
             {
                 const unsigned long long pos = wave_append(exc, n_slow);
                 if (exc) slow[pos] = (unsigned int)i;
@@ -844,7 +843,11 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
             // dedup: per-vkey max ts over the valid rows (late rows included, as in the reference's batch frame)
             bool claimed = false;
             long long dh = -1;
+#ifdef HM_ABL_NODEDUP
+            if (false) {
+#else
             if (ok) {
+#endif
                 const unsigned long long v = vkey[i];
                 if (v == EMPTY_VKEY) {
                     bad++;
@@ -861,7 +864,12 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
             const unsigned long long pos = wave_append(claimed, n_dused);
             if (claimed) dused[pos] = (unsigned int)dh;
             // LDS pre-aggregation of the window's rows
+#ifdef HM_ABL_NOAGG
+            if ((fl & F_AGG) && !exc) abl_sink ^= cell;
+            if (false) {
+#else
             if ((fl & F_AGG) && !exc) {
+#endif
                 const bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
                 const double sp = sv ? speed[i] : 0.0;
                 unsigned h = (unsigned)(tile_hash(cell, ws) & (LA_SLOTS - 1));
@@ -882,20 +890,27 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
             }
         }
         __syncthreads();
-        if (S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, out, st);
+        if (S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, out, st, WL, census, census_ok);
     }
-    if (S.occ > 0) la_flush(S, out, st);
+    if (S.occ > 0) la_flush(S, out, st, WL, census, census_ok);
+    __syncthreads();
+    census_ok &= wl_flush(WL, census);
+#ifdef HM_ABL_NOAGG
+    if (abl_sink == 42) st->pad[0] = abl_sink;
+#endif
     nvalid = wave_sum(nvalid);
     nlate = wave_sum(nlate);
     bad = wave_sum(bad);
     mx = wave_max(mx);
     const unsigned long long rt = __ballot(dretry);
+    const unsigned long long cbad = __ballot(!census_ok);
     if (lane_id() == 0) {
         if (nvalid) atomicAdd(&st->n_valid, nvalid);
         if (nlate) atomicAdd(&st->n_late, nlate);
         if (mx != INT64_MIN) atomicMax(&st->max_ts_ms, mx);
         if (bad) atomicAdd(&st->bad_vkey, bad);
         if (rt) atomicAdd(&st->dedup_retry, 1ull);
+        if (cbad) atomicAdd(&st->overflow, 1ull);
     }
 }
 
@@ -904,13 +919,19 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
                                                       const int64_t *__restrict__ ts, const double *__restrict__ speed,
                                                       const uint8_t *__restrict__ speed_valid, int res, int64_t tile_us,
                                                       const unsigned int *__restrict__ slow, const unsigned long long *n_slow,
-                                                      TilePartial *__restrict__ out, DevStats *st) {
+                                                      TilePartial *__restrict__ out, WinCount *cmap, DevStats *st) {
+    __shared__ WinLds WL;
+    wl_init(WL);
+    __syncthreads();
+    const CensusSink census{cmap};
+    bool ok = true;
     const int64_t m = (int64_t)*n_slow;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < m; base += stride) {
         const int64_t q = base + threadIdx.x;
         const bool in = q < m;
         TilePartial p;
+        p.reserved = 0;
         if (in) {
             const unsigned i = slow[q];
             const int64_t t = ts[i];
@@ -927,7 +948,11 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
         }
         const unsigned long long pos = wave_append(in, &st->n_partials);
         if (in) out[pos] = p;
+        ok &= wave_count_windows(in, in ? wenc_of(p.wstart) : 0ull, 1ull, WL, census);
     }
+    __syncthreads();
+    ok &= wl_flush(WL, census);
+    if (__ballot(!ok) && lane_id() == 0) atomicAdd(&st->overflow, 1ull);
 }
 
 // =====================================================================================================
@@ -1094,25 +1119,25 @@ struct hm_ctx {
     std::string err;
     hipEvent_t ev[8] = {};
     double timings[7] = {0, 0, 0, 0, 0, 0, 0};
-    bool force_atomic_merge = false;   // MOBHEAT_MERGE=atomic (tuning / tests): skip partition + owned merge
     // per-event
     DevBuf in_lat, in_lon, in_ts, in_speed, in_sv, in_vkey, in_rv;
     DevBuf cell, wstart, flags, win, rows, block_counts, block_offs;
     DevBuf partials, cands, parts_sorted, rp_H, rp_O, rp_btot, rp_boff;
     DevBuf slow;   // k_ingest's fast-path exceptions (event indices) for k_ingest_exact
-    // persistent tile state: open-addressing table + an equally sized compaction target (double buffer).
-    // Eviction is lazy: a key whose window end <= the eviction watermark can never be updated again (every
-    // later row of its window is dropped as late), so it stays in place, is excluded from n_state through the
-    // per-window live counts, and is dropped when the table is next compacted.
-    TileSlot *tab = nullptr, *tab_alt = nullptr;
-    unsigned long long cap = 0;
-    int64_t occ = 0;                  // non-empty slots (live + dead) since the last compaction
+    // persistent tile state: one table per live window (kernels.h: GenDesc); released tables are pooled and
+    // reused without clearing
+    struct Gen { unsigned long long wenc; TileSlot *tab; int log2cap; unsigned rbits; int64_t keys; };
+    std::vector<Gen> gens;
+    std::vector<std::pair<TileSlot *, int>> pool;   // (table, log2 slots)
+    GenDesc *d_gmap = nullptr, *h_gmap = nullptr;   // device map window -> table (host mirror)
+    GenDesc *d_glist = nullptr, *h_glist = nullptr; // the same descriptors as a dense list (kernels' LDS cache)
+    int n_glist = 0;
+    bool census_ready = false;                      // k_ingest filled d_cmap for this batch's partials
+    WinCount *d_cmap = nullptr, *h_cmap = nullptr;  // census of the current batch's partials per window
     int64_t state_size = 0;           // live keys after the last batch
-    int64_t dead_end_us = INT64_MIN;  // keys with window end <= this are dead
-    WinCount *wmap = nullptr, *h_wmap = nullptr;
-    int wmap_used = 0;
-    DevBuf touched;
-    DevBuf bin_cnt, bin_off;   // k_merge_owned: touched keys per table region, their output offsets
+    DevBuf touched;                   // slot addresses of the keys touched this batch (per-bin segments)
+    DevBuf bin_cnt, bin_off;          // k_merge_owned: touched keys per bin, their output offsets
+    DevBuf parts_regrow;              // growth: the old tables' keys as partial records
     unsigned long long seq = 0;
     // dedup table (persistent, cleared through its used list)
     DedupSlot *dtab = nullptr;
@@ -1148,6 +1173,7 @@ static std::string g_create_err;
 // 255: result count of the last ordered compaction
 constexpr int DUSED_WORD = 253;
 constexpr int SLOW_WORD = 252;   // number of k_ingest fast-path exceptions of the current batch
+constexpr int REGROW_WORD = 251; // records dumped by k_dump_gen
 
 #define HIPCHK(ctx, expr)                                                                             \
     do {                                                                                              \
@@ -1199,83 +1225,209 @@ static uint64_t next_pow2(uint64_t v) {
     return p;
 }
 
-// Region geometry of a table of `cap` slots: RP_BINS owned regions (the partition's bins) once every region
-// has >= 2^MIN_REGION_BITS slots (at load <= 1/2 the fullest of 4096 regions then stays far below full);
-// smaller tables are one region (atomic merge path only).
-constexpr int MIN_REGION_BITS = 10;
-static bool regioned(unsigned long long cap) { return (63 - __builtin_clzll(cap)) >= RP_BITS + MIN_REGION_BITS; }
-static unsigned long long region_mask(unsigned long long cap) {
-    int log2cap = 63 - __builtin_clzll(cap);
-    return regioned(cap) ? (UINT64_C(1) << (log2cap - RP_BITS)) - 1 : cap - 1;
+// ---- per-window state tables (kernels.h: GenDesc) ----
+static int ilog2(uint64_t v) { return 63 - __builtin_clzll(v); }
+
+// Geometry of a window's table for `keys` keys receiving `parts` partials per batch: load <= 1/2, regions of
+// >= 2^REGION_MIN_BITS slots, and enough regions that one merge workgroup gets <= ~16k of the window's partials
+// (a hot window with few keys is still merged in parallel).
+static void gen_geometry(const hm_ctx *ctx, int64_t keys, int64_t parts, int min_log2, int &log2cap, unsigned &rbits) {
+    int L = ilog2(next_pow2((uint64_t)std::max<int64_t>(2 * keys, 1024)));
+    if (ctx->cfg.state_capacity_hint > 0) L = std::max(L, std::min(24, ilog2(next_pow2((uint64_t)ctx->cfg.state_capacity_hint))));
+    const int want_rb = std::min(RP_BITS, ilog2(next_pow2((uint64_t)std::max<int64_t>((parts + 16383) / 16384, 1))));
+    L = std::max({L, want_rb + REGION_MIN_BITS, min_log2});
+    rbits = (unsigned)std::min(RP_BITS, L - REGION_MIN_BITS);
+    log2cap = L;
 }
 
-static int alloc_table(hm_ctx *ctx, unsigned long long cap, TileSlot **out) {
-    TileSlot *t = nullptr;
-    if (hipMalloc(&t, cap * sizeof(TileSlot)) != hipSuccess) {
-        (void)hipGetLastError();
-        return set_err(ctx, HM_E_NOMEM, "state table alloc of %llu slots failed", cap);
+// A table of >= 2^log2cap slots: the smallest pooled table of 2^log2cap or 2^(log2cap+1) slots (not cleared: see
+// kernels.h; a window whose key count sits near a power of two must not miss the pool and pay a multi-GB hipMalloc
+// every batch), else a new one zeroed once.  log2cap and rbits return the table's actual geometry.
+static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **out) {
+    int best = -1;
+    for (size_t i = 0; i < ctx->pool.size(); i++) {
+        const int l = ctx->pool[i].second;
+        if (l >= log2cap && l <= log2cap + 1 && (best < 0 || l < ctx->pool[best].second)) best = (int)i;
     }
-    HIPCHK(ctx, hipMemsetAsync(t, 0, cap * sizeof(TileSlot), ctx->stream));
+    if (best >= 0) {
+        *out = ctx->pool[best].first;
+        log2cap = ctx->pool[best].second;
+        rbits = (unsigned)std::min(RP_BITS, log2cap - REGION_MIN_BITS);
+        ctx->pool.erase(ctx->pool.begin() + best);
+        return HM_OK;
+    }
+    const size_t bytes = (size_t(1) << log2cap) * sizeof(TileSlot);
+    TileSlot *t = nullptr;
+    if (hipMalloc(&t, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        for (auto &pt : ctx->pool) (void)hipFree(pt.first);
+        ctx->pool.clear();
+        if (hipMalloc(&t, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            return set_err(ctx, HM_E_NOMEM, "state table of 2^%d slots: out of device memory", log2cap);
+        }
+    }
+    HIPCHK(ctx, hipMemsetAsync(t, 0, bytes, ctx->stream));
     *out = t;
     return HM_OK;
 }
+// (the stream must have drained every kernel that reads the table)
+static void table_release(hm_ctx *ctx, TileSlot *t, int log2cap) {
+    ctx->pool.emplace_back(t, log2cap);
+    while (ctx->pool.size() > 8) {
+        (void)hipFree(ctx->pool.front().first);
+        ctx->pool.erase(ctx->pool.begin());
+    }
+}
 
-// Make room for `incoming` new keys: compact (drop dead keys) into the alternate table when occupancy would
-// exceed 1/2 or the window map is filling up; grow both tables when the live keys alone would not fit.
-static int state_reserve(hm_ctx *ctx, int64_t incoming) {
-    bool wmap_full = ctx->wmap_used > WMAP_SLOTS * 3 / 4;
-    if (ctx->occ + incoming <= (int64_t)(ctx->cap / 2) && !wmap_full) return HM_OK;
-    unsigned long long want = ctx->cap;
-    while ((unsigned long long)(ctx->state_size + incoming) * 2 > want) want <<= 1;
-    TileSlot *dst = nullptr;
-    int rc;
-    if (want == ctx->cap) {
-        dst = ctx->tab_alt;
-        HIPCHK(ctx, hipMemsetAsync(dst, 0, want * sizeof(TileSlot), ctx->stream));
-    } else if ((rc = alloc_table(ctx, want, &dst))) {
-        return rc;
+static int gens_upload(hm_ctx *ctx) {
+    memset(ctx->h_gmap, 0, GMAP_SLOTS * sizeof(GenDesc));
+    for (const auto &g : ctx->gens) {
+        unsigned h = (unsigned)(mix64(g.wenc) & (GMAP_SLOTS - 1));
+        while (ctx->h_gmap[h].wenc) h = (h + 1) & (GMAP_SLOTS - 1);
+        GenDesc &d = ctx->h_gmap[h];
+        d.wenc = g.wenc;
+        d.tab = g.tab;
+        d.rbits = g.rbits;
+        d.rshift = (unsigned)g.log2cap - g.rbits;
+        d.rmask = (UINT64_C(1) << d.rshift) - 1;
+        d.count = (unsigned long long)g.keys;
     }
-    HIPCHK(ctx, hipMemsetAsync(ctx->wmap, 0, WMAP_SLOTS * sizeof(WinCount), ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(ctx->d_st, 0, sizeof(DevStats), ctx->stream));
-    hipLaunchKernelGGL(k_rehash, dim3(grid_for(ctx->cap, 256, 256 * 32)), dim3(256), 0, ctx->stream, ctx->tab, ctx->cap, dst,
-                       want - 1, region_mask(want), ctx->cfg.tile_us, ctx->dead_end_us, ctx->wmap, ctx->d_st);
-    HIPCHK(ctx, hipGetLastError());
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "state compaction overflow");
-    if (want == ctx->cap) {
-        std::swap(ctx->tab, ctx->tab_alt);
-    } else {
-        HIPCHK(ctx, hipFree(ctx->tab));
-        HIPCHK(ctx, hipFree(ctx->tab_alt));
-        ctx->tab = dst;
-        ctx->tab_alt = nullptr;
-        if (hipMalloc(&ctx->tab_alt, want * sizeof(TileSlot)) != hipSuccess) {
-            (void)hipGetLastError();
-            return set_err(ctx, HM_E_NOMEM, "state table alloc of %llu slots failed", want);
-        }
-        ctx->cap = want;
-        if ((rc = ensure(ctx, ctx->touched, want * sizeof(unsigned int)))) return rc;
-    }
-    ctx->occ = (int64_t)ctx->h_st->n_state_new;
-    ctx->wmap_used = 0;   // refreshed after the next merge
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_gmap, ctx->h_gmap, GMAP_SLOTS * sizeof(GenDesc), hipMemcpyHostToDevice, ctx->stream));
+    ctx->n_glist = 0;
+    for (int q = 0; q < GMAP_SLOTS; q++)
+        if (ctx->h_gmap[q].wenc) ctx->h_glist[ctx->n_glist++] = ctx->h_gmap[q];
+    if (ctx->n_glist)
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_glist, ctx->h_glist, ctx->n_glist * sizeof(GenDesc), hipMemcpyHostToDevice, ctx->stream));
     return HM_OK;
 }
 
-// After a batch: keys with window end <= the eviction watermark are dead from now on; n_state = live keys.
-static int state_account(hm_ctx *ctx, int64_t evict_wm_ms) {
-    ctx->dead_end_us = evict_wm_ms * 1000;
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_wmap, ctx->wmap, WMAP_SLOTS * sizeof(WinCount), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    int64_t live = 0;
-    int used = 0;
-    for (int i = 0; i < WMAP_SLOTS; i++) {
-        if (!ctx->h_wmap[i].wenc) continue;
-        used++;
-        if (wdec(ctx->h_wmap[i].wenc) + ctx->cfg.tile_us > ctx->dead_end_us) live += (int64_t)ctx->h_wmap[i].count;
+// radix partition of n partial records into RP_BINS bins (one per (window, region)); the sorted copy goes to
+// ctx->parts_sorted, bin b starts at rp_O[b * ntiles]
+static int partition(hm_ctx *ctx, const TilePartial *parts, int64_t n, int64_t &ntiles) {
+    ntiles = std::max<int64_t>((n + RP_TILE - 1) / RP_TILE, 1);
+    const int64_t m = (int64_t)RP_BINS * ntiles;
+    const int64_t nb = (m + SC_PER - 1) / SC_PER;
+    int rc;
+    if ((rc = ensure(ctx, ctx->parts_sorted, std::max<int64_t>(n, 1) * sizeof(TilePartial))) || (rc = ensure(ctx, ctx->rp_H, m * 4)) ||
+        (rc = ensure(ctx, ctx->rp_O, m * 8)) || (rc = ensure(ctx, ctx->rp_btot, nb * 4)) || (rc = ensure(ctx, ctx->rp_boff, nb * 8)))
+        return rc;
+    hipLaunchKernelGGL(k_rp_hist, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, (const GenDesc *)ctx->d_gmap,
+                       (const GenDesc *)ctx->d_glist, ctx->n_glist, (unsigned *)ctx->rp_H.p, ntiles, ctx->d_st);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_H.p, m,
+                       (unsigned long long *)ctx->rp_O.p, (unsigned *)ctx->rp_btot.p);
+    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_btot.p, nb,
+                       (unsigned long long *)ctx->rp_boff.p, ctx->d_scratch + 254);
+    hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, (unsigned long long *)ctx->rp_O.p, m,
+                       (const unsigned long long *)ctx->rp_boff.p);
+    hipLaunchKernelGGL(k_rp_scatter, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, (const GenDesc *)ctx->d_gmap,
+                       (const GenDesc *)ctx->d_glist, ctx->n_glist, (const unsigned long long *)ctx->rp_O.p, ntiles,
+                       (TilePartial *)ctx->parts_sorted.p);
+    HIPCHK(ctx, hipGetLastError());
+    return HM_OK;
+}
+
+static int merge_sorted(hm_ctx *ctx, int64_t n, int64_t ntiles, int rehash) {
+    int rc;
+    if ((rc = ensure(ctx, ctx->touched, std::max<int64_t>(n, 1) * 8)) || (rc = ensure(ctx, ctx->bin_cnt, RP_BINS * 4)) ||
+        (rc = ensure(ctx, ctx->bin_off, RP_BINS * 8)))
+        return rc;
+    hipLaunchKernelGGL(k_merge_owned, dim3(RP_BINS), dim3(MO_THREADS), 0, ctx->stream, (const TilePartial *)ctx->parts_sorted.p, n,
+                       (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
+                       ctx->n_glist, ctx->seq, rehash,
+                       (unsigned long long *)ctx->touched.p, (unsigned *)ctx->bin_cnt.p, ctx->d_st);
+    HIPCHK(ctx, hipGetLastError());
+    return HM_OK;
+}
+
+// Census of the batch's partials per window; give every window a table large enough for its keys after this
+// batch (new windows: a new table; windows that would pass load 1/2: a larger table, filled by dumping the
+// old one and merging the dump in rehash mode); upload the window map.
+static int gens_prepare(hm_ctx *ctx, const TilePartial *parts, int64_t n) {
+    if (!ctx->census_ready) {   // partials from other ranks (stage API): count them here
+        HIPCHK(ctx, hipMemsetAsync(ctx->d_cmap, 0, GMAP_SLOTS * sizeof(WinCount), ctx->stream));
+        hipLaunchKernelGGL(k_census, dim3(grid_for(n, 256, 256 * 8)), dim3(256), 0, ctx->stream, parts, n, ctx->d_cmap, ctx->d_st);
+        HIPCHK(ctx, hipGetLastError());
     }
+    ctx->census_ready = false;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_cmap, ctx->d_cmap, GMAP_SLOTS * sizeof(WinCount), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "more than %d windows in one batch", GMAP_SLOTS);
+    std::vector<hm_ctx::Gen> old;   // tables being replaced by larger ones
+    int rc;
+    for (int q = 0; q < GMAP_SLOTS; q++) {
+        const WinCount &w = ctx->h_cmap[q];
+        if (!w.wenc) continue;
+        const int64_t c = (int64_t)w.count;
+        auto it = std::find_if(ctx->gens.begin(), ctx->gens.end(), [&](const hm_ctx::Gen &g) { return g.wenc == w.wenc; });
+        int L;
+        unsigned rb;
+        if (it == ctx->gens.end()) {
+            gen_geometry(ctx, c, c, 0, L, rb);
+            TileSlot *t = nullptr;
+            if ((rc = table_acquire(ctx, L, rb, &t))) return rc;
+            ctx->gens.push_back({w.wenc, t, L, rb, 0});
+        } else if ((it->keys + c) * 2 > (int64_t(1) << it->log2cap)) {
+            gen_geometry(ctx, it->keys + c, c, it->log2cap + 1, L, rb);
+            TileSlot *t = nullptr;
+            if ((rc = table_acquire(ctx, L, rb, &t))) return rc;
+            old.push_back(*it);
+            it->tab = t;
+            it->log2cap = L;
+            it->rbits = rb;   // keys unchanged: the rehash merge moves them without counting
+        }
+    }
+    if ((int)ctx->gens.size() > GMAP_SLOTS / 2)
+        return set_err(ctx, HM_E_OVERFLOW, "%zu live windows exceed the window map (%d)", ctx->gens.size(), GMAP_SLOTS / 2);
+    if ((rc = gens_upload(ctx))) return rc;
+    if (!old.empty()) {
+        int64_t moved = 0;
+        for (const auto &g : old) moved += g.keys;
+        if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(moved, 1) * sizeof(TilePartial)))) return rc;
+        HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
+        for (const auto &g : old) {
+            GenDesc d{};
+            d.wenc = g.wenc;
+            d.tab = g.tab;
+            d.rbits = g.rbits;
+            d.rshift = (unsigned)g.log2cap - g.rbits;
+            d.rmask = (UINT64_C(1) << d.rshift) - 1;
+            hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
+                               (TilePartial *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD);
+        }
+        HIPCHK(ctx, hipGetLastError());
+        int64_t ntiles;
+        if ((rc = partition(ctx, (const TilePartial *)ctx->parts_regrow.p, moved, ntiles))) return rc;
+        if ((rc = merge_sorted(ctx, moved, ntiles, 1))) return rc;
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        for (const auto &g : old) table_release(ctx, g.tab, g.log2cap);
+    }
+    return HM_OK;
+}
+
+// After a batch: every window's key count from the device; windows whose end <= the eviction watermark are
+// released whole (their rows are late from now on); n_state = keys of the live windows.
+static int state_account(hm_ctx *ctx, int64_t evict_wm_ms) {
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_gmap, ctx->d_gmap, GMAP_SLOTS * sizeof(GenDesc), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    const int64_t dead_end_us = evict_wm_ms * 1000;
+    int64_t live = 0;
+    std::vector<hm_ctx::Gen> keep;
+    for (auto &g : ctx->gens) {
+        unsigned h = (unsigned)(mix64(g.wenc) & (GMAP_SLOTS - 1));
+        for (int p = 0; p < GMAP_SLOTS && ctx->h_gmap[h].wenc; p++, h = (h + 1) & (GMAP_SLOTS - 1))
+            if (ctx->h_gmap[h].wenc == g.wenc) { g.keys = (int64_t)ctx->h_gmap[h].count; break; }
+        if (wdec(g.wenc) + ctx->cfg.tile_us <= dead_end_us) {
+            table_release(ctx, g.tab, g.log2cap);
+        } else {
+            live += g.keys;
+            keep.push_back(g);
+        }
+    }
+    ctx->gens.swap(keep);
     ctx->state_size = live;
-    ctx->wmap_used = used;
     return HM_OK;
 }
 
@@ -1377,6 +1529,7 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
     if ((rc = dedup_prepare(ctx, dedup_fused_keys(ctx, n)))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_st, 0, sizeof(DevStats), ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + SLOW_WORD, 0, 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_cmap, 0, GMAP_SLOTS * sizeof(WinCount), ctx->stream));
     long long init[2] = {INT64_MIN, INT64_MAX};
     HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->max_ts_ms, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
@@ -1386,10 +1539,11 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
         hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(LA_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.sp, I.sv, I.vk,
                            n, ctx->cfg.h3_res, ctx->cfg.tile_us, late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
                            (TilePartial *)ctx->partials.p, ctx->dtab, ctx->dcap - 1, (unsigned int *)ctx->dused.p,
-                           ctx->d_scratch + DUSED_WORD, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, ctx->d_st);
+                           ctx->d_scratch + DUSED_WORD, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, ctx->d_cmap,
+                           ctx->d_st);
         hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, I.ts, I.sp, I.sv,
                            ctx->cfg.h3_res, ctx->cfg.tile_us, (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
-                           (TilePartial *)ctx->partials.p, ctx->d_st);
+                           (TilePartial *)ctx->partials.p, ctx->d_cmap, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
         ctx->dedup_dirty = true;
     }
@@ -1440,71 +1594,31 @@ static int ensure_outputs(hm_ctx *ctx, int64_t n_rows) {
 static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts) {
     int rc;
     ctx->n_partials_merged = n_parts;
-    if ((rc = state_reserve(ctx, n_parts))) return rc;
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_touched, 0, 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_state_new, 0, 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
     ctx->seq++;
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
-    // group the partials by table region so the merge works region by region
-    int log2cap = 63 - __builtin_clzll(ctx->cap);
-    if (n_parts >= (int64_t)RP_TILE && regioned(ctx->cap) && !ctx->force_atomic_merge) {
-        int64_t ntiles = (n_parts + RP_TILE - 1) / RP_TILE;
-        int64_t m = (int64_t)RP_BINS * ntiles;
-        int64_t nb = (m + SC_PER - 1) / SC_PER;
-        if ((rc = ensure(ctx, ctx->parts_sorted, n_parts * sizeof(TilePartial))) || (rc = ensure(ctx, ctx->rp_H, m * 4)) ||
-            (rc = ensure(ctx, ctx->rp_O, m * 8)) || (rc = ensure(ctx, ctx->rp_btot, nb * 4)) || (rc = ensure(ctx, ctx->rp_boff, nb * 8)))
-            return rc;
-        int shift = log2cap - RP_BITS;
-        unsigned long long mask = ctx->cap - 1;
-        hipLaunchKernelGGL(k_rp_hist, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n_parts, mask, shift,
-                           (unsigned *)ctx->rp_H.p, ntiles);
-        hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_H.p, m,
-                           (unsigned long long *)ctx->rp_O.p, (unsigned *)ctx->rp_btot.p);
-        hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_btot.p, nb,
-                           (unsigned long long *)ctx->rp_boff.p, ctx->d_scratch + 254);
-        hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, (unsigned long long *)ctx->rp_O.p, m,
-                           (const unsigned long long *)ctx->rp_boff.p);
-        hipLaunchKernelGGL(k_rp_scatter, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n_parts, mask, shift,
-                           (const unsigned long long *)ctx->rp_O.p, ntiles, (TilePartial *)ctx->parts_sorted.p);
-        HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
-        if ((rc = ensure(ctx, ctx->bin_cnt, RP_BINS * 4)) || (rc = ensure(ctx, ctx->bin_off, RP_BINS * 8))) return rc;
-        hipLaunchKernelGGL(k_merge_owned, dim3(RP_BINS), dim3(MO_THREADS), 0, ctx->stream,
-                           (const TilePartial *)ctx->parts_sorted.p, n_parts, (const unsigned long long *)ctx->rp_O.p, ntiles,
-                           RP_BINS, ctx->tab, mask, region_mask(ctx->cap), ctx->seq, (unsigned int *)ctx->touched.p,
-                           (unsigned *)ctx->bin_cnt.p, ctx->wmap, ctx->d_st);
-        HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
-        hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->bin_cnt.p, (int64_t)RP_BINS,
-                           (unsigned long long *)ctx->bin_off.p, &ctx->d_st->n_touched);
-        if ((rc = ensure_outputs(ctx, n_parts))) return rc;
-        hipLaunchKernelGGL(k_emit_bins, dim3(RP_BINS), dim3(256), 0, ctx->stream, ctx->tab, (const unsigned int *)ctx->touched.p,
-                           (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, (const unsigned *)ctx->bin_cnt.p,
-                           (const unsigned long long *)ctx->bin_off.p, (uint64_t *)ctx->o_cell.p, (int64_t *)ctx->o_ws.p,
-                           (int64_t *)ctx->o_cnt.p, (double *)ctx->o_sp.p, (uint8_t *)ctx->o_spn.p, (double *)ctx->o_lon.p,
-                           (double *)ctx->o_lat.p);
-        HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
-        return HM_OK;
-    } else {
-        HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
-        if (n_parts > 0) {
-            hipLaunchKernelGGL(k_merge, dim3(grid_for(n_parts, 256)), dim3(256), 0, ctx->stream, parts, n_parts, ctx->tab,
-                               ctx->cap - 1, region_mask(ctx->cap), ctx->seq, (unsigned int *)ctx->touched.p, ctx->wmap,
-                               ctx->d_st);
-            HIPCHK(ctx, hipGetLastError());
-        }
-    }
-    HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
     if ((rc = ensure_outputs(ctx, n_parts))) return rc;
-    if (n_parts > 0) {
-        hipLaunchKernelGGL(k_emit, dim3(grid_for(n_parts, 256)), dim3(256), 0, ctx->stream, ctx->tab,
-                           (const unsigned int *)ctx->touched.p, &ctx->d_st->n_touched, (uint64_t *)ctx->o_cell.p,
-                           (int64_t *)ctx->o_ws.p, (int64_t *)ctx->o_cnt.p, (double *)ctx->o_sp.p, (uint8_t *)ctx->o_spn.p,
-                           (double *)ctx->o_lon.p, (double *)ctx->o_lat.p);
-        HIPCHK(ctx, hipGetLastError());
+    if (n_parts == 0) {
+        for (int e : {7, 4, 5}) HIPCHK(ctx, hipEventRecord(ctx->ev[e], ctx->stream));
+        return HM_OK;
     }
+    // census + window tables, then the partition into (window, region) bins
+    if ((rc = gens_prepare(ctx, parts, n_parts))) return rc;
+    int64_t ntiles;
+    if ((rc = partition(ctx, parts, n_parts, ntiles))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
+    if ((rc = merge_sorted(ctx, n_parts, ntiles, 0))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->bin_cnt.p, (int64_t)RP_BINS,
+                       (unsigned long long *)ctx->bin_off.p, &ctx->d_st->n_touched);
+    hipLaunchKernelGGL(k_emit_bins, dim3(RP_BINS), dim3(256), 0, ctx->stream, (const unsigned long long *)ctx->touched.p,
+                       (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, (const unsigned *)ctx->bin_cnt.p,
+                       (const unsigned long long *)ctx->bin_off.p, (uint64_t *)ctx->o_cell.p, (int64_t *)ctx->o_ws.p,
+                       (int64_t *)ctx->o_cnt.p, (double *)ctx->o_sp.p, (uint8_t *)ctx->o_spn.p, (double *)ctx->o_lon.p,
+                       (double *)ctx->o_lat.p);
+    HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
     return HM_OK;
 }
@@ -1617,7 +1731,6 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     hm_ctx *ctx = new hm_ctx();
     ctx->cfg = *cfg;
     ctx->device = cfg->device;
-    if (const char *mm = getenv("MOBHEAT_MERGE")) ctx->force_atomic_merge = strcmp(mm, "atomic") == 0;
     auto fail = [&](const char *what) {
         g_create_err = std::string(what) + ": " + ctx->err;
         hm_destroy(ctx);
@@ -1644,19 +1757,16 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         return fail("create");
     }
     if (hipMemset(ctx->d_scratch, 0, 256 * 8) != hipSuccess) { ctx->err = "scratch init"; return fail("create"); }
-    unsigned long long cap = next_pow2((unsigned long long)std::max<int64_t>(cfg->state_capacity_hint, 1 << 16));
-    if (alloc_table(ctx, cap, &ctx->tab) || hipMalloc(&ctx->tab_alt, cap * sizeof(TileSlot)) != hipSuccess) {
-        if (ctx->err.empty()) ctx->err = "state table alloc";
-        return fail("create");
-    }
-    ctx->cap = cap;
-    if (hipMalloc(&ctx->wmap, WMAP_SLOTS * sizeof(WinCount)) != hipSuccess ||
-        hipHostMalloc(&ctx->h_wmap, WMAP_SLOTS * sizeof(WinCount), hipHostMallocDefault) != hipSuccess ||
-        hipMemset(ctx->wmap, 0, WMAP_SLOTS * sizeof(WinCount)) != hipSuccess) {
+    if (hipMalloc(&ctx->d_gmap, GMAP_SLOTS * sizeof(GenDesc)) != hipSuccess ||
+        hipHostMalloc(&ctx->h_gmap, GMAP_SLOTS * sizeof(GenDesc), hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&ctx->d_cmap, GMAP_SLOTS * sizeof(WinCount)) != hipSuccess ||
+        hipMalloc(&ctx->d_glist, GMAP_SLOTS * sizeof(GenDesc)) != hipSuccess ||
+        hipHostMalloc(&ctx->h_glist, GMAP_SLOTS * sizeof(GenDesc), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&ctx->h_cmap, GMAP_SLOTS * sizeof(WinCount), hipHostMallocDefault) != hipSuccess ||
+        hipMemset(ctx->d_gmap, 0, GMAP_SLOTS * sizeof(GenDesc)) != hipSuccess) {
         ctx->err = "window map alloc";
         return fail("create");
     }
-    if (ensure(ctx, ctx->touched, cap * sizeof(unsigned int))) return fail("create");
     if (cfg->batch_capacity_hint > 0) {
         if (dedup_prepare(ctx, cfg->batch_capacity_hint)) return fail("create");
     }
@@ -1671,15 +1781,20 @@ void hm_destroy(hm_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     DevBuf *bufs[] = {&ctx->in_lat, &ctx->in_lon, &ctx->in_ts, &ctx->in_speed, &ctx->in_sv, &ctx->in_vkey, &ctx->in_rv,
                       &ctx->cell, &ctx->wstart, &ctx->flags, &ctx->win, &ctx->rows, &ctx->block_counts, &ctx->block_offs,
-                      &ctx->partials, &ctx->cands, &ctx->slow,
+                      &ctx->partials, &ctx->cands, &ctx->slow, &ctx->parts_sorted, &ctx->parts_regrow, &ctx->rp_H, &ctx->rp_O,
+                      &ctx->rp_btot, &ctx->rp_boff,
                       &ctx->touched, &ctx->bin_cnt, &ctx->bin_off, &ctx->dused, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
                       &ctx->o_lon, &ctx->o_lat};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
-    if (ctx->tab) (void)hipFree(ctx->tab);
-    if (ctx->tab_alt) (void)hipFree(ctx->tab_alt);
-    if (ctx->wmap) (void)hipFree(ctx->wmap);
-    if (ctx->h_wmap) (void)hipHostFree(ctx->h_wmap);
+    for (auto &g : ctx->gens) (void)hipFree(g.tab);
+    for (auto &pt : ctx->pool) (void)hipFree(pt.first);
+    if (ctx->d_gmap) (void)hipFree(ctx->d_gmap);
+    if (ctx->h_gmap) (void)hipHostFree(ctx->h_gmap);
+    if (ctx->d_cmap) (void)hipFree(ctx->d_cmap);
+    if (ctx->d_glist) (void)hipFree(ctx->d_glist);
+    if (ctx->h_glist) (void)hipHostFree(ctx->h_glist);
+    if (ctx->h_cmap) (void)hipHostFree(ctx->h_cmap);
     if (ctx->dtab) (void)hipFree(ctx->dtab);
     void *hbufs[] = {ctx->h_cell, ctx->h_ws, ctx->h_cnt, ctx->h_sp, ctx->h_spn, ctx->h_lon, ctx->h_lat, ctx->h_rows};
     for (void *p : hbufs)
@@ -1718,6 +1833,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
     // 2. snap + local pre-aggregation
     if ((rc = phase_local(ctx, I, late_wm))) return rc;
+    ctx->census_ready = true;   // k_ingest counted its own partials per window (the merge's input here)
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     DevStats s1 = *ctx->h_st;
@@ -1734,7 +1850,6 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     DevStats s2 = *ctx->h_st;
     if (s2.overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     if (s2.bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved (%llu rows)", s2.bad_vkey);
-    ctx->occ += (int64_t)s2.n_state_new;
     int64_t n_rows = (int64_t)ctx->h_scratch[255];
     record_timings(ctx);
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, n_rows, (const int64_t *)ctx->rows.p, out_memory, out))) return rc;
@@ -1897,7 +2012,6 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, 
         HIPCHK(ctx, hipGetLastError());
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    ctx->occ += (int64_t)s2.n_state_new;
     record_timings(ctx);
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, 0, nullptr, out_memory, out))) return rc;
     if ((rc = state_account(ctx, ctx->wm_cur))) return rc;

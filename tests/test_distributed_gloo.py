@@ -17,7 +17,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 TILE_DT = np.dtype([("cell", "<u8"), ("ws", "<i8"), ("count", "<i8"), ("nsp", "<i8"), ("ssp", "<f8"), ("slat", "<f8"),
-                    ("slon", "<f8")])
+                    ("slon", "<f8"), ("reserved", "<u8")])   # HM_TILE_REC_BYTES = 64
 CAND_DT = np.dtype([("vkey", "<u8"), ("ts", "<i8"), ("row", "<i8"), ("origin", "<i8")])
 
 

@@ -291,23 +291,36 @@ def test_foreach_batch_func_capture_sink():
     assert sorted(op._filter["_id"] for op in pos) == sorted(f"mbta|v{r:05d}" for r in exp["latest_rows"])
 
 
-def test_owned_and_atomic_merge_paths_agree(monkeypatch):
-    """The region-owned merge (regioned table, >= 64k partials) and the atomic merge (small table, and forced
-    on a regioned table) must give the oracle's result on duplicate-heavy clustered data, over batches that
-    update existing keys."""
+def test_window_tables_growth_many_windows_and_reuse():
+    """Per-window state tables: a window whose keys outgrow its table across batches (dump + rehash merge),
+    a hot window with few keys and many partials, a batch spanning 300 windows (300 tables), and a long run
+    of advancing batches whose evicted windows' tables are reused uncleared by later windows."""
     from mobheat import HeatmapEngine, synth
     from oracle.spark_oracle import SparkHeatmapOracle
     rng = np.random.default_rng(21)
-    engines = [HeatmapEngine(h3_res=10, state_capacity_hint=1 << 16), HeatmapEngine(h3_res=10, state_capacity_hint=1 << 23)]
-    monkeypatch.setenv("MOBHEAT_MERGE", "atomic")
-    engines.append(HeatmapEngine(h3_res=10, state_capacity_hint=1 << 23))
-    monkeypatch.delenv("MOBHEAT_MERGE")
-    oracles = [SparkHeatmapOracle(h3_res=10) for _ in engines]
-    for epoch, start in enumerate((0, 4, 8)):
-        b = synth.c3_city(seed=30 + epoch, n=2_000_000, hotspots=500, n_vehicles=3000)
-        b["ts_us"] = synth.T0 + start * 60_000_000 + rng.integers(0, 8 * 60_000_000, b["lat"].size)
-        for eng, ora in zip(engines, oracles):
-            res, exp = _run(eng, ora, b, epoch)
-            assert_batch_equal(res, exp)
-    for e in engines:
-        e.close()
+    eng = HeatmapEngine(h3_res=12)
+    ora = SparkHeatmapOracle(h3_res=12)
+    minute = 60_000_000
+    plan = [
+        # (n, lat/lon box km, start minute, span minutes): window [0,5) grows from ~5k to ~250k keys
+        (5_000, 5.0, 0, 4), (60_000, 20.0, 0, 4), (400_000, 40.0, 1, 3),
+        # 300 windows in one batch, then advancing batches that evict and reuse tables
+        (300_000, 10.0, 2, 1500), (50_000, 10.0, 1500, 10), (50_000, 10.0, 1510, 10), (80_000, 30.0, 1520, 10),
+        (80_000, 30.0, 1530, 10), (2_000, 0.5, 1540, 4),
+    ]
+    for epoch, (n, km, start, span) in enumerate(plan):
+        lat = 37.98 + rng.uniform(-0.5, 0.5, n) * km / 111.0
+        lon = 23.73 + rng.uniform(-0.5, 0.5, n) * km / 88.0
+        ts = synth.T0 + start * minute + rng.integers(0, span * minute, n)
+        b = dict(lat=lat, lon=lon, ts_us=ts, speed=rng.uniform(0, 90, n), speed_valid=rng.random(n) > 0.1,
+                 vkey=rng.integers(0, 4000, n).astype(np.uint64), row_valid=None)
+        res, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res, exp)
+    # hot window: 200 keys, 2M events -> many partials of few keys
+    n = 2_000_000
+    lat = 37.98 + rng.integers(0, 200, n) * 1e-3
+    b = dict(lat=lat, lon=np.full(n, 23.73), ts_us=synth.T0 + 1560 * minute + rng.integers(0, 4 * minute, n),
+             speed=rng.uniform(0, 90, n), speed_valid=None, vkey=rng.integers(0, 4000, n).astype(np.uint64), row_valid=None)
+    res, exp = _run(eng, ora, b, len(plan))
+    assert_batch_equal(res, exp)
+    eng.close()
