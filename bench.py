@@ -107,10 +107,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # (ranks beyond the visible GPUs share them round-robin: lets a 1-GPU box rehearse the N>1 path)
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL ("nccl") over xGMI; MOBHEAT_DIST_BACKEND=gloo only to rehearse several ranks on one GPU (RCCL
+        # refuses two ranks on one device)
+        backend = os.environ.get("MOBHEAT_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
 
     import mobheat
     from mobheat.distributed import LibStages, ShardedHeatmap
