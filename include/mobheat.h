@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 3
+#define HM_ABI_VERSION 4
 
 /* error codes */
 #define HM_OK 0
@@ -122,8 +122,9 @@ int hm_latlng_to_cell(const double *lat, const double *lon, int64_t n, int32_t r
 /* ---- multi-GPU stage API (one context per GPU/rank; the caller performs the exchanges) ----
  * Record layouts (little endian, packed):
  *   tile partial  (64 B): u64 cell, i64 window_start_us, i64 count, i64 n_speed, f64 sum_speed,
- *                         f64 sum_lat, f64 sum_lon, u64 reserved (0; pads the record to one 64-B line so that
- *                         scattered records are whole-line writes)
+ *                         f64 sum_lat, f64 sum_lon, u64 key_hash (the producer's hash of (cell, window_start),
+ *                         which routes the record to its owner rank and state region; the 8 B also pad the
+ *                         record to one 64-B line so that scattered records are whole-line writes)
  *   latest cand.  (32 B): u64 vkey, i64 ts_us, i64 row, i64 origin_rank
  * All exchange buffers are caller-owned device memory (e.g. torch tensors handed to RCCL), sized in records.
  * 1. hm_stage_local: snap + filter + window + local pre-aggregation + local latest candidates; both record

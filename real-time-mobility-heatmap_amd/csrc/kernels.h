@@ -38,7 +38,7 @@ struct alignas(64) TilePartial {
     double sspeed;
     double slat;
     double slon;
-    uint64_t reserved;
+    uint64_t aux;   // tile_hash(cell, wstart), computed once by the producer; growth records: the slot's touched word
 };
 static_assert(sizeof(TilePartial) == 64, "TilePartial is 64 B");
 
@@ -60,21 +60,27 @@ HM_HD int64_t wdec(unsigned long long e) { return (int64_t)(e ^ (UINT64_C(1) << 
 // is w's.  (Safe because a window never returns once evicted -- its rows are late from then on -- and a
 // growing window only moves to larger tables, never back into one that still holds its stale keys.)
 // A table of 2^L slots is split into 2^rbits regions of >= 256 slots; a key's region is taken from hash bits
-// [20, 32) and its slot from the low bits, linear probing wraps inside the region.  The radix partition
-// sends all partials of (window, region) to ONE bin = (region << (12 - rbits)) | (window salt), so the merge
-// workgroup of a bin is the only writer of the regions it receives.
+// [19, 32) and its slot from the low bits, linear probing wraps inside the region.  The radix partition
+// sends all partials of (window, region) to ONE bin = (region << (REGION_BITS - rbits)) | (window salt), so the
+// merge workgroup of a bin is the only writer of the regions it receives.
 constexpr int GMAP_SLOTS = 4096;        // live windows per context (open addressing by wenc)
 constexpr int REGION_MIN_BITS = 8;      // >= 256 slots per region (overflow-free at load <= 1/2)
+constexpr int REGION_BITS = 13;         // at most 2^13 regions per table = radix bins of the partition
 struct GenDesc {
     unsigned long long wenc;   // 0 = empty map slot
     TileSlot *tab;
     unsigned long long rmask;  // slots per region - 1
     unsigned int rshift;       // log2(slots per region)
-    unsigned int rbits;        // log2(regions), <= 12
+    unsigned int rbits;        // log2(regions), <= REGION_BITS
     unsigned long long count;  // keys of this window in its table (the merge adds created keys)
-    unsigned long long pad;
+    unsigned long long batch_parts;   // partials of the current batch in this window (0: not merged into now)
 };
 static_assert(sizeof(GenDesc) == 48, "GenDesc is 48 B");
+// Every table of 2^L slots is followed by 2^L one-byte slot tags (0 = empty, else tag8 of the key's hash), zeroed
+// whenever the table is (re)acquired.  The owner merge keeps a region's tags in LDS, so finding a free slot for a
+// new key reads nothing from HBM and an occupied slot is read only when its tag matches (1/255 of mismatches).
+HM_HD uint8_t *gen_tags(const GenDesc &g) { return (uint8_t *)(g.tab + ((g.rmask + 1) << g.rbits)); }
+HM_HD unsigned tag8(uint64_t h) { const unsigned t = (unsigned)(h >> 40) & 0xffu; return t ? t : 1u; }
 
 // partial count per window of a batch (the census that sizes the tables)
 struct WinCount {
@@ -116,8 +122,8 @@ HM_HD uint64_t tile_hash(uint64_t cell, int64_t w) { return mix64(cell ^ mix64((
 HM_HD uint64_t vkey_hash(uint64_t v) { return mix64(v ^ UINT64_C(0x2545f4914f6cdd1d)); }
 // owner rank of a key: taken from high hash bits so it is independent of the table index bits
 HM_HD int owner_of(uint64_t h, int nranks) { return (int)(((h >> 32) * (uint64_t)nranks) >> 32); }
-// a key's 12-bit region field (independent of the table size and of the owner bits)
-HM_HD unsigned region_field(uint64_t h) { return (unsigned)(h >> 20) & 4095u; }
+// a key's REGION_BITS-bit region field, hash bits [19, 32) (independent of the table size and of the owner bits)
+HM_HD unsigned region_field(uint64_t h) { return (unsigned)(h >> 19) & ((1u << REGION_BITS) - 1); }
 HM_HD unsigned window_salt(unsigned long long we) { return (unsigned)mix64(we ^ UINT64_C(0x51ed270b27e5b3c1)); }
 
 }  // namespace hm

@@ -7,11 +7,13 @@
 //                 (cell, windowStart) -> count, n_speed, sum speed/lat/lon into 64-B partial records
 //                 (Spark's partial HashAggregate, :112-123)
 //   [multi-GPU: partials partitioned by owner rank, exchanged by the caller with RCCL all-to-all]
-//   k_census      partials per window -> sizes each window's state table (kernels.h: GenDesc)
+//   k_census      partials per window -> sizes each window's state table (kernels.h: GenDesc); on one GPU
+//                 k_ingest counts its own partials and this pass is skipped
 //   k_rp_*        radix partition of the partials into one bin per (window, table region)
 //   k_merge_owned one workgroup per bin merges its partials into the persistent per-window state tables
-//                 (update mode, :243; Spark's StateStoreRestore/Save), marking touched keys
-//   k_emit_bins   touched keys -> output rows with cumulative count/avg (:124-132)
+//                 (update mode, :243; Spark's StateStoreRestore/Save) with the regions' slot tags in LDS, and
+//                 writes each touched key's cumulative output row (:124-132) into the bin's row segment
+//   k_rows_compact  the per-bin row segments -> dense update-mode rows
 //   eviction      (watermark, :107) releases a window's whole table; k_dump_gen + a rehash merge grow one
 //   k_dedup_flag  latest position per (provider, vehicleId): rows whose ts equals the max (:204-207)
 //
@@ -84,7 +86,7 @@ __device__ __forceinline__ int gmap_find(const GenDesc *gm, unsigned long long w
     return -1;
 }
 __device__ __forceinline__ unsigned long long home_slot(const GenDesc &g, uint64_t h) {
-    return ((unsigned long long)(region_field(h) >> (12 - g.rbits)) << g.rshift) | (h & g.rmask);
+    return ((unsigned long long)(region_field(h) >> (REGION_BITS - g.rbits)) << g.rshift) | (h & g.rmask);
 }
 // linear probing wraps inside the key's region
 __device__ __forceinline__ unsigned long long next_slot(unsigned long long s, unsigned long long rmask) {
@@ -112,14 +114,14 @@ __device__ __forceinline__ const GenDesc *gen_lookup(const GenCache &C, const Ge
     const int g = gmap_find(gm, we);
     return g < 0 ? nullptr : &gm[g];
 }
-// radix bin of a key: every partial of one (window, region) lands in one bin; -1 if the window has no table
-__device__ __forceinline__ int bin_of_c(const GenCache &C, const GenDesc *gm, uint64_t cell, int64_t w) {
+// radix bin of a key (hash h): every partial of one (window, region) lands in one bin; -1 if the window has no table
+__device__ __forceinline__ int bin_of_c(const GenCache &C, const GenDesc *gm, uint64_t h, int64_t w) {
     const unsigned long long we = wenc_of(w);
     const GenDesc *g = gen_lookup(C, gm, we);
     if (!g) return -1;
-    const unsigned rb = g->rbits;
-    const unsigned reg = region_field(tile_hash(cell, w)) >> (12 - rb);
-    return (int)((reg << (12 - rb)) | (window_salt(we) & ((1u << (12 - rb)) - 1)));
+    const unsigned sb = REGION_BITS - g->rbits;
+    const unsigned reg = region_field(h) >> sb;
+    return (int)((reg << sb) | (window_salt(we) & ((1u << sb) - 1)));
 }
 
 // census map: partial count per window (open addressing; counts added by one atomic per window per workgroup)
@@ -297,9 +299,9 @@ __device__ void la_flush(LaShared &S, TilePartial *out, DevStats *st, WinLds &WL
         ok &= wave_count_windows(present, wenc_of(S.w[s]), 1ull, WL, census);   // census for the merge
         if (present) {
             TilePartial p;
-            p.reserved = 0;
             p.cell = S.cell[s];
             p.wstart = S.w[s];
+            p.aux = tile_hash(p.cell, p.wstart);
             p.count = (int64_t)(S.cnt[s] & 0xffffffffull);
             p.nspeed = (int64_t)(S.cnt[s] >> 32);
             p.sspeed = S.ssp[s];
@@ -337,7 +339,7 @@ __global__ __launch_bounds__(256) void k_census(const TilePartial *__restrict__ 
     if (__ballot(!ok) && lane_id() == 0) atomicAdd(&st->overflow, 1ull);
 }
 
-// growth: the live keys of one window's old table as partial records (reserved = the key's touched seq), to be
+// growth: the live keys of one window's old table as partial records (aux = the key's touched word), to be
 // merged into its new table by k_merge_owned in rehash mode
 __global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, TilePartial *__restrict__ out, unsigned long long *n_out) {
     const unsigned long long cap = (g.rmask + 1) << g.rbits;
@@ -356,7 +358,7 @@ __global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, TilePartial *__rest
             p.sspeed = sl.sspeed;
             p.slat = sl.slat;
             p.slon = sl.slon;
-            p.reserved = sl.touched;
+            p.aux = sl.touched;
         }
         const unsigned long long pos = wave_append(live, n_out);
         if (live) out[pos] = p;
@@ -368,19 +370,20 @@ __global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, TilePartial *__rest
 // one merge workgroup owns each region: tile histogram (LDS) -> digit-major exclusive scan -> LDS-cursor
 // scatter.  Records are one 64-B line each, so the scattered writes are whole lines.
 // =====================================================================================================
-constexpr int RP_BITS = 12;
+constexpr int RP_BITS = REGION_BITS;
 constexpr int RP_BINS = 1 << RP_BITS;
 constexpr int RP_TILE = 65536;         // partials per tile (one workgroup)
 constexpr int RP_THREADS = 256;
 
-__device__ __forceinline__ unsigned rp_digit(const TilePartial &p, const GenCache &C, const GenDesc *gm, bool &bad) {
-    const int b = bin_of_c(C, gm, p.cell, p.wstart);
+// aux_hash: the records carry their key hash in aux (not growth records)
+__device__ __forceinline__ unsigned rp_digit(const TilePartial &p, const GenCache &C, const GenDesc *gm, bool aux_hash, bool &bad) {
+    const int b = bin_of_c(C, gm, aux_hash ? p.aux : tile_hash(p.cell, p.wstart), p.wstart);
     bad |= b < 0;
     return b < 0 ? 0u : (unsigned)b;
 }
 
 __global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const TilePartial *__restrict__ parts, int64_t n, const GenDesc *gm,
-                                                       const GenDesc *glist, int n_glist, unsigned *__restrict__ H,
+                                                       const GenDesc *glist, int n_glist, int aux_hash, unsigned *__restrict__ H,
                                                        int64_t ntiles, DevStats *st) {
     __shared__ unsigned h[RP_BINS];
     __shared__ GenCache C;
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const TilePartial *__res
     int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
     int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
     bool bad = false;
-    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) atomicAdd(&h[rp_digit(parts[i], C, gm, bad)], 1u);
+    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) atomicAdd(&h[rp_digit(parts[i], C, gm, aux_hash, bad)], 1u);
     __syncthreads();
     for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) H[(int64_t)d * ntiles + blockIdx.x] = h[d];
     if (__ballot(bad) && lane_id() == 0) atomicAdd(&st->overflow, 1ull);
@@ -427,35 +430,48 @@ __global__ __launch_bounds__(256) void k_scan_add(unsigned long long *__restrict
 }
 
 __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const TilePartial *__restrict__ parts, int64_t n,
-                                                          const GenDesc *gm, const GenDesc *glist, int n_glist,
+                                                          const GenDesc *gm, const GenDesc *glist, int n_glist, int aux_hash,
                                                           const unsigned long long *__restrict__ O, int64_t ntiles,
                                                           TilePartial *__restrict__ dst) {
-    __shared__ unsigned long long cur[RP_BINS];
+    __shared__ unsigned cur[RP_BINS];   // positions < 2^32 (partition() checks n)
     __shared__ GenCache C;
     gc_load(C, glist, n_glist);
-    for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) cur[d] = O[(int64_t)d * ntiles + blockIdx.x];
+    for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
     __syncthreads();
     int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
     int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
     for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) {
         TilePartial p = parts[i];
         bool bad = false;
-        unsigned long long pos = atomicAdd(&cur[rp_digit(p, C, gm, bad)], 1ull);
+        const unsigned pos = atomicAdd(&cur[rp_digit(p, C, gm, aux_hash, bad)], 1u);
         dst[pos] = p;
     }
 }
 
 // =====================================================================================================
-// K3': owner merge. The workgroup of a bin is the only writer of the (window, region)s the partition sent it,
-// so the state is updated with plain loads/stores instead of device-scope atomics. Within a workgroup, each
-// chunk of 256 partials is first de-duplicated in LDS; free slots are claimed through an LDS claim set (keyed
-// by slot address), so two keys of a chunk never take the same slot; chunks are applied in order.
-// rehash != 0: growth (k_dump_gen records into the window's new table): created slots keep the record's
-// touched seq, nothing is marked touched for emission.
+// K3': owner merge + emission. The workgroup of a bin is the only writer of the (window, region)s the partition
+// sent it, so the state is updated with plain loads/stores instead of device-scope atomics. Each chunk of 256
+// partials is first de-duplicated in LDS; then one lane per unique key finds its slot:
+//  * resident windows (the bin's regions of the windows this batch merges into, while their tags fit in
+//    MO_TAG_BYTES of LDS): probing runs over the region's slot tags in LDS and a free slot is claimed with an
+//    LDS CAS on its tag -- a new key reads nothing from HBM; an occupied slot is read only on a tag match;
+//  * other windows (too many/too large regions, or growth): probing reads the slots' window words from HBM and
+//    free slots are claimed through an LDS claim set keyed by slot address; the tag byte is stored to HBM.
+// The update-mode output row of a key (cumulative count/avg, heatmap_stream.py:124-132,243) is written at its
+// first touch in the batch to row b0 + k of the bin's segment (b0 = the bin's first partial, k = touch order
+// in the bin; the slot's `touched` word keeps (batch seq, k)), and rewritten in place when a later chunk
+// updates the key again; k_rows_compact closes the gaps left by keys that had several partials.
+// rehash != 0: growth (k_dump_gen records into the window's new table): created slots keep the record's touched
+// word, no rows are written.
 // =====================================================================================================
 constexpr int MO_THREADS = 256;
 constexpr int MO_LSLOTS = 512;
-constexpr int MO_CLAIM = 1024;
+constexpr int MO_CLAIM = 512;
+#ifndef HM_MO_TAG_BYTES
+#define HM_MO_TAG_BYTES 32768
+#endif
+constexpr int MO_TAG_BYTES = HM_MO_TAG_BYTES;   // LDS for resident region tags per workgroup
+constexpr int MO_RES_MAX = 8;                    // resident (window, region)s per bin
 
 struct MoShared {
     unsigned long long kc[MO_LSLOTS];
@@ -465,11 +481,22 @@ struct MoShared {
     double ssp[MO_LSLOTS];
     double slat[MO_LSLOTS];
     double slon[MO_LSLOTS];
-    unsigned long long tsq[MO_LSLOTS];    // rehash mode: the key's touched seq
-    unsigned long long claim[MO_CLAIM];   // claimed slot address, 0 = free
+    unsigned long long tsq[MO_LSLOTS];    // rehash mode: the key's touched word
+    unsigned long long kh[MO_LSLOTS];     // the key's tile_hash
+    unsigned long long claim[MO_CLAIM];   // claimed slot address, 0 = free (non-resident windows)
     unsigned short uniq[MO_THREADS];
     unsigned n_uniq;
     unsigned n_touched;                   // keys of the current bin touched for the first time this batch
+    unsigned claim_used;                  // the claim set holds entries of this chunk
+    int n_res;
+    unsigned res_new[MO_RES_MAX];         // keys created in the resident region this bin
+    unsigned long long res_we[MO_RES_MAX];
+    TileSlot *res_slots[MO_RES_MAX];      // the region's first slot
+    uint8_t *res_gtags[MO_RES_MAX];       // the region's tags in HBM
+    unsigned res_off[MO_RES_MAX];         // byte offset of the region's tags in `tags`
+    unsigned res_mask[MO_RES_MAX];        // slots per region - 1
+    unsigned res_dirty[MO_RES_MAX];
+    unsigned tags[MO_TAG_BYTES / 4];
 };
 
 template <typename T>
@@ -477,10 +504,33 @@ __device__ __forceinline__ T ld_l2(const T *p) {   // bypass the CU's L1 (chunks
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+struct RowsOut {   // update-mode output rows (SoA), heatmap_stream.py:124-132
+    uint64_t *cell;
+    int64_t *ws;
+    int64_t *cnt;
+    double *sp;
+    uint8_t *spnull;
+    double *lon;
+    double *lat;
+};
+// Spark Average: sum / count (count of non-null inputs) as double; null when that count is 0
+__device__ __forceinline__ void put_row(const RowsOut &o, int64_t t, uint64_t cell, unsigned long long we,
+                                        unsigned long long count, unsigned long long nspeed, double sspeed, double slat,
+                                        double slon) {
+    o.cell[t] = cell;
+    o.ws[t] = wdec(we);
+    o.cnt[t] = (int64_t)count;
+    const bool null_sp = nspeed == 0;
+    o.sp[t] = null_sp ? 0.0 : sspeed / (double)nspeed;
+    o.spnull[t] = null_sp;
+    o.lon[t] = slon / (double)count;
+    o.lat[t] = slat / (double)count;
+}
+
 __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *__restrict__ parts, int64_t n,
                                                             const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
                                                             GenDesc *gm, const GenDesc *glist, int n_glist,
-                                                            unsigned long long seq, int rehash, unsigned long long *touched,
+                                                            unsigned seq, int rehash, RowsOut rows,
                                                             unsigned *bin_cnt, DevStats *st) {
     __shared__ MoShared S;
     __shared__ WinLds WL;
@@ -494,11 +544,45 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
     for (int q = t; q < MO_LSLOTS; q += MO_THREADS) { S.kc[q] = 0; S.kw[q] = 0; S.cnt[q] = 0; S.nsp[q] = 0;
         S.ssp[q] = 0.0; S.slat[q] = 0.0; S.slon[q] = 0.0; S.tsq[q] = 0; }
     for (int q = t; q < MO_CLAIM; q += MO_THREADS) S.claim[q] = 0;
-    if (t == 0) { S.n_uniq = 0; S.n_touched = 0; }
+    if (t == 0) { S.n_uniq = 0; S.n_touched = 0; S.claim_used = 0; }
     __syncthreads();
     for (int bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
         const int64_t b0 = (int64_t)O[(int64_t)bin * ntiles];
         const int64_t b1 = bin + 1 < nbins ? (int64_t)O[(int64_t)(bin + 1) * ntiles] : n;
+        // 0. the bin's resident regions: windows merged into this batch whose region maps to this bin
+        if (t == 0) {
+            int nr = 0;
+            unsigned off = 0;
+            if (!rehash && C.n >= 0 && b1 > b0) {
+                for (int q = 0; q < C.n; q++) {
+                    const GenDesc &g = C.e[q];
+                    if (!g.batch_parts) continue;
+                    const unsigned sb = REGION_BITS - g.rbits, smask = (1u << sb) - 1;
+                    if (((unsigned)bin & smask) != (window_salt(g.wenc) & smask)) continue;
+                    const unsigned slots = (unsigned)g.rmask + 1;
+                    if (nr == MO_RES_MAX || off + slots > (unsigned)MO_TAG_BYTES) continue;
+                    const unsigned long long first = (unsigned long long)((unsigned)bin >> sb) << g.rshift;
+                    S.res_we[nr] = g.wenc;
+                    S.res_slots[nr] = g.tab + first;
+                    S.res_gtags[nr] = gen_tags(g) + first;
+                    S.res_off[nr] = off;
+                    S.res_mask[nr] = slots - 1;
+                    S.res_dirty[nr] = 0;
+                    S.res_new[nr] = 0;
+                    off += slots;
+                    nr++;
+                }
+            }
+            S.n_res = nr;
+        }
+        __syncthreads();
+        const int nres = S.n_res;
+        for (int r = 0; r < nres; r++) {
+            const unsigned *src = (const unsigned *)S.res_gtags[r];
+            const unsigned w0 = S.res_off[r] >> 2, nw = (S.res_mask[r] + 1) >> 2;
+            for (unsigned q = t; q < nw; q += MO_THREADS) S.tags[w0 + q] = src[q];
+        }
+        __syncthreads();
         // software pipeline: the next chunk's record is loaded while this chunk is merged
         TilePartial nxt;
         if (b0 + t < b1) nxt = parts[b0 + t];
@@ -509,12 +593,13 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
             if (i + MO_THREADS < b1) nxt = parts[i + MO_THREADS];
             if (i < b1) {
                 const unsigned long long we = wenc_of(p.wstart);
-                unsigned h = (unsigned)(mix64(tile_hash(p.cell, p.wstart)) & (MO_LSLOTS - 1));
+                const uint64_t hk = rehash ? tile_hash(p.cell, p.wstart) : p.aux;
+                unsigned h = (unsigned)(hk >> 48) & (MO_LSLOTS - 1);   // bits apart from region/slot/tag/owner
                 for (int probe = 0; probe < MO_LSLOTS; probe++) {
                     unsigned long long oc = atomicCAS(&S.kc[h], 0ull, (unsigned long long)p.cell);
                     if (oc == 0 || oc == p.cell) {
                         unsigned long long ow = atomicCAS(&S.kw[h], 0ull, we);
-                        if (ow == 0) { unsigned k = atomicAdd(&S.n_uniq, 1u); S.uniq[k] = (unsigned short)h; }
+                        if (ow == 0) { unsigned k = atomicAdd(&S.n_uniq, 1u); S.uniq[k] = (unsigned short)h; S.kh[h] = hk; }
                         if (ow == 0 || ow == we) break;
                     }
                     h = (h + 1) & (MO_LSLOTS - 1);
@@ -524,94 +609,147 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
                 atomicAdd(&S.ssp[h], p.sspeed);
                 atomicAdd(&S.slat[h], p.slat);
                 atomicAdd(&S.slon[h], p.slon);
-                if (rehash) atomicMax(&S.tsq[h], (unsigned long long)p.reserved);
+                if (rehash) S.tsq[h] = p.aux;   // growth records are unique keys
             }
             __syncthreads();
-            // 2. one lane per unique key: find its slot in its window's table, or claim a free one (LDS claim set)
+            // 2. one lane per unique key: find its slot in its window's table, or claim a free one
             const unsigned nu = S.n_uniq;
             const bool active = (unsigned)t < nu;
             TileSlot *gslot = nullptr;
             bool created = false;
-            int ls = 0;
+            int ls = 0, r = -1;
             unsigned long long c = 0, we = 0;
             if (active) {
                 ls = S.uniq[t];
                 c = S.kc[ls];
                 we = S.kw[ls];
-                const GenDesc *g = gen_lookup(C, gm, we);
-                if (g) {
-                    TileSlot *const tab = g->tab;
-                    const unsigned long long rmask = g->rmask;
-                    unsigned long long sidx = home_slot(*g, tile_hash(c, wdec(we)));
-                    for (unsigned long long probe = 0; probe <= rmask; probe++) {
-                        TileSlot *sl = &tab[sidx];
-                        if (ld_l2(&sl->wenc) != we) {   // free for this window (never used, or an evicted window's key)
-                            const unsigned long long key = (unsigned long long)sl;
-                            unsigned ch = (unsigned)(mix64(key) & (MO_CLAIM - 1));
-                            bool mine = false;
-                            for (int k = 0; k < MO_CLAIM; k++) {
-                                unsigned long long o = atomicCAS(&S.claim[ch], 0ull, key);
-                                if (o == 0) { mine = true; break; }
-                                if (o == key) break;
-                                ch = (ch + 1) & (MO_CLAIM - 1);
-                            }
-                            if (mine) { gslot = sl; created = true; break; }
-                        } else if (ld_l2(&sl->cell) == c) {
-                            gslot = sl;
-                            break;
+                const uint64_t hk = S.kh[ls];
+                const unsigned tg = tag8(hk);
+                for (int q = 0; q < nres; q++)
+                    if (S.res_we[q] == we) r = q;
+                if (r >= 0) {
+                    const unsigned rmask = S.res_mask[r], off = S.res_off[r];
+                    TileSlot *const base = S.res_slots[r];
+                    unsigned s = (unsigned)hk & rmask;
+                    for (unsigned probe = 0; probe <= rmask; probe++) {
+                        const unsigned bi = off + s, sh = (bi & 3) * 8;
+                        unsigned *const wp = &S.tags[bi >> 2];
+                        unsigned w = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        unsigned b = (w >> sh) & 0xffu;
+                        while (b == 0) {   // free: claim it (another lane may be claiming a neighbour in the word)
+                            const unsigned o = atomicCAS(wp, w, w | (tg << sh));
+                            if (o == w) { created = true; break; }
+                            w = o;
+                            b = (w >> sh) & 0xffu;
                         }
-                        sidx = next_slot(sidx, rmask);
+                        if (created) { gslot = base + s; S.res_dirty[r] = 1; atomicAdd(&S.res_new[r], 1u); break; }
+                        if (b == tg) {
+                            TileSlot *sl = base + s;
+                            if (ld_l2(&sl->cell) == c && ld_l2(&sl->wenc) == we) { gslot = sl; break; }
+                        }
+                        s = (s + 1) & rmask;
+                    }
+                } else {
+                    const GenDesc *g = gen_lookup(C, gm, we);
+                    if (g) {
+                        S.claim_used = 1;
+                        TileSlot *const tab = g->tab;
+                        const unsigned long long rmask = g->rmask;
+                        unsigned long long sidx = home_slot(*g, hk);
+                        for (unsigned long long probe = 0; probe <= rmask; probe++) {
+                            TileSlot *sl = &tab[sidx];
+                            if (ld_l2(&sl->wenc) != we) {   // free for this window (never used, or another window's key)
+                                const unsigned long long key = (unsigned long long)sl;
+                                unsigned ch = (unsigned)(mix64(key) & (MO_CLAIM - 1));
+                                bool mine = false;
+                                for (int k = 0; k < MO_CLAIM; k++) {
+                                    unsigned long long o = atomicCAS(&S.claim[ch], 0ull, key);
+                                    if (o == 0) { mine = true; break; }
+                                    if (o == key) break;
+                                    ch = (ch + 1) & (MO_CLAIM - 1);
+                                }
+                                if (mine) { gslot = sl; created = true; gen_tags(*g)[sidx] = (uint8_t)tg; break; }
+                            } else if (ld_l2(&sl->cell) == c) {
+                                gslot = sl;
+                                break;
+                            }
+                            sidx = next_slot(sidx, rmask);
+                        }
                     }
                 }
                 if (!gslot) overflow = true;
             }
-            // 3. apply (this workgroup is the only writer of these regions)
-            bool first = false;
-            if (gslot) {
-                if (created) {
-                    TileSlot v;
-                    v.cell = c;
-                    v.wenc = we;
-                    v.count = S.cnt[ls];
-                    v.nspeed = S.nsp[ls];
-                    v.sspeed = S.ssp[ls];
-                    v.slat = S.slat[ls];
-                    v.slon = S.slon[ls];
-                    v.touched = rehash ? S.tsq[ls] : seq;
-                    *gslot = v;
-                    first = !rehash;
-                    created_cnt++;
-                } else {
-                    const unsigned long long tc = ld_l2(&gslot->touched);
-                    first = !rehash && tc != seq;
-                    gslot->count = ld_l2(&gslot->count) + S.cnt[ls];
-                    if (S.nsp[ls]) {
-                        gslot->nspeed = ld_l2(&gslot->nspeed) + S.nsp[ls];
-                        gslot->sspeed = ld_l2(&gslot->sspeed) + S.ssp[ls];
-                    }
-                    gslot->slat = ld_l2(&gslot->slat) + S.slat[ls];
-                    gslot->slon = ld_l2(&gslot->slon) + S.slon[ls];
-                    if (first) gslot->touched = seq;
-                }
+            // 3. apply (this workgroup is the only writer of these regions) and write the key's output row
+            unsigned long long ocnt = 0, onsp = 0, tc = 0;
+            double ossp = 0.0, oslat = 0.0, oslon = 0.0;
+            if (gslot && !created) {
+                tc = ld_l2(&gslot->touched);
+                ocnt = ld_l2(&gslot->count);
+                onsp = ld_l2(&gslot->nspeed);
+                ossp = ld_l2(&gslot->sspeed);
+                oslat = ld_l2(&gslot->slat);
+                oslon = ld_l2(&gslot->slon);
             }
-            // created keys count for their window (rehash: the host already carries the moved keys)
-            if (!wave_count_windows(created && !rehash, we, 1ull, WL, sink)) overflow = true;
-            // the bin's touched keys go to its own segment [b0, b0 + n) of the list (an LDS counter, no global atomic)
+            const bool retouch = !rehash && gslot && !created && (unsigned)(tc >> 32) == seq;
+            const bool first = !rehash && gslot && !retouch;
             const unsigned long long fb = __ballot(first);
             unsigned tbase = 0;
             if (lane_id() == 0 && fb) tbase = atomicAdd(&S.n_touched, (unsigned)__popcll(fb));
             tbase = __shfl(tbase, 0, 64);
-            if (first) touched[b0 + tbase + (unsigned)__popcll(fb & ((1ull << lane_id()) - 1))] = (unsigned long long)gslot;
+            const unsigned krow = first ? tbase + (unsigned)__popcll(fb & ((1ull << lane_id()) - 1)) : (unsigned)tc;
+            if (gslot) {
+                TileSlot v;
+                v.cell = c;
+                v.wenc = we;
+                v.count = ocnt + S.cnt[ls];
+                v.nspeed = onsp + S.nsp[ls];
+                v.sspeed = S.nsp[ls] ? ossp + S.ssp[ls] : ossp;
+                v.slat = oslat + S.slat[ls];
+                v.slon = oslon + S.slon[ls];
+                v.touched = rehash ? S.tsq[ls] : ((unsigned long long)seq << 32) | krow;
+                if (created) {
+                    *gslot = v;
+                    created_cnt++;
+                } else {
+                    gslot->count = v.count;
+                    if (S.nsp[ls]) {
+                        gslot->nspeed = v.nspeed;
+                        gslot->sspeed = v.sspeed;
+                    }
+                    gslot->slat = v.slat;
+                    gslot->slon = v.slon;
+                    if (first) gslot->touched = v.touched;
+                }
+#ifndef HM_ABL_NOROWS
+                if (!rehash) put_row(rows, b0 + krow, c, we, v.count, v.nspeed, v.sspeed, v.slat, v.slon);
+#endif
+            }
+            // created keys of non-resident windows count for their window here (resident ones: res_new); rehash:
+            // the host already carries the moved keys
+            const bool count_here = created && !rehash && r < 0;
+            if (__ballot(count_here) && !wave_count_windows(count_here, we, 1ull, WL, sink)) overflow = true;
             // 4. make this chunk's stores visible to the next chunk's probes, reset the LDS tables
+#ifndef HM_ABL_NOFENCE
             __threadfence_block();
+#endif
             __syncthreads();
             if (active) {
                 S.kc[ls] = 0; S.kw[ls] = 0; S.cnt[ls] = 0; S.nsp[ls] = 0;
                 S.ssp[ls] = 0.0; S.slat[ls] = 0.0; S.slon[ls] = 0.0; S.tsq[ls] = 0;
             }
-            for (int q = t; q < MO_CLAIM; q += MO_THREADS) S.claim[q] = 0;
-            if (t == 0) S.n_uniq = 0;
+            if (S.claim_used)
+                for (int q = t; q < MO_CLAIM; q += MO_THREADS) S.claim[q] = 0;
             __syncthreads();
+            if (t == 0) { S.n_uniq = 0; S.claim_used = 0; }
+            __syncthreads();
+        }
+        // 5. write the resident regions' tags back
+        if (t < nres && S.res_new[t] && !gmap_add(gm, S.res_we[t], S.res_new[t])) overflow = true;
+        for (int r = 0; r < nres; r++) {
+            if (!S.res_dirty[r]) continue;
+            unsigned *dst = (unsigned *)S.res_gtags[r];
+            const unsigned w0 = S.res_off[r] >> 2, nw = (S.res_mask[r] + 1) >> 2;
+            for (unsigned q = t; q < nw; q += MO_THREADS) dst[q] = S.tags[w0 + q];
         }
         if (t == 0) { bin_cnt[bin] = S.n_touched; S.n_touched = 0; }
         __syncthreads();
@@ -626,35 +764,26 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
 }
 
 // =====================================================================================================
-// K4: emit touched keys (update-mode output rows, cumulative aggregates)
-// Spark Average: sum / count (count of non-null inputs) as double; null when that count is 0
-__device__ __forceinline__ void emit_row(const TileSlot &s, int64_t t, uint64_t *o_cell, int64_t *o_ws, int64_t *o_cnt,
-                                         double *o_sp, uint8_t *o_spnull, double *o_lon, double *o_lat) {
-    o_cell[t] = s.cell;
-    o_ws[t] = wdec(s.wenc);
-    o_cnt[t] = (int64_t)s.count;
-    bool null_sp = s.nspeed == 0;
-    o_sp[t] = null_sp ? 0.0 : s.sspeed / (double)s.nspeed;
-    o_spnull[t] = null_sp;
-    o_lon[t] = s.slon / (double)s.count;
-    o_lat[t] = s.slat / (double)s.count;
-}
-// after k_merge_owned: bin b's touched keys (slot addresses) are touched[seg0(b), seg0(b) + cnt[b]), its rows go
-// to off[b]...
-__global__ __launch_bounds__(256) void k_emit_bins(const unsigned long long *__restrict__ touched,
-                                                   const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
-                                                   const unsigned *__restrict__ cnt, const unsigned long long *__restrict__ off,
-                                                   uint64_t *o_cell, int64_t *o_ws, int64_t *o_cnt, double *o_sp,
-                                                   uint8_t *o_spnull, double *o_lon, double *o_lat) {
+// K4: close the gaps between the bins' row segments: bin b's rows [O(b), O(b) + cnt[b]) -> [off[b], ...)
+// =====================================================================================================
+__global__ __launch_bounds__(256) void k_rows_compact(RowsOut src, RowsOut dst, const unsigned long long *__restrict__ O,
+                                                      int64_t ntiles, int nbins, const unsigned *__restrict__ cnt,
+                                                      const unsigned long long *__restrict__ off) {
     for (int bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
-        const int64_t seg = (int64_t)O[(int64_t)bin * ntiles];
-        const int64_t o = (int64_t)off[bin];
+        const int64_t s0 = (int64_t)O[(int64_t)bin * ntiles];
+        const int64_t d0 = (int64_t)off[bin];
         const unsigned c = cnt[bin];
-        for (unsigned k = threadIdx.x; k < c; k += blockDim.x)
-            emit_row(*(const TileSlot *)touched[seg + k], o + k, o_cell, o_ws, o_cnt, o_sp, o_spnull, o_lon, o_lat);
+        for (unsigned k = threadIdx.x; k < c; k += blockDim.x) {
+            dst.cell[d0 + k] = src.cell[s0 + k];
+            dst.ws[d0 + k] = src.ws[s0 + k];
+            dst.cnt[d0 + k] = src.cnt[s0 + k];
+            dst.sp[d0 + k] = src.sp[s0 + k];
+            dst.spnull[d0 + k] = src.spnull[s0 + k];
+            dst.lon[d0 + k] = src.lon[s0 + k];
+            dst.lat[d0 + k] = src.lat[s0 + k];
+        }
     }
 }
-
 // =====================================================================================================
 // K5: latest position per (provider, vehicleId)
 // =====================================================================================================
@@ -931,7 +1060,6 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
         const int64_t q = base + threadIdx.x;
         const bool in = q < m;
         TilePartial p;
-        p.reserved = 0;
         if (in) {
             const unsigned i = slow[q];
             const int64_t t = ts[i];
@@ -945,6 +1073,7 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
             p.sspeed = sv ? speed[i] : 0.0;
             p.slat = lat[i];
             p.slon = lon[i];
+            p.aux = tile_hash(p.cell, p.wstart);
         }
         const unsigned long long pos = wave_append(in, &st->n_partials);
         if (in) out[pos] = p;
@@ -1039,7 +1168,7 @@ template <typename Rec>
 __device__ __forceinline__ int rec_owner(const Rec &r, int nranks);
 template <>
 __device__ __forceinline__ int rec_owner<TilePartial>(const TilePartial &r, int nranks) {
-    return owner_of(tile_hash(r.cell, r.wstart), nranks);
+    return owner_of(r.aux, nranks);   // the producer's tile_hash
 }
 template <>
 __device__ __forceinline__ int rec_owner<Cand>(const Cand &r, int nranks) {
@@ -1060,16 +1189,34 @@ __global__ __launch_bounds__(256) void k_part_count(const Rec *__restrict__ recs
     for (int r = threadIdx.x; r < nranks; r += blockDim.x)
         if (sc[r]) atomicAdd(&counts[r], sc[r]);
 }
-// scatter with per-owner cursors (order within an owner's segment is unspecified)
+// scatter with per-owner cursors (order within an owner's segment is unspecified): per tile of 4096 records,
+// LDS counts per owner, ONE global cursor reservation per (workgroup tile, owner), LDS ranks for the positions
+constexpr int PS_PER = 16;
 template <typename Rec>
 __global__ __launch_bounds__(256) void k_part_scatter(const Rec *__restrict__ recs, const unsigned long long *n_dev, int nranks,
                                                       unsigned long long *cursor, Rec *__restrict__ out) {
+    __shared__ unsigned cnt[64];
+    __shared__ unsigned long long base[64];
     const int64_t n = (int64_t)*n_dev;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        Rec r = recs[i];
-        unsigned long long p = atomicAdd(&cursor[rec_owner(r, nranks)], 1ull);
-        out[p] = r;
+    const int64_t tile = 256 * PS_PER;
+    for (int64_t t0 = (int64_t)blockIdx.x * tile; t0 < n; t0 += (int64_t)gridDim.x * tile) {
+        if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        int own[PS_PER];
+        unsigned loc[PS_PER];
+        for (int q = 0; q < PS_PER; q++) {
+            const int64_t i = t0 + q * 256 + threadIdx.x;
+            own[q] = i < n ? rec_owner(recs[i], nranks) : -1;
+            loc[q] = own[q] >= 0 ? atomicAdd(&cnt[own[q]], 1u) : 0u;
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < nranks && cnt[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], (unsigned long long)cnt[threadIdx.x]);
+        __syncthreads();
+        for (int q = 0; q < PS_PER; q++) {
+            const int64_t i = t0 + q * 256 + threadIdx.x;
+            if (own[q] >= 0) out[base[own[q]] + loc[q]] = recs[i];
+        }
+        __syncthreads();
     }
 }
 
@@ -1126,7 +1273,7 @@ struct hm_ctx {
     DevBuf slow;   // k_ingest's fast-path exceptions (event indices) for k_ingest_exact
     // persistent tile state: one table per live window (kernels.h: GenDesc); released tables are pooled and
     // reused without clearing
-    struct Gen { unsigned long long wenc; TileSlot *tab; int log2cap; unsigned rbits; int64_t keys; };
+    struct Gen { unsigned long long wenc; TileSlot *tab; int log2cap; unsigned rbits; int64_t keys; int64_t batch_parts; };
     std::vector<Gen> gens;
     std::vector<std::pair<TileSlot *, int>> pool;   // (table, log2 slots)
     GenDesc *d_gmap = nullptr, *h_gmap = nullptr;   // device map window -> table (host mirror)
@@ -1135,7 +1282,7 @@ struct hm_ctx {
     bool census_ready = false;                      // k_ingest filled d_cmap for this batch's partials
     WinCount *d_cmap = nullptr, *h_cmap = nullptr;  // census of the current batch's partials per window
     int64_t state_size = 0;           // live keys after the last batch
-    DevBuf touched;                   // slot addresses of the keys touched this batch (per-bin segments)
+    DevBuf s_cell, s_ws, s_cnt, s_sp, s_spn, s_lon, s_lat;   // k_merge_owned's rows in per-bin segments (with gaps)
     DevBuf bin_cnt, bin_off;          // k_merge_owned: touched keys per bin, their output offsets
     DevBuf parts_regrow;              // growth: the old tables' keys as partial records
     unsigned long long seq = 0;
@@ -1254,9 +1401,11 @@ static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **
         log2cap = ctx->pool[best].second;
         rbits = (unsigned)std::min(RP_BITS, log2cap - REGION_MIN_BITS);
         ctx->pool.erase(ctx->pool.begin() + best);
+        // the slots keep the previous window's keys (never matched: other wenc), the tags start empty
+        HIPCHK(ctx, hipMemsetAsync((uint8_t *)(*out + (size_t(1) << log2cap)), 0, size_t(1) << log2cap, ctx->stream));
         return HM_OK;
     }
-    const size_t bytes = (size_t(1) << log2cap) * sizeof(TileSlot);
+    const size_t bytes = (size_t(1) << log2cap) * (sizeof(TileSlot) + 1);   // slots, then one tag byte per slot
     TileSlot *t = nullptr;
     if (hipMalloc(&t, bytes) != hipSuccess) {
         (void)hipGetLastError();
@@ -1293,6 +1442,7 @@ static int gens_upload(hm_ctx *ctx) {
         d.rshift = (unsigned)g.log2cap - g.rbits;
         d.rmask = (UINT64_C(1) << d.rshift) - 1;
         d.count = (unsigned long long)g.keys;
+        d.batch_parts = (unsigned long long)g.batch_parts;
     }
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_gmap, ctx->h_gmap, GMAP_SLOTS * sizeof(GenDesc), hipMemcpyHostToDevice, ctx->stream));
     ctx->n_glist = 0;
@@ -1305,7 +1455,8 @@ static int gens_upload(hm_ctx *ctx) {
 
 // radix partition of n partial records into RP_BINS bins (one per (window, region)); the sorted copy goes to
 // ctx->parts_sorted, bin b starts at rp_O[b * ntiles]
-static int partition(hm_ctx *ctx, const TilePartial *parts, int64_t n, int64_t &ntiles) {
+static int partition(hm_ctx *ctx, const TilePartial *parts, int64_t n, int aux_hash, int64_t &ntiles) {
+    if (n > (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "%lld partial records in one merge exceed 2^32-1", (long long)n);
     ntiles = std::max<int64_t>((n + RP_TILE - 1) / RP_TILE, 1);
     const int64_t m = (int64_t)RP_BINS * ntiles;
     const int64_t nb = (m + SC_PER - 1) / SC_PER;
@@ -1314,7 +1465,7 @@ static int partition(hm_ctx *ctx, const TilePartial *parts, int64_t n, int64_t &
         (rc = ensure(ctx, ctx->rp_O, m * 8)) || (rc = ensure(ctx, ctx->rp_btot, nb * 4)) || (rc = ensure(ctx, ctx->rp_boff, nb * 8)))
         return rc;
     hipLaunchKernelGGL(k_rp_hist, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, (const GenDesc *)ctx->d_gmap,
-                       (const GenDesc *)ctx->d_glist, ctx->n_glist, (unsigned *)ctx->rp_H.p, ntiles, ctx->d_st);
+                       (const GenDesc *)ctx->d_glist, ctx->n_glist, aux_hash, (unsigned *)ctx->rp_H.p, ntiles, ctx->d_st);
     hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_H.p, m,
                        (unsigned long long *)ctx->rp_O.p, (unsigned *)ctx->rp_btot.p);
     hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_btot.p, nb,
@@ -1322,21 +1473,37 @@ static int partition(hm_ctx *ctx, const TilePartial *parts, int64_t n, int64_t &
     hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, (unsigned long long *)ctx->rp_O.p, m,
                        (const unsigned long long *)ctx->rp_boff.p);
     hipLaunchKernelGGL(k_rp_scatter, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, (const GenDesc *)ctx->d_gmap,
-                       (const GenDesc *)ctx->d_glist, ctx->n_glist, (const unsigned long long *)ctx->rp_O.p, ntiles,
+                       (const GenDesc *)ctx->d_glist, ctx->n_glist, aux_hash, (const unsigned long long *)ctx->rp_O.p, ntiles,
                        (TilePartial *)ctx->parts_sorted.p);
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
 }
 
+static RowsOut rows_of(DevBuf &cell, DevBuf &ws, DevBuf &cnt, DevBuf &sp, DevBuf &spn, DevBuf &lon, DevBuf &lat) {
+    return RowsOut{(uint64_t *)cell.p, (int64_t *)ws.p, (int64_t *)cnt.p, (double *)sp.p, (uint8_t *)spn.p,
+                   (double *)lon.p, (double *)lat.p};
+}
+static RowsOut staged_rows(hm_ctx *ctx) {
+    return rows_of(ctx->s_cell, ctx->s_ws, ctx->s_cnt, ctx->s_sp, ctx->s_spn, ctx->s_lon, ctx->s_lat);
+}
+
+// the batch sequence number kept in the slots' touched words (32 bits, never 0: fresh slots hold 0)
+static unsigned seq32(const hm_ctx *ctx) { return (unsigned)(ctx->seq % 0xffffffffull) + 1u; }
+
 static int merge_sorted(hm_ctx *ctx, int64_t n, int64_t ntiles, int rehash) {
     int rc;
-    if ((rc = ensure(ctx, ctx->touched, std::max<int64_t>(n, 1) * 8)) || (rc = ensure(ctx, ctx->bin_cnt, RP_BINS * 4)) ||
-        (rc = ensure(ctx, ctx->bin_off, RP_BINS * 8)))
+    if ((rc = ensure(ctx, ctx->bin_cnt, RP_BINS * 4)) || (rc = ensure(ctx, ctx->bin_off, RP_BINS * 8)))
         return rc;
+    if (!rehash) {
+        const int64_t m = std::max<int64_t>(n, 1);
+        if ((rc = ensure(ctx, ctx->s_cell, m * 8)) || (rc = ensure(ctx, ctx->s_ws, m * 8)) || (rc = ensure(ctx, ctx->s_cnt, m * 8)) ||
+            (rc = ensure(ctx, ctx->s_sp, m * 8)) || (rc = ensure(ctx, ctx->s_spn, m)) || (rc = ensure(ctx, ctx->s_lon, m * 8)) ||
+            (rc = ensure(ctx, ctx->s_lat, m * 8)))
+            return rc;
+    }
     hipLaunchKernelGGL(k_merge_owned, dim3(RP_BINS), dim3(MO_THREADS), 0, ctx->stream, (const TilePartial *)ctx->parts_sorted.p, n,
                        (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
-                       ctx->n_glist, ctx->seq, rehash,
-                       (unsigned long long *)ctx->touched.p, (unsigned *)ctx->bin_cnt.p, ctx->d_st);
+                       ctx->n_glist, seq32(ctx), rehash, staged_rows(ctx), (unsigned *)ctx->bin_cnt.p, ctx->d_st);
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
 }
@@ -1357,6 +1524,7 @@ static int gens_prepare(hm_ctx *ctx, const TilePartial *parts, int64_t n) {
     if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "more than %d windows in one batch", GMAP_SLOTS);
     std::vector<hm_ctx::Gen> old;   // tables being replaced by larger ones
     int rc;
+    for (auto &g : ctx->gens) g.batch_parts = 0;
     for (int q = 0; q < GMAP_SLOTS; q++) {
         const WinCount &w = ctx->h_cmap[q];
         if (!w.wenc) continue;
@@ -1368,8 +1536,10 @@ static int gens_prepare(hm_ctx *ctx, const TilePartial *parts, int64_t n) {
             gen_geometry(ctx, c, c, 0, L, rb);
             TileSlot *t = nullptr;
             if ((rc = table_acquire(ctx, L, rb, &t))) return rc;
-            ctx->gens.push_back({w.wenc, t, L, rb, 0});
-        } else if ((it->keys + c) * 2 > (int64_t(1) << it->log2cap)) {
+            ctx->gens.push_back({w.wenc, t, L, rb, 0, c});
+            continue;
+        }
+        if ((it->keys + c) * 2 > (int64_t(1) << it->log2cap)) {
             gen_geometry(ctx, it->keys + c, c, it->log2cap + 1, L, rb);
             TileSlot *t = nullptr;
             if ((rc = table_acquire(ctx, L, rb, &t))) return rc;
@@ -1378,6 +1548,7 @@ static int gens_prepare(hm_ctx *ctx, const TilePartial *parts, int64_t n) {
             it->log2cap = L;
             it->rbits = rb;   // keys unchanged: the rehash merge moves them without counting
         }
+        it->batch_parts = c;
     }
     if ((int)ctx->gens.size() > GMAP_SLOTS / 2)
         return set_err(ctx, HM_E_OVERFLOW, "%zu live windows exceed the window map (%d)", ctx->gens.size(), GMAP_SLOTS / 2);
@@ -1399,7 +1570,7 @@ static int gens_prepare(hm_ctx *ctx, const TilePartial *parts, int64_t n) {
         }
         HIPCHK(ctx, hipGetLastError());
         int64_t ntiles;
-        if ((rc = partition(ctx, (const TilePartial *)ctx->parts_regrow.p, moved, ntiles))) return rc;
+        if ((rc = partition(ctx, (const TilePartial *)ctx->parts_regrow.p, moved, 0, ntiles))) return rc;
         if ((rc = merge_sorted(ctx, moved, ntiles, 1))) return rc;
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         for (const auto &g : old) table_release(ctx, g.tab, g.log2cap);
@@ -1607,17 +1778,16 @@ static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_par
     // census + window tables, then the partition into (window, region) bins
     if ((rc = gens_prepare(ctx, parts, n_parts))) return rc;
     int64_t ntiles;
-    if ((rc = partition(ctx, parts, n_parts, ntiles))) return rc;
+    if ((rc = partition(ctx, parts, n_parts, 1, ntiles))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
     if ((rc = merge_sorted(ctx, n_parts, ntiles, 0))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
     hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->bin_cnt.p, (int64_t)RP_BINS,
                        (unsigned long long *)ctx->bin_off.p, &ctx->d_st->n_touched);
-    hipLaunchKernelGGL(k_emit_bins, dim3(RP_BINS), dim3(256), 0, ctx->stream, (const unsigned long long *)ctx->touched.p,
+    hipLaunchKernelGGL(k_rows_compact, dim3(RP_BINS), dim3(256), 0, ctx->stream, staged_rows(ctx),
+                       rows_of(ctx->o_cell, ctx->o_ws, ctx->o_cnt, ctx->o_sp, ctx->o_spn, ctx->o_lon, ctx->o_lat),
                        (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, (const unsigned *)ctx->bin_cnt.p,
-                       (const unsigned long long *)ctx->bin_off.p, (uint64_t *)ctx->o_cell.p, (int64_t *)ctx->o_ws.p,
-                       (int64_t *)ctx->o_cnt.p, (double *)ctx->o_sp.p, (uint8_t *)ctx->o_spn.p, (double *)ctx->o_lon.p,
-                       (double *)ctx->o_lat.p);
+                       (const unsigned long long *)ctx->bin_off.p);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
     return HM_OK;
@@ -1783,7 +1953,7 @@ void hm_destroy(hm_ctx *ctx) {
                       &ctx->cell, &ctx->wstart, &ctx->flags, &ctx->win, &ctx->rows, &ctx->block_counts, &ctx->block_offs,
                       &ctx->partials, &ctx->cands, &ctx->slow, &ctx->parts_sorted, &ctx->parts_regrow, &ctx->rp_H, &ctx->rp_O,
                       &ctx->rp_btot, &ctx->rp_boff,
-                      &ctx->touched, &ctx->bin_cnt, &ctx->bin_off, &ctx->dused, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
+                      &ctx->s_cell, &ctx->s_ws, &ctx->s_cnt, &ctx->s_sp, &ctx->s_spn, &ctx->s_lon, &ctx->s_lat, &ctx->bin_cnt, &ctx->bin_off, &ctx->dused, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
                       &ctx->o_lon, &ctx->o_lat};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);

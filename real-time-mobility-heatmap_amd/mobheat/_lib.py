@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MOBHEAT_LIB: load another build of the same ABI (kernel variants under csrc/variants/ for tuning runs)
 LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
 
-HM_ABI_VERSION = 3
+HM_ABI_VERSION = 4
 HM_MEM_HOST = 0
 HM_MEM_DEVICE = 1
 HM_TILE_REC_BYTES = 64

@@ -4,7 +4,7 @@ Replaces Spark's shuffle of the two aggregations (spark.sql.shuffle.partitions =
 heatmap_stream.py:44): every rank snaps and pre-aggregates its own shard of the micro-batch, then ONE
 all-to-all per record kind routes
 
-  * tile partials  (64-B records: cell, windowStart, count, n_speed, sum speed/lat/lon) to owner rank
+  * tile partials  (64-B records: cell, windowStart, count, n_speed, sum speed/lat/lon, key hash) to owner rank
     hash(cell, windowStart) % world, which merges them into the persistent state it owns and emits them;
   * latest-position candidates (32-B records: vkey, ts, row, origin rank) to owner hash(vkey) % world,
     which keeps the rows tied at the global max and routes the winning row indices back to their origin;
@@ -114,10 +114,16 @@ class ShardedHeatmap:
         return self.stages.finish(winner_recv, int(sum(wrc)), out_memory, out)
 
 
+def tile_hash(cell, wstart):
+    """Python twin of kernels.h tile_hash (the key_hash field of a tile partial record)."""
+    with np.errstate(over="ignore"):
+        return _mix64(np.asarray(cell, np.uint64) ^ _mix64(np.asarray(wstart).astype(np.uint64) +
+                                                           np.uint64(0x9E3779B97F4A7C15)))
+
+
 def tile_owner(cell, wstart, world):
     """Python twin of the device routing (kernels.h owner_of(tile_hash(...)))."""
-    return _owner(_mix64(np.asarray(cell, np.uint64) ^ _mix64(np.asarray(wstart).astype(np.uint64) +
-                                                               np.uint64(0x9E3779B97F4A7C15))), world)
+    return _owner(tile_hash(cell, wstart), world)
 
 
 def vkey_owner(vkey, world):

@@ -17,7 +17,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 TILE_DT = np.dtype([("cell", "<u8"), ("ws", "<i8"), ("count", "<i8"), ("nsp", "<i8"), ("ssp", "<f8"), ("slat", "<f8"),
-                    ("slon", "<f8"), ("reserved", "<u8")])   # HM_TILE_REC_BYTES = 64
+                    ("slon", "<f8"), ("key_hash", "<u8")])   # HM_TILE_REC_BYTES = 64
 CAND_DT = np.dtype([("vkey", "<u8"), ("ts", "<i8"), ("row", "<i8"), ("origin", "<i8")])
 
 
@@ -28,7 +28,7 @@ class OracleStages:
         self.res = res
 
     def local(self, epoch, b, world, rank):
-        from mobheat.distributed import tile_owner, vkey_owner
+        from mobheat.distributed import _owner as owner_of, tile_hash, vkey_owner
         from oracle import h3_oracle
         o = self.o
         valid = o.valid_mask(b["lat"], b["lon"], b["ts_us"], b["row_valid"])
@@ -50,7 +50,8 @@ class OracleStages:
             recs["ssp"] = np.bincount(inv[sv], weights=b["speed"][agg][sv], minlength=uq.size)
             recs["slat"] = np.bincount(inv, weights=b["lat"][agg], minlength=uq.size)
             recs["slon"] = np.bincount(inv, weights=b["lon"][agg], minlength=uq.size)
-        own = tile_owner(recs["cell"], recs["ws"], world)
+        recs["key_hash"] = tile_hash(recs["cell"], recs["ws"])
+        own = owner_of(recs["key_hash"], world)
         order = np.argsort(own, kind="stable")
         tcounts = np.bincount(own, minlength=world).tolist()
         tile_send = torch.from_numpy(recs[order].view(np.uint8).copy())
