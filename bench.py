@@ -6,9 +6,10 @@ OpenSky-like global batch of 1e8 events uniform on the sphere, 50k vehicle ids, 
 (3 five-minute windows), 10% null speeds -- at the metric's H3 resolution 8 (configs[1] quotes res 7;
 --res 7 runs that).  One step = one micro-batch through the whole hot path on device-resident inputs:
 one fused pass over the events (k_ingest: filter + latLngToCell + window + late test + LDS pre-aggregation +
-per-vehicle max ts), census of the partials per window (sizes the per-window state tables), radix partition into
-(window, region) bins, the region-owned merge into the persistent update-mode state (k_merge_owned), emission
-(k_emit_bins), eviction (whole window tables released), and the latest-position flags + compaction.
+per-vehicle max ts + census of the partials per window, which sizes the per-window state tables), radix partition
+into (window, region) bins, the region-owned merge into the persistent update-mode state that also writes the
+update-mode rows (k_merge_owned), row compaction (k_rows_compact), eviction (whole window tables released), and
+the latest-position flags + compaction.
 Every step is a NEW micro-batch: its timestamps are the previous step's + 15 min (precomputed before the
 timed region), so the stream advances, windows close and are evicted, and no row is late.
 For N>1 each rank runs the sharded path (mobheat.distributed: RCCL all-to-all of partials by owner).
@@ -36,12 +37,13 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector peak: 1024 SIMDs x 16 FMA lanes x
 SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 # algorithmic HBM bytes per unit: per event (ingest, dedup), per partial record (partition,
-# merge), per emitted tile (emit).  ingest also writes 64 B per partial (added below).
+# merge), per emitted tile (emit = the row compaction).  ingest also writes 64 B per partial (added below).
 BYTES = {
     "ingest": 43,      # read lat 8 + lon 8 + ts 8 + speed 8 + speed_valid 1 + vkey 8 + row_valid 1; write flags 1
-    "partition": 256,  # per 64-B partial: census read + histogram read + scatter read + write
-    "merge": 200,      # per partial: read 64 B record + 64 B state line read + 64 B written + 8 B touched address
-    "emit": 121,       # per emitted tile: 64 B state line + 8 B address read, 49 B row written
+    "partition": 192,  # per 64-B partial: histogram read + scatter read + scatter write
+    "merge": 177,      # per partial: read 64 B record, write the 64 B state line (a new key: its slot tag is in
+                       # LDS, nothing read) and the 49 B update-mode row
+    "emit": 98,        # per emitted tile: 49 B row read from the bin's segment, 49 B written densely
     "dedup": 20,       # per event: vkey 8 + ts 8 + flags 1 read, win flag 1 written, 2 x 1 B compaction reads
 }
 # k_ingest's HBM traffic and VALU instruction mix per event of this workload were counted by rocprofv3 PMC

@@ -372,7 +372,10 @@ __global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, TilePartial *__rest
 // =====================================================================================================
 constexpr int RP_BITS = REGION_BITS;
 constexpr int RP_BINS = 1 << RP_BITS;
-constexpr int RP_TILE = 65536;         // partials per tile (one workgroup)
+#ifndef HM_RP_TILE
+#define HM_RP_TILE 65536
+#endif
+constexpr int RP_TILE = HM_RP_TILE;    // partials per tile (one workgroup)
 constexpr int RP_THREADS = 256;
 
 // aux_hash: the records carry their key hash in aux (not growth records)
@@ -444,7 +447,14 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const TilePartial *__
         TilePartial p = parts[i];
         bool bad = false;
         const unsigned pos = atomicAdd(&cur[rp_digit(p, C, gm, aux_hash, bad)], 1u);
+#ifdef HM_RP_NT
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const v4u *src4 = (const v4u *)&p;
+        v4u *d4 = (v4u *)&dst[pos];
+        for (int q = 0; q < 4; q++) __builtin_nontemporal_store(src4[q], &d4[q]);
+#else
         dst[pos] = p;
+#endif
     }
 }
 
