@@ -161,6 +161,8 @@ int hm_memcpy(void *dst, const void *src, int64_t bytes, int32_t kind); /* 0 H2D
 /* Self-test entry (host-side execution of the device numerics; no GPU needed): evaluates the
  * extended-precision emulation used by the kernels, op codes as oracle_ld_ops(). */
 int hm_selftest_ld_ops(const double *a, int64_t n, int32_t op, double *out);
+/* floor(t[i] / d) by k_ingest's invariant-divisor multiply (kernels.h FloorDiv), executed on the host */
+int hm_selftest_floor_div(const int64_t *t, int64_t n, int64_t d, int64_t *out);
 /* Host-side execution of the device latLngToCell code path (for debugging without a GPU; uses host libm
  * for the transcendental functions, so it is NOT the device numerics). */
 int hm_selftest_latlng_to_cell_host(const double *lat, const double *lon, int64_t n, int32_t res,

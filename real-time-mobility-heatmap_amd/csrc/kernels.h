@@ -119,6 +119,41 @@ HM_HD uint64_t mix64(uint64_t x) {
     return x;
 }
 HM_HD uint64_t tile_hash(uint64_t cell, int64_t w) { return mix64(cell ^ mix64((uint64_t)w + UINT64_C(0x9e3779b97f4a7c15))); }
+// floor(t / d) for d >= 1 by an invariant-divisor multiply (Granlund & Montgomery 1994, Fig. 4.1, N = 64):
+// m = floor(2^64 (2^l - d) / d) + 1, l = ceil(log2 d); exact for every 64-bit dividend.  make_floor_div (host).
+struct FloorDiv {
+    uint64_t m;
+    int s1, s2;
+    int64_t d;
+};
+HM_HD uint64_t umulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+HM_HD uint64_t udiv_inv(uint64_t u, const FloorDiv &D) {
+    const uint64_t hi = umulhi64(D.m, u);
+    return (hi + ((u - hi) >> D.s1)) >> D.s2;
+}
+HM_HD int64_t floor_div(int64_t t, const FloorDiv &D) {
+    if (t >= 0) return (int64_t)udiv_inv((uint64_t)t, D);
+    return -(int64_t)udiv_inv((uint64_t)(-(t + 1)), D) - 1;   // floor((-1 - u) / d) = -(u / d) - 1
+}
+inline FloorDiv make_floor_div(int64_t d) {
+    FloorDiv D;
+    int l = 0;
+    while ((UINT64_C(1) << l) < (uint64_t)d && l < 63) l++;
+    if ((UINT64_C(1) << l) < (uint64_t)d) l = 64;
+    const unsigned __int128 two_l = l == 64 ? ((unsigned __int128)1 << 64) : ((unsigned __int128)1 << l);
+    D.m = (uint64_t)((((unsigned __int128)1 << 64) * (two_l - (uint64_t)d)) / (uint64_t)d + 1);
+    D.s1 = l < 1 ? l : 1;
+    D.s2 = l > 1 ? l - 1 : 0;
+    D.d = d;
+    return D;
+}
+
 HM_HD uint64_t vkey_hash(uint64_t v) { return mix64(v ^ UINT64_C(0x2545f4914f6cdd1d)); }
 // owner rank of a key: taken from high hash bits so it is independent of the table index bits
 HM_HD int owner_of(uint64_t h, int nranks) { return (int)(((h >> 32) * (uint64_t)nranks) >> 32); }

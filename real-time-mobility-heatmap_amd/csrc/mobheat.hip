@@ -253,36 +253,81 @@ constexpr int LA_THREADS = 256;
 #ifndef HM_LA_SLOTS
 #define HM_LA_SLOTS 512
 #endif
-constexpr int LA_SLOTS = HM_LA_SLOTS;  // LDS hash slots per workgroup (48 B each)
+constexpr int LA_SLOTS = HM_LA_SLOTS;  // LDS hash slots per workgroup (40 B each)
 constexpr int LA_CHUNK = LA_SLOTS / 2; // events inserted between occupancy checks
 constexpr int LA_FLUSH_AT = LA_SLOTS * 3 / 4 - LA_CHUNK;    // occupancy bound before a chunk: <= 3/4 full after
 static_assert(LA_CHUNK % LA_THREADS == 0 && LA_SLOTS % LA_THREADS == 0, "LDS table geometry");
 
+// LDS key of a (cell, window): a cell of the context's resolution has constant bits 52-63 (mode 1, reserved 0,
+// res), so its low 52 bits plus a 6-bit index into the workgroup's window table (the window starts seen since
+// the last flush) make one 64-bit key: one CAS per probe.
+constexpr int LA_WT = 64;                                   // window table slots per workgroup
+constexpr uint64_t LA_CELL_LO = (UINT64_C(1) << 52) - 1;
+constexpr uint64_t LA_EMPTY = ~UINT64_C(0);                 // never a key: a key's bits 58-63 are zero
+__device__ __forceinline__ uint64_t la_key(uint64_t cell, unsigned widx) { return (cell & LA_CELL_LO) | ((uint64_t)widx << 52); }
+__device__ __forceinline__ unsigned la_slot(uint64_t key) {
+    return (unsigned)((key * UINT64_C(0x9e3779b97f4a7c15)) >> 40) & (LA_SLOTS - 1);
+}
+
 struct LaShared {
-    unsigned long long cell[LA_SLOTS];
-    long long w[LA_SLOTS];
+    unsigned long long key[LA_SLOTS];   // la_key, LA_EMPTY = free
     unsigned long long cnt[LA_SLOTS];   // low 32: count, high 32: n_speed
     double ssp[LA_SLOTS];
     double slat[LA_SLOTS];
     double slon[LA_SLOTS];
+    long long wt[LA_WT];                // window starts (EMPTY_WIN = free)
+    unsigned wcnt[LA_WT];               // partials per window at a flush (the census)
     unsigned int occ;
     unsigned int scan[LA_THREADS / 64];
     unsigned long long base;
 };
 
-__device__ void la_flush(LaShared &S, TilePartial *out, DevStats *st, WinLds &WL, const CensusSink &census, bool &ok) {
+// index of window start ws in the workgroup's window table (inserted if new); -1 when the table is full
+__device__ __forceinline__ int la_window(LaShared &S, int64_t ws, int64_t q) {
+    unsigned h = (unsigned)q & (LA_WT - 1);   // consecutive windows -> distinct slots
+    for (int probe = 0; probe < LA_WT; probe++) {
+        long long w = S.wt[h];
+        if (w == ws) return (int)h;
+        if (w == EMPTY_WIN) {
+            w = (long long)atomicCAS((unsigned long long *)&S.wt[h], (unsigned long long)EMPTY_WIN, (unsigned long long)ws);
+            if (w == EMPTY_WIN || w == ws) return (int)h;
+        }
+        h = (h + 1) & (LA_WT - 1);
+    }
+    return -1;
+}
+
+// a row that found no window-table slot: its own partial record (rare; out of line to spare registers)
+__device__ __forceinline__ bool la_direct(TilePartial *out, DevStats *st, WinLds &WL, const CensusSink &census, uint64_t cell,
+                                       int64_t ws, bool sv, double sp, double la, double lo) {
+    TilePartial p;
+    p.cell = cell;
+    p.wstart = ws;
+    p.count = 1;
+    p.nspeed = sv;
+    p.sspeed = sp;
+    p.slat = la;
+    p.slon = lo;
+    p.aux = tile_hash(cell, ws);
+    out[atomicAdd(&st->n_partials, 1ull)] = p;
+    return wl_add(WL, census, wenc_of(ws), 1ull);
+}
+
+// partial records of the table's keys; resets the table and the window table
+__device__ void la_flush(LaShared &S, uint64_t cell_hi, TilePartial *out, DevStats *st, WinLds &WL, const CensusSink &census,
+                         bool &ok) {
     __syncthreads();
-    const int per = LA_SLOTS / LA_THREADS;  // 4
-    int t = threadIdx.x;
+    constexpr int per = LA_SLOTS / LA_THREADS;
+    const int t = threadIdx.x;
     unsigned c = 0;
-    for (int q = 0; q < per; q++) c += S.cell[t * per + q] != EMPTY_CELL;
+    for (int q = 0; q < per; q++) c += S.key[t * per + q] != LA_EMPTY;
     // block exclusive scan of c
     unsigned incl = c;
     for (int o = 1; o < 64; o <<= 1) {
         unsigned v = __shfl_up(incl, o, 64);
         if (lane_id() >= o) incl += v;
     }
-    int wv = t >> 6;
+    const int wv = t >> 6;
     if (lane_id() == 63) S.scan[wv] = incl;
     __syncthreads();
     unsigned wave_off = 0, total = 0;
@@ -294,27 +339,34 @@ __device__ void la_flush(LaShared &S, TilePartial *out, DevStats *st, WinLds &WL
     __syncthreads();
     unsigned long long pos = S.base + wave_off + incl - c;
     for (int q = 0; q < per; q++) {
-        int s = t * per + q;
-        const bool present = S.cell[s] != EMPTY_CELL;
-        ok &= wave_count_windows(present, wenc_of(S.w[s]), 1ull, WL, census);   // census for the merge
-        if (present) {
+        const int s = t * per + q;
+        const uint64_t k = S.key[s];
+        if (k != LA_EMPTY) {
+            const unsigned widx = (unsigned)(k >> 52);
             TilePartial p;
-            p.cell = S.cell[s];
-            p.wstart = S.w[s];
-            p.aux = tile_hash(p.cell, p.wstart);
+            p.cell = (k & LA_CELL_LO) | cell_hi;
+            p.wstart = S.wt[widx];
             p.count = (int64_t)(S.cnt[s] & 0xffffffffull);
             p.nspeed = (int64_t)(S.cnt[s] >> 32);
             p.sspeed = S.ssp[s];
             p.slat = S.slat[s];
             p.slon = S.slon[s];
+            p.aux = tile_hash(p.cell, p.wstart);
             out[pos++] = p;
+            atomicAdd(&S.wcnt[widx], 1u);
         }
-        S.cell[s] = EMPTY_CELL;
-        S.w[s] = EMPTY_WIN;
+        S.key[s] = LA_EMPTY;
         S.cnt[s] = 0;
         S.ssp[s] = 0.0;
         S.slat[s] = 0.0;
         S.slon[s] = 0.0;
+    }
+    __syncthreads();
+    // census of the flushed partials per window (LDS; the global map is updated once per workgroup)
+    if (t < LA_WT) {
+        if (S.wcnt[t]) ok &= wl_add(WL, census, wenc_of(S.wt[t]), (unsigned long long)S.wcnt[t]);
+        S.wcnt[t] = 0;
+        S.wt[t] = EMPTY_WIN;
     }
     if (t == 0) S.occ = 0;
     __syncthreads();
@@ -912,7 +964,7 @@ constexpr unsigned long long DEDUP_FUSED_PROBES = 256;
 __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     const double *__restrict__ lat, const double *__restrict__ lon, const int64_t *__restrict__ ts,
     const uint8_t *__restrict__ row_valid, const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
-    const uint64_t *__restrict__ vkey, int64_t n, int res, int64_t tile_us, int64_t late_end_us,
+    const uint64_t *__restrict__ vkey, int64_t n, int res, FloorDiv wdiv, int64_t late_end_us,
     uint8_t *__restrict__ flags_out, TilePartial *__restrict__ out, DedupSlot *dtab, unsigned long long dmask,
     unsigned int *dused, unsigned long long *n_dused, unsigned int *__restrict__ slow, unsigned long long *n_slow,
     WinCount *cmap, DevStats *st) {
@@ -921,18 +973,20 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     wl_init(WL);
     const CensusSink census{cmap};
     bool census_ok = true;
+    const int64_t tile_us = wdiv.d;
+    const uint64_t cell_hi = (UINT64_C(1) << 59) | ((uint64_t)res << 52);   // mode 1, reserved 0, resolution
     for (int s = threadIdx.x; s < LA_SLOTS; s += LA_THREADS) {
-        S.cell[s] = EMPTY_CELL;
-        S.w[s] = EMPTY_WIN;
+        S.key[s] = LA_EMPTY;
         S.cnt[s] = 0;
         S.ssp[s] = 0.0;
         S.slat[s] = 0.0;
         S.slon[s] = 0.0;
     }
+    for (int s = threadIdx.x; s < LA_WT; s += LA_THREADS) { S.wt[s] = EMPTY_WIN; S.wcnt[s] = 0; }
     if (threadIdx.x == 0) S.occ = 0;
     __syncthreads();
     unsigned long long nvalid = 0, nlate = 0, bad = 0;
-    long long mx = INT64_MIN;
+    long long tmax = INT64_MIN;
     bool dretry = false;
 #ifdef HM_ABL_NOAGG
     unsigned long long abl_sink = 0;
@@ -955,22 +1009,21 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
                             t > INT64_MIN + 2 * tile_us && t < INT64_MAX - 2 * tile_us;
             uint8_t fl = 0;
             uint64_t cell = EMPTY_CELL;
-            int64_t ws = EMPTY_WIN;
+            int widx = -1;   // the window's slot in the workgroup's window table (-1: table full, rare)
             if (ok) {
-                int64_t rem = t % tile_us;
-                if (rem < 0) rem += tile_us;
-                ws = t - rem;
+                const int64_t wq = floor_div(t, wdiv);   // tumbling window: floor(t / tile) (Spark TimeWindowing)
+                const int64_t ws = wq * tile_us;
                 const bool late = (ws + tile_us) <= late_end_us;
                 fl = late ? (F_VALID | F_LATE) : (F_VALID | F_AGG);
                 nvalid++;
                 nlate += late;
-                const long long ms = (long long)(t / 1000);
-                mx = ms > mx ? ms : mx;
+                tmax = t > tmax ? t : tmax;
+                if (!late) widx = la_window(S, ws, wq);   // (an exception's window stays unused: no census)
             }
             // cell of the aggregated rows; margin exceptions go to k_ingest_exact (exact path, own partial record)
             bool exc = false;
 #ifdef HM_ABL_NOCELL   // ablation builds (tools/ablate_ingest.sh): a hash stands in for the cell
-            if (fl & F_AGG) cell = (mix64(__builtin_bit_cast(uint64_t, la) ^ mix64(__builtin_bit_cast(uint64_t, lo))) & ~(UINT64_C(0xffff) << 48)) | (UINT64_C(1) << 59);
+            if (fl & F_AGG) cell = (mix64(__builtin_bit_cast(uint64_t, la) ^ mix64(__builtin_bit_cast(uint64_t, lo))) & LA_CELL_LO) | cell_hi;
 #else
             if (fl & F_AGG) exc = !latLngToCellFast(la, lo, res, c_tab, cell);
 #endif
@@ -1003,6 +1056,7 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
             const unsigned long long pos = wave_append(claimed, n_dused);
             if (claimed) dused[pos] = (unsigned int)dh;
             // LDS pre-aggregation of the window's rows
+            bool fresh = false;
 #ifdef HM_ABL_NOAGG
             if ((fl & F_AGG) && !exc) abl_sink ^= cell;
             if (false) {
@@ -1011,27 +1065,34 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
 #endif
                 const bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
                 const double sp = sv ? speed[i] : 0.0;
-                unsigned h = (unsigned)(tile_hash(cell, ws) & (LA_SLOTS - 1));
-                for (int probe = 0; probe < LA_SLOTS; probe++) {
-                    unsigned long long old = atomicCAS(&S.cell[h], (unsigned long long)EMPTY_CELL, (unsigned long long)cell);
-                    if (old == EMPTY_CELL) atomicAdd(&S.occ, 1u);
-                    if (old == EMPTY_CELL || old == cell) {
-                        long long ow = (long long)atomicCAS((unsigned long long *)&S.w[h], (unsigned long long)EMPTY_WIN,
-                                                            (unsigned long long)ws);
-                        if (ow == EMPTY_WIN || ow == ws) break;
+                if (widx >= 0) {
+                    const uint64_t key = la_key(cell, (unsigned)widx);
+                    unsigned h = la_slot(key);
+                    for (int probe = 0; probe < LA_SLOTS; probe++) {
+                        uint64_t k = __hip_atomic_load(&S.key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (k == key) break;
+                        if (k == LA_EMPTY) {
+                            k = atomicCAS(&S.key[h], LA_EMPTY, key);
+                            if (k == LA_EMPTY) { fresh = true; break; }
+                            if (k == key) break;
+                        }
+                        h = (h + 1) & (LA_SLOTS - 1);
                     }
-                    h = (h + 1) & (LA_SLOTS - 1);
+                    atomicAdd(&S.cnt[h], 1ull | ((unsigned long long)sv << 32));
+                    if (sv) atomicAdd(&S.ssp[h], sp);
+                    atomicAdd(&S.slat[h], la);
+                    atomicAdd(&S.slon[h], lo);
+                } else {   // more than LA_WT windows since the last flush: the row is its own partial record
+                    census_ok &= la_direct(out, st, WL, census, cell, floor_div(t, wdiv) * tile_us, sv, sp, la, lo);
                 }
-                atomicAdd(&S.cnt[h], 1ull | ((unsigned long long)sv << 32));
-                if (sv) atomicAdd(&S.ssp[h], sp);
-                atomicAdd(&S.slat[h], la);
-                atomicAdd(&S.slon[h], lo);
             }
+            const unsigned long long fb = __ballot(fresh);
+            if (fb && lane_id() == (unsigned)(__ffsll((long long)fb) - 1)) atomicAdd(&S.occ, (unsigned)__popcll(fb));
         }
         __syncthreads();
-        if (S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, out, st, WL, census, census_ok);
+        if (S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, cell_hi, out, st, WL, census, census_ok);
     }
-    if (S.occ > 0) la_flush(S, out, st, WL, census, census_ok);
+    if (S.occ > 0) la_flush(S, cell_hi, out, st, WL, census, census_ok);
     __syncthreads();
     census_ok &= wl_flush(WL, census);
 #ifdef HM_ABL_NOAGG
@@ -1040,13 +1101,13 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     nvalid = wave_sum(nvalid);
     nlate = wave_sum(nlate);
     bad = wave_sum(bad);
-    mx = wave_max(mx);
+    tmax = wave_max(tmax);
     const unsigned long long rt = __ballot(dretry);
     const unsigned long long cbad = __ballot(!census_ok);
     if (lane_id() == 0) {
         if (nvalid) atomicAdd(&st->n_valid, nvalid);
         if (nlate) atomicAdd(&st->n_late, nlate);
-        if (mx != INT64_MIN) atomicMax(&st->max_ts_ms, mx);
+        if (tmax != INT64_MIN) atomicMax(&st->max_ts_ms, (long long)(tmax / 1000));   // trunc(max) = max(trunc)
         if (bad) atomicAdd(&st->bad_vkey, bad);
         if (rt) atomicAdd(&st->dedup_retry, 1ull);
         if (cbad) atomicAdd(&st->overflow, 1ull);
@@ -1718,7 +1779,7 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
         int64_t nchunks = (n + LA_CHUNK - 1) / LA_CHUNK;
         int blocks = (int)std::min<int64_t>(nchunks, ctx->ingest_grid);
         hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(LA_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.sp, I.sv, I.vk,
-                           n, ctx->cfg.h3_res, ctx->cfg.tile_us, late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
+                           n, ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
                            (TilePartial *)ctx->partials.p, ctx->dtab, ctx->dcap - 1, (unsigned int *)ctx->dused.p,
                            ctx->d_scratch + DUSED_WORD, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, ctx->d_cmap,
                            ctx->d_st);
@@ -1779,14 +1840,14 @@ static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_par
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_state_new, 0, 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
     ctx->seq++;
-    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
     if ((rc = ensure_outputs(ctx, n_parts))) return rc;
     if (n_parts == 0) {
-        for (int e : {7, 4, 5}) HIPCHK(ctx, hipEventRecord(ctx->ev[e], ctx->stream));
+        for (int e : {3, 7, 4, 5}) HIPCHK(ctx, hipEventRecord(ctx->ev[e], ctx->stream));
         return HM_OK;
     }
-    // census + window tables, then the partition into (window, region) bins
+    // census + window tables (host), then the partition into (window, region) bins (timed from here)
     if ((rc = gens_prepare(ctx, parts, n_parts))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
     int64_t ntiles;
     if ((rc = partition(ctx, parts, n_parts, 1, ntiles))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
@@ -2266,6 +2327,13 @@ int hm_selftest_ld_ops(const double *a, int64_t n, int32_t op, double *out) {
         }
         out[i] = r;
     }
+    return HM_OK;
+}
+
+int hm_selftest_floor_div(const int64_t *t, int64_t n, int64_t d, int64_t *out) {
+    if (!t || !out || n < 0 || d < 1) return HM_E_INVALID;
+    const FloorDiv D = make_floor_div(d);
+    for (int64_t i = 0; i < n; i++) out[i] = floor_div(t[i], D);
     return HM_OK;
 }
 

@@ -70,6 +70,7 @@ SIGNATURES = {
     "hm_device_free": (c_i32, [c_i32, c_vp]),
     "hm_memcpy": (c_i32, [c_vp, c_vp, c_i64, c_i32]),
     "hm_selftest_ld_ops": (c_i32, [c_vp, c_i64, c_i32, c_vp]),
+    "hm_selftest_floor_div": (c_i32, [c_vp, c_i64, c_i64, c_vp]),
     "hm_selftest_latlng_to_cell_host": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp]),
     "hm_selftest_latlng_to_cell_fast_host": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
@@ -120,6 +121,15 @@ def ld_ops_selftest(a, op):
     a = np.ascontiguousarray(a, dtype=np.float64)
     out = np.empty_like(a)
     check(lib.hm_selftest_ld_ops(ptr(a), a.size, op, ptr(out)))
+    return out
+
+
+def floor_div_selftest(t, d):
+    """Host execution of k_ingest's window division floor(t / d) (kernels.h FloorDiv)."""
+    lib = load()
+    t = np.ascontiguousarray(t, dtype=np.int64)
+    out = np.empty_like(t)
+    check(lib.hm_selftest_floor_div(ptr(t), t.size, int(d), ptr(out)))
     return out
 
 

@@ -206,3 +206,22 @@ def test_fast_path_rarely_falls_back(mobheat_lib):
     for res in (0, 7, 8, 12, 15):
         _, fell_back = _lib.latlng_to_cell_fast_host_selftest(lat, lon, res)
         assert fell_back.mean() < 1e-3, (res, fell_back.mean())
+
+
+@pytest.mark.parametrize("d", [1, 2, 3, 7, 1000, 300_000_000, 60_000_000, 86_400_000_000, 2**31 - 1, 2**32 + 1,
+                               2**62 + 12345, 2**63 - 1])
+def test_window_floor_division_is_exact(d):
+    """k_ingest's tumbling-window division (Spark TimeWindowing floor-mod, heatmap_stream.py:115) by an
+    invariant-divisor multiply equals Python's exact floor division on random and edge dividends."""
+    from mobheat import _lib
+    rng = np.random.default_rng(d % 1000)
+    t = np.concatenate([
+        rng.integers(-2**63, 2**63 - 1, 20000, dtype=np.int64, endpoint=True),
+        rng.integers(-10**16, 10**16, 20000, dtype=np.int64),
+        np.array([x for x in (0, 1, -1, d - 1, d, d + 1, -d, -d - 1, -d + 1, 2**63 - 1, -2**63, -2**63 + 1, 2**62,
+                              -2**62) if -2**63 <= x < 2**63], dtype=np.int64),
+        (np.arange(-50, 50, dtype=np.int64) * (d if d < 2**56 else 1)),
+    ])
+    got = _lib.floor_div_selftest(t, d)
+    want = np.array([int(x) // d for x in t.tolist()], dtype=np.int64)
+    assert np.array_equal(got, want)
