@@ -425,7 +425,7 @@ __global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, TilePartial *__rest
 constexpr int RP_BITS = REGION_BITS;
 constexpr int RP_BINS = 1 << RP_BITS;
 #ifndef HM_RP_TILE
-#define HM_RP_TILE 65536
+#define HM_RP_TILE 131072
 #endif
 constexpr int RP_TILE = HM_RP_TILE;    // partials per tile (one workgroup)
 constexpr int RP_THREADS = 256;
@@ -493,20 +493,30 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const TilePartial *__
     gc_load(C, glist, n_glist);
     for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
     __syncthreads();
-    int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
-    int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
-    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) {
-        TilePartial p = parts[i];
-        bool bad = false;
-        const unsigned pos = atomicAdd(&cur[rp_digit(p, C, gm, aux_hash, bad)], 1u);
-#ifdef HM_RP_NT
-        typedef unsigned v4u __attribute__((ext_vector_type(4)));
-        const v4u *src4 = (const v4u *)&p;
-        v4u *d4 = (v4u *)&dst[pos];
-        for (int q = 0; q < 4; q++) __builtin_nontemporal_store(src4[q], &d4[q]);
-#else
-        dst[pos] = p;
-#endif
+    // four lanes per record, 16 B each: every load/store instruction covers 16 whole 64-B records (16 lines)
+    // instead of one line per lane, which is what bounds this kernel's vector-memory issue
+    const int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
+    const int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
+    const uint4 *__restrict__ src = (const uint4 *)parts;
+    uint4 *__restrict__ d4 = (uint4 *)dst;
+    const int q = threadIdx.x & 3, lead = (int)(lane_id() & ~3);
+    for (int64_t i = t0 + (threadIdx.x >> 2); i - (threadIdx.x >> 2) < t1; i += RP_THREADS / 4) {
+        const bool in = i < t1;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (in) v = src[i * 4 + q];
+        // the lead lane of the record gathers cell, wstart (its own quarter) and the hash (quarter 3)
+        const unsigned hz = __shfl(v.z, lead + 3, 64), hw = __shfl(v.w, lead + 3, 64);
+        unsigned pos = 0;
+        if (in && q == 0) {
+            TilePartial p;
+            p.cell = (uint64_t)v.x | ((uint64_t)v.y << 32);
+            p.wstart = (int64_t)((uint64_t)v.z | ((uint64_t)v.w << 32));
+            p.aux = (uint64_t)hz | ((uint64_t)hw << 32);
+            bool bad = false;
+            pos = atomicAdd(&cur[rp_digit(p, C, gm, aux_hash, bad)], 1u);
+        }
+        pos = __shfl(pos, lead, 64);
+        if (in) d4[(int64_t)pos * 4 + q] = v;
     }
 }
 
