@@ -522,44 +522,42 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const TilePartial *__
 
 // =====================================================================================================
 // K3': owner merge + emission. The workgroup of a bin is the only writer of the (window, region)s the partition
-// sent it, so the state is updated with plain loads/stores instead of device-scope atomics. Each chunk of 256
-// partials is first de-duplicated in LDS; then one lane per unique key finds its slot:
+// sent it, so the state is updated with plain loads/stores instead of device-scope atomics. Per chunk of 256
+// partials (one per lane), each lane finds its key's slot and claims it in an LDS claim set keyed by slot
+// address; a lane whose slot is already claimed by the same key in this chunk adds its values into the
+// claimer's LDS staging entry and is done (in-chunk de-duplication without a separate hash table):
 //  * resident windows (the bin's regions of the windows this batch merges into, while their tags fit in
-//    MO_TAG_BYTES of LDS): probing runs over the region's slot tags in LDS and a free slot is claimed with an
-//    LDS CAS on its tag -- a new key reads nothing from HBM; an occupied slot is read only on a tag match;
-//  * other windows (too many/too large regions, or growth): probing reads the slots' window words from HBM and
-//    free slots are claimed through an LDS claim set keyed by slot address; the tag byte is stored to HBM.
+//    MO_TAG_BYTES of LDS): probing runs over the region's slot tags in LDS -- a new key reads nothing from HBM;
+//    an occupied slot not claimed in this chunk is read only on a tag match;
+//  * other windows (too many/too large regions, or growth): probing reads the slots' window words from HBM;
+//    the tag byte of a created slot is stored to HBM.
 // The update-mode output row of a key (cumulative count/avg, heatmap_stream.py:124-132,243) is written at its
 // first touch in the batch to row b0 + k of the bin's segment (b0 = the bin's first partial, k = touch order
 // in the bin; the slot's `touched` word keeps (batch seq, k)), and rewritten in place when a later chunk
 // updates the key again; k_rows_compact closes the gaps left by keys that had several partials.
-// rehash != 0: growth (k_dump_gen records into the window's new table): created slots keep the record's touched
-// word, no rows are written.
+// rehash != 0: growth (k_dump_gen records, unique keys, into the window's new table): created slots keep the
+// record's touched word, no rows are written.
 // =====================================================================================================
 constexpr int MO_THREADS = 256;
-constexpr int MO_LSLOTS = 512;
 constexpr int MO_CLAIM = 512;
 #ifndef HM_MO_TAG_BYTES
-#define HM_MO_TAG_BYTES 32768
+#define HM_MO_TAG_BYTES 24576
 #endif
 constexpr int MO_TAG_BYTES = HM_MO_TAG_BYTES;   // LDS for resident region tags per workgroup
 constexpr int MO_RES_MAX = 8;                    // resident (window, region)s per bin
 
 struct MoShared {
-    unsigned long long kc[MO_LSLOTS];
-    unsigned long long kw[MO_LSLOTS];
-    unsigned long long cnt[MO_LSLOTS];
-    unsigned long long nsp[MO_LSLOTS];
-    double ssp[MO_LSLOTS];
-    double slat[MO_LSLOTS];
-    double slon[MO_LSLOTS];
-    unsigned long long tsq[MO_LSLOTS];    // rehash mode: the key's touched word
-    unsigned long long kh[MO_LSLOTS];     // the key's tile_hash
-    unsigned long long claim[MO_CLAIM];   // claimed slot address, 0 = free (non-resident windows)
-    unsigned short uniq[MO_THREADS];
-    unsigned n_uniq;
+    // this chunk's records by lane; a duplicate key's values are added into its claimer's entry
+    unsigned long long sc[MO_THREADS];
+    unsigned long long sh[MO_THREADS];
+    unsigned long long sw[MO_THREADS];
+    unsigned long long scnt[MO_THREADS];
+    unsigned long long snsp[MO_THREADS];
+    double sssp[MO_THREADS];
+    double sslat[MO_THREADS];
+    double sslon[MO_THREADS];
+    unsigned long long claim[MO_CLAIM];   // (slot address << 16) | claimer lane; 0 = free
     unsigned n_touched;                   // keys of the current bin touched for the first time this batch
-    unsigned claim_used;                  // the claim set holds entries of this chunk
     int n_res;
     unsigned res_new[MO_RES_MAX];         // keys created in the resident region this bin
     unsigned long long res_we[MO_RES_MAX];
@@ -574,6 +572,42 @@ struct MoShared {
 template <typename T>
 __device__ __forceinline__ T ld_l2(const T *p) {   // bypass the CU's L1 (chunks of one workgroup re-read slots)
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned mo_claim_home(unsigned long long addr) {
+    return (unsigned)(((addr >> 6) * UINT64_C(0x9e3779b97f4a7c15)) >> 40) & (MO_CLAIM - 1);
+}
+// claim slot `addr` for `lane`: -1 = claimed (entry index in ci), else the lane that already holds it
+__device__ __forceinline__ int mo_claim(MoShared &S, unsigned long long addr, int lane, int &ci) {
+    const unsigned long long packed = (addr << 16) | (unsigned)lane;
+    unsigned h = mo_claim_home(addr);
+    for (int k = 0; k < MO_CLAIM; k++) {
+        const unsigned long long o = atomicCAS(&S.claim[h], 0ull, packed);
+        if (o == 0) { ci = (int)h; return -1; }
+        if ((o >> 16) == addr) return (int)(o & 0xffff);
+        h = (h + 1) & (MO_CLAIM - 1);
+    }
+    return -2;
+}
+// the lane holding slot `addr` in this chunk, -1 if none
+__device__ __forceinline__ int mo_holder(MoShared &S, unsigned long long addr) {
+    unsigned h = mo_claim_home(addr);
+    for (int k = 0; k < MO_CLAIM; k++) {
+        const unsigned long long o = __hip_atomic_load(&S.claim[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (o == 0) return -1;
+        if ((o >> 16) == addr) return (int)(o & 0xffff);
+        h = (h + 1) & (MO_CLAIM - 1);
+    }
+    return -1;
+}
+// a duplicate of lane x's key: add this record's values into x's staging entry
+__device__ __forceinline__ void mo_add_into(MoShared &S, int x, const TilePartial &p) {
+    atomicAdd(&S.scnt[x], (unsigned long long)p.count);
+    if (p.nspeed) {
+        atomicAdd(&S.snsp[x], (unsigned long long)p.nspeed);
+        atomicAdd(&S.sssp[x], p.sspeed);
+    }
+    atomicAdd(&S.sslat[x], p.slat);
+    atomicAdd(&S.sslon[x], p.slon);
 }
 
 struct RowsOut {   // update-mode output rows (SoA), heatmap_stream.py:124-132
@@ -613,10 +647,8 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
     const int t = threadIdx.x;
     unsigned long long created_cnt = 0;
     bool overflow = false;
-    for (int q = t; q < MO_LSLOTS; q += MO_THREADS) { S.kc[q] = 0; S.kw[q] = 0; S.cnt[q] = 0; S.nsp[q] = 0;
-        S.ssp[q] = 0.0; S.slat[q] = 0.0; S.slon[q] = 0.0; S.tsq[q] = 0; }
     for (int q = t; q < MO_CLAIM; q += MO_THREADS) S.claim[q] = 0;
-    if (t == 0) { S.n_uniq = 0; S.n_touched = 0; S.claim_used = 0; }
+    if (t == 0) S.n_touched = 0;
     __syncthreads();
     for (int bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
         const int64_t b0 = (int64_t)O[(int64_t)bin * ntiles];
@@ -659,98 +691,95 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
         TilePartial nxt;
         if (b0 + t < b1) nxt = parts[b0 + t];
         for (int64_t c0 = b0; c0 < b1; c0 += MO_THREADS) {
-            // 1. de-duplicate the chunk in LDS
+            // 1. stage this chunk's records in LDS
             const int64_t i = c0 + t;
+            const bool has = i < b1;
             const TilePartial p = nxt;
             if (i + MO_THREADS < b1) nxt = parts[i + MO_THREADS];
-            if (i < b1) {
-                const unsigned long long we = wenc_of(p.wstart);
-                const uint64_t hk = rehash ? tile_hash(p.cell, p.wstart) : p.aux;
-                unsigned h = (unsigned)(hk >> 48) & (MO_LSLOTS - 1);   // bits apart from region/slot/tag/owner
-                for (int probe = 0; probe < MO_LSLOTS; probe++) {
-                    unsigned long long oc = atomicCAS(&S.kc[h], 0ull, (unsigned long long)p.cell);
-                    if (oc == 0 || oc == p.cell) {
-                        unsigned long long ow = atomicCAS(&S.kw[h], 0ull, we);
-                        if (ow == 0) { unsigned k = atomicAdd(&S.n_uniq, 1u); S.uniq[k] = (unsigned short)h; S.kh[h] = hk; }
-                        if (ow == 0 || ow == we) break;
-                    }
-                    h = (h + 1) & (MO_LSLOTS - 1);
-                }
-                atomicAdd(&S.cnt[h], (unsigned long long)p.count);
-                atomicAdd(&S.nsp[h], (unsigned long long)p.nspeed);
-                atomicAdd(&S.ssp[h], p.sspeed);
-                atomicAdd(&S.slat[h], p.slat);
-                atomicAdd(&S.slon[h], p.slon);
-                if (rehash) S.tsq[h] = p.aux;   // growth records are unique keys
+            const unsigned long long we = wenc_of(p.wstart);
+            const uint64_t hk = rehash ? tile_hash(p.cell, p.wstart) : p.aux;
+            if (has) {
+                S.sc[t] = p.cell;
+                S.sh[t] = hk;
+                S.sw[t] = we;
+                S.scnt[t] = (unsigned long long)p.count;
+                S.snsp[t] = (unsigned long long)p.nspeed;
+                S.sssp[t] = p.sspeed;
+                S.sslat[t] = p.slat;
+                S.sslon[t] = p.slon;
             }
             __syncthreads();
-            // 2. one lane per unique key: find its slot in its window's table, or claim a free one
-            const unsigned nu = S.n_uniq;
-            const bool active = (unsigned)t < nu;
+            // 2. find and claim the key's slot, or join the lane that holds it
             TileSlot *gslot = nullptr;
             bool created = false;
-            int ls = 0, r = -1;
-            unsigned long long c = 0, we = 0;
-            if (active) {
-                ls = S.uniq[t];
-                c = S.kc[ls];
-                we = S.kw[ls];
-                const uint64_t hk = S.kh[ls];
-                const unsigned tg = tag8(hk);
+            int r = -1, ci = -1;
+            const unsigned tg = tag8(hk);
+            if (has) {
+                bool done = false;
                 for (int q = 0; q < nres; q++)
                     if (S.res_we[q] == we) r = q;
                 if (r >= 0) {
                     const unsigned rmask = S.res_mask[r], off = S.res_off[r];
                     TileSlot *const base = S.res_slots[r];
                     unsigned s = (unsigned)hk & rmask;
-                    for (unsigned probe = 0; probe <= rmask; probe++) {
+                    for (unsigned probe = 0; probe <= rmask && !done; probe++) {
+                        TileSlot *const sl = base + s;
+                        const unsigned long long addr = (unsigned long long)sl;
                         const unsigned bi = off + s, sh = (bi & 3) * 8;
-                        unsigned *const wp = &S.tags[bi >> 2];
-                        unsigned w = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        unsigned b = (w >> sh) & 0xffu;
-                        while (b == 0) {   // free: claim it (another lane may be claiming a neighbour in the word)
-                            const unsigned o = atomicCAS(wp, w, w | (tg << sh));
-                            if (o == w) { created = true; break; }
-                            w = o;
-                            b = (w >> sh) & 0xffu;
-                        }
-                        if (created) { gslot = base + s; S.res_dirty[r] = 1; atomicAdd(&S.res_new[r], 1u); break; }
-                        if (b == tg) {
-                            TileSlot *sl = base + s;
-                            if (ld_l2(&sl->cell) == c && ld_l2(&sl->wenc) == we) { gslot = sl; break; }
+                        const unsigned b = (__hip_atomic_load(&S.tags[bi >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> sh) & 0xffu;
+                        if (b == 0 || b == tg) {
+                            int x = b == 0 ? -1 : mo_holder(S, addr);
+                            bool old_match = false;
+                            if (b == tg && x < 0) old_match = ld_l2(&sl->cell) == p.cell && ld_l2(&sl->wenc) == we;
+                            if (b == 0 || old_match) {
+                                x = mo_claim(S, addr, t, ci);
+                                if (x == -1) {
+                                    gslot = sl;
+                                    created = b == 0;
+                                    if (created) {
+                                        atomicOr(&S.tags[bi >> 2], tg << sh);
+                                        S.res_dirty[r] = 1;
+                                        atomicAdd(&S.res_new[r], 1u);
+                                    }
+                                    done = true;
+                                }
+                            }
+                            if (!done && x >= 0 && S.sc[x] == p.cell && S.sh[x] == hk) {   // same key, this chunk
+                                mo_add_into(S, x, p);
+                                done = true;
+                            }
                         }
                         s = (s + 1) & rmask;
                     }
                 } else {
                     const GenDesc *g = gen_lookup(C, gm, we);
                     if (g) {
-                        S.claim_used = 1;
                         TileSlot *const tab = g->tab;
                         const unsigned long long rmask = g->rmask;
                         unsigned long long sidx = home_slot(*g, hk);
-                        for (unsigned long long probe = 0; probe <= rmask; probe++) {
-                            TileSlot *sl = &tab[sidx];
-                            if (ld_l2(&sl->wenc) != we) {   // free for this window (never used, or another window's key)
-                                const unsigned long long key = (unsigned long long)sl;
-                                unsigned ch = (unsigned)(mix64(key) & (MO_CLAIM - 1));
-                                bool mine = false;
-                                for (int k = 0; k < MO_CLAIM; k++) {
-                                    unsigned long long o = atomicCAS(&S.claim[ch], 0ull, key);
-                                    if (o == 0) { mine = true; break; }
-                                    if (o == key) break;
-                                    ch = (ch + 1) & (MO_CLAIM - 1);
+                        for (unsigned long long probe = 0; probe <= rmask && !done; probe++) {
+                            TileSlot *const sl = &tab[sidx];
+                            const unsigned long long addr = (unsigned long long)sl;
+                            const bool free_here = ld_l2(&sl->wenc) != we;   // never used, or another window's key
+                            if (free_here || ld_l2(&sl->cell) == p.cell) {
+                                const int x = mo_claim(S, addr, t, ci);
+                                if (x == -1) {
+                                    gslot = sl;
+                                    created = free_here;
+                                    if (created) gen_tags(*g)[sidx] = (uint8_t)tg;
+                                    done = true;
+                                } else if (S.sc[x] == p.cell && S.sh[x] == hk) {
+                                    mo_add_into(S, x, p);
+                                    done = true;
                                 }
-                                if (mine) { gslot = sl; created = true; gen_tags(*g)[sidx] = (uint8_t)tg; break; }
-                            } else if (ld_l2(&sl->cell) == c) {
-                                gslot = sl;
-                                break;
                             }
                             sidx = next_slot(sidx, rmask);
                         }
                     }
                 }
-                if (!gslot) overflow = true;
+                if (!done) overflow = true;
             }
+            __syncthreads();
             // 3. apply (this workgroup is the only writer of these regions) and write the key's output row
             unsigned long long ocnt = 0, onsp = 0, tc = 0;
             double ossp = 0.0, oslat = 0.0, oslon = 0.0;
@@ -770,21 +799,22 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
             tbase = __shfl(tbase, 0, 64);
             const unsigned krow = first ? tbase + (unsigned)__popcll(fb & ((1ull << lane_id()) - 1)) : (unsigned)tc;
             if (gslot) {
+                const unsigned long long acnt = S.scnt[t], ansp = S.snsp[t];
                 TileSlot v;
-                v.cell = c;
+                v.cell = p.cell;
                 v.wenc = we;
-                v.count = ocnt + S.cnt[ls];
-                v.nspeed = onsp + S.nsp[ls];
-                v.sspeed = S.nsp[ls] ? ossp + S.ssp[ls] : ossp;
-                v.slat = oslat + S.slat[ls];
-                v.slon = oslon + S.slon[ls];
-                v.touched = rehash ? S.tsq[ls] : ((unsigned long long)seq << 32) | krow;
+                v.count = ocnt + acnt;
+                v.nspeed = onsp + ansp;
+                v.sspeed = ansp ? ossp + S.sssp[t] : ossp;
+                v.slat = oslat + S.sslat[t];
+                v.slon = oslon + S.sslon[t];
+                v.touched = rehash ? p.aux : ((unsigned long long)seq << 32) | krow;
                 if (created) {
                     *gslot = v;
                     created_cnt++;
                 } else {
                     gslot->count = v.count;
-                    if (S.nsp[ls]) {
+                    if (ansp) {
                         gslot->nspeed = v.nspeed;
                         gslot->sspeed = v.sspeed;
                     }
@@ -793,26 +823,18 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
                     if (first) gslot->touched = v.touched;
                 }
 #ifndef HM_ABL_NOROWS
-                if (!rehash) put_row(rows, b0 + krow, c, we, v.count, v.nspeed, v.sspeed, v.slat, v.slon);
+                if (!rehash) put_row(rows, b0 + krow, p.cell, we, v.count, v.nspeed, v.sspeed, v.slat, v.slon);
 #endif
             }
             // created keys of non-resident windows count for their window here (resident ones: res_new); rehash:
             // the host already carries the moved keys
             const bool count_here = created && !rehash && r < 0;
             if (__ballot(count_here) && !wave_count_windows(count_here, we, 1ull, WL, sink)) overflow = true;
-            // 4. make this chunk's stores visible to the next chunk's probes, reset the LDS tables
+            // 4. make this chunk's stores visible to the next chunk's probes; release the claims
 #ifndef HM_ABL_NOFENCE
             __threadfence_block();
 #endif
-            __syncthreads();
-            if (active) {
-                S.kc[ls] = 0; S.kw[ls] = 0; S.cnt[ls] = 0; S.nsp[ls] = 0;
-                S.ssp[ls] = 0.0; S.slat[ls] = 0.0; S.slon[ls] = 0.0; S.tsq[ls] = 0;
-            }
-            if (S.claim_used)
-                for (int q = t; q < MO_CLAIM; q += MO_THREADS) S.claim[q] = 0;
-            __syncthreads();
-            if (t == 0) { S.n_uniq = 0; S.claim_used = 0; }
+            if (ci >= 0) S.claim[ci] = 0;
             __syncthreads();
         }
         // 5. write the resident regions' tags back
