@@ -60,12 +60,15 @@ HM_HD int64_t wdec(unsigned long long e) { return (int64_t)(e ^ (UINT64_C(1) << 
 // is w's.  (Safe because a window never returns once evicted -- its rows are late from then on -- and a
 // growing window only moves to larger tables, never back into one that still holds its stale keys.)
 // A table of 2^L slots is split into 2^rbits regions of >= 256 slots; a key's region is taken from hash bits
-// [19, 32) and its slot from the low bits, linear probing wraps inside the region.  The radix partition
+// [32 - REGION_BITS, 32) and its slot from the low bits, linear probing wraps inside the region.  The radix partition
 // sends all partials of (window, region) to ONE bin = (region << (REGION_BITS - rbits)) | (window salt), so the
 // merge workgroup of a bin is the only writer of the regions it receives.
 constexpr int GMAP_SLOTS = 4096;        // live windows per context (open addressing by wenc)
 constexpr int REGION_MIN_BITS = 8;      // >= 256 slots per region (overflow-free at load <= 1/2)
-constexpr int REGION_BITS = 13;         // at most 2^13 regions per table = radix bins of the partition
+#ifndef HM_REGION_BITS
+#define HM_REGION_BITS 13
+#endif
+constexpr int REGION_BITS = HM_REGION_BITS;   // at most 2^REGION_BITS regions per table = radix bins of the partition
 struct GenDesc {
     unsigned long long wenc;   // 0 = empty map slot
     TileSlot *tab;
@@ -157,8 +160,9 @@ inline FloorDiv make_floor_div(int64_t d) {
 HM_HD uint64_t vkey_hash(uint64_t v) { return mix64(v ^ UINT64_C(0x2545f4914f6cdd1d)); }
 // owner rank of a key: taken from high hash bits so it is independent of the table index bits
 HM_HD int owner_of(uint64_t h, int nranks) { return (int)(((h >> 32) * (uint64_t)nranks) >> 32); }
-// a key's REGION_BITS-bit region field, hash bits [19, 32) (independent of the table size and of the owner bits)
-HM_HD unsigned region_field(uint64_t h) { return (unsigned)(h >> 19) & ((1u << REGION_BITS) - 1); }
+// a key's REGION_BITS-bit region field, hash bits [32 - REGION_BITS, 32) (independent of the table size and of
+// the owner bits)
+HM_HD unsigned region_field(uint64_t h) { return (unsigned)(h >> (32 - REGION_BITS)) & ((1u << REGION_BITS) - 1); }
 HM_HD unsigned window_salt(unsigned long long we) { return (unsigned)mix64(we ^ UINT64_C(0x51ed270b27e5b3c1)); }
 
 }  // namespace hm

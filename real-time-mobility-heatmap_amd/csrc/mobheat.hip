@@ -964,24 +964,46 @@ __global__ __launch_bounds__(256) void k_dedup_max(const uint64_t *__restrict__ 
     }
 }
 
-// winner flag per row (or candidate): ts == max ts of its vkey
+// winner flag per row (or candidate): ts == max ts of its vkey.  DF_U rows per thread, their first probes
+// issued together, each probe one 16-B slot load (key and max ts): the lookups' latencies overlap.
+constexpr int DF_U = 4;
 __global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__ vkey, const int64_t *__restrict__ ts,
                                                     const uint8_t *__restrict__ flags, const Cand *__restrict__ cands, int64_t n,
                                                     const DedupSlot *__restrict__ tab, unsigned long long mask,
                                                     uint8_t *__restrict__ win) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        bool take;
-        unsigned long long v;
-        long long t;
-        if (cands) { take = true; v = cands[i].vkey; t = cands[i].ts; }
-        else { take = (flags[i] & F_VALID) != 0; v = take ? vkey[i] : 0; t = take ? ts[i] : 0; }
-        uint8_t w = 0;
-        if (take && v != EMPTY_VKEY) {
-            long long h = find_vkey(tab, mask, v);
-            w = (h >= 0 && tab[h].maxts == t) ? 1 : 0;
+    const int64_t step = (int64_t)blockDim.x * DF_U;
+    for (int64_t base = (int64_t)blockIdx.x * step; base < n; base += (int64_t)gridDim.x * step) {
+        unsigned long long v[DF_U], h[DF_U];
+        long long t[DF_U];
+        bool take[DF_U];
+        for (int u = 0; u < DF_U; u++) {
+            const int64_t i = base + u * blockDim.x + threadIdx.x;
+            take[u] = false;
+            v[u] = 0;
+            t[u] = 0;
+            if (i < n) {
+                if (cands) { take[u] = true; v[u] = cands[i].vkey; t[u] = cands[i].ts; }
+                else if (flags[i] & F_VALID) { take[u] = true; v[u] = vkey[i]; t[u] = ts[i]; }
+            }
+            take[u] = take[u] && v[u] != EMPTY_VKEY;
+            h[u] = vkey_hash(v[u]) & mask;
         }
-        win[i] = w;
+        DedupSlot sl[DF_U];
+        for (int u = 0; u < DF_U; u++)
+            if (take[u]) sl[u] = tab[h[u]];
+        for (int u = 0; u < DF_U; u++) {
+            const int64_t i = base + u * blockDim.x + threadIdx.x;
+            uint8_t w = 0;
+            if (take[u]) {
+                for (unsigned long long probe = 0; probe <= mask; probe++) {
+                    if (sl[u].vkey == v[u]) { w = sl[u].maxts == t[u]; break; }
+                    if (sl[u].vkey == EMPTY_VKEY) break;
+                    h[u] = (h[u] + 1) & mask;
+                    sl[u] = tab[h[u]];
+                }
+            }
+            if (i < n) win[i] = w;
+        }
     }
 }
 
