@@ -430,16 +430,19 @@ constexpr int RP_BINS = 1 << RP_BITS;
 constexpr int RP_TILE = HM_RP_TILE;    // partials per tile (one workgroup)
 constexpr int RP_THREADS = 256;
 
-// aux_hash: the records carry their key hash in aux (not growth records)
-__device__ __forceinline__ unsigned rp_digit(const TilePartial &p, const GenCache &C, const GenDesc *gm, bool aux_hash, bool &bad) {
+// the radix digit of a partial: its (window, region) bin, or with nranks > 0 its owner rank (the multi-GPU
+// exchange, hm_stage_local); aux_hash: the records carry their key hash in aux (not growth records)
+__device__ __forceinline__ unsigned rp_digit(const TilePartial &p, const GenCache &C, const GenDesc *gm, bool aux_hash,
+                                             int nranks, bool &bad) {
+    if (nranks > 0) return (unsigned)owner_of(p.aux, nranks);
     const int b = bin_of_c(C, gm, aux_hash ? p.aux : tile_hash(p.cell, p.wstart), p.wstart);
     bad |= b < 0;
     return b < 0 ? 0u : (unsigned)b;
 }
 
 __global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const TilePartial *__restrict__ parts, int64_t n, const GenDesc *gm,
-                                                       const GenDesc *glist, int n_glist, int aux_hash, unsigned *__restrict__ H,
-                                                       int64_t ntiles, DevStats *st) {
+                                                       const GenDesc *glist, int n_glist, int aux_hash, int nranks, int nbins,
+                                                       unsigned *__restrict__ H, int64_t ntiles, DevStats *st) {
     __shared__ unsigned h[RP_BINS];
     __shared__ GenCache C;
     gc_load(C, glist, n_glist);
@@ -448,9 +451,9 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const TilePartial *__res
     int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
     int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
     bool bad = false;
-    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) atomicAdd(&h[rp_digit(parts[i], C, gm, aux_hash, bad)], 1u);
+    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) atomicAdd(&h[rp_digit(parts[i], C, gm, aux_hash, nranks, bad)], 1u);
     __syncthreads();
-    for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) H[(int64_t)d * ntiles + blockIdx.x] = h[d];
+    for (int d = threadIdx.x; d < nbins; d += RP_THREADS) H[(int64_t)d * ntiles + blockIdx.x] = h[d];
     if (__ballot(bad) && lane_id() == 0) atomicAdd(&st->overflow, 1ull);
 }
 
@@ -478,6 +481,10 @@ __global__ __launch_bounds__(1024) void k_scan_blocks(const unsigned *__restrict
     }
     if (threadIdx.x == 1023) block_tot[blockIdx.x] = (unsigned)sh[1023];
 }
+// first offset of each digit (the owner partition's per-rank segment starts)
+__global__ void k_digit_starts(const unsigned long long *__restrict__ O, int64_t ntiles, int nbins, unsigned long long *out) {
+    for (int d = threadIdx.x; d < nbins; d += blockDim.x) out[d] = O[(int64_t)d * ntiles];
+}
 __global__ __launch_bounds__(256) void k_scan_add(unsigned long long *__restrict__ out, int64_t m,
                                                   const unsigned long long *__restrict__ block_off) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -486,12 +493,12 @@ __global__ __launch_bounds__(256) void k_scan_add(unsigned long long *__restrict
 
 __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const TilePartial *__restrict__ parts, int64_t n,
                                                           const GenDesc *gm, const GenDesc *glist, int n_glist, int aux_hash,
-                                                          const unsigned long long *__restrict__ O, int64_t ntiles,
-                                                          TilePartial *__restrict__ dst) {
+                                                          int nranks, int nbins, const unsigned long long *__restrict__ O,
+                                                          int64_t ntiles, TilePartial *__restrict__ dst) {
     __shared__ unsigned cur[RP_BINS];   // positions < 2^32 (partition() checks n)
     __shared__ GenCache C;
     gc_load(C, glist, n_glist);
-    for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
+    for (int d = threadIdx.x; d < nbins; d += RP_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
     __syncthreads();
     // four lanes per record, 16 B each: every load/store instruction covers 16 whole 64-B records (16 lines)
     // instead of one line per lane, which is what bounds this kernel's vector-memory issue
@@ -513,7 +520,7 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const TilePartial *__
             p.wstart = (int64_t)((uint64_t)v.z | ((uint64_t)v.w << 32));
             p.aux = (uint64_t)hz | ((uint64_t)hw << 32);
             bool bad = false;
-            pos = atomicAdd(&cur[rp_digit(p, C, gm, aux_hash, bad)], 1u);
+            pos = atomicAdd(&cur[rp_digit(p, C, gm, aux_hash, nranks, bad)], 1u);
         }
         pos = __shfl(pos, lead, 64);
         if (in) d4[(int64_t)pos * 4 + q] = v;
@@ -1580,17 +1587,21 @@ static int gens_upload(hm_ctx *ctx) {
 
 // radix partition of n partial records into RP_BINS bins (one per (window, region)); the sorted copy goes to
 // ctx->parts_sorted, bin b starts at rp_O[b * ntiles]
-static int partition(hm_ctx *ctx, const TilePartial *parts, int64_t n, int aux_hash, int64_t &ntiles) {
+static int partition(hm_ctx *ctx, const TilePartial *parts, int64_t n, int aux_hash, int64_t &ntiles, int nranks = 0,
+                     TilePartial *dst = nullptr) {
+    const int nbins = nranks > 0 ? nranks : RP_BINS;
     if (n > (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "%lld partial records in one merge exceed 2^32-1", (long long)n);
     ntiles = std::max<int64_t>((n + RP_TILE - 1) / RP_TILE, 1);
-    const int64_t m = (int64_t)RP_BINS * ntiles;
+    const int64_t m = (int64_t)nbins * ntiles;
     const int64_t nb = (m + SC_PER - 1) / SC_PER;
     int rc;
-    if ((rc = ensure(ctx, ctx->parts_sorted, std::max<int64_t>(n, 1) * sizeof(TilePartial))) || (rc = ensure(ctx, ctx->rp_H, m * 4)) ||
-        (rc = ensure(ctx, ctx->rp_O, m * 8)) || (rc = ensure(ctx, ctx->rp_btot, nb * 4)) || (rc = ensure(ctx, ctx->rp_boff, nb * 8)))
+    if (!dst && (rc = ensure(ctx, ctx->parts_sorted, std::max<int64_t>(n, 1) * sizeof(TilePartial)))) return rc;
+    if ((rc = ensure(ctx, ctx->rp_H, m * 4)) || (rc = ensure(ctx, ctx->rp_O, m * 8)) || (rc = ensure(ctx, ctx->rp_btot, nb * 4)) ||
+        (rc = ensure(ctx, ctx->rp_boff, nb * 8)))
         return rc;
     hipLaunchKernelGGL(k_rp_hist, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, (const GenDesc *)ctx->d_gmap,
-                       (const GenDesc *)ctx->d_glist, ctx->n_glist, aux_hash, (unsigned *)ctx->rp_H.p, ntiles, ctx->d_st);
+                       (const GenDesc *)ctx->d_glist, ctx->n_glist, aux_hash, nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles,
+                       ctx->d_st);
     hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_H.p, m,
                        (unsigned long long *)ctx->rp_O.p, (unsigned *)ctx->rp_btot.p);
     hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_btot.p, nb,
@@ -1598,8 +1609,8 @@ static int partition(hm_ctx *ctx, const TilePartial *parts, int64_t n, int aux_h
     hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, (unsigned long long *)ctx->rp_O.p, m,
                        (const unsigned long long *)ctx->rp_boff.p);
     hipLaunchKernelGGL(k_rp_scatter, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, (const GenDesc *)ctx->d_gmap,
-                       (const GenDesc *)ctx->d_glist, ctx->n_glist, aux_hash, (const unsigned long long *)ctx->rp_O.p, ntiles,
-                       (TilePartial *)ctx->parts_sorted.p);
+                       (const GenDesc *)ctx->d_glist, ctx->n_glist, aux_hash, nranks, nbins, (const unsigned long long *)ctx->rp_O.p,
+                       ntiles, dst ? dst : (TilePartial *)ctx->parts_sorted.p);
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
 }
@@ -2227,11 +2238,9 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     hipLaunchKernelGGL(k_make_cands, dim3(grid_for(std::max<int64_t>(I.n, 1), 256)), dim3(256), 0, ctx->stream,
                        (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, I.vk, I.ts, rank, (Cand *)ctx->cands.p);
     HIPCHK(ctx, hipGetLastError());
-    // partition both record kinds by owner rank
+    // partition both record kinds by owner rank: candidates by counts + cursors here, tile partials below
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch, 0, 128 * 8, ctx->stream));
     int gb = grid_for(std::max<int64_t>(I.n, 1), 256);
-    hipLaunchKernelGGL(k_part_count<TilePartial>, dim3(gb), dim3(256), 0, ctx->stream, (const TilePartial *)ctx->partials.p,
-                       &ctx->d_st->n_partials, nranks, ctx->d_scratch);
     hipLaunchKernelGGL(k_part_count<Cand>, dim3(gb), dim3(256), 0, ctx->stream, (const Cand *)ctx->cands.p, ctx->d_scratch + 255,
                        nranks, ctx->d_scratch + 64);
     HIPCHK(ctx, hipGetLastError());
@@ -2244,19 +2253,31 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     if ((int64_t)ctx->h_st->n_partials > tile_send_cap || (int64_t)ctx->h_scratch[255] > cand_send_cap)
         return set_err(ctx, HM_E_INVALID, "send buffer too small (%llu tiles, %llu candidates)", ctx->h_st->n_partials,
                        ctx->h_scratch[255]);
-    // exclusive offsets -> cursors
+    // candidates: exclusive offsets -> cursors
     unsigned long long cur[128];
     unsigned long long acc = 0;
-    for (int r = 0; r < nranks; r++) { cur[r] = acc; tile_send_counts[r] = (int64_t)ctx->h_scratch[r]; acc += ctx->h_scratch[r]; }
-    acc = 0;
     for (int r = 0; r < nranks; r++) { cur[64 + r] = acc; cand_send_counts[r] = (int64_t)ctx->h_scratch[64 + r]; acc += ctx->h_scratch[64 + r]; }
-    HIPCHK(ctx, hipMemcpyAsync(ctx->d_scratch, cur, 128 * 8, hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_part_scatter<TilePartial>, dim3(gb), dim3(256), 0, ctx->stream, (const TilePartial *)ctx->partials.p,
-                       &ctx->d_st->n_partials, nranks, ctx->d_scratch, (TilePartial *)tile_send_buf);
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_scratch + 64, cur + 64, 64 * 8, hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(k_part_scatter<Cand>, dim3(gb), dim3(256), 0, ctx->stream, (const Cand *)ctx->cands.p, ctx->d_scratch + 255,
                        nranks, ctx->d_scratch + 64, (Cand *)cand_send_buf);
     HIPCHK(ctx, hipGetLastError());
+    // tile partials: the radix partition with the owner rank as the digit, straight into the send buffer
+    const int64_t n_parts = (int64_t)ctx->h_st->n_partials;
+    if (n_parts > 0) {
+        int64_t ntiles;
+        if ((rc = partition(ctx, (const TilePartial *)ctx->partials.p, n_parts, 1, ntiles, nranks, (TilePartial *)tile_send_buf)))
+            return rc;
+        hipLaunchKernelGGL(k_digit_starts, dim3(1), dim3(64), 0, ctx->stream, (const unsigned long long *)ctx->rp_O.p, ntiles, nranks,
+                           ctx->d_scratch);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 64 * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    for (int r = 0; r < nranks; r++) {
+        const int64_t start = n_parts > 0 ? (int64_t)ctx->h_scratch[r] : 0;
+        const int64_t end = n_parts > 0 && r + 1 < nranks ? (int64_t)ctx->h_scratch[r + 1] : n_parts;
+        tile_send_counts[r] = end - start;
+    }
     if (sizes) {
         sizes->n_tile_partials = (int64_t)ctx->h_st->n_partials;
         sizes->n_cands = 0;
