@@ -259,9 +259,9 @@ constexpr int LA_FLUSH_AT = LA_SLOTS * 3 / 4 - LA_CHUNK;    // occupancy bound b
 static_assert(LA_CHUNK % LA_THREADS == 0 && LA_SLOTS % LA_THREADS == 0, "LDS table geometry");
 
 // LDS key of a (cell, window): a cell of the context's resolution has constant bits 52-63 (mode 1, reserved 0,
-// res), so its low 52 bits plus a 6-bit index into the workgroup's window table (the window starts seen since
-// the last flush) make one 64-bit key: one CAS per probe.
-constexpr int LA_WT = 64;                                   // window table slots per workgroup
+// res), so its low 52 bits plus an index into the workgroup's window table (the window starts seen since the last
+// flush) make one 64-bit key: one CAS per probe.
+constexpr int LA_WT = 32;                                   // window table slots per workgroup
 constexpr uint64_t LA_CELL_LO = (UINT64_C(1) << 52) - 1;
 constexpr uint64_t LA_EMPTY = ~UINT64_C(0);                 // never a key: a key's bits 58-63 are zero
 __device__ __forceinline__ uint64_t la_key(uint64_t cell, unsigned widx) { return (cell & LA_CELL_LO) | ((uint64_t)widx << 52); }
@@ -269,12 +269,14 @@ __device__ __forceinline__ unsigned la_slot(uint64_t key) {
     return (unsigned)((key * UINT64_C(0x9e3779b97f4a7c15)) >> 40) & (LA_SLOTS - 1);
 }
 
-struct LaShared {
+struct LaShared {   // (the six slot arrays are consecutive: la_flush addresses them as words[6][LA_SLOTS])
     unsigned long long key[LA_SLOTS];   // la_key, LA_EMPTY = free
     unsigned long long cnt[LA_SLOTS];   // low 32: count, high 32: n_speed
     double ssp[LA_SLOTS];
     double slat[LA_SLOTS];
     double slon[LA_SLOTS];
+    unsigned long long aux[LA_SLOTS];   // la_flush: the key's tile_hash
+    unsigned short order[LA_SLOTS];     // la_flush: output record -> slot
     long long wt[LA_WT];                // window starts (EMPTY_WIN = free)
     unsigned wcnt[LA_WT];               // partials per window at a flush (the census)
     unsigned int occ;
@@ -313,7 +315,9 @@ __device__ __forceinline__ bool la_direct(TilePartial *out, DevStats *st, WinLds
     return wl_add(WL, census, wenc_of(ws), 1ull);
 }
 
-// partial records of the table's keys; resets the table and the window table
+// partial records of the table's keys; resets the table and the window table.  Pass 1 (a thread per two slots)
+// numbers the keys, hashes them and counts them per window; pass 2 writes the records with four lanes per 64-B
+// record, 16 B each, so that every store instruction covers 16 whole records.
 __device__ void la_flush(LaShared &S, uint64_t cell_hi, TilePartial *out, DevStats *st, WinLds &WL, const CensusSink &census,
                          bool &ok) {
     __syncthreads();
@@ -336,32 +340,42 @@ __device__ void la_flush(LaShared &S, uint64_t cell_hi, TilePartial *out, DevSta
         total += S.scan[q];
     }
     if (t == 0) S.base = total ? atomicAdd(&st->n_partials, (unsigned long long)total) : 0;
-    __syncthreads();
-    unsigned long long pos = S.base + wave_off + incl - c;
+    unsigned idx = wave_off + incl - c;
     for (int q = 0; q < per; q++) {
         const int s = t * per + q;
         const uint64_t k = S.key[s];
         if (k != LA_EMPTY) {
             const unsigned widx = (unsigned)(k >> 52);
-            TilePartial p;
-            p.cell = (k & LA_CELL_LO) | cell_hi;
-            p.wstart = S.wt[widx];
-            p.count = (int64_t)(S.cnt[s] & 0xffffffffull);
-            p.nspeed = (int64_t)(S.cnt[s] >> 32);
-            p.sspeed = S.ssp[s];
-            p.slat = S.slat[s];
-            p.slon = S.slon[s];
-            p.aux = tile_hash(p.cell, p.wstart);
-            out[pos++] = p;
+            S.aux[s] = tile_hash((k & LA_CELL_LO) | cell_hi, S.wt[widx]);
+            S.order[idx++] = (unsigned short)s;
             atomicAdd(&S.wcnt[widx], 1u);
         }
+    }
+    __syncthreads();
+    {
+        const unsigned long long *W = S.key;   // words[6][LA_SLOTS]: key, cnt, ssp, slat, slon, aux
+        uint4 *__restrict__ o4 = (uint4 *)(out + S.base);
+        const int qq = t & 3;
+        const int i1 = qq == 0 ? 0 : qq == 1 ? 1 : qq == 2 ? 2 : 4;
+        const int i2 = qq == 2 ? 3 : 5;
+        for (unsigned r = (unsigned)t >> 2; r < total; r += LA_THREADS / 4) {
+            const unsigned s = S.order[r];
+            const uint64_t w1 = W[i1 * LA_SLOTS + s], w2 = W[i2 * LA_SLOTS + s];
+            const uint64_t wsv = (uint64_t)S.wt[(w1 >> 52) & (LA_WT - 1)];
+            const uint64_t a = qq == 0 ? (w1 & LA_CELL_LO) | cell_hi : qq == 1 ? (w1 & 0xffffffffull) : w1;
+            const uint64_t b = qq == 0 ? wsv : qq == 1 ? (w1 >> 32) : w2;
+            o4[(uint64_t)r * 4 + qq] = make_uint4((unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32));
+        }
+    }
+    __syncthreads();
+    for (int q = 0; q < per; q++) {
+        const int s = t * per + q;
         S.key[s] = LA_EMPTY;
         S.cnt[s] = 0;
         S.ssp[s] = 0.0;
         S.slat[s] = 0.0;
         S.slon[s] = 0.0;
     }
-    __syncthreads();
     // census of the flushed partials per window (LDS; the global map is updated once per workgroup)
     if (t < LA_WT) {
         if (S.wcnt[t]) ok &= wl_add(WL, census, wenc_of(S.wt[t]), (unsigned long long)S.wcnt[t]);
