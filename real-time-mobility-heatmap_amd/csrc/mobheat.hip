@@ -917,6 +917,24 @@ __device__ __forceinline__ long long find_or_claim_vkey(DedupSlot *tab, unsigned
     }
     return -1;
 }
+// find_or_claim_vkey that also returns the slot's max ts, read together with its key (one round trip; a stale max
+// is <= the true one and only costs the caller an extra atomicMax)
+__device__ __forceinline__ long long find_or_claim_vkey_ts(DedupSlot *tab, unsigned long long mask, unsigned long long v,
+                                                           bool &claimed, unsigned long long max_probe, long long &cur_max) {
+    unsigned long long h = vkey_hash(v) & mask;
+    claimed = false;
+    for (unsigned long long probe = 0; probe < max_probe; probe++) {
+        unsigned long long cur = __hip_atomic_load(&tab[h].vkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cur_max = __hip_atomic_load(&tab[h].maxts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == EMPTY_VKEY) {
+            cur = atomicCAS(&tab[h].vkey, EMPTY_VKEY, v);
+            if (cur == EMPTY_VKEY) { claimed = true; return (long long)h; }
+        }
+        if (cur == v) return (long long)h;
+        h = (h + 1) & mask;
+    }
+    return -1;
+}
 __device__ __forceinline__ long long find_vkey(const DedupSlot *tab, unsigned long long mask, unsigned long long v) {
     unsigned long long h = vkey_hash(v) & mask;
     for (unsigned long long probe = 0; probe <= mask; probe++) {
@@ -1002,9 +1020,9 @@ __global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__
             take[u] = false;
             v[u] = 0;
             t[u] = 0;
-            if (i < n) {
+            if (i < n) {   // (the row's loads do not wait for its flag: one dependent latency less)
                 if (cands) { take[u] = true; v[u] = cands[i].vkey; t[u] = cands[i].ts; }
-                else if (flags[i] & F_VALID) { take[u] = true; v[u] = vkey[i]; t[u] = ts[i]; }
+                else { v[u] = vkey[i]; t[u] = ts[i]; take[u] = (flags[i] & F_VALID) != 0; }
             }
             take[u] = take[u] && v[u] != EMPTY_VKEY;
             h[u] = vkey_hash(v[u]) & mask;
@@ -1119,13 +1137,10 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
                 if (v == EMPTY_VKEY) {
                     bad++;
                 } else {
-                    dh = find_or_claim_vkey(dtab, dmask, v, claimed, DEDUP_FUSED_PROBES);
-                    if (dh < 0) {
-                        dretry = true;
-                    } else {
-                        const long long cur = __hip_atomic_load(&dtab[dh].maxts, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (t > cur) atomicMax(&dtab[dh].maxts, (long long)t);
-                    }
+                    long long cur = INT64_MIN;
+                    dh = find_or_claim_vkey_ts(dtab, dmask, v, claimed, DEDUP_FUSED_PROBES, cur);
+                    if (dh < 0) dretry = true;
+                    else if (t > cur) atomicMax(&dtab[dh].maxts, (long long)t);
                 }
             }
             const unsigned long long pos = wave_append(claimed, n_dused);
