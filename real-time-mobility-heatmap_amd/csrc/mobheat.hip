@@ -96,19 +96,39 @@ __device__ __forceinline__ unsigned long long next_slot(unsigned long long s, un
 // LDS copy of the live windows' table descriptors (a batch touches a few windows; the global map is the
 // fallback when there are more than GC_MAX)
 constexpr int GC_MAX = 32;
+constexpr int GC_IDX = 64;   // open-addressing index over the cached descriptors
 struct GenCache {
     GenDesc e[GC_MAX];
+    signed char idx[GC_IDX];   // -1 = empty
     int n;   // -1: use the global map
 };
+__device__ __forceinline__ unsigned gc_home(unsigned long long we) {
+    return (unsigned)((we * UINT64_C(0x9e3779b97f4a7c15)) >> 58);   // 6 bits
+}
+// (callers __syncthreads() before the first lookup)
 __device__ __forceinline__ void gc_load(GenCache &C, const GenDesc *glist, int n) {
-    if (threadIdx.x == 0) C.n = n <= GC_MAX ? n : -1;
+    if (threadIdx.x == 0) {
+        C.n = n <= GC_MAX ? n : -1;
+        for (int q = 0; q < GC_IDX; q++) C.idx[q] = -1;
+        if (n <= GC_MAX)
+            for (int q = 0; q < n; q++) {
+                unsigned h = gc_home(glist[q].wenc);
+                while (C.idx[h] >= 0) h = (h + 1) & (GC_IDX - 1);
+                C.idx[h] = (signed char)q;
+            }
+    }
     if (n <= GC_MAX)
         for (int q = threadIdx.x; q < n; q += blockDim.x) C.e[q] = glist[q];
 }
 __device__ __forceinline__ const GenDesc *gen_lookup(const GenCache &C, const GenDesc *gm, unsigned long long we) {
     if (C.n >= 0) {
-        for (int q = 0; q < C.n; q++)
-            if (C.e[q].wenc == we) return &C.e[q];
+        unsigned h = gc_home(we);
+        for (int p = 0; p < GC_IDX; p++) {
+            const int i = C.idx[h];
+            if (i < 0) return nullptr;
+            if (C.e[i].wenc == we) return &C.e[i];
+            h = (h + 1) & (GC_IDX - 1);
+        }
         return nullptr;
     }
     const int g = gmap_find(gm, we);
@@ -282,6 +302,7 @@ struct LaShared {   // (the six slot arrays are consecutive: la_flush addresses 
     unsigned int occ;
     unsigned int scan[LA_THREADS / 64];
     unsigned long long base;
+    unsigned dskip;                     // the fused dedup has given up (st->dedup_retry) -- skip it
 };
 
 // index of window start ws in the workgroup's window table (inserted if new); -1 when the table is full
@@ -565,7 +586,7 @@ constexpr int MO_CLAIM = 512;
 #define HM_MO_TAG_BYTES 24576
 #endif
 constexpr int MO_TAG_BYTES = HM_MO_TAG_BYTES;   // LDS for resident region tags per workgroup
-constexpr int MO_RES_MAX = 8;                    // resident (window, region)s per bin
+constexpr int MO_RES_MAX = 16;                   // resident (window, region)s per bin
 
 struct MoShared {
     // this chunk's records by lane; a duplicate key's values are added into its claimer's entry
@@ -1052,7 +1073,12 @@ __global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__
 // LDS pre-aggregation of (cell, windowStart) into partial records (:112-123). The fp64 cell computation
 // dominates; the aggregation's LDS atomics and the dedup's table atomics overlap with it.
 // =====================================================================================================
-constexpr unsigned long long DEDUP_FUSED_PROBES = 256;
+// The fused per-vkey max gives up on a key after DEDUP_FUSED_PROBES probes (its table was sized from the previous
+// batch and is too small); the first give-up is published in st->dedup_retry and later chunks skip the fused
+// dedup, which phase_dedup then reruns over the whole batch on a full-size table.  (Published in *dgiveup, a word
+// on a cache line of its own, and polled every 16 chunks: polling a DevStats word every chunk, whose line all
+// flushes hit with atomics, made k_ingest 4x slower.)
+constexpr unsigned long long DEDUP_FUSED_PROBES = 32;
 
 __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     const double *__restrict__ lat, const double *__restrict__ lon, const int64_t *__restrict__ ts,
@@ -1060,7 +1086,7 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     const uint64_t *__restrict__ vkey, int64_t n, int res, FloorDiv wdiv, int64_t late_end_us,
     uint8_t *__restrict__ flags_out, TilePartial *__restrict__ out, DedupSlot *dtab, unsigned long long dmask,
     unsigned int *dused, unsigned long long *n_dused, unsigned int *__restrict__ slow, unsigned long long *n_slow,
-    WinCount *cmap, DevStats *st) {
+    unsigned long long *dgiveup, WinCount *cmap, DevStats *st) {
     __shared__ LaShared S;
     __shared__ WinLds WL;
     wl_init(WL);
@@ -1076,7 +1102,7 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
         S.slon[s] = 0.0;
     }
     for (int s = threadIdx.x; s < LA_WT; s += LA_THREADS) { S.wt[s] = EMPTY_WIN; S.wcnt[s] = 0; }
-    if (threadIdx.x == 0) S.occ = 0;
+    if (threadIdx.x == 0) { S.occ = 0; S.dskip = 0; }
     __syncthreads();
     unsigned long long nvalid = 0, nlate = 0, bad = 0;
     long long tmax = INT64_MIN;
@@ -1131,7 +1157,7 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
 #ifdef HM_ABL_NODEDUP
             if (false) {
 #else
-            if (ok) {
+            if (ok && !S.dskip) {
 #endif
                 const unsigned long long v = vkey[i];
                 if (v == EMPTY_VKEY) {
@@ -1139,8 +1165,12 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
                 } else {
                     long long cur = INT64_MIN;
                     dh = find_or_claim_vkey_ts(dtab, dmask, v, claimed, DEDUP_FUSED_PROBES, cur);
-                    if (dh < 0) dretry = true;
-                    else if (t > cur) atomicMax(&dtab[dh].maxts, (long long)t);
+                    if (dh < 0) {
+                        if (!dretry) atomicExch(dgiveup, 1ull);
+                        dretry = true;
+                    } else if (t > cur) {
+                        atomicMax(&dtab[dh].maxts, (long long)t);
+                    }
                 }
             }
             const unsigned long long pos = wave_append(claimed, n_dused);
@@ -1179,6 +1209,9 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
             const unsigned long long fb = __ballot(fresh);
             if (fb && lane_id() == (unsigned)(__ffsll((long long)fb) - 1)) atomicAdd(&S.occ, (unsigned)__popcll(fb));
         }
+        // poll the give-up flag now and then (its own cache line: DevStats takes every flush's atomics)
+        if (threadIdx.x == 0 && !S.dskip && ((ch / gridDim.x) & 15) == 15)
+            S.dskip = __hip_atomic_load(dgiveup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
         __syncthreads();
         if (S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, cell_hi, out, st, WL, census, census_ok);
     }
@@ -1448,10 +1481,17 @@ struct hm_ctx {
     DevBuf parts_regrow;              // growth: the old tables' keys as partial records
     unsigned long long seq = 0;
     // dedup table (persistent, cleared through its used list)
-    DedupSlot *dtab = nullptr;
-    unsigned long long dcap = 0;
-    DevBuf dused;
-    bool dedup_dirty = false;
+    // latest-position tables (16-B slots, cleared through their used lists): `fused` is k_ingest's, sized from the
+    // last batch's distinct vkeys and kept small (cache residency is its speed); `full` serves the max pass when
+    // the fused one gave up, and received candidates (multi-GPU): grow-only, so it is allocated once
+    struct DedupTable {
+        DedupSlot *tab = nullptr;
+        unsigned long long cap = 0;
+        DevBuf used;
+        bool dirty = false;
+        int used_word = 0;   // d_scratch word counting the used slots
+    } dfused, dfull;
+    DedupTable *dlast = nullptr;   // the table the last batch's flags were computed on
     int64_t dedup_seen = 0;
     int64_t n_partials_merged = 0;   // partial records of the last merge (hm_batch_out.n_partials)
     int ingest_grid = 0;             // k_ingest's persistent grid: resident workgroups per CU x CUs     // distinct vkeys of the last batch (sizes k_ingest's fused dedup table)
@@ -1480,8 +1520,10 @@ static std::string g_create_err;
 // DUSED_WORD: used-slot count of the persistent dedup table (survives until the table is cleared),
 // 255: result count of the last ordered compaction
 constexpr int DUSED_WORD = 253;
+constexpr int FULL_USED_WORD = 240;   // used-slot count of the full dedup table
 constexpr int SLOW_WORD = 252;   // number of k_ingest fast-path exceptions of the current batch
 constexpr int REGROW_WORD = 251; // records dumped by k_dump_gen
+constexpr int GIVEUP_WORD = 232; // k_ingest's fused dedup gave up (a cache line of its own: words 232-239)
 
 #define HIPCHK(ctx, expr)                                                                             \
     do {                                                                                              \
@@ -1767,36 +1809,38 @@ static int state_account(hm_ctx *ctx, int64_t evict_wm_ms) {
     return HM_OK;
 }
 
-// Clear the dedup table through the last batch's used list and make sure it holds `n_keys` keys at <= 1/2 load.
-static int dedup_prepare(hm_ctx *ctx, int64_t n_keys) {
-    if (ctx->dedup_dirty) {
-        hipLaunchKernelGGL(k_clear_dedup, dim3(grid_for(ctx->dcap, 256)), dim3(256), 0, ctx->stream, ctx->dtab,
-                           (const unsigned int *)ctx->dused.p, ctx->d_scratch + DUSED_WORD);
+// Clear a dedup table through its used list and make sure it holds `n_keys` keys at <= 1/2 load; shrink: the
+// table is also reallocated when it is more than twice the size needed (the fused table: cache residency).
+static int dedup_prepare(hm_ctx *ctx, hm_ctx::DedupTable &d, int64_t n_keys, bool shrink) {
+    if (d.dirty) {
+        hipLaunchKernelGGL(k_clear_dedup, dim3(grid_for(d.cap, 256)), dim3(256), 0, ctx->stream, d.tab,
+                           (const unsigned int *)d.used.p, ctx->d_scratch + d.used_word);
         HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + DUSED_WORD, 0, 8, ctx->stream));
-        ctx->dedup_dirty = false;
+        HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + d.used_word, 0, 8, ctx->stream));
+        d.dirty = false;
     }
     unsigned long long want = next_pow2((unsigned long long)std::max<int64_t>(2 * n_keys, 1024));
-    // keep the table when it fits and is not far larger than needed (a cache-resident table is the point)
-    if (ctx->dtab && ctx->dcap >= want && ctx->dcap <= 8 * want) return HM_OK;
-    if (ctx->dtab) {
+    // (a 2 MB fused table stays in every XCD's L2, an 8 MB one does not: k_ingest 6.9 -> 28 ms on the bench)
+    if (d.tab && d.cap >= want && (!shrink || d.cap <= 2 * want)) return HM_OK;
+    if (d.tab) {
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        HIPCHK(ctx, hipFree(ctx->dtab));
-        ctx->dtab = nullptr;
+        HIPCHK(ctx, hipFree(d.tab));
+        d.tab = nullptr;
     }
-    if (hipMalloc(&ctx->dtab, want * sizeof(DedupSlot)) != hipSuccess) {
+    if (hipMalloc(&d.tab, want * sizeof(DedupSlot)) != hipSuccess) {
         (void)hipGetLastError();
         return set_err(ctx, HM_E_NOMEM, "dedup table alloc failed");
     }
-    ctx->dcap = want;
-    hipLaunchKernelGGL(k_init_dedup, dim3(grid_for(want, 256)), dim3(256), 0, ctx->stream, ctx->dtab, want);
+    d.cap = want;
+    hipLaunchKernelGGL(k_init_dedup, dim3(grid_for(want, 256)), dim3(256), 0, ctx->stream, d.tab, want);
     HIPCHK(ctx, hipGetLastError());
-    return ensure(ctx, ctx->dused, want * sizeof(unsigned int));
+    return ensure(ctx, d.used, want * sizeof(unsigned int));
 }
 // k_ingest's table: sized from the last batch's distinct vkeys (small and cache-resident), not from n; a batch
 // with many more keys makes the fused probes give up and phase_dedup reruns the max pass on a full-size table.
 static int64_t dedup_fused_keys(const hm_ctx *ctx, int64_t n) {
-    return std::min<int64_t>(n, std::max<int64_t>(int64_t(1) << 15, ctx->dedup_seen + ctx->dedup_seen / 4));
+    const int64_t guess = ctx->dedup_seen > 0 ? ctx->dedup_seen + ctx->dedup_seen / 4 : int64_t(1) << 18;   // first batch
+    return std::min<int64_t>(n, std::max<int64_t>(int64_t(1) << 15, guess));
 }
 
 // ordered compaction of byte flags -> int64 indices into ctx->rows; count into d_scratch[255]
@@ -1862,9 +1906,10 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
     if ((rc = ensure(ctx, ctx->flags, n)) || (rc = ensure(ctx, ctx->win, n)) || (rc = ensure(ctx, ctx->rows, n * 8)) ||
         (rc = ensure(ctx, ctx->partials, n * sizeof(TilePartial))) || (rc = ensure(ctx, ctx->slow, n * sizeof(unsigned int))))
         return rc;
-    if ((rc = dedup_prepare(ctx, dedup_fused_keys(ctx, n)))) return rc;
+    if ((rc = dedup_prepare(ctx, ctx->dfused, dedup_fused_keys(ctx, n), true))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_st, 0, sizeof(DevStats), ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + SLOW_WORD, 0, 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + GIVEUP_WORD, 0, 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->d_cmap, 0, GMAP_SLOTS * sizeof(WinCount), ctx->stream));
     long long init[2] = {INT64_MIN, INT64_MAX};
     HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->max_ts_ms, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
@@ -1874,14 +1919,14 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
         int blocks = (int)std::min<int64_t>(nchunks, ctx->ingest_grid);
         hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(LA_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.sp, I.sv, I.vk,
                            n, ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
-                           (TilePartial *)ctx->partials.p, ctx->dtab, ctx->dcap - 1, (unsigned int *)ctx->dused.p,
-                           ctx->d_scratch + DUSED_WORD, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, ctx->d_cmap,
-                           ctx->d_st);
+                           (TilePartial *)ctx->partials.p, ctx->dfused.tab, ctx->dfused.cap - 1,
+                           (unsigned int *)ctx->dfused.used.p, ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
+                           ctx->d_scratch + GIVEUP_WORD, ctx->d_cmap, ctx->d_st);
         hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, I.ts, I.sp, I.sv,
                            ctx->cfg.h3_res, ctx->cfg.tile_us, (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
                            (TilePartial *)ctx->partials.p, ctx->d_cmap, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
-        ctx->dedup_dirty = true;
+        ctx->dfused.dirty = true;
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
@@ -1893,23 +1938,22 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
 static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t n, bool rerun_max) {
     int rc;
     const bool need_max = cands != nullptr || rerun_max;
-    if (need_max) {
-        if (I) ctx->dedup_dirty = true;   // rows: k_ingest's partial table is cleared through its used list
-        if ((rc = dedup_prepare(ctx, n))) return rc;
-    }
+    hm_ctx::DedupTable &d = need_max ? ctx->dfull : ctx->dfused;
+    if (need_max && (rc = dedup_prepare(ctx, d, n, false))) return rc;
+    ctx->dlast = &d;
     if ((rc = ensure(ctx, ctx->win, std::max<int64_t>(n, 1))) || (rc = ensure(ctx, ctx->rows, std::max<int64_t>(n, 1) * 8)))
         return rc;
     if (n > 0) {
         if (need_max) {
             hipLaunchKernelGGL(k_dedup_max, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, I ? I->vk : nullptr,
-                               I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, ctx->dtab, ctx->dcap - 1,
-                               (unsigned int *)ctx->dused.p, ctx->d_scratch + DUSED_WORD, ctx->d_st);
+                               I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, d.tab, d.cap - 1,
+                               (unsigned int *)d.used.p, ctx->d_scratch + d.used_word, ctx->d_st);
+            d.dirty = true;
         }
         hipLaunchKernelGGL(k_dedup_flag, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, I ? I->vk : nullptr,
-                           I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, ctx->dtab, ctx->dcap - 1,
+                           I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, d.tab, d.cap - 1,
                            (uint8_t *)ctx->win.p);
         HIPCHK(ctx, hipGetLastError());
-        ctx->dedup_dirty = true;
         if ((rc = compact_flags(ctx, (const uint8_t *)ctx->win.p, n, (int64_t *)ctx->rows.p))) return rc;
     } else {
         HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + 255, 0, 8, ctx->stream));
@@ -2084,6 +2128,13 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
             ctx->err = "occupancy query";
             return fail("create");
         }
+        // the occupancy API can report one block per CU more than fits (MI355X_MICROARCH.md, correctness
+        // boundaries: SGPR counts 81-112); k_ingest is persistent, so an extra block per CU would only run once
+        // a resident one finished.  Bound it by the LDS each block takes.
+        hipFuncAttributes fa{};
+        if (hipFuncGetAttributes(&fa, (const void *)k_ingest) == hipSuccess && fa.sharedSizeBytes > 0)
+            per_cu = std::min<int>(per_cu, (int)(163840 / fa.sharedSizeBytes));
+        if (getenv("MOBHEAT_DEBUG")) fprintf(stderr, "mobheat: k_ingest %d blocks/CU x %d CUs (LDS %zu B)\n", per_cu, cus, fa.sharedSizeBytes);
         ctx->ingest_grid = std::max(1, per_cu) * std::max(1, cus);
     }
     if (hipMalloc(&ctx->d_st, sizeof(DevStats)) != hipSuccess || hipHostMalloc(&ctx->h_st, sizeof(DevStats)) != hipSuccess ||
@@ -2102,9 +2153,8 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         ctx->err = "window map alloc";
         return fail("create");
     }
-    if (cfg->batch_capacity_hint > 0) {
-        if (dedup_prepare(ctx, cfg->batch_capacity_hint)) return fail("create");
-    }
+    ctx->dfused.used_word = DUSED_WORD;
+    ctx->dfull.used_word = FULL_USED_WORD;
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) { ctx->err = "sync"; return fail("create"); }
     *out = ctx;
     return HM_OK;
@@ -2118,7 +2168,7 @@ void hm_destroy(hm_ctx *ctx) {
                       &ctx->cell, &ctx->wstart, &ctx->flags, &ctx->win, &ctx->rows, &ctx->block_counts, &ctx->block_offs,
                       &ctx->partials, &ctx->cands, &ctx->slow, &ctx->parts_sorted, &ctx->parts_regrow, &ctx->rp_H, &ctx->rp_O,
                       &ctx->rp_btot, &ctx->rp_boff,
-                      &ctx->s_cell, &ctx->s_ws, &ctx->s_cnt, &ctx->s_sp, &ctx->s_spn, &ctx->s_lon, &ctx->s_lat, &ctx->bin_cnt, &ctx->bin_off, &ctx->dused, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
+                      &ctx->s_cell, &ctx->s_ws, &ctx->s_cnt, &ctx->s_sp, &ctx->s_spn, &ctx->s_lon, &ctx->s_lat, &ctx->bin_cnt, &ctx->bin_off, &ctx->dfused.used, &ctx->dfull.used, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
                       &ctx->o_lon, &ctx->o_lat};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
@@ -2130,7 +2180,8 @@ void hm_destroy(hm_ctx *ctx) {
     if (ctx->d_glist) (void)hipFree(ctx->d_glist);
     if (ctx->h_glist) (void)hipHostFree(ctx->h_glist);
     if (ctx->h_cmap) (void)hipHostFree(ctx->h_cmap);
-    if (ctx->dtab) (void)hipFree(ctx->dtab);
+    if (ctx->dfused.tab) (void)hipFree(ctx->dfused.tab);
+    if (ctx->dfull.tab) (void)hipFree(ctx->dfull.tab);
     void *hbufs[] = {ctx->h_cell, ctx->h_ws, ctx->h_cnt, ctx->h_sp, ctx->h_spn, ctx->h_lon, ctx->h_lat, ctx->h_rows};
     for (void *p : hbufs)
         if (p) (void)hipHostFree(p);
@@ -2178,10 +2229,9 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if ((rc = phase_dedup(ctx, &I, nullptr, I.n, s1.dedup_retry != 0))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch + DUSED_WORD, ctx->d_scratch + DUSED_WORD, 3 * 8, hipMemcpyDeviceToHost,
-                               ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 256 * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    ctx->dedup_seen = (int64_t)ctx->h_scratch[DUSED_WORD];
+    ctx->dedup_seen = (int64_t)ctx->h_scratch[ctx->dlast->used_word];   // distinct vkeys of this batch
     DevStats s2 = *ctx->h_st;
     if (s2.overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     if (s2.bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved (%llu rows)", s2.bad_vkey);
@@ -2278,7 +2328,7 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     if (ctx->h_st->bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved");
-    ctx->dedup_seen = (int64_t)ctx->h_scratch[DUSED_WORD];
+    ctx->dedup_seen = (int64_t)ctx->h_scratch[ctx->dlast->used_word];
     if ((int64_t)ctx->h_st->n_partials > tile_send_cap || (int64_t)ctx->h_scratch[255] > cand_send_cap)
         return set_err(ctx, HM_E_INVALID, "send buffer too small (%llu tiles, %llu candidates)", ctx->h_st->n_partials,
                        ctx->h_scratch[255]);
