@@ -2155,6 +2155,18 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     }
     ctx->dfused.used_word = DUSED_WORD;
     ctx->dfull.used_word = FULL_USED_WORD;
+    // batch_capacity_hint: reserve the per-batch buffers now (multi-GB allocations would otherwise land in the
+    // first batches; each later batch only grows them when it is larger)
+    if (cfg->batch_capacity_hint > 0) {
+        const int64_t n = cfg->batch_capacity_hint;
+        const size_t tp = sizeof(TilePartial);
+        if (ensure(ctx, ctx->flags, n) || ensure(ctx, ctx->win, n) || ensure(ctx, ctx->rows, n * 8) ||
+            ensure(ctx, ctx->partials, n * tp) || ensure(ctx, ctx->slow, n * 4) || ensure(ctx, ctx->parts_sorted, n * tp) ||
+            ensure(ctx, ctx->s_cell, n * 8) || ensure(ctx, ctx->s_ws, n * 8) || ensure(ctx, ctx->s_cnt, n * 8) ||
+            ensure(ctx, ctx->s_sp, n * 8) || ensure(ctx, ctx->s_spn, n) || ensure(ctx, ctx->s_lon, n * 8) ||
+            ensure(ctx, ctx->s_lat, n * 8) || ensure_outputs(ctx, n))
+            return fail("create");
+    }
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) { ctx->err = "sync"; return fail("create"); }
     *out = ctx;
     return HM_OK;
