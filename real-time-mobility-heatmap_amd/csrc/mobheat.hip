@@ -1080,6 +1080,11 @@ __global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__
 // flushes hit with atomics, made k_ingest 4x slower.)
 constexpr unsigned long long DEDUP_FUSED_PROBES = 32;
 
+// DIRECT: no LDS pre-aggregation -- every aggregated row is its own partial record (staged in LDS, stored four
+// lanes per record).  The host picks it when the previous batch's partials were > 80% of its aggregated rows
+// (nearly every key distinct: the LDS table's probes, atomics and flushes then buy nothing, cf. Spark's adaptive
+// skipping of partial aggregation when its reduction ratio is poor).
+template <bool DIRECT>
 __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     const double *__restrict__ lat, const double *__restrict__ lon, const int64_t *__restrict__ ts,
     const uint8_t *__restrict__ row_valid, const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
@@ -1175,8 +1180,44 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
             }
             const unsigned long long pos = wave_append(claimed, n_dused);
             if (claimed) dused[pos] = (unsigned int)dh;
-            // LDS pre-aggregation of the window's rows
             bool fresh = false;
+            if constexpr (DIRECT) {
+                // every aggregated row is a partial record: block-wide positions, staged in LDS, stored
+                // four lanes per 64-B record
+                const bool rec = (fl & F_AGG) && !exc;
+                const unsigned long long bal = __ballot(rec);
+                const int wv = threadIdx.x >> 6;
+                if (lane_id() == 0) S.scan[wv] = (unsigned)__popcll(bal);
+                __syncthreads();
+                unsigned woff = 0, total = 0;
+                for (int k = 0; k < LA_THREADS / 64; k++) {
+                    if (k < wv) woff += S.scan[k];
+                    total += S.scan[k];
+                }
+                if (threadIdx.x == 0) S.base = total ? atomicAdd(&st->n_partials, (unsigned long long)total) : 0;
+                uint4 *stage = (uint4 *)S.key;   // key, cnt, ssp, slat: 16 KB = 256 records
+                if (rec) {
+                    const unsigned r = woff + (unsigned)__popcll(bal & ((1ull << lane_id()) - 1));
+                    const bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
+                    const double sp = sv ? speed[i] : 0.0;
+                    const int64_t ws = widx >= 0 ? (int64_t)S.wt[widx] : floor_div(t, wdiv) * tile_us;
+                    const uint64_t h = tile_hash(cell, ws);
+                    const uint64_t spb = __builtin_bit_cast(uint64_t, sp), lab = __builtin_bit_cast(uint64_t, la),
+                                   lob = __builtin_bit_cast(uint64_t, lo);
+                    stage[r * 4 + 0] = make_uint4((unsigned)cell, (unsigned)(cell >> 32), (unsigned)ws, (unsigned)((uint64_t)ws >> 32));
+                    stage[r * 4 + 1] = make_uint4(1u, 0u, sv ? 1u : 0u, 0u);
+                    stage[r * 4 + 2] = make_uint4((unsigned)spb, (unsigned)(spb >> 32), (unsigned)lab, (unsigned)(lab >> 32));
+                    stage[r * 4 + 3] = make_uint4((unsigned)lob, (unsigned)(lob >> 32), (unsigned)h, (unsigned)(h >> 32));
+                    if (widx >= 0) atomicAdd(&S.wcnt[widx], 1u);
+                    else census_ok &= wl_add(WL, census, wenc_of(ws), 1ull);
+                }
+                __syncthreads();
+                uint4 *__restrict__ o4 = (uint4 *)(out + S.base);
+                for (unsigned r = (unsigned)threadIdx.x >> 2; r < total; r += LA_THREADS / 4)
+                    o4[(uint64_t)r * 4 + (threadIdx.x & 3)] = stage[r * 4 + (threadIdx.x & 3)];
+                __syncthreads();
+            } else {
+            // LDS pre-aggregation of the window's rows
 #ifdef HM_ABL_NOAGG
             if ((fl & F_AGG) && !exc) abl_sink ^= cell;
             if (false) {
@@ -1206,6 +1247,7 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
                     census_ok &= la_direct(out, st, WL, census, cell, floor_div(t, wdiv) * tile_us, sv, sp, la, lo);
                 }
             }
+            }
             const unsigned long long fb = __ballot(fresh);
             if (fb && lane_id() == (unsigned)(__ffsll((long long)fb) - 1)) atomicAdd(&S.occ, (unsigned)__popcll(fb));
         }
@@ -1213,9 +1255,14 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
         if (threadIdx.x == 0 && !S.dskip && ((ch / gridDim.x) & 15) == 15)
             S.dskip = __hip_atomic_load(dgiveup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
         __syncthreads();
-        if (S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, cell_hi, out, st, WL, census, census_ok);
+        if (!DIRECT && S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, cell_hi, out, st, WL, census, census_ok);
     }
     if (S.occ > 0) la_flush(S, cell_hi, out, st, WL, census, census_ok);
+    if constexpr (DIRECT) {   // the window table was never flushed: its census
+        __syncthreads();
+        if (threadIdx.x < LA_WT && S.wcnt[threadIdx.x])
+            census_ok &= wl_add(WL, census, wenc_of(S.wt[threadIdx.x]), (unsigned long long)S.wcnt[threadIdx.x]);
+    }
     __syncthreads();
     census_ok &= wl_flush(WL, census);
 #ifdef HM_ABL_NOAGG
@@ -1494,7 +1541,10 @@ struct hm_ctx {
     DedupTable *dlast = nullptr;   // the table the last batch's flags were computed on
     int64_t dedup_seen = 0;
     int64_t n_partials_merged = 0;   // partial records of the last merge (hm_batch_out.n_partials)
-    int ingest_grid = 0;             // k_ingest's persistent grid: resident workgroups per CU x CUs     // distinct vkeys of the last batch (sizes k_ingest's fused dedup table)
+    int ingest_grid[2] = {0, 0};     // k_ingest<DIRECT>'s persistent grid: resident workgroups per CU x CUs
+    int ingest_mode = 0;             // 0 adaptive, 1 direct, 2 LDS pre-aggregation
+    double agg_ratio = 0.0;          // partials / aggregated rows of the last batch (adaptive mode)
+    bool last_direct = false;
     // outputs (device + pinned host)
     DevBuf o_cell, o_ws, o_cnt, o_sp, o_spn, o_lon, o_lat;
     void *h_cell = nullptr, *h_ws = nullptr, *h_cnt = nullptr, *h_sp = nullptr, *h_spn = nullptr, *h_lon = nullptr,
@@ -1916,8 +1966,10 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
     if (n > 0) {
         int64_t nchunks = (n + LA_CHUNK - 1) / LA_CHUNK;
-        int blocks = (int)std::min<int64_t>(nchunks, ctx->ingest_grid);
-        hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(LA_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.sp, I.sv, I.vk,
+        const bool direct = ctx->ingest_mode == 1 || (ctx->ingest_mode == 0 && ctx->agg_ratio > 0.8);
+        ctx->last_direct = direct;
+        int blocks = (int)std::min<int64_t>(nchunks, ctx->ingest_grid[direct]);
+        hipLaunchKernelGGL(direct ? k_ingest<true> : k_ingest<false>, dim3(blocks), dim3(LA_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.sp, I.sv, I.vk,
                            n, ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
                            (TilePartial *)ctx->partials.p, ctx->dfused.tab, ctx->dfused.cap - 1,
                            (unsigned int *)ctx->dfused.used.p, ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
@@ -1959,6 +2011,13 @@ static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t 
         HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + 255, 0, 8, ctx->stream));
     }
     return HM_OK;
+}
+
+// partials per aggregated row of the batch just ingested (picks the next batch's k_ingest mode); only batches
+// with enough rows to tell
+static void note_agg_ratio(hm_ctx *ctx, const DevStats &s) {
+    const int64_t agg = (int64_t)s.n_valid - (int64_t)s.n_late;
+    if (agg >= (int64_t)1 << 16) ctx->agg_ratio = (double)s.n_partials / (double)agg;
 }
 
 static int ensure_outputs(hm_ctx *ctx, int64_t n_rows) {
@@ -2121,9 +2180,10 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     H3Tables T = make_tables();
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &T, sizeof(T)) != hipSuccess) { ctx->err = "tables"; return fail("create"); }
-    {
+    for (int direct = 0; direct < 2; direct++) {
+        const void *kern = direct ? (const void *)k_ingest<true> : (const void *)k_ingest<false>;
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_ingest, LA_THREADS, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, LA_THREADS, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) {
             ctx->err = "occupancy query";
             return fail("create");
@@ -2132,11 +2192,14 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         // boundaries: SGPR counts 81-112); k_ingest is persistent, so an extra block per CU would only run once
         // a resident one finished.  Bound it by the LDS each block takes.
         hipFuncAttributes fa{};
-        if (hipFuncGetAttributes(&fa, (const void *)k_ingest) == hipSuccess && fa.sharedSizeBytes > 0)
+        if (hipFuncGetAttributes(&fa, kern) == hipSuccess && fa.sharedSizeBytes > 0)
             per_cu = std::min<int>(per_cu, (int)(163840 / fa.sharedSizeBytes));
-        if (getenv("MOBHEAT_DEBUG")) fprintf(stderr, "mobheat: k_ingest %d blocks/CU x %d CUs (LDS %zu B)\n", per_cu, cus, fa.sharedSizeBytes);
-        ctx->ingest_grid = std::max(1, per_cu) * std::max(1, cus);
+        if (getenv("MOBHEAT_DEBUG"))
+            fprintf(stderr, "mobheat: k_ingest<%d> %d blocks/CU x %d CUs (LDS %zu B)\n", direct, per_cu, cus, fa.sharedSizeBytes);
+        ctx->ingest_grid[direct] = std::max(1, per_cu) * std::max(1, cus);
     }
+    // MOBHEAT_INGEST_MODE=lds|direct pins k_ingest's partial aggregation (tests); default: adaptive
+    if (const char *m = getenv("MOBHEAT_INGEST_MODE")) ctx->ingest_mode = !strcmp(m, "direct") ? 1 : !strcmp(m, "lds") ? 2 : 0;
     if (hipMalloc(&ctx->d_st, sizeof(DevStats)) != hipSuccess || hipHostMalloc(&ctx->h_st, sizeof(DevStats)) != hipSuccess ||
         hipMalloc(&ctx->d_scratch, 256 * 8) != hipSuccess || hipHostMalloc(&ctx->h_scratch, 256 * 8) != hipSuccess) {
         ctx->err = "stats alloc";
@@ -2235,6 +2298,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     DevStats s1 = *ctx->h_st;
+    note_agg_ratio(ctx, s1);
     // 3. merge into state + emit
     if ((rc = phase_merge_emit(ctx, (const TilePartial *)ctx->partials.p, (int64_t)s1.n_partials))) return rc;
     // 4. dedup over the batch's valid rows
@@ -2324,6 +2388,7 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     // local dedup over rows -> local winners -> candidates
+    note_agg_ratio(ctx, *ctx->h_st);
     if ((rc = phase_dedup(ctx, &I, nullptr, I.n, ctx->h_st->dedup_retry != 0))) return rc;
     if ((rc = ensure(ctx, ctx->cands, std::max<int64_t>(I.n, 1) * sizeof(Cand)))) return rc;
     hipLaunchKernelGGL(k_make_cands, dim3(grid_for(std::max<int64_t>(I.n, 1), 256)), dim3(256), 0, ctx->stream,

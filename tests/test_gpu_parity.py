@@ -324,3 +324,29 @@ def test_window_tables_growth_many_windows_and_reuse():
     res, exp = _run(eng, ora, b, len(plan))
     assert_batch_equal(res, exp)
     eng.close()
+
+
+@pytest.mark.parametrize("mode", ["direct", "lds"])
+def test_ingest_modes_parity(mode, monkeypatch):
+    """k_ingest's two partial-aggregation modes pinned (MOBHEAT_INGEST_MODE): LDS pre-aggregation and direct
+    (one partial per row, picked adaptively when nearly every key is distinct) give the oracle's results on a
+    multi-batch stream with late rows, ties, nulls, an empty batch, many windows and few hot keys."""
+    from mobheat import HeatmapEngine, synth
+    from oracle.spark_oracle import SparkHeatmapOracle
+    monkeypatch.setenv("MOBHEAT_INGEST_MODE", mode)
+    rng = np.random.default_rng(31)
+    eng = HeatmapEngine(h3_res=10)
+    ora = SparkHeatmapOracle(h3_res=10)
+    minute = 60_000_000
+    plan = [(0, 7, 40000, 500), (5, 6, 60000, 20), (0, 0, 0, 1), (14, 9, 30000, 500), (1, 300, 50000, 500),
+            (320, 4, 80000, 3)]
+    for epoch, (start, span, n, ncells) in enumerate(plan):
+        lat = 37.98 + rng.integers(0, ncells, n) * 2e-3 + rng.uniform(0, 1e-4, n)
+        lon = 23.73 + rng.uniform(-0.1, 0.1, n) if ncells > 100 else np.full(n, 23.73)
+        ts = synth.T0 + start * minute + rng.integers(0, max(span, 1) * minute, n)
+        ts[: n // 50] = ts[n // 50: 2 * (n // 50)]
+        b = dict(lat=lat, lon=lon, ts_us=ts, speed=rng.uniform(0, 90, n), speed_valid=rng.random(n) > 0.2,
+                 vkey=rng.integers(0, 700, n).astype(np.uint64), row_valid=rng.random(n) > 0.01)
+        res, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res, exp)
+    eng.close()
