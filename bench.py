@@ -37,11 +37,11 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector peak: 1024 SIMDs x 16 FMA lanes x
 SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 # algorithmic HBM bytes per unit: per event (ingest, dedup), per partial record (partition,
-# merge), per emitted tile (emit = the row compaction).  ingest also writes 64 B per partial (added below).
+# merge), per emitted tile (emit = the row compaction).  ingest also writes 48 B per partial (added below).
 BYTES = {
     "ingest": 43,      # read lat 8 + lon 8 + ts 8 + speed 8 + speed_valid 1 + vkey 8 + row_valid 1; write flags 1
-    "partition": 192,  # per 64-B partial: histogram read + scatter read + scatter write
-    "merge": 177,      # per partial: read 64 B record, write the 64 B state line (a new key: its slot tag is in
+    "partition": 144,  # per 48-B partial: histogram read + scatter read + scatter write
+    "merge": 161,      # per partial: read 48 B record, write the 64 B state line (a new key: its slot tag is in
                        # LDS, nothing read) and the 49 B update-mode row
     "emit": 98,        # per emitted tile: 49 B row read from the bin's segment, 49 B written densely
     "dedup": 20,       # per event: vkey 8 + ts 8 + flags 1 read, win flag 1 written, 2 x 1 B compaction reads
@@ -168,7 +168,7 @@ def main():
     n_parts = int(last.n_partials) if last is not None else 0
     units = {"ingest": n, "dedup": n, "partition": n_parts, "merge": n_parts, "emit": n_tiles}
     launch_bytes = {k: BYTES[k] * units[k] for k in BYTES}
-    launch_bytes["ingest"] += 64 * n_parts
+    launch_bytes["ingest"] += 48 * n_parts
     dom = max(BYTES, key=lambda k: avg_ms[k])
     gbs = launch_bytes[dom] / (avg_ms[dom] * 1e-3) / 1e9 if avg_ms[dom] > 0 else 0.0
     # Roofline of the dominant kernel, priced on HBM (the metric's "% HBM peak").  For k_ingest the PMC file

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 4
+#define HM_ABI_VERSION 5
 
 /* error codes */
 #define HM_OK 0
@@ -121,10 +121,9 @@ int hm_latlng_to_cell(const double *lat, const double *lon, int64_t n, int32_t r
 
 /* ---- multi-GPU stage API (one context per GPU/rank; the caller performs the exchanges) ----
  * Record layouts (little endian, packed):
- *   tile partial  (64 B): u64 cell, i64 window_start_us, i64 count, i64 n_speed, f64 sum_speed,
- *                         f64 sum_lat, f64 sum_lon, u64 key_hash (the producer's hash of (cell, window_start),
- *                         which routes the record to its owner rank and state region; the 8 B also pad the
- *                         record to one 64-B line so that scattered records are whole-line writes)
+ *   tile partial  (48 B): u64 cell, i64 window_start_us, u32 count, u32 n_speed, f64 sum_speed,
+ *                         f64 sum_lat, f64 sum_lon  (three 16-B parts; the owner rank and state region are
+ *                         functions of (cell, window_start), recomputed by every consumer)
  *   latest cand.  (32 B): u64 vkey, i64 ts_us, i64 row, i64 origin_rank
  * All exchange buffers are caller-owned device memory (e.g. torch tensors handed to RCCL), sized in records.
  * 1. hm_stage_local: snap + filter + window + local pre-aggregation + local latest candidates; both record
@@ -135,7 +134,7 @@ int hm_latlng_to_cell(const double *lat, const double *lon, int64_t n, int32_t r
  *    this rank owns, reduces the received candidates to winners, and writes the winners' row indices grouped
  *    by origin rank into winner_send_buf (capacity >= n_cand_recv) with per-origin counts.
  * 4. caller: exchange winners back; hm_stage_finish takes the received winners (rows of this rank). */
-#define HM_TILE_REC_BYTES 64
+#define HM_TILE_REC_BYTES 48
 #define HM_CAND_REC_BYTES 32
 typedef struct hm_stage_sizes {
     int64_t n_tile_partials;      /* total tile partial records produced locally */

@@ -28,19 +28,47 @@ struct alignas(64) TileSlot {
 };
 static_assert(sizeof(TileSlot) == 64, "TileSlot must be one 64-B line");
 
-// tile partial record exchanged between stages / ranks (HM_TILE_REC_BYTES = 64): one 64-B line, so the
-// radix scatter's randomly placed records are whole-line writes (no read-modify-write of partial lines)
-struct alignas(64) TilePartial {
+// tile partial record exchanged between stages / ranks (HM_TILE_REC_BYTES = 48): three 16-B parts, so that three
+// lanes move one record with 16-B accesses.  count/nspeed are a batch's rows (< 2^32).  The key's
+// hash is not carried: the consumers (partition, merge) recompute it -- they are memory-bound, and the bytes are
+// read and written five times per batch and sent over xGMI on several GPUs.
+struct alignas(16) TilePartial {
     uint64_t cell;
     int64_t wstart;
-    int64_t count;
-    int64_t nspeed;
+    uint32_t count;
+    uint32_t nspeed;
     double sspeed;
     double slat;
     double slon;
-    uint64_t aux;   // tile_hash(cell, wstart), computed once by the producer; growth records: the slot's touched word
 };
-static_assert(sizeof(TilePartial) == 64, "TilePartial is 64 B");
+static_assert(sizeof(TilePartial) == 48, "TilePartial is 48 B");
+// a partial after the radix partition (k_rp_scatter): one 64-B line, so that the scatter's randomly placed records
+// are whole-line writes (48-B records straddle 32-B sectors: partition 4.4 -> 7.3 ms), carrying the key's hash
+// for the merge
+struct alignas(64) SortedRec {
+    uint64_t cell;
+    int64_t wstart;
+    uint64_t count;
+    uint64_t nspeed;
+    double sspeed;
+    double slat;
+    double slon;
+    uint64_t hash;   // tile_hash(cell, wstart)
+};
+static_assert(sizeof(SortedRec) == 64, "SortedRec is 64 B");
+// growth record: a live key of a window's old table moved into its new one (k_dump_gen -> rehash merge); keeps the
+// slot's cumulative u64 counts and its touched word
+struct alignas(64) GrowRec {
+    uint64_t cell;
+    int64_t wstart;
+    uint64_t count;
+    uint64_t nspeed;
+    double sspeed;
+    double slat;
+    double slon;
+    uint64_t touched;
+};
+static_assert(sizeof(GrowRec) == 64, "GrowRec is 64 B");
 
 // latest-position candidate (HM_CAND_REC_BYTES = 32)
 struct Cand {

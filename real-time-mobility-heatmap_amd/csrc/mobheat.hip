@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/mobheat.h"
@@ -289,13 +290,12 @@ __device__ __forceinline__ unsigned la_slot(uint64_t key) {
     return (unsigned)((key * UINT64_C(0x9e3779b97f4a7c15)) >> 40) & (LA_SLOTS - 1);
 }
 
-struct LaShared {   // (the six slot arrays are consecutive: la_flush addresses them as words[6][LA_SLOTS])
+struct LaShared {   // (the five slot arrays are consecutive: la_flush addresses them as words[5][LA_SLOTS])
     unsigned long long key[LA_SLOTS];   // la_key, LA_EMPTY = free
-    unsigned long long cnt[LA_SLOTS];   // low 32: count, high 32: n_speed
+    unsigned long long cnt[LA_SLOTS];   // low 32: count, high 32: n_speed (= TilePartial's count, nspeed words)
     double ssp[LA_SLOTS];
     double slat[LA_SLOTS];
     double slon[LA_SLOTS];
-    unsigned long long aux[LA_SLOTS];   // la_flush: the key's tile_hash
     unsigned short order[LA_SLOTS];     // la_flush: output record -> slot
     long long wt[LA_WT];                // window starts (EMPTY_WIN = free)
     unsigned wcnt[LA_WT];               // partials per window at a flush (the census)
@@ -331,14 +331,13 @@ __device__ __forceinline__ bool la_direct(TilePartial *out, DevStats *st, WinLds
     p.sspeed = sp;
     p.slat = la;
     p.slon = lo;
-    p.aux = tile_hash(cell, ws);
     out[atomicAdd(&st->n_partials, 1ull)] = p;
     return wl_add(WL, census, wenc_of(ws), 1ull);
 }
 
 // partial records of the table's keys; resets the table and the window table.  Pass 1 (a thread per two slots)
-// numbers the keys, hashes them and counts them per window; pass 2 writes the records with four lanes per 64-B
-// record, 16 B each, so that every store instruction covers 16 whole records.
+// numbers the keys and counts them per window; pass 2 writes the records with three lanes per 48-B record, 16 B
+// each, so that every store instruction covers 21 whole records.
 __device__ void la_flush(LaShared &S, uint64_t cell_hi, TilePartial *out, DevStats *st, WinLds &WL, const CensusSink &census,
                          bool &ok) {
     __syncthreads();
@@ -367,25 +366,24 @@ __device__ void la_flush(LaShared &S, uint64_t cell_hi, TilePartial *out, DevSta
         const uint64_t k = S.key[s];
         if (k != LA_EMPTY) {
             const unsigned widx = (unsigned)(k >> 52);
-            S.aux[s] = tile_hash((k & LA_CELL_LO) | cell_hi, S.wt[widx]);
             S.order[idx++] = (unsigned short)s;
             atomicAdd(&S.wcnt[widx], 1u);
         }
     }
     __syncthreads();
-    {
-        const unsigned long long *W = S.key;   // words[6][LA_SLOTS]: key, cnt, ssp, slat, slon, aux
+    if (t < 3 * (LA_THREADS / 3)) {
+        const unsigned long long *W = S.key;   // words[5][LA_SLOTS]: key, cnt, ssp, slat, slon
         uint4 *__restrict__ o4 = (uint4 *)(out + S.base);
-        const int qq = t & 3;
-        const int i1 = qq == 0 ? 0 : qq == 1 ? 1 : qq == 2 ? 2 : 4;
-        const int i2 = qq == 2 ? 3 : 5;
-        for (unsigned r = (unsigned)t >> 2; r < total; r += LA_THREADS / 4) {
+        const int qq = t % 3;
+        // part 0: (cell, window start), 1: (count | n_speed, sum speed), 2: (sum lat, sum lon)
+        const int i1 = qq == 0 ? 0 : qq == 1 ? 1 : 3;
+        const int i2 = qq == 1 ? 2 : 4;
+        for (unsigned r = (unsigned)t / 3; r < total; r += LA_THREADS / 3) {
             const unsigned s = S.order[r];
             const uint64_t w1 = W[i1 * LA_SLOTS + s], w2 = W[i2 * LA_SLOTS + s];
-            const uint64_t wsv = (uint64_t)S.wt[(w1 >> 52) & (LA_WT - 1)];
-            const uint64_t a = qq == 0 ? (w1 & LA_CELL_LO) | cell_hi : qq == 1 ? (w1 & 0xffffffffull) : w1;
-            const uint64_t b = qq == 0 ? wsv : qq == 1 ? (w1 >> 32) : w2;
-            o4[(uint64_t)r * 4 + qq] = make_uint4((unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32));
+            const uint64_t a = qq == 0 ? (w1 & LA_CELL_LO) | cell_hi : w1;
+            const uint64_t b = qq == 0 ? (uint64_t)S.wt[(w1 >> 52) & (LA_WT - 1)] : w2;
+            o4[(uint64_t)r * 3 + qq] = make_uint4((unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32));
         }
     }
     __syncthreads();
@@ -428,24 +426,24 @@ __global__ __launch_bounds__(256) void k_census(const TilePartial *__restrict__ 
 
 // growth: the live keys of one window's old table as partial records (aux = the key's touched word), to be
 // merged into its new table by k_merge_owned in rehash mode
-__global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, TilePartial *__restrict__ out, unsigned long long *n_out) {
+__global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, GrowRec *__restrict__ out, unsigned long long *n_out) {
     const unsigned long long cap = (g.rmask + 1) << g.rbits;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < (int64_t)cap; base += stride) {
         const int64_t i = base + threadIdx.x;
         bool live = false;
-        TilePartial p;
+        GrowRec p;
         if (i < (int64_t)cap) {
             const TileSlot sl = g.tab[i];
             live = sl.wenc == g.wenc;
             p.cell = sl.cell;
             p.wstart = wdec(sl.wenc);
-            p.count = (int64_t)sl.count;
-            p.nspeed = (int64_t)sl.nspeed;
+            p.count = sl.count;
+            p.nspeed = sl.nspeed;
             p.sspeed = sl.sspeed;
             p.slat = sl.slat;
             p.slon = sl.slon;
-            p.aux = sl.touched;
+            p.touched = sl.touched;
         }
         const unsigned long long pos = wave_append(live, n_out);
         if (live) out[pos] = p;
@@ -465,18 +463,20 @@ constexpr int RP_BINS = 1 << RP_BITS;
 constexpr int RP_TILE = HM_RP_TILE;    // partials per tile (one workgroup)
 constexpr int RP_THREADS = 256;
 
-// the radix digit of a partial: its (window, region) bin, or with nranks > 0 its owner rank (the multi-GPU
-// exchange, hm_stage_local); aux_hash: the records carry their key hash in aux (not growth records)
-__device__ __forceinline__ unsigned rp_digit(const TilePartial &p, const GenCache &C, const GenDesc *gm, bool aux_hash,
-                                             int nranks, bool &bad) {
-    if (nranks > 0) return (unsigned)owner_of(p.aux, nranks);
-    const int b = bin_of_c(C, gm, aux_hash ? p.aux : tile_hash(p.cell, p.wstart), p.wstart);
+// the radix digit of a key: its (window, region) bin, or with nranks > 0 its owner rank (the multi-GPU
+// exchange, hm_stage_local)
+__device__ __forceinline__ unsigned rp_digit(uint64_t cell, int64_t ws, const GenCache &C, const GenDesc *gm, int nranks,
+                                             bool &bad) {
+    const uint64_t h = tile_hash(cell, ws);
+    if (nranks > 0) return (unsigned)owner_of(h, nranks);
+    const int b = bin_of_c(C, gm, h, ws);
     bad |= b < 0;
     return b < 0 ? 0u : (unsigned)b;
 }
 
-__global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const TilePartial *__restrict__ parts, int64_t n, const GenDesc *gm,
-                                                       const GenDesc *glist, int n_glist, int aux_hash, int nranks, int nbins,
+template <typename Rec>
+__global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const Rec *__restrict__ parts, int64_t n, const GenDesc *gm,
+                                                       const GenDesc *glist, int n_glist, int nranks, int nbins,
                                                        unsigned *__restrict__ H, int64_t ntiles, DevStats *st) {
     __shared__ unsigned h[RP_BINS];
     __shared__ GenCache C;
@@ -486,7 +486,8 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const TilePartial *__res
     int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
     int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
     bool bad = false;
-    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) atomicAdd(&h[rp_digit(parts[i], C, gm, aux_hash, nranks, bad)], 1u);
+    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS)
+        atomicAdd(&h[rp_digit(parts[i].cell, parts[i].wstart, C, gm, nranks, bad)], 1u);
     __syncthreads();
     for (int d = threadIdx.x; d < nbins; d += RP_THREADS) H[(int64_t)d * ntiles + blockIdx.x] = h[d];
     if (__ballot(bad) && lane_id() == 0) atomicAdd(&st->overflow, 1ull);
@@ -526,39 +527,90 @@ __global__ __launch_bounds__(256) void k_scan_add(unsigned long long *__restrict
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) out[i] += block_off[i / SC_PER];
 }
 
-__global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const TilePartial *__restrict__ parts, int64_t n,
-                                                          const GenDesc *gm, const GenDesc *glist, int n_glist, int aux_hash,
+// output part q (16 B) of record `rec` of a wave's 64: In = Out is a plain copy; TilePartial (48 B) -> SortedRec
+// (64 B) widens the counts and appends the key hash the digit lane computed
+template <typename In, typename Out>
+__device__ __forceinline__ uint4 rp_part(const uint4 *__restrict__ src, int64_t rec, int q, uint64_t h) {
+    if constexpr (std::is_same<In, Out>::value) {
+        return src[rec * (sizeof(In) / 16) + q];
+    } else {
+        static_assert(std::is_same<In, TilePartial>::value && std::is_same<Out, SortedRec>::value, "conversion");
+        const uint4 *r = src + rec * 3;
+        if (q == 0) return r[0];
+        if (q == 1) { const uint4 a = r[1]; return make_uint4(a.x, 0u, a.y, 0u); }
+        if (q == 2) { const uint4 a = r[1], b = r[2]; return make_uint4(a.z, a.w, b.x, b.y); }
+        const uint4 b = r[2];
+        return make_uint4(b.z, b.w, (unsigned)h, (unsigned)(h >> 32));
+    }
+}
+
+// Per wave and iteration, 64 records: each lane reads its record's first 16 B (cell, window start) and takes its
+// digit and position (all lanes busy with the hash); then the wave writes the 64 records as sizeof(Out)/16 rounds
+// of 16-B parts, whole 64-B lines at random places -- per-lane 64-B records bounded this kernel's vector-memory
+// issue (6.4 -> 3.5 ms per 1e8 records).
+template <typename In, typename Out>
+__global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict__ parts, int64_t n,
+                                                          const GenDesc *gm, const GenDesc *glist, int n_glist,
                                                           int nranks, int nbins, const unsigned long long *__restrict__ O,
-                                                          int64_t ntiles, TilePartial *__restrict__ dst) {
+                                                          int64_t ntiles, Out *__restrict__ dst) {
+    constexpr int QI = sizeof(In) / 16, QO = sizeof(Out) / 16;
+    constexpr bool widen = !std::is_same<In, Out>::value;
     __shared__ unsigned cur[RP_BINS];   // positions < 2^32 (partition() checks n)
     __shared__ GenCache C;
+    __shared__ uint4 stage[widen ? (RP_THREADS / 64) * 64 * QI : 1];   // widening: each wave's 64 input records
     gc_load(C, glist, n_glist);
     for (int d = threadIdx.x; d < nbins; d += RP_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
     __syncthreads();
-    // four lanes per record, 16 B each: every load/store instruction covers 16 whole 64-B records (16 lines)
-    // instead of one line per lane, which is what bounds this kernel's vector-memory issue
     const int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
     const int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
     const uint4 *__restrict__ src = (const uint4 *)parts;
     uint4 *__restrict__ d4 = (uint4 *)dst;
-    const int q = threadIdx.x & 3, lead = (int)(lane_id() & ~3);
-    for (int64_t i = t0 + (threadIdx.x >> 2); i - (threadIdx.x >> 2) < t1; i += RP_THREADS / 4) {
-        const bool in = i < t1;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (in) v = src[i * 4 + q];
-        // the lead lane of the record gathers cell, wstart (its own quarter) and the hash (quarter 3)
-        const unsigned hz = __shfl(v.z, lead + 3, 64), hw = __shfl(v.w, lead + 3, 64);
+    const int ln = lane_id();
+    for (int64_t i0 = t0 + (int64_t)(threadIdx.x >> 6) * 64; i0 < t1; i0 += RP_THREADS) {
+        const int64_t i = i0 + ln;
         unsigned pos = 0;
-        if (in && q == 0) {
-            TilePartial p;
-            p.cell = (uint64_t)v.x | ((uint64_t)v.y << 32);
-            p.wstart = (int64_t)((uint64_t)v.z | ((uint64_t)v.w << 32));
-            p.aux = (uint64_t)hz | ((uint64_t)hw << 32);
+        uint64_t h = 0;
+        if (i < t1) {
+            const uint4 k = src[i * QI];   // part 0 = (cell, window start)
+            const uint64_t cell = (uint64_t)k.x | ((uint64_t)k.y << 32);
+            const int64_t ws = (int64_t)((uint64_t)k.z | ((uint64_t)k.w << 32));
+            h = tile_hash(cell, ws);
             bool bad = false;
-            pos = atomicAdd(&cur[rp_digit(p, C, gm, aux_hash, nranks, bad)], 1u);
+            unsigned d;
+            if (nranks > 0) {
+                d = (unsigned)owner_of(h, nranks);
+            } else {
+                const int b = bin_of_c(C, gm, h, ws);
+                d = b < 0 ? 0u : (unsigned)b;
+                bad = b < 0;
+            }
+            (void)bad;
+            pos = atomicAdd(&cur[d], 1u);
         }
-        pos = __shfl(pos, lead, 64);
-        if (in) d4[(int64_t)pos * 4 + q] = v;
+        const int64_t nrec = t1 - i0 < 64 ? t1 - i0 : 64;
+        if constexpr (widen) {
+            // the wave's records through LDS: QI contiguous 1-KB loads in, then each lane builds output parts
+            uint4 *ws = stage + (threadIdx.x >> 6) * 64 * QI;
+            for (int r = 0; r < QI; r++) {
+                const int idx = r * 64 + ln;
+                if (idx < nrec * QI) ws[idx] = src[i0 * QI + idx];
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            for (int r = 0; r < QO; r++) {
+                const int idx = r * 64 + ln, rec = idx / QO, q = idx % QO;
+                const unsigned p = __shfl(pos, rec, 64);
+                const unsigned hl = __shfl((unsigned)h, rec, 64), hh = __shfl((unsigned)(h >> 32), rec, 64);
+                if (rec < nrec) d4[(int64_t)p * QO + q] = rp_part<In, Out>(ws, rec, q, (uint64_t)hl | ((uint64_t)hh << 32));
+            }
+            __builtin_amdgcn_wave_barrier();
+        } else {
+            for (int r = 0; r < QO; r++) {
+                const int idx = r * 64 + ln, rec = idx / QO, q = idx % QO;
+                const unsigned p = __shfl(pos, rec, 64);
+                if (rec < nrec) d4[(int64_t)p * QO + q] = src[(i0 + rec) * QI + q];
+            }
+        }
     }
 }
 
@@ -642,7 +694,8 @@ __device__ __forceinline__ int mo_holder(MoShared &S, unsigned long long addr) {
     return -1;
 }
 // a duplicate of lane x's key: add this record's values into x's staging entry
-__device__ __forceinline__ void mo_add_into(MoShared &S, int x, const TilePartial &p) {
+template <typename Rec>
+__device__ __forceinline__ void mo_add_into(MoShared &S, int x, const Rec &p) {
     atomicAdd(&S.scnt[x], (unsigned long long)p.count);
     if (p.nspeed) {
         atomicAdd(&S.snsp[x], (unsigned long long)p.nspeed);
@@ -675,11 +728,13 @@ __device__ __forceinline__ void put_row(const RowsOut &o, int64_t t, uint64_t ce
     o.lat[t] = slat / (double)count;
 }
 
-__global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *__restrict__ parts, int64_t n,
+// Rec = SortedRec: a batch's partials (partitioned); Rec = GrowRec: growth (rehash)
+template <typename Rec>
+__global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restrict__ parts, int64_t n,
                                                             const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
                                                             GenDesc *gm, const GenDesc *glist, int n_glist,
-                                                            unsigned seq, int rehash, RowsOut rows,
-                                                            unsigned *bin_cnt, DevStats *st) {
+                                                            unsigned seq, RowsOut rows, unsigned *bin_cnt, DevStats *st) {
+    constexpr bool rehash = std::is_same<Rec, GrowRec>::value;
     __shared__ MoShared S;
     __shared__ WinLds WL;
     __shared__ GenCache C;
@@ -730,16 +785,18 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
         }
         __syncthreads();
         // software pipeline: the next chunk's record is loaded while this chunk is merged
-        TilePartial nxt;
+        Rec nxt;
         if (b0 + t < b1) nxt = parts[b0 + t];
         for (int64_t c0 = b0; c0 < b1; c0 += MO_THREADS) {
             // 1. stage this chunk's records in LDS
             const int64_t i = c0 + t;
             const bool has = i < b1;
-            const TilePartial p = nxt;
+            const Rec p = nxt;
             if (i + MO_THREADS < b1) nxt = parts[i + MO_THREADS];
             const unsigned long long we = wenc_of(p.wstart);
-            const uint64_t hk = rehash ? tile_hash(p.cell, p.wstart) : p.aux;
+            uint64_t hk;
+            if constexpr (rehash) hk = tile_hash(p.cell, p.wstart);
+            else hk = p.hash;
             if (has) {
                 S.sc[t] = p.cell;
                 S.sh[t] = hk;
@@ -850,7 +907,8 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const TilePartial *_
                 v.sspeed = ansp ? ossp + S.sssp[t] : ossp;
                 v.slat = oslat + S.sslat[t];
                 v.slon = oslon + S.sslon[t];
-                v.touched = rehash ? p.aux : ((unsigned long long)seq << 32) | krow;
+                if constexpr (rehash) v.touched = p.touched;
+                else v.touched = ((unsigned long long)seq << 32) | krow;
                 if (created) {
                     *gslot = v;
                     created_cnt++;
@@ -1195,26 +1253,23 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
                     total += S.scan[k];
                 }
                 if (threadIdx.x == 0) S.base = total ? atomicAdd(&st->n_partials, (unsigned long long)total) : 0;
-                uint4 *stage = (uint4 *)S.key;   // key, cnt, ssp, slat: 16 KB = 256 records
+                uint4 *stage = (uint4 *)S.key;   // key, cnt, ssp: 12 KB = 256 records
                 if (rec) {
                     const unsigned r = woff + (unsigned)__popcll(bal & ((1ull << lane_id()) - 1));
                     const bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
                     const double sp = sv ? speed[i] : 0.0;
                     const int64_t ws = widx >= 0 ? (int64_t)S.wt[widx] : floor_div(t, wdiv) * tile_us;
-                    const uint64_t h = tile_hash(cell, ws);
                     const uint64_t spb = __builtin_bit_cast(uint64_t, sp), lab = __builtin_bit_cast(uint64_t, la),
                                    lob = __builtin_bit_cast(uint64_t, lo);
-                    stage[r * 4 + 0] = make_uint4((unsigned)cell, (unsigned)(cell >> 32), (unsigned)ws, (unsigned)((uint64_t)ws >> 32));
-                    stage[r * 4 + 1] = make_uint4(1u, 0u, sv ? 1u : 0u, 0u);
-                    stage[r * 4 + 2] = make_uint4((unsigned)spb, (unsigned)(spb >> 32), (unsigned)lab, (unsigned)(lab >> 32));
-                    stage[r * 4 + 3] = make_uint4((unsigned)lob, (unsigned)(lob >> 32), (unsigned)h, (unsigned)(h >> 32));
+                    stage[r * 3 + 0] = make_uint4((unsigned)cell, (unsigned)(cell >> 32), (unsigned)ws, (unsigned)((uint64_t)ws >> 32));
+                    stage[r * 3 + 1] = make_uint4(1u, sv ? 1u : 0u, (unsigned)spb, (unsigned)(spb >> 32));
+                    stage[r * 3 + 2] = make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32));
                     if (widx >= 0) atomicAdd(&S.wcnt[widx], 1u);
                     else census_ok &= wl_add(WL, census, wenc_of(ws), 1ull);
                 }
                 __syncthreads();
                 uint4 *__restrict__ o4 = (uint4 *)(out + S.base);
-                for (unsigned r = (unsigned)threadIdx.x >> 2; r < total; r += LA_THREADS / 4)
-                    o4[(uint64_t)r * 4 + (threadIdx.x & 3)] = stage[r * 4 + (threadIdx.x & 3)];
+                for (unsigned k = threadIdx.x; k < 3 * total; k += LA_THREADS) o4[k] = stage[k];   // contiguous 48-B records
                 __syncthreads();
             } else {
             // LDS pre-aggregation of the window's rows
@@ -1314,7 +1369,6 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
             p.sspeed = sv ? speed[i] : 0.0;
             p.slat = lat[i];
             p.slon = lon[i];
-            p.aux = tile_hash(p.cell, p.wstart);
         }
         const unsigned long long pos = wave_append(in, &st->n_partials);
         if (in) out[pos] = p;
@@ -1409,7 +1463,7 @@ template <typename Rec>
 __device__ __forceinline__ int rec_owner(const Rec &r, int nranks);
 template <>
 __device__ __forceinline__ int rec_owner<TilePartial>(const TilePartial &r, int nranks) {
-    return owner_of(r.aux, nranks);   // the producer's tile_hash
+    return owner_of(tile_hash(r.cell, r.wstart), nranks);
 }
 template <>
 __device__ __forceinline__ int rec_owner<Cand>(const Cand &r, int nranks) {
@@ -1708,30 +1762,31 @@ static int gens_upload(hm_ctx *ctx) {
 
 // radix partition of n partial records into RP_BINS bins (one per (window, region)); the sorted copy goes to
 // ctx->parts_sorted, bin b starts at rp_O[b * ntiles]
-static int partition(hm_ctx *ctx, const TilePartial *parts, int64_t n, int aux_hash, int64_t &ntiles, int nranks = 0,
-                     TilePartial *dst = nullptr) {
+// In -> Out: TilePartial -> SortedRec (a batch's partials, into parts_sorted), GrowRec -> GrowRec (growth, into
+// parts_sorted), TilePartial -> TilePartial (the owner partition, into the caller's send buffer)
+template <typename In, typename Out>
+static int partition(hm_ctx *ctx, const In *parts, int64_t n, int64_t &ntiles, int nranks = 0, Out *dst = nullptr) {
     const int nbins = nranks > 0 ? nranks : RP_BINS;
     if (n > (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "%lld partial records in one merge exceed 2^32-1", (long long)n);
     ntiles = std::max<int64_t>((n + RP_TILE - 1) / RP_TILE, 1);
     const int64_t m = (int64_t)nbins * ntiles;
     const int64_t nb = (m + SC_PER - 1) / SC_PER;
     int rc;
-    if (!dst && (rc = ensure(ctx, ctx->parts_sorted, std::max<int64_t>(n, 1) * sizeof(TilePartial)))) return rc;
+    if (!dst && (rc = ensure(ctx, ctx->parts_sorted, std::max<int64_t>(n, 1) * sizeof(Out)))) return rc;
     if ((rc = ensure(ctx, ctx->rp_H, m * 4)) || (rc = ensure(ctx, ctx->rp_O, m * 8)) || (rc = ensure(ctx, ctx->rp_btot, nb * 4)) ||
         (rc = ensure(ctx, ctx->rp_boff, nb * 8)))
         return rc;
-    hipLaunchKernelGGL(k_rp_hist, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, (const GenDesc *)ctx->d_gmap,
-                       (const GenDesc *)ctx->d_glist, ctx->n_glist, aux_hash, nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles,
-                       ctx->d_st);
+    hipLaunchKernelGGL(k_rp_hist<In>, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, (const GenDesc *)ctx->d_gmap,
+                       (const GenDesc *)ctx->d_glist, ctx->n_glist, nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles, ctx->d_st);
     hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_H.p, m,
                        (unsigned long long *)ctx->rp_O.p, (unsigned *)ctx->rp_btot.p);
     hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_btot.p, nb,
                        (unsigned long long *)ctx->rp_boff.p, ctx->d_scratch + 254);
     hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, (unsigned long long *)ctx->rp_O.p, m,
                        (const unsigned long long *)ctx->rp_boff.p);
-    hipLaunchKernelGGL(k_rp_scatter, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, (const GenDesc *)ctx->d_gmap,
-                       (const GenDesc *)ctx->d_glist, ctx->n_glist, aux_hash, nranks, nbins, (const unsigned long long *)ctx->rp_O.p,
-                       ntiles, dst ? dst : (TilePartial *)ctx->parts_sorted.p);
+    hipLaunchKernelGGL((k_rp_scatter<In, Out>), dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n,
+                       (const GenDesc *)ctx->d_gmap, (const GenDesc *)ctx->d_glist, ctx->n_glist, nranks, nbins,
+                       (const unsigned long long *)ctx->rp_O.p, ntiles, dst ? dst : (Out *)ctx->parts_sorted.p);
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
 }
@@ -1747,7 +1802,9 @@ static RowsOut staged_rows(hm_ctx *ctx) {
 // the batch sequence number kept in the slots' touched words (32 bits, never 0: fresh slots hold 0)
 static unsigned seq32(const hm_ctx *ctx) { return (unsigned)(ctx->seq % 0xffffffffull) + 1u; }
 
-static int merge_sorted(hm_ctx *ctx, int64_t n, int64_t ntiles, int rehash) {
+template <typename Rec>
+static int merge_sorted(hm_ctx *ctx, int64_t n, int64_t ntiles) {
+    constexpr bool rehash = std::is_same<Rec, GrowRec>::value;
     int rc;
     if ((rc = ensure(ctx, ctx->bin_cnt, RP_BINS * 4)) || (rc = ensure(ctx, ctx->bin_off, RP_BINS * 8)))
         return rc;
@@ -1758,9 +1815,9 @@ static int merge_sorted(hm_ctx *ctx, int64_t n, int64_t ntiles, int rehash) {
             (rc = ensure(ctx, ctx->s_lat, m * 8)))
             return rc;
     }
-    hipLaunchKernelGGL(k_merge_owned, dim3(RP_BINS), dim3(MO_THREADS), 0, ctx->stream, (const TilePartial *)ctx->parts_sorted.p, n,
+    hipLaunchKernelGGL(k_merge_owned<Rec>, dim3(RP_BINS), dim3(MO_THREADS), 0, ctx->stream, (const Rec *)ctx->parts_sorted.p, n,
                        (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
-                       ctx->n_glist, seq32(ctx), rehash, staged_rows(ctx), (unsigned *)ctx->bin_cnt.p, ctx->d_st);
+                       ctx->n_glist, seq32(ctx), staged_rows(ctx), (unsigned *)ctx->bin_cnt.p, ctx->d_st);
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
 }
@@ -1813,7 +1870,7 @@ static int gens_prepare(hm_ctx *ctx, const TilePartial *parts, int64_t n) {
     if (!old.empty()) {
         int64_t moved = 0;
         for (const auto &g : old) moved += g.keys;
-        if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(moved, 1) * sizeof(TilePartial)))) return rc;
+        if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(moved, 1) * sizeof(GrowRec)))) return rc;
         HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
         for (const auto &g : old) {
             GenDesc d{};
@@ -1823,12 +1880,12 @@ static int gens_prepare(hm_ctx *ctx, const TilePartial *parts, int64_t n) {
             d.rshift = (unsigned)g.log2cap - g.rbits;
             d.rmask = (UINT64_C(1) << d.rshift) - 1;
             hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
-                               (TilePartial *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD);
+                               (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD);
         }
         HIPCHK(ctx, hipGetLastError());
         int64_t ntiles;
-        if ((rc = partition(ctx, (const TilePartial *)ctx->parts_regrow.p, moved, 0, ntiles))) return rc;
-        if ((rc = merge_sorted(ctx, moved, ntiles, 1))) return rc;
+        if ((rc = partition<GrowRec, GrowRec>(ctx, (const GrowRec *)ctx->parts_regrow.p, moved, ntiles))) return rc;
+        if ((rc = merge_sorted<GrowRec>(ctx, moved, ntiles))) return rc;
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         for (const auto &g : old) table_release(ctx, g.tab, g.log2cap);
     }
@@ -2046,9 +2103,9 @@ static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_par
     if ((rc = gens_prepare(ctx, parts, n_parts))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
     int64_t ntiles;
-    if ((rc = partition(ctx, parts, n_parts, 1, ntiles))) return rc;
+    if ((rc = partition<TilePartial, SortedRec>(ctx, parts, n_parts, ntiles))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
-    if ((rc = merge_sorted(ctx, n_parts, ntiles, 0))) return rc;
+    if ((rc = merge_sorted<SortedRec>(ctx, n_parts, ntiles))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
     hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->bin_cnt.p, (int64_t)RP_BINS,
                        (unsigned long long *)ctx->bin_off.p, &ctx->d_st->n_touched);
@@ -2224,7 +2281,8 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         const int64_t n = cfg->batch_capacity_hint;
         const size_t tp = sizeof(TilePartial);
         if (ensure(ctx, ctx->flags, n) || ensure(ctx, ctx->win, n) || ensure(ctx, ctx->rows, n * 8) ||
-            ensure(ctx, ctx->partials, n * tp) || ensure(ctx, ctx->slow, n * 4) || ensure(ctx, ctx->parts_sorted, n * tp) ||
+            ensure(ctx, ctx->partials, n * tp) || ensure(ctx, ctx->slow, n * 4) ||
+            ensure(ctx, ctx->parts_sorted, n * sizeof(SortedRec)) ||
             ensure(ctx, ctx->s_cell, n * 8) || ensure(ctx, ctx->s_ws, n * 8) || ensure(ctx, ctx->s_cnt, n * 8) ||
             ensure(ctx, ctx->s_sp, n * 8) || ensure(ctx, ctx->s_spn, n) || ensure(ctx, ctx->s_lon, n * 8) ||
             ensure(ctx, ctx->s_lat, n * 8) || ensure_outputs(ctx, n))
@@ -2421,7 +2479,8 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     const int64_t n_parts = (int64_t)ctx->h_st->n_partials;
     if (n_parts > 0) {
         int64_t ntiles;
-        if ((rc = partition(ctx, (const TilePartial *)ctx->partials.p, n_parts, 1, ntiles, nranks, (TilePartial *)tile_send_buf)))
+        if ((rc = partition<TilePartial, TilePartial>(ctx, (const TilePartial *)ctx->partials.p, n_parts, ntiles, nranks,
+                                                      (TilePartial *)tile_send_buf)))
             return rc;
         hipLaunchKernelGGL(k_digit_starts, dim3(1), dim3(64), 0, ctx->stream, (const unsigned long long *)ctx->rp_O.p, ntiles, nranks,
                            ctx->d_scratch);

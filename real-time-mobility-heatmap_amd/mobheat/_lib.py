@@ -14,10 +14,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MOBHEAT_LIB: load another build of the same ABI (kernel variants under csrc/variants/ for tuning runs)
 LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
 
-HM_ABI_VERSION = 4
+HM_ABI_VERSION = 5
 HM_MEM_HOST = 0
 HM_MEM_DEVICE = 1
-HM_TILE_REC_BYTES = 64
+HM_TILE_REC_BYTES = 48
 HM_CAND_REC_BYTES = 32
 
 c_i32, c_i64, c_u64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double, ctypes.c_void_p

@@ -4,7 +4,7 @@ Replaces Spark's shuffle of the two aggregations (spark.sql.shuffle.partitions =
 heatmap_stream.py:44): every rank snaps and pre-aggregates its own shard of the micro-batch, then ONE
 all-to-all per record kind routes
 
-  * tile partials  (64-B records: cell, windowStart, count, n_speed, sum speed/lat/lon, key hash) to owner rank
+  * tile partials  (48-B records: cell, windowStart, count, n_speed, sum speed/lat/lon) to owner rank
     hash(cell, windowStart) % world, which merges them into the persistent state it owns and emits them;
   * latest-position candidates (32-B records: vkey, ts, row, origin rank) to owner hash(vkey) % world,
     which keeps the rows tied at the global max and routes the winning row indices back to their origin;

@@ -16,8 +16,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-TILE_DT = np.dtype([("cell", "<u8"), ("ws", "<i8"), ("count", "<i8"), ("nsp", "<i8"), ("ssp", "<f8"), ("slat", "<f8"),
-                    ("slon", "<f8"), ("key_hash", "<u8")])   # HM_TILE_REC_BYTES = 64
+TILE_DT = np.dtype([("cell", "<u8"), ("ws", "<i8"), ("count", "<u4"), ("nsp", "<u4"), ("ssp", "<f8"), ("slat", "<f8"),
+                    ("slon", "<f8")])   # HM_TILE_REC_BYTES = 48
 CAND_DT = np.dtype([("vkey", "<u8"), ("ts", "<i8"), ("row", "<i8"), ("origin", "<i8")])
 
 
@@ -50,8 +50,7 @@ class OracleStages:
             recs["ssp"] = np.bincount(inv[sv], weights=b["speed"][agg][sv], minlength=uq.size)
             recs["slat"] = np.bincount(inv, weights=b["lat"][agg], minlength=uq.size)
             recs["slon"] = np.bincount(inv, weights=b["lon"][agg], minlength=uq.size)
-        recs["key_hash"] = tile_hash(recs["cell"], recs["ws"])
-        own = owner_of(recs["key_hash"], world)
+        own = owner_of(tile_hash(recs["cell"], recs["ws"]), world)
         order = np.argsort(own, kind="stable")
         tcounts = np.bincount(own, minlength=world).tolist()
         tile_send = torch.from_numpy(recs[order].view(np.uint8).copy())
