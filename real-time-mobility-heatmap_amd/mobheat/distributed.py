@@ -24,19 +24,23 @@ from ._lib import HM_CAND_REC_BYTES, HM_MEM_DEVICE, HM_MEM_HOST, HM_TILE_REC_BYT
 
 
 def exchange(send, send_counts, rec_bytes, device):
-    """all_to_all of variable-size record runs; send_counts[r] records go to rank r. Returns (recv, counts)."""
+    """all_to_all of variable-size record runs; send_counts[r] records go to rank r. Returns (recv, counts),
+    recv a uint8 tensor.  The payload moves as 8-byte words (records are 48, 32 or 8 bytes): a rank's share at
+    1e8 events per GPU is several GB, past 2^31 single-byte elements."""
     world = dist.get_world_size()
+    assert rec_bytes % 8 == 0
+    w = rec_bytes // 8
     sc = torch.tensor(send_counts, dtype=torch.int64, device=device)
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc)
     recv_counts = rc.cpu().tolist()
     nrecv = int(sum(recv_counts))
-    recv = torch.empty(max(nrecv * rec_bytes, 1), dtype=torch.uint8, device=device)
+    recv = torch.empty(max(nrecv * w, 2), dtype=torch.int64, device=device)
     nsend = int(sum(send_counts))
-    dist.all_to_all_single(recv[: nrecv * rec_bytes], send[: nsend * rec_bytes],
-                           [c * rec_bytes for c in recv_counts], [c * rec_bytes for c in send_counts])
+    dist.all_to_all_single(recv[: nrecv * w], send[: nsend * rec_bytes].view(torch.int64),
+                           [c * w for c in recv_counts], [c * w for c in send_counts])
     assert len(recv_counts) == world
-    return recv, recv_counts
+    return recv.view(torch.uint8), recv_counts
 
 
 class LibStages:
