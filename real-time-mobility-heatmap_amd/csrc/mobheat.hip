@@ -632,8 +632,11 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict_
 // rehash != 0: growth (k_dump_gen records, unique keys, into the window's new table): created slots keep the
 // record's touched word, no rows are written.
 // =====================================================================================================
-constexpr int MO_THREADS = 256;
-constexpr int MO_CLAIM = 512;
+#ifndef HM_MO_THREADS
+#define HM_MO_THREADS 512
+#endif
+constexpr int MO_THREADS = HM_MO_THREADS;      // partials per chunk (one per lane)
+constexpr int MO_CLAIM = 2 * MO_THREADS;
 #ifndef HM_MO_TAG_BYTES
 #define HM_MO_TAG_BYTES 24576
 #endif
