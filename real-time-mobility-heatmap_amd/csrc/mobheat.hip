@@ -270,7 +270,10 @@ __global__ __launch_bounds__(256) void k_cells_exact(const double *__restrict__ 
 // =====================================================================================================
 // K2: LDS pre-aggregation into partial records (persistent blocks, flush when the table fills)
 // =====================================================================================================
-constexpr int LA_THREADS = 256;
+#ifndef HM_LA_THREADS
+#define HM_LA_THREADS 256
+#endif
+constexpr int LA_THREADS = HM_LA_THREADS;
 #ifndef HM_LA_SLOTS
 #define HM_LA_SLOTS 512
 #endif
