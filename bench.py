@@ -97,7 +97,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--events", type=int, default=100_000_000, help="events per step per GPU")
     ap.add_argument("--res", type=int, default=8)
     ap.add_argument("--cpu-sample", type=int, default=3_000_000)
