@@ -521,8 +521,10 @@ HM_HD void sincos_small(double x, double &s, double &c) {
 HM_HD double dmin(double a, double b) { return a < b ? a : b; }
 
 // The fast path.  Returns false when the caller must use latLngToCellDeg; otherwise `out` is upstream's cell
-// (0 where the reference's UDF returns None).
-HM_HD bool latLngToCellFast(double lat_deg, double lng_deg, int res, const H3Tables &T, uint64_t &out) {
+// (0 where the reference's UDF returns None).  fc = T.faceCenterPoint, fu = T.fastU[res & 1], or copies of them
+// (k_ingest keeps them in LDS: lane-indexed reads there do not queue behind its outstanding global loads).
+HM_HD bool latLngToCellFastP(double lat_deg, double lng_deg, int res, const H3Tables &T, const double (*fc)[3],
+                             const double (*fu)[2][3], uint64_t &out) {
     out = 0;
     if (!(lat_deg >= -90.0 && lat_deg <= 90.0 && lng_deg >= -180.0 && lng_deg <= 180.0)) return true;
     double sl, cl, sg, cg;
@@ -541,11 +543,11 @@ HM_HD bool latLngToCellFast(double lat_deg, double lng_deg, int res, const H3Tab
         }
         if (!(best - second > 1e-5f)) return false;
     }
-    const double *c = T.faceCenterPoint[face];
+    const double *c = fc[face];
     const double pc = fma(px, c[0], fma(py, c[1], pz * c[2]));
     const double sqd = 2.0 - 2.0 * pc;
     if (!(sqd > 1e-12)) return false;                     // within ~6 m of a face centre: exact path
-    const double(*u)[3] = T.fastU[res & 1][face];
+    const double(*u)[3] = fu[face];
     const double S = T.fastScale[res];
     const double inv = S / pc;
     const double vx = fma(px, u[0][0], fma(py, u[0][1], pz * u[0][2])) * inv;
@@ -605,6 +607,9 @@ HM_HD bool latLngToCellFast(double lat_deg, double lng_deg, int res, const H3Tab
     ijkNormalize(h);
     out = faceIjkToH3(face, h, res, T);
     return true;
+}
+HM_HD bool latLngToCellFast(double lat_deg, double lng_deg, int res, const H3Tables &T, uint64_t &out) {
+    return latLngToCellFastP(lat_deg, lng_deg, res, T, T.faceCenterPoint, T.fastU[res & 1], out);
 }
 
 }  // namespace hm

@@ -138,7 +138,8 @@ struct DevStats {
     unsigned long long overflow;    // nonzero: a hash table probe bound was exceeded
     unsigned long long bad_vkey;
     unsigned long long dedup_retry; // k_ingest: a vkey probe hit its bound; rerun k_dedup_max on a larger table
-    unsigned long long pad[4];
+    unsigned long long n_gaps;      // partial slots holding no record (direct k_ingest: rows that aggregate nothing)
+    unsigned long long pad[3];
 };
 
 HM_HD uint64_t mix64(uint64_t x) {

@@ -481,18 +481,24 @@ template <typename Rec>
 __global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const Rec *__restrict__ parts, int64_t n, const GenDesc *gm,
                                                        const GenDesc *glist, int n_glist, int nranks, int nbins,
                                                        unsigned *__restrict__ H, int64_t ntiles, DevStats *st) {
-    __shared__ unsigned h[RP_BINS];
+    __shared__ unsigned h[RP_BINS + 1];
     __shared__ GenCache C;
     gc_load(C, glist, n_glist);
-    for (int d = threadIdx.x; d < RP_BINS; d += RP_THREADS) h[d] = 0;
+    for (int d = threadIdx.x; d <= RP_BINS; d += RP_THREADS) h[d] = 0;
     __syncthreads();
     int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
     int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
     bool bad = false;
-    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS)
-        atomicAdd(&h[rp_digit(parts[i].cell, parts[i].wstart, C, gm, nranks, bad)], 1u);
+    unsigned gaps = 0;   // gaps (cell 0) count in the extra digit nbins, after every bin
+    for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) {
+        const uint64_t cell = parts[i].cell;
+        if (cell == EMPTY_CELL) gaps++;
+        else atomicAdd(&h[rp_digit(cell, parts[i].wstart, C, gm, nranks, bad)], 1u);
+    }
+    gaps = (unsigned)wave_sum((unsigned long long)gaps);
+    if (gaps && lane_id() == 0) atomicAdd(&h[nbins], gaps);
     __syncthreads();
-    for (int d = threadIdx.x; d < nbins; d += RP_THREADS) H[(int64_t)d * ntiles + blockIdx.x] = h[d];
+    for (int d = threadIdx.x; d <= nbins; d += RP_THREADS) H[(int64_t)d * ntiles + blockIdx.x] = h[d];
     if (__ballot(bad) && lane_id() == 0) atomicAdd(&st->overflow, 1ull);
 }
 
@@ -558,7 +564,7 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict_
                                                           int64_t ntiles, Out *__restrict__ dst) {
     constexpr int QI = sizeof(In) / 16, QO = sizeof(Out) / 16;
     constexpr bool widen = !std::is_same<In, Out>::value;
-    __shared__ unsigned cur[RP_BINS];   // positions < 2^32 (partition() checks n)
+    __shared__ unsigned cur[RP_BINS];   // positions < 2^32 - 1 (partition() checks n)
     __shared__ GenCache C;
     __shared__ uint4 stage[widen ? (RP_THREADS / 64) * 64 * QI : 1];   // widening: each wave's 64 input records
     gc_load(C, glist, n_glist);
@@ -571,24 +577,23 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict_
     const int ln = lane_id();
     for (int64_t i0 = t0 + (int64_t)(threadIdx.x >> 6) * 64; i0 < t1; i0 += RP_THREADS) {
         const int64_t i = i0 + ln;
-        unsigned pos = 0;
+        unsigned pos = ~0u;   // ~0u: a gap (cell 0), not moved (its digit nbins lies after every bin)
         uint64_t h = 0;
         if (i < t1) {
             const uint4 k = src[i * QI];   // part 0 = (cell, window start)
             const uint64_t cell = (uint64_t)k.x | ((uint64_t)k.y << 32);
             const int64_t ws = (int64_t)((uint64_t)k.z | ((uint64_t)k.w << 32));
-            h = tile_hash(cell, ws);
-            bool bad = false;
-            unsigned d;
-            if (nranks > 0) {
-                d = (unsigned)owner_of(h, nranks);
-            } else {
-                const int b = bin_of_c(C, gm, h, ws);
-                d = b < 0 ? 0u : (unsigned)b;
-                bad = b < 0;
+            if (cell != EMPTY_CELL) {
+                h = tile_hash(cell, ws);
+                unsigned d;
+                if (nranks > 0) {
+                    d = (unsigned)owner_of(h, nranks);
+                } else {
+                    const int b = bin_of_c(C, gm, h, ws);
+                    d = b < 0 ? 0u : (unsigned)b;   // (k_rp_hist flagged it)
+                }
+                pos = atomicAdd(&cur[d], 1u);
             }
-            (void)bad;
-            pos = atomicAdd(&cur[d], 1u);
         }
         const int64_t nrec = t1 - i0 < 64 ? t1 - i0 : 64;
         if constexpr (widen) {
@@ -604,14 +609,14 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict_
                 const int idx = r * 64 + ln, rec = idx / QO, q = idx % QO;
                 const unsigned p = __shfl(pos, rec, 64);
                 const unsigned hl = __shfl((unsigned)h, rec, 64), hh = __shfl((unsigned)(h >> 32), rec, 64);
-                if (rec < nrec) d4[(int64_t)p * QO + q] = rp_part<In, Out>(ws, rec, q, (uint64_t)hl | ((uint64_t)hh << 32));
+                if (rec < nrec && p != ~0u) d4[(int64_t)p * QO + q] = rp_part<In, Out>(ws, rec, q, (uint64_t)hl | ((uint64_t)hh << 32));
             }
             __builtin_amdgcn_wave_barrier();
         } else {
             for (int r = 0; r < QO; r++) {
                 const int idx = r * 64 + ln, rec = idx / QO, q = idx % QO;
                 const unsigned p = __shfl(pos, rec, 64);
-                if (rec < nrec) d4[(int64_t)p * QO + q] = src[(i0 + rec) * QI + q];
+                if (rec < nrec && p != ~0u) d4[(int64_t)p * QO + q] = src[(i0 + rec) * QI + q];
             }
         }
     }
@@ -755,7 +760,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
     __syncthreads();
     for (int bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
         const int64_t b0 = (int64_t)O[(int64_t)bin * ntiles];
-        const int64_t b1 = bin + 1 < nbins ? (int64_t)O[(int64_t)(bin + 1) * ntiles] : n;
+        const int64_t b1 = (int64_t)O[(int64_t)(bin + 1) * ntiles];   // (digit nbins: the gaps, after every bin)
         // 0. the bin's resident regions: windows merged into this batch whose region maps to this bin
         if (t == 0) {
             int nr = 0;
@@ -1158,6 +1163,9 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     unsigned long long *dgiveup, WinCount *cmap, DevStats *st) {
     __shared__ LaShared S;
     __shared__ WinLds WL;
+    __shared__ double Fc[20][3], Fu[20][2][3];   // the fast path's per-face tables (res parity): LDS reads
+    for (int k = threadIdx.x; k < 60; k += LA_THREADS) (&Fc[0][0])[k] = (&c_tab.faceCenterPoint[0][0])[k];
+    for (int k = threadIdx.x; k < 120; k += LA_THREADS) (&Fu[0][0][0])[k] = (&c_tab.fastU[res & 1][0][0][0])[k];
     wl_init(WL);
     const CensusSink census{cmap};
     bool census_ok = true;
@@ -1173,9 +1181,10 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     for (int s = threadIdx.x; s < LA_WT; s += LA_THREADS) { S.wt[s] = EMPTY_WIN; S.wcnt[s] = 0; }
     if (threadIdx.x == 0) { S.occ = 0; S.dskip = 0; }
     __syncthreads();
-    unsigned long long nvalid = 0, nlate = 0, bad = 0;
+    unsigned long long nvalid = 0, nlate = 0, bad = 0, gaps = 0;
     long long tmax = INT64_MIN;
     bool dretry = false;
+    if (DIRECT && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st->n_partials, (unsigned long long)n);   // slot i = row i
 #ifdef HM_ABL_NOAGG
     unsigned long long abl_sink = 0;
 #endif
@@ -1186,15 +1195,28 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
             const bool in = i < n;
             double la = 0.0, lo = 0.0;
             int64_t t = 0;
+            unsigned long long v = EMPTY_VKEY;
             bool rv = true;
             if (in) {
                 la = lat[i];
                 lo = lon[i];
                 t = ts[i];
+                v = vkey[i];
                 if (row_valid) rv = row_valid[i] != 0;
             }
             const bool ok = in && rv && la >= -90.0 && la <= 90.0 && lo >= -180.0 && lo <= 180.0 &&
                             t > INT64_MIN + 2 * tile_us && t < INT64_MAX - 2 * tile_us;
+            // dedup: the vkey's home slot is loaded now, its latency hidden behind the cell computation (a plain
+            // load: a stale copy can only show the slot empty or its max lower, both of which the atomics below
+            // correct)
+#ifdef HM_ABL_NODEDUP
+            const bool dd = false;
+#else
+            const bool dd = ok && v != EMPTY_VKEY && !__hip_atomic_load(&S.dskip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+            const unsigned long long dh0 = vkey_hash(v) & dmask;
+            DedupSlot d0{EMPTY_VKEY, 0};
+            if (dd) d0 = dtab[dh0];
             uint8_t fl = 0;
             uint64_t cell = EMPTY_CELL;
             int widx = -1;   // the window's slot in the workgroup's window table (-1: table full, rare)
@@ -1213,7 +1235,7 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
 #ifdef HM_ABL_NOCELL   // ablation builds (tools/ablate_ingest.sh): a hash stands in for the cell
             if (fl & F_AGG) cell = (mix64(__builtin_bit_cast(uint64_t, la) ^ mix64(__builtin_bit_cast(uint64_t, lo))) & LA_CELL_LO) | cell_hi;
 #else
-            if (fl & F_AGG) exc = !latLngToCellFast(la, lo, res, c_tab, cell);
+            if (fl & F_AGG) exc = !latLngToCellFastP(la, lo, res, c_tab, Fc, Fu, cell);
 #endif
             {
                 const unsigned long long pos = wave_append(exc, n_slow);
@@ -1223,60 +1245,56 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
             // dedup: per-vkey max ts over the valid rows (late rows included, as in the reference's batch frame)
             bool claimed = false;
             long long dh = -1;
-#ifdef HM_ABL_NODEDUP
-            if (false) {
-#else
-            if (ok && !S.dskip) {
-#endif
-                const unsigned long long v = vkey[i];
-                if (v == EMPTY_VKEY) {
-                    bad++;
-                } else {
-                    long long cur = INT64_MIN;
-                    dh = find_or_claim_vkey_ts(dtab, dmask, v, claimed, DEDUP_FUSED_PROBES, cur);
-                    if (dh < 0) {
-                        if (!dretry) atomicExch(dgiveup, 1ull);
-                        dretry = true;
-                    } else if (t > cur) {
-                        atomicMax(&dtab[dh].maxts, (long long)t);
-                    }
+            bad += ok && v == EMPTY_VKEY;
+            if (dd) {
+                long long cur = d0.maxts;
+                if (d0.vkey == v) dh = (long long)dh0;   // the usual case: the key sits in its home slot
+                else dh = find_or_claim_vkey_ts(dtab, dmask, v, claimed, DEDUP_FUSED_PROBES, cur);
+                if (dh < 0) {
+                    if (!dretry) atomicExch(dgiveup, 1ull);
+                    dretry = true;
+                } else if (t > cur) {
+                    atomicMax(&dtab[dh].maxts, (long long)t);
                 }
             }
             const unsigned long long pos = wave_append(claimed, n_dused);
             if (claimed) dused[pos] = (unsigned int)dh;
             bool fresh = false;
             if constexpr (DIRECT) {
-                // every aggregated row is a partial record: block-wide positions, staged in LDS, stored
-                // four lanes per 64-B record
+                // Row i owns partial slot i: no reservation (one device-wide atomic per chunk on a single counter
+                // serialised this kernel at ~13 ns each, 5 ms per 1e8 events).  An aggregated row stores its
+                // record there, any other row a gap (cell 0) that the partition skips; an exception's slot is
+                // filled by k_ingest_exact.  The wave's 64 records go through LDS and out as 3 KB contiguous.
                 const bool rec = (fl & F_AGG) && !exc;
-                const unsigned long long bal = __ballot(rec);
-                const int wv = threadIdx.x >> 6;
-                if (lane_id() == 0) S.scan[wv] = (unsigned)__popcll(bal);
-                __syncthreads();
-                unsigned woff = 0, total = 0;
-                for (int k = 0; k < LA_THREADS / 64; k++) {
-                    if (k < wv) woff += S.scan[k];
-                    total += S.scan[k];
-                }
-                if (threadIdx.x == 0) S.base = total ? atomicAdd(&st->n_partials, (unsigned long long)total) : 0;
-                uint4 *stage = (uint4 *)S.key;   // key, cnt, ssp: 12 KB = 256 records
+                const int ln = lane_id();
+                uint4 *stage = (uint4 *)S.key + (threadIdx.x >> 6) * 64 * 3;   // key, cnt, ssp: 12 KB = 256 records
+                uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0, r2 = r0;
                 if (rec) {
-                    const unsigned r = woff + (unsigned)__popcll(bal & ((1ull << lane_id()) - 1));
                     const bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
                     const double sp = sv ? speed[i] : 0.0;
                     const int64_t ws = widx >= 0 ? (int64_t)S.wt[widx] : floor_div(t, wdiv) * tile_us;
                     const uint64_t spb = __builtin_bit_cast(uint64_t, sp), lab = __builtin_bit_cast(uint64_t, la),
                                    lob = __builtin_bit_cast(uint64_t, lo);
-                    stage[r * 3 + 0] = make_uint4((unsigned)cell, (unsigned)(cell >> 32), (unsigned)ws, (unsigned)((uint64_t)ws >> 32));
-                    stage[r * 3 + 1] = make_uint4(1u, sv ? 1u : 0u, (unsigned)spb, (unsigned)(spb >> 32));
-                    stage[r * 3 + 2] = make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32));
+                    r0 = make_uint4((unsigned)cell, (unsigned)(cell >> 32), (unsigned)ws, (unsigned)((uint64_t)ws >> 32));
+                    r1 = make_uint4(1u, sv ? 1u : 0u, (unsigned)spb, (unsigned)(spb >> 32));
+                    r2 = make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32));
                     if (widx >= 0) atomicAdd(&S.wcnt[widx], 1u);
                     else census_ok &= wl_add(WL, census, wenc_of(ws), 1ull);
                 }
-                __syncthreads();
-                uint4 *__restrict__ o4 = (uint4 *)(out + S.base);
-                for (unsigned k = threadIdx.x; k < 3 * total; k += LA_THREADS) o4[k] = stage[k];   // contiguous 48-B records
-                __syncthreads();
+                gaps += in && !(fl & F_AGG);
+                stage[ln * 3 + 0] = r0;
+                stage[ln * 3 + 1] = r1;
+                stage[ln * 3 + 2] = r2;
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                const int64_t i0 = i - ln;
+                const int64_t nrec3 = (n - i0 < 64 ? n - i0 : 64) * 3;
+                uint4 *__restrict__ o4 = (uint4 *)(out + i0);
+#ifndef HM_ABL_NOREC
+                for (int r = 0; r < 3; r++)
+                    if (r * 64 + ln < nrec3) o4[r * 64 + ln] = stage[r * 64 + ln];
+#endif
+                __builtin_amdgcn_wave_barrier();
             } else {
             // LDS pre-aggregation of the window's rows
 #ifdef HM_ABL_NOAGG
@@ -1314,9 +1332,12 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
         }
         // poll the give-up flag now and then (its own cache line: DevStats takes every flush's atomics)
         if (threadIdx.x == 0 && !S.dskip && ((ch / gridDim.x) & 15) == 15)
-            S.dskip = __hip_atomic_load(dgiveup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-        __syncthreads();
-        if (!DIRECT && S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, cell_hi, out, st, WL, census, census_ok);
+            __hip_atomic_store(&S.dskip, __hip_atomic_load(dgiveup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ? 1u : 0u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if constexpr (!DIRECT) {   // (direct: no block-wide state between chunks; dskip is read at the next poll)
+            __syncthreads();
+            if (S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, cell_hi, out, st, WL, census, census_ok);
+        }
     }
     if (S.occ > 0) la_flush(S, cell_hi, out, st, WL, census, census_ok);
     if constexpr (DIRECT) {   // the window table was never flushed: its census
@@ -1332,6 +1353,7 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
     nvalid = wave_sum(nvalid);
     nlate = wave_sum(nlate);
     bad = wave_sum(bad);
+    if (DIRECT) gaps = wave_sum(gaps);
     tmax = wave_max(tmax);
     const unsigned long long rt = __ballot(dretry);
     const unsigned long long cbad = __ballot(!census_ok);
@@ -1340,17 +1362,19 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
         if (nlate) atomicAdd(&st->n_late, nlate);
         if (tmax != INT64_MIN) atomicMax(&st->max_ts_ms, (long long)(tmax / 1000));   // trunc(max) = max(trunc)
         if (bad) atomicAdd(&st->bad_vkey, bad);
+        if (gaps) atomicAdd(&st->n_gaps, gaps);
         if (rt) atomicAdd(&st->dedup_retry, 1ull);
         if (cbad) atomicAdd(&st->overflow, 1ull);
     }
 }
 
-// exceptions of k_ingest's fast path: upstream's exact sequence, one partial record per event
+// exceptions of k_ingest's fast path: upstream's exact sequence, one partial record per event (direct: into the
+// row's own slot, else appended)
 __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__ lat, const double *__restrict__ lon,
                                                       const int64_t *__restrict__ ts, const double *__restrict__ speed,
                                                       const uint8_t *__restrict__ speed_valid, int res, int64_t tile_us,
                                                       const unsigned int *__restrict__ slow, const unsigned long long *n_slow,
-                                                      TilePartial *__restrict__ out, WinCount *cmap, DevStats *st) {
+                                                      bool direct, TilePartial *__restrict__ out, WinCount *cmap, DevStats *st) {
     __shared__ WinLds WL;
     wl_init(WL);
     __syncthreads();
@@ -1376,7 +1400,7 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
             p.slat = lat[i];
             p.slon = lon[i];
         }
-        const unsigned long long pos = wave_append(in, &st->n_partials);
+        const unsigned long long pos = direct ? (in ? slow[q] : 0ull) : wave_append(in, &st->n_partials);
         if (in) out[pos] = p;
         ok &= wave_count_windows(in, in ? wenc_of(p.wstart) : 0ull, 1ull, WL, census);
     }
@@ -1773,9 +1797,9 @@ static int gens_upload(hm_ctx *ctx) {
 template <typename In, typename Out>
 static int partition(hm_ctx *ctx, const In *parts, int64_t n, int64_t &ntiles, int nranks = 0, Out *dst = nullptr) {
     const int nbins = nranks > 0 ? nranks : RP_BINS;
-    if (n > (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "%lld partial records in one merge exceed 2^32-1", (long long)n);
+    if (n >= (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "%lld partial records in one merge exceed 2^32-2", (long long)n);
     ntiles = std::max<int64_t>((n + RP_TILE - 1) / RP_TILE, 1);
-    const int64_t m = (int64_t)nbins * ntiles;
+    const int64_t m = (int64_t)(nbins + 1) * ntiles;   // digit nbins: gaps (cell 0), which the scatter drops
     const int64_t nb = (m + SC_PER - 1) / SC_PER;
     int rc;
     if (!dst && (rc = ensure(ctx, ctx->parts_sorted, std::max<int64_t>(n, 1) * sizeof(Out)))) return rc;
@@ -2039,7 +2063,7 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
                            ctx->d_scratch + GIVEUP_WORD, ctx->d_cmap, ctx->d_st);
         hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, I.ts, I.sp, I.sv,
                            ctx->cfg.h3_res, ctx->cfg.tile_us, (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
-                           (TilePartial *)ctx->partials.p, ctx->d_cmap, ctx->d_st);
+                           direct, (TilePartial *)ctx->partials.p, ctx->d_cmap, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
         ctx->dfused.dirty = true;
     }
@@ -2080,7 +2104,7 @@ static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t 
 // with enough rows to tell
 static void note_agg_ratio(hm_ctx *ctx, const DevStats &s) {
     const int64_t agg = (int64_t)s.n_valid - (int64_t)s.n_late;
-    if (agg >= (int64_t)1 << 16) ctx->agg_ratio = (double)s.n_partials / (double)agg;
+    if (agg >= (int64_t)1 << 16) ctx->agg_ratio = (double)(s.n_partials - s.n_gaps) / (double)agg;
 }
 
 static int ensure_outputs(hm_ctx *ctx, int64_t n_rows) {
@@ -2093,15 +2117,16 @@ static int ensure_outputs(hm_ctx *ctx, int64_t n_rows) {
     return HM_OK;
 }
 
-static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts) {
+// parts[0, n_parts) holds n_parts - n_gaps records (and n_gaps gaps: cell 0, direct k_ingest)
+static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts, int64_t n_gaps) {
     int rc;
-    ctx->n_partials_merged = n_parts;
+    ctx->n_partials_merged = n_parts - n_gaps;
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_touched, 0, 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_state_new, 0, 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
     ctx->seq++;
     if ((rc = ensure_outputs(ctx, n_parts))) return rc;
-    if (n_parts == 0) {
+    if (n_parts == n_gaps) {
         for (int e : {3, 7, 4, 5}) HIPCHK(ctx, hipEventRecord(ctx->ev[e], ctx->stream));
         return HM_OK;
     }
@@ -2364,7 +2389,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     DevStats s1 = *ctx->h_st;
     note_agg_ratio(ctx, s1);
     // 3. merge into state + emit
-    if ((rc = phase_merge_emit(ctx, (const TilePartial *)ctx->partials.p, (int64_t)s1.n_partials))) return rc;
+    if ((rc = phase_merge_emit(ctx, (const TilePartial *)ctx->partials.p, (int64_t)s1.n_partials, (int64_t)s1.n_gaps))) return rc;
     // 4. dedup over the batch's valid rows
     if ((rc = phase_dedup(ctx, &I, nullptr, I.n, s1.dedup_retry != 0))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
@@ -2470,8 +2495,9 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     if (ctx->h_st->bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved");
     ctx->dedup_seen = (int64_t)ctx->h_scratch[ctx->dlast->used_word];
-    if ((int64_t)ctx->h_st->n_partials > tile_send_cap || (int64_t)ctx->h_scratch[255] > cand_send_cap)
-        return set_err(ctx, HM_E_INVALID, "send buffer too small (%llu tiles, %llu candidates)", ctx->h_st->n_partials,
+    const int64_t n_records = (int64_t)(ctx->h_st->n_partials - ctx->h_st->n_gaps);
+    if (n_records > tile_send_cap || (int64_t)ctx->h_scratch[255] > cand_send_cap)
+        return set_err(ctx, HM_E_INVALID, "send buffer too small (%lld tiles, %llu candidates)", (long long)n_records,
                        ctx->h_scratch[255]);
     // candidates: exclusive offsets -> cursors
     unsigned long long cur[128];
@@ -2488,19 +2514,19 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
         if ((rc = partition<TilePartial, TilePartial>(ctx, (const TilePartial *)ctx->partials.p, n_parts, ntiles, nranks,
                                                       (TilePartial *)tile_send_buf)))
             return rc;
-        hipLaunchKernelGGL(k_digit_starts, dim3(1), dim3(64), 0, ctx->stream, (const unsigned long long *)ctx->rp_O.p, ntiles, nranks,
-                           ctx->d_scratch);
+        hipLaunchKernelGGL(k_digit_starts, dim3(1), dim3(128), 0, ctx->stream, (const unsigned long long *)ctx->rp_O.p, ntiles,
+                           nranks + 1, ctx->d_scratch);
         HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 64 * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, (nranks + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     for (int r = 0; r < nranks; r++) {
         const int64_t start = n_parts > 0 ? (int64_t)ctx->h_scratch[r] : 0;
-        const int64_t end = n_parts > 0 && r + 1 < nranks ? (int64_t)ctx->h_scratch[r + 1] : n_parts;
+        const int64_t end = n_parts > 0 ? (int64_t)ctx->h_scratch[r + 1] : 0;   // [nranks]: the gaps' digit
         tile_send_counts[r] = end - start;
     }
     if (sizes) {
-        sizes->n_tile_partials = (int64_t)ctx->h_st->n_partials;
+        sizes->n_tile_partials = n_records;
         sizes->n_cands = 0;
         for (int r = 0; r < nranks; r++) sizes->n_cands += cand_send_counts[r];
         sizes->batch_max_event_ms = ctx->h_st->max_ts_ms;
@@ -2524,7 +2550,7 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, 
     int rc;
     memset(out, 0, sizeof(*out));
     int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
-    if ((rc = phase_merge_emit(ctx, (const TilePartial *)tile_recv_dev, n_tile_recv))) return rc;
+    if ((rc = phase_merge_emit(ctx, (const TilePartial *)tile_recv_dev, n_tile_recv, 0))) return rc;
     // owner-side dedup over received candidates
     if ((rc = phase_dedup(ctx, nullptr, (const Cand *)cand_recv_dev, n_cand_recv, true))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch, 0, 128 * 8, ctx->stream));

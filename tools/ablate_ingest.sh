@@ -11,4 +11,6 @@ build noagg "-DHM_ABL_NOAGG" &
 build nocell "-DHM_ABL_NOCELL" &
 build cellsonly "-DHM_ABL_NOAGG -DHM_ABL_NODEDUP" &
 build aggonly "-DHM_ABL_NOCELL -DHM_ABL_NODEDUP" &
+build norec "-DHM_ABL_NOREC" &
+build recnocell "-DHM_ABL_NOREC -DHM_ABL_NOCELL" &
 wait
