@@ -40,15 +40,17 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9
 # merge), per emitted tile (emit = the row compaction).  ingest also writes 48 B per partial (added below).
 BYTES = {
     "ingest": 43,      # read lat 8 + lon 8 + ts 8 + speed 8 + speed_valid 1 + vkey 8 + row_valid 1; write flags 1
-    "partition": 144,  # per 48-B partial: histogram read + scatter read + scatter write
-    "merge": 161,      # per partial: read 48 B record, write the 64 B state line (a new key: its slot tag is in
-                       # LDS, nothing read) and the 49 B update-mode row
+    "partition": 160,  # per partial: histogram read 48 B + scatter read 48 B + scatter write of the 64-B SortedRec
+    "merge": 177,      # per partial: read the 64-B SortedRec, write the 64 B state line (a new key: its slot tag
+                       # is in LDS, nothing read) and the 49 B update-mode row
     "emit": 98,        # per emitted tile: 49 B row read from the bin's segment, 49 B written densely
     "dedup": 20,       # per event: vkey 8 + ts 8 + flags 1 read, win flag 1 written, 2 x 1 B compaction reads
 }
-# k_ingest's HBM traffic and VALU instruction mix per event of this workload were counted by rocprofv3 PMC
-# passes of this same command (tools/ingest_pmc.py -> profiles/r1/ingest_pmc.json).
-PMC_FILE = os.path.join(ROOT, "profiles", "r1", "ingest_pmc.json")
+# HBM traffic per dispatch of every kernel and k_ingest's VALU instruction mix per event of this workload were
+# counted by rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r1/kernel_pmc.json).
+PMC_FILE = os.path.join(ROOT, "profiles", "r1", "kernel_pmc.json")
+STAGE_KERNELS = {"ingest": ["k_ingest"], "partition": ["k_rp_hist", "k_rp_scatter"], "merge": ["k_merge_owned"],
+                 "emit": ["k_rows_compact"], "dedup": ["k_dedup_flag"]}
 
 
 def ingest_pmc(res):
@@ -176,11 +178,13 @@ def main():
     # side: k_ingest is VALU/latency bound, so the HBM fraction alone understates how busy it is.
     roof = {"bound": "hbm", "kernel": dom, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": gbs / HBM_PEAK_GBS, "traffic": None}
-    pmc = ingest_pmc(args.res) if dom == "ingest" else None
-    if pmc is not None:
-        sec = avg_ms[dom] * 1e-3
-        roof["traffic"] = pmc["hbm_bytes_per_event"] * n
+    pmc = ingest_pmc(args.res)
+    if pmc is not None and all(k in pmc.get("kernels", {}) for k in STAGE_KERNELS[dom]):
+        # FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, per dispatch, summed over the stage's kernels
+        roof["traffic"] = sum(pmc["kernels"][k]["hbm_bytes"] for k in STAGE_KERNELS[dom])
         roof["traffic_source"] = os.path.relpath(PMC_FILE, ROOT)
+    if pmc is not None and dom == "ingest":
+        sec = avg_ms[dom] * 1e-3
         tf = pmc["fp64_flops_per_event"] * n / sec / 1e12
         # VALU issue: SIMD-32 pipes, 2 cycles per wave64 32-bit op, 4 per fp64 op (MI355X_MICROARCH.md)
         simd_cycles = (pmc["valu_f64_insts_per_event"] * 4 + pmc["valu_other_insts_per_event"] * 2) * n / 64

@@ -11,7 +11,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INS
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVES SQ_BUSY_CU_CYCLES SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d $O/pmc_sq -o run --output-format csv -- $P > $O/pmc_sq.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- $P > $O/pmc_fetch.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- $P > $O/pmc_write.log 2>&1 && \
-python3 tools/ingest_pmc.py --res 8 --events 100000000 --out profiles/r1/ingest_pmc.json $O/pmc_f64 $O/pmc_sq $O/pmc_fetch $O/pmc_write > $O/ingest_pmc.log 2>&1 ; \
-cp profiles/r1/ingest_pmc.json $O/ ; \
+python3 tools/ingest_pmc.py --res 8 --events 100000000 --out profiles/r1/kernel_pmc.json $O/pmc_f64 $O/pmc_sq $O/pmc_fetch $O/pmc_write > $O/ingest_pmc.log 2>&1 ; \
+cp profiles/r1/kernel_pmc.json $O/ ; \
 timeout -k 10 600 python3 bench.py > $O/bench.log 2>&1
 rc=$?; echo "done rc=$rc"; exit $rc

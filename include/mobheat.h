@@ -19,6 +19,9 @@
  *   hm_stage_* (multi-GPU)       -- the same batch split into local pre-aggregation, an owner-partitioned
  *                                   exchange (the caller moves the records with RCCL all-to-all), and the
  *                                   owner-side merge; replaces Spark's shuffle (spark.sql.shuffle.partitions, :44).
+ *   hm_state_export / _import    -- the state store behind .option("checkpointLocation", CHECKPOINT_DIR)
+ *                                   (:37,244): the tile state + watermark after a committed epoch, and its
+ *                                   restore into a fresh context after a restart (the epoch is then replayed).
  */
 #ifndef MOBHEAT_H
 #define MOBHEAT_H
@@ -28,7 +31,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 5
+#define HM_ABI_VERSION 6
 
 /* error codes */
 #define HM_OK 0
@@ -50,7 +53,8 @@ typedef struct hm_config {
                                          watermark, state evicted by the current one; 0 = both current */
     int64_t tile_us;                /* window length in microseconds: TILE_MINUTES*60e6 (default 5 min) */
     int64_t watermark_delay_ms;     /* withWatermark delay (reference: 10 minutes = 600000) */
-    int64_t state_capacity_hint;    /* initial slots of the persistent tile state (0 = default) */
+    int64_t state_capacity_hint;    /* expected keys of the largest window: its table is reserved at create
+                                       (0 = allocate on demand) */
     int64_t batch_capacity_hint;    /* expected max events per batch (0 = grow on demand) */
 } hm_config;
 
@@ -171,6 +175,38 @@ int hm_selftest_latlng_to_cell_host(const double *lat, const double *lon, int64_
  * exact path was taken (may be NULL). */
 int hm_selftest_latlng_to_cell_fast_host(const double *lat, const double *lon, int64_t n, int32_t res,
                                          uint64_t *out, uint8_t *fell_back);
+
+/* Tile-state checkpoint (Spark's state store version after an epoch, heatmap_stream.py:37,244).
+ * One record per live (cellId, windowStart) key: the cumulative aggregates the next batches build on.
+ * reserved must be 0 on import. Records are in no particular order. */
+typedef struct hm_state_rec {
+    uint64_t cell;
+    int64_t window_start_us;
+    int64_t count;        /* count(1) so far */
+    int64_t n_speed;      /* non-null speedKmh rows so far */
+    double sum_speed;
+    double sum_lat;
+    double sum_lon;
+    int64_t reserved;
+} hm_state_rec;   /* 64 B */
+
+typedef struct hm_state_info {
+    int64_t epoch_id;            /* last epoch processed by the context (-1: none) */
+    int64_t n_keys;              /* records */
+    int64_t watermark_ms;        /* the watermark the next batch evicts with */
+    int64_t prev_watermark_ms;   /* the one it drops late rows with (late_uses_prev_watermark) */
+    int64_t tile_us;             /* must match the importing context's config */
+    int64_t watermark_delay_ms;  /* idem */
+    int32_t h3_res;              /* idem */
+    int32_t reserved;
+} hm_state_info;
+
+/* Fills *info; with recs != NULL also writes info->n_keys records to recs (host memory, cap records:
+ * HM_E_INVALID if cap < n_keys). Call once with recs = NULL for the size. Not between stage calls. */
+int hm_state_export(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs, int64_t cap);
+/* Restores an exported state into a context that has processed no batch (HM_E_STATE otherwise); the
+ * config fields of info must equal the context's (HM_E_INVALID). recs: info->n_keys distinct keys, host memory. */
+int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *recs);
 
 /* Timing of the last hm_process_batch / stage call on the library's stream (HIP events), milliseconds
  * per phase: index 0 ingest (k_ingest: filter + cells + windows + pre-aggregation + dedup max), 1 reserved

@@ -25,6 +25,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
+#include <ctime>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -1678,6 +1680,20 @@ static int set_err(hm_ctx *ctx, int code, const char *fmt, ...) {
     return code;
 }
 
+// MOBHEAT_TRACE=1: every device allocation of the library (size, host wall time) to stderr
+static bool g_trace = getenv("MOBHEAT_TRACE") && getenv("MOBHEAT_TRACE")[0] == '1';
+static double wall_ms() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
+}
+static hipError_t dev_malloc(void **p, size_t bytes, const char *what) {
+    const double t0 = g_trace ? wall_ms() : 0;
+    const hipError_t e = hipMalloc(p, bytes);
+    if (g_trace) fprintf(stderr, "[mobheat] hipMalloc %-12s %10.3f GB %8.1f ms\n", what, bytes / 1e9, wall_ms() - t0);
+    return e;
+}
+
 static int ensure(hm_ctx *ctx, DevBuf &b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return HM_OK;
     if (b.p) {
@@ -1688,7 +1704,7 @@ static int ensure(hm_ctx *ctx, DevBuf &b, size_t bytes) {
     }
     size_t want = std::max<size_t>(bytes, 256);
     want = (want + 4095) & ~(size_t)4095;
-    if (hipMalloc(&b.p, want) != hipSuccess) {
+    if (dev_malloc(&b.p, want, "buffer") != hipSuccess) {
         (void)hipGetLastError();
         return set_err(ctx, HM_E_NOMEM, "hipMalloc(%zu) failed", want);
     }
@@ -1717,7 +1733,6 @@ static int ilog2(uint64_t v) { return 63 - __builtin_clzll(v); }
 // (a hot window with few keys is still merged in parallel).
 static void gen_geometry(const hm_ctx *ctx, int64_t keys, int64_t parts, int min_log2, int &log2cap, unsigned &rbits) {
     int L = ilog2(next_pow2((uint64_t)std::max<int64_t>(2 * keys, 1024)));
-    if (ctx->cfg.state_capacity_hint > 0) L = std::max(L, std::min(24, ilog2(next_pow2((uint64_t)ctx->cfg.state_capacity_hint))));
     const int want_rb = std::min(RP_BITS, ilog2(next_pow2((uint64_t)std::max<int64_t>((parts + 16383) / 16384, 1))));
     L = std::max({L, want_rb + REGION_MIN_BITS, min_log2});
     rbits = (unsigned)std::min(RP_BITS, L - REGION_MIN_BITS);
@@ -1744,7 +1759,7 @@ static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **
     }
     const size_t bytes = (size_t(1) << log2cap) * (sizeof(TileSlot) + 1);   // slots, then one tag byte per slot
     TileSlot *t = nullptr;
-    if (hipMalloc(&t, bytes) != hipSuccess) {
+    if (dev_malloc((void **)&t, bytes, "state table") != hipSuccess) {
         (void)hipGetLastError();
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         for (auto &pt : ctx->pool) (void)hipFree(pt.first);
@@ -1964,7 +1979,7 @@ static int dedup_prepare(hm_ctx *ctx, hm_ctx::DedupTable &d, int64_t n_keys, boo
         HIPCHK(ctx, hipFree(d.tab));
         d.tab = nullptr;
     }
-    if (hipMalloc(&d.tab, want * sizeof(DedupSlot)) != hipSuccess) {
+    if (dev_malloc((void **)&d.tab, want * sizeof(DedupSlot), "dedup table") != hipSuccess) {
         (void)hipGetLastError();
         return set_err(ctx, HM_E_NOMEM, "dedup table alloc failed");
     }
@@ -2319,6 +2334,15 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
             ensure(ctx, ctx->s_lat, n * 8) || ensure_outputs(ctx, n))
             return fail("create");
     }
+    // state_capacity_hint: one window table for that many keys, reserved now into the pool (a 70-GB table costs
+    // ~2 s in hipMalloc: C5's first batch)
+    if (cfg->state_capacity_hint > 0) {
+        int L = ilog2(next_pow2((uint64_t)std::max<int64_t>(2 * cfg->state_capacity_hint, 1024)));
+        unsigned rb = 0;
+        TileSlot *t = nullptr;
+        if (table_acquire(ctx, L, rb, &t)) return fail("create");
+        table_release(ctx, t, L);
+    }
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) { ctx->err = "sync"; return fail("create"); }
     *out = ctx;
     return HM_OK;
@@ -2609,6 +2633,116 @@ int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_r
         out->latest_row = (const int64_t *)ctx->h_rows;
     }
     ctx->stage = 0;
+    return HM_OK;
+}
+
+// ---- tile-state checkpoint (Spark's state store behind checkpointLocation, heatmap_stream.py:37,244) ----
+// Export: every live window's keys dumped by k_dump_gen (the growth path's kernel) into one GrowRec array, copied
+// to the caller; the touched word (this context's batch sequence) is cleared -- it means nothing elsewhere.
+static void state_info_of(const hm_ctx *ctx, hm_state_info *info, int64_t n_keys) {
+    memset(info, 0, sizeof(*info));
+    info->epoch_id = ctx->epoch;
+    info->n_keys = n_keys;
+    info->watermark_ms = ctx->wm_cur;
+    info->prev_watermark_ms = ctx->wm_prev;
+    info->tile_us = ctx->cfg.tile_us;
+    info->watermark_delay_ms = ctx->cfg.watermark_delay_ms;
+    info->h3_res = ctx->cfg.h3_res;
+}
+
+int hm_state_export(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs, int64_t cap) {
+    static_assert(sizeof(hm_state_rec) == sizeof(GrowRec), "hm_state_rec mirrors GrowRec");
+    if (!ctx || !info) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->stage != 0) return set_err(ctx, HM_E_STATE, "hm_state_export between stage calls");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int64_t n = 0;
+    for (const auto &g : ctx->gens) n += g.keys;
+    state_info_of(ctx, info, n);
+    if (!recs) return HM_OK;
+    if (cap < n) return set_err(ctx, HM_E_INVALID, "state of %lld keys does not fit %lld records", (long long)n, (long long)cap);
+    if (n == 0) return HM_OK;
+    int rc;
+    if ((rc = ensure(ctx, ctx->parts_regrow, n * sizeof(GrowRec)))) return rc;
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
+    for (const auto &g : ctx->gens) {
+        GenDesc d{};
+        d.wenc = g.wenc;
+        d.tab = g.tab;
+        d.rbits = g.rbits;
+        d.rshift = (unsigned)g.log2cap - g.rbits;
+        d.rmask = (UINT64_C(1) << d.rshift) - 1;
+        hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
+                           (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD);
+    }
+    HIPCHK(ctx, hipGetLastError());
+    unsigned long long dumped = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&dumped, ctx->d_scratch + REGROW_WORD, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if ((int64_t)dumped != n) return set_err(ctx, HM_E_STATE, "state dump found %llu keys, expected %lld", dumped, (long long)n);
+    HIPCHK(ctx, hipMemcpy(recs, ctx->parts_regrow.p, n * sizeof(GrowRec), hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; i++) recs[i].reserved = 0;
+    return HM_OK;
+}
+
+// Import: the records' windows get tables sized as a batch's new windows would be, then the records are merged
+// through the growth path (partition + k_merge_owned in rehash mode: no counting, no rows, no touched update).
+int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *recs) {
+    if (!ctx || !info || info->n_keys < 0 || (info->n_keys > 0 && !recs))
+        return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->epoch != -1 || ctx->stage != 0 || !ctx->gens.empty())
+        return set_err(ctx, HM_E_STATE, "hm_state_import into a context that already processed a batch");
+    if (info->h3_res != ctx->cfg.h3_res || info->tile_us != ctx->cfg.tile_us || info->watermark_delay_ms != ctx->cfg.watermark_delay_ms)
+        return set_err(ctx, HM_E_INVALID, "checkpoint of res %d / window %lld us / delay %lld ms does not match the context",
+                       info->h3_res, (long long)info->tile_us, (long long)info->watermark_delay_ms);
+    const int64_t n = info->n_keys;
+    if (n >= (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "%lld state records exceed 2^32-2", (long long)n);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    // census per window + record checks (the device trusts them: a zero cell is a gap, reserved is touched)
+    std::vector<std::pair<unsigned long long, int64_t>> wins;
+    size_t last = 0;
+    const int64_t T = ctx->cfg.tile_us;
+    for (int64_t i = 0; i < n; i++) {
+        const hm_state_rec &r = recs[i];
+        if (r.cell == 0 || r.reserved != 0 || r.count < 1 || r.n_speed < 0 || r.n_speed > r.count ||
+            ((r.window_start_us % T) + T) % T != 0)
+            return set_err(ctx, HM_E_INVALID, "state record %lld is malformed", (long long)i);
+        const unsigned long long we = wenc_of(r.window_start_us);
+        if (last >= wins.size() || wins[last].first != we) {
+            last = 0;
+            while (last < wins.size() && wins[last].first != we) last++;
+            if (last == wins.size()) {
+                if ((int)wins.size() >= GMAP_SLOTS / 2)
+                    return set_err(ctx, HM_E_OVERFLOW, "checkpoint holds more than %d windows", GMAP_SLOTS / 2);
+                wins.emplace_back(we, 0);
+            }
+        }
+        wins[last].second++;
+    }
+    int rc;
+    for (const auto &w : wins) {
+        int L;
+        unsigned rb;
+        gen_geometry(ctx, w.second, w.second, 0, L, rb);
+        TileSlot *t = nullptr;
+        if ((rc = table_acquire(ctx, L, rb, &t))) return rc;
+        ctx->gens.push_back({w.first, t, L, rb, w.second, 0});
+    }
+    if ((rc = gens_upload(ctx))) return rc;
+    if (n > 0) {
+        if ((rc = ensure(ctx, ctx->parts_regrow, n * sizeof(GrowRec)))) return rc;
+        HIPCHK(ctx, hipMemcpy(ctx->parts_regrow.p, recs, n * sizeof(GrowRec), hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
+        int64_t ntiles;
+        if ((rc = partition<GrowRec, GrowRec>(ctx, (const GrowRec *)ctx->parts_regrow.p, n, ntiles))) return rc;
+        if ((rc = merge_sorted<GrowRec>(ctx, n, ntiles))) return rc;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow while restoring the state");
+    }
+    ctx->state_size = n;
+    ctx->wm_cur = info->watermark_ms;
+    ctx->wm_prev = info->prev_watermark_ms;
+    ctx->epoch = info->epoch_id;
     return HM_OK;
 }
 

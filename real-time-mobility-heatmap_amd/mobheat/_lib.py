@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MOBHEAT_LIB: load another build of the same ABI (kernel variants under csrc/variants/ for tuning runs)
 LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
 
-HM_ABI_VERSION = 5
+HM_ABI_VERSION = 6
 HM_MEM_HOST = 0
 HM_MEM_DEVICE = 1
 HM_TILE_REC_BYTES = 48
@@ -54,6 +54,16 @@ class HmStageSizes(ctypes.Structure):
                 ("n_valid", c_i64), ("n_late", c_i64)]
 
 
+class HmStateInfo(ctypes.Structure):
+    _fields_ = [("epoch_id", c_i64), ("n_keys", c_i64), ("watermark_ms", c_i64), ("prev_watermark_ms", c_i64),
+                ("tile_us", c_i64), ("watermark_delay_ms", c_i64), ("h3_res", c_i32), ("reserved", c_i32)]
+
+
+# hm_state_rec (64 B): one live (cellId, windowStart) key of the tile state
+STATE_REC_DTYPE = np.dtype([("cell", "<u8"), ("window_start_us", "<i8"), ("count", "<i8"), ("n_speed", "<i8"),
+                            ("sum_speed", "<f8"), ("sum_lat", "<f8"), ("sum_lon", "<f8"), ("reserved", "<i8")])
+assert STATE_REC_DTYPE.itemsize == 64
+
 _P = ctypes.POINTER
 # name -> (restype, argtypes); must match include/mobheat.h (tests/test_abi.py checks the symbol set)
 SIGNATURES = {
@@ -73,6 +83,8 @@ SIGNATURES = {
     "hm_selftest_floor_div": (c_i32, [c_vp, c_i64, c_i64, c_vp]),
     "hm_selftest_latlng_to_cell_host": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp]),
     "hm_selftest_latlng_to_cell_fast_host": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "hm_state_export": (c_i32, [c_vp, _P(HmStateInfo), c_vp, c_i64]),
+    "hm_state_import": (c_i32, [c_vp, _P(HmStateInfo), c_vp]),
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_abi_version": (c_i32, []),
 }

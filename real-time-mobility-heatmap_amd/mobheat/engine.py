@@ -10,7 +10,10 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import HM_MEM_DEVICE, HM_MEM_HOST, HmBatchIn, HmBatchOut, HmConfig, check, ptr
+from ._lib import (HM_MEM_DEVICE, HM_MEM_HOST, STATE_REC_DTYPE, HmBatchIn, HmBatchOut, HmConfig, HmStateInfo, check,
+                   ptr)
+
+_INFO_FIELDS = [f for f, _ in HmStateInfo._fields_ if f != "reserved"]
 
 
 @dataclass
@@ -103,6 +106,38 @@ class HeatmapEngine:
                                          ctypes.byref(out)), self._ctx, "hm_process_batch")
         return out
 
+    # ---- tile-state checkpoint (Spark's state store under checkpointLocation, heatmap_stream.py:37,244) ----
+    def export_state(self):
+        """(info dict, records) of the persistent tile state after the last batch: one STATE_REC_DTYPE record per
+        live (cell, windowStart) key with its cumulative count / non-null speed count / sums, plus the epoch and
+        watermarks the next batch continues from."""
+        info = HmStateInfo()
+        check(self._lib.hm_state_export(self._ctx, ctypes.byref(info), None, 0), self._ctx, "hm_state_export")
+        recs = np.zeros(int(info.n_keys), STATE_REC_DTYPE)
+        if recs.size:
+            check(self._lib.hm_state_export(self._ctx, ctypes.byref(info), ptr(recs), recs.size), self._ctx,
+                  "hm_state_export")
+        return {f: int(getattr(info, f)) for f in _INFO_FIELDS}, recs
+
+    def import_state(self, info, recs):
+        """Restore an exported state into this engine (which must not have processed a batch yet)."""
+        recs = np.ascontiguousarray(recs, dtype=STATE_REC_DTYPE)
+        hi = HmStateInfo(**{f: int(info[f]) for f in _INFO_FIELDS})
+        hi.n_keys = recs.size
+        check(self._lib.hm_state_import(self._ctx, ctypes.byref(hi), ptr(recs) if recs.size else None), self._ctx,
+              "hm_state_import")
+
+    def save_state(self, path):
+        """export_state() written atomically to `path` (.npz: plain arrays, no pickles)."""
+        info, recs = self.export_state()
+        save_state_file(path, info, recs)
+        return info
+
+    def load_state(self, path):
+        info, recs = load_state_file(path)
+        self.import_state(info, recs)
+        return info
+
     def last_timings(self):
         ms = (ctypes.c_double * 7)()
         check(self._lib.hm_last_timings(self._ctx, ms, 7), self._ctx)
@@ -124,6 +159,25 @@ class HeatmapEngine:
                            n_in=int(out.n_in), n_valid=int(out.n_valid), n_late=int(out.n_late),
                            n_state=int(out.n_state), batch_max_event_ms=int(out.batch_max_event_ms),
                            watermark_ms=int(out.watermark_ms), late_watermark_ms=int(out.late_watermark_ms))
+
+
+def save_state_file(path, info, recs):
+    import os
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "wb") as f:
+        np.savez(f, info=np.array([info[k] for k in _INFO_FIELDS], np.int64), recs=recs)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+
+
+def load_state_file(path):
+    with np.load(path, allow_pickle=False) as z:
+        vals = z["info"]
+        recs = z["recs"]
+    if vals.size != len(_INFO_FIELDS) or recs.dtype != STATE_REC_DTYPE:
+        raise RuntimeError(f"{path}: not a mobheat state checkpoint")
+    return {k: int(v) for k, v in zip(_INFO_FIELDS, vals)}, recs
 
 
 def latlng_to_cell(lat, lon, res, device=0):

@@ -32,16 +32,55 @@ TTL_MIN = int(os.getenv("TTL_MINUTES", "45"))
 WATERMARK_DELAY_MS = 10 * 60 * 1000          # withWatermark("eventTs", "10 minutes"), :107
 BULK_CHUNK = 1000                              # :191, :230
 DEVICE = int(os.getenv("MOBHEAT_DEVICE", os.getenv("LOCAL_RANK", "0")))
+# Spark keeps the aggregation state under checkpointLocation (:37, :244); the GPU state is checkpointed beside it
+# (CHECKPOINT_DIR/mobheat-state/state-<epoch>.npz) after each committed batch when MOBHEAT_STATE_CHECKPOINT=1.
+CHECKPOINT_DIR = os.getenv("CHECKPOINT", "/tmp/heatmap-checkpoint")
+STATE_CHECKPOINT = os.getenv("MOBHEAT_STATE_CHECKPOINT", "0") == "1"
+STATE_KEEP = 2     # the newest two: an epoch replayed after a crash between our save and Spark's commit log
 
 _ENGINE = None
 
 
-def get_engine():
+def _state_dir():
+    return os.path.join(CHECKPOINT_DIR, "mobheat-state")
+
+
+def _checkpoints():
+    """[(epoch, path)] of the saved states, oldest first."""
+    d = _state_dir()
+    if not os.path.isdir(d):
+        return []
+    out = []
+    for name in os.listdir(d):
+        if name.startswith("state-") and name.endswith(".npz"):
+            try:
+                out.append((int(name[6:-4]), os.path.join(d, name)))
+            except ValueError:
+                pass
+    return sorted(out)
+
+
+def get_engine(epoch_id=None):
+    """The process's engine; a new one resumes from the newest state checkpoint older than `epoch_id` (Spark
+    re-runs the first uncommitted epoch on the state of the one before it)."""
     global _ENGINE
     if _ENGINE is None:
-        _ENGINE = HeatmapEngine(h3_res=H3_RES, tile_minutes=TILE_MIN, watermark_delay_ms=WATERMARK_DELAY_MS,
-                                device=DEVICE)
+        eng = HeatmapEngine(h3_res=H3_RES, tile_minutes=TILE_MIN, watermark_delay_ms=WATERMARK_DELAY_MS,
+                            device=DEVICE)
+        if STATE_CHECKPOINT and epoch_id is not None:
+            older = [(e, p) for e, p in _checkpoints() if e < int(epoch_id)]
+            if older:
+                eng.load_state(older[-1][1])
+        _ENGINE = eng
     return _ENGINE
+
+
+def save_state_checkpoint(epoch_id):
+    """Write the engine's state after `epoch_id` and keep the newest STATE_KEEP checkpoints."""
+    os.makedirs(_state_dir(), exist_ok=True)
+    get_engine().save_state(os.path.join(_state_dir(), f"state-{int(epoch_id)}.npz"))
+    for _, p in _checkpoints()[:-STATE_KEEP]:
+        os.remove(p)
 
 
 def reset_engine():
@@ -218,7 +257,7 @@ def _flush(sink, collection, ops):
 def foreach_batch_func(df, epoch_id: int):
     """Runs on each micro-batch (reference heatmap_stream.py:150): tiles + latest positions -> MongoDB."""
     cols = batch_columns(df)
-    res = get_engine().process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"],
+    res = get_engine(epoch_id).process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"],
                                      cols["speed_valid"], cols["vkey"], cols["row_valid"])
     sink = SINK_FACTORY()
     try:
@@ -228,4 +267,6 @@ def foreach_batch_func(df, epoch_id: int):
         _flush(sink, "positions_latest", position_ops(cols, res.latest_rows))
     finally:
         sink.close()
+    if STATE_CHECKPOINT:   # after the writes succeeded: the batch is committed
+        save_state_checkpoint(epoch_id)
     return res

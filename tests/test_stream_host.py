@@ -5,6 +5,7 @@ Expected documents are written out literally from reference heatmap_stream.py:16
 encoded as UTC milliseconds, sub-millisecond digits dropped -- SURVEY.md App. A.7).
 """
 import datetime
+import os
 
 import bson
 import numpy as np
@@ -113,3 +114,48 @@ def test_iso_ts_strings_parse_like_to_timestamp():
     c = stream.batch_columns(df)
     assert c["ts_us"][0] == 1758890710 * 1_000_000
     assert c["row_valid"].tolist() == [True, False]
+
+
+def test_state_checkpoint_files_and_resume_choice(tmp_path, monkeypatch):
+    """CPU: the state checkpoint's file format round-trips (plain arrays, no pickles) and a restarted engine
+    resumes from the newest checkpoint OLDER than the incoming epoch (Spark re-runs the first uncommitted epoch
+    on the state of the one before it, reference heatmap_stream.py:37,244)."""
+    from mobheat import engine as eng_mod
+    from mobheat._lib import STATE_REC_DTYPE
+    recs = np.zeros(3, STATE_REC_DTYPE)
+    recs["cell"] = [1, 2, 3]
+    recs["sum_speed"] = [0.5, np.nan, -1.25]
+    info = dict(epoch_id=7, n_keys=3, watermark_ms=11, prev_watermark_ms=10, tile_us=300_000_000,
+                watermark_delay_ms=600_000, h3_res=8)
+    p = str(tmp_path / "s.npz")
+    eng_mod.save_state_file(p, info, recs)
+    info2, recs2 = eng_mod.load_state_file(p)
+    assert info2 == info
+    np.testing.assert_array_equal(recs2.view(np.uint8), recs.view(np.uint8))
+
+    loaded = []
+
+    class FakeEngine:
+        def __init__(self, **kw):
+            pass
+
+        def load_state(self, path):
+            loaded.append(os.path.basename(path))
+
+        def close(self):
+            pass
+
+    monkeypatch.setattr(stream, "HeatmapEngine", FakeEngine)
+    monkeypatch.setattr(stream, "CHECKPOINT_DIR", str(tmp_path))
+    monkeypatch.setattr(stream, "STATE_CHECKPOINT", True)
+    os.makedirs(stream._state_dir())
+    for e in (3, 4, 12):
+        open(os.path.join(stream._state_dir(), f"state-{e}.npz"), "wb").close()
+    open(os.path.join(stream._state_dir(), "state-x.npz"), "wb").close()
+    assert [e for e, _ in stream._checkpoints()] == [3, 4, 12]
+    for epoch, want in ((13, "state-12.npz"), (12, "state-4.npz"), (5, "state-4.npz"), (4, "state-3.npz"), (3, None)):
+        stream.reset_engine()
+        loaded.clear()
+        stream.get_engine(epoch)
+        assert loaded == ([want] if want else [])
+    stream.reset_engine()
