@@ -22,6 +22,9 @@
  *   hm_state_export / _import    -- the state store behind .option("checkpointLocation", CHECKPOINT_DIR)
  *                                   (:37,244): the tile state + watermark after a committed epoch, and its
  *                                   restore into a fresh context after a restart (the epoch is then replayed).
+ *   hm_encode_tile_updates       -- the tiles half of the batch writer (:164-196): one MongoDB `update`
+ *                                   statement {q, u: {$set: doc}, multi, upsert} per emitted tile, BSON-encoded
+ *                                   on the GPU exactly as pymongo encodes the reference's UpdateOne.
  */
 #ifndef MOBHEAT_H
 #define MOBHEAT_H
@@ -207,6 +210,35 @@ int hm_state_export(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs, int64_
 /* Restores an exported state into a context that has processed no batch (HM_E_STATE otherwise); the
  * config fields of info must equal the context's (HM_E_INVALID). recs: info->n_keys distinct keys, host memory. */
 int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *recs);
+
+/* Tiles of the last batch as MongoDB update statements (reference heatmap_stream.py:164-196): statement i is
+ * bytes[offsets[i], offsets[i+1]), the BSON document {q: {_id}, u: {$set: doc}, multi: false, upsert: true}
+ * that pymongo sends for the reference's UpdateOne({"_id": _id}, {"$set": doc}, upsert=True), doc as :164-188.
+ * Datetimes are pyspark's naive local wall times: the caller gives, for each window of hm_last_windows (same
+ * order), the local UTC offset in seconds at the window's start and at its end. Outputs are library-owned
+ * until the next call (device or pinned host memory per out_memory). */
+typedef struct hm_tile_doc_cfg {
+    const char *city;               /* CITY, UTF-8, at most 64 bytes */
+    int32_t city_len;
+    int32_t reserved;
+    int64_t ttl_ms;                 /* TTL_MINUTES * 60000 (staleAt = windowEnd + TTL) */
+    int64_t n_windows;
+    const int64_t *window_start_us; /* = hm_last_windows */
+    const int64_t *start_offset_s;
+    const int64_t *end_offset_s;
+} hm_tile_doc_cfg;
+
+/* The distinct window starts of the last batch's emitted tiles, ascending (*n = count; up to cap written). */
+int hm_last_windows(hm_ctx *ctx, int64_t *window_start_us, int64_t cap, int64_t *n);
+int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_memory, const uint8_t **bytes,
+                           const int64_t **offsets, int64_t *n_docs);
+
+/* Host execution of hm_encode_tile_updates' statement encoder on caller arrays (no GPU needed): statement i
+ * is bytes[offsets[i], offsets[i+1]) (offsets: n+1 entries; HM_E_INVALID if cap bytes do not suffice). */
+int hm_selftest_tile_statements(const hm_tile_doc_cfg *cfg, int32_t h3_res, int64_t tile_us, const uint64_t *cell,
+                                const int64_t *ws, const int64_t *cnt, const double *sp, const uint8_t *spn,
+                                const double *lon, const double *lat, int64_t n, uint8_t *bytes, int64_t cap,
+                                int64_t *offsets);
 
 /* Timing of the last hm_process_batch / stage call on the library's stream (HIP events), milliseconds
  * per phase: index 0 ingest (k_ingest: filter + cells + windows + pre-aggregation + dedup max), 1 reserved

@@ -33,6 +33,7 @@
 
 #include "../../include/mobheat.h"
 #include "kernels.h"
+#include "bson_docs.h"
 
 #define H3T_CONST static const
 #include "h3_tables.inc"
@@ -1644,6 +1645,12 @@ struct hm_ctx {
     // watermark (ms)
     int64_t wm_prev = 0, wm_cur = 0;
     int64_t epoch = -1;
+    // tile update statements (hm_encode_tile_updates): the last batch's emitted tiles and their windows
+    int64_t last_n_tiles = 0;
+    std::vector<int64_t> batch_windows;
+    DevBuf td_sizes, td_off, td_btot, td_boff, td_bytes, td_params;
+    void *h_td_bytes = nullptr, *h_td_off = nullptr;
+    size_t h_td_bytes_cap = 0, h_td_off_cap = 0;
     // stage API state
     int stage = 0;
     int nranks = 1, rank = 0;
@@ -1887,6 +1894,7 @@ static int gens_prepare(hm_ctx *ctx, const TilePartial *parts, int64_t n) {
     for (int q = 0; q < GMAP_SLOTS; q++) {
         const WinCount &w = ctx->h_cmap[q];
         if (!w.wenc) continue;
+        ctx->batch_windows.push_back(wdec(w.wenc));
         const int64_t c = (int64_t)w.count;
         auto it = std::find_if(ctx->gens.begin(), ctx->gens.end(), [&](const hm_ctx::Gen &g) { return g.wenc == w.wenc; });
         int L;
@@ -2140,6 +2148,7 @@ static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_par
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_state_new, 0, 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
     ctx->seq++;
+    ctx->batch_windows.clear();
     if ((rc = ensure_outputs(ctx, n_parts))) return rc;
     if (n_parts == n_gaps) {
         for (int e : {3, 7, 4, 5}) HIPCHK(ctx, hipEventRecord(ctx->ev[e], ctx->stream));
@@ -2168,6 +2177,8 @@ static int finish_outputs(hm_ctx *ctx, int64_t n_tiles, int64_t n_rows, const in
                           hm_batch_out *out) {
     out->n_tiles = n_tiles;
     out->n_latest = n_rows;
+    ctx->last_n_tiles = n_tiles;
+    std::sort(ctx->batch_windows.begin(), ctx->batch_windows.end());
     if (out_memory == HM_MEM_DEVICE) {
         out->cell = (const uint64_t *)ctx->o_cell.p;
         out->window_start_us = (const int64_t *)ctx->o_ws.p;
@@ -2357,7 +2368,8 @@ void hm_destroy(hm_ctx *ctx) {
                       &ctx->partials, &ctx->cands, &ctx->slow, &ctx->parts_sorted, &ctx->parts_regrow, &ctx->rp_H, &ctx->rp_O,
                       &ctx->rp_btot, &ctx->rp_boff,
                       &ctx->s_cell, &ctx->s_ws, &ctx->s_cnt, &ctx->s_sp, &ctx->s_spn, &ctx->s_lon, &ctx->s_lat, &ctx->bin_cnt, &ctx->bin_off, &ctx->dfused.used, &ctx->dfull.used, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
-                      &ctx->o_lon, &ctx->o_lat};
+                      &ctx->o_lon, &ctx->o_lat, &ctx->td_sizes, &ctx->td_off, &ctx->td_btot, &ctx->td_boff, &ctx->td_bytes,
+                      &ctx->td_params};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &g : ctx->gens) (void)hipFree(g.tab);
@@ -2370,7 +2382,8 @@ void hm_destroy(hm_ctx *ctx) {
     if (ctx->h_cmap) (void)hipHostFree(ctx->h_cmap);
     if (ctx->dfused.tab) (void)hipFree(ctx->dfused.tab);
     if (ctx->dfull.tab) (void)hipFree(ctx->dfull.tab);
-    void *hbufs[] = {ctx->h_cell, ctx->h_ws, ctx->h_cnt, ctx->h_sp, ctx->h_spn, ctx->h_lon, ctx->h_lat, ctx->h_rows};
+    void *hbufs[] = {ctx->h_cell, ctx->h_ws, ctx->h_cnt, ctx->h_sp, ctx->h_spn, ctx->h_lon, ctx->h_lat, ctx->h_rows,
+                     ctx->h_td_bytes, ctx->h_td_off};
     for (void *p : hbufs)
         if (p) (void)hipHostFree(p);
     if (ctx->d_st) (void)hipFree(ctx->d_st);
@@ -2746,6 +2759,129 @@ int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *
     return HM_OK;
 }
 
+// ---- tiles as MongoDB update statements (bson_docs.h; reference heatmap_stream.py:164-196) ----
+int hm_last_windows(hm_ctx *ctx, int64_t *window_start_us, int64_t cap, int64_t *n) {
+    if (!ctx || !n || cap < 0 || (cap > 0 && !window_start_us)) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    *n = (int64_t)ctx->batch_windows.size();
+    for (int64_t i = 0; i < *n && i < cap; i++) window_start_us[i] = ctx->batch_windows[i];
+    return HM_OK;
+}
+
+static int64_t civil_year(int64_t s) {   // proleptic Gregorian year of a second count since 1970 (host)
+    int64_t z = s / 86400 - ((s % 86400) < 0) + 719468;
+    const int64_t era = (z >= 0 ? z : z - 146096) / 146097, doe = z - era * 146097;
+    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365, doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const int64_t mp = (5 * doy + 2) / 153;
+    return yoe + era * 400 + (mp >= 10);
+}
+
+int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_memory, const uint8_t **bytes,
+                           const int64_t **offsets, int64_t *n_docs) {
+    if (!ctx || !cfg || !bytes || !offsets || !n_docs || cfg->city_len < 0 || (cfg->city_len > 0 && !cfg->city) ||
+        cfg->n_windows < 0 || (cfg->n_windows > 0 && (!cfg->window_start_us || !cfg->start_offset_s || !cfg->end_offset_s)))
+        return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (cfg->city_len > TD_MAX_CITY) return set_err(ctx, HM_E_INVALID, "city of %d bytes (at most %d)", cfg->city_len, TD_MAX_CITY);
+    const int64_t n = ctx->last_n_tiles;
+    const auto &W = ctx->batch_windows;
+    if (cfg->n_windows != (int64_t)W.size()) return set_err(ctx, HM_E_INVALID, "%lld window offsets for %zu windows", (long long)cfg->n_windows, W.size());
+    for (size_t k = 0; k < W.size(); k++) {
+        if (cfg->window_start_us[k] != W[k]) return set_err(ctx, HM_E_INVALID, "window offsets not in hm_last_windows order");
+        const int64_t a = W[k] / 1000000 - (W[k] % 1000000 < 0) + cfg->start_offset_s[k];
+        const int64_t b = (W[k] + ctx->cfg.tile_us) / 1000000 + cfg->end_offset_s[k];
+        if (civil_year(a) < 1000 || civil_year(a) > 9999 || civil_year(b) > 9999)
+            return set_err(ctx, HM_E_INVALID, "window start %lld us: year outside 1000-9999", (long long)W[k]);
+        if (W[k] % 1000000 != 0) return set_err(ctx, HM_E_INVALID, "window start %lld us is not a whole second", (long long)W[k]);
+    }
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc;
+    const int nw = (int)W.size();
+    // parameters: city bytes, then the window table (3 x nw int64)
+    const size_t pbytes = 64 + (size_t)nw * 24;
+    if ((rc = ensure(ctx, ctx->td_params, pbytes)) || (rc = ensure(ctx, ctx->td_off, (n + 1) * 8)) ||
+        (rc = ensure(ctx, ctx->td_sizes, std::max<int64_t>(n, 1) * 4)))
+        return rc;
+    std::vector<uint8_t> hp(pbytes, 0);
+    if (cfg->city_len) memcpy(hp.data(), cfg->city, cfg->city_len);
+    if (nw) {
+        memcpy(hp.data() + 64, W.data(), nw * 8);
+        memcpy(hp.data() + 64 + nw * 8, cfg->start_offset_s, nw * 8);
+        memcpy(hp.data() + 64 + nw * 16, cfg->end_offset_s, nw * 8);
+    }
+    HIPCHK(ctx, hipMemcpyAsync(ctx->td_params.p, hp.data(), pbytes, hipMemcpyHostToDevice, ctx->stream));
+    TileDocParams P;
+    P.city = (const uint8_t *)ctx->td_params.p;
+    P.city_len = cfg->city_len;
+    P.h3_res = ctx->cfg.h3_res;
+    P.tile_us = ctx->cfg.tile_us;
+    P.ttl_ms = cfg->ttl_ms;
+    P.win_start_us = (const int64_t *)((uint8_t *)ctx->td_params.p + 64);
+    P.off_start_s = P.win_start_us + nw;
+    P.off_end_s = P.win_start_us + 2 * nw;
+    P.n_win = nw;
+    unsigned long long *off = (unsigned long long *)ctx->td_off.p;
+    int64_t total = 0;
+    if (n > 0) {
+        if (nw == 0) return set_err(ctx, HM_E_STATE, "tiles without windows");
+        hipLaunchKernelGGL(k_tile_doc_sizes, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, P, (const uint64_t *)ctx->o_cell.p,
+                           (const int64_t *)ctx->o_ws.p, (const int64_t *)ctx->o_cnt.p, n, (unsigned *)ctx->td_sizes.p);
+        const int64_t nb = (n + SC_PER - 1) / SC_PER;
+        if ((rc = ensure(ctx, ctx->td_btot, nb * 4)) || (rc = ensure(ctx, ctx->td_boff, nb * 8))) return rc;
+        hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->td_sizes.p, n, off,
+                           (unsigned *)ctx->td_btot.p);
+        hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->td_btot.p, nb,
+                           (unsigned long long *)ctx->td_boff.p, off + n);
+        hipLaunchKernelGGL(k_scan_add, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, off, n, (const unsigned long long *)ctx->td_boff.p);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if ((rc = ensure(ctx, ctx->td_bytes, total + 16))) return rc;
+        // LDS staging sized by the longest statement this city/resolution can produce (int64 count, 16 hex
+        // digits): occupancy is bounded by it (~400 B per statement -> 3 workgroups per CU)
+        TileDocParams Ph = P;
+        Ph.city = (const uint8_t *)cfg->city;
+        Ph.win_start_us = W.data();
+        Ph.off_start_s = cfg->start_offset_s;
+        Ph.off_end_s = cfg->end_offset_s;
+        const int max_doc = tile_statement(nullptr, Ph, ~0ull, W[0], INT64_MAX, 0.0, 1, 0.0, 0.0);
+        if (max_doc > TD_MAX_DOC) return set_err(ctx, HM_E_INVALID, "statement of %d bytes exceeds %d", max_doc, TD_MAX_DOC);
+        const size_t lds = (size_t)TD_THREADS * ((max_doc + 15) & ~15) + 32;
+        if (lds > 65536)
+            HIPCHK(ctx, hipFuncSetAttribute((const void *)k_tile_docs, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(k_tile_docs, dim3(grid_for(n, TD_THREADS)), dim3(TD_THREADS), lds, ctx->stream, P, (const uint64_t *)ctx->o_cell.p,
+                           (const int64_t *)ctx->o_ws.p, (const int64_t *)ctx->o_cnt.p, (const double *)ctx->o_sp.p,
+                           (const uint8_t *)ctx->o_spn.p, (const double *)ctx->o_lon.p, (const double *)ctx->o_lat.p, n,
+                           (const unsigned long long *)off, (uint8_t *)ctx->td_bytes.p);
+        HIPCHK(ctx, hipGetLastError());
+    } else {
+        HIPCHK(ctx, hipMemsetAsync(off, 0, 8, ctx->stream));
+        if ((rc = ensure(ctx, ctx->td_bytes, 16))) return rc;
+    }
+    *n_docs = n;
+    if (out_memory == HM_MEM_DEVICE) {
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        *bytes = (const uint8_t *)ctx->td_bytes.p;
+        *offsets = (const int64_t *)ctx->td_off.p;
+        return HM_OK;
+    }
+    size_t dummy = 0;
+    if ((size_t)total + 16 > ctx->h_td_bytes_cap || !ctx->h_td_bytes) {
+        const size_t want = (size_t)total + total / 4 + 4096;
+        if ((rc = ensure_host(ctx, &ctx->h_td_bytes, dummy, want, 1))) return rc;
+        ctx->h_td_bytes_cap = want;
+    }
+    if ((size_t)n + 1 > ctx->h_td_off_cap || !ctx->h_td_off) {
+        const size_t want = (size_t)n + n / 4 + 1024;
+        if ((rc = ensure_host(ctx, &ctx->h_td_off, dummy, want, 8))) return rc;
+        ctx->h_td_off_cap = want;
+    }
+    if (total) HIPCHK(ctx, hipMemcpyAsync(ctx->h_td_bytes, ctx->td_bytes.p, total, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_td_off, off, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    *bytes = (const uint8_t *)ctx->h_td_bytes;
+    *offsets = (const int64_t *)ctx->h_td_off;
+    return HM_OK;
+}
+
 int hm_device_alloc(int32_t device, int64_t bytes, void **ptr) {
     if (!ptr || bytes < 0) return HM_E_INVALID;
     if (hipSetDevice(device) != hipSuccess) return HM_E_HIP;
@@ -2758,6 +2894,34 @@ int hm_device_free(int32_t device, void *ptr) {
 int hm_memcpy(void *dst, const void *src, int64_t bytes, int32_t kind) {
     hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
     return hipMemcpy(dst, src, bytes, k) == hipSuccess ? HM_OK : HM_E_HIP;
+}
+
+// host execution of the statement encoder (bson_docs.h) on caller arrays: bytes (capacity cap) + offsets[n+1]
+int hm_selftest_tile_statements(const hm_tile_doc_cfg *cfg, int32_t h3_res, int64_t tile_us, const uint64_t *cell,
+                                const int64_t *ws, const int64_t *cnt, const double *sp, const uint8_t *spn,
+                                const double *lon, const double *lat, int64_t n, uint8_t *bytes, int64_t cap,
+                                int64_t *offsets) {
+    if (!cfg || n < 0 || !offsets || cfg->n_windows <= 0 || cfg->city_len < 0 || cfg->city_len > TD_MAX_CITY) return HM_E_INVALID;
+    TileDocParams P;
+    P.city = (const uint8_t *)cfg->city;
+    P.city_len = cfg->city_len;
+    P.h3_res = h3_res;
+    P.tile_us = tile_us;
+    P.ttl_ms = cfg->ttl_ms;
+    P.win_start_us = cfg->window_start_us;
+    P.off_start_s = cfg->start_offset_s;
+    P.off_end_s = cfg->end_offset_s;
+    P.n_win = (int)cfg->n_windows;
+    int64_t o = 0;
+    for (int64_t i = 0; i < n; i++) {
+        offsets[i] = o;
+        const int len = tile_statement(nullptr, P, cell[i], ws[i], cnt[i], sp[i], spn[i], lon[i], lat[i]);
+        if (o + len > cap) return HM_E_INVALID;
+        tile_statement(bytes + o, P, cell[i], ws[i], cnt[i], sp[i], spn[i], lon[i], lat[i]);
+        o += len;
+    }
+    offsets[n] = o;
+    return HM_OK;
 }
 
 int hm_selftest_ld_ops(const double *a, int64_t n, int32_t op, double *out) {

@@ -59,6 +59,11 @@ class HmStateInfo(ctypes.Structure):
                 ("tile_us", c_i64), ("watermark_delay_ms", c_i64), ("h3_res", c_i32), ("reserved", c_i32)]
 
 
+class HmTileDocCfg(ctypes.Structure):
+    _fields_ = [("city", ctypes.c_char_p), ("city_len", c_i32), ("reserved", c_i32), ("ttl_ms", c_i64),
+                ("n_windows", c_i64), ("window_start_us", c_vp), ("start_offset_s", c_vp), ("end_offset_s", c_vp)]
+
+
 # hm_state_rec (64 B): one live (cellId, windowStart) key of the tile state
 STATE_REC_DTYPE = np.dtype([("cell", "<u8"), ("window_start_us", "<i8"), ("count", "<i8"), ("n_speed", "<i8"),
                             ("sum_speed", "<f8"), ("sum_lat", "<f8"), ("sum_lon", "<f8"), ("reserved", "<i8")])
@@ -85,6 +90,10 @@ SIGNATURES = {
     "hm_selftest_latlng_to_cell_fast_host": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "hm_state_export": (c_i32, [c_vp, _P(HmStateInfo), c_vp, c_i64]),
     "hm_state_import": (c_i32, [c_vp, _P(HmStateInfo), c_vp]),
+    "hm_last_windows": (c_i32, [c_vp, c_vp, c_i64, _P(c_i64)]),
+    "hm_encode_tile_updates": (c_i32, [c_vp, _P(HmTileDocCfg), c_i32, _P(c_vp), _P(c_vp), _P(c_i64)]),
+    "hm_selftest_tile_statements": (c_i32, [_P(HmTileDocCfg), c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                            c_i64, c_vp, c_i64, c_vp]),
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_abi_version": (c_i32, []),
 }
@@ -164,3 +173,45 @@ def latlng_to_cell_fast_host_selftest(lat, lon, res):
     fb = np.empty(lat.size, dtype=np.uint8)
     check(lib.hm_selftest_latlng_to_cell_fast_host(ptr(lat), ptr(lon), lat.size, res, ptr(out), ptr(fb)))
     return out, fb.astype(bool)
+
+
+def local_offsets_s(window_start_us, tile_us):
+    """Local-time offsets (s) at each window's start and end, as the reference's datetimes carry them: pyspark's
+    TimestampType.fromInternal gives naive local wall times (datetime.fromtimestamp), which bson then encodes as
+    if they were UTC (reference heatmap_stream.py:166-177 via stream._spark_datetime)."""
+    import calendar
+    import datetime as _dt
+
+    def off(us):
+        s = int(us) // 1_000_000
+        return calendar.timegm(_dt.datetime.fromtimestamp(s).timetuple()) - s
+    ws = np.ascontiguousarray(window_start_us, dtype=np.int64)
+    return (np.array([off(w) for w in ws], np.int64), np.array([off(w + tile_us) for w in ws], np.int64))
+
+
+def tile_doc_cfg(city, ttl_minutes, window_start_us, tile_us):
+    """hm_tile_doc_cfg for the given windows; the returned tuple keeps the arrays alive."""
+    cb = city.encode("utf-8")
+    ws = np.ascontiguousarray(window_start_us, dtype=np.int64)
+    so, eo = local_offsets_s(ws, tile_us)
+    cfg = HmTileDocCfg(city=cb, city_len=len(cb), ttl_ms=int(ttl_minutes) * 60_000, n_windows=ws.size,
+                       window_start_us=ptr(ws), start_offset_s=ptr(so), end_offset_s=ptr(eo))
+    return cfg, (cb, ws, so, eo)
+
+
+def tile_statements_selftest(tiles, city, h3_res, ttl_minutes, tile_us):
+    """Host execution of the GPU statement encoder on a TileRows (no GPU): (bytes uint8, offsets int64)."""
+    lib = load()
+    n = len(tiles)
+    wins = np.unique(tiles.window_start_us) if n else np.zeros(1, np.int64)
+    cfg, keep = tile_doc_cfg(city, ttl_minutes, wins, tile_us)
+    cap = 600 * max(n, 1)
+    buf = np.zeros(cap, np.uint8)
+    offs = np.zeros(n + 1, np.int64)
+    a = [np.ascontiguousarray(x) for x in (tiles.cell.astype(np.uint64), tiles.window_start_us.astype(np.int64),
+                                           tiles.count.astype(np.int64), tiles.avg_speed.astype(np.float64),
+                                           tiles.speed_null.astype(np.uint8), tiles.avg_lon.astype(np.float64),
+                                           tiles.avg_lat.astype(np.float64))]
+    check(lib.hm_selftest_tile_statements(ctypes.byref(cfg), int(h3_res), int(tile_us), *[ptr(x) for x in a], n,
+                                          ptr(buf), cap, ptr(offs)), None, "hm_selftest_tile_statements")
+    return buf[:offs[-1]].copy(), offs

@@ -138,6 +138,39 @@ class HeatmapEngine:
         self.import_state(info, recs)
         return info
 
+    # ---- tiles as MongoDB update statements, BSON-encoded on the GPU (reference heatmap_stream.py:164-196) ----
+    def encode_tile_updates(self, city, ttl_minutes):
+        """The last batch's tiles as the `update` statements pymongo would send for the reference's UpdateOne ops:
+        (bytes uint8, offsets int64[n+1]); statement i = bytes[offsets[i]:offsets[i+1]].  Valid until the next
+        call (copied out here)."""
+        n = ctypes.c_int64()
+        check(self._lib.hm_last_windows(self._ctx, None, 0, ctypes.byref(n)), self._ctx, "hm_last_windows")
+        wins = np.zeros(n.value, np.int64)
+        if wins.size:
+            check(self._lib.hm_last_windows(self._ctx, ptr(wins), wins.size, ctypes.byref(n)), self._ctx, "hm_last_windows")
+        cfg, keep = _lib.tile_doc_cfg(city, ttl_minutes, wins, self.tile_us)
+        pb, po, nd = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+        check(self._lib.hm_encode_tile_updates(self._ctx, ctypes.byref(cfg), HM_MEM_HOST, ctypes.byref(pb),
+                                               ctypes.byref(po), ctypes.byref(nd)), self._ctx, "hm_encode_tile_updates")
+        offs = np.ctypeslib.as_array(ctypes.cast(po, ctypes.POINTER(ctypes.c_int64)), shape=(nd.value + 1,)).copy()
+        total = int(offs[-1])
+        buf = (np.ctypeslib.as_array(ctypes.cast(pb, ctypes.POINTER(ctypes.c_uint8)), shape=(total,)).copy()
+               if total else np.zeros(0, np.uint8))
+        return buf, offs
+
+    def encode_tile_updates_device(self, city, ttl_minutes):
+        """The same, left on the device: (device pointer of the bytes, of the offsets, n statements)."""
+        n = ctypes.c_int64()
+        check(self._lib.hm_last_windows(self._ctx, None, 0, ctypes.byref(n)), self._ctx, "hm_last_windows")
+        wins = np.zeros(n.value, np.int64)
+        if wins.size:
+            check(self._lib.hm_last_windows(self._ctx, ptr(wins), wins.size, ctypes.byref(n)), self._ctx, "hm_last_windows")
+        cfg, keep = _lib.tile_doc_cfg(city, ttl_minutes, wins, self.tile_us)
+        pb, po, nd = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+        check(self._lib.hm_encode_tile_updates(self._ctx, ctypes.byref(cfg), HM_MEM_DEVICE, ctypes.byref(pb),
+                                               ctypes.byref(po), ctypes.byref(nd)), self._ctx, "hm_encode_tile_updates")
+        return pb.value, po.value, nd.value
+
     def last_timings(self):
         ms = (ctypes.c_double * 7)()
         check(self._lib.hm_last_timings(self._ctx, ms, 7), self._ctx)

@@ -103,6 +103,18 @@ class MongoSink:
     def bulk_write(self, collection, ops):
         self._db[collection].bulk_write(ops, ordered=False)
 
+    def update_raw(self, collection, statements):
+        """One unordered `update` command of pre-encoded statements (RawBSONDocument): the command pymongo's
+        bulk_write(ordered=False) sends for the same UpdateOne ops; write errors raise BulkWriteError like it."""
+        from bson.son import SON
+        from pymongo.errors import BulkWriteError
+        res = self._db.command(SON([("update", collection), ("updates", statements), ("ordered", False)]))
+        if res.get("writeErrors") or res.get("writeConcernError"):
+            raise BulkWriteError({"writeErrors": list(res.get("writeErrors", [])),
+                                  "writeConcernErrors": [res["writeConcernError"]] if res.get("writeConcernError") else [],
+                                  "nInserted": 0, "nUpserted": len(res.get("upserted", [])), "nMatched": res.get("n", 0),
+                                  "nModified": res.get("nModified", 0), "nRemoved": 0, "upserted": res.get("upserted", [])})
+
     def close(self):
         self._client.close()
 
@@ -253,6 +265,16 @@ def _flush(sink, collection, ops):
         sink.bulk_write(collection, ops[i:i + BULK_CHUNK])
 
 
+def _flush_statements(sink, collection, buf, offs):
+    """Pre-encoded update statements (hm_encode_tile_updates) in unordered batches of BULK_CHUNK (:191-196)."""
+    from bson.raw_bson import RawBSONDocument
+    b = buf.tobytes()   # (pymongo encodes RawBSONDocument from bytes only)
+    o = offs.tolist()
+    for i in range(0, len(o) - 1, BULK_CHUNK):
+        j = min(i + BULK_CHUNK, len(o) - 1)
+        sink.update_raw(collection, [RawBSONDocument(b[o[k]:o[k + 1]]) for k in range(i, j)])
+
+
 # ------------------ the drop-in boundary ------------------
 def foreach_batch_func(df, epoch_id: int):
     """Runs on each micro-batch (reference heatmap_stream.py:150): tiles + latest positions -> MongoDB."""
@@ -261,8 +283,9 @@ def foreach_batch_func(df, epoch_id: int):
                                      cols["speed_valid"], cols["vkey"], cols["row_valid"])
     sink = SINK_FACTORY()
     try:
-        # ---- 1) Upsert tiles (TTL via staleAt) ----
-        _flush(sink, "tiles", tile_ops(res.tiles))
+        # ---- 1) Upsert tiles (TTL via staleAt): the UpdateOne statements, BSON-encoded on the GPU ----
+        buf, offs = get_engine().encode_tile_updates(CITY, TTL_MIN)
+        _flush_statements(sink, "tiles", buf, offs)
         # ---- 2) latest per (provider, vehicleId) within this micro-batch ----
         _flush(sink, "positions_latest", position_ops(cols, res.latest_rows))
     finally:

@@ -159,6 +159,10 @@ def test_foreach_batch_func_restart_replays_epoch(tmp_path, monkeypatch):
         def bulk_write(self, coll, ops):
             Capture.ops.extend((coll, op._filter["_id"], op._doc) for op in ops)
 
+        def update_raw(self, coll, stmts):
+            import bson
+            Capture.ops.extend((coll, d["q"]["_id"], d["u"]) for d in (bson.decode(st.raw) for st in stmts))
+
         def close(self):
             pass
 

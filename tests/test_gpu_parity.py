@@ -260,6 +260,15 @@ def test_foreach_batch_func_capture_sink():
             assert len(ops) <= 1000
             Capture.ops.setdefault(coll, []).extend(ops)
 
+        def update_raw(self, coll, stmts):   # GPU-encoded statements: decoded back to (filter, update) pairs
+            import types
+            import bson
+            assert len(stmts) <= 1000
+            for st in stmts:
+                d = bson.decode(st.raw)
+                assert d["multi"] is False and d["upsert"] is True
+                Capture.ops.setdefault(coll, []).append(types.SimpleNamespace(_filter=d["q"], _doc=d["u"]))
+
         def close(self):
             pass
 

@@ -1,0 +1,99 @@
+"""GPU: the tiles sink's update statements BSON-encoded on the MI355X.
+
+Bar: bit-exact -- every statement equals the bytes pymongo encodes for the reference's UpdateOne
+(reference heatmap_stream.py:164-196; pymongo/synchronous/bulk.py add_update builds {q, u, multi, upsert}).
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+from test_stream_host import _reference_statements
+
+pytestmark = pytest.mark.gpu
+
+
+def _split(buf, offs):
+    return [buf[offs[i]:offs[i + 1]].tobytes() for i in range(offs.size - 1)]
+
+
+def test_c1_batch_statements_match_pymongo():
+    from mobheat import HeatmapEngine, synth
+    eng = HeatmapEngine(h3_res=8)
+    res = eng.process_batch(0, **synth.c1_boston())
+    buf, offs = eng.encode_tile_updates("ath", 45)
+    assert offs.size == len(res.tiles) + 1 > 100
+    assert _split(buf, offs) == _reference_statements(res.tiles, "ath", 8, 45)
+    eng.close()
+
+
+@pytest.mark.parametrize("tz", ["EET-2EEST,M3.5.0/3,M10.5.0/4", "UTC"])
+def test_stream_statements_local_time_and_dst(tz):
+    """Several batches around the EU DST change (2025-10-26 01:00 UTC), pyspark's naive local datetimes."""
+    from mobheat import HeatmapEngine
+    old = os.environ.get("TZ")
+    os.environ["TZ"] = tz
+    time.tzset()
+    try:
+        rng = np.random.default_rng(41)
+        eng = HeatmapEngine(h3_res=10, tile_minutes=5)
+        t0 = 1761440100 * 1_000_000 - 20 * 60_000_000
+        for e in range(4):
+            n = 30000
+            b = dict(lat=rng.uniform(37.90, 38.05, n), lon=rng.uniform(23.60, 23.85, n),
+                     ts_us=t0 + e * 10 * 60_000_000 + rng.integers(0, 15 * 60_000_000, n), speed=rng.uniform(0, 90, n),
+                     speed_valid=rng.random(n) > 0.3, vkey=rng.integers(0, 300, n).astype(np.uint64), row_valid=None)
+            res = eng.process_batch(e, **b)
+            buf, offs = eng.encode_tile_updates("αθήνα", 45)
+            assert _split(buf, offs) == _reference_statements(res.tiles, "αθήνα", 10, 45)
+        eng.close()
+    finally:
+        if old is None:
+            del os.environ["TZ"]
+        else:
+            os.environ["TZ"] = old
+        time.tzset()
+
+
+def test_large_batch_statements_and_device_copy():
+    """2e6 events at res 8 (~2e6 tiles): every statement equals the host execution of the same encoder, a
+    random sample equals pymongo's bytes, and the device-resident copy equals the host one."""
+    import ctypes
+    from mobheat import HeatmapEngine, _lib
+    from mobheat.engine import TileRows
+    rng = np.random.default_rng(42)
+    n = 2_000_000
+    eng = HeatmapEngine(h3_res=8)
+    res = eng.process_batch(0, lat=np.degrees(np.arcsin(rng.uniform(-1, 1, n))), lon=rng.uniform(-180, 180, n),
+                            ts_us=1759572000_000_000 + rng.integers(0, 15 * 60_000_000, n), speed=rng.uniform(0, 80, n),
+                            speed_valid=rng.random(n) > 0.1, vkey=rng.integers(0, 50000, n).astype(np.uint64))
+    buf, offs = eng.encode_tile_updates("ath", 45)
+    hb, ho = _lib.tile_statements_selftest(res.tiles, "ath", 8, 45, eng.tile_us)
+    np.testing.assert_array_equal(offs, ho)
+    np.testing.assert_array_equal(buf, hb)
+    pick = rng.choice(len(res.tiles), 2000, replace=False)
+    sub = TileRows(**{f: getattr(res.tiles, f)[pick] for f in TileRows.__dataclass_fields__})
+    assert [buf[offs[i]:offs[i + 1]].tobytes() for i in pick] == _reference_statements(sub, "ath", 8, 45)
+    pb, po, nd = eng.encode_tile_updates_device("ath", 45)
+    assert nd == len(res.tiles)
+    dev_offs = np.zeros(nd + 1, np.int64)
+    dev_buf = np.zeros(int(offs[-1]), np.uint8)
+    _lib.check(_lib.load().hm_memcpy(dev_offs.ctypes.data, po, dev_offs.nbytes, 1))
+    _lib.check(_lib.load().hm_memcpy(dev_buf.ctypes.data, pb, dev_buf.nbytes, 1))
+    np.testing.assert_array_equal(dev_offs, offs)
+    np.testing.assert_array_equal(dev_buf, buf)
+    eng.close()
+    del ctypes
+
+
+def test_empty_batch_and_errors():
+    from mobheat import HeatmapEngine
+    eng = HeatmapEngine(h3_res=8)
+    z = np.zeros(0)
+    eng.process_batch(0, lat=z, lon=z, ts_us=np.zeros(0, np.int64))
+    buf, offs = eng.encode_tile_updates("ath", 45)
+    assert buf.size == 0 and offs.tolist() == [0]
+    with pytest.raises(RuntimeError, match="city"):
+        eng.encode_tile_updates("x" * 65, 45)
+    eng.close()

@@ -159,3 +159,88 @@ def test_state_checkpoint_files_and_resume_choice(tmp_path, monkeypatch):
         stream.get_engine(epoch)
         assert loaded == ([want] if want else [])
     stream.reset_engine()
+
+
+def _reference_statements(tiles, city, h3_res, ttl_min):
+    """What pymongo sends for the reference's tile UpdateOne ops: bson of {q, u, multi: False, upsert: True}
+    (pymongo/synchronous/bulk.py add_update), the ops built as heatmap_stream.py:164-188 (stream.tile_ops)."""
+    return [bson.encode({"q": op._filter, "u": op._doc, "multi": False, "upsert": True})
+            for op in stream.tile_ops(tiles, city=city, h3_res=h3_res, ttl_min=ttl_min)]
+
+
+def _edge_tiles(rng, n, tile_us, t0_us):
+    ws = t0_us + tile_us * rng.integers(-3, 4, n)
+    cnt = rng.integers(1, 5000, n)
+    cnt[:3] = [2**31 - 1, 2**31, 2**40]                       # int32 / int64 boundary
+    sp = rng.uniform(0, 120, n)
+    sp[3:6] = [0.0, -0.0, np.nan]
+    lon = rng.uniform(-180, 180, n)
+    lat = rng.uniform(-90, 90, n)
+    lon[6:8] = [-0.0, 0.0]
+    lat[8:10] = [-0.0, np.nan]
+    cell = rng.integers(0x08000000_00000000, 0x08ffffff_ffffffff, n, dtype=np.uint64)
+    cell[10] = 0x1                                           # short hex (not a valid cell: formatting only)
+    return TileRows(cell=cell, window_start_us=ws, window_end_us=ws + tile_us, count=cnt, avg_speed=sp,
+                    speed_null=rng.random(n) < 0.2, avg_lon=lon, avg_lat=lat)
+
+
+@pytest.mark.parametrize("tz", ["UTC", "EET-2EEST,M3.5.0/3,M10.5.0/4", "EST+5EDT,M3.2.0/2,M11.1.0/2"])
+@pytest.mark.parametrize("h3_res,city,tile_min", [(8, "ath", 5), (12, "αθήνα-" + "x" * 40, 15), (0, "", 1)])
+def test_gpu_statement_encoder_matches_pymongo(tz, h3_res, city, tile_min):
+    """CPU: the GPU encoder's code (host execution, hm_selftest_tile_statements) writes exactly the bytes pymongo
+    encodes for the reference's UpdateOne ops -- under local time zones with DST transitions inside windows
+    (pyspark's naive local datetimes), int32/int64 counts, +-0.0 and NaN averages, null speeds, res 0-15."""
+    import time
+    from mobheat import _lib
+    old = os.environ.get("TZ")
+    os.environ["TZ"] = tz
+    time.tzset()
+    try:
+        rng = np.random.default_rng(h3_res)
+        tile_us = tile_min * 60_000_000
+        # 2025-10-26 00:55 UTC: the EU DST change (01:00 UTC) falls inside a window; 2025-11-02 06:00 UTC: the US one
+        t0 = (1761440100 if tz.startswith("EET") else 1762063200) * 1_000_000
+        t0 -= t0 % tile_us
+        tiles = _edge_tiles(rng, 400, tile_us, t0)
+        buf, offs = _lib.tile_statements_selftest(tiles, city, h3_res, 45, tile_us)
+        exp = _reference_statements(tiles, city, h3_res, 45)
+        assert offs.size == len(exp) + 1
+        for i, e in enumerate(exp):
+            got = buf[offs[i]:offs[i + 1]].tobytes()
+            assert got == e, (i, bson.decode(got), bson.decode(e))
+    finally:
+        if old is None:
+            del os.environ["TZ"]
+        else:
+            os.environ["TZ"] = old
+        time.tzset()
+
+
+def test_statement_batches_and_update_command(monkeypatch):
+    """CPU: GPU-encoded statements go out in unordered `update` commands of <= 1000 (reference :191-196); the
+    command is the one pymongo's bulk_write sends, and write errors raise BulkWriteError like bulk_write does."""
+    from bson.raw_bson import RawBSONDocument
+    from pymongo.errors import BulkWriteError
+    from mobheat import _lib
+    t = _edge_tiles(np.random.default_rng(5), 2500, 300_000_000, 1759572000_000_000)
+    buf, offs = _lib.tile_statements_selftest(t, "ath", 8, 45, 300_000_000)
+    cmds = []
+
+    class DB:
+        reply = {"ok": 1, "n": 0}
+
+        def command(self, cmd):
+            cmds.append(bson.decode(bson.encode(cmd)))       # encodable with the raw statements inside
+            return DB.reply
+
+    sink = stream.MongoSink.__new__(stream.MongoSink)
+    sink._db = DB()
+    stream._flush_statements(sink, "tiles", buf, offs)
+    assert [len(c["updates"]) for c in cmds] == [1000, 1000, 500]
+    assert all(list(c) == ["update", "updates", "ordered"] and c["update"] == "tiles" and c["ordered"] is False for c in cmds)
+    exp = _reference_statements(t, "ath", 8, 45)
+    got = [bson.encode(u) for c in cmds for u in c["updates"]]
+    assert got == exp
+    DB.reply = {"ok": 1, "n": 1, "writeErrors": [{"index": 0, "code": 11000, "errmsg": "dup"}]}
+    with pytest.raises(BulkWriteError):
+        sink.update_raw("tiles", [RawBSONDocument(exp[0])])
