@@ -25,6 +25,7 @@
  *   hm_encode_tile_updates       -- the tiles half of the batch writer (:164-196): one MongoDB `update`
  *                                   statement {q, u: {$set: doc}, multi, upsert} per emitted tile, BSON-encoded
  *                                   on the GPU exactly as pymongo encodes the reference's UpdateOne.
+ *   hm_encode_position_updates   -- the positions half (:198-235): one positions_latest statement per latest row.
  */
 #ifndef MOBHEAT_H
 #define MOBHEAT_H
@@ -233,12 +234,38 @@ int hm_last_windows(hm_ctx *ctx, int64_t *window_start_us, int64_t cap, int64_t 
 int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_memory, const uint8_t **bytes,
                            const int64_t **offsets, int64_t *n_docs);
 
+/* Latest positions of the last hm_process_batch as positions_latest update statements (reference
+ * heatmap_stream.py:211-235): {q: {_id: "provider|vehicleId", $or: [{ts: {$exists: false}}, {ts: {$lt: ts}}]},
+ * u: {$set: {provider, vehicleId, ts, loc}}, multi: false, upsert: true}, in latest_row order. The strings come
+ * from the batch's dictionaries (the vkey the caller passed = provider_code * n_vehicles + vehicle_code; string k
+ * of a dictionary = bytes[offsets[k], offsets[k+1]), UTF-8); ts is the naive local datetime of eventTs, with the
+ * local UTC offset of each 900-s bucket floor(ts_s / 900) - bucket0 given by bucket_offset_s. Not after stage
+ * calls (HM_E_STATE). Outputs as hm_encode_tile_updates. */
+typedef struct hm_position_doc_cfg {
+    int64_t n_providers;
+    const int64_t *provider_offsets;   /* n_providers + 1 */
+    const char *provider_bytes;
+    int64_t n_vehicles;
+    const int64_t *vehicle_offsets;    /* n_vehicles + 1 */
+    const char *vehicle_bytes;
+    int64_t bucket0;
+    int64_t n_buckets;
+    const int64_t *bucket_offset_s;
+} hm_position_doc_cfg;
+int hm_encode_position_updates(hm_ctx *ctx, const hm_position_doc_cfg *cfg, int32_t out_memory, const uint8_t **bytes,
+                               const int64_t **offsets, int64_t *n_docs);
+
 /* Host execution of hm_encode_tile_updates' statement encoder on caller arrays (no GPU needed): statement i
  * is bytes[offsets[i], offsets[i+1]) (offsets: n+1 entries; HM_E_INVALID if cap bytes do not suffice). */
 int hm_selftest_tile_statements(const hm_tile_doc_cfg *cfg, int32_t h3_res, int64_t tile_us, const uint64_t *cell,
                                 const int64_t *ws, const int64_t *cnt, const double *sp, const uint8_t *spn,
                                 const double *lon, const double *lat, int64_t n, uint8_t *bytes, int64_t cap,
                                 int64_t *offsets);
+
+/* Host execution of hm_encode_position_updates' encoder on caller rows (row i: vkey[i], ts[i], lat[i], lon[i]). */
+int hm_selftest_position_statements(const hm_position_doc_cfg *cfg, const uint64_t *vkey, const int64_t *ts,
+                                    const double *lat, const double *lon, int64_t n, uint8_t *bytes, int64_t cap,
+                                    int64_t *offsets);
 
 /* Timing of the last hm_process_batch / stage call on the library's stream (HIP events), milliseconds
  * per phase: index 0 ingest (k_ingest: filter + cells + windows + pre-aggregation + dedup max), 1 reserved

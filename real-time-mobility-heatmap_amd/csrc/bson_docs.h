@@ -236,4 +236,122 @@ __global__ __launch_bounds__(TD_THREADS) void k_tile_docs(TileDocParams P, const
     }
 }
 
+// ---- positions_latest statements (reference heatmap_stream.py:211-228) ----
+// UpdateOne({"_id": f"{provider}|{vehicleId}", "$or": [{"ts": {"$exists": False}}, {"ts": {"$lt": ts}}]},
+//           {"$set": {provider, vehicleId, ts, loc: {type: "Point", coordinates: [lon, lat]}}}, upsert=True)
+// for each latest row; provider / vehicleId come from the batch's string dictionaries (the host's factorization:
+// vkey = provider_code * n_vehicles + vehicle_code), ts is pyspark's naive local datetime of eventTs (the local
+// offset from a table of 900-s buckets), lat/lon the row's values as float().
+struct PosDocParams {
+    const int64_t *p_off;   // n_p + 1 offsets into p_bytes
+    const uint8_t *p_bytes;
+    const int64_t *v_off;
+    const uint8_t *v_bytes;
+    int64_t n_vehicles;
+    int64_t n_providers;
+    int64_t bucket0;        // first 900-s bucket (floor(ts_s / 900)) and the local offset (s) of each
+    int64_t n_buckets;
+    const int64_t *bucket_off;
+};
+
+// the row's codes and time bucket lie inside the caller's tables (else the host reports an error)
+HM_HD bool position_ok(const PosDocParams &P, uint64_t vkey, int64_t ts_us) {
+    if (P.n_vehicles <= 0 || vkey / (uint64_t)P.n_vehicles >= (uint64_t)P.n_providers) return false;
+    const int64_t b = floordiv(floordiv(ts_us, 1000000), 900) - P.bucket0;
+    return b >= 0 && b < P.n_buckets;
+}
+
+HM_HD int64_t bson_date_ms(int64_t ts_us, int64_t off_s) {
+    const int64_t s = floordiv(ts_us, 1000000);
+    return (s + off_s) * 1000 + (ts_us - s * 1000000) / 1000;
+}
+
+HM_HD int position_statement(uint8_t *dst, const PosDocParams &P, uint64_t vkey, int64_t ts_us, double lat, double lon) {
+    const int64_t pc = (int64_t)(vkey / (uint64_t)P.n_vehicles), vc = (int64_t)(vkey % (uint64_t)P.n_vehicles);
+    const uint8_t *ps = P.p_bytes + P.p_off[pc], *vs = P.v_bytes + P.v_off[vc];
+    const int pl = (int)(P.p_off[pc + 1] - P.p_off[pc]), vl = (int)(P.v_off[vc + 1] - P.v_off[vc]);
+    const int64_t date = bson_date_ms(ts_us, P.bucket_off[floordiv(floordiv(ts_us, 1000000), 900) - P.bucket0]);
+    BsonW w{dst, 0};
+    const int top = w.begin();
+    w.key(0x03, "q");
+    const int q = w.begin();
+    w.key(0x02, "_id");
+    w.i32(pl + 1 + vl + 1);
+    for (int k = 0; k < pl; k++) w.u8(ps[k]);
+    w.u8('|');
+    for (int k = 0; k < vl; k++) w.u8(vs[k]);
+    w.u8(0);
+    w.key(0x04, "$or");
+    const int arr = w.begin();
+    w.key(0x03, "0");
+    const int e0 = w.begin();
+    w.key(0x03, "ts");
+    const int e0t = w.begin();
+    w.key(0x08, "$exists");
+    w.u8(0);
+    w.end(e0t);
+    w.end(e0);
+    w.key(0x03, "1");
+    const int e1 = w.begin();
+    w.key(0x03, "ts");
+    const int e1t = w.begin();
+    w.key(0x09, "$lt");
+    w.i64(date);
+    w.end(e1t);
+    w.end(e1);
+    w.end(arr);
+    w.end(q);
+    w.key(0x03, "u");
+    const int u = w.begin();
+    w.key(0x03, "$set");
+    const int set = w.begin();
+    str_field(w, "provider", ps, pl);
+    str_field(w, "vehicleId", vs, vl);
+    w.key(0x09, "ts");
+    w.i64(date);
+    w.key(0x03, "loc");
+    const int c = w.begin();
+    str_field(w, "type", (const uint8_t *)"Point", 5);
+    w.key(0x04, "coordinates");
+    const int a = w.begin();
+    w.key(0x01, "0");
+    w.f64(lon);
+    w.key(0x01, "1");
+    w.f64(lat);
+    w.end(a);
+    w.end(c);
+    w.end(set);
+    w.end(u);
+    w.key(0x08, "multi");
+    w.u8(0);
+    w.key(0x08, "upsert");
+    w.u8(1);
+    w.end(top);
+    return w.n;
+}
+
+// sizes (pass 1) and statements written straight to HBM (pass 2: one thread per statement; positions are at most
+// one per vehicle, and their strings make the lengths vary, so there is no LDS staging)
+__global__ __launch_bounds__(256) void k_pos_doc_sizes(PosDocParams P, const int64_t *__restrict__ rows, int64_t n,
+                                                       const uint64_t *__restrict__ vk, const int64_t *__restrict__ ts,
+                                                       unsigned *__restrict__ sizes, unsigned long long *bad) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t r = rows[i];
+        const bool ok = position_ok(P, vk[r], ts[r]);
+        if (!ok) atomicAdd(bad, 1ull);
+        sizes[i] = ok ? (unsigned)position_statement(nullptr, P, vk[r], ts[r], 0.0, 0.0) : 0u;
+    }
+}
+__global__ __launch_bounds__(256) void k_pos_docs(PosDocParams P, const int64_t *__restrict__ rows, int64_t n,
+                                                  const uint64_t *__restrict__ vk, const int64_t *__restrict__ ts,
+                                                  const double *__restrict__ lat, const double *__restrict__ lon,
+                                                  const unsigned long long *__restrict__ off, uint8_t *__restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t r = rows[i];
+        if (position_ok(P, vk[r], ts[r])) position_statement(out + off[i], P, vk[r], ts[r], lat[r], lon[r]);
+    }
+}
+
 }  // namespace hm

@@ -1647,6 +1647,10 @@ struct hm_ctx {
     int64_t epoch = -1;
     // tile update statements (hm_encode_tile_updates): the last batch's emitted tiles and their windows
     int64_t last_n_tiles = 0;
+    int64_t last_n_latest = -1;   // the last hm_process_batch's latest rows (ctx->rows) and its input columns
+    const uint64_t *last_vk = nullptr;
+    const int64_t *last_ts = nullptr;
+    const double *last_lat = nullptr, *last_lon = nullptr;
     std::vector<int64_t> batch_windows;
     DevBuf td_sizes, td_off, td_btot, td_boff, td_bytes, td_params;
     void *h_td_bytes = nullptr, *h_td_off = nullptr;
@@ -1666,7 +1670,9 @@ constexpr int DUSED_WORD = 253;
 constexpr int FULL_USED_WORD = 240;   // used-slot count of the full dedup table
 constexpr int SLOW_WORD = 252;   // number of k_ingest fast-path exceptions of the current batch
 constexpr int REGROW_WORD = 251; // records dumped by k_dump_gen
-constexpr int GIVEUP_WORD = 232; // k_ingest's fused dedup gave up (a cache line of its own: words 232-239)
+constexpr int GIVEUP_WORD = 232;
+constexpr int POSBAD_WORD = 241; // position statements: rows outside the caller's dictionaries
+// (GIVEUP_WORD: k_ingest's fused dedup gave up, a cache line of its own: words 232-239)
 
 #define HIPCHK(ctx, expr)                                                                             \
     do {                                                                                              \
@@ -2412,6 +2418,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     HIPCHK(ctx, hipSetDevice(ctx->device));
     memset(out, 0, sizeof(*out));
     ctx->epoch = epoch_id;
+    ctx->last_n_latest = -1;
     int rc;
     // 1. evict with this batch's eviction watermark happened at the end of the previous batch (see below)
     int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
@@ -2438,6 +2445,11 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if (s2.overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     if (s2.bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved (%llu rows)", s2.bad_vkey);
     int64_t n_rows = (int64_t)ctx->h_scratch[255];
+    ctx->last_n_latest = n_rows;
+    ctx->last_vk = I.vk;
+    ctx->last_ts = I.ts;
+    ctx->last_lat = I.lat;
+    ctx->last_lon = I.lon;
     record_timings(ctx);
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, n_rows, (const int64_t *)ctx->rows.p, out_memory, out))) return rc;
     // 5. eviction after emission with this batch's watermark (lazy: see hm_ctx), then advance the watermark
@@ -2504,6 +2516,7 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc;
     ctx->epoch = epoch_id;
+    ctx->last_n_latest = -1;   // (hm_encode_position_updates: single-context batches only)
     ctx->nranks = nranks;
     ctx->rank = rank;
     int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
@@ -2775,6 +2788,37 @@ static int64_t civil_year(int64_t s) {   // proleptic Gregorian year of a second
     return yoe + era * 400 + (mp >= 10);
 }
 
+// the statements in ctx->td_bytes / td_off: handed out on the device or copied to pinned host buffers
+static int statements_out(hm_ctx *ctx, int64_t n, int64_t total, int32_t out_memory, const uint8_t **bytes,
+                          const int64_t **offsets, int64_t *n_docs) {
+    int rc;
+    unsigned long long *off = (unsigned long long *)ctx->td_off.p;
+    *n_docs = n;
+    if (out_memory == HM_MEM_DEVICE) {
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        *bytes = (const uint8_t *)ctx->td_bytes.p;
+        *offsets = (const int64_t *)ctx->td_off.p;
+        return HM_OK;
+    }
+    size_t dummy = 0;
+    if ((size_t)total + 16 > ctx->h_td_bytes_cap || !ctx->h_td_bytes) {
+        const size_t want = (size_t)total + total / 4 + 4096;
+        if ((rc = ensure_host(ctx, &ctx->h_td_bytes, dummy, want, 1))) return rc;
+        ctx->h_td_bytes_cap = want;
+    }
+    if ((size_t)n + 1 > ctx->h_td_off_cap || !ctx->h_td_off) {
+        const size_t want = (size_t)n + n / 4 + 1024;
+        if ((rc = ensure_host(ctx, &ctx->h_td_off, dummy, want, 8))) return rc;
+        ctx->h_td_off_cap = want;
+    }
+    if (total) HIPCHK(ctx, hipMemcpyAsync(ctx->h_td_bytes, ctx->td_bytes.p, total, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_td_off, off, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    *bytes = (const uint8_t *)ctx->h_td_bytes;
+    *offsets = (const int64_t *)ctx->h_td_off;
+    return HM_OK;
+}
+
 int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_memory, const uint8_t **bytes,
                            const int64_t **offsets, int64_t *n_docs) {
     if (!ctx || !cfg || !bytes || !offsets || !n_docs || cfg->city_len < 0 || (cfg->city_len > 0 && !cfg->city) ||
@@ -2856,30 +2900,89 @@ int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_
         HIPCHK(ctx, hipMemsetAsync(off, 0, 8, ctx->stream));
         if ((rc = ensure(ctx, ctx->td_bytes, 16))) return rc;
     }
-    *n_docs = n;
-    if (out_memory == HM_MEM_DEVICE) {
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        *bytes = (const uint8_t *)ctx->td_bytes.p;
-        *offsets = (const int64_t *)ctx->td_off.p;
-        return HM_OK;
-    }
-    size_t dummy = 0;
-    if ((size_t)total + 16 > ctx->h_td_bytes_cap || !ctx->h_td_bytes) {
-        const size_t want = (size_t)total + total / 4 + 4096;
-        if ((rc = ensure_host(ctx, &ctx->h_td_bytes, dummy, want, 1))) return rc;
-        ctx->h_td_bytes_cap = want;
-    }
-    if ((size_t)n + 1 > ctx->h_td_off_cap || !ctx->h_td_off) {
-        const size_t want = (size_t)n + n / 4 + 1024;
-        if ((rc = ensure_host(ctx, &ctx->h_td_off, dummy, want, 8))) return rc;
-        ctx->h_td_off_cap = want;
-    }
-    if (total) HIPCHK(ctx, hipMemcpyAsync(ctx->h_td_bytes, ctx->td_bytes.p, total, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_td_off, off, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    *bytes = (const uint8_t *)ctx->h_td_bytes;
-    *offsets = (const int64_t *)ctx->h_td_off;
+    return statements_out(ctx, n, total, out_memory, bytes, offsets, n_docs);
+}
+
+// latest positions of the last hm_process_batch as positions_latest update statements (bson_docs.h)
+static int pos_params(hm_ctx *ctx, const hm_position_doc_cfg *cfg, PosDocParams &P, std::vector<uint8_t> &hp) {
+    const int64_t np_ = cfg->n_providers, nv = cfg->n_vehicles, nb = cfg->n_buckets;
+    if (np_ < 0 || nv < 0 || nb < 0 || (np_ && (!cfg->provider_offsets || !cfg->provider_bytes)) ||
+        (nv && (!cfg->vehicle_offsets || !cfg->vehicle_bytes)) || (nb && !cfg->bucket_offset_s))
+        return set_err(ctx, HM_E_INVALID, "bad position dictionaries");
+    const int64_t pb = np_ ? cfg->provider_offsets[np_] : 0, vb = nv ? cfg->vehicle_offsets[nv] : 0;
+    for (int64_t k = 0; k < np_; k++)
+        if (cfg->provider_offsets[k] < 0 || cfg->provider_offsets[k] > cfg->provider_offsets[k + 1] ||
+            cfg->provider_offsets[k + 1] - cfg->provider_offsets[k] > (1 << 20))
+            return set_err(ctx, HM_E_INVALID, "provider offsets");
+    for (int64_t k = 0; k < nv; k++)
+        if (cfg->vehicle_offsets[k] < 0 || cfg->vehicle_offsets[k] > cfg->vehicle_offsets[k + 1] ||
+            cfg->vehicle_offsets[k + 1] - cfg->vehicle_offsets[k] > (1 << 20))
+            return set_err(ctx, HM_E_INVALID, "vehicle offsets");
+    // one device block: offsets (8-B aligned) first, then the string bytes
+    const size_t o_p = 0, o_v = o_p + (np_ + 1) * 8, o_b = o_v + (nv + 1) * 8, o_ps = o_b + nb * 8, o_vs = o_ps + pb;
+    hp.assign(o_vs + vb + 8, 0);
+    if (np_) memcpy(hp.data() + o_p, cfg->provider_offsets, (np_ + 1) * 8);
+    if (nv) memcpy(hp.data() + o_v, cfg->vehicle_offsets, (nv + 1) * 8);
+    if (nb) memcpy(hp.data() + o_b, cfg->bucket_offset_s, nb * 8);
+    if (pb) memcpy(hp.data() + o_ps, cfg->provider_bytes, pb);
+    if (vb) memcpy(hp.data() + o_vs, cfg->vehicle_bytes, vb);
+    int rc;
+    if ((rc = ensure(ctx, ctx->td_params, hp.size()))) return rc;
+    HIPCHK(ctx, hipMemcpyAsync(ctx->td_params.p, hp.data(), hp.size(), hipMemcpyHostToDevice, ctx->stream));
+    uint8_t *d = (uint8_t *)ctx->td_params.p;
+    P.p_off = (const int64_t *)(d + o_p);
+    P.v_off = (const int64_t *)(d + o_v);
+    P.bucket_off = (const int64_t *)(d + o_b);
+    P.p_bytes = d + o_ps;
+    P.v_bytes = d + o_vs;
+    P.n_providers = np_;
+    P.n_vehicles = nv;
+    P.bucket0 = cfg->bucket0;
+    P.n_buckets = nb;
     return HM_OK;
+}
+
+int hm_encode_position_updates(hm_ctx *ctx, const hm_position_doc_cfg *cfg, int32_t out_memory, const uint8_t **bytes,
+                               const int64_t **offsets, int64_t *n_docs) {
+    if (!ctx || !cfg || !bytes || !offsets || !n_docs) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->last_n_latest < 0) return set_err(ctx, HM_E_STATE, "no hm_process_batch latest rows to encode");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int64_t n = ctx->last_n_latest;
+    int rc;
+    PosDocParams P;
+    std::vector<uint8_t> hp;
+    if ((rc = pos_params(ctx, cfg, P, hp))) return rc;
+    if ((rc = ensure(ctx, ctx->td_off, (n + 1) * 8)) || (rc = ensure(ctx, ctx->td_sizes, std::max<int64_t>(n, 1) * 4))) return rc;
+    unsigned long long *off = (unsigned long long *)ctx->td_off.p;
+    int64_t total = 0;
+    if (n > 0) {
+        const int64_t *rows = (const int64_t *)ctx->rows.p;
+        HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + POSBAD_WORD, 0, 8, ctx->stream));
+        hipLaunchKernelGGL(k_pos_doc_sizes, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, P, rows, n, ctx->last_vk,
+                           ctx->last_ts, (unsigned *)ctx->td_sizes.p, ctx->d_scratch + POSBAD_WORD);
+        const int64_t nb = (n + SC_PER - 1) / SC_PER;
+        if ((rc = ensure(ctx, ctx->td_btot, nb * 4)) || (rc = ensure(ctx, ctx->td_boff, nb * 8))) return rc;
+        hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->td_sizes.p, n, off,
+                           (unsigned *)ctx->td_btot.p);
+        hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->td_btot.p, nb,
+                           (unsigned long long *)ctx->td_boff.p, off + n);
+        hipLaunchKernelGGL(k_scan_add, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, off, n, (const unsigned long long *)ctx->td_boff.p);
+        HIPCHK(ctx, hipGetLastError());
+        unsigned long long hb[2] = {0, 0};
+        HIPCHK(ctx, hipMemcpyAsync(&hb[0], off + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(&hb[1], ctx->d_scratch + POSBAD_WORD, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (hb[1]) return set_err(ctx, HM_E_INVALID, "%llu latest rows outside the provider/vehicle dictionaries or time buckets", hb[1]);
+        total = (int64_t)hb[0];
+        if ((rc = ensure(ctx, ctx->td_bytes, total + 16))) return rc;
+        hipLaunchKernelGGL(k_pos_docs, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, P, rows, n, ctx->last_vk, ctx->last_ts,
+                           ctx->last_lat, ctx->last_lon, (const unsigned long long *)off, (uint8_t *)ctx->td_bytes.p);
+        HIPCHK(ctx, hipGetLastError());
+    } else {
+        HIPCHK(ctx, hipMemsetAsync(off, 0, 8, ctx->stream));
+        if ((rc = ensure(ctx, ctx->td_bytes, 16))) return rc;
+    }
+    return statements_out(ctx, n, total, out_memory, bytes, offsets, n_docs);
 }
 
 int hm_device_alloc(int32_t device, int64_t bytes, void **ptr) {
@@ -2918,6 +3021,34 @@ int hm_selftest_tile_statements(const hm_tile_doc_cfg *cfg, int32_t h3_res, int6
         const int len = tile_statement(nullptr, P, cell[i], ws[i], cnt[i], sp[i], spn[i], lon[i], lat[i]);
         if (o + len > cap) return HM_E_INVALID;
         tile_statement(bytes + o, P, cell[i], ws[i], cnt[i], sp[i], spn[i], lon[i], lat[i]);
+        o += len;
+    }
+    offsets[n] = o;
+    return HM_OK;
+}
+
+// host execution of the positions statement encoder (bson_docs.h) on caller rows (vkey, ts, lat, lon per row)
+int hm_selftest_position_statements(const hm_position_doc_cfg *cfg, const uint64_t *vkey, const int64_t *ts,
+                                    const double *lat, const double *lon, int64_t n, uint8_t *bytes, int64_t cap,
+                                    int64_t *offsets) {
+    if (!cfg || n < 0 || !offsets) return HM_E_INVALID;
+    PosDocParams P;
+    P.p_off = cfg->provider_offsets;
+    P.p_bytes = (const uint8_t *)cfg->provider_bytes;
+    P.v_off = cfg->vehicle_offsets;
+    P.v_bytes = (const uint8_t *)cfg->vehicle_bytes;
+    P.n_providers = cfg->n_providers;
+    P.n_vehicles = cfg->n_vehicles;
+    P.bucket0 = cfg->bucket0;
+    P.n_buckets = cfg->n_buckets;
+    P.bucket_off = cfg->bucket_offset_s;
+    int64_t o = 0;
+    for (int64_t i = 0; i < n; i++) {
+        offsets[i] = o;
+        if (!position_ok(P, vkey[i], ts[i])) return HM_E_INVALID;
+        const int len = position_statement(nullptr, P, vkey[i], ts[i], lat[i], lon[i]);
+        if (o + len > cap) return HM_E_INVALID;
+        position_statement(bytes + o, P, vkey[i], ts[i], lat[i], lon[i]);
         o += len;
     }
     offsets[n] = o;

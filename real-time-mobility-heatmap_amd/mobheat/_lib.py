@@ -64,6 +64,12 @@ class HmTileDocCfg(ctypes.Structure):
                 ("n_windows", c_i64), ("window_start_us", c_vp), ("start_offset_s", c_vp), ("end_offset_s", c_vp)]
 
 
+class HmPositionDocCfg(ctypes.Structure):
+    _fields_ = [("n_providers", c_i64), ("provider_offsets", c_vp), ("provider_bytes", c_vp),
+                ("n_vehicles", c_i64), ("vehicle_offsets", c_vp), ("vehicle_bytes", c_vp),
+                ("bucket0", c_i64), ("n_buckets", c_i64), ("bucket_offset_s", c_vp)]
+
+
 # hm_state_rec (64 B): one live (cellId, windowStart) key of the tile state
 STATE_REC_DTYPE = np.dtype([("cell", "<u8"), ("window_start_us", "<i8"), ("count", "<i8"), ("n_speed", "<i8"),
                             ("sum_speed", "<f8"), ("sum_lat", "<f8"), ("sum_lon", "<f8"), ("reserved", "<i8")])
@@ -94,6 +100,9 @@ SIGNATURES = {
     "hm_encode_tile_updates": (c_i32, [c_vp, _P(HmTileDocCfg), c_i32, _P(c_vp), _P(c_vp), _P(c_i64)]),
     "hm_selftest_tile_statements": (c_i32, [_P(HmTileDocCfg), c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_i64, c_vp, c_i64, c_vp]),
+    "hm_encode_position_updates": (c_i32, [c_vp, _P(HmPositionDocCfg), c_i32, _P(c_vp), _P(c_vp), _P(c_i64)]),
+    "hm_selftest_position_statements": (c_i32, [_P(HmPositionDocCfg), c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                                c_vp]),
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_abi_version": (c_i32, []),
 }
@@ -214,4 +223,64 @@ def tile_statements_selftest(tiles, city, h3_res, ttl_minutes, tile_us):
                                            tiles.avg_lat.astype(np.float64))]
     check(lib.hm_selftest_tile_statements(ctypes.byref(cfg), int(h3_res), int(tile_us), *[ptr(x) for x in a], n,
                                           ptr(buf), cap, ptr(offs)), None, "hm_selftest_tile_statements")
+    return buf[:offs[-1]].copy(), offs
+
+
+MAX_TIME_BUCKETS = 1 << 17   # 900-s buckets of local offsets a position batch may span (~3.7 years)
+
+
+def _dictionary(strings):
+    """(n, offsets int64[n+1], bytes) of a list of str, UTF-8 (Arrow's string layout)."""
+    import pyarrow as pa
+    arr = pa.array(list(strings), type=pa.large_string())
+    n = len(arr)
+    offs = np.frombuffer(arr.buffers()[1], dtype=np.int64, count=n + 1, offset=arr.offset * 8).copy() if n else np.zeros(1, np.int64)
+    offs -= offs[0]
+    data = arr.buffers()[2]
+    raw = np.frombuffer(data, dtype=np.uint8).copy() if data is not None and offs[-1] else np.zeros(1, np.uint8)
+    return n, offs, raw
+
+
+def position_doc_cfg(provider_uniques, vehicle_uniques, ts_min_us, ts_max_us):
+    """hm_position_doc_cfg for a batch's string dictionaries (pandas.factorize uniques, the order the vkeys were
+    built in) and the eventTs range of its latest rows; the returned tuple keeps the arrays alive.  The local
+    offset is taken per 900-s bucket (and checked constant over each bucket)."""
+    import calendar
+    import datetime as _dt
+    np_, po, pb = _dictionary(provider_uniques)
+    nv, vo, vb = _dictionary(vehicle_uniques)
+    b0 = int(ts_min_us) // 1_000_000 // 900
+    b1 = int(ts_max_us) // 1_000_000 // 900
+    if b1 - b0 + 1 > MAX_TIME_BUCKETS:
+        raise RuntimeError(f"latest positions span {b1 - b0 + 1} 900-s buckets (at most {MAX_TIME_BUCKETS})")
+
+    def off(s):
+        return calendar.timegm(_dt.datetime.fromtimestamp(s).timetuple()) - s
+    bo = np.array([off(b * 900) for b in range(b0, b1 + 1)], np.int64)
+    if any(off(b * 900 + 899) != bo[b - b0] for b in range(b0, b1 + 1)):
+        raise RuntimeError("a local-time offset change inside a 900-s bucket")
+    cfg = HmPositionDocCfg(n_providers=np_, provider_offsets=ptr(po), provider_bytes=ptr(pb), n_vehicles=max(nv, 1),
+                           vehicle_offsets=ptr(vo), vehicle_bytes=ptr(vb), bucket0=b0, n_buckets=bo.size,
+                           bucket_offset_s=ptr(bo))
+    if nv == 0:   # (no valid row: an empty dictionary of one empty string keeps the offsets well formed)
+        vo2 = np.zeros(2, np.int64)
+        cfg.vehicle_offsets = ptr(vo2)
+        return cfg, (po, pb, vo, vb, bo, vo2)
+    return cfg, (po, pb, vo, vb, bo)
+
+
+def position_statements_selftest(provider_uniques, vehicle_uniques, vkey, ts_us, lat, lon):
+    """Host execution of the GPU positions encoder on rows (no GPU): (bytes uint8, offsets int64)."""
+    lib = load()
+    vkey = np.ascontiguousarray(vkey, dtype=np.uint64)
+    ts_us = np.ascontiguousarray(ts_us, dtype=np.int64)
+    lat = np.ascontiguousarray(lat, dtype=np.float64)
+    lon = np.ascontiguousarray(lon, dtype=np.float64)
+    n = vkey.size
+    cfg, keep = position_doc_cfg(provider_uniques, vehicle_uniques, ts_us.min() if n else 0, ts_us.max() if n else 0)
+    cap = 1024 * max(n, 1) + 8 * int(keep[1].size + keep[3].size)
+    buf = np.zeros(cap, np.uint8)
+    offs = np.zeros(n + 1, np.int64)
+    check(lib.hm_selftest_position_statements(ctypes.byref(cfg), ptr(vkey), ptr(ts_us), ptr(lat), ptr(lon), n, ptr(buf),
+                                              cap, ptr(offs)), None, "hm_selftest_position_statements")
     return buf[:offs[-1]].copy(), offs

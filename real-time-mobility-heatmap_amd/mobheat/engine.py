@@ -139,10 +139,10 @@ class HeatmapEngine:
         return info
 
     # ---- tiles as MongoDB update statements, BSON-encoded on the GPU (reference heatmap_stream.py:164-196) ----
-    def encode_tile_updates(self, city, ttl_minutes):
+    def encode_tile_updates(self, city, ttl_minutes, copy=False):
         """The last batch's tiles as the `update` statements pymongo would send for the reference's UpdateOne ops:
-        (bytes uint8, offsets int64[n+1]); statement i = bytes[offsets[i]:offsets[i+1]].  Valid until the next
-        call (copied out here)."""
+        (bytes uint8, offsets int64[n+1]); statement i = bytes[offsets[i]:offsets[i+1]].  Views of the library's
+        pinned buffers, valid until the next call on this engine (copy=True to keep them)."""
         n = ctypes.c_int64()
         check(self._lib.hm_last_windows(self._ctx, None, 0, ctypes.byref(n)), self._ctx, "hm_last_windows")
         wins = np.zeros(n.value, np.int64)
@@ -152,11 +152,18 @@ class HeatmapEngine:
         pb, po, nd = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
         check(self._lib.hm_encode_tile_updates(self._ctx, ctypes.byref(cfg), HM_MEM_HOST, ctypes.byref(pb),
                                                ctypes.byref(po), ctypes.byref(nd)), self._ctx, "hm_encode_tile_updates")
-        offs = np.ctypeslib.as_array(ctypes.cast(po, ctypes.POINTER(ctypes.c_int64)), shape=(nd.value + 1,)).copy()
-        total = int(offs[-1])
-        buf = (np.ctypeslib.as_array(ctypes.cast(pb, ctypes.POINTER(ctypes.c_uint8)), shape=(total,)).copy()
-               if total else np.zeros(0, np.uint8))
-        return buf, offs
+        return _host_statements(pb, po, nd, copy)
+
+    def encode_position_updates(self, provider_uniques, vehicle_uniques, ts_min_us, ts_max_us, copy=False):
+        """The last batch's latest rows as positions_latest update statements (reference heatmap_stream.py:211-235):
+        (bytes uint8, offsets int64[n+1]).  The dictionaries are the batch's factorization its vkeys were built
+        from (vkey = provider_code * n_vehicles + vehicle_code); [ts_min_us, ts_max_us] covers the rows' eventTs."""
+        cfg, keep = _lib.position_doc_cfg(provider_uniques, vehicle_uniques, ts_min_us, ts_max_us)
+        pb, po, nd = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+        check(self._lib.hm_encode_position_updates(self._ctx, ctypes.byref(cfg), HM_MEM_HOST, ctypes.byref(pb),
+                                                   ctypes.byref(po), ctypes.byref(nd)), self._ctx,
+              "hm_encode_position_updates")
+        return _host_statements(pb, po, nd, copy)
 
     def encode_tile_updates_device(self, city, ttl_minutes):
         """The same, left on the device: (device pointer of the bytes, of the offsets, n statements)."""
@@ -192,6 +199,16 @@ class HeatmapEngine:
                            n_in=int(out.n_in), n_valid=int(out.n_valid), n_late=int(out.n_late),
                            n_state=int(out.n_state), batch_max_event_ms=int(out.batch_max_event_ms),
                            watermark_ms=int(out.watermark_ms), late_watermark_ms=int(out.late_watermark_ms))
+
+
+def _host_statements(pb, po, nd, copy):
+    """(bytes, offsets) of statements in the library's pinned host buffers: views valid until the next call on the
+    engine unless copy=True (a 1e8-tile batch is ~37 GB: a copy costs seconds)."""
+    offs = np.ctypeslib.as_array(ctypes.cast(po, ctypes.POINTER(ctypes.c_int64)), shape=(nd.value + 1,))
+    total = int(offs[-1])
+    buf = (np.ctypeslib.as_array(ctypes.cast(pb, ctypes.POINTER(ctypes.c_uint8)), shape=(total,))
+           if total else np.zeros(0, np.uint8))
+    return (buf.copy(), offs.copy()) if copy else (buf, offs)
 
 
 def save_state_file(path, info, recs):

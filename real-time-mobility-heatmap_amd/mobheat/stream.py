@@ -193,7 +193,7 @@ def batch_columns(df):
     row_valid = (pc_codes >= 0) & (vc_codes >= 0) & ts_valid        # provider/vehicleId/eventTs non-null (:99-103)
     vkey = np.where(row_valid, pc_codes.astype(np.int64) * max(len(v_uni), 1) + vc_codes, 0).astype(np.uint64)
     return dict(n=n, lat=lat, lon=lon, ts_us=ts_us, speed=speed, speed_valid=speed_valid, vkey=vkey,
-                row_valid=row_valid, provider=prov, vehicleId=vid)
+                row_valid=row_valid, provider=prov, vehicleId=vid, provider_uniques=p_uni, vehicle_uniques=v_uni)
 
 
 # ------------------ document builders (reference :164-188 and :211-228) ------------------
@@ -268,11 +268,10 @@ def _flush(sink, collection, ops):
 def _flush_statements(sink, collection, buf, offs):
     """Pre-encoded update statements (hm_encode_tile_updates) in unordered batches of BULK_CHUNK (:191-196)."""
     from bson.raw_bson import RawBSONDocument
-    b = buf.tobytes()   # (pymongo encodes RawBSONDocument from bytes only)
-    o = offs.tolist()
+    o = offs.tolist()   # (pymongo encodes RawBSONDocument from bytes only: one copy per statement)
     for i in range(0, len(o) - 1, BULK_CHUNK):
         j = min(i + BULK_CHUNK, len(o) - 1)
-        sink.update_raw(collection, [RawBSONDocument(b[o[k]:o[k + 1]]) for k in range(i, j)])
+        sink.update_raw(collection, [RawBSONDocument(buf[o[k]:o[k + 1]].tobytes()) for k in range(i, j)])
 
 
 # ------------------ the drop-in boundary ------------------
@@ -286,8 +285,13 @@ def foreach_batch_func(df, epoch_id: int):
         # ---- 1) Upsert tiles (TTL via staleAt): the UpdateOne statements, BSON-encoded on the GPU ----
         buf, offs = get_engine().encode_tile_updates(CITY, TTL_MIN)
         _flush_statements(sink, "tiles", buf, offs)
-        # ---- 2) latest per (provider, vehicleId) within this micro-batch ----
-        _flush(sink, "positions_latest", position_ops(cols, res.latest_rows))
+        # ---- 2) latest per (provider, vehicleId) within this micro-batch: statements encoded on the GPU ----
+        rows = res.latest_rows
+        if rows.size:
+            t = cols["ts_us"][rows]
+            buf, offs = get_engine().encode_position_updates(cols["provider_uniques"], cols["vehicle_uniques"],
+                                                             int(t.min()), int(t.max()))
+            _flush_statements(sink, "positions_latest", buf, offs)
     finally:
         sink.close()
     if STATE_CHECKPOINT:   # after the writes succeeded: the batch is committed

@@ -97,3 +97,32 @@ def test_empty_batch_and_errors():
     with pytest.raises(RuntimeError, match="city"):
         eng.encode_tile_updates("x" * 65, 45)
     eng.close()
+
+
+def test_position_statements_match_pymongo():
+    """The positions half: a C5-like batch (vehicles with several updates and ties) through foreach's columns;
+    the GPU statements equal pymongo's bytes for the reference's positions_latest UpdateOne ops."""
+    import bson
+    import pandas as pd
+    from mobheat import HeatmapEngine, stream
+    rng = np.random.default_rng(43)
+    n = 200_000
+    ts = 1759572000_000_000 + rng.integers(0, 60, n) * 1_000_000 + rng.integers(0, 3, n) * 1000
+    df = pd.DataFrame({"provider": rng.choice(["mbta", "opensky"], n),
+                       "vehicleId": [f"V{int(x)}" for x in rng.integers(0, 20000, n)],
+                       "lat": rng.uniform(42.2, 42.45, n), "lon": rng.uniform(-71.2, -70.95, n),
+                       "speedKmh": rng.uniform(0, 80, n), "eventTs": pd.to_datetime(ts, unit="us")})
+    cols = stream.batch_columns(df)
+    eng = HeatmapEngine(h3_res=8)
+    res = eng.process_batch(0, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"], cols["speed_valid"],
+                            cols["vkey"], cols["row_valid"])
+    rows = res.latest_rows
+    assert rows.size > 20000   # ties: several rows for some vehicles
+    t = cols["ts_us"][rows]
+    buf, offs = eng.encode_position_updates(cols["provider_uniques"], cols["vehicle_uniques"], int(t.min()), int(t.max()))
+    exp = [bson.encode({"q": op._filter, "u": op._doc, "multi": False, "upsert": True})
+           for op in stream.position_ops(cols, rows)]
+    assert _split(buf, offs) == exp
+    with pytest.raises(RuntimeError, match="dictionaries"):
+        eng.encode_position_updates(cols["provider_uniques"][:1], cols["vehicle_uniques"], int(t.min()), int(t.max()))
+    eng.close()

@@ -244,3 +244,42 @@ def test_statement_batches_and_update_command(monkeypatch):
     DB.reply = {"ok": 1, "n": 1, "writeErrors": [{"index": 0, "code": 11000, "errmsg": "dup"}]}
     with pytest.raises(BulkWriteError):
         sink.update_raw("tiles", [RawBSONDocument(exp[0])])
+
+
+@pytest.mark.parametrize("tz", ["UTC", "EET-2EEST,M3.5.0/3,M10.5.0/4"])
+def test_gpu_position_encoder_matches_pymongo(tz):
+    """CPU: the positions statement encoder (host execution of the GPU code) writes the bytes pymongo encodes for
+    the reference's positions_latest UpdateOne (heatmap_stream.py:211-228): string dictionaries from the batch's
+    factorization (non-ASCII ids, two providers), naive local eventTs with microseconds across a DST change."""
+    import time
+    from mobheat import _lib
+    old = os.environ.get("TZ")
+    os.environ["TZ"] = tz
+    time.tzset()
+    try:
+        rng = np.random.default_rng(9)
+        n = 3000
+        t0 = 1761440100 * 1_000_000 - 3 * 3600 * 1_000_000
+        df = pd.DataFrame({"provider": rng.choice(["mbta", "opensky-ψ"], n),
+                           "vehicleId": [f"v{int(x)}-ώ" if x % 7 == 0 else f"BUS_{int(x)}" for x in rng.integers(0, 800, n)],
+                           "lat": rng.uniform(-90, 90, n), "lon": rng.uniform(-180, 180, n),
+                           "speedKmh": rng.uniform(0, 90, n),
+                           "eventTs": pd.to_datetime(t0 + rng.integers(0, 6 * 3600 * 1_000_000, n), unit="us")})
+        df.loc[5, "lat"] = -0.0
+        cols = stream.batch_columns(df)
+        rows = np.sort(rng.choice(n, 500, replace=False))
+        buf, offs = _lib.position_statements_selftest(cols["provider_uniques"], cols["vehicle_uniques"],
+                                                      cols["vkey"][rows], cols["ts_us"][rows], cols["lat"][rows],
+                                                      cols["lon"][rows])
+        exp = [bson.encode({"q": op._filter, "u": op._doc, "multi": False, "upsert": True})
+               for op in stream.position_ops(cols, rows)]
+        assert offs.size == len(exp) + 1
+        for i, e in enumerate(exp):
+            got = buf[offs[i]:offs[i + 1]].tobytes()
+            assert got == e, (i, bson.decode(got), bson.decode(e))
+    finally:
+        if old is None:
+            del os.environ["TZ"]
+        else:
+            os.environ["TZ"] = old
+        time.tzset()
