@@ -8,7 +8,7 @@ OpenSky-like global batch of 1e8 events uniform on the sphere, 50k vehicle ids, 
 one fused pass over the events (k_ingest: filter + latLngToCell + window + late test + LDS pre-aggregation +
 per-vehicle max ts + census of the partials per window, which sizes the per-window state tables), radix partition
 into (window, region) bins, the region-owned merge into the persistent update-mode state that also writes the
-update-mode rows (k_merge_owned), row compaction (k_rows_compact), eviction (whole window tables released), and
+update-mode rows (k_merge_owned), in-place densification of the rows (k_fill_gaps), eviction (whole window tables released), and
 the latest-position flags + compaction.
 Every step is a NEW micro-batch: its timestamps are the previous step's + 15 min (precomputed before the
 timed region), so the stream advances, windows close and are evicted, and no row is late.
@@ -43,14 +43,14 @@ BYTES = {
     "partition": 160,  # per partial: histogram read 48 B + scatter read 48 B + scatter write of the 64-B SortedRec
     "merge": 177,      # per partial: read the 64-B SortedRec, write the 64 B state line (a new key: its slot tag
                        # is in LDS, nothing read) and the 49 B update-mode row
-    "emit": 98,        # per emitted tile: 49 B row read from the bin's segment, 49 B written densely
+    "emit": 98,        # per gap filled: a 49-B row read from above the dense size and written into the gap
     "dedup": 20,       # per event: vkey 8 + ts 8 + flags 1 read, win flag 1 written, 2 x 1 B compaction reads
 }
 # HBM traffic per dispatch of every kernel and k_ingest's VALU instruction mix per event of this workload were
 # counted by rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r1/kernel_pmc.json).
 PMC_FILE = os.path.join(ROOT, "profiles", "r1", "kernel_pmc.json")
 STAGE_KERNELS = {"ingest": ["k_ingest"], "partition": ["k_rp_hist", "k_rp_scatter"], "merge": ["k_merge_owned"],
-                 "emit": ["k_rows_compact"], "dedup": ["k_dedup_flag"]}
+                 "emit": ["k_fill_gaps"], "dedup": ["k_dedup_flag"]}
 
 
 def ingest_pmc(res):
@@ -168,7 +168,7 @@ def main():
     avg_ms = {k: v / K for k, v in kt.items()}
     n_tiles = int(last.n_tiles) if last is not None else 0
     n_parts = int(last.n_partials) if last is not None else 0
-    units = {"ingest": n, "dedup": n, "partition": n_parts, "merge": n_parts, "emit": n_tiles}
+    units = {"ingest": n, "dedup": n, "partition": n_parts, "merge": n_parts, "emit": max(n_parts - n_tiles, 0)}
     launch_bytes = {k: BYTES[k] * units[k] for k in BYTES}
     launch_bytes["ingest"] += 48 * n_parts
     dom = max(BYTES, key=lambda k: avg_ms[k])

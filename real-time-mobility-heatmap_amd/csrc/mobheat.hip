@@ -13,7 +13,7 @@
 //   k_merge_owned one workgroup per bin merges its partials into the persistent per-window state tables
 //                 (update mode, :243; Spark's StateStoreRestore/Save) with the regions' slot tags in LDS, and
 //                 writes each touched key's cumulative output row (:124-132) into the bin's row segment
-//   k_rows_compact  the per-bin row segments -> dense update-mode rows
+//   k_fill_gaps     the per-bin row segments -> dense update-mode rows (in place: gap rows filled from the tail)
 //   eviction      (watermark, :107) releases a window's whole table; k_dump_gen + a rehash merge grow one
 //   k_dedup_flag  latest position per (provider, vehicleId): rows whose ts equals the max (:204-207)
 //
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict_
 // The update-mode output row of a key (cumulative count/avg, heatmap_stream.py:124-132,243) is written at its
 // first touch in the batch to row b0 + k of the bin's segment (b0 = the bin's first partial, k = touch order
 // in the bin; the slot's `touched` word keeps (batch seq, k)), and rewritten in place when a later chunk
-// updates the key again; k_rows_compact closes the gaps left by keys that had several partials.
+// updates the key again; k_fill_gaps closes the gaps left by keys that had several partials.
 // rehash != 0: growth (k_dump_gen records, unique keys, into the window's new table): created slots keep the
 // record's touched word, no rows are written.
 // =====================================================================================================
@@ -974,21 +974,47 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
 // =====================================================================================================
 // K4: close the gaps between the bins' row segments: bin b's rows [O(b), O(b) + cnt[b]) -> [off[b], ...)
 // =====================================================================================================
-__global__ __launch_bounds__(256) void k_rows_compact(RowsOut src, RowsOut dst, const unsigned long long *__restrict__ O,
-                                                      int64_t ntiles, int nbins, const unsigned *__restrict__ cnt,
-                                                      const unsigned long long *__restrict__ off) {
-    for (int bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
-        const int64_t s0 = (int64_t)O[(int64_t)bin * ntiles];
-        const int64_t d0 = (int64_t)off[bin];
-        const unsigned c = cnt[bin];
-        for (unsigned k = threadIdx.x; k < c; k += blockDim.x) {
-            dst.cell[d0 + k] = src.cell[s0 + k];
-            dst.ws[d0 + k] = src.ws[s0 + k];
-            dst.cnt[d0 + k] = src.cnt[s0 + k];
-            dst.sp[d0 + k] = src.sp[s0 + k];
-            dst.spnull[d0 + k] = src.spnull[s0 + k];
-            dst.lon[d0 + k] = src.lon[s0 + k];
-            dst.lat[d0 + k] = src.lat[s0 + k];
+// In-place densification of the per-bin row segments: bin b's merged rows are [s_b, s_b + c_b) of the staging
+// arrays (s_b = the bin's first partial, c_b its touched keys), so the rows [0, T) (T = sum c_b) are dense except
+// for the gaps left by keys with several partials; each gap below T takes one row from above T (gap i <- the i-th
+// row at or above T, both counted in bin order).  Moves only the ~2% gap rows instead of every row.
+__global__ __launch_bounds__(256) void k_gap_counts(const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
+                                                    const unsigned *__restrict__ cnt, const unsigned long long *__restrict__ T_ptr,
+                                                    unsigned *__restrict__ g, unsigned *__restrict__ v) {
+    const unsigned long long T = *T_ptr;
+    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nbins; b += gridDim.x * blockDim.x) {
+        const unsigned long long s = O[(int64_t)b * ntiles], e = O[(int64_t)(b + 1) * ntiles], c = cnt[b];
+        const unsigned long long glo = s + c, ghi = e < T ? e : T;
+        g[b] = ghi > glo ? (unsigned)(ghi - glo) : 0u;
+        const unsigned long long vlo = s > T ? s : T, vhi = s + c;
+        v[b] = vhi > vlo ? (unsigned)(vhi - vlo) : 0u;
+    }
+}
+__global__ __launch_bounds__(256) void k_fill_gaps(RowsOut r, const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
+                                                   const unsigned *__restrict__ cnt, const unsigned long long *__restrict__ T_ptr,
+                                                   const unsigned *__restrict__ g, const unsigned long long *__restrict__ goff,
+                                                   const unsigned long long *__restrict__ voff) {
+    const unsigned long long T = *T_ptr;
+    for (int b = blockIdx.x; b < nbins; b += gridDim.x) {
+        const unsigned ng = g[b];
+        if (!ng) continue;
+        const unsigned long long dst0 = O[(int64_t)b * ntiles] + cnt[b], g0 = goff[b];
+        for (unsigned k = threadIdx.x; k < ng; k += blockDim.x) {
+            const unsigned long long i = g0 + k;
+            int lo = 0, hi = nbins;   // last bin with voff <= i
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (voff[mid] <= i) lo = mid; else hi = mid;
+            }
+            const unsigned long long sb = O[(int64_t)lo * ntiles];
+            const int64_t src = (int64_t)((sb > T ? sb : T) + (i - voff[lo])), dst = (int64_t)(dst0 + k);
+            r.cell[dst] = r.cell[src];
+            r.ws[dst] = r.ws[src];
+            r.cnt[dst] = r.cnt[src];
+            r.sp[dst] = r.sp[src];
+            r.spnull[dst] = r.spnull[src];
+            r.lon[dst] = r.lon[src];
+            r.lat[dst] = r.lat[src];
         }
     }
 }
@@ -1613,6 +1639,7 @@ struct hm_ctx {
     DevBuf s_cell, s_ws, s_cnt, s_sp, s_spn, s_lon, s_lat;   // k_merge_owned's rows in per-bin segments (with gaps)
     DevBuf bin_cnt, bin_off;          // k_merge_owned: touched keys per bin, their output offsets
     DevBuf parts_regrow;              // growth: the old tables' keys as partial records
+    DevBuf gapbuf;                    // k_gap_counts / k_fill_gaps: per-bin gap and donor counts + donor offsets
     unsigned long long seq = 0;
     // dedup table (persistent, cleared through its used list)
     // latest-position tables (16-B slots, cleared through their used lists): `fused` is k_ingest's, sized from the
@@ -1671,6 +1698,7 @@ constexpr int FULL_USED_WORD = 240;   // used-slot count of the full dedup table
 constexpr int SLOW_WORD = 252;   // number of k_ingest fast-path exceptions of the current batch
 constexpr int REGROW_WORD = 251; // records dumped by k_dump_gen
 constexpr int GIVEUP_WORD = 232;
+constexpr int GAPS_WORD = 242;   // 242-243: totals of the gap / donor scans
 constexpr int POSBAD_WORD = 241; // position statements: rows outside the caller's dictionaries
 // (GIVEUP_WORD: k_ingest's fused dedup gave up, a cache line of its own: words 232-239)
 
@@ -2170,11 +2198,26 @@ static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_par
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
     hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->bin_cnt.p, (int64_t)RP_BINS,
                        (unsigned long long *)ctx->bin_off.p, &ctx->d_st->n_touched);
-    hipLaunchKernelGGL(k_rows_compact, dim3(RP_BINS), dim3(256), 0, ctx->stream, staged_rows(ctx),
-                       rows_of(ctx->o_cell, ctx->o_ws, ctx->o_cnt, ctx->o_sp, ctx->o_spn, ctx->o_lon, ctx->o_lat),
-                       (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, (const unsigned *)ctx->bin_cnt.p,
-                       (const unsigned long long *)ctx->bin_off.p);
+    // densify the staged segments in place (k_gap_counts / k_fill_gaps); they become the outputs (buffer swap)
+    if ((rc = ensure(ctx, ctx->gapbuf, (size_t)RP_BINS * 24))) return rc;
+    unsigned *gg = (unsigned *)ctx->gapbuf.p, *gv = gg + RP_BINS;
+    unsigned long long *gvo = (unsigned long long *)(gv + RP_BINS), *ggo = (unsigned long long *)ctx->bin_off.p;
+    const unsigned long long *O = (const unsigned long long *)ctx->rp_O.p;
+    hipLaunchKernelGGL(k_gap_counts, dim3(grid_for(RP_BINS, 256)), dim3(256), 0, ctx->stream, O, ntiles, RP_BINS,
+                       (const unsigned *)ctx->bin_cnt.p, &ctx->d_st->n_touched, gg, gv);
+    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, gg, (int64_t)RP_BINS, ggo, ctx->d_scratch + GAPS_WORD);
+    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, gv, (int64_t)RP_BINS, gvo, ctx->d_scratch + GAPS_WORD + 1);
+    hipLaunchKernelGGL(k_fill_gaps, dim3(RP_BINS), dim3(256), 0, ctx->stream, staged_rows(ctx), O, ntiles, RP_BINS,
+                       (const unsigned *)ctx->bin_cnt.p, &ctx->d_st->n_touched, (const unsigned *)gg,
+                       (const unsigned long long *)ggo, (const unsigned long long *)gvo);
     HIPCHK(ctx, hipGetLastError());
+    std::swap(ctx->s_cell, ctx->o_cell);
+    std::swap(ctx->s_ws, ctx->o_ws);
+    std::swap(ctx->s_cnt, ctx->o_cnt);
+    std::swap(ctx->s_sp, ctx->o_sp);
+    std::swap(ctx->s_spn, ctx->o_spn);
+    std::swap(ctx->s_lon, ctx->o_lon);
+    std::swap(ctx->s_lat, ctx->o_lat);
     HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
     return HM_OK;
 }
@@ -2375,7 +2418,7 @@ void hm_destroy(hm_ctx *ctx) {
                       &ctx->rp_btot, &ctx->rp_boff,
                       &ctx->s_cell, &ctx->s_ws, &ctx->s_cnt, &ctx->s_sp, &ctx->s_spn, &ctx->s_lon, &ctx->s_lat, &ctx->bin_cnt, &ctx->bin_off, &ctx->dfused.used, &ctx->dfull.used, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
                       &ctx->o_lon, &ctx->o_lat, &ctx->td_sizes, &ctx->td_off, &ctx->td_btot, &ctx->td_boff, &ctx->td_bytes,
-                      &ctx->td_params};
+                      &ctx->td_params, &ctx->gapbuf};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &g : ctx->gens) (void)hipFree(g.tab);
