@@ -12,7 +12,8 @@ constexpr int64_t EMPTY_WIN = INT64_MIN;                  // window starts are >
 constexpr uint64_t EMPTY_VKEY = ~UINT64_C(0);             // reserved by the ABI
 constexpr int WAVE = 64;
 
-enum : uint8_t { F_VALID = 1, F_AGG = 2, F_LATE = 4 };
+// F_CAND: the row's ts was >= its vkey's max when k_ingest's fused dedup saw it (every final winner is one)
+enum : uint8_t { F_VALID = 1, F_AGG = 2, F_LATE = 4, F_CAND = 8 };
 
 // one persistent tile-state slot = one 64-B line. An all-zero slot is empty (tables are cleared with a
 // memset): the window word holds wenc = windowStart ^ 2^63, and windowStart = INT64_MIN is never valid.

@@ -1128,7 +1128,7 @@ constexpr int DF_U = 4;
 __global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__ vkey, const int64_t *__restrict__ ts,
                                                     const uint8_t *__restrict__ flags, const Cand *__restrict__ cands, int64_t n,
                                                     const DedupSlot *__restrict__ tab, unsigned long long mask,
-                                                    uint8_t *__restrict__ win) {
+                                                    uint8_t *__restrict__ win, bool only_cand) {
     const int64_t step = (int64_t)blockDim.x * DF_U;
     for (int64_t base = (int64_t)blockIdx.x * step; base < n; base += (int64_t)gridDim.x * step) {
         unsigned long long v[DF_U], h[DF_U];
@@ -1139,9 +1139,12 @@ __global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__
             take[u] = false;
             v[u] = 0;
             t[u] = 0;
-            if (i < n) {   // (the row's loads do not wait for its flag: one dependent latency less)
+            if (i < n) {
                 if (cands) { take[u] = true; v[u] = cands[i].vkey; t[u] = cands[i].ts; }
-                else { v[u] = vkey[i]; t[u] = ts[i]; take[u] = (flags[i] & F_VALID) != 0; }
+                else if (only_cand) {   // k_ingest's max saw every row: only its candidates can be at the max
+                    take[u] = (flags[i] & F_CAND) != 0;
+                    if (take[u]) { v[u] = vkey[i]; t[u] = ts[i]; }
+                } else { v[u] = vkey[i]; t[u] = ts[i]; take[u] = (flags[i] & F_VALID) != 0; }   // (loads not waiting for the flag)
             }
             take[u] = take[u] && v[u] != EMPTY_VKEY;
             h[u] = vkey_hash(v[u]) & mask;
@@ -1270,11 +1273,11 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
                 const unsigned long long pos = wave_append(exc, n_slow);
                 if (exc) slow[pos] = (unsigned int)i;
             }
-            if (in) flags_out[i] = fl;
             // dedup: per-vkey max ts over the valid rows (late rows included, as in the reference's batch frame)
             bool claimed = false;
             long long dh = -1;
             bad += ok && v == EMPTY_VKEY;
+            bool cand = false;
             if (dd) {
                 long long cur = d0.maxts;
                 if (d0.vkey == v) dh = (long long)dh0;   // the usual case: the key sits in its home slot
@@ -1282,10 +1285,13 @@ __global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
                 if (dh < 0) {
                     if (!dretry) atomicExch(dgiveup, 1ull);
                     dretry = true;
-                } else if (t > cur) {
-                    atomicMax(&dtab[dh].maxts, (long long)t);
+                } else {
+                    // (cur may be stale, i.e. below the slot's max: a superset of the rows at the final max)
+                    cand = t >= cur || claimed;
+                    if (t > cur) atomicMax(&dtab[dh].maxts, (long long)t);
                 }
             }
+            if (in) flags_out[i] = fl | (cand ? F_CAND : 0);
             const unsigned long long pos = wave_append(claimed, n_dused);
             if (claimed) dused[pos] = (unsigned int)dh;
             bool fresh = false;
@@ -2148,7 +2154,7 @@ static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t 
         }
         hipLaunchKernelGGL(k_dedup_flag, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, I ? I->vk : nullptr,
                            I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, d.tab, d.cap - 1,
-                           (uint8_t *)ctx->win.p);
+                           (uint8_t *)ctx->win.p, !need_max);
         HIPCHK(ctx, hipGetLastError());
         if ((rc = compact_flags(ctx, (const uint8_t *)ctx->win.p, n, (int64_t *)ctx->rows.p))) return rc;
     } else {
@@ -2393,6 +2399,9 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
             ensure(ctx, ctx->s_sp, n * 8) || ensure(ctx, ctx->s_spn, n) || ensure(ctx, ctx->s_lon, n * 8) ||
             ensure(ctx, ctx->s_lat, n * 8) || ensure_outputs(ctx, n))
             return fail("create");
+        // the full dedup table a batch of n rows may need (when k_ingest's cache-sized table gives up: C5's first
+        // batch paid a 17-GB hipMalloc inside the batch)
+        if (dedup_prepare(ctx, ctx->dfull, n, false)) return fail("create");
     }
     // state_capacity_hint: one window table for that many keys, reserved now into the pool (a 70-GB table costs
     // ~2 s in hipMalloc: C5's first batch)
