@@ -82,7 +82,11 @@ class HeatmapEngine:
             pass
 
     # ---- host-memory batch (the foreach_batch_func path) ----
-    def process_batch(self, epoch_id, lat, lon, ts_us, speed=None, speed_valid=None, vkey=None, row_valid=None):
+    def process_batch(self, epoch_id, lat, lon, ts_us, speed=None, speed_valid=None, vkey=None, row_valid=None,
+                      copy=True):
+        """One micro-batch from host columns (the foreach_batch_func path).  copy=False returns views of the
+        library's pinned output buffers, valid until the next call on this engine (a 1e8-tile batch's outputs are
+        ~5 GB: copying them costs about as much as the whole GPU pipeline and both PCIe transfers)."""
         n = int(np.asarray(lat).size)
         lat = np.ascontiguousarray(lat, dtype=np.float64)
         lon = np.ascontiguousarray(lon, dtype=np.float64)
@@ -95,7 +99,7 @@ class HeatmapEngine:
         out = HmBatchOut()
         check(self._lib.hm_process_batch(self._ctx, int(epoch_id), ctypes.byref(b), HM_MEM_HOST, ctypes.byref(out)),
               self._ctx, "hm_process_batch")
-        return self._result_from_host(out)
+        return self._result_from_host(out, copy)
 
     # ---- device-resident batch (bench / multi-GPU): raw device pointers, results stay on the device ----
     def process_batch_device(self, epoch_id, n, lat, lon, ts_us, speed, speed_valid, vkey, row_valid):
@@ -183,17 +187,17 @@ class HeatmapEngine:
         check(self._lib.hm_last_timings(self._ctx, ms, 7), self._ctx)
         return {"ingest": ms[0], "merge": ms[2], "emit": ms[3], "dedup": ms[4], "total": ms[5], "partition": ms[6]}
 
-    def _result_from_host(self, out):
+    def _result_from_host(self, out, copy=True):
         def arr(p, n, dt):
             if n == 0 or not p:
                 return np.zeros(0, dt)
-            return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))),
-                                         shape=(n,)).copy()
+            a = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(n,))
+            return a.copy() if copy else a
         nt = int(out.n_tiles)
         ws = arr(out.window_start_us, nt, np.int64)
         tiles = TileRows(cell=arr(out.cell, nt, np.uint64), window_start_us=ws, window_end_us=ws + self.tile_us,
                          count=arr(out.count, nt, np.int64), avg_speed=arr(out.avg_speed, nt, np.float64),
-                         speed_null=arr(out.speed_null, nt, np.uint8).astype(bool),
+                         speed_null=arr(out.speed_null, nt, np.uint8).view(np.bool_),
                          avg_lon=arr(out.avg_lon, nt, np.float64), avg_lat=arr(out.avg_lat, nt, np.float64))
         return BatchResult(tiles=tiles, latest_rows=arr(out.latest_row, int(out.n_latest), np.int64),
                            n_in=int(out.n_in), n_valid=int(out.n_valid), n_late=int(out.n_late),

@@ -279,7 +279,7 @@ def foreach_batch_func(df, epoch_id: int):
     """Runs on each micro-batch (reference heatmap_stream.py:150): tiles + latest positions -> MongoDB."""
     cols = batch_columns(df)
     res = get_engine(epoch_id).process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"],
-                                     cols["speed_valid"], cols["vkey"], cols["row_valid"])
+                                     cols["speed_valid"], cols["vkey"], cols["row_valid"], copy=False)
     sink = SINK_FACTORY()
     try:
         # ---- 1) Upsert tiles (TTL via staleAt): the UpdateOne statements, BSON-encoded on the GPU ----
