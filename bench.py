@@ -53,12 +53,13 @@ STAGE_KERNELS = {"ingest": ["k_ingest"], "partition": ["k_rp_hist", "k_rp_scatte
                  "emit": ["k_fill_gaps"], "dedup": ["k_dedup_flag"]}
 
 
-def ingest_pmc(res):
+def ingest_pmc(res, n, world):
+    """The PMC file's counts, only when they were taken on this exact workload (one GPU, same res and batch)."""
     try:
         d = json.load(open(PMC_FILE))
     except (OSError, ValueError):
         return None
-    return d if d.get("h3_res") == res else None
+    return d if d.get("h3_res") == res and d.get("events_per_dispatch") == n and world == 1 else None
 
 
 def gen_batch(n, steps, seed, dev):
@@ -178,7 +179,7 @@ def main():
     # side: k_ingest is VALU/latency bound, so the HBM fraction alone understates how busy it is.
     roof = {"bound": "hbm", "kernel": dom, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": gbs / HBM_PEAK_GBS, "traffic": None}
-    pmc = ingest_pmc(args.res)
+    pmc = ingest_pmc(args.res, n, world)
     if pmc is not None and all(k in pmc.get("kernels", {}) for k in STAGE_KERNELS[dom]):
         # FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, per dispatch, summed over the stage's kernels
         roof["traffic"] = sum(pmc["kernels"][k]["hbm_bytes"] for k in STAGE_KERNELS[dom])
