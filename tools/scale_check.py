@@ -11,7 +11,13 @@ checked through size-independent properties (the oracle cannot run these sizes):
       (two rows at the vehicle's max), randomly permuted.  Checks: exactly one latest row per vehicle, two for
       the tie subset, every latest row carries its vehicle's max timestamp.
 
-usage: python tools/scale_check.py [--config c4|c5|all] [--scale 1.0]   (prints one JSON line per config)
+  C3  one GPU's shard of configs[2]: 1.25e8 of the 1e9 city-scale events (Zipf(1.1) over 2,000 hot spots with
+      200 m Gaussian jitter in a 50x50 km box, res 9, 10 min per batch), four batches advancing 10 min: the
+      heavily repeated keys exercise k_ingest's LDS pre-aggregation.  Checks: counts sum to the valid rows, no
+      key emitted twice, tiles per batch << events; eight batches, the steady-state rate is the median of the
+      last four (the first ones allocate window tables sized by their partial counts until the pool holds them).
+
+usage: python tools/scale_check.py [--config c3|c4|c5|all] [--scale 1.0]   (prints one JSON line per config)
 """
 import argparse
 import json
@@ -105,6 +111,56 @@ def run_c4(dev, scale):
     return report
 
 
+def run_c3(dev, scale):
+    import mobheat
+    g = torch.Generator(device=dev)
+    g.manual_seed(2)
+    n = int(125_000_000 * scale)
+    dlat = 50.0 / 2 / 111.32
+    dlon = 50.0 / 2 / (111.32 * np.cos(np.radians(ATHENS[0])))
+    hs = 2000
+    hs_lat = ATHENS[0] + (torch.rand(hs, generator=g, device=dev, dtype=torch.float64) * 2 - 1) * dlat
+    hs_lon = ATHENS[1] + (torch.rand(hs, generator=g, device=dev, dtype=torch.float64) * 2 - 1) * dlon
+    w = 1.0 / torch.arange(1, hs + 1, device=dev, dtype=torch.float64) ** 1.1
+    h = torch.multinomial(w / w.sum(), n, replacement=True, generator=g)
+    sig_lat = 200.0 / 111_320.0
+    sig_lon = 200.0 / (111_320.0 * np.cos(np.radians(ATHENS[0])))
+    lat = hs_lat[h] + torch.randn(n, generator=g, device=dev, dtype=torch.float64) * sig_lat
+    lon = hs_lon[h] + torch.randn(n, generator=g, device=dev, dtype=torch.float64) * sig_lon
+    del h
+    ts0 = torch.randint(0, 10 * MIN_US, (n,), generator=g, device=dev, dtype=torch.int64)
+    d = dict(lat=lat, lon=lon, ts=ts0.clone(), speed=torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 80,
+             sv=(torch.rand(n, generator=g, device=dev) >= 0.15).to(torch.uint8),
+             vkey=torch.randint(0, 200_000, (n,), generator=g, device=dev, dtype=torch.int64),
+             rv=torch.ones(n, dtype=torch.uint8, device=dev))
+    eng = mobheat.HeatmapEngine(h3_res=9, device=dev.index or 0, batch_capacity_hint=n)
+    report = {"config": "C3 (one GPU's shard)", "events_per_batch": n, "h3_res": 9, "batches": []}
+    rates = []
+    for b in range(8):
+        d["ts"].copy_(ts0 + T0 + b * 10 * MIN_US)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        out = eng.process_batch_device(b, **ptrs(d, n))
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        nt = int(out.n_tiles)
+        cell = dev_array(out.cell, nt, torch.int64, dev)
+        ws = dev_array(out.window_start_us, nt, torch.int64, dev)
+        cnt = dev_array(out.count, nt, torch.int64, dev)
+        assert no_duplicate_keys(cell, ws), f"batch {b}: a key emitted twice"
+        assert int(cnt.sum()) == int(out.n_valid) - int(out.n_late) == n, "counts do not add up to the rows"
+        assert nt < n // 20, "C3 keys should repeat heavily"
+        tm = eng.last_timings()
+        report["batches"].append({"ms": round(dt * 1e3, 1), "events_per_s": n / dt, "tiles": nt,
+                                  "partials": int(out.n_partials), "kernel_ms": {k: round(v, 2) for k, v in tm.items()}})
+        if b >= 4:
+            rates.append(n / dt)
+    report["steady_events_per_s"] = float(np.median(rates))
+    report["ok"] = True
+    eng.close()
+    return report
+
+
 def run_c5(dev, scale):
     import mobheat
     g = torch.Generator(device=dev)
@@ -150,13 +206,13 @@ def run_c5(dev, scale):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="all", choices=["c4", "c5", "all"])
+    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "all"])
     ap.add_argument("--scale", type=float, default=1.0)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    for c in (["c4", "c5"] if a.config == "all" else [a.config]):
-        r = run_c4(dev, a.scale) if c == "c4" else run_c5(dev, a.scale)
+    for c in (["c3", "c4", "c5"] if a.config == "all" else [a.config]):
+        r = {"c3": run_c3, "c4": run_c4, "c5": run_c5}[c](dev, a.scale)
         print(json.dumps(r), flush=True)
         torch.cuda.empty_cache()
 
