@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 6
+#define HM_ABI_VERSION 7
 
 /* error codes */
 #define HM_OK 0
@@ -60,6 +60,8 @@ typedef struct hm_config {
     int64_t state_capacity_hint;    /* expected keys of the largest window: its table is reserved at create
                                        (0 = allocate on demand) */
     int64_t batch_capacity_hint;    /* expected max events per batch (0 = grow on demand) */
+    int64_t state_arena_bytes;      /* device memory reserved (and zeroed) at create for the window tables; tables
+                                       are carved from it before any allocation in a batch (0 = none) */
 } hm_config;
 
 /* One micro-batch of raw events, structure of arrays. All arrays have n entries.

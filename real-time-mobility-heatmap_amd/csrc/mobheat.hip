@@ -1642,6 +1642,10 @@ struct hm_ctx {
     struct Gen { unsigned long long wenc; TileSlot *tab; int log2cap; unsigned rbits; int64_t keys; int64_t batch_parts; };
     std::vector<Gen> gens;
     std::vector<std::pair<TileSlot *, int>> pool;   // (table, log2 slots)
+    // state_arena_bytes: window tables carved from one zeroed reservation made at create (no driver allocation
+    // inside a batch); carved tables are pooled like the others but never freed before the arena
+    uint8_t *arena = nullptr;
+    size_t arena_bytes = 0, arena_used = 0;
     GenDesc *d_gmap = nullptr, *h_gmap = nullptr;   // device map window -> table (host mirror)
     GenDesc *d_glist = nullptr, *h_glist = nullptr; // the same descriptors as a dense list (kernels' LDS cache)
     int n_glist = 0;
@@ -1792,6 +1796,10 @@ static void gen_geometry(const hm_ctx *ctx, int64_t keys, int64_t parts, int min
     log2cap = L;
 }
 
+static bool in_arena(const hm_ctx *ctx, const void *p) {
+    return ctx->arena && (const uint8_t *)p >= ctx->arena && (const uint8_t *)p < ctx->arena + ctx->arena_bytes;
+}
+
 // A table of >= 2^log2cap slots: the smallest pooled table of 2^log2cap or 2^(log2cap+1) slots (not cleared: see
 // kernels.h; a window whose key count sits near a power of two must not miss the pool and pay a multi-GB hipMalloc
 // every batch), else a new one zeroed once.  log2cap and rbits return the table's actual geometry.
@@ -1815,11 +1823,18 @@ static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **
     }
     const size_t bytes = (size_t(1) << log2cap) * (sizeof(TileSlot) + 1);   // slots, then one tag byte per slot
     TileSlot *t = nullptr;
+    if (ctx->arena && ctx->arena_used + bytes <= ctx->arena_bytes) {   // zeroed at create, never handed out before
+        *out = (TileSlot *)(ctx->arena + ctx->arena_used);
+        ctx->arena_used += (bytes + 255) & ~(size_t)255;
+        return HM_OK;
+    }
     if (dev_malloc((void **)&t, bytes, "state table") != hipSuccess) {
         (void)hipGetLastError();
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        for (auto &pt : ctx->pool) (void)hipFree(pt.first);
-        ctx->pool.clear();
+        std::vector<std::pair<TileSlot *, int>> keep;
+        for (auto &pt : ctx->pool)
+            if (in_arena(ctx, pt.first)) keep.push_back(pt); else (void)hipFree(pt.first);
+        ctx->pool.swap(keep);
         if (hipMalloc(&t, bytes) != hipSuccess) {
             (void)hipGetLastError();
             return set_err(ctx, HM_E_NOMEM, "state table of 2^%d slots: out of device memory", log2cap);
@@ -1832,9 +1847,13 @@ static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **
 // (the stream must have drained every kernel that reads the table)
 static void table_release(hm_ctx *ctx, TileSlot *t, int log2cap) {
     ctx->pool.emplace_back(t, log2cap);
-    while (ctx->pool.size() > 8) {
-        (void)hipFree(ctx->pool.front().first);
-        ctx->pool.erase(ctx->pool.begin());
+    size_t own = 0;   // pooled tables of our own allocations (arena tables stay pooled)
+    for (auto &pt : ctx->pool) own += !in_arena(ctx, pt.first);
+    for (size_t i = 0; own > 8 && i < ctx->pool.size();) {
+        if (in_arena(ctx, ctx->pool[i].first)) { i++; continue; }
+        (void)hipFree(ctx->pool[i].first);
+        ctx->pool.erase(ctx->pool.begin() + i);
+        own--;
     }
 }
 
@@ -2412,6 +2431,16 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         // batch paid a 17-GB hipMalloc inside the batch)
         if (dedup_prepare(ctx, ctx->dfull, n, false)) return fail("create");
     }
+    if (cfg->state_arena_bytes > 0) {
+        ctx->arena_bytes = (size_t)cfg->state_arena_bytes & ~(size_t)255;
+        if (dev_malloc((void **)&ctx->arena, ctx->arena_bytes, "state arena") != hipSuccess) {
+            (void)hipGetLastError();
+            ctx->arena = nullptr;
+            ctx->err = "state arena: out of device memory";
+            return fail("create");
+        }
+        hipLaunchKernelGGL(k_zero16, dim3(256 * 32), dim3(256), 0, ctx->stream, (uint4 *)ctx->arena, (int64_t)(ctx->arena_bytes / 16));
+    }
     // state_capacity_hint: one window table for that many keys, reserved now into the pool (a 70-GB table costs
     // ~2 s in hipMalloc: C5's first batch)
     if (cfg->state_capacity_hint > 0) {
@@ -2439,8 +2468,11 @@ void hm_destroy(hm_ctx *ctx) {
                       &ctx->td_params, &ctx->gapbuf};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
-    for (auto &g : ctx->gens) (void)hipFree(g.tab);
-    for (auto &pt : ctx->pool) (void)hipFree(pt.first);
+    for (auto &g : ctx->gens)
+        if (!in_arena(ctx, g.tab)) (void)hipFree(g.tab);
+    for (auto &pt : ctx->pool)
+        if (!in_arena(ctx, pt.first)) (void)hipFree(pt.first);
+    if (ctx->arena) (void)hipFree(ctx->arena);
     if (ctx->d_gmap) (void)hipFree(ctx->d_gmap);
     if (ctx->h_gmap) (void)hipHostFree(ctx->h_gmap);
     if (ctx->d_cmap) (void)hipFree(ctx->d_cmap);

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MOBHEAT_LIB: load another build of the same ABI (kernel variants under csrc/variants/ for tuning runs)
 LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
 
-HM_ABI_VERSION = 6
+HM_ABI_VERSION = 7
 HM_MEM_HOST = 0
 HM_MEM_DEVICE = 1
 HM_TILE_REC_BYTES = 48
@@ -27,7 +27,7 @@ class HmConfig(ctypes.Structure):
     _fields_ = [
         ("abi_version", c_i32), ("h3_res", c_i32), ("device", c_i32), ("late_uses_prev_watermark", c_i32),
         ("tile_us", c_i64), ("watermark_delay_ms", c_i64), ("state_capacity_hint", c_i64),
-        ("batch_capacity_hint", c_i64),
+        ("batch_capacity_hint", c_i64), ("state_arena_bytes", c_i64),
     ]
 
 

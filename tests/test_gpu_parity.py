@@ -359,3 +359,23 @@ def test_ingest_modes_parity(mode, monkeypatch):
         res, exp = _run(eng, ora, b, epoch)
         assert_batch_equal(res, exp)
     eng.close()
+
+
+@pytest.mark.parametrize("arena_mb", [1, 48])
+def test_state_arena_tables(arena_mb):
+    """Window tables carved from a create-time arena (state_arena_bytes): a small arena runs out mid-stream and
+    later tables come from hipMalloc; evicted arena tables are pooled and reused -- results equal the oracle."""
+    from mobheat import HeatmapEngine
+    from oracle.spark_oracle import SparkHeatmapOracle
+    rng = np.random.default_rng(61)
+    eng = HeatmapEngine(h3_res=10, state_arena_bytes=arena_mb << 20)
+    ora = SparkHeatmapOracle(h3_res=10)
+    t0 = 1_759_572_000_000_000
+    for epoch in range(10):
+        n = 40000
+        b = dict(lat=rng.uniform(37.90, 38.05, n), lon=rng.uniform(23.60, 23.85, n),
+                 ts_us=t0 + epoch * 7 * 60_000_000 + rng.integers(0, 12 * 60_000_000, n), speed=rng.uniform(0, 90, n),
+                 speed_valid=rng.random(n) > 0.2, vkey=rng.integers(0, 800, n).astype(np.uint64), row_valid=None)
+        res, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res, exp)
+    eng.close()
