@@ -379,3 +379,26 @@ def test_state_arena_tables(arena_mb):
         res, exp = _run(eng, ora, b, epoch)
         assert_batch_equal(res, exp)
     eng.close()
+
+
+@pytest.mark.parametrize("res", [0, 7, 15])
+def test_global_batch_other_resolutions(res):
+    """The whole pipeline at configs[1]'s res 7 and the extreme resolutions, on a global batch with edge points
+    (poles, the antimeridian, pentagon centres), two batches so cumulative state is exercised."""
+    from mobheat import HeatmapEngine, synth
+    from oracle.spark_oracle import SparkHeatmapOracle
+    rng = np.random.default_rng(70 + res)
+    eng = HeatmapEngine(h3_res=res)
+    ora = SparkHeatmapOracle(h3_res=res)
+    el, eo = synth.edge_points()
+    for epoch in range(2):
+        n = 30000
+        lat = np.r_[np.degrees(np.arcsin(rng.uniform(-1, 1, n))), el]
+        lon = np.r_[rng.uniform(-180, 180, n), eo]
+        m = lat.size
+        b = dict(lat=lat, lon=lon, ts_us=1_759_572_000_000_000 + epoch * 300_000_000 + rng.integers(0, 600_000_000, m),
+                 speed=rng.uniform(0, 900, m), speed_valid=rng.random(m) > 0.1,
+                 vkey=rng.integers(0, 5000, m).astype(np.uint64), row_valid=rng.random(m) > 0.01)
+        res_, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res_, exp)
+    eng.close()
