@@ -539,6 +539,21 @@ __global__ __launch_bounds__(256) void k_scan_add(unsigned long long *__restrict
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) out[i] += block_off[i / SC_PER];
 }
 
+// HM_NT_STORES bit 0: the partition scatter's 16-B stores non-temporal; bit 1: the merge's output rows (both written
+// once, read by the next kernel from HBM)
+#ifndef HM_NT_STORES
+#define HM_NT_STORES 2
+#endif
+typedef unsigned hm_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_stream(uint4 *p, uint4 v) {
+    if constexpr ((HM_NT_STORES & 1) != 0) {
+        const hm_v4u w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, (hm_v4u *)p);
+    } else {
+        *p = v;
+    }
+}
+
 // output part q (16 B) of record `rec` of a wave's 64: In = Out is a plain copy; TilePartial (48 B) -> SortedRec
 // (64 B) widens the counts and appends the key hash the digit lane computed
 template <typename In, typename Out>
@@ -612,14 +627,14 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict_
                 const int idx = r * 64 + ln, rec = idx / QO, q = idx % QO;
                 const unsigned p = __shfl(pos, rec, 64);
                 const unsigned hl = __shfl((unsigned)h, rec, 64), hh = __shfl((unsigned)(h >> 32), rec, 64);
-                if (rec < nrec && p != ~0u) d4[(int64_t)p * QO + q] = rp_part<In, Out>(ws, rec, q, (uint64_t)hl | ((uint64_t)hh << 32));
+                if (rec < nrec && p != ~0u) st_stream(&d4[(int64_t)p * QO + q], rp_part<In, Out>(ws, rec, q, (uint64_t)hl | ((uint64_t)hh << 32)));
             }
             __builtin_amdgcn_wave_barrier();
         } else {
             for (int r = 0; r < QO; r++) {
                 const int idx = r * 64 + ln, rec = idx / QO, q = idx % QO;
                 const unsigned p = __shfl(pos, rec, 64);
-                if (rec < nrec && p != ~0u) d4[(int64_t)p * QO + q] = src[(i0 + rec) * QI + q];
+                if (rec < nrec && p != ~0u) st_stream(&d4[(int64_t)p * QO + q], src[(i0 + rec) * QI + q]);
             }
         }
     }
@@ -732,14 +747,24 @@ struct RowsOut {   // update-mode output rows (SoA), heatmap_stream.py:124-132
 __device__ __forceinline__ void put_row(const RowsOut &o, int64_t t, uint64_t cell, unsigned long long we,
                                         unsigned long long count, unsigned long long nspeed, double sspeed, double slat,
                                         double slon) {
-    o.cell[t] = cell;
-    o.ws[t] = wdec(we);
-    o.cnt[t] = (int64_t)count;
     const bool null_sp = nspeed == 0;
-    o.sp[t] = null_sp ? 0.0 : sspeed / (double)nspeed;
-    o.spnull[t] = null_sp;
-    o.lon[t] = slon / (double)count;
-    o.lat[t] = slat / (double)count;
+    if constexpr ((HM_NT_STORES & 2) != 0) {
+        __builtin_nontemporal_store(cell, &o.cell[t]);
+        __builtin_nontemporal_store(wdec(we), &o.ws[t]);
+        __builtin_nontemporal_store((int64_t)count, &o.cnt[t]);
+        __builtin_nontemporal_store(null_sp ? 0.0 : sspeed / (double)nspeed, &o.sp[t]);
+        __builtin_nontemporal_store((uint8_t)null_sp, &o.spnull[t]);
+        __builtin_nontemporal_store(slon / (double)count, &o.lon[t]);
+        __builtin_nontemporal_store(slat / (double)count, &o.lat[t]);
+    } else {
+        o.cell[t] = cell;
+        o.ws[t] = wdec(we);
+        o.cnt[t] = (int64_t)count;
+        o.sp[t] = null_sp ? 0.0 : sspeed / (double)nspeed;
+        o.spnull[t] = null_sp;
+        o.lon[t] = slon / (double)count;
+        o.lat[t] = slat / (double)count;
+    }
 }
 
 // Rec = SortedRec: a batch's partials (partitioned); Rec = GrowRec: growth (rehash)
