@@ -554,6 +554,21 @@ __device__ __forceinline__ void st_stream(uint4 *p, uint4 v) {
     }
 }
 
+// bit 2: the merge's partitioned records loaded non-temporal (each is read once)
+template <typename Rec>
+__device__ __forceinline__ Rec ld_stream(const Rec *p) {
+    if constexpr ((HM_NT_STORES & 4) != 0 && sizeof(Rec) % 16 == 0) {
+        Rec r;
+        const hm_v4u *s = (const hm_v4u *)p;
+        hm_v4u *d = (hm_v4u *)&r;
+#pragma unroll
+        for (int q = 0; q < (int)(sizeof(Rec) / 16); q++) d[q] = __builtin_nontemporal_load(s + q);
+        return r;
+    } else {
+        return *p;
+    }
+}
+
 // output part q (16 B) of record `rec` of a wave's 64: In = Out is a plain copy; TilePartial (48 B) -> SortedRec
 // (64 B) widens the counts and appends the key hash the digit lane computed
 template <typename In, typename Out>
@@ -825,13 +840,13 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
         __syncthreads();
         // software pipeline: the next chunk's record is loaded while this chunk is merged
         Rec nxt;
-        if (b0 + t < b1) nxt = parts[b0 + t];
+        if (b0 + t < b1) nxt = ld_stream(parts + b0 + t);
         for (int64_t c0 = b0; c0 < b1; c0 += MO_THREADS) {
             // 1. stage this chunk's records in LDS
             const int64_t i = c0 + t;
             const bool has = i < b1;
             const Rec p = nxt;
-            if (i + MO_THREADS < b1) nxt = parts[i + MO_THREADS];
+            if (i + MO_THREADS < b1) nxt = ld_stream(parts + i + MO_THREADS);
             const unsigned long long we = wenc_of(p.wstart);
             uint64_t hk;
             if constexpr (rehash) hk = tile_hash(p.cell, p.wstart);
