@@ -542,7 +542,7 @@ __global__ __launch_bounds__(256) void k_scan_add(unsigned long long *__restrict
 // HM_NT_STORES bit 0: the partition scatter's 16-B stores non-temporal; bit 1: the merge's output rows (both written
 // once, read by the next kernel from HBM)
 #ifndef HM_NT_STORES
-#define HM_NT_STORES 2
+#define HM_NT_STORES 0
 #endif
 typedef unsigned hm_v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_stream(uint4 *p, uint4 v) {
