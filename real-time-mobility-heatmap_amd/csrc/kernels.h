@@ -71,6 +71,49 @@ struct alignas(64) GrowRec {
 };
 static_assert(sizeof(GrowRec) == 64, "GrowRec is 64 B");
 
+// ---- event keys (k_ingest's one output word per row) ----
+// A cell of the context's resolution has constant bits 52-63 (mode 1, reserved 0, resolution), so a row's
+// (cell, window) fits one word: the cell's low 52 bits and, in bits 52-63, 1 + the window's slot in the batch's
+// window registry (WREG_SLOTS windows per batch).  0 = the row aggregates nothing (invalid, late, no window slot).
+constexpr uint64_t CELL_LO = (UINT64_C(1) << 52) - 1;
+constexpr int WREG_SLOTS = 4095;
+HM_HD uint64_t ekey_make(uint64_t cell, unsigned widx) { return (cell & CELL_LO) | ((uint64_t)(widx + 1) << 52); }
+HM_HD unsigned ekey_widx(uint64_t k) { return (unsigned)(k >> 52) - 1u; }
+HM_HD uint64_t cell_hi_of(int res) { return (UINT64_C(1) << 59) | ((uint64_t)res << 52); }
+
+// the direct path's partial record: one aggregated row (count 1), 32 B, so that the partition's randomly placed
+// records are whole 32-B sectors.  speed = SPEED_NULL_BITS when speedKmh is null (a signalling-NaN payload: input
+// NaNs are stored as the canonical quiet NaN, which Spark's double arithmetic yields too).
+struct alignas(32) EventRec {
+    uint64_t key;    // ekey
+    double speed;
+    double lat;
+    double lon;
+};
+static_assert(sizeof(EventRec) == 32, "EventRec is 32 B");
+constexpr uint64_t SPEED_NULL_BITS = UINT64_C(0x7ff0000000000001);
+constexpr uint64_t CANON_NAN_BITS = UINT64_C(0x7ff8000000000000);
+
+// per-window parameters of the batch, indexed by registry slot (the direct path's partition and merge)
+struct alignas(32) WInfo {
+    unsigned long long wenc;   // window start ^ 2^63
+    uint64_t inner;            // mix64(windowStart + golden): tile_hash(cell, ws) = mix64(cell ^ inner)
+    unsigned binp;             // radix bin parameters: (REGION_BITS - rbits) << 24 | (window salt & smask)
+    unsigned pad[3];
+};
+static_assert(sizeof(WInfo) == 32, "WInfo is 32 B");
+
+// table mode (low cardinality): an aggregate evicted from k_agg's LDS table, bucketed by key hash for k_bin_reduce
+struct alignas(16) AggRec {
+    uint64_t key;              // ekey
+    unsigned long long cnt;    // count | n_speed << 32
+    double ssp;
+    double slat;
+    double slon;
+    uint64_t pad;
+};
+static_assert(sizeof(AggRec) == 48, "AggRec is 48 B");
+
 // latest-position candidate (HM_CAND_REC_BYTES = 32)
 struct Cand {
     uint64_t vkey;
@@ -139,8 +182,10 @@ struct DevStats {
     unsigned long long overflow;    // nonzero: a hash table probe bound was exceeded
     unsigned long long bad_vkey;
     unsigned long long dedup_retry; // k_ingest: a vkey probe hit its bound; rerun k_dedup_max on a larger table
-    unsigned long long n_gaps;      // partial slots holding no record (direct k_ingest: rows that aggregate nothing)
-    unsigned long long pad[3];
+    unsigned long long n_gaps;      // partial slots holding no record (gaps)
+    unsigned long long win_overflow; // k_ingest: rows of windows beyond the batch's window registry (WREG_SLOTS)
+    unsigned long long agg_spill;   // table mode: aggregates that did not fit a bucket (sent as partial records)
+    unsigned long long n_evicted;   // table mode: aggregates k_agg evicted into the buckets
 };
 
 HM_HD uint64_t mix64(uint64_t x) {
@@ -151,7 +196,8 @@ HM_HD uint64_t mix64(uint64_t x) {
     x ^= x >> 33;
     return x;
 }
-HM_HD uint64_t tile_hash(uint64_t cell, int64_t w) { return mix64(cell ^ mix64((uint64_t)w + UINT64_C(0x9e3779b97f4a7c15))); }
+HM_HD uint64_t window_inner(int64_t w) { return mix64((uint64_t)w + UINT64_C(0x9e3779b97f4a7c15)); }
+HM_HD uint64_t tile_hash(uint64_t cell, int64_t w) { return mix64(cell ^ window_inner(w)); }
 // floor(t / d) for d >= 1 by an invariant-divisor multiply (Granlund & Montgomery 1994, Fig. 4.1, N = 64):
 // m = floor(2^64 (2^l - d) / d) + 1, l = ceil(log2 d); exact for every 64-bit dividend.  make_floor_div (host).
 struct FloorDiv {

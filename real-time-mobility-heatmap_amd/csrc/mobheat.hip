@@ -271,144 +271,49 @@ __global__ __launch_bounds__(256) void k_cells_exact(const double *__restrict__ 
 }
 
 // =====================================================================================================
-// K2: LDS pre-aggregation into partial records (persistent blocks, flush when the table fills)
+// K2: the batch's window registry.  Every window a batch aggregates into gets a slot (its index widx, kept in
+// the rows' event keys, kernels.h ekey); a workgroup caches the windows it has seen in LDS.
 // =====================================================================================================
-#ifndef HM_LA_THREADS
-#define HM_LA_THREADS 256
-#endif
-constexpr int LA_THREADS = HM_LA_THREADS;
-#ifndef HM_LA_SLOTS
-#define HM_LA_SLOTS 512
-#endif
-constexpr int LA_SLOTS = HM_LA_SLOTS;  // LDS hash slots per workgroup (40 B each)
-constexpr int LA_CHUNK = LA_SLOTS / 2; // events inserted between occupancy checks
-constexpr int LA_FLUSH_AT = LA_SLOTS * 3 / 4 - LA_CHUNK;    // occupancy bound before a chunk: <= 3/4 full after
-static_assert(LA_CHUNK % LA_THREADS == 0 && LA_SLOTS % LA_THREADS == 0, "LDS table geometry");
-
-// LDS key of a (cell, window): a cell of the context's resolution has constant bits 52-63 (mode 1, reserved 0,
-// res), so its low 52 bits plus an index into the workgroup's window table (the window starts seen since the last
-// flush) make one 64-bit key: one CAS per probe.
-constexpr int LA_WT = 32;                                   // window table slots per workgroup
-constexpr uint64_t LA_CELL_LO = (UINT64_C(1) << 52) - 1;
-constexpr uint64_t LA_EMPTY = ~UINT64_C(0);                 // never a key: a key's bits 58-63 are zero
-__device__ __forceinline__ uint64_t la_key(uint64_t cell, unsigned widx) { return (cell & LA_CELL_LO) | ((uint64_t)widx << 52); }
-__device__ __forceinline__ unsigned la_slot(uint64_t key) {
-    return (unsigned)((key * UINT64_C(0x9e3779b97f4a7c15)) >> 40) & (LA_SLOTS - 1);
-}
-
-struct LaShared {   // (the five slot arrays are consecutive: la_flush addresses them as words[5][LA_SLOTS])
-    unsigned long long key[LA_SLOTS];   // la_key, LA_EMPTY = free
-    unsigned long long cnt[LA_SLOTS];   // low 32: count, high 32: n_speed (= TilePartial's count, nspeed words)
-    double ssp[LA_SLOTS];
-    double slat[LA_SLOTS];
-    double slon[LA_SLOTS];
-    unsigned short order[LA_SLOTS];     // la_flush: output record -> slot
-    long long wt[LA_WT];                // window starts (EMPTY_WIN = free)
-    unsigned wcnt[LA_WT];               // partials per window at a flush (the census)
-    unsigned int occ;
-    unsigned int scan[LA_THREADS / 64];
-    unsigned long long base;
-    unsigned dskip;                     // the fused dedup has given up (st->dedup_retry) -- skip it
-};
-
-// index of window start ws in the workgroup's window table (inserted if new); -1 when the table is full
-__device__ __forceinline__ int la_window(LaShared &S, int64_t ws, int64_t q) {
-    unsigned h = (unsigned)q & (LA_WT - 1);   // consecutive windows -> distinct slots
-    for (int probe = 0; probe < LA_WT; probe++) {
-        long long w = S.wt[h];
-        if (w == ws) return (int)h;
-        if (w == EMPTY_WIN) {
-            w = (long long)atomicCAS((unsigned long long *)&S.wt[h], (unsigned long long)EMPTY_WIN, (unsigned long long)ws);
-            if (w == EMPTY_WIN || w == ws) return (int)h;
-        }
-        h = (h + 1) & (LA_WT - 1);
+// registry slot of window quotient wq (enc = wenc of its start); -1 when the registry is full
+__device__ __forceinline__ int wreg_find(unsigned long long *reg, int64_t wq, unsigned long long enc) {
+    unsigned h = (unsigned)((uint64_t)wq % (uint64_t)WREG_SLOTS);   // consecutive windows -> consecutive slots
+    for (int p = 0; p < WREG_SLOTS; p++) {
+        // a stale (L2) copy can only show a slot empty: the CAS then returns its owner
+        unsigned long long cur = __hip_atomic_load(&reg[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == 0) cur = atomicCAS(&reg[h], 0ull, enc);
+        if (cur == 0 || cur == enc) return (int)h;
+        h = h + 1 == (unsigned)WREG_SLOTS ? 0u : h + 1;
     }
     return -1;
 }
-
-// a row that found no window-table slot: its own partial record (rare; out of line to spare registers)
-__device__ __forceinline__ bool la_direct(TilePartial *out, DevStats *st, WinLds &WL, const CensusSink &census, uint64_t cell,
-                                       int64_t ws, bool sv, double sp, double la, double lo) {
-    TilePartial p;
-    p.cell = cell;
-    p.wstart = ws;
-    p.count = 1;
-    p.nspeed = sv;
-    p.sspeed = sp;
-    p.slat = la;
-    p.slon = lo;
-    out[atomicAdd(&st->n_partials, 1ull)] = p;
-    return wl_add(WL, census, wenc_of(ws), 1ull);
+// per-workgroup cache of registry slots: one word per entry, ((wq mod 2^52) << 12) | (widx + 1), 0 = empty, so that
+// one CAS publishes both (hm_create requires tile_us >= 1 s: |wq| < 2^44, so wq mod 2^52 identifies the window)
+constexpr int WC_SLOTS = 32;
+struct WinCacheL {
+    unsigned long long e[WC_SLOTS];
+    unsigned cnt[WC_SLOTS];   // aggregated rows per cached window (the direct path's census)
+};
+__device__ __forceinline__ void wc_init(WinCacheL &C) {
+    for (int q = threadIdx.x; q < WC_SLOTS; q += blockDim.x) { C.e[q] = 0; C.cnt[q] = 0; }
 }
-
-// partial records of the table's keys; resets the table and the window table.  Pass 1 (a thread per two slots)
-// numbers the keys and counts them per window; pass 2 writes the records with three lanes per 48-B record, 16 B
-// each, so that every store instruction covers 21 whole records.
-__device__ void la_flush(LaShared &S, uint64_t cell_hi, TilePartial *out, DevStats *st, WinLds &WL, const CensusSink &census,
-                         bool &ok) {
-    __syncthreads();
-    constexpr int per = LA_SLOTS / LA_THREADS;
-    const int t = threadIdx.x;
-    unsigned c = 0;
-    for (int q = 0; q < per; q++) c += S.key[t * per + q] != LA_EMPTY;
-    // block exclusive scan of c
-    unsigned incl = c;
-    for (int o = 1; o < 64; o <<= 1) {
-        unsigned v = __shfl_up(incl, o, 64);
-        if (lane_id() >= o) incl += v;
-    }
-    const int wv = t >> 6;
-    if (lane_id() == 63) S.scan[wv] = incl;
-    __syncthreads();
-    unsigned wave_off = 0, total = 0;
-    for (int q = 0; q < LA_THREADS / 64; q++) {
-        if (q < wv) wave_off += S.scan[q];
-        total += S.scan[q];
-    }
-    if (t == 0) S.base = total ? atomicAdd(&st->n_partials, (unsigned long long)total) : 0;
-    unsigned idx = wave_off + incl - c;
-    for (int q = 0; q < per; q++) {
-        const int s = t * per + q;
-        const uint64_t k = S.key[s];
-        if (k != LA_EMPTY) {
-            const unsigned widx = (unsigned)(k >> 52);
-            S.order[idx++] = (unsigned short)s;
-            atomicAdd(&S.wcnt[widx], 1u);
+// widx of window wq (-1: registry full); slot = its cache entry (-1: the cache is full)
+__device__ __forceinline__ int wc_lookup(WinCacheL &C, unsigned long long *reg, int64_t wq, unsigned long long enc, int &slot) {
+    const unsigned long long tag = (uint64_t)wq & CELL_LO;
+    unsigned h = (unsigned)wq & (WC_SLOTS - 1);
+    int w = -2;
+    for (int p = 0; p < WC_SLOTS; p++) {
+        unsigned long long c = __hip_atomic_load(&C.e[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (c == 0) {
+            if (w == -2) w = wreg_find(reg, wq, enc);
+            if (w < 0) { slot = -1; return -1; }
+            c = atomicCAS(&C.e[h], 0ull, (tag << 12) | (unsigned long long)(w + 1));
+            if (c == 0) { slot = (int)h; return w; }
         }
+        if ((c >> 12) == tag) { slot = (int)h; return (int)(c & 0xfff) - 1; }
+        h = (h + 1) & (WC_SLOTS - 1);
     }
-    __syncthreads();
-    if (t < 3 * (LA_THREADS / 3)) {
-        const unsigned long long *W = S.key;   // words[5][LA_SLOTS]: key, cnt, ssp, slat, slon
-        uint4 *__restrict__ o4 = (uint4 *)(out + S.base);
-        const int qq = t % 3;
-        // part 0: (cell, window start), 1: (count | n_speed, sum speed), 2: (sum lat, sum lon)
-        const int i1 = qq == 0 ? 0 : qq == 1 ? 1 : 3;
-        const int i2 = qq == 1 ? 2 : 4;
-        for (unsigned r = (unsigned)t / 3; r < total; r += LA_THREADS / 3) {
-            const unsigned s = S.order[r];
-            const uint64_t w1 = W[i1 * LA_SLOTS + s], w2 = W[i2 * LA_SLOTS + s];
-            const uint64_t a = qq == 0 ? (w1 & LA_CELL_LO) | cell_hi : w1;
-            const uint64_t b = qq == 0 ? (uint64_t)S.wt[(w1 >> 52) & (LA_WT - 1)] : w2;
-            o4[(uint64_t)r * 3 + qq] = make_uint4((unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32));
-        }
-    }
-    __syncthreads();
-    for (int q = 0; q < per; q++) {
-        const int s = t * per + q;
-        S.key[s] = LA_EMPTY;
-        S.cnt[s] = 0;
-        S.ssp[s] = 0.0;
-        S.slat[s] = 0.0;
-        S.slon[s] = 0.0;
-    }
-    // census of the flushed partials per window (LDS; the global map is updated once per workgroup)
-    if (t < LA_WT) {
-        if (S.wcnt[t]) ok &= wl_add(WL, census, wenc_of(S.wt[t]), (unsigned long long)S.wcnt[t]);
-        S.wcnt[t] = 0;
-        S.wt[t] = EMPTY_WIN;
-    }
-    if (t == 0) S.occ = 0;
-    __syncthreads();
+    slot = -1;
+    return w == -2 ? wreg_find(reg, wq, enc) : w;
 }
 
 // census of a batch's partials per window (sizes the window tables before the merge)
@@ -466,7 +371,14 @@ constexpr int RP_BINS = 1 << RP_BITS;
 #ifndef HM_RP_TILE
 #define HM_RP_TILE 131072
 #endif
-constexpr int RP_TILE = HM_RP_TILE;    // partials per tile (one workgroup)
+constexpr int RP_TILE = HM_RP_TILE;    // partials per tile (one workgroup) at most
+// records per tile for n records: RP_TILE for large partitions, smaller ones so that a small partition (table mode's
+// partials, a stage merge) still spreads over the CUs (every tile writes a full histogram: at least 4096 records)
+static inline int64_t rp_tile_for(int64_t n) {
+    int64_t t = 4096;
+    while (t < RP_TILE && t * 512 < n) t <<= 1;
+    return t;
+}
 constexpr int RP_THREADS = 256;
 
 // the radix digit of a key: its (window, region) bin, or with nranks > 0 its owner rank (the multi-GPU
@@ -481,7 +393,7 @@ __device__ __forceinline__ unsigned rp_digit(uint64_t cell, int64_t ws, const Ge
 }
 
 template <typename Rec>
-__global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const Rec *__restrict__ parts, int64_t n, const GenDesc *gm,
+__global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const Rec *__restrict__ parts, int64_t n, int64_t tile, const GenDesc *gm,
                                                        const GenDesc *glist, int n_glist, int nranks, int nbins,
                                                        unsigned *__restrict__ H, int64_t ntiles, DevStats *st) {
     __shared__ unsigned h[RP_BINS + 1];
@@ -489,8 +401,8 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_hist(const Rec *__restrict__ 
     gc_load(C, glist, n_glist);
     for (int d = threadIdx.x; d <= RP_BINS; d += RP_THREADS) h[d] = 0;
     __syncthreads();
-    int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
-    int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
+    int64_t t0 = (int64_t)blockIdx.x * tile;
+    int64_t t1 = t0 + tile < n ? t0 + tile : n;
     bool bad = false;
     unsigned gaps = 0;   // gaps (cell 0) count in the extra digit nbins, after every bin
     for (int64_t i = t0 + threadIdx.x; i < t1; i += RP_THREADS) {
@@ -591,7 +503,7 @@ __device__ __forceinline__ uint4 rp_part(const uint4 *__restrict__ src, int64_t 
 // of 16-B parts, whole 64-B lines at random places -- per-lane 64-B records bounded this kernel's vector-memory
 // issue (6.4 -> 3.5 ms per 1e8 records).
 template <typename In, typename Out>
-__global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict__ parts, int64_t n,
+__global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict__ parts, int64_t n, int64_t tile,
                                                           const GenDesc *gm, const GenDesc *glist, int n_glist,
                                                           int nranks, int nbins, const unsigned long long *__restrict__ O,
                                                           int64_t ntiles, Out *__restrict__ dst) {
@@ -603,8 +515,8 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict_
     gc_load(C, glist, n_glist);
     for (int d = threadIdx.x; d < nbins; d += RP_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
     __syncthreads();
-    const int64_t t0 = (int64_t)blockIdx.x * RP_TILE;
-    const int64_t t1 = t0 + RP_TILE < n ? t0 + RP_TILE : n;
+    const int64_t t0 = (int64_t)blockIdx.x * tile;
+    const int64_t t1 = t0 + tile < n ? t0 + tile : n;
     const uint4 *__restrict__ src = (const uint4 *)parts;
     uint4 *__restrict__ d4 = (uint4 *)dst;
     const int ln = lane_id();
@@ -653,6 +565,461 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict_
             }
         }
     }
+}
+
+// =====================================================================================================
+// K2c: radix partition of the direct path: the batch's event keys (8 B per row) -> EventRecs (32 B) in
+// (window, region) bins, or (multi-GPU) 48-B TilePartials grouped by owner rank.  The histogram reads only the
+// keys; the scatter reads a record's speed/lat/lon only for aggregated rows.
+// =====================================================================================================
+// the key's radix digit: with nranks > 0 its owner rank, else its (window, region) bin (binp: kernels.h WInfo)
+__device__ __forceinline__ unsigned ev_digit(uint64_t h, unsigned binp, int nranks) {
+    if (nranks > 0) return (unsigned)owner_of(h, nranks);
+    const unsigned sb = binp >> 24;
+    return ((region_field(h) >> sb) << sb) | (binp & 0xffffffu);
+}
+
+constexpr int EV_THREADS = 512;
+__global__ __launch_bounds__(EV_THREADS) void k_ev_hist(const uint64_t *__restrict__ keys, int64_t n, int64_t tile,
+                                                       const WInfo *__restrict__ winfo, uint64_t cell_hi, int nranks, int nbins,
+                                                       unsigned *__restrict__ H, int64_t ntiles) {
+    __shared__ unsigned h[RP_BINS + 1];
+    for (int d = threadIdx.x; d <= nbins; d += EV_THREADS) h[d] = 0;
+    __syncthreads();
+    const int64_t t0 = (int64_t)blockIdx.x * tile;
+    const int64_t t1 = t0 + tile < n ? t0 + tile : n;
+    unsigned gaps = 0;   // rows without a key count in the extra digit nbins, after every bin
+    constexpr int U = 8;   // loads in flight per lane
+    for (int64_t b = t0 + threadIdx.x; b < t1; b += (int64_t)EV_THREADS * U) {
+        uint64_t k[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) k[u] = b + u * EV_THREADS < t1 ? __builtin_nontemporal_load(&keys[b + u * EV_THREADS]) : 0;
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (b + u * EV_THREADS >= t1) continue;
+            if (!k[u]) { gaps++; continue; }
+            const WInfo &wi = winfo[ekey_widx(k[u])];
+            const uint64_t hh = mix64(((k[u] & CELL_LO) | cell_hi) ^ wi.inner);
+            atomicAdd(&h[ev_digit(hh, wi.binp, nranks)], 1u);
+        }
+    }
+    gaps = (unsigned)wave_sum((unsigned long long)gaps);
+    if (gaps && lane_id() == 0) atomicAdd(&h[nbins], gaps);
+    __syncthreads();
+    for (int d = threadIdx.x; d <= nbins; d += EV_THREADS) H[(int64_t)d * ntiles + blockIdx.x] = h[d];
+}
+
+// Per wave and round, 64 rows: each lane takes its row's digit and position (LDS cursor) and builds its record in
+// LDS; then the wave writes the 64 records as rounds of 16-B parts, consecutive lanes covering consecutive parts of
+// one record (whole 32-B sectors / 48-B records at random places).  Out = EventRec (the direct path) or TilePartial
+// (the owner partition of hm_stage_local: count 1, window start from the registry).
+template <typename Out>
+__global__ __launch_bounds__(EV_THREADS) void k_ev_scatter(const uint64_t *__restrict__ keys, int64_t n, int64_t tile,
+                                                          const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
+                                                          const double *__restrict__ lat, const double *__restrict__ lon,
+                                                          const WInfo *__restrict__ winfo, uint64_t cell_hi, int nranks, int nbins,
+                                                          const unsigned long long *__restrict__ O, int64_t ntiles,
+                                                          Out *__restrict__ dst) {
+    constexpr int QO = sizeof(Out) / 16;
+    __shared__ unsigned cur[RP_BINS];   // positions < 2^32 - 1 (hm_process_batch checks n)
+    __shared__ uint4 stage[(EV_THREADS / 64) * 64 * QO];
+    for (int d = threadIdx.x; d < nbins; d += EV_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
+    __syncthreads();
+    const int64_t t0 = (int64_t)blockIdx.x * tile;
+    const int64_t t1 = t0 + tile < n ? t0 + tile : n;
+    uint4 *__restrict__ d4 = (uint4 *)dst;
+    uint4 *ws = stage + (threadIdx.x >> 6) * 64 * QO;
+    const int ln = lane_id();
+    // a row's columns, loaded one round ahead (every load of a round is issued before the first is used)
+    struct Row { uint64_t k; double sp, la, lo; uint8_t sv; };
+    auto load = [&](int64_t i) {
+        Row r{0, 0.0, 0.0, 0.0, 0};
+        if (i < t1) {
+            r.k = __builtin_nontemporal_load(&keys[i]);
+            r.sp = speed ? __builtin_nontemporal_load(&speed[i]) : 0.0;
+            r.sv = speed ? (speed_valid ? __builtin_nontemporal_load(&speed_valid[i]) : (uint8_t)1) : (uint8_t)0;
+            r.la = __builtin_nontemporal_load(&lat[i]);
+            r.lo = __builtin_nontemporal_load(&lon[i]);
+        }
+        return r;
+    };
+    int64_t i0 = t0 + (int64_t)(threadIdx.x >> 6) * 64;
+    Row nx = load(i0 + ln);
+    for (; i0 < t1; i0 += EV_THREADS) {
+        const Row r = nx;
+        nx = load(i0 + EV_THREADS + ln);
+        unsigned pos = ~0u;   // ~0u: no record
+        if (r.k) {
+            const uint64_t k = r.k;
+            const WInfo &wi = winfo[ekey_widx(k)];
+            const uint64_t cell = (k & CELL_LO) | cell_hi;
+            const uint64_t hh = mix64(cell ^ wi.inner);
+            pos = atomicAdd(&cur[ev_digit(hh, wi.binp, nranks)], 1u);
+            const bool sv = r.sv != 0;
+            const double sp = sv ? r.sp : 0.0;
+            const uint64_t lab = __builtin_bit_cast(uint64_t, r.la), lob = __builtin_bit_cast(uint64_t, r.lo);
+            if constexpr (std::is_same<Out, EventRec>::value) {
+                const uint64_t spb = !sv ? SPEED_NULL_BITS : sp != sp ? CANON_NAN_BITS : __builtin_bit_cast(uint64_t, sp);
+                ws[ln * 2 + 0] = make_uint4((unsigned)k, (unsigned)(k >> 32), (unsigned)spb, (unsigned)(spb >> 32));
+                ws[ln * 2 + 1] = make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32));
+            } else {
+                static_assert(std::is_same<Out, TilePartial>::value, "k_ev_scatter output");
+                const uint64_t w = (uint64_t)wdec(wi.wenc), spb = __builtin_bit_cast(uint64_t, sp);
+                ws[ln * 3 + 0] = make_uint4((unsigned)cell, (unsigned)(cell >> 32), (unsigned)w, (unsigned)(w >> 32));
+                ws[ln * 3 + 1] = make_uint4(1u, sv ? 1u : 0u, (unsigned)spb, (unsigned)(spb >> 32));
+                ws[ln * 3 + 2] = make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (int q = 0; q < QO; q++) {
+            const int idx = q * 64 + ln, rec = idx / QO, part = idx % QO;
+            const unsigned p = __shfl(pos, rec, 64);
+            if (p != ~0u) d4[(int64_t)p * QO + part] = ws[idx];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// =====================================================================================================
+// K2d: table mode (low-cardinality batches: few distinct (cell, window) keys, heavily repeated -- city-scale data).
+// Per-workgroup partial aggregation cannot get far below the keys a workgroup sees (a Zipf tail of keys that
+// recur about once per workgroup), so the batch is aggregated in two LDS passes instead of per-row partials:
+//  k_agg         one 1024-thread workgroup per CU streams a contiguous span of the event keys through an LDS
+//                table of AG_SLOTS aggregates; when it fills, the entries with the lowest counts are evicted (the
+//                hot keys stay resident until the end) into 256 buckets by key hash (x 8 sub-buckets by XCD, for
+//                locality only: any placement is correct);
+//  k_bin_reduce  one workgroup per bucket aggregates its evicted entries (a bucket holds 1/256 of the keys) and
+//                writes one partial record per key -> the usual partition + merge.
+// =====================================================================================================
+constexpr int AG_THREADS = 1024;
+constexpr int AG_SLOTS = 3840;                  // 40 B each: 150 KB of LDS, one workgroup per CU
+constexpr int AG_PER = AG_SLOTS / AG_THREADS + (AG_SLOTS % AG_THREADS != 0);
+constexpr int AG_FLUSH_AT = AG_SLOTS - AG_THREADS;   // a round adds at most AG_THREADS keys
+constexpr int AG_KEEP_MAX = AG_SLOTS / 3;       // aggregates kept resident by a flush
+constexpr int AG_PROBES = 64;
+constexpr int AG_BINS = 256, AG_SUB = 8;        // buckets x sub-buckets (XCD)
+struct AgTable {
+    unsigned long long key[AG_SLOTS];   // ekey, 0 = free
+    unsigned long long cnt[AG_SLOTS];   // count | n_speed << 32
+    double ssp[AG_SLOTS];
+    double slat[AG_SLOTS];
+    double slon[AG_SLOTS];
+    unsigned occ;
+    unsigned keep_from;
+    unsigned hist[16];
+    unsigned bcnt[AG_BINS];
+    unsigned long long bbase[AG_BINS];
+    unsigned scan[AG_THREADS / 64];
+    unsigned long long obase;
+};
+__device__ __forceinline__ unsigned ag_home(uint64_t k) { return (unsigned)(((mix64(k) >> 32) * (uint64_t)AG_SLOTS) >> 32); }
+__device__ __forceinline__ unsigned ag_bin(uint64_t k) { return (unsigned)mix64(k ^ UINT64_C(0x94d049bb133111eb)) & (AG_BINS - 1); }
+__device__ __forceinline__ unsigned xcc_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+    return v & (AG_SUB - 1);
+}
+__device__ __forceinline__ void ag_clear(AgTable &T) {
+    for (int s = threadIdx.x; s < AG_SLOTS; s += AG_THREADS) {
+        T.key[s] = 0;
+        T.cnt[s] = 0;
+        T.ssp[s] = 0.0;
+        T.slat[s] = 0.0;
+        T.slon[s] = 0.0;
+    }
+    if (threadIdx.x == 0) T.occ = 0;
+}
+// add an aggregate for key k (inserted if new); false when no slot was found within AG_PROBES
+__device__ __forceinline__ bool ag_add(AgTable &T, uint64_t k, unsigned long long c, double ssp, double sla, double slo,
+                                       bool &fresh) {
+    unsigned h = ag_home(k);
+    fresh = false;
+    for (int p = 0; p < AG_PROBES; p++) {
+        unsigned long long cur = __hip_atomic_load(&T.key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == 0) {
+            cur = atomicCAS(&T.key[h], 0ull, (unsigned long long)k);
+            fresh = cur == 0;
+        }
+        if (cur == 0 || cur == k) {
+            atomicAdd(&T.cnt[h], c);
+            if (c >> 32) atomicAdd(&T.ssp[h], ssp);   // (only non-null speeds: Spark's sum skips nulls)
+            atomicAdd(&T.slat[h], sla);
+            atomicAdd(&T.slon[h], slo);
+            return true;
+        }
+        h = h + 1 == (unsigned)AG_SLOTS ? 0u : h + 1;
+    }
+    return false;
+}
+// one partial record for key k (rare spill paths and k_bin_reduce's output), appended to out
+__device__ __forceinline__ TilePartial ag_partial(uint64_t k, unsigned long long c, double ssp, double sla, double slo,
+                                                  const unsigned long long *wreg, uint64_t cell_hi) {
+    TilePartial p;
+    p.cell = (k & CELL_LO) | cell_hi;
+    p.wstart = wdec(wreg[ekey_widx(k)]);
+    p.count = (uint32_t)c;
+    p.nspeed = (uint32_t)(c >> 32);
+    p.sspeed = ssp;
+    p.slat = sla;
+    p.slon = slo;
+    return p;
+}
+__device__ __forceinline__ void ag_spill(uint64_t k, unsigned long long c, double ssp, double sla, double slo,
+                                         const unsigned long long *wreg, uint64_t cell_hi, TilePartial *out, DevStats *st,
+                                         WinLds &WL, const CensusSink &census, bool &ok) {
+    const TilePartial p = ag_partial(k, c, ssp, sla, slo, wreg, cell_hi);
+    out[atomicAdd(&st->n_partials, 1ull)] = p;
+    atomicAdd(&st->agg_spill, 1ull);
+    ok &= wl_add(WL, census, wenc_of(p.wstart), 1ull);
+}
+// k_agg's flush: the entries below the keep threshold go to their buckets; kept ones are re-inserted into the
+// cleared table (so that probe chains stay intact).  final: every entry is evicted.
+__device__ void ag_flush(AgTable &T, bool final, AggRec *__restrict__ bucket, unsigned long long *cursor, unsigned cap,
+                         const unsigned long long *wreg, uint64_t cell_hi, TilePartial *out, DevStats *st, WinLds &WL,
+                         const CensusSink &census, bool &ok) {
+    const int t = threadIdx.x;
+    if (t < 16) T.hist[t] = 0;
+    for (int b = t; b < AG_BINS; b += AG_THREADS) T.bcnt[b] = 0;
+    __syncthreads();
+    int lg[AG_PER];
+    for (int q = 0; q < AG_PER; q++) {
+        const int s = t + q * AG_THREADS;
+        lg[q] = -1;
+        if (s < AG_SLOTS && T.key[s]) {
+            const unsigned c = (unsigned)T.cnt[s];
+            lg[q] = min(31 - __clz(c), 15);
+            atomicAdd(&T.hist[lg[q]], 1u);
+        }
+    }
+    __syncthreads();
+    if (t == 0) {   // keep the entries with count >= 2^kf, at most AG_KEEP_MAX of them (kf >= 1: singletons go)
+        unsigned kf = 16, acc = 0;
+        if (!final)
+            for (int b = 15; b >= 1; b--) {
+                if (acc + T.hist[b] > (unsigned)AG_KEEP_MAX) break;
+                acc += T.hist[b];
+                kf = (unsigned)b;
+            }
+        T.keep_from = kf;
+    }
+    __syncthreads();
+    const int kf = (int)T.keep_from;
+    unsigned rk[AG_PER];
+    for (int q = 0; q < AG_PER; q++) {
+        const int s = t + q * AG_THREADS;
+        rk[q] = 0;
+        if (lg[q] >= 0 && lg[q] < kf) rk[q] = atomicAdd(&T.bcnt[ag_bin(T.key[s])], 1u);
+    }
+    __syncthreads();
+    const unsigned xs = xcc_id();
+    for (int b = t; b < AG_BINS; b += AG_THREADS)
+        if (T.bcnt[b]) T.bbase[b] = atomicAdd(&cursor[b * AG_SUB + xs], (unsigned long long)T.bcnt[b]);
+    __syncthreads();
+    uint64_t kk[AG_PER];
+    unsigned long long kc[AG_PER];
+    double ks[AG_PER], kla[AG_PER], klo[AG_PER];
+    unsigned long long evicted = 0;
+    for (int q = 0; q < AG_PER; q++) {
+        const int s = t + q * AG_THREADS;
+        kk[q] = 0;
+        if (lg[q] < 0) continue;
+        const uint64_t k = T.key[s];
+        const unsigned long long c = T.cnt[s];
+        const double a = T.ssp[s], b = T.slat[s], d = T.slon[s];
+        if (lg[q] >= kf) {
+            kk[q] = k; kc[q] = c; ks[q] = a; kla[q] = b; klo[q] = d;
+            continue;
+        }
+        evicted++;
+        const unsigned bin = ag_bin(k);
+        const unsigned long long pos = T.bbase[bin] + rk[q];
+        if (pos < cap) {
+            AggRec r;
+            r.key = k;
+            r.cnt = c;
+            r.ssp = a;
+            r.slat = b;
+            r.slon = d;
+            r.pad = 0;
+            bucket[(uint64_t)(bin * AG_SUB + xs) * cap + pos] = r;
+        } else {
+            ag_spill(k, c, a, b, d, wreg, cell_hi, out, st, WL, census, ok);
+        }
+    }
+    evicted = wave_sum(evicted);
+    if (evicted && lane_id() == 0) atomicAdd(&st->n_evicted, evicted);
+    __syncthreads();
+    ag_clear(T);
+    __syncthreads();
+    unsigned kept = 0;
+    for (int q = 0; q < AG_PER; q++) {
+        bool fresh;
+        if (kk[q]) { ag_add(T, kk[q], kc[q], ks[q], kla[q], klo[q], fresh); kept++; }   // (<= AG_KEEP_MAX: always fits)
+    }
+    kept = (unsigned)wave_sum((unsigned long long)kept);
+    if (kept && lane_id() == 0) atomicAdd(&T.occ, kept);
+    __syncthreads();
+}
+
+// keys inserted into the LDS table so far, identical in every thread: per round each wave adds its fresh keys to
+// one of three LDS counters, a barrier, every thread reads it; the counter two rounds ahead is cleared (its last
+// readers passed the previous barrier, its next writers are a barrier away), so one barrier per round suffices
+struct FreshCount {
+    unsigned *c;
+    int r3 = 0;
+    unsigned occ = 0;
+    __device__ explicit FreshCount(unsigned *ctr) : c(ctr) {}
+    __device__ unsigned round(bool fresh) {
+        const unsigned long long fb = __ballot(fresh);
+        if (fb && lane_id() == 0) atomicAdd(&c[r3], (unsigned)__popcll(fb));
+        __syncthreads();
+        occ += c[r3];
+        if (threadIdx.x == 0) c[r3 == 0 ? 2 : r3 - 1] = 0;
+        r3 = r3 == 2 ? 0 : r3 + 1;
+        return occ;
+    }
+};
+
+__global__ __launch_bounds__(AG_THREADS) void k_agg(const uint64_t *__restrict__ keys, int64_t n, int64_t span,
+                                                    const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
+                                                    const double *__restrict__ lat, const double *__restrict__ lon,
+                                                    AggRec *__restrict__ bucket, unsigned long long *cursor, unsigned cap,
+                                                    const unsigned long long *wreg, uint64_t cell_hi, TilePartial *out,
+                                                    WinCount *cmap, DevStats *st) {
+    __shared__ AgTable T;
+    __shared__ WinLds WL;
+    __shared__ unsigned fresh_ctr[3];
+    ag_clear(T);
+    wl_init(WL);
+    if (threadIdx.x < 3) fresh_ctr[threadIdx.x] = 0;
+    __syncthreads();
+    const CensusSink census{cmap};
+    bool ok = true;
+    const int64_t b0 = (int64_t)blockIdx.x * span;
+    const int64_t b1 = b0 + span < n ? b0 + span : n;
+    FreshCount FC(fresh_ctr);
+    // a row's columns, loaded one round ahead (the round's loads are in flight while the previous one aggregates)
+    struct Row { uint64_t k; double sp, la, lo; bool sv; };
+    auto load = [&](int64_t i) {
+        Row r{0, 0.0, 0.0, 0.0, false};
+        if (i < b1) {
+            r.k = __builtin_nontemporal_load(&keys[i]);
+            r.sv = speed ? (speed_valid ? __builtin_nontemporal_load(&speed_valid[i]) != 0 : true) : false;
+            r.sp = speed ? __builtin_nontemporal_load(&speed[i]) : 0.0;
+            r.la = __builtin_nontemporal_load(&lat[i]);
+            r.lo = __builtin_nontemporal_load(&lon[i]);
+        }
+        return r;
+    };
+    Row nx = load(b0 + threadIdx.x);
+    for (int64_t c0 = b0; c0 < b1; c0 += AG_THREADS) {
+        const Row r = nx;
+        nx = load(c0 + AG_THREADS + threadIdx.x);
+        const uint64_t k = r.k;
+        bool fresh = false;
+        if (k) {
+            const double sp = r.sv ? r.sp : 0.0, la = r.la, lo = r.lo;
+            const unsigned long long c = 1ull | ((unsigned long long)r.sv << 32);
+            if (!ag_add(T, k, c, sp, la, lo, fresh)) ag_spill(k, c, sp, la, lo, wreg, cell_hi, out, st, WL, census, ok);
+        }
+        if (FC.round(fresh) > (unsigned)AG_FLUSH_AT) {
+            ag_flush(T, false, bucket, cursor, cap, wreg, cell_hi, out, st, WL, census, ok);
+            FC.occ = T.occ;
+        }
+    }
+    ag_flush(T, true, bucket, cursor, cap, wreg, cell_hi, out, st, WL, census, ok);
+    __syncthreads();
+    ok &= wl_flush(WL, census);
+    if (__ballot(!ok) && lane_id() == 0) atomicAdd(&st->overflow, 1ull);
+}
+
+// every entry of the table as a partial record (a block-wide scan reserves one contiguous run), counted per window
+__device__ void ag_emit_all(AgTable &T, const unsigned long long *wreg, uint64_t cell_hi, TilePartial *__restrict__ out,
+                            DevStats *st, WinLds &WL, const CensusSink &census, bool &ok) {
+    const int t = threadIdx.x;
+    unsigned c = 0;
+    for (int q = 0; q < AG_PER; q++) {
+        const int s = t + q * AG_THREADS;
+        c += s < AG_SLOTS && T.key[s] != 0;
+    }
+    unsigned incl = c;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned v = __shfl_up(incl, o, 64);
+        if (lane_id() >= o) incl += v;
+    }
+    const int wv = t >> 6;
+    if (lane_id() == 63) T.scan[wv] = incl;
+    __syncthreads();
+    unsigned off = 0, total = 0;
+    for (int q = 0; q < AG_THREADS / 64; q++) {
+        if (q < wv) off += T.scan[q];
+        total += T.scan[q];
+    }
+    if (t == 0) T.obase = total ? atomicAdd(&st->n_partials, (unsigned long long)total) : 0;
+    __syncthreads();
+    unsigned long long pos = T.obase + off + incl - c;
+    for (int q = 0; q < AG_PER; q++) {
+        const int s = t + q * AG_THREADS;
+        const bool live = s < AG_SLOTS && T.key[s] != 0;
+        unsigned long long we = 0;
+        if (live) {
+            const TilePartial p = ag_partial(T.key[s], T.cnt[s], T.ssp[s], T.slat[s], T.slon[s], wreg, cell_hi);
+            out[pos++] = p;
+            we = wenc_of(p.wstart);
+        }
+        ok &= wave_count_windows(live, we, 1ull, WL, census);
+    }
+    __syncthreads();
+    ag_clear(T);
+    __syncthreads();
+}
+
+// one workgroup per bucket: its sub-buckets' aggregates -> one partial record per key (more if the bucket holds
+// more keys than the table: it is then emitted whenever it fills)
+__global__ __launch_bounds__(AG_THREADS) void k_bin_reduce(const AggRec *__restrict__ bucket, const unsigned long long *cursor,
+                                                           unsigned cap, const unsigned long long *wreg, uint64_t cell_hi,
+                                                           TilePartial *__restrict__ out, WinCount *cmap, DevStats *st) {
+    __shared__ AgTable T;
+    __shared__ WinLds WL;
+    __shared__ unsigned long long sub_end[AG_SUB + 1];
+    __shared__ unsigned fresh_ctr[3];
+    ag_clear(T);
+    wl_init(WL);
+    if (threadIdx.x < 3) fresh_ctr[threadIdx.x] = 0;
+    const int bin = blockIdx.x;
+    if (threadIdx.x == 0) {
+        unsigned long long acc = 0;
+        sub_end[0] = 0;
+        for (int x = 0; x < AG_SUB; x++) {
+            const unsigned long long c = cursor[bin * AG_SUB + x];
+            acc += c < cap ? c : cap;
+            sub_end[x + 1] = acc;
+        }
+    }
+    __syncthreads();
+    const CensusSink census{cmap};
+    bool ok = true;
+    const unsigned long long total = sub_end[AG_SUB];
+    FreshCount FC(fresh_ctr);
+    for (unsigned long long c0 = 0; c0 < total; c0 += AG_THREADS) {
+        const unsigned long long j = c0 + threadIdx.x;
+        bool fresh = false;
+        if (j < total) {
+            int x = 0;
+            while (j >= sub_end[x + 1]) x++;
+            const AggRec r = bucket[(uint64_t)(bin * AG_SUB + x) * cap + (j - sub_end[x])];
+            if (!ag_add(T, r.key, r.cnt, r.ssp, r.slat, r.slon, fresh))
+                ag_spill(r.key, r.cnt, r.ssp, r.slat, r.slon, wreg, cell_hi, out, st, WL, census, ok);
+        }
+        if (FC.round(fresh) > (unsigned)AG_FLUSH_AT) {
+            ag_emit_all(T, wreg, cell_hi, out, st, WL, census, ok);
+            FC.occ = 0;
+        }
+    }
+    ag_emit_all(T, wreg, cell_hi, out, st, WL, census, ok);
+    ok &= wl_flush(WL, census);
+    if (__ballot(!ok) && lane_id() == 0) atomicAdd(&st->overflow, 1ull);
 }
 
 // =====================================================================================================
@@ -737,13 +1104,33 @@ __device__ __forceinline__ int mo_holder(MoShared &S, unsigned long long addr) {
     }
     return -1;
 }
+// a merge input record, normalised: SortedRec (table mode / stage merge), GrowRec (growth), EventRec (direct path)
+struct MRec {
+    uint64_t cell;
+    unsigned long long we;   // wenc of the window start
+    uint64_t hk;             // tile_hash(cell, window start)
+    unsigned long long cnt, nsp;
+    double ssp, slat, slon;
+    unsigned long long touched;   // GrowRec only
+};
+__device__ __forceinline__ MRec mrec_of(const SortedRec &p, const WInfo *, uint64_t) {
+    return MRec{p.cell, wenc_of(p.wstart), p.hash, p.count, p.nspeed, p.sspeed, p.slat, p.slon, 0ull};
+}
+__device__ __forceinline__ MRec mrec_of(const GrowRec &p, const WInfo *, uint64_t) {
+    return MRec{p.cell, wenc_of(p.wstart), tile_hash(p.cell, p.wstart), p.count, p.nspeed, p.sspeed, p.slat, p.slon, p.touched};
+}
+__device__ __forceinline__ MRec mrec_of(const EventRec &p, const WInfo *winfo, uint64_t cell_hi) {
+    const WInfo &wi = winfo[ekey_widx(p.key)];
+    const uint64_t cell = (p.key & CELL_LO) | cell_hi;
+    const bool sv = __builtin_bit_cast(uint64_t, p.speed) != SPEED_NULL_BITS;
+    return MRec{cell, wi.wenc, mix64(cell ^ wi.inner), 1ull, sv ? 1ull : 0ull, sv ? p.speed : 0.0, p.lat, p.lon, 0ull};
+}
 // a duplicate of lane x's key: add this record's values into x's staging entry
-template <typename Rec>
-__device__ __forceinline__ void mo_add_into(MoShared &S, int x, const Rec &p) {
-    atomicAdd(&S.scnt[x], (unsigned long long)p.count);
-    if (p.nspeed) {
-        atomicAdd(&S.snsp[x], (unsigned long long)p.nspeed);
-        atomicAdd(&S.sssp[x], p.sspeed);
+__device__ __forceinline__ void mo_add_into(MoShared &S, int x, const MRec &p) {
+    atomicAdd(&S.scnt[x], p.cnt);
+    if (p.nsp) {
+        atomicAdd(&S.snsp[x], p.nsp);
+        atomicAdd(&S.sssp[x], p.ssp);
     }
     atomicAdd(&S.sslat[x], p.slat);
     atomicAdd(&S.sslon[x], p.slon);
@@ -782,11 +1169,12 @@ __device__ __forceinline__ void put_row(const RowsOut &o, int64_t t, uint64_t ce
     }
 }
 
-// Rec = SortedRec: a batch's partials (partitioned); Rec = GrowRec: growth (rehash)
+// Rec = SortedRec: a batch's partials (partitioned); EventRec: the direct path's rows; GrowRec: growth (rehash)
 template <typename Rec>
 __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restrict__ parts, int64_t n,
                                                             const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
                                                             GenDesc *gm, const GenDesc *glist, int n_glist,
+                                                            const WInfo *__restrict__ winfo, uint64_t cell_hi,
                                                             unsigned seq, RowsOut rows, unsigned *bin_cnt, DevStats *st) {
     constexpr bool rehash = std::is_same<Rec, GrowRec>::value;
     __shared__ MoShared S;
@@ -845,19 +1233,18 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             // 1. stage this chunk's records in LDS
             const int64_t i = c0 + t;
             const bool has = i < b1;
-            const Rec p = nxt;
+            MRec p{};
+            if (has) p = mrec_of(nxt, winfo, cell_hi);
             if (i + MO_THREADS < b1) nxt = ld_stream(parts + i + MO_THREADS);
-            const unsigned long long we = wenc_of(p.wstart);
-            uint64_t hk;
-            if constexpr (rehash) hk = tile_hash(p.cell, p.wstart);
-            else hk = p.hash;
+            const unsigned long long we = p.we;
+            const uint64_t hk = p.hk;
             if (has) {
                 S.sc[t] = p.cell;
                 S.sh[t] = hk;
                 S.sw[t] = we;
-                S.scnt[t] = (unsigned long long)p.count;
-                S.snsp[t] = (unsigned long long)p.nspeed;
-                S.sssp[t] = p.sspeed;
+                S.scnt[t] = p.cnt;
+                S.snsp[t] = p.nsp;
+                S.sssp[t] = p.ssp;
                 S.sslat[t] = p.slat;
                 S.sslon[t] = p.slon;
             }
@@ -892,7 +1279,6 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                                     if (created) {
                                         atomicOr(&S.tags[bi >> 2], tg << sh);
                                         S.res_dirty[r] = 1;
-                                        atomicAdd(&S.res_new[r], 1u);
                                     }
                                     done = true;
                                 }
@@ -931,6 +1317,11 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                     }
                 }
                 if (!done) overflow = true;
+            }
+            // keys created in the resident regions, one LDS add per region and wave
+            for (int q = 0; q < nres; q++) {
+                const unsigned long long m = __ballot(created && r == q);
+                if (m && lane_id() == 0) atomicAdd(&S.res_new[q], (unsigned)__popcll(m));
             }
             __syncthreads();
             // 3. apply (this workgroup is the only writer of these regions) and write the key's output row
@@ -1216,278 +1607,165 @@ __global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__
 
 // =====================================================================================================
 // K1: ingest. One pass over the events: the filter (heatmap_stream.py:96-104), latLngToCell (the UDF,
-// :65-75), the tumbling window and late test (:107,115), the per-vkey max ts of the dedup (:200-203), and
-// LDS pre-aggregation of (cell, windowStart) into partial records (:112-123). The fp64 cell computation
-// dominates; the aggregation's LDS atomics and the dedup's table atomics overlap with it.
+// :65-75), the tumbling window and late test (:107,115), the batch's window registry, the per-vkey max ts of the
+// dedup (:200-203), and one event key per row (kernels.h ekey: cell + window slot; 0 = not aggregated) -- the
+// input of both aggregation paths (direct: partition + merge; table: k_agg + k_bin_reduce).  The fp64 cell
+// computation dominates; the dedup's table atomics overlap with it.
 // =====================================================================================================
 // The fused per-vkey max gives up on a key after DEDUP_FUSED_PROBES probes (its table was sized from the previous
-// batch and is too small); the first give-up is published in st->dedup_retry and later chunks skip the fused
-// dedup, which phase_dedup then reruns over the whole batch on a full-size table.  (Published in *dgiveup, a word
-// on a cache line of its own, and polled every 16 chunks: polling a DevStats word every chunk, whose line all
-// flushes hit with atomics, made k_ingest 4x slower.)
+// batch and is too small); the first give-up is published in *dgiveup, a word on a cache line of its own, polled
+// every 16 rounds (polling a DevStats word every round, a line other atomics hit, made the ingest 4x slower), and
+// later rounds skip the fused dedup, which phase_dedup then reruns over the whole batch on a full-size table.
 constexpr unsigned long long DEDUP_FUSED_PROBES = 32;
+constexpr int IG_THREADS = 256;
 
-// DIRECT: no LDS pre-aggregation -- every aggregated row is its own partial record (staged in LDS, stored four
-// lanes per record).  The host picks it when the previous batch's partials were > 80% of its aggregated rows
-// (nearly every key distinct: the LDS table's probes, atomics and flushes then buy nothing, cf. Spark's adaptive
-// skipping of partial aggregation when its reduction ratio is poor).
-template <bool DIRECT>
-__global__ __launch_bounds__(LA_THREADS) HM_SNAP_ATTR void k_ingest(
-    const double *__restrict__ lat, const double *__restrict__ lon, const int64_t *__restrict__ ts,
-    const uint8_t *__restrict__ row_valid, const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
-    const uint64_t *__restrict__ vkey, int64_t n, int res, FloorDiv wdiv, int64_t late_end_us,
-    uint8_t *__restrict__ flags_out, TilePartial *__restrict__ out, DedupSlot *dtab, unsigned long long dmask,
-    unsigned int *dused, unsigned long long *n_dused, unsigned int *__restrict__ slow, unsigned long long *n_slow,
-    unsigned long long *dgiveup, WinCount *cmap, DevStats *st) {
-    __shared__ LaShared S;
-    __shared__ WinLds WL;
-    __shared__ double Fc[20][3], Fu[20][2][3];   // the fast path's per-face tables (res parity): LDS reads
-    for (int k = threadIdx.x; k < 60; k += LA_THREADS) (&Fc[0][0])[k] = (&c_tab.faceCenterPoint[0][0])[k];
-    for (int k = threadIdx.x; k < 120; k += LA_THREADS) (&Fu[0][0][0])[k] = (&c_tab.fastU[res & 1][0][0][0])[k];
-    wl_init(WL);
-    const CensusSink census{cmap};
-    bool census_ok = true;
-    const int64_t tile_us = wdiv.d;
-    const uint64_t cell_hi = (UINT64_C(1) << 59) | ((uint64_t)res << 52);   // mode 1, reserved 0, resolution
-    for (int s = threadIdx.x; s < LA_SLOTS; s += LA_THREADS) {
-        S.key[s] = LA_EMPTY;
-        S.cnt[s] = 0;
-        S.ssp[s] = 0.0;
-        S.slat[s] = 0.0;
-        S.slon[s] = 0.0;
+// wave-cooperative count: lanes with pred add 1 to cnt[slot] (one LDS add per distinct slot per wave)
+__device__ __forceinline__ void wave_count_slots(bool pred, int slot, unsigned *cnt) {
+    unsigned long long pend = __ballot(pred);
+    while (pend) {
+        const int leader = __ffsll((long long)pend) - 1;
+        const int s = __shfl(slot, leader, 64);
+        const unsigned long long m = __ballot(pred && slot == s);
+        if (lane_id() == leader) atomicAdd(&cnt[s], (unsigned)__popcll(m));
+        pend &= ~m;
     }
-    for (int s = threadIdx.x; s < LA_WT; s += LA_THREADS) { S.wt[s] = EMPTY_WIN; S.wcnt[s] = 0; }
-    if (threadIdx.x == 0) { S.occ = 0; S.dskip = 0; }
+}
+
+__global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
+    const double *__restrict__ lat, const double *__restrict__ lon, const int64_t *__restrict__ ts,
+    const uint8_t *__restrict__ row_valid, const uint64_t *__restrict__ vkey, int64_t n, int res, FloorDiv wdiv,
+    int64_t late_end_us, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ keys_out, DedupSlot *dtab,
+    unsigned long long dmask, unsigned int *dused, unsigned long long *n_dused, unsigned int *__restrict__ slow,
+    unsigned long long *n_slow, unsigned long long *dgiveup, unsigned long long *wreg, unsigned long long *wcount,
+    DevStats *st) {
+    __shared__ WinCacheL WC;
+    __shared__ double Fc[20][3], Fu[20][2][3];   // the fast path's per-face tables (res parity): LDS reads
+    __shared__ unsigned dskip;                    // the fused dedup has given up (*dgiveup) -- skip it
+    for (int k = threadIdx.x; k < 60; k += IG_THREADS) (&Fc[0][0])[k] = (&c_tab.faceCenterPoint[0][0])[k];
+    for (int k = threadIdx.x; k < 120; k += IG_THREADS) (&Fu[0][0][0])[k] = (&c_tab.fastU[res & 1][0][0][0])[k];
+    wc_init(WC);
+    if (threadIdx.x == 0) dskip = 0;
     __syncthreads();
-    unsigned long long nvalid = 0, nlate = 0, bad = 0, gaps = 0;
+    const int64_t tile_us = wdiv.d;
+    unsigned long long nvalid = 0, nlate = 0, bad = 0, wover = 0;
     long long tmax = INT64_MIN;
     bool dretry = false;
-    if (DIRECT && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&st->n_partials, (unsigned long long)n);   // slot i = row i
-#ifdef HM_ABL_NOAGG
-    unsigned long long abl_sink = 0;
-#endif
-    const int64_t nchunks = (n + LA_CHUNK - 1) / LA_CHUNK;
-    for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-        for (int q = 0; q < LA_CHUNK / LA_THREADS; q++) {
-            const int64_t i = ch * LA_CHUNK + q * LA_THREADS + threadIdx.x;
-            const bool in = i < n;
-            double la = 0.0, lo = 0.0;
-            int64_t t = 0;
-            unsigned long long v = EMPTY_VKEY;
-            bool rv = true;
-            if (in) {
-                la = lat[i];
-                lo = lon[i];
-                t = ts[i];
-                v = vkey[i];
-                if (row_valid) rv = row_valid[i] != 0;
-            }
-            const bool ok = in && rv && la >= -90.0 && la <= 90.0 && lo >= -180.0 && lo <= 180.0 &&
-                            t > INT64_MIN + 2 * tile_us && t < INT64_MAX - 2 * tile_us;
-            // dedup: the vkey's home slot is loaded now, its latency hidden behind the cell computation (a plain
-            // load: a stale copy can only show the slot empty or its max lower, both of which the atomics below
-            // correct)
+    int round = 0;
+    for (int64_t base = (int64_t)blockIdx.x * IG_THREADS; base < n; base += (int64_t)gridDim.x * IG_THREADS, round++) {
+        const int64_t i = base + threadIdx.x;
+        const bool in = i < n;
+        double la = 0.0, lo = 0.0;
+        int64_t t = 0;
+        unsigned long long v = EMPTY_VKEY;
+        bool rv = true;
+        if (in) {
+            la = lat[i];
+            lo = lon[i];
+            t = ts[i];
+            v = vkey[i];
+            if (row_valid) rv = row_valid[i] != 0;
+        }
+        const bool ok = in && rv && la >= -90.0 && la <= 90.0 && lo >= -180.0 && lo <= 180.0 &&
+                        t > INT64_MIN + 2 * tile_us && t < INT64_MAX - 2 * tile_us;
+        // dedup: the vkey's home slot is loaded now, its latency hidden behind the cell computation (a plain load:
+        // a stale copy can only show the slot empty or its max lower, both of which the atomics below correct)
 #ifdef HM_ABL_NODEDUP
-            const bool dd = false;
+        const bool dd = false;
 #else
-            const bool dd = ok && v != EMPTY_VKEY && !__hip_atomic_load(&S.dskip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const bool dd = ok && v != EMPTY_VKEY && !__hip_atomic_load(&dskip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
-            const unsigned long long dh0 = vkey_hash(v) & dmask;
-            DedupSlot d0{EMPTY_VKEY, 0};
-            if (dd) d0 = dtab[dh0];
-            uint8_t fl = 0;
-            uint64_t cell = EMPTY_CELL;
-            int widx = -1;   // the window's slot in the workgroup's window table (-1: table full, rare)
-            if (ok) {
-                const int64_t wq = floor_div(t, wdiv);   // tumbling window: floor(t / tile) (Spark TimeWindowing)
-                const int64_t ws = wq * tile_us;
-                const bool late = (ws + tile_us) <= late_end_us;
-                fl = late ? (F_VALID | F_LATE) : (F_VALID | F_AGG);
-                nvalid++;
-                nlate += late;
-                tmax = t > tmax ? t : tmax;
-                if (!late) widx = la_window(S, ws, wq);   // (an exception's window stays unused: no census)
+        const unsigned long long dh0 = vkey_hash(v) & dmask;
+        DedupSlot d0{EMPTY_VKEY, 0};
+        if (dd) d0 = dtab[dh0];
+        uint8_t fl = 0;
+        int widx = -1, wslot = -1;
+        if (ok) {
+            const int64_t wq = floor_div(t, wdiv);   // tumbling window: floor(t / tile) (Spark TimeWindowing)
+            const int64_t ws = wq * tile_us;
+            const bool late = (ws + tile_us) <= late_end_us;
+            fl = late ? (F_VALID | F_LATE) : (F_VALID | F_AGG);
+            nvalid++;
+            nlate += late;
+            tmax = t > tmax ? t : tmax;
+            if (!late) {
+                widx = wc_lookup(WC, wreg, wq, wenc_of(ws), wslot);
+                if (widx < 0) { wover++; fl = F_VALID; }   // registry full: the batch fails (hm_process_batch)
             }
-            // cell of the aggregated rows; margin exceptions go to k_ingest_exact (exact path, own partial record)
-            bool exc = false;
+        }
+        // cell of the aggregated rows; margin exceptions go to k_ingest_exact (exact path), which fills their key
+        bool exc = false;
+        uint64_t cell = EMPTY_CELL;
 #ifdef HM_ABL_NOCELL   // ablation builds (tools/ablate_ingest.sh): a hash stands in for the cell
-            if (fl & F_AGG) cell = (mix64(__builtin_bit_cast(uint64_t, la) ^ mix64(__builtin_bit_cast(uint64_t, lo))) & LA_CELL_LO) | cell_hi;
+        if (fl & F_AGG) cell = mix64(__builtin_bit_cast(uint64_t, la) ^ mix64(__builtin_bit_cast(uint64_t, lo)));
 #else
-            if (fl & F_AGG) exc = !latLngToCellFastP(la, lo, res, c_tab, Fc, Fu, cell);
+        if (fl & F_AGG) exc = !latLngToCellFastP(la, lo, res, c_tab, Fc, Fu, cell);
 #endif
-            {
-                const unsigned long long pos = wave_append(exc, n_slow);
-                if (exc) slow[pos] = (unsigned int)i;
-            }
-            // dedup: per-vkey max ts over the valid rows (late rows included, as in the reference's batch frame)
-            bool claimed = false;
-            long long dh = -1;
-            bad += ok && v == EMPTY_VKEY;
-            bool cand = false;
-            if (dd) {
-                long long cur = d0.maxts;
-                if (d0.vkey == v) dh = (long long)dh0;   // the usual case: the key sits in its home slot
-                else dh = find_or_claim_vkey_ts(dtab, dmask, v, claimed, DEDUP_FUSED_PROBES, cur);
-                if (dh < 0) {
-                    if (!dretry) atomicExch(dgiveup, 1ull);
-                    dretry = true;
-                } else {
-                    // (cur may be stale, i.e. below the slot's max: a superset of the rows at the final max)
-                    cand = t >= cur || claimed;
-                    if (t > cur) atomicMax(&dtab[dh].maxts, (long long)t);
-                }
-            }
-            if (in) flags_out[i] = fl | (cand ? F_CAND : 0);
-            const unsigned long long pos = wave_append(claimed, n_dused);
-            if (claimed) dused[pos] = (unsigned int)dh;
-            bool fresh = false;
-            if constexpr (DIRECT) {
-                // Row i owns partial slot i: no reservation (one device-wide atomic per chunk on a single counter
-                // serialised this kernel at ~13 ns each, 5 ms per 1e8 events).  An aggregated row stores its
-                // record there, any other row a gap (cell 0) that the partition skips; an exception's slot is
-                // filled by k_ingest_exact.  The wave's 64 records go through LDS and out as 3 KB contiguous.
-                const bool rec = (fl & F_AGG) && !exc;
-                const int ln = lane_id();
-                uint4 *stage = (uint4 *)S.key + (threadIdx.x >> 6) * 64 * 3;   // key, cnt, ssp: 12 KB = 256 records
-                uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0, r2 = r0;
-                if (rec) {
-                    const bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
-                    const double sp = sv ? speed[i] : 0.0;
-                    const int64_t ws = widx >= 0 ? (int64_t)S.wt[widx] : floor_div(t, wdiv) * tile_us;
-                    const uint64_t spb = __builtin_bit_cast(uint64_t, sp), lab = __builtin_bit_cast(uint64_t, la),
-                                   lob = __builtin_bit_cast(uint64_t, lo);
-                    r0 = make_uint4((unsigned)cell, (unsigned)(cell >> 32), (unsigned)ws, (unsigned)((uint64_t)ws >> 32));
-                    r1 = make_uint4(1u, sv ? 1u : 0u, (unsigned)spb, (unsigned)(spb >> 32));
-                    r2 = make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32));
-                    if (widx >= 0) atomicAdd(&S.wcnt[widx], 1u);
-                    else census_ok &= wl_add(WL, census, wenc_of(ws), 1ull);
-                }
-                gaps += in && !(fl & F_AGG);
-                stage[ln * 3 + 0] = r0;
-                stage[ln * 3 + 1] = r1;
-                stage[ln * 3 + 2] = r2;
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                const int64_t i0 = i - ln;
-                const int64_t nrec3 = (n - i0 < 64 ? n - i0 : 64) * 3;
-                uint4 *__restrict__ o4 = (uint4 *)(out + i0);
-#ifndef HM_ABL_NOREC
-                for (int r = 0; r < 3; r++)
-                    if (r * 64 + ln < nrec3) o4[r * 64 + ln] = stage[r * 64 + ln];
-#endif
-                __builtin_amdgcn_wave_barrier();
+        {
+            const unsigned long long pos = wave_append(exc, n_slow);
+            if (exc) slow[pos] = (unsigned int)i;
+        }
+        // dedup: per-vkey max ts over the valid rows (late rows included, as in the reference's batch frame)
+        bool claimed = false;
+        long long dh = -1;
+        bad += ok && v == EMPTY_VKEY;
+        bool cand = false;
+        if (dd) {
+            long long cur = d0.maxts;
+            if (d0.vkey == v) dh = (long long)dh0;   // the usual case: the key sits in its home slot
+            else dh = find_or_claim_vkey_ts(dtab, dmask, v, claimed, DEDUP_FUSED_PROBES, cur);
+            if (dh < 0) {
+                if (!dretry) atomicExch(dgiveup, 1ull);
+                dretry = true;
             } else {
-            // LDS pre-aggregation of the window's rows
-#ifdef HM_ABL_NOAGG
-            if ((fl & F_AGG) && !exc) abl_sink ^= cell;
-            if (false) {
-#else
-            if ((fl & F_AGG) && !exc) {
-#endif
-                const bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
-                const double sp = sv ? speed[i] : 0.0;
-                if (widx >= 0) {
-                    const uint64_t key = la_key(cell, (unsigned)widx);
-                    unsigned h = la_slot(key);
-                    for (int probe = 0; probe < LA_SLOTS; probe++) {
-                        uint64_t k = __hip_atomic_load(&S.key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (k == key) break;
-                        if (k == LA_EMPTY) {
-                            k = atomicCAS(&S.key[h], LA_EMPTY, key);
-                            if (k == LA_EMPTY) { fresh = true; break; }
-                            if (k == key) break;
-                        }
-                        h = (h + 1) & (LA_SLOTS - 1);
-                    }
-                    atomicAdd(&S.cnt[h], 1ull | ((unsigned long long)sv << 32));
-                    if (sv) atomicAdd(&S.ssp[h], sp);
-                    atomicAdd(&S.slat[h], la);
-                    atomicAdd(&S.slon[h], lo);
-                } else {   // more than LA_WT windows since the last flush: the row is its own partial record
-                    census_ok &= la_direct(out, st, WL, census, cell, floor_div(t, wdiv) * tile_us, sv, sp, la, lo);
-                }
+                // (cur may be stale, i.e. below the slot's max: a superset of the rows at the final max)
+                cand = t >= cur || claimed;
+                if (t > cur) atomicMax(&dtab[dh].maxts, (long long)t);
             }
-            }
-            const unsigned long long fb = __ballot(fresh);
-            if (fb && lane_id() == (unsigned)(__ffsll((long long)fb) - 1)) atomicAdd(&S.occ, (unsigned)__popcll(fb));
         }
-        // poll the give-up flag now and then (its own cache line: DevStats takes every flush's atomics)
-        if (threadIdx.x == 0 && !S.dskip && ((ch / gridDim.x) & 15) == 15)
-            __hip_atomic_store(&S.dskip, __hip_atomic_load(dgiveup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ? 1u : 0u,
+        const bool agg = (fl & F_AGG) != 0;
+        if (in) {
+            flags_out[i] = fl | (cand ? F_CAND : 0);
+            keys_out[i] = agg ? ekey_make(exc ? 0 : cell, (unsigned)widx) : 0;
+        }
+        const unsigned long long pos = wave_append(claimed, n_dused);
+        if (claimed) dused[pos] = (unsigned int)dh;
+        // census: aggregated rows per window (sizes the window tables of the direct path)
+        wave_count_slots(agg && wslot >= 0, wslot, WC.cnt);
+        if (agg && wslot < 0) atomicAdd(&wcount[widx], 1ull);
+        // poll the give-up flag now and then (its own cache line)
+        if (threadIdx.x == 0 && (round & 15) == 15 && !dskip)
+            __hip_atomic_store(&dskip, __hip_atomic_load(dgiveup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ? 1u : 0u,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if constexpr (!DIRECT) {   // (direct: no block-wide state between chunks; dskip is read at the next poll)
-            __syncthreads();
-            if (S.occ > (unsigned)LA_FLUSH_AT) la_flush(S, cell_hi, out, st, WL, census, census_ok);
-        }
-    }
-    if (S.occ > 0) la_flush(S, cell_hi, out, st, WL, census, census_ok);
-    if constexpr (DIRECT) {   // the window table was never flushed: its census
-        __syncthreads();
-        if (threadIdx.x < LA_WT && S.wcnt[threadIdx.x])
-            census_ok &= wl_add(WL, census, wenc_of(S.wt[threadIdx.x]), (unsigned long long)S.wcnt[threadIdx.x]);
     }
     __syncthreads();
-    census_ok &= wl_flush(WL, census);
-#ifdef HM_ABL_NOAGG
-    if (abl_sink == 42) st->pad[0] = abl_sink;
-#endif
+    for (int q = threadIdx.x; q < WC_SLOTS; q += IG_THREADS)
+        if (WC.cnt[q]) atomicAdd(&wcount[(WC.e[q] & 0xfff) - 1], (unsigned long long)WC.cnt[q]);
     nvalid = wave_sum(nvalid);
     nlate = wave_sum(nlate);
     bad = wave_sum(bad);
-    if (DIRECT) gaps = wave_sum(gaps);
+    wover = wave_sum(wover);
     tmax = wave_max(tmax);
     const unsigned long long rt = __ballot(dretry);
-    const unsigned long long cbad = __ballot(!census_ok);
     if (lane_id() == 0) {
         if (nvalid) atomicAdd(&st->n_valid, nvalid);
         if (nlate) atomicAdd(&st->n_late, nlate);
         if (tmax != INT64_MIN) atomicMax(&st->max_ts_ms, (long long)(tmax / 1000));   // trunc(max) = max(trunc)
         if (bad) atomicAdd(&st->bad_vkey, bad);
-        if (gaps) atomicAdd(&st->n_gaps, gaps);
+        if (wover) atomicAdd(&st->win_overflow, wover);
         if (rt) atomicAdd(&st->dedup_retry, 1ull);
-        if (cbad) atomicAdd(&st->overflow, 1ull);
     }
 }
 
-// exceptions of k_ingest's fast path: upstream's exact sequence, one partial record per event (direct: into the
-// row's own slot, else appended)
-__global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__ lat, const double *__restrict__ lon,
-                                                      const int64_t *__restrict__ ts, const double *__restrict__ speed,
-                                                      const uint8_t *__restrict__ speed_valid, int res, int64_t tile_us,
+// exceptions of k_ingest's fast path: upstream's exact sequence; the cell bits go into the row's key (k_ingest
+// wrote its window slot)
+__global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__ lat, const double *__restrict__ lon, int res,
                                                       const unsigned int *__restrict__ slow, const unsigned long long *n_slow,
-                                                      bool direct, TilePartial *__restrict__ out, WinCount *cmap, DevStats *st) {
-    __shared__ WinLds WL;
-    wl_init(WL);
-    __syncthreads();
-    const CensusSink census{cmap};
-    bool ok = true;
+                                                      uint64_t *__restrict__ keys) {
     const int64_t m = (int64_t)*n_slow;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < m; base += stride) {
-        const int64_t q = base + threadIdx.x;
-        const bool in = q < m;
-        TilePartial p;
-        if (in) {
-            const unsigned i = slow[q];
-            const int64_t t = ts[i];
-            int64_t rem = t % tile_us;
-            if (rem < 0) rem += tile_us;
-            const bool sv = speed ? (speed_valid ? speed_valid[i] != 0 : true) : false;
-            p.cell = latLngToCellDeg(lat[i], lon[i], res, c_tab);
-            p.wstart = t - rem;
-            p.count = 1;
-            p.nspeed = sv;
-            p.sspeed = sv ? speed[i] : 0.0;
-            p.slat = lat[i];
-            p.slon = lon[i];
-        }
-        const unsigned long long pos = direct ? (in ? slow[q] : 0ull) : wave_append(in, &st->n_partials);
-        if (in) out[pos] = p;
-        ok &= wave_count_windows(in, in ? wenc_of(p.wstart) : 0ull, 1ull, WL, census);
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (int64_t)gridDim.x * blockDim.x) {
+        const unsigned i = slow[q];
+        keys[i] |= latLngToCellDeg(lat[i], lon[i], res, c_tab) & CELL_LO;
     }
-    __syncthreads();
-    ok &= wl_flush(WL, census);
-    if (__ballot(!ok) && lane_id() == 0) atomicAdd(&st->overflow, 1ull);
 }
 
 // =====================================================================================================
@@ -1711,10 +1989,20 @@ struct hm_ctx {
     DedupTable *dlast = nullptr;   // the table the last batch's flags were computed on
     int64_t dedup_seen = 0;
     int64_t n_partials_merged = 0;   // partial records of the last merge (hm_batch_out.n_partials)
-    int ingest_grid[2] = {0, 0};     // k_ingest<DIRECT>'s persistent grid: resident workgroups per CU x CUs
-    int ingest_mode = 0;             // 0 adaptive, 1 direct, 2 LDS pre-aggregation
-    double agg_ratio = 0.0;          // partials / aggregated rows of the last batch (adaptive mode)
-    bool last_direct = false;
+    int ingest_grid = 0;             // k_ingest's persistent grid: resident workgroups per CU x CUs
+    int n_cus = 0;
+    // aggregation path: direct (event records -> partition -> merge) or table (k_agg + k_bin_reduce, low
+    // cardinality); MOBHEAT_INGEST_MODE pins one (0 adaptive, 1 direct, 2 table)
+    int ingest_mode = 0;
+    int64_t prev_agg_rows = 0, prev_keys = 0;   // aggregated rows and distinct keys of the last batch
+    bool last_table = false;
+    DevBuf keys;                     // k_ingest's event key per row (kernels.h ekey)
+    unsigned long long *d_wreg = nullptr, *h_wreg = nullptr;     // the batch's window registry (WREG_SLOTS wenc)
+    unsigned long long *d_wcount = nullptr, *h_wcount = nullptr; // aggregated rows per registry slot (census)
+    WInfo *d_winfo = nullptr, *h_winfo = nullptr;   // per registry slot: window parameters of the direct path
+    DevBuf agg_bucket, agg_cursor;   // table mode: k_agg's buckets (AG_BINS x AG_SUB x cap AggRecs) + fill cursors
+    unsigned agg_cap = 0;            // AggRecs per sub-bucket
+    std::vector<unsigned long long> h_agg_cursor;
     // outputs (device + pinned host)
     DevBuf o_cell, o_ws, o_cnt, o_sp, o_spn, o_lon, o_lat;
     void *h_cell = nullptr, *h_ws = nullptr, *h_cnt = nullptr, *h_sp = nullptr, *h_spn = nullptr, *h_lon = nullptr,
@@ -1742,6 +2030,7 @@ struct hm_ctx {
     int stage = 0;
     int nranks = 1, rank = 0;
     int64_t stage_n_in = 0;
+    int64_t stage_agg_rows = 0;
     hm_stage_sizes stage_sizes{};
 };
 
@@ -1920,32 +2209,70 @@ static int gens_upload(hm_ctx *ctx) {
     return HM_OK;
 }
 
-// radix partition of n partial records into RP_BINS bins (one per (window, region)); the sorted copy goes to
-// ctx->parts_sorted, bin b starts at rp_O[b * ntiles]
-// In -> Out: TilePartial -> SortedRec (a batch's partials, into parts_sorted), GrowRec -> GrowRec (growth, into
-// parts_sorted), TilePartial -> TilePartial (the owner partition, into the caller's send buffer)
-template <typename In, typename Out>
-static int partition(hm_ctx *ctx, const In *parts, int64_t n, int64_t &ntiles, int nranks = 0, Out *dst = nullptr) {
-    const int nbins = nranks > 0 ? nranks : RP_BINS;
-    if (n >= (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "%lld partial records in one merge exceed 2^32-2", (long long)n);
-    ntiles = std::max<int64_t>((n + RP_TILE - 1) / RP_TILE, 1);
-    const int64_t m = (int64_t)(nbins + 1) * ntiles;   // digit nbins: gaps (cell 0), which the scatter drops
+struct Inputs {   // a batch's device columns
+    const double *lat, *lon, *sp;
+    const int64_t *ts;
+    const uint8_t *sv, *rv;
+    const uint64_t *vk;
+    int64_t n;
+};
+
+// exclusive scan of the m = (nbins + 1) x ntiles tile histogram rp_H into rp_O (digit-major)
+static int rp_scan(hm_ctx *ctx, int64_t m) {
     const int64_t nb = (m + SC_PER - 1) / SC_PER;
     int rc;
-    if (!dst && (rc = ensure(ctx, ctx->parts_sorted, std::max<int64_t>(n, 1) * sizeof(Out)))) return rc;
-    if ((rc = ensure(ctx, ctx->rp_H, m * 4)) || (rc = ensure(ctx, ctx->rp_O, m * 8)) || (rc = ensure(ctx, ctx->rp_btot, nb * 4)) ||
-        (rc = ensure(ctx, ctx->rp_boff, nb * 8)))
-        return rc;
-    hipLaunchKernelGGL(k_rp_hist<In>, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, (const GenDesc *)ctx->d_gmap,
-                       (const GenDesc *)ctx->d_glist, ctx->n_glist, nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles, ctx->d_st);
+    if ((rc = ensure(ctx, ctx->rp_btot, nb * 4)) || (rc = ensure(ctx, ctx->rp_boff, nb * 8))) return rc;
     hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_H.p, m,
                        (unsigned long long *)ctx->rp_O.p, (unsigned *)ctx->rp_btot.p);
     hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_btot.p, nb,
                        (unsigned long long *)ctx->rp_boff.p, ctx->d_scratch + 254);
     hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, (unsigned long long *)ctx->rp_O.p, m,
                        (const unsigned long long *)ctx->rp_boff.p);
-    hipLaunchKernelGGL((k_rp_scatter<In, Out>), dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n,
+    return HM_OK;
+}
+
+// radix partition of n partial records into RP_BINS bins (one per (window, region)); the sorted copy goes to
+// ctx->parts_sorted, bin b starts at rp_O[b * ntiles]
+// In -> Out: TilePartial -> SortedRec (table mode / stage merge, into parts_sorted), GrowRec -> GrowRec (growth, into
+// parts_sorted), TilePartial -> TilePartial (the owner partition, into the caller's send buffer)
+template <typename In, typename Out>
+static int partition(hm_ctx *ctx, const In *parts, int64_t n, int64_t &ntiles, int nranks = 0, Out *dst = nullptr) {
+    const int nbins = nranks > 0 ? nranks : RP_BINS;
+    if (n >= (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "%lld partial records in one merge exceed 2^32-2", (long long)n);
+    const int64_t tile = rp_tile_for(n);
+    ntiles = std::max<int64_t>((n + tile - 1) / tile, 1);
+    const int64_t m = (int64_t)(nbins + 1) * ntiles;   // digit nbins: gaps (cell 0), which the scatter drops
+    int rc;
+    if (!dst && (rc = ensure(ctx, ctx->parts_sorted, std::max<int64_t>(n, 1) * sizeof(Out)))) return rc;
+    if ((rc = ensure(ctx, ctx->rp_H, m * 4)) || (rc = ensure(ctx, ctx->rp_O, m * 8))) return rc;
+    hipLaunchKernelGGL(k_rp_hist<In>, dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, tile, (const GenDesc *)ctx->d_gmap,
+                       (const GenDesc *)ctx->d_glist, ctx->n_glist, nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles, ctx->d_st);
+    if ((rc = rp_scan(ctx, m))) return rc;
+    hipLaunchKernelGGL((k_rp_scatter<In, Out>), dim3(ntiles), dim3(RP_THREADS), 0, ctx->stream, parts, n, tile,
                        (const GenDesc *)ctx->d_gmap, (const GenDesc *)ctx->d_glist, ctx->n_glist, nranks, nbins,
+                       (const unsigned long long *)ctx->rp_O.p, ntiles, dst ? dst : (Out *)ctx->parts_sorted.p);
+    HIPCHK(ctx, hipGetLastError());
+    return HM_OK;
+}
+
+// the direct path's partition: the batch's n event keys -> EventRecs in (window, region) bins (parts_sorted), or
+// with nranks > 0 TilePartials grouped by owner rank into dst; rows without a key fall into digit nbins (dropped)
+template <typename Out>
+static int ev_partition(hm_ctx *ctx, const Inputs &I, int64_t &ntiles, int nranks = 0, Out *dst = nullptr) {
+    const int nbins = nranks > 0 ? nranks : RP_BINS;
+    const int64_t n = I.n;
+    const int64_t tile = rp_tile_for(n);
+    ntiles = std::max<int64_t>((n + tile - 1) / tile, 1);
+    const int64_t m = (int64_t)(nbins + 1) * ntiles;
+    int rc;
+    if (!dst && (rc = ensure(ctx, ctx->parts_sorted, std::max<int64_t>(n, 1) * sizeof(Out)))) return rc;
+    if ((rc = ensure(ctx, ctx->rp_H, m * 4)) || (rc = ensure(ctx, ctx->rp_O, m * 8))) return rc;
+    const uint64_t ch = cell_hi_of(ctx->cfg.h3_res);
+    hipLaunchKernelGGL(k_ev_hist, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, (const uint64_t *)ctx->keys.p, n, tile,
+                       (const WInfo *)ctx->d_winfo, ch, nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles);
+    if ((rc = rp_scan(ctx, m))) return rc;
+    hipLaunchKernelGGL(k_ev_scatter<Out>, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, (const uint64_t *)ctx->keys.p, n, tile,
+                       I.sp, I.sv, I.lat, I.lon, (const WInfo *)ctx->d_winfo, ch, nranks, nbins,
                        (const unsigned long long *)ctx->rp_O.p, ntiles, dst ? dst : (Out *)ctx->parts_sorted.p);
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
@@ -1962,31 +2289,31 @@ static RowsOut staged_rows(hm_ctx *ctx) {
 // the batch sequence number kept in the slots' touched words (32 bits, never 0: fresh slots hold 0)
 static unsigned seq32(const hm_ctx *ctx) { return (unsigned)(ctx->seq % 0xffffffffull) + 1u; }
 
+// merge the partitioned records (ctx->parts_sorted) of n_rows staging rows
 template <typename Rec>
-static int merge_sorted(hm_ctx *ctx, int64_t n, int64_t ntiles) {
+static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles) {
     constexpr bool rehash = std::is_same<Rec, GrowRec>::value;
     int rc;
     if ((rc = ensure(ctx, ctx->bin_cnt, RP_BINS * 4)) || (rc = ensure(ctx, ctx->bin_off, RP_BINS * 8)))
         return rc;
     if (!rehash) {
-        const int64_t m = std::max<int64_t>(n, 1);
+        const int64_t m = std::max<int64_t>(n_rows, 1);
         if ((rc = ensure(ctx, ctx->s_cell, m * 8)) || (rc = ensure(ctx, ctx->s_ws, m * 8)) || (rc = ensure(ctx, ctx->s_cnt, m * 8)) ||
             (rc = ensure(ctx, ctx->s_sp, m * 8)) || (rc = ensure(ctx, ctx->s_spn, m)) || (rc = ensure(ctx, ctx->s_lon, m * 8)) ||
             (rc = ensure(ctx, ctx->s_lat, m * 8)))
             return rc;
     }
-    hipLaunchKernelGGL(k_merge_owned<Rec>, dim3(RP_BINS), dim3(MO_THREADS), 0, ctx->stream, (const Rec *)ctx->parts_sorted.p, n,
+    hipLaunchKernelGGL(k_merge_owned<Rec>, dim3(RP_BINS), dim3(MO_THREADS), 0, ctx->stream, (const Rec *)ctx->parts_sorted.p, n_rows,
                        (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
-                       ctx->n_glist, seq32(ctx), staged_rows(ctx), (unsigned *)ctx->bin_cnt.p, ctx->d_st);
+                       ctx->n_glist, (const WInfo *)ctx->d_winfo, cell_hi_of(ctx->cfg.h3_res), seq32(ctx), staged_rows(ctx),
+                       (unsigned *)ctx->bin_cnt.p, ctx->d_st);
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
 }
 
-// Census of the batch's partials per window; give every window a table large enough for its keys after this
-// batch (new windows: a new table; windows that would pass load 1/2: a larger table, filled by dumping the
-// old one and merging the dump in rehash mode); upload the window map.
-static int gens_prepare(hm_ctx *ctx, const TilePartial *parts, int64_t n) {
-    if (!ctx->census_ready) {   // partials from other ranks (stage API): count them here
+// census of partial records per window (the stage merge's received partials; table mode counts its own)
+static int census_of_partials(hm_ctx *ctx, const TilePartial *parts, int64_t n, std::vector<WinCount> &census) {
+    if (!ctx->census_ready) {
         HIPCHK(ctx, hipMemsetAsync(ctx->d_cmap, 0, GMAP_SLOTS * sizeof(WinCount), ctx->stream));
         hipLaunchKernelGGL(k_census, dim3(grid_for(n, 256, 256 * 8)), dim3(256), 0, ctx->stream, parts, n, ctx->d_cmap, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
@@ -1996,12 +2323,58 @@ static int gens_prepare(hm_ctx *ctx, const TilePartial *parts, int64_t n) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "more than %d windows in one batch", GMAP_SLOTS);
+    census.clear();
+    for (int q = 0; q < GMAP_SLOTS; q++)
+        if (ctx->h_cmap[q].wenc) census.push_back(ctx->h_cmap[q]);
+    return HM_OK;
+}
+// census of the direct path: the registry's windows and their aggregated rows (h_wreg / h_wcount, read back after
+// k_ingest)
+static void census_of_registry(const hm_ctx *ctx, std::vector<WinCount> &census) {
+    census.clear();
+    for (int w = 0; w < WREG_SLOTS; w++)
+        if (ctx->h_wreg[w] && ctx->h_wcount[w]) census.push_back(WinCount{ctx->h_wreg[w], ctx->h_wcount[w]});
+}
+
+// WInfo of every registry slot in use (after gens_prepare when with_bins: the radix bin parameters need the
+// window's table geometry)
+static int winfo_upload(hm_ctx *ctx, bool with_bins) {
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));   // (h_winfo is reused: the previous upload must be done)
+    WInfo *h = ctx->h_winfo;
+    int lo = WREG_SLOTS, hi = -1;
+    for (int w = 0; w < WREG_SLOTS; w++) {
+        const unsigned long long we = ctx->h_wreg[w];
+        if (!we) continue;
+        WInfo &x = h[w];
+        memset(&x, 0, sizeof x);
+        x.wenc = we;
+        x.inner = window_inner(wdec(we));
+        if (with_bins) {
+            unsigned rbits = 0;
+            bool found = false;
+            for (const auto &g : ctx->gens)
+                if (g.wenc == we) { rbits = g.rbits; found = true; break; }
+            if (!found) return set_err(ctx, HM_E_STATE, "window without a state table");
+            const unsigned sb = REGION_BITS - rbits;
+            x.binp = (sb << 24) | (window_salt(we) & ((1u << sb) - 1));
+        }
+        lo = std::min(lo, w);
+        hi = std::max(hi, w);
+    }
+    if (hi >= lo)
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_winfo + lo, h + lo, (size_t)(hi - lo + 1) * sizeof(WInfo), hipMemcpyHostToDevice,
+                                   ctx->stream));
+    return HM_OK;
+}
+
+// Give every window of the census a table large enough for its keys after this batch (new windows: a new table;
+// windows that would pass load 1/2: a larger table, filled by dumping the old one and merging the dump in rehash
+// mode); upload the window map.
+static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census) {
     std::vector<hm_ctx::Gen> old;   // tables being replaced by larger ones
     int rc;
     for (auto &g : ctx->gens) g.batch_parts = 0;
-    for (int q = 0; q < GMAP_SLOTS; q++) {
-        const WinCount &w = ctx->h_cmap[q];
-        if (!w.wenc) continue;
+    for (const WinCount &w : census) {
         ctx->batch_windows.push_back(wdec(w.wenc));
         const int64_t c = (int64_t)w.count;
         auto it = std::find_if(ctx->gens.begin(), ctx->gens.end(), [&](const hm_ctx::Gen &g) { return g.wenc == w.wenc; });
@@ -2160,46 +2533,94 @@ static int ensure_host(hm_ctx *ctx, void **p, size_t &cap_el, size_t want_el, si
 }
 
 // ---- batch phases shared by the single-GPU and stage paths ----
-struct Inputs {
-    const double *lat, *lon, *sp;
-    const int64_t *ts;
-    const uint8_t *sv, *rv;
-    const uint64_t *vk;
-    int64_t n;
-};
-
+// k_ingest + k_ingest_exact: flags, event keys, the window registry and its census, dedup max, batch statistics
 static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
     int64_t n = I.n;
     int rc;
     if ((rc = ensure(ctx, ctx->flags, n)) || (rc = ensure(ctx, ctx->win, n)) || (rc = ensure(ctx, ctx->rows, n * 8)) ||
-        (rc = ensure(ctx, ctx->partials, n * sizeof(TilePartial))) || (rc = ensure(ctx, ctx->slow, n * sizeof(unsigned int))))
+        (rc = ensure(ctx, ctx->keys, n * 8)) || (rc = ensure(ctx, ctx->slow, n * sizeof(unsigned int))))
         return rc;
     if ((rc = dedup_prepare(ctx, ctx->dfused, dedup_fused_keys(ctx, n), true))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_st, 0, sizeof(DevStats), ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + SLOW_WORD, 0, 8, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + GIVEUP_WORD, 0, 8, ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(ctx->d_cmap, 0, GMAP_SLOTS * sizeof(WinCount), ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_wreg, 0, (WREG_SLOTS + 1) * 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_wcount, 0, (WREG_SLOTS + 1) * 8, ctx->stream));
     long long init[2] = {INT64_MIN, INT64_MAX};
     HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->max_ts_ms, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
     if (n > 0) {
-        int64_t nchunks = (n + LA_CHUNK - 1) / LA_CHUNK;
-        const bool direct = ctx->ingest_mode == 1 || (ctx->ingest_mode == 0 && ctx->agg_ratio > 0.8);
-        ctx->last_direct = direct;
-        int blocks = (int)std::min<int64_t>(nchunks, ctx->ingest_grid[direct]);
-        hipLaunchKernelGGL(direct ? k_ingest<true> : k_ingest<false>, dim3(blocks), dim3(LA_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.sp, I.sv, I.vk,
-                           n, ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
-                           (TilePartial *)ctx->partials.p, ctx->dfused.tab, ctx->dfused.cap - 1,
-                           (unsigned int *)ctx->dfused.used.p, ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
-                           ctx->d_scratch + GIVEUP_WORD, ctx->d_cmap, ctx->d_st);
-        hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, I.ts, I.sp, I.sv,
-                           ctx->cfg.h3_res, ctx->cfg.tile_us, (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
-                           direct, (TilePartial *)ctx->partials.p, ctx->d_cmap, ctx->d_st);
+        const int blocks = (int)std::min<int64_t>((n + IG_THREADS - 1) / IG_THREADS, ctx->ingest_grid);
+        hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(IG_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.vk, n,
+                           ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
+                           (uint64_t *)ctx->keys.p, ctx->dfused.tab, ctx->dfused.cap - 1, (unsigned int *)ctx->dfused.used.p,
+                           ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
+                           ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st);
+        hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, ctx->cfg.h3_res,
+                           (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, (uint64_t *)ctx->keys.p);
         HIPCHK(ctx, hipGetLastError());
         ctx->dfused.dirty = true;
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
-    HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    // the batch statistics and the registry with its census, read back together
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_wreg, ctx->d_wreg, WREG_SLOTS * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_wcount, ctx->d_wcount, WREG_SLOTS * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->h_st->win_overflow)
+        return set_err(ctx, HM_E_OVERFLOW, "more than %d distinct windows in one micro-batch (%llu rows)", WREG_SLOTS,
+                       ctx->h_st->win_overflow);
+    return HM_OK;
+}
+
+// Aggregation path of the batch: table mode when the last batches had few distinct keys that repeat a lot (their
+// aggregates fit k_bin_reduce's LDS tables), else the direct path.
+static bool choose_table(const hm_ctx *ctx, int64_t n_agg) {
+    if (ctx->ingest_mode) return ctx->ingest_mode == 2;
+    return n_agg >= (int64_t(1) << 16) && ctx->prev_keys > 0 && ctx->prev_keys <= (int64_t)AG_BINS * (AG_SLOTS / 2) &&
+           ctx->prev_agg_rows >= 8 * ctx->prev_keys;
+}
+
+// table mode: k_agg + k_bin_reduce -> one partial record per key of the batch (ctx->partials, count *n_parts),
+// census in d_cmap
+static int phase_table(hm_ctx *ctx, const Inputs &I, int64_t n_agg, int64_t *n_parts) {
+    int rc;
+    const int64_t n = I.n;
+    if ((rc = ensure(ctx, ctx->partials, std::max<int64_t>(n_agg, 1) * sizeof(TilePartial)))) return rc;
+    const int nsub = AG_BINS * AG_SUB;
+    if (ctx->agg_cap == 0)   // first table batch: room for about a quarter of the rows evicted twice over
+        ctx->agg_cap = (unsigned)std::min<int64_t>(std::max<int64_t>(4096, n_agg / (2 * nsub)), int64_t(1) << 30);
+    if ((rc = ensure(ctx, ctx->agg_bucket, (size_t)nsub * ctx->agg_cap * sizeof(AggRec))) ||
+        (rc = ensure(ctx, ctx->agg_cursor, (size_t)nsub * 8)))
+        return rc;
+    HIPCHK(ctx, hipMemsetAsync(ctx->agg_cursor.p, 0, (size_t)nsub * 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_cmap, 0, GMAP_SLOTS * sizeof(WinCount), ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_partials, 0, 8, ctx->stream));
+    if (n > 0) {
+        const int64_t per = (n + ctx->n_cus - 1) / ctx->n_cus;
+        const int64_t span = std::max<int64_t>((per + AG_THREADS - 1) / AG_THREADS, 1) * AG_THREADS;
+        const uint64_t ch = cell_hi_of(ctx->cfg.h3_res);
+        hipLaunchKernelGGL(k_agg, dim3((unsigned)((n + span - 1) / span)), dim3(AG_THREADS), 0, ctx->stream,
+                           (const uint64_t *)ctx->keys.p, n, span, I.sp, I.sv, I.lat, I.lon, (AggRec *)ctx->agg_bucket.p,
+                           (unsigned long long *)ctx->agg_cursor.p, ctx->agg_cap, (const unsigned long long *)ctx->d_wreg, ch,
+                           (TilePartial *)ctx->partials.p, ctx->d_cmap, ctx->d_st);
+        hipLaunchKernelGGL(k_bin_reduce, dim3(AG_BINS), dim3(AG_THREADS), 0, ctx->stream, (const AggRec *)ctx->agg_bucket.p,
+                           (const unsigned long long *)ctx->agg_cursor.p, ctx->agg_cap, (const unsigned long long *)ctx->d_wreg,
+                           ch, (TilePartial *)ctx->partials.p, ctx->d_cmap, ctx->d_st);
+        HIPCHK(ctx, hipGetLastError());
+    }
+    ctx->h_agg_cursor.resize(nsub);
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_agg_cursor.data(), ctx->agg_cursor.p, (size_t)nsub * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "more than %d windows in one batch", GMAP_SLOTS);
+    *n_parts = (int64_t)ctx->h_st->n_partials;
+    // the next table batch's sub-bucket capacity: twice this batch's fullest one (shrinks slowly)
+    unsigned long long mx = 0;
+    for (unsigned long long c : ctx->h_agg_cursor) mx = std::max(mx, c);
+    const unsigned want = (unsigned)std::min<unsigned long long>(std::max<unsigned long long>(4096, 2 * mx), 1ull << 30);
+    if (want > ctx->agg_cap || want < ctx->agg_cap / 4) ctx->agg_cap = want;
+    ctx->census_ready = true;
     return HM_OK;
 }
 
@@ -2231,13 +2652,6 @@ static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t 
     return HM_OK;
 }
 
-// partials per aggregated row of the batch just ingested (picks the next batch's k_ingest mode); only batches
-// with enough rows to tell
-static void note_agg_ratio(hm_ctx *ctx, const DevStats &s) {
-    const int64_t agg = (int64_t)s.n_valid - (int64_t)s.n_late;
-    if (agg >= (int64_t)1 << 16) ctx->agg_ratio = (double)(s.n_partials - s.n_gaps) / (double)agg;
-}
-
 static int ensure_outputs(hm_ctx *ctx, int64_t n_rows) {
     int rc;
     int64_t m = std::max<int64_t>(n_rows, 1);
@@ -2248,31 +2662,11 @@ static int ensure_outputs(hm_ctx *ctx, int64_t n_rows) {
     return HM_OK;
 }
 
-// parts[0, n_parts) holds n_parts - n_gaps records (and n_gaps gaps: cell 0, direct k_ingest)
-static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts, int64_t n_gaps) {
+// densify the merge's per-bin row segments into the output rows (k_gap_counts / k_fill_gaps, then a buffer swap)
+static int rows_densify(hm_ctx *ctx, int64_t ntiles) {
     int rc;
-    ctx->n_partials_merged = n_parts - n_gaps;
-    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_touched, 0, 8, ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_state_new, 0, 8, ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
-    ctx->seq++;
-    ctx->batch_windows.clear();
-    if ((rc = ensure_outputs(ctx, n_parts))) return rc;
-    if (n_parts == n_gaps) {
-        for (int e : {3, 7, 4, 5}) HIPCHK(ctx, hipEventRecord(ctx->ev[e], ctx->stream));
-        return HM_OK;
-    }
-    // census + window tables (host), then the partition into (window, region) bins (timed from here)
-    if ((rc = gens_prepare(ctx, parts, n_parts))) return rc;
-    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
-    int64_t ntiles;
-    if ((rc = partition<TilePartial, SortedRec>(ctx, parts, n_parts, ntiles))) return rc;
-    HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
-    if ((rc = merge_sorted<SortedRec>(ctx, n_parts, ntiles))) return rc;
-    HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
     hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->bin_cnt.p, (int64_t)RP_BINS,
                        (unsigned long long *)ctx->bin_off.p, &ctx->d_st->n_touched);
-    // densify the staged segments in place (k_gap_counts / k_fill_gaps); they become the outputs (buffer swap)
     if ((rc = ensure(ctx, ctx->gapbuf, (size_t)RP_BINS * 24))) return rc;
     unsigned *gg = (unsigned *)ctx->gapbuf.p, *gv = gg + RP_BINS;
     unsigned long long *gvo = (unsigned long long *)(gv + RP_BINS), *ggo = (unsigned long long *)ctx->bin_off.p;
@@ -2292,6 +2686,58 @@ static int phase_merge_emit(hm_ctx *ctx, const TilePartial *parts, int64_t n_par
     std::swap(ctx->s_spn, ctx->o_spn);
     std::swap(ctx->s_lon, ctx->o_lon);
     std::swap(ctx->s_lat, ctx->o_lat);
+    return HM_OK;
+}
+
+static int merge_begin(hm_ctx *ctx, int64_t n_rows) {
+    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_touched, 0, 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_state_new, 0, 8, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
+    ctx->seq++;
+    ctx->batch_windows.clear();
+    return ensure_outputs(ctx, n_rows);
+}
+static int merge_nothing(hm_ctx *ctx) {
+    for (int e : {3, 7, 4, 5}) HIPCHK(ctx, hipEventRecord(ctx->ev[e], ctx->stream));
+    return HM_OK;
+}
+
+// partial records parts[0, n_parts) (table mode, stage merge): census -> window tables -> partition -> merge -> rows
+static int merge_partials(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts) {
+    int rc;
+    ctx->n_partials_merged = n_parts;
+    if ((rc = merge_begin(ctx, n_parts))) return rc;
+    if (n_parts == 0) { ctx->census_ready = false; return merge_nothing(ctx); }
+    std::vector<WinCount> census;
+    if ((rc = census_of_partials(ctx, parts, n_parts, census)) || (rc = gens_prepare(ctx, census))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    int64_t ntiles;
+    if ((rc = partition<TilePartial, SortedRec>(ctx, parts, n_parts, ntiles))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
+    if ((rc = merge_sorted<SortedRec>(ctx, n_parts, ntiles))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+    if ((rc = rows_densify(ctx, ntiles))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+    return HM_OK;
+}
+
+// the direct path: the batch's event keys (k_ingest) -> census from the registry -> window tables -> event partition
+// -> merge -> rows.  n_rec = aggregated rows (keys != 0)
+static int merge_events(hm_ctx *ctx, const Inputs &I, int64_t n_rec) {
+    int rc;
+    ctx->n_partials_merged = n_rec;
+    if ((rc = merge_begin(ctx, I.n))) return rc;
+    if (n_rec == 0) return merge_nothing(ctx);
+    std::vector<WinCount> census;
+    census_of_registry(ctx, census);
+    if ((rc = gens_prepare(ctx, census)) || (rc = winfo_upload(ctx, true))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    int64_t ntiles;
+    if ((rc = ev_partition<EventRec>(ctx, I, ntiles))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
+    if ((rc = merge_sorted<EventRec>(ctx, I.n, ntiles))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+    if ((rc = rows_densify(ctx, ntiles))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
     return HM_OK;
 }
@@ -2384,6 +2830,7 @@ static void record_timings(hm_ctx *ctx) {
     ctx->timings[5] = el(0, 6);
     ctx->timings[2] = el(7, 4);   // merge proper
     ctx->timings[6] = el(3, 7);   // partition by table region
+    (void)hipGetLastError();      // (an event a path did not record: its timing reads -1, no sticky error)
 }
 
 extern "C" {
@@ -2395,7 +2842,9 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     if (!cfg || !out) { g_create_err = "null argument"; return HM_E_INVALID; }
     if (cfg->abi_version != HM_ABI_VERSION) { g_create_err = "ABI version mismatch"; return HM_E_INVALID; }
     if (cfg->h3_res < 0 || cfg->h3_res > 15) { g_create_err = "h3_res out of range"; return HM_E_INVALID; }
-    if (cfg->tile_us <= 0 || cfg->watermark_delay_ms < 0) { g_create_err = "bad tile/watermark"; return HM_E_INVALID; }
+    // (windows of at least a second: TILE_MINUTES is whole minutes in the reference, heatmap_stream.py:29; the
+    // window registry's LDS cache relies on |ts / tile_us| < 2^51)
+    if (cfg->tile_us < 1000000 || cfg->watermark_delay_ms < 0) { g_create_err = "bad tile/watermark"; return HM_E_INVALID; }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         (void)hipGetLastError();
@@ -2417,10 +2866,9 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     H3Tables T = make_tables();
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &T, sizeof(T)) != hipSuccess) { ctx->err = "tables"; return fail("create"); }
-    for (int direct = 0; direct < 2; direct++) {
-        const void *kern = direct ? (const void *)k_ingest<true> : (const void *)k_ingest<false>;
+    {
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, LA_THREADS, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_ingest, IG_THREADS, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) {
             ctx->err = "occupancy query";
             return fail("create");
@@ -2429,14 +2877,24 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         // boundaries: SGPR counts 81-112); k_ingest is persistent, so an extra block per CU would only run once
         // a resident one finished.  Bound it by the LDS each block takes.
         hipFuncAttributes fa{};
-        if (hipFuncGetAttributes(&fa, kern) == hipSuccess && fa.sharedSizeBytes > 0)
+        if (hipFuncGetAttributes(&fa, (const void *)k_ingest) == hipSuccess && fa.sharedSizeBytes > 0)
             per_cu = std::min<int>(per_cu, (int)(163840 / fa.sharedSizeBytes));
         if (getenv("MOBHEAT_DEBUG"))
-            fprintf(stderr, "mobheat: k_ingest<%d> %d blocks/CU x %d CUs (LDS %zu B)\n", direct, per_cu, cus, fa.sharedSizeBytes);
-        ctx->ingest_grid[direct] = std::max(1, per_cu) * std::max(1, cus);
+            fprintf(stderr, "mobheat: k_ingest %d blocks/CU x %d CUs (LDS %zu B)\n", per_cu, cus, fa.sharedSizeBytes);
+        ctx->ingest_grid = std::max(1, per_cu) * std::max(1, cus);
+        ctx->n_cus = std::max(1, cus);
     }
-    // MOBHEAT_INGEST_MODE=lds|direct pins k_ingest's partial aggregation (tests); default: adaptive
-    if (const char *m = getenv("MOBHEAT_INGEST_MODE")) ctx->ingest_mode = !strcmp(m, "direct") ? 1 : !strcmp(m, "lds") ? 2 : 0;
+    // MOBHEAT_INGEST_MODE=direct|table pins the aggregation path (tests); default: adaptive
+    if (const char *m = getenv("MOBHEAT_INGEST_MODE")) ctx->ingest_mode = !strcmp(m, "direct") ? 1 : !strcmp(m, "table") ? 2 : 0;
+    if (hipMalloc(&ctx->d_wreg, (WREG_SLOTS + 1) * 8) != hipSuccess || hipMalloc(&ctx->d_wcount, (WREG_SLOTS + 1) * 8) != hipSuccess ||
+        hipHostMalloc(&ctx->h_wreg, (WREG_SLOTS + 1) * 8, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(&ctx->h_wcount, (WREG_SLOTS + 1) * 8, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&ctx->d_winfo, (WREG_SLOTS + 1) * sizeof(WInfo)) != hipSuccess ||
+        hipHostMalloc(&ctx->h_winfo, (WREG_SLOTS + 1) * sizeof(WInfo), hipHostMallocDefault) != hipSuccess ||
+        hipMemset(ctx->d_winfo, 0, (WREG_SLOTS + 1) * sizeof(WInfo)) != hipSuccess) {
+        ctx->err = "window registry alloc";
+        return fail("create");
+    }
     if (hipMalloc(&ctx->d_st, sizeof(DevStats)) != hipSuccess || hipHostMalloc(&ctx->h_st, sizeof(DevStats)) != hipSuccess ||
         hipMalloc(&ctx->d_scratch, 256 * 8) != hipSuccess || hipHostMalloc(&ctx->h_scratch, 256 * 8) != hipSuccess) {
         ctx->err = "stats alloc";
@@ -2460,9 +2918,10 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     if (cfg->batch_capacity_hint > 0) {
         const int64_t n = cfg->batch_capacity_hint;
         const size_t tp = sizeof(TilePartial);
+        (void)tp;
         if (ensure(ctx, ctx->flags, n) || ensure(ctx, ctx->win, n) || ensure(ctx, ctx->rows, n * 8) ||
-            ensure(ctx, ctx->partials, n * tp) || ensure(ctx, ctx->slow, n * 4) ||
-            ensure(ctx, ctx->parts_sorted, n * sizeof(SortedRec)) ||
+            ensure(ctx, ctx->keys, n * 8) || ensure(ctx, ctx->slow, n * 4) ||
+            ensure(ctx, ctx->parts_sorted, n * sizeof(EventRec)) ||
             ensure(ctx, ctx->s_cell, n * 8) || ensure(ctx, ctx->s_ws, n * 8) || ensure(ctx, ctx->s_cnt, n * 8) ||
             ensure(ctx, ctx->s_sp, n * 8) || ensure(ctx, ctx->s_spn, n) || ensure(ctx, ctx->s_lon, n * 8) ||
             ensure(ctx, ctx->s_lat, n * 8) || ensure_outputs(ctx, n))
@@ -2505,7 +2964,7 @@ void hm_destroy(hm_ctx *ctx) {
                       &ctx->rp_btot, &ctx->rp_boff,
                       &ctx->s_cell, &ctx->s_ws, &ctx->s_cnt, &ctx->s_sp, &ctx->s_spn, &ctx->s_lon, &ctx->s_lat, &ctx->bin_cnt, &ctx->bin_off, &ctx->dfused.used, &ctx->dfull.used, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
                       &ctx->o_lon, &ctx->o_lat, &ctx->td_sizes, &ctx->td_off, &ctx->td_btot, &ctx->td_boff, &ctx->td_bytes,
-                      &ctx->td_params, &ctx->gapbuf};
+                      &ctx->td_params, &ctx->gapbuf, &ctx->keys, &ctx->agg_bucket, &ctx->agg_cursor};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &g : ctx->gens)
@@ -2513,6 +2972,12 @@ void hm_destroy(hm_ctx *ctx) {
     for (auto &pt : ctx->pool)
         if (!in_arena(ctx, pt.first)) (void)hipFree(pt.first);
     if (ctx->arena) (void)hipFree(ctx->arena);
+    if (ctx->d_wreg) (void)hipFree(ctx->d_wreg);
+    if (ctx->d_wcount) (void)hipFree(ctx->d_wcount);
+    if (ctx->h_wreg) (void)hipHostFree(ctx->h_wreg);
+    if (ctx->h_wcount) (void)hipHostFree(ctx->h_wcount);
+    if (ctx->d_winfo) (void)hipFree(ctx->d_winfo);
+    if (ctx->h_winfo) (void)hipHostFree(ctx->h_winfo);
     if (ctx->d_gmap) (void)hipFree(ctx->d_gmap);
     if (ctx->h_gmap) (void)hipHostFree(ctx->h_gmap);
     if (ctx->d_cmap) (void)hipFree(ctx->d_cmap);
@@ -2545,7 +3010,7 @@ int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n) {
 
 int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t out_memory, hm_batch_out *out) {
     if (!ctx || !in || !out || in->n < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
-    if (in->n > (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds 2^32-1", (long long)in->n);
+    if (in->n > (int64_t)UINT32_MAX - 1) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds 2^32-2", (long long)in->n);
     if (in->n > 0 && (!in->lat || !in->lon || !in->ts_us || !in->vkey))
         return set_err(ctx, HM_E_INVALID, "lat, lon, ts_us and vkey are required");
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -2558,15 +3023,22 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     Inputs I;
     I.n = in->n;
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
-    // 2. snap + local pre-aggregation
+    // 2. snap + window registry + event keys
     if ((rc = phase_local(ctx, I, late_wm))) return rc;
-    ctx->census_ready = true;   // k_ingest counted its own partials per window (the merge's input here)
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     DevStats s1 = *ctx->h_st;
-    note_agg_ratio(ctx, s1);
-    // 3. merge into state + emit
-    if ((rc = phase_merge_emit(ctx, (const TilePartial *)ctx->partials.p, (int64_t)s1.n_partials, (int64_t)s1.n_gaps))) return rc;
+    const int64_t n_agg = (int64_t)s1.n_valid - (int64_t)s1.n_late;
+    // 3. aggregate, merge into state + emit (table mode: two LDS passes first; direct: every row a record)
+    const bool table = choose_table(ctx, n_agg);
+    ctx->last_table = table;
+    if (table) {
+        int64_t n_parts = 0;
+        if ((rc = phase_table(ctx, I, n_agg, &n_parts))) return rc;
+        HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+        if ((rc = merge_partials(ctx, (const TilePartial *)ctx->partials.p, n_parts))) return rc;
+    } else {
+        HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+        if ((rc = merge_events(ctx, I, n_agg))) return rc;
+    }
     // 4. dedup over the batch's valid rows
     if ((rc = phase_dedup(ctx, &I, nullptr, I.n, s1.dedup_retry != 0))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
@@ -2585,6 +3057,11 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     ctx->last_lon = I.lon;
     record_timings(ctx);
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, n_rows, (const int64_t *)ctx->rows.p, out_memory, out))) return rc;
+    // the next batch's aggregation path is chosen from this one's cardinality
+    if (n_agg >= (int64_t(1) << 16)) {
+        ctx->prev_agg_rows = n_agg;
+        ctx->prev_keys = (int64_t)s2.n_touched;
+    }
     // 5. eviction after emission with this batch's watermark (lazy: see hm_ctx), then advance the watermark
     if ((rc = state_account(ctx, ctx->wm_cur))) return rc;
     fill_stats(ctx, out, in->n, s1, late_wm);
@@ -2657,11 +3134,17 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     I.n = in->n;
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
     if ((rc = phase_local(ctx, I, late_wm))) return rc;
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    const DevStats s1 = *ctx->h_st;
+    const int64_t n_agg = (int64_t)s1.n_valid - (int64_t)s1.n_late;
+    // tile partials: table mode aggregates the shard first (one record per key); the direct path sends every row
+    const bool table = choose_table(ctx, n_agg);
+    ctx->last_table = table;
+    int64_t n_records = n_agg;
+    if (table && (rc = phase_table(ctx, I, n_agg, &n_records))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    ctx->census_ready = false;   // (the owner counts what it receives)
     // local dedup over rows -> local winners -> candidates
-    note_agg_ratio(ctx, *ctx->h_st);
-    if ((rc = phase_dedup(ctx, &I, nullptr, I.n, ctx->h_st->dedup_retry != 0))) return rc;
+    if ((rc = phase_dedup(ctx, &I, nullptr, I.n, s1.dedup_retry != 0))) return rc;
     if ((rc = ensure(ctx, ctx->cands, std::max<int64_t>(I.n, 1) * sizeof(Cand)))) return rc;
     hipLaunchKernelGGL(k_make_cands, dim3(grid_for(std::max<int64_t>(I.n, 1), 256)), dim3(256), 0, ctx->stream,
                        (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, I.vk, I.ts, rank, (Cand *)ctx->cands.p);
@@ -2678,7 +3161,6 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     if (ctx->h_st->bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved");
     ctx->dedup_seen = (int64_t)ctx->h_scratch[ctx->dlast->used_word];
-    const int64_t n_records = (int64_t)(ctx->h_st->n_partials - ctx->h_st->n_gaps);
     if (n_records > tile_send_cap || (int64_t)ctx->h_scratch[255] > cand_send_cap)
         return set_err(ctx, HM_E_INVALID, "send buffer too small (%lld tiles, %llu candidates)", (long long)n_records,
                        ctx->h_scratch[255]);
@@ -2691,12 +3173,17 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
                        nranks, ctx->d_scratch + 64, (Cand *)cand_send_buf);
     HIPCHK(ctx, hipGetLastError());
     // tile partials: the radix partition with the owner rank as the digit, straight into the send buffer
-    const int64_t n_parts = (int64_t)ctx->h_st->n_partials;
-    if (n_parts > 0) {
+    if (n_records > 0) {
         int64_t ntiles;
-        if ((rc = partition<TilePartial, TilePartial>(ctx, (const TilePartial *)ctx->partials.p, n_parts, ntiles, nranks,
-                                                      (TilePartial *)tile_send_buf)))
-            return rc;
+        if (table) {
+            if ((rc = partition<TilePartial, TilePartial>(ctx, (const TilePartial *)ctx->partials.p, n_records, ntiles, nranks,
+                                                          (TilePartial *)tile_send_buf)))
+                return rc;
+        } else {
+            if ((rc = winfo_upload(ctx, false)) ||
+                (rc = ev_partition<TilePartial>(ctx, I, ntiles, nranks, (TilePartial *)tile_send_buf)))
+                return rc;
+        }
         hipLaunchKernelGGL(k_digit_starts, dim3(1), dim3(128), 0, ctx->stream, (const unsigned long long *)ctx->rp_O.p, ntiles,
                            nranks + 1, ctx->d_scratch);
         HIPCHK(ctx, hipGetLastError());
@@ -2704,19 +3191,23 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     for (int r = 0; r < nranks; r++) {
-        const int64_t start = n_parts > 0 ? (int64_t)ctx->h_scratch[r] : 0;
-        const int64_t end = n_parts > 0 ? (int64_t)ctx->h_scratch[r + 1] : 0;   // [nranks]: the gaps' digit
+        const int64_t start = n_records > 0 ? (int64_t)ctx->h_scratch[r] : 0;
+        const int64_t end = n_records > 0 ? (int64_t)ctx->h_scratch[r + 1] : 0;   // [nranks]: the gaps' digit
         tile_send_counts[r] = end - start;
     }
+    ctx->stage_agg_rows = n_agg;
     if (sizes) {
         sizes->n_tile_partials = n_records;
         sizes->n_cands = 0;
         for (int r = 0; r < nranks; r++) sizes->n_cands += cand_send_counts[r];
-        sizes->batch_max_event_ms = ctx->h_st->max_ts_ms;
-        sizes->n_valid = (int64_t)ctx->h_st->n_valid;
-        sizes->n_late = (int64_t)ctx->h_st->n_late;
-        ctx->stage_sizes = *sizes;
+        sizes->batch_max_event_ms = s1.max_ts_ms;
+        sizes->n_valid = (int64_t)s1.n_valid;
+        sizes->n_late = (int64_t)s1.n_late;
     }
+    ctx->stage_sizes.n_tile_partials = n_records;
+    ctx->stage_sizes.batch_max_event_ms = s1.max_ts_ms;
+    ctx->stage_sizes.n_valid = (int64_t)s1.n_valid;
+    ctx->stage_sizes.n_late = (int64_t)s1.n_late;
     ctx->stage_n_in = I.n;
     ctx->stage = 1;
     return HM_OK;
@@ -2733,7 +3224,7 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, 
     int rc;
     memset(out, 0, sizeof(*out));
     int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
-    if ((rc = phase_merge_emit(ctx, (const TilePartial *)tile_recv_dev, n_tile_recv, 0))) return rc;
+    if ((rc = merge_partials(ctx, (const TilePartial *)tile_recv_dev, n_tile_recv))) return rc;
     // owner-side dedup over received candidates
     if ((rc = phase_dedup(ctx, nullptr, (const Cand *)cand_recv_dev, n_cand_recv, true))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch, 0, 128 * 8, ctx->stream));
@@ -2760,6 +3251,10 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, 
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     record_timings(ctx);
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, 0, nullptr, out_memory, out))) return rc;
+    if (ctx->stage_agg_rows >= (int64_t(1) << 16)) {   // this rank's share of the keys stands in for the shard's
+        ctx->prev_agg_rows = ctx->stage_agg_rows;
+        ctx->prev_keys = (int64_t)s2.n_touched;
+    }
     if ((rc = state_account(ctx, ctx->wm_cur))) return rc;
     DevStats sf{};
     sf.n_valid = ctx->stage_sizes.n_valid;

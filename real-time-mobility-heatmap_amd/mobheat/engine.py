@@ -43,6 +43,7 @@ class BatchResult:
     batch_max_event_ms: int
     watermark_ms: int
     late_watermark_ms: int
+    n_partials: int = 0         # partial records merged (direct path: aggregated rows; table mode: ~ distinct keys)
 
 
 def _u8(a, n):
@@ -185,7 +186,8 @@ class HeatmapEngine:
     def last_timings(self):
         ms = (ctypes.c_double * 7)()
         check(self._lib.hm_last_timings(self._ctx, ms, 7), self._ctx)
-        return {"ingest": ms[0], "merge": ms[2], "emit": ms[3], "dedup": ms[4], "total": ms[5], "partition": ms[6]}
+        return {"ingest": ms[0], "aggregate": ms[1], "merge": ms[2], "emit": ms[3], "dedup": ms[4], "total": ms[5],
+                "partition": ms[6]}
 
     def _result_from_host(self, out, copy=True):
         def arr(p, n, dt):
@@ -202,7 +204,8 @@ class HeatmapEngine:
         return BatchResult(tiles=tiles, latest_rows=arr(out.latest_row, int(out.n_latest), np.int64),
                            n_in=int(out.n_in), n_valid=int(out.n_valid), n_late=int(out.n_late),
                            n_state=int(out.n_state), batch_max_event_ms=int(out.batch_max_event_ms),
-                           watermark_ms=int(out.watermark_ms), late_watermark_ms=int(out.late_watermark_ms))
+                           watermark_ms=int(out.watermark_ms), late_watermark_ms=int(out.late_watermark_ms),
+                           n_partials=int(out.n_partials))
 
 
 def _host_statements(pb, po, nd, copy):

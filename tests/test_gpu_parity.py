@@ -208,12 +208,21 @@ def test_high_cardinality_res12_two_batches():
 
 
 def test_clustered_city_res9():
+    """C3-shaped batches (Zipf hot spots, res 9): the first batch takes the direct path (no history), the next ones
+    the table mode (few distinct keys, heavily repeated), which must collapse the partials to about the key count."""
     from mobheat import HeatmapEngine, synth
     from oracle.spark_oracle import SparkHeatmapOracle
-    b = synth.c3_city(n=3_000_000, n_vehicles=5000)
     eng = HeatmapEngine(h3_res=9)
-    res, exp = _run(eng, SparkHeatmapOracle(h3_res=9), b, 0)
-    assert_batch_equal(res, exp)
+    ora = SparkHeatmapOracle(h3_res=9)
+    for epoch in range(3):
+        b = synth.c3_city(seed=2 + epoch, n=3_000_000, n_vehicles=5000)
+        b["ts_us"] = b["ts_us"] + epoch * 600_000_000
+        res, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res, exp)
+        if epoch == 0:
+            assert res.n_partials == res.n_valid - res.n_late           # direct: one record per aggregated row
+        else:
+            assert res.n_partials <= 4 * len(res.tiles), (res.n_partials, len(res.tiles))   # table mode
     eng.close()
 
 
@@ -335,11 +344,12 @@ def test_window_tables_growth_many_windows_and_reuse():
     eng.close()
 
 
-@pytest.mark.parametrize("mode", ["direct", "lds"])
+@pytest.mark.parametrize("mode", ["direct", "table"])
 def test_ingest_modes_parity(mode, monkeypatch):
-    """k_ingest's two partial-aggregation modes pinned (MOBHEAT_INGEST_MODE): LDS pre-aggregation and direct
-    (one partial per row, picked adaptively when nearly every key is distinct) give the oracle's results on a
-    multi-batch stream with late rows, ties, nulls, an empty batch, many windows and few hot keys."""
+    """The two aggregation paths pinned (MOBHEAT_INGEST_MODE): direct (every aggregated row a 32-B record through
+    the partition and merge) and table (k_agg's LDS table with hot-key retention + k_bin_reduce, picked adaptively
+    for low-cardinality batches) give the oracle's results on a multi-batch stream with late rows, ties, nulls, an
+    empty batch, many windows and few hot keys."""
     from mobheat import HeatmapEngine, synth
     from oracle.spark_oracle import SparkHeatmapOracle
     monkeypatch.setenv("MOBHEAT_INGEST_MODE", mode)
