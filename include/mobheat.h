@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 7
+#define HM_ABI_VERSION 8
 
 /* error codes */
 #define HM_OK 0
@@ -241,7 +241,8 @@ int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_
  * u: {$set: {provider, vehicleId, ts, loc}}, multi: false, upsert: true}, in latest_row order. The strings come
  * from the batch's dictionaries (the vkey the caller passed = provider_code * n_vehicles + vehicle_code; string k
  * of a dictionary = bytes[offsets[k], offsets[k+1]), UTF-8); ts is the naive local datetime of eventTs, with the
- * local UTC offset of each 900-s bucket floor(ts_s / 900) - bucket0 given by bucket_offset_s. Not after stage
+ * local UTC offset of the row's 900-s bucket floor(ts_s / 900): bucket_offset_s[k] for bucket_ids[k] (the distinct
+ * buckets of the latest rows, strictly ascending; a row whose bucket is absent fails the call). Not after stage
  * calls (HM_E_STATE). Outputs as hm_encode_tile_updates. */
 typedef struct hm_position_doc_cfg {
     int64_t n_providers;
@@ -250,9 +251,9 @@ typedef struct hm_position_doc_cfg {
     int64_t n_vehicles;
     const int64_t *vehicle_offsets;    /* n_vehicles + 1 */
     const char *vehicle_bytes;
-    int64_t bucket0;
     int64_t n_buckets;
-    const int64_t *bucket_offset_s;
+    const int64_t *bucket_ids;         /* n_buckets, strictly ascending */
+    const int64_t *bucket_offset_s;    /* n_buckets */
 } hm_position_doc_cfg;
 int hm_encode_position_updates(hm_ctx *ctx, const hm_position_doc_cfg *cfg, int32_t out_memory, const uint8_t **bytes,
                                const int64_t **offsets, int64_t *n_docs);

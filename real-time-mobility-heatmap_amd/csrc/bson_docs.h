@@ -25,8 +25,8 @@
 namespace hm {
 
 constexpr int TD_THREADS = 128;
-constexpr int TD_MAX_DOC = 576;    // bytes per statement with a city of <= TD_MAX_CITY bytes (checked on the host)
-constexpr int TD_MAX_CITY = 64;
+constexpr int TD_MAX_DOC = 576;    // statements up to this size go through k_tile_docs' LDS staging (a city of <= 64
+                                   // bytes); longer ones (a long CITY) are written by k_tile_docs_direct
 
 struct TileDocParams {
     const uint8_t *city;          // device copy, city_len bytes
@@ -236,12 +236,24 @@ __global__ __launch_bounds__(TD_THREADS) void k_tile_docs(TileDocParams P, const
     }
 }
 
+// statements longer than TD_MAX_DOC (a long CITY): each thread writes its own statement straight to HBM
+__global__ __launch_bounds__(256) void k_tile_docs_direct(TileDocParams P, const uint64_t *__restrict__ cell, const int64_t *__restrict__ ws,
+                                                          const int64_t *__restrict__ cnt, const double *__restrict__ sp,
+                                                          const uint8_t *__restrict__ spn, const double *__restrict__ lon,
+                                                          const double *__restrict__ lat, int64_t n,
+                                                          const unsigned long long *__restrict__ off, uint8_t *__restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        tile_statement(out + off[i], P, cell[i], ws[i], cnt[i], sp[i], spn[i], lon[i], lat[i]);
+}
+
 // ---- positions_latest statements (reference heatmap_stream.py:211-228) ----
 // UpdateOne({"_id": f"{provider}|{vehicleId}", "$or": [{"ts": {"$exists": False}}, {"ts": {"$lt": ts}}]},
 //           {"$set": {provider, vehicleId, ts, loc: {type: "Point", coordinates: [lon, lat]}}}, upsert=True)
 // for each latest row; provider / vehicleId come from the batch's string dictionaries (the host's factorization:
 // vkey = provider_code * n_vehicles + vehicle_code), ts is pyspark's naive local datetime of eventTs (the local
-// offset from a table of 900-s buckets), lat/lon the row's values as float().
+// offset of the row's 900-s bucket floor(ts_s / 900), looked up in the caller's sorted list of the buckets the rows
+// use), lat/lon the row's values as float().
 struct PosDocParams {
     const int64_t *p_off;   // n_p + 1 offsets into p_bytes
     const uint8_t *p_bytes;
@@ -249,16 +261,27 @@ struct PosDocParams {
     const uint8_t *v_bytes;
     int64_t n_vehicles;
     int64_t n_providers;
-    int64_t bucket0;        // first 900-s bucket (floor(ts_s / 900)) and the local offset (s) of each
-    int64_t n_buckets;
+    int64_t n_buckets;      // distinct 900-s buckets floor(ts_s / 900) of the rows, ascending, and the local
+    const int64_t *bucket_id;   // offset (s) of each
     const int64_t *bucket_off;
 };
+
+// index of the row's 900-s bucket in P.bucket_id (binary search), -1 if absent
+HM_HD int64_t position_bucket(const PosDocParams &P, int64_t ts_us) {
+    const int64_t b = floordiv(floordiv(ts_us, 1000000), 900);
+    int64_t lo = 0, hi = P.n_buckets;
+    while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (P.bucket_id[mid] < b) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < P.n_buckets && P.bucket_id[lo] == b ? lo : -1;
+}
 
 // the row's codes and time bucket lie inside the caller's tables (else the host reports an error)
 HM_HD bool position_ok(const PosDocParams &P, uint64_t vkey, int64_t ts_us) {
     if (P.n_vehicles <= 0 || vkey / (uint64_t)P.n_vehicles >= (uint64_t)P.n_providers) return false;
-    const int64_t b = floordiv(floordiv(ts_us, 1000000), 900) - P.bucket0;
-    return b >= 0 && b < P.n_buckets;
+    return position_bucket(P, ts_us) >= 0;
 }
 
 HM_HD int64_t bson_date_ms(int64_t ts_us, int64_t off_s) {
@@ -270,7 +293,7 @@ HM_HD int position_statement(uint8_t *dst, const PosDocParams &P, uint64_t vkey,
     const int64_t pc = (int64_t)(vkey / (uint64_t)P.n_vehicles), vc = (int64_t)(vkey % (uint64_t)P.n_vehicles);
     const uint8_t *ps = P.p_bytes + P.p_off[pc], *vs = P.v_bytes + P.v_off[vc];
     const int pl = (int)(P.p_off[pc + 1] - P.p_off[pc]), vl = (int)(P.v_off[vc + 1] - P.v_off[vc]);
-    const int64_t date = bson_date_ms(ts_us, P.bucket_off[floordiv(floordiv(ts_us, 1000000), 900) - P.bucket0]);
+    const int64_t date = bson_date_ms(ts_us, P.bucket_off[position_bucket(P, ts_us)]);
     BsonW w{dst, 0};
     const int top = w.begin();
     w.key(0x03, "q");

@@ -3452,7 +3452,7 @@ int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_
     if (!ctx || !cfg || !bytes || !offsets || !n_docs || cfg->city_len < 0 || (cfg->city_len > 0 && !cfg->city) ||
         cfg->n_windows < 0 || (cfg->n_windows > 0 && (!cfg->window_start_us || !cfg->start_offset_s || !cfg->end_offset_s)))
         return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
-    if (cfg->city_len > TD_MAX_CITY) return set_err(ctx, HM_E_INVALID, "city of %d bytes (at most %d)", cfg->city_len, TD_MAX_CITY);
+    if (cfg->city_len > (1 << 20)) return set_err(ctx, HM_E_INVALID, "city of %d bytes (at most 1 MiB)", cfg->city_len);
     const int64_t n = ctx->last_n_tiles;
     const auto &W = ctx->batch_windows;
     if (cfg->n_windows != (int64_t)W.size()) return set_err(ctx, HM_E_INVALID, "%lld window offsets for %zu windows", (long long)cfg->n_windows, W.size());
@@ -3467,17 +3467,18 @@ int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc;
     const int nw = (int)W.size();
-    // parameters: city bytes, then the window table (3 x nw int64)
-    const size_t pbytes = 64 + (size_t)nw * 24;
+    // parameters: city bytes (padded to 16), then the window table (3 x nw int64)
+    const size_t cbytes = ((size_t)cfg->city_len + 15) & ~(size_t)15;
+    const size_t pbytes = cbytes + (size_t)nw * 24 + 16;
     if ((rc = ensure(ctx, ctx->td_params, pbytes)) || (rc = ensure(ctx, ctx->td_off, (n + 1) * 8)) ||
         (rc = ensure(ctx, ctx->td_sizes, std::max<int64_t>(n, 1) * 4)))
         return rc;
     std::vector<uint8_t> hp(pbytes, 0);
     if (cfg->city_len) memcpy(hp.data(), cfg->city, cfg->city_len);
     if (nw) {
-        memcpy(hp.data() + 64, W.data(), nw * 8);
-        memcpy(hp.data() + 64 + nw * 8, cfg->start_offset_s, nw * 8);
-        memcpy(hp.data() + 64 + nw * 16, cfg->end_offset_s, nw * 8);
+        memcpy(hp.data() + cbytes, W.data(), nw * 8);
+        memcpy(hp.data() + cbytes + nw * 8, cfg->start_offset_s, nw * 8);
+        memcpy(hp.data() + cbytes + nw * 16, cfg->end_offset_s, nw * 8);
     }
     HIPCHK(ctx, hipMemcpyAsync(ctx->td_params.p, hp.data(), pbytes, hipMemcpyHostToDevice, ctx->stream));
     TileDocParams P;
@@ -3486,7 +3487,7 @@ int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_
     P.h3_res = ctx->cfg.h3_res;
     P.tile_us = ctx->cfg.tile_us;
     P.ttl_ms = cfg->ttl_ms;
-    P.win_start_us = (const int64_t *)((uint8_t *)ctx->td_params.p + 64);
+    P.win_start_us = (const int64_t *)((uint8_t *)ctx->td_params.p + cbytes);
     P.off_start_s = P.win_start_us + nw;
     P.off_end_s = P.win_start_us + 2 * nw;
     P.n_win = nw;
@@ -3515,14 +3516,20 @@ int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_
         Ph.off_start_s = cfg->start_offset_s;
         Ph.off_end_s = cfg->end_offset_s;
         const int max_doc = tile_statement(nullptr, Ph, ~0ull, W[0], INT64_MAX, 0.0, 1, 0.0, 0.0);
-        if (max_doc > TD_MAX_DOC) return set_err(ctx, HM_E_INVALID, "statement of %d bytes exceeds %d", max_doc, TD_MAX_DOC);
-        const size_t lds = (size_t)TD_THREADS * ((max_doc + 15) & ~15) + 32;
-        if (lds > 65536)
-            HIPCHK(ctx, hipFuncSetAttribute((const void *)k_tile_docs, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(k_tile_docs, dim3(grid_for(n, TD_THREADS)), dim3(TD_THREADS), lds, ctx->stream, P, (const uint64_t *)ctx->o_cell.p,
-                           (const int64_t *)ctx->o_ws.p, (const int64_t *)ctx->o_cnt.p, (const double *)ctx->o_sp.p,
-                           (const uint8_t *)ctx->o_spn.p, (const double *)ctx->o_lon.p, (const double *)ctx->o_lat.p, n,
-                           (const unsigned long long *)off, (uint8_t *)ctx->td_bytes.p);
+        if (max_doc > TD_MAX_DOC) {   // a long CITY: no LDS staging
+            hipLaunchKernelGGL(k_tile_docs_direct, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, P, (const uint64_t *)ctx->o_cell.p,
+                               (const int64_t *)ctx->o_ws.p, (const int64_t *)ctx->o_cnt.p, (const double *)ctx->o_sp.p,
+                               (const uint8_t *)ctx->o_spn.p, (const double *)ctx->o_lon.p, (const double *)ctx->o_lat.p, n,
+                               (const unsigned long long *)off, (uint8_t *)ctx->td_bytes.p);
+        } else {
+            const size_t lds = (size_t)TD_THREADS * ((max_doc + 15) & ~15) + 32;
+            if (lds > 65536)
+                HIPCHK(ctx, hipFuncSetAttribute((const void *)k_tile_docs, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL(k_tile_docs, dim3(grid_for(n, TD_THREADS)), dim3(TD_THREADS), lds, ctx->stream, P, (const uint64_t *)ctx->o_cell.p,
+                               (const int64_t *)ctx->o_ws.p, (const int64_t *)ctx->o_cnt.p, (const double *)ctx->o_sp.p,
+                               (const uint8_t *)ctx->o_spn.p, (const double *)ctx->o_lon.p, (const double *)ctx->o_lat.p, n,
+                               (const unsigned long long *)off, (uint8_t *)ctx->td_bytes.p);
+        }
         HIPCHK(ctx, hipGetLastError());
     } else {
         HIPCHK(ctx, hipMemsetAsync(off, 0, 8, ctx->stream));
@@ -3535,8 +3542,10 @@ int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_
 static int pos_params(hm_ctx *ctx, const hm_position_doc_cfg *cfg, PosDocParams &P, std::vector<uint8_t> &hp) {
     const int64_t np_ = cfg->n_providers, nv = cfg->n_vehicles, nb = cfg->n_buckets;
     if (np_ < 0 || nv < 0 || nb < 0 || (np_ && (!cfg->provider_offsets || !cfg->provider_bytes)) ||
-        (nv && (!cfg->vehicle_offsets || !cfg->vehicle_bytes)) || (nb && !cfg->bucket_offset_s))
+        (nv && (!cfg->vehicle_offsets || !cfg->vehicle_bytes)) || (nb && (!cfg->bucket_ids || !cfg->bucket_offset_s)))
         return set_err(ctx, HM_E_INVALID, "bad position dictionaries");
+    for (int64_t k = 1; k < nb; k++)
+        if (cfg->bucket_ids[k - 1] >= cfg->bucket_ids[k]) return set_err(ctx, HM_E_INVALID, "bucket ids not ascending");
     const int64_t pb = np_ ? cfg->provider_offsets[np_] : 0, vb = nv ? cfg->vehicle_offsets[nv] : 0;
     for (int64_t k = 0; k < np_; k++)
         if (cfg->provider_offsets[k] < 0 || cfg->provider_offsets[k] > cfg->provider_offsets[k + 1] ||
@@ -3547,10 +3556,12 @@ static int pos_params(hm_ctx *ctx, const hm_position_doc_cfg *cfg, PosDocParams 
             cfg->vehicle_offsets[k + 1] - cfg->vehicle_offsets[k] > (1 << 20))
             return set_err(ctx, HM_E_INVALID, "vehicle offsets");
     // one device block: offsets (8-B aligned) first, then the string bytes
-    const size_t o_p = 0, o_v = o_p + (np_ + 1) * 8, o_b = o_v + (nv + 1) * 8, o_ps = o_b + nb * 8, o_vs = o_ps + pb;
+    const size_t o_p = 0, o_v = o_p + (np_ + 1) * 8, o_bi = o_v + (nv + 1) * 8, o_b = o_bi + nb * 8, o_ps = o_b + nb * 8,
+                 o_vs = o_ps + pb;
     hp.assign(o_vs + vb + 8, 0);
     if (np_) memcpy(hp.data() + o_p, cfg->provider_offsets, (np_ + 1) * 8);
     if (nv) memcpy(hp.data() + o_v, cfg->vehicle_offsets, (nv + 1) * 8);
+    if (nb) memcpy(hp.data() + o_bi, cfg->bucket_ids, nb * 8);
     if (nb) memcpy(hp.data() + o_b, cfg->bucket_offset_s, nb * 8);
     if (pb) memcpy(hp.data() + o_ps, cfg->provider_bytes, pb);
     if (vb) memcpy(hp.data() + o_vs, cfg->vehicle_bytes, vb);
@@ -3560,12 +3571,12 @@ static int pos_params(hm_ctx *ctx, const hm_position_doc_cfg *cfg, PosDocParams 
     uint8_t *d = (uint8_t *)ctx->td_params.p;
     P.p_off = (const int64_t *)(d + o_p);
     P.v_off = (const int64_t *)(d + o_v);
+    P.bucket_id = (const int64_t *)(d + o_bi);
     P.bucket_off = (const int64_t *)(d + o_b);
     P.p_bytes = d + o_ps;
     P.v_bytes = d + o_vs;
     P.n_providers = np_;
     P.n_vehicles = nv;
-    P.bucket0 = cfg->bucket0;
     P.n_buckets = nb;
     return HM_OK;
 }
@@ -3632,7 +3643,7 @@ int hm_selftest_tile_statements(const hm_tile_doc_cfg *cfg, int32_t h3_res, int6
                                 const int64_t *ws, const int64_t *cnt, const double *sp, const uint8_t *spn,
                                 const double *lon, const double *lat, int64_t n, uint8_t *bytes, int64_t cap,
                                 int64_t *offsets) {
-    if (!cfg || n < 0 || !offsets || cfg->n_windows <= 0 || cfg->city_len < 0 || cfg->city_len > TD_MAX_CITY) return HM_E_INVALID;
+    if (!cfg || n < 0 || !offsets || cfg->n_windows <= 0 || cfg->city_len < 0 || cfg->city_len > (1 << 20)) return HM_E_INVALID;
     TileDocParams P;
     P.city = (const uint8_t *)cfg->city;
     P.city_len = cfg->city_len;
@@ -3667,8 +3678,8 @@ int hm_selftest_position_statements(const hm_position_doc_cfg *cfg, const uint64
     P.v_bytes = (const uint8_t *)cfg->vehicle_bytes;
     P.n_providers = cfg->n_providers;
     P.n_vehicles = cfg->n_vehicles;
-    P.bucket0 = cfg->bucket0;
     P.n_buckets = cfg->n_buckets;
+    P.bucket_id = cfg->bucket_ids;
     P.bucket_off = cfg->bucket_offset_s;
     int64_t o = 0;
     for (int64_t i = 0; i < n; i++) {

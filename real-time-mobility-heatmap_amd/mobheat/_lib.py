@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MOBHEAT_LIB: load another build of the same ABI (kernel variants under csrc/variants/ for tuning runs)
 LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
 
-HM_ABI_VERSION = 7
+HM_ABI_VERSION = 8
 HM_MEM_HOST = 0
 HM_MEM_DEVICE = 1
 HM_TILE_REC_BYTES = 48
@@ -67,7 +67,7 @@ class HmTileDocCfg(ctypes.Structure):
 class HmPositionDocCfg(ctypes.Structure):
     _fields_ = [("n_providers", c_i64), ("provider_offsets", c_vp), ("provider_bytes", c_vp),
                 ("n_vehicles", c_i64), ("vehicle_offsets", c_vp), ("vehicle_bytes", c_vp),
-                ("bucket0", c_i64), ("n_buckets", c_i64), ("bucket_offset_s", c_vp)]
+                ("n_buckets", c_i64), ("bucket_ids", c_vp), ("bucket_offset_s", c_vp)]
 
 
 # hm_state_rec (64 B): one live (cellId, windowStart) key of the tile state
@@ -214,7 +214,7 @@ def tile_statements_selftest(tiles, city, h3_res, ttl_minutes, tile_us):
     n = len(tiles)
     wins = np.unique(tiles.window_start_us) if n else np.zeros(1, np.int64)
     cfg, keep = tile_doc_cfg(city, ttl_minutes, wins, tile_us)
-    cap = 600 * max(n, 1)
+    cap = (600 + 3 * len(city.encode("utf-8"))) * max(n, 1)   # (the city is in q._id, $set._id and $set.city)
     buf = np.zeros(cap, np.uint8)
     offs = np.zeros(n + 1, np.int64)
     a = [np.ascontiguousarray(x) for x in (tiles.cell.astype(np.uint64), tiles.window_start_us.astype(np.int64),
@@ -224,9 +224,6 @@ def tile_statements_selftest(tiles, city, h3_res, ttl_minutes, tile_us):
     check(lib.hm_selftest_tile_statements(ctypes.byref(cfg), int(h3_res), int(tile_us), *[ptr(x) for x in a], n,
                                           ptr(buf), cap, ptr(offs)), None, "hm_selftest_tile_statements")
     return buf[:offs[-1]].copy(), offs
-
-
-MAX_TIME_BUCKETS = 1 << 17   # 900-s buckets of local offsets a position batch may span (~3.7 years)
 
 
 def _dictionary(strings):
@@ -241,32 +238,37 @@ def _dictionary(strings):
     return n, offs, raw
 
 
-def position_doc_cfg(provider_uniques, vehicle_uniques, ts_min_us, ts_max_us):
-    """hm_position_doc_cfg for a batch's string dictionaries (pandas.factorize uniques, the order the vkeys were
-    built in) and the eventTs range of its latest rows; the returned tuple keeps the arrays alive.  The local
-    offset is taken per 900-s bucket (and checked constant over each bucket)."""
+def time_buckets(ts_us):
+    """The distinct 900-s buckets floor(ts_s / 900) of the rows' eventTs (ascending) and the local-time offset of
+    each (pyspark's naive local datetimes, stream._spark_datetime).  Only the buckets the rows use are looked up, so
+    a batch mixing a 1970 GPS time with current traffic costs two lookups, not 55 years of buckets."""
     import calendar
     import datetime as _dt
-    np_, po, pb = _dictionary(provider_uniques)
-    nv, vo, vb = _dictionary(vehicle_uniques)
-    b0 = int(ts_min_us) // 1_000_000 // 900
-    b1 = int(ts_max_us) // 1_000_000 // 900
-    if b1 - b0 + 1 > MAX_TIME_BUCKETS:
-        raise RuntimeError(f"latest positions span {b1 - b0 + 1} 900-s buckets (at most {MAX_TIME_BUCKETS})")
+    ts_us = np.asarray(ts_us, dtype=np.int64)
+    ids = np.unique(np.floor_divide(np.floor_divide(ts_us, 1_000_000), 900)) if ts_us.size else np.zeros(0, np.int64)
 
     def off(s):
         return calendar.timegm(_dt.datetime.fromtimestamp(s).timetuple()) - s
-    bo = np.array([off(b * 900) for b in range(b0, b1 + 1)], np.int64)
-    if any(off(b * 900 + 899) != bo[b - b0] for b in range(b0, b1 + 1)):
+    offs = np.array([off(int(b) * 900) for b in ids], np.int64)
+    if any(off(int(b) * 900 + 899) != o for b, o in zip(ids, offs)):
         raise RuntimeError("a local-time offset change inside a 900-s bucket")
+    return np.ascontiguousarray(ids, np.int64), offs
+
+
+def position_doc_cfg(provider_uniques, vehicle_uniques, ts_us):
+    """hm_position_doc_cfg for a batch's string dictionaries (pandas.factorize uniques, the order the vkeys were
+    built in) and the eventTs of its latest rows; the returned tuple keeps the arrays alive."""
+    np_, po, pb = _dictionary(provider_uniques)
+    nv, vo, vb = _dictionary(vehicle_uniques)
+    bi, bo = time_buckets(ts_us)
     cfg = HmPositionDocCfg(n_providers=np_, provider_offsets=ptr(po), provider_bytes=ptr(pb), n_vehicles=max(nv, 1),
-                           vehicle_offsets=ptr(vo), vehicle_bytes=ptr(vb), bucket0=b0, n_buckets=bo.size,
-                           bucket_offset_s=ptr(bo))
+                           vehicle_offsets=ptr(vo), vehicle_bytes=ptr(vb), n_buckets=bi.size,
+                           bucket_ids=ptr(bi) if bi.size else None, bucket_offset_s=ptr(bo) if bo.size else None)
     if nv == 0:   # (no valid row: an empty dictionary of one empty string keeps the offsets well formed)
         vo2 = np.zeros(2, np.int64)
         cfg.vehicle_offsets = ptr(vo2)
-        return cfg, (po, pb, vo, vb, bo, vo2)
-    return cfg, (po, pb, vo, vb, bo)
+        return cfg, (po, pb, vo, vb, bi, bo, vo2)
+    return cfg, (po, pb, vo, vb, bi, bo)
 
 
 def position_statements_selftest(provider_uniques, vehicle_uniques, vkey, ts_us, lat, lon):
@@ -277,7 +279,7 @@ def position_statements_selftest(provider_uniques, vehicle_uniques, vkey, ts_us,
     lat = np.ascontiguousarray(lat, dtype=np.float64)
     lon = np.ascontiguousarray(lon, dtype=np.float64)
     n = vkey.size
-    cfg, keep = position_doc_cfg(provider_uniques, vehicle_uniques, ts_us.min() if n else 0, ts_us.max() if n else 0)
+    cfg, keep = position_doc_cfg(provider_uniques, vehicle_uniques, ts_us)
     cap = 1024 * max(n, 1) + 8 * int(keep[1].size + keep[3].size)
     buf = np.zeros(cap, np.uint8)
     offs = np.zeros(n + 1, np.int64)

@@ -100,6 +100,9 @@ class ShardedHeatmap:
         self.device = device
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
+        # the last batch's receive buffers: with out_memory=HM_MEM_DEVICE, out.latest_row points into winner_recv
+        # (hm_stage_finish), so they stay alive until the next process_batch call
+        self._recv = None
 
     def process_batch(self, epoch, batch, out_memory=HM_MEM_DEVICE, sync=None):
         sync = sync or (lambda: torch.cuda.current_stream(self.device).synchronize()
@@ -115,6 +118,7 @@ class ShardedHeatmap:
                                                       out_memory)
         winner_recv, wrc = exchange(winner_send, wcounts, 8, self.device)
         sync()
+        self._recv = (tile_recv, cand_recv, winner_recv)
         return self.stages.finish(winner_recv, int(sum(wrc)), out_memory, out)
 
 

@@ -159,11 +159,12 @@ class HeatmapEngine:
                                                ctypes.byref(po), ctypes.byref(nd)), self._ctx, "hm_encode_tile_updates")
         return _host_statements(pb, po, nd, copy)
 
-    def encode_position_updates(self, provider_uniques, vehicle_uniques, ts_min_us, ts_max_us, copy=False):
+    def encode_position_updates(self, provider_uniques, vehicle_uniques, latest_ts_us, copy=False):
         """The last batch's latest rows as positions_latest update statements (reference heatmap_stream.py:211-235):
         (bytes uint8, offsets int64[n+1]).  The dictionaries are the batch's factorization its vkeys were built
-        from (vkey = provider_code * n_vehicles + vehicle_code); [ts_min_us, ts_max_us] covers the rows' eventTs."""
-        cfg, keep = _lib.position_doc_cfg(provider_uniques, vehicle_uniques, ts_min_us, ts_max_us)
+        from (vkey = provider_code * n_vehicles + vehicle_code); latest_ts_us = the latest rows' eventTs (their
+        900-s buckets' local offsets are looked up on the host)."""
+        cfg, keep = _lib.position_doc_cfg(provider_uniques, vehicle_uniques, latest_ts_us)
         pb, po, nd = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
         check(self._lib.hm_encode_position_updates(self._ctx, ctypes.byref(cfg), HM_MEM_HOST, ctypes.byref(pb),
                                                    ctypes.byref(po), ctypes.byref(nd)), self._ctx,

@@ -33,12 +33,14 @@ WATERMARK_DELAY_MS = 10 * 60 * 1000          # withWatermark("eventTs", "10 minu
 BULK_CHUNK = 1000                              # :191, :230
 DEVICE = int(os.getenv("MOBHEAT_DEVICE", os.getenv("LOCAL_RANK", "0")))
 # Spark keeps the aggregation state under checkpointLocation (:37, :244); the GPU state is checkpointed beside it
-# (CHECKPOINT_DIR/mobheat-state/state-<epoch>.npz) after each committed batch when MOBHEAT_STATE_CHECKPOINT=1.
+# (CHECKPOINT_DIR/mobheat-state/state-<epoch>.npz) after each committed batch.  On by default whenever CHECKPOINT is
+# set (the reference always restores its state from there); MOBHEAT_STATE_CHECKPOINT=0/1 overrides.
 CHECKPOINT_DIR = os.getenv("CHECKPOINT", "/tmp/heatmap-checkpoint")
-STATE_CHECKPOINT = os.getenv("MOBHEAT_STATE_CHECKPOINT", "0") == "1"
+STATE_CHECKPOINT = os.getenv("MOBHEAT_STATE_CHECKPOINT", "1" if "CHECKPOINT" in os.environ else "0") == "1"
 STATE_KEEP = 2     # the newest two: an epoch replayed after a crash between our save and Spark's commit log
 
 _ENGINE = None
+_LAST_EPOCH = None   # the last epoch merged into _ENGINE's state (a replay of it must not be merged twice)
 
 
 def _state_dir():
@@ -63,7 +65,11 @@ def _checkpoints():
 def get_engine(epoch_id=None):
     """The process's engine; a new one resumes from the newest state checkpoint older than `epoch_id` (Spark
     re-runs the first uncommitted epoch on the state of the one before it)."""
-    global _ENGINE
+    global _ENGINE, _LAST_EPOCH
+    if _ENGINE is not None and epoch_id is not None and _LAST_EPOCH is not None and int(epoch_id) <= _LAST_EPOCH:
+        # Spark re-runs an epoch this engine already merged (the query restarted in this process): rebuild the state
+        # of the epoch before it instead of merging the batch a second time
+        reset_engine()
     if _ENGINE is None:
         eng = HeatmapEngine(h3_res=H3_RES, tile_minutes=TILE_MIN, watermark_delay_ms=WATERMARK_DELAY_MS,
                             device=DEVICE)
@@ -84,11 +90,12 @@ def save_state_checkpoint(epoch_id):
 
 
 def reset_engine():
-    """Drop the persistent state (a new streaming query)."""
-    global _ENGINE
+    """Drop the persistent state (a new streaming query, or a batch that failed after its merge)."""
+    global _ENGINE, _LAST_EPOCH
     if _ENGINE is not None:
         _ENGINE.close()
     _ENGINE = None
+    _LAST_EPOCH = None
 
 
 # ------------------ sinks ------------------
@@ -123,6 +130,26 @@ SINK_FACTORY = MongoSink   # tests replace this with an in-memory capture sink
 
 
 # ------------------ batch columns ------------------
+def _pandas_to_arrow(pdf):
+    """A pandas frame as Arrow WITHOUT pandas' NaN -> null mapping on float columns: a NaN speedKmh (Spark's JSON reader
+    accepts NaN tokens, SURVEY App. A.2) must stay NaN so that avg(speedKmh) is NaN (App. A.4), while a missing value
+    (None in an object column, pd.NA in a nullable column) is null."""
+    import pyarrow as pa
+    cols = {}
+    for name in pdf.columns:
+        c = pdf[name]
+        if c.dtype.kind == "f":            # numpy float: NaN is a value, there is no null
+            cols[str(name)] = pa.array(c.to_numpy(), from_pandas=False)
+        elif c.dtype == object:            # None -> null, float('nan') -> NaN
+            try:
+                cols[str(name)] = pa.array(c.to_numpy(), from_pandas=False)
+            except (pa.ArrowInvalid, pa.ArrowTypeError):
+                cols[str(name)] = pa.array(c, from_pandas=True)
+        else:                              # nullable extension dtypes, datetimes (NaT -> null), ints, strings
+            cols[str(name)] = pa.array(c, from_pandas=True)
+    return pa.table(cols) if cols else pa.table({})
+
+
 def _to_arrow(df):
     import pyarrow as pa
     if isinstance(df, pa.Table):
@@ -132,13 +159,18 @@ def _to_arrow(df):
     try:
         import pandas as pd
         if isinstance(df, pd.DataFrame):
-            return pa.Table.from_pandas(df, preserve_index=False)
+            return _pandas_to_arrow(df)
     except ImportError:
         pass
-    if hasattr(df, "toArrow"):           # pyspark >= 4
+    if hasattr(df, "toArrow"):           # pyspark >= 4: Arrow batches with Spark's nulls
         return df.toArrow()
-    if hasattr(df, "toPandas"):          # pyspark 3.x (Arrow-enabled conversion)
-        return pa.Table.from_pandas(df.toPandas(), preserve_index=False)
+    if hasattr(df, "_collect_as_arrow"):  # pyspark 3.x: the same batches (toPandas would turn null doubles into NaN)
+        batches = df._collect_as_arrow()
+        if batches:
+            return pa.Table.from_batches(batches)
+        return _pandas_to_arrow(df.limit(0).toPandas())
+    if hasattr(df, "toPandas"):
+        return _pandas_to_arrow(df.toPandas())
     raise TypeError(f"unsupported batch type {type(df)!r}")
 
 
@@ -277,9 +309,17 @@ def _flush_statements(sink, collection, buf, offs):
 # ------------------ the drop-in boundary ------------------
 def foreach_batch_func(df, epoch_id: int):
     """Runs on each micro-batch (reference heatmap_stream.py:150): tiles + latest positions -> MongoDB."""
+    global _LAST_EPOCH
     cols = batch_columns(df)
-    res = get_engine(epoch_id).process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"],
-                                     cols["speed_valid"], cols["vkey"], cols["row_valid"], copy=False)
+    eng = get_engine(epoch_id)
+    try:
+        res = eng.process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"], cols["speed_valid"],
+                                cols["vkey"], cols["row_valid"], copy=False)
+    except BaseException:
+        reset_engine()   # the state may hold part of the batch: the next attempt rebuilds it from the checkpoint
+        raise
+    _LAST_EPOCH = int(epoch_id)
+    committed = False
     sink = SINK_FACTORY()
     try:
         # ---- 1) Upsert tiles (TTL via staleAt): the UpdateOne statements, BSON-encoded on the GPU ----
@@ -288,12 +328,16 @@ def foreach_batch_func(df, epoch_id: int):
         # ---- 2) latest per (provider, vehicleId) within this micro-batch: statements encoded on the GPU ----
         rows = res.latest_rows
         if rows.size:
-            t = cols["ts_us"][rows]
             buf, offs = get_engine().encode_position_updates(cols["provider_uniques"], cols["vehicle_uniques"],
-                                                             int(t.min()), int(t.max()))
+                                                             cols["ts_us"][rows])
             _flush_statements(sink, "positions_latest", buf, offs)
+        if STATE_CHECKPOINT:   # after the writes succeeded: the batch is committed
+            save_state_checkpoint(epoch_id)
+        committed = True
     finally:
         sink.close()
-    if STATE_CHECKPOINT:   # after the writes succeeded: the batch is committed
-        save_state_checkpoint(epoch_id)
+        if not committed:
+            # the writes (or the checkpoint) failed and Spark will re-run this epoch: drop the state that already
+            # holds it, so the retry starts from the checkpoint of the epoch before (or empty without checkpoints)
+            reset_engine()
     return res

@@ -282,11 +282,16 @@ def test_foreach_batch_func_capture_sink():
             pass
 
     b = synth.c1_boston(n=3000)
+    # a few NaN speeds (Spark's JSON reader accepts NaN tokens): avg(speedKmh) of their tiles is NaN, which the sink
+    # keeps (float(NaN or 0.0) is NaN, heatmap_stream.py:169); null speeds (None) are skipped by avg
+    nan_rows = np.flatnonzero(b["speed_valid"] & b["row_valid"])[:5]
+    b["speed"] = b["speed"].copy()
+    b["speed"][nan_rows] = np.nan
     df = pd.DataFrame({
         "provider": ["mbta"] * len(b["lat"]),
         "vehicleId": [None if not v else f"v{i:05d}" for i, v in enumerate(b["row_valid"])],
         "lat": b["lat"], "lon": b["lon"],
-        "speedKmh": np.where(b["speed_valid"], b["speed"], np.nan),
+        "speedKmh": pd.Series([float(x) if v else None for x, v in zip(b["speed"], b["speed_valid"])], dtype=object),
         "eventTs": pd.to_datetime(b["ts_us"], unit="us"),
     })
     stream.reset_engine()
@@ -305,6 +310,7 @@ def test_foreach_batch_func_capture_sink():
         d = tiles[_id]
         assert d["count"] == x["count"] and d["cellId"] == format(x["cell"], "x")
         assert _close(d["avgSpeedKmh"], x["avg_speed"] or 0.0)
+    assert sum(np.isnan(d["avgSpeedKmh"]) for d in tiles.values()) >= 1   # the NaN rows' tiles
     pos = Capture.ops["positions_latest"]
     assert sorted(op._filter["_id"] for op in pos) == sorted(f"mbta|v{r:05d}" for r in exp["latest_rows"])
 

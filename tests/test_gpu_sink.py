@@ -18,13 +18,15 @@ def _split(buf, offs):
     return [buf[offs[i]:offs[i + 1]].tobytes() for i in range(offs.size - 1)]
 
 
-def test_c1_batch_statements_match_pymongo():
+@pytest.mark.parametrize("city", ["ath", "greater-" * 40 + "αθήνα"])
+def test_c1_batch_statements_match_pymongo(city):
+    """C1 through the GPU encoder; a CITY of 330 bytes takes the unstaged encoder (k_tile_docs_direct)."""
     from mobheat import HeatmapEngine, synth
     eng = HeatmapEngine(h3_res=8)
     res = eng.process_batch(0, **synth.c1_boston())
-    buf, offs = eng.encode_tile_updates("ath", 45)
+    buf, offs = eng.encode_tile_updates(city, 45)
     assert offs.size == len(res.tiles) + 1 > 100
-    assert _split(buf, offs) == _reference_statements(res.tiles, "ath", 8, 45)
+    assert _split(buf, offs) == _reference_statements(res.tiles, city, 8, 45)
     eng.close()
 
 
@@ -119,10 +121,10 @@ def test_position_statements_match_pymongo():
     rows = res.latest_rows
     assert rows.size > 20000   # ties: several rows for some vehicles
     t = cols["ts_us"][rows]
-    buf, offs = eng.encode_position_updates(cols["provider_uniques"], cols["vehicle_uniques"], int(t.min()), int(t.max()))
+    buf, offs = eng.encode_position_updates(cols["provider_uniques"], cols["vehicle_uniques"], t)
     exp = [bson.encode({"q": op._filter, "u": op._doc, "multi": False, "upsert": True})
            for op in stream.position_ops(cols, rows)]
     assert _split(buf, offs) == exp
     with pytest.raises(RuntimeError, match="dictionaries"):
-        eng.encode_position_updates(cols["provider_uniques"][:1], cols["vehicle_uniques"], int(t.min()), int(t.max()))
+        eng.encode_position_updates(cols["provider_uniques"][:1], cols["vehicle_uniques"], t)
     eng.close()

@@ -93,19 +93,36 @@ def test_batch_columns_nulls_and_keys(kind):
         "vehicleId": ["a", "b", "a", "a", None],
         "lat": [42.3, None, 42.3, 10.0, 42.3],
         "lon": [-71.0, -71.0, -71.0, 20.0, -71.0],
-        "speedKmh": [10.0, None, 3.0, float("nan"), 1.0],
+        "speedKmh": pd.Series([10.0, None, 3.0, float("nan"), 1.0], dtype=object),   # null != NaN
         "eventTs": pd.to_datetime(["2025-10-04T10:22:05Z", "2025-10-04T10:22:06Z", None, "2025-10-04T10:22:07.500Z",
                                    "2025-10-04T10:22:08Z"], utc=True, format="ISO8601"),
     })
-    src = df if kind == "pandas" else pa.Table.from_pandas(df, preserve_index=False)
+    src = df if kind == "pandas" else stream._pandas_to_arrow(df)
     c = stream.batch_columns(src)
     assert c["n"] == 5
     assert c["row_valid"].tolist() == [True, True, False, True, False]
     assert np.isnan(c["lat"][1])
-    assert c["speed_valid"].tolist()[:2] == [True, False]
+    # a null speed is not aggregated (speed_valid 0); a NaN speed is a value (avg -> NaN)
+    assert c["speed_valid"].tolist() == [True, False, True, True, True]
+    assert np.isnan(c["speed"][3])
     assert c["ts_us"][3] == 1759573327_500000
     k = c["vkey"]
     assert k[0] != k[1] and k[0] != k[3]       # (mbta,a) vs (mbta,b) vs (opensky,a)
+
+
+def test_nan_speed_is_not_null_at_the_boundary():
+    """pandas float64 NaN, Arrow NaN and Arrow null reach the engine as NaN / NaN / null (pa.Table.from_pandas would
+    turn the NaNs into nulls, and avg would then skip them instead of yielding NaN)."""
+    df = pd.DataFrame({"provider": ["p"] * 3, "vehicleId": ["a", "b", "c"], "lat": [1.0, 2.0, 3.0],
+                       "lon": [1.0, 2.0, 3.0], "speedKmh": [np.nan, 5.0, np.nan],
+                       "eventTs": pd.to_datetime([1759572000] * 3, unit="s")})
+    c = stream.batch_columns(df)
+    assert c["speed_valid"].tolist() == [True, True, True] and np.isnan(c["speed"][[0, 2]]).all()
+    t = pa.table({"provider": ["p"] * 3, "vehicleId": ["a", "b", "c"], "lat": [1.0, 2.0, 3.0], "lon": [1.0, 2.0, 3.0],
+                  "speedKmh": pa.array([float("nan"), None, 4.0], pa.float64()),
+                  "eventTs": pa.array([1759572000_000_000] * 3, pa.timestamp("us", tz="UTC"))})
+    c = stream.batch_columns(t)
+    assert c["speed_valid"].tolist() == [True, False, True] and np.isnan(c["speed"][0])
 
 
 def test_iso_ts_strings_parse_like_to_timestamp():
@@ -185,7 +202,8 @@ def _edge_tiles(rng, n, tile_us, t0_us):
 
 
 @pytest.mark.parametrize("tz", ["UTC", "EET-2EEST,M3.5.0/3,M10.5.0/4", "EST+5EDT,M3.2.0/2,M11.1.0/2"])
-@pytest.mark.parametrize("h3_res,city,tile_min", [(8, "ath", 5), (12, "αθήνα-" + "x" * 40, 15), (0, "", 1)])
+@pytest.mark.parametrize("h3_res,city,tile_min", [(8, "ath", 5), (12, "αθήνα-" + "x" * 40, 15), (0, "", 1),
+                                                  (9, "greater-" * 40 + "αθήνα", 5)])
 def test_gpu_statement_encoder_matches_pymongo(tz, h3_res, city, tile_min):
     """CPU: the GPU encoder's code (host execution, hm_selftest_tile_statements) writes exactly the bytes pymongo
     encodes for the reference's UpdateOne ops -- under local time zones with DST transitions inside windows
@@ -283,3 +301,102 @@ def test_gpu_position_encoder_matches_pymongo(tz):
         else:
             os.environ["TZ"] = old
         time.tzset()
+
+
+@pytest.mark.parametrize("tz", ["UTC", "EST+5EDT,M3.2.0/2,M11.1.0/2"])
+def test_position_encoder_wide_time_span(tz):
+    """A batch whose latest rows mix a default GPS time (1970-01-01, before the epoch too) with current traffic
+    and a far-future row: only the 900-s buckets the rows use are looked up (no dense span table), and every
+    statement equals pymongo's bytes for the reference's positions_latest op (heatmap_stream.py:211-228)."""
+    import time
+    from mobheat import _lib
+    old = os.environ.get("TZ")
+    os.environ["TZ"] = tz
+    time.tzset()
+    try:
+        ts = np.array([0, -1, 1_000_000 * 86400 * 20000 + 123456, 1759572000_000_000 + 999_999,
+                       1759572000_000_000 + 7 * 900_000_000, 4102444800_000_000], np.int64)
+        n = ts.size
+        df = pd.DataFrame({"provider": ["mbta"] * n, "vehicleId": [f"v{i}" for i in range(n)],
+                           "lat": np.linspace(-60, 60, n), "lon": np.linspace(-170, 170, n), "speedKmh": [1.0] * n,
+                           "eventTs": pd.to_datetime(ts, unit="us")})
+        cols = stream.batch_columns(df)
+        rows = np.arange(n)
+        ids, offs_s = _lib.time_buckets(cols["ts_us"][rows])
+        assert ids.size == 6 and np.all(np.diff(ids) > 0)   # (-1 us lies in bucket -1)
+        buf, offs = _lib.position_statements_selftest(cols["provider_uniques"], cols["vehicle_uniques"],
+                                                      cols["vkey"][rows], cols["ts_us"][rows], cols["lat"][rows],
+                                                      cols["lon"][rows])
+        exp = [bson.encode({"q": op._filter, "u": op._doc, "multi": False, "upsert": True})
+               for op in stream.position_ops(cols, rows)]
+        assert [buf[offs[i]:offs[i + 1]].tobytes() for i in range(n)] == exp
+    finally:
+        if old is None:
+            del os.environ["TZ"]
+        else:
+            os.environ["TZ"] = old
+        time.tzset()
+
+
+def test_failed_writes_and_replays_do_not_merge_twice(tmp_path, monkeypatch):
+    """CPU, host logic of foreach_batch_func: a batch whose Mongo writes fail must not leave its rows in the
+    state (Spark re-runs the epoch: reference heatmap_stream.py:192-235 raise, :249), and an epoch the live engine
+    already merged is re-run on the state of the epoch before it, not on top of itself."""
+    created, merged = [], []
+
+    class FakeEngine:
+        def __init__(self, **kw):
+            self.epochs = []
+            created.append(self)
+
+        def load_state(self, path):
+            self.epochs.append(("loaded", os.path.basename(path)))
+
+        def process_batch(self, epoch_id, *a, **kw):
+            self.epochs.append(epoch_id)
+            merged.append(epoch_id)
+
+            class R:
+                latest_rows = np.zeros(0, np.int64)
+            return R()
+
+        def encode_tile_updates(self, city, ttl):
+            doc = np.frombuffer(bson.encode({"q": {"_id": "x"}}), np.uint8)
+            return doc, np.array([0, doc.size], np.int64)
+
+        def save_state(self, path):
+            open(path, "wb").close()
+
+        def close(self):
+            pass
+
+    fail = {"on": False}
+
+    class Sink:
+        def update_raw(self, coll, statements):
+            if fail["on"]:
+                raise IOError("mongo down")
+
+        def close(self):
+            pass
+
+    monkeypatch.setattr(stream, "HeatmapEngine", FakeEngine)
+    monkeypatch.setattr(stream, "SINK_FACTORY", Sink)
+    monkeypatch.setattr(stream, "CHECKPOINT_DIR", str(tmp_path))
+    monkeypatch.setattr(stream, "STATE_CHECKPOINT", True)
+    df = pd.DataFrame({"provider": ["p"], "vehicleId": ["v"], "lat": [1.0], "lon": [2.0], "speedKmh": [3.0],
+                       "eventTs": pd.to_datetime([1759572000], unit="s")})
+    stream.reset_engine()
+    stream.foreach_batch_func(df, 0)
+    stream.foreach_batch_func(df, 1)
+    assert len(created) == 1 and created[0].epochs == [0, 1]
+    fail["on"] = True
+    with pytest.raises(IOError):
+        stream.foreach_batch_func(df, 2)
+    assert stream._ENGINE is None                        # the state holding epoch 2 was dropped
+    fail["on"] = False
+    stream.foreach_batch_func(df, 2)                     # the retry: a new engine from the checkpoint of epoch 1
+    assert created[-1].epochs == [("loaded", "state-1.npz"), 2]
+    stream.foreach_batch_func(df, 2)                     # a replay of a merged epoch in the same process
+    assert created[-1].epochs == [("loaded", "state-1.npz"), 2] and len(created) == 3
+    stream.reset_engine()
