@@ -5,13 +5,16 @@ Workload (N=1 and per rank for N>1, weak scaling): BASELINE.json configs[1] shap
 OpenSky-like global batch of 1e8 events uniform on the sphere, 50k vehicle ids, 15 minutes of event time
 (3 five-minute windows), 10% null speeds -- at the metric's H3 resolution 8 (configs[1] quotes res 7;
 --res 7 runs that).  One step = one micro-batch through the whole hot path on device-resident inputs:
-one fused pass over the events (k_ingest: filter + latLngToCell + window + late test + LDS pre-aggregation +
-per-vehicle max ts + census of the partials per window, which sizes the per-window state tables), radix partition
-into (window, region) bins, the region-owned merge into the persistent update-mode state that also writes the
-update-mode rows (k_merge_owned), in-place densification of the rows (k_fill_gaps), eviction (whole window tables released), and
-the latest-position flags + compaction.
+one fused pass over the events (k_ingest: filter + latLngToCell + window + late test + per-vehicle max ts + one
+event key per row + census of the rows per window, which sizes the per-window state tables), then either the direct
+path (radix partition of the rows into (window, region) bins, the region-owned merge into the persistent
+update-mode state that also writes the update-mode rows) or, for low-cardinality batches, table mode (two LDS
+aggregation passes first); in-place densification of the rows (k_fill_gaps), eviction (whole window tables
+released), and the latest-position flags + compaction.
 Every step is a NEW micro-batch: its timestamps are the previous step's + 15 min (precomputed before the
-timed region), so the stream advances, windows close and are evicted, and no row is late.
+timed region), so the stream advances, windows close and are evicted, and no row is late.  A second leg
+(`state_read_leg`, N=1 only) times the regime where batches update open windows: 1 minute of event time per step,
+advancing 1 minute, res 7.
 For N>1 each rank runs the sharded path (mobheat.distributed: RCCL all-to-all of partials by owner).
 
 Prints ONE JSON line (rank 0).  See DESIGN.md for the roofline's algorithmic-byte accounting.
@@ -36,21 +39,34 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector peak: 1024 SIMDs x 16 FMA lanes x 2 x 2.4 GHz
 SIMDS, CLOCK_HZ = 1024, 2.4e9
 
-# algorithmic HBM bytes per unit: per event (ingest, dedup), per partial record (partition,
-# merge), per emitted tile (emit = the row compaction).  ingest also writes 48 B per partial (added below).
-BYTES = {
-    "ingest": 43,      # read lat 8 + lon 8 + ts 8 + speed 8 + speed_valid 1 + vkey 8 + row_valid 1; write flags 1
-    "partition": 160,  # per partial: histogram read 48 B + scatter read 48 B + scatter write of the 64-B SortedRec
-    "merge": 177,      # per partial: read the 64-B SortedRec, write the 64 B state line (a new key: its slot tag
-                       # is in LDS, nothing read) and the 49 B update-mode row
-    "emit": 98,        # per gap filled: a 49-B row read from above the dense size and written into the gap
-    "dedup": 20,       # per event: vkey 8 + ts 8 + flags 1 read, win flag 1 written, 2 x 1 B compaction reads
-}
-# HBM traffic per dispatch of every kernel and k_ingest's VALU instruction mix per event of this workload were
-# counted by rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r1/kernel_pmc.json).
-PMC_FILE = os.path.join(ROOT, "profiles", "r1", "kernel_pmc.json")
-STAGE_KERNELS = {"ingest": ["k_ingest"], "partition": ["k_rp_hist", "k_rp_scatter"], "merge": ["k_merge_owned"],
-                 "emit": ["k_fill_gaps"], "dedup": ["k_dedup_flag"]}
+# Algorithmic HBM bytes of each stage, from the batch's counts (hm_last_counts): n events, R partial
+# records merged (direct path: one per aggregated row), T tiles emitted, E of them keys that existed before the batch
+# (their 64-B state line is read).
+#   direct path   ingest 42/event (lat, lon, ts, vkey 8 each + row_valid 1 read; flags 1 + event key 8 written)
+#                 partition 16/event (k_ev_hist and k_ev_scatter read the key) + 65/record (speed, speed_valid,
+#                           lat, lon read: 33; the 32-B EventRec written)
+#                 merge 32/record read + 113/tile (64-B state line + 49-B row written) + 64/pre-existing key read
+#                 emit 98/gap (a 49-B row moved into a gap; gaps = R - T), dedup 20/event
+#   table mode    aggregate 41/event + 48/record, partition 160/record (48 + 48 read, 64 written), merge 64/record
+#                 read + 113/tile + 64/pre-existing key
+def stage_bytes(n, c):
+    R, T = c["partials"], c["tiles"]
+    E = max(T - c["state_new"], 0)
+    b = {"ingest": 42 * n, "dedup": 20 * n, "emit": 98 * max(R - T, 0)}
+    if c["table_mode"]:
+        b.update(aggregate=41 * n + 48 * R, partition=160 * R, merge=64 * R + 113 * T + 64 * E)
+    else:
+        b.update(aggregate=0, partition=16 * n + 65 * R, merge=32 * R + 113 * T + 64 * E)
+    return b
+
+
+STAGES = ["ingest", "aggregate", "partition", "merge", "emit", "dedup"]
+# HBM traffic per dispatch of every kernel and k_ingest's VALU instruction mix per event of this workload, counted by
+# rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r2/kernel_pmc.json).
+PMC_FILE = os.path.join(ROOT, "profiles", "r2", "kernel_pmc.json")
+STAGE_KERNELS = {"ingest": ["k_ingest"], "aggregate": ["k_agg", "k_bin_reduce"],
+                 "partition": ["k_ev_hist", "k_ev_scatter"], "merge": ["k_merge_owned"], "emit": ["k_fill_gaps"],
+                 "dedup": ["k_dedup_flag"]}
 
 
 def ingest_pmc(res, n, world):
@@ -62,14 +78,15 @@ def ingest_pmc(res, n, world):
     return d if d.get("h3_res") == res and d.get("events_per_dispatch") == n and world == 1 else None
 
 
-def gen_batch(n, steps, seed, dev):
-    """C2-shaped batch generated on the device (inputs resident in HBM before timing)."""
+def gen_batch(n, steps, seed, dev, span_us=SPAN_US, advance_us=SPAN_US):
+    """C2-shaped batch generated on the device (inputs resident in HBM before timing); step s's timestamps are
+    step 0's + s * advance_us."""
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
     lat = torch.rad2deg(torch.asin(torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 2 - 1))
     lon = torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 360.0 - 180.0
-    base = T0 + torch.randint(0, SPAN_US, (n,), generator=g, device=dev, dtype=torch.int64)
-    ts = [base + s * SPAN_US for s in range(steps)]
+    base = T0 + torch.randint(0, span_us, (n,), generator=g, device=dev, dtype=torch.int64)
+    ts = [base + s * advance_us for s in range(steps)]
     speed = torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 80.0
     sv = (torch.rand(n, generator=g, device=dev) >= 0.10).to(torch.uint8)
     vkey = torch.randint(0, 50_000, (n,), generator=g, device=dev, dtype=torch.int64)
@@ -96,6 +113,62 @@ def cpu_baseline(sample, res):
                       f"{dt:.1f} s"}
 
 
+def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank):
+    """Warmup + exactly K timed steps (barrier + synchronize on both sides, max over ranks); per-stage HIP-event
+    times (the library's events on its own stream) and algorithmic bytes of the timed steps."""
+    import mobheat
+    from mobheat.distributed import LibStages, ShardedHeatmap
+    total_steps = args.warmup + args.steps
+    data = gen_batch(n, total_steps, seed=seed, dev=dev, span_us=span_us, advance_us=advance_us)
+    eng = mobheat.HeatmapEngine(h3_res=res, device=local, batch_capacity_hint=n)
+    sharded = ShardedHeatmap(LibStages(eng), dev) if world > 1 else None
+
+    def step(s):
+        ptrs = dict(n=n, lat=data["lat"].data_ptr(), lon=data["lon"].data_ptr(), ts_us=data["ts"][s].data_ptr(),
+                    speed=data["speed"].data_ptr(), speed_valid=data["sv"].data_ptr(), vkey=data["vkey"].data_ptr(),
+                    row_valid=data["rv"].data_ptr())
+        if sharded is None:
+            return eng.process_batch_device(s, **ptrs)
+        return sharded.process_batch(s, ptrs)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kt = {k: 0.0 for k in STAGES}
+    kb = {k: 0.0 for k in STAGES}
+    step_ms = []
+    counts = None
+    t0 = time.perf_counter()
+    for s in range(args.warmup, total_steps):
+        ts0 = time.perf_counter()
+        step(s)
+        step_ms.append((time.perf_counter() - ts0) * 1e3)
+        tm = eng.last_timings()
+        counts = eng.last_counts()
+        for k in STAGES:
+            kt[k] += max(tm[k], 0.0)
+        for k, v in stage_bytes(n, counts).items():
+            kb[k] += v
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    eng.close()
+    del data
+    torch.cuda.empty_cache()
+    K = args.steps
+    return dict(elapsed=elapsed, step_ms=step_ms, kt={k: v / K for k, v in kt.items()},
+                kb={k: v / K for k, v in kb.items()}, counts=counts)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -105,6 +178,7 @@ def main():
     ap.add_argument("--res", type=int, default=8)
     ap.add_argument("--cpu-sample", type=int, default=3_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-state-leg", action="store_true", help="skip the 1-minute-advance state-read leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -122,61 +196,15 @@ def main():
         backend = os.environ.get("MOBHEAT_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
 
-    import mobheat
-    from mobheat.distributed import LibStages, ShardedHeatmap
     n = args.events
-    total_steps = args.warmup + args.steps
-    data = gen_batch(n, total_steps, seed=1 + 7919 * rank, dev=dev)
-    eng = mobheat.HeatmapEngine(h3_res=args.res, device=local, batch_capacity_hint=n)
-    sharded = ShardedHeatmap(LibStages(eng), dev) if world > 1 else None
-
-    def step(s):
-        ptrs = dict(n=n, lat=data["lat"].data_ptr(), lon=data["lon"].data_ptr(), ts_us=data["ts"][s].data_ptr(),
-                    speed=data["speed"].data_ptr(), speed_valid=data["sv"].data_ptr(), vkey=data["vkey"].data_ptr(),
-                    row_valid=data["rv"].data_ptr())
-        if sharded is None:
-            return eng.process_batch_device(s, **ptrs)
-        return sharded.process_batch(s, ptrs)
-
-    for s in range(args.warmup):
-        step(s)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    kt = {k: 0.0 for k in BYTES}
-    t0 = time.perf_counter()
-    last = None
-    step_ms = []
-    for s in range(args.warmup, total_steps):
-        ts0 = time.perf_counter()
-        last = step(s)
-        step_ms.append((time.perf_counter() - ts0) * 1e3)
-        tm = eng.last_timings()
-        for k in BYTES:
-            kt[k] += tm[k]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-
     K = args.steps
-    avg_ms = {k: v / K for k, v in kt.items()}
-    n_tiles = int(last.n_tiles) if last is not None else 0
-    n_parts = int(last.n_partials) if last is not None else 0
-    units = {"ingest": n, "dedup": n, "partition": n_parts, "merge": n_parts, "emit": max(n_parts - n_tiles, 0)}
-    launch_bytes = {k: BYTES[k] * units[k] for k in BYTES}
-    launch_bytes["ingest"] += 48 * n_parts
-    dom = max(BYTES, key=lambda k: avg_ms[k])
-    gbs = launch_bytes[dom] / (avg_ms[dom] * 1e-3) / 1e9 if avg_ms[dom] > 0 else 0.0
-    # Roofline of the dominant kernel, priced on HBM (the metric's "% HBM peak").  For k_ingest the PMC file
-    # (rocprofv3 passes of this same command, tools/ingest_pmc.py) adds the measured HBM traffic and the VALU
-    # side: k_ingest is VALU/latency bound, so the HBM fraction alone understates how busy it is.
+    A = run_leg(args, n, args.res, SPAN_US, SPAN_US, 1 + 7919 * rank, dev, local, world, rank)
+    elapsed, avg_ms, kb, c = A["elapsed"], A["kt"], A["kb"], A["counts"]
+    ms_step = elapsed / K * 1e3
+    # Roofline of the dominant stage by time, priced on HBM (the metric's "% HBM peak"), with the PMC-counted
+    # traffic of its kernels when the PMC file was taken on this exact workload (tools/ingest_pmc.py).
+    dom = max(STAGES, key=lambda k: avg_ms[k])
+    gbs = kb[dom] / (avg_ms[dom] * 1e-3) / 1e9 if avg_ms[dom] > 0 else 0.0
     roof = {"bound": "hbm", "kernel": dom, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": gbs / HBM_PEAK_GBS, "traffic": None}
     pmc = ingest_pmc(args.res, n, world)
@@ -184,34 +212,54 @@ def main():
         # FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, per dispatch, summed over the stage's kernels
         roof["traffic"] = sum(pmc["kernels"][k]["hbm_bytes"] for k in STAGE_KERNELS[dom])
         roof["traffic_source"] = os.path.relpath(PMC_FILE, ROOT)
-    if pmc is not None and dom == "ingest":
-        sec = avg_ms[dom] * 1e-3
+    if pmc is not None:
+        # k_ingest is bound by VALU issue and latency, not HBM: its VALU side from the same PMC file
+        sec = avg_ms["ingest"] * 1e-3
         tf = pmc["fp64_flops_per_event"] * n / sec / 1e12
         # VALU issue: SIMD-32 pipes, 2 cycles per wave64 32-bit op, 4 per fp64 op (MI355X_MICROARCH.md)
         simd_cycles = (pmc["valu_f64_insts_per_event"] * 4 + pmc["valu_other_insts_per_event"] * 2) * n / 64
-        roof["valu"] = {"fp64_tflops": tf, "fp64_peak_tflops": FP64_PEAK_TFLOPS, "fp64_frac": tf / FP64_PEAK_TFLOPS,
-                        "issue_frac": simd_cycles / (SIMDS * CLOCK_HZ * sec),
-                        "valu_insts_per_event": pmc["valu_insts_per_event"],
-                        "fp64_flops_per_event": pmc["fp64_flops_per_event"]}
-    roof.update({"kernel_ms": {k: round(v, 3) for k, v in avg_ms.items()}, "algorithmic_bytes_per_launch": launch_bytes[dom],
-                 "units_per_launch": units[dom]})
+        roof["ingest_valu"] = {"fp64_tflops": tf, "fp64_peak_tflops": FP64_PEAK_TFLOPS, "fp64_frac": tf / FP64_PEAK_TFLOPS,
+                               "issue_frac": simd_cycles / (SIMDS * CLOCK_HZ * sec),
+                               "valu_insts_per_event": pmc["valu_insts_per_event"],
+                               "fp64_flops_per_event": pmc["fp64_flops_per_event"]}
+    step_bytes = sum(kb.values())
+    roof.update({"kernel_ms": {k: round(v, 3) for k, v in avg_ms.items()}, "algorithmic_bytes_per_launch": kb[dom],
+                 "units_per_launch": {"events": n, "records": c["partials"], "tiles": c["tiles"]},
+                 # the whole step: every stage's algorithmic bytes / the step's wall time / 8 TB/s
+                 "step": {"algorithmic_bytes": step_bytes, "ms": ms_step,
+                          "achieved_gbs": step_bytes / (ms_step * 1e-3) / 1e9,
+                          "frac": step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS}})
     value = world * n * K / elapsed
     out = {
         "metric": METRIC, "value": value, "unit": "events/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
-        "ms_per_step": elapsed / K * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f64", "data": "synthetic",
         "config": {"workload": f"C2-shaped global batch: {n:,} events/step/GPU uniform on the sphere, 50k vehicles, "
                                f"15 min of event time (3 windows) per step, advancing 15 min per step; H3 res {args.res}",
                    "events_per_step_per_gpu": n, "h3_res": args.res, "parallelism": f"dp{world}",
-                   "tiles_emitted_last_step": n_tiles, "partials_last_step": n_parts},
+                   "tiles_emitted_last_step": c["tiles"], "partials_last_step": c["partials"],
+                   "table_mode": c["table_mode"]},
         "roofline": roof,
     }
+    if world == 1 and not args.no_state_leg:
+        # second leg: the state-read regime of the reference's ~2-s trigger (README.md:134-135) -- each micro-batch
+        # holds 1 minute of event time and the stream advances 1 minute per step, so consecutive batches update the
+        # same open windows and the merge reads existing state lines.  res 7 (configs[1]'s resolution): 1e8 events
+        # per minute re-touch most of a window's keys from its second batch on.
+        B = run_leg(args, n, 7, 60_000_000, 60_000_000, 2, dev, local, world, rank)
+        bms = B["elapsed"] / K * 1e3
+        bb = sum(B["kb"].values())
+        out["state_read_leg"] = {
+            "value": n * K / B["elapsed"], "unit": "events/s", "ms_per_step": bms, "h3_res": 7,
+            "workload": f"{n:,} events/step uniform on the sphere, 1 min of event time per step, advancing 1 min per step",
+            "kernel_ms": {k: round(v, 3) for k, v in B["kt"].items()},
+            "tiles_last_step": B["counts"]["tiles"], "state_keys_created_last_step": B["counts"]["state_new"],
+            "step_frac": bb / (bms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.res)
     if rank == 0:
-        print("per-step ms (host wall, rank 0): " + " ".join(f"{x:.1f}" for x in step_ms), file=sys.stderr, flush=True)
+        print("per-step ms (host wall, rank 0): " + " ".join(f"{x:.1f}" for x in A["step_ms"]), file=sys.stderr, flush=True)
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

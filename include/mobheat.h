@@ -275,6 +275,10 @@ int hm_selftest_position_statements(const hm_position_doc_cfg *cfg, const uint64
  * (0), 2 merge, 3 emit, 4 dedup (flag + compaction), 5 total, 6 region partition. */
 int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n);
 
+/* Counts of the last hm_process_batch (up to n of them): [0] keys created in the tile state, [1] partial records
+ * merged (direct path: aggregated rows; table mode: ~ distinct keys), [2] tiles emitted, [3] 1 if table mode ran. */
+int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n);
+
 /* HM_ABI_VERSION the library was built with (callers check it before hm_create). */
 int32_t hm_abi_version(void);
 

@@ -1768,6 +1768,43 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
     }
 }
 
+// Heavy hitters in the batch's event keys, for the choice of the aggregation path when the last batch says nothing
+// (the first batch, or a sudden change of the data): HS_SAMPLE keys at an even stride, bitonic-sorted in LDS, the
+// longest run of equal keys -> DevStats.sample_max_run.  A key holding a few % of the rows would put that share of the
+// batch through one merge workgroup (one bin) on the direct path; table mode aggregates it in LDS first.
+constexpr int HS_SAMPLE = 4096, HS_THREADS = 1024;
+__global__ __launch_bounds__(HS_THREADS) void k_sample_heavy(const uint64_t *__restrict__ keys, int64_t n, DevStats *st) {
+    __shared__ unsigned long long k[HS_SAMPLE];
+    __shared__ unsigned best;
+    const int t = threadIdx.x;
+    const int64_t stride = n / HS_SAMPLE > 0 ? n / HS_SAMPLE : 1;
+    for (int q = t; q < HS_SAMPLE; q += HS_THREADS) {
+        const int64_t i = (int64_t)q * stride;
+        const uint64_t v = i < n ? keys[i] : 0;
+        k[q] = v ? v : ~0ull;   // rows without a key sort last and are not counted
+    }
+    if (t == 0) best = 0;
+    __syncthreads();
+    for (int size = 2; size <= HS_SAMPLE; size <<= 1)
+        for (int stride2 = size >> 1; stride2 > 0; stride2 >>= 1) {
+            for (int q = t; q < HS_SAMPLE / 2; q += HS_THREADS) {
+                const int lo = 2 * q - (q & (stride2 - 1)), hi = lo + stride2;
+                const bool up = (lo & size) == 0;
+                const unsigned long long a = k[lo], b = k[hi];
+                if ((a > b) == up) { k[lo] = b; k[hi] = a; }
+            }
+            __syncthreads();
+        }
+    for (int q = t; q < HS_SAMPLE; q += HS_THREADS) {
+        if (k[q] == ~0ull || (q > 0 && k[q - 1] == k[q])) continue;   // q starts a run of a real key
+        int e = q + 1;
+        while (e < HS_SAMPLE && k[e] == k[q]) e++;
+        atomicMax(&best, (unsigned)(e - q));
+    }
+    __syncthreads();
+    if (t == 0) st->sample_max_run = best;
+}
+
 // =====================================================================================================
 // ordered compaction of a 0/1 byte array -> indices (deterministic, ascending)
 // =====================================================================================================
@@ -1996,6 +2033,7 @@ struct hm_ctx {
     int ingest_mode = 0;
     int64_t prev_agg_rows = 0, prev_keys = 0;   // aggregated rows and distinct keys of the last batch
     bool last_table = false;
+    int64_t last_counts[4] = {0, 0, 0, 0};   // hm_last_counts
     DevBuf keys;                     // k_ingest's event key per row (kernels.h ekey)
     unsigned long long *d_wreg = nullptr, *h_wreg = nullptr;     // the batch's window registry (WREG_SLOTS wenc)
     unsigned long long *d_wcount = nullptr, *h_wcount = nullptr; // aggregated rows per registry slot (census)
@@ -2117,7 +2155,15 @@ static int ilog2(uint64_t v) { return 63 - __builtin_clzll(v); }
 // Geometry of a window's table for `keys` keys receiving `parts` partials per batch: load <= 1/2, regions of
 // >= 2^REGION_MIN_BITS slots, and enough regions that one merge workgroup gets <= ~16k of the window's partials
 // (a hot window with few keys is still merged in parallel).
+// H3 cells at a resolution (2 + 120 * 7^res): no window can hold more keys than that
+static int64_t h3_cells_at(int res) {
+    int64_t c = 120;
+    for (int r = 0; r < res; r++) c *= 7;
+    return c + 2;
+}
+
 static void gen_geometry(const hm_ctx *ctx, int64_t keys, int64_t parts, int min_log2, int &log2cap, unsigned &rbits) {
+    keys = std::min(keys, h3_cells_at(ctx->cfg.h3_res));   // (the census bounds keys by rows; the grid bounds them too)
     int L = ilog2(next_pow2((uint64_t)std::max<int64_t>(2 * keys, 1024)));
     const int want_rb = std::min(RP_BITS, ilog2(next_pow2((uint64_t)std::max<int64_t>((parts + 16383) / 16384, 1))));
     L = std::max({L, want_rb + REGION_MIN_BITS, min_log2});
@@ -2387,7 +2433,7 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census) {
             ctx->gens.push_back({w.wenc, t, L, rb, 0, c});
             continue;
         }
-        if ((it->keys + c) * 2 > (int64_t(1) << it->log2cap)) {
+        if (std::min(it->keys + c, h3_cells_at(ctx->cfg.h3_res)) * 2 > (int64_t(1) << it->log2cap)) {
             gen_geometry(ctx, it->keys + c, c, it->log2cap + 1, L, rb);
             TileSlot *t = nullptr;
             if ((rc = table_acquire(ctx, L, rb, &t))) return rc;
@@ -2558,6 +2604,7 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
                            ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st);
         hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, ctx->cfg.h3_res,
                            (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, (uint64_t *)ctx->keys.p);
+        hipLaunchKernelGGL(k_sample_heavy, dim3(1), dim3(HS_THREADS), 0, ctx->stream, (const uint64_t *)ctx->keys.p, n, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
         ctx->dfused.dirty = true;
     }
@@ -2574,11 +2621,13 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
 }
 
 // Aggregation path of the batch: table mode when the last batches had few distinct keys that repeat a lot (their
-// aggregates fit k_bin_reduce's LDS tables), else the direct path.
-static bool choose_table(const hm_ctx *ctx, int64_t n_agg) {
+// aggregates fit k_bin_reduce's LDS tables), or when this batch's key sample shows heavy hitters (a key in >= 1/256
+// of the sampled rows: k_sample_heavy), else the direct path.
+static bool choose_table(const hm_ctx *ctx, int64_t n_agg, unsigned long long sample_max_run) {
     if (ctx->ingest_mode) return ctx->ingest_mode == 2;
-    return n_agg >= (int64_t(1) << 16) && ctx->prev_keys > 0 && ctx->prev_keys <= (int64_t)AG_BINS * (AG_SLOTS / 2) &&
-           ctx->prev_agg_rows >= 8 * ctx->prev_keys;
+    if (n_agg < (int64_t(1) << 16)) return false;
+    if (sample_max_run >= (unsigned long long)(HS_SAMPLE / 256)) return true;
+    return ctx->prev_keys > 0 && ctx->prev_keys <= (int64_t)AG_BINS * (AG_SLOTS / 2) && ctx->prev_agg_rows >= 8 * ctx->prev_keys;
 }
 
 // table mode: k_agg + k_bin_reduce -> one partial record per key of the batch (ctx->partials, count *n_parts),
@@ -3008,6 +3057,12 @@ int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n) {
     return HM_OK;
 }
 
+int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n) {
+    if (!ctx || !c) return HM_E_INVALID;
+    for (int i = 0; i < n && i < 4; i++) c[i] = ctx->last_counts[i];
+    return HM_OK;
+}
+
 int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t out_memory, hm_batch_out *out) {
     if (!ctx || !in || !out || in->n < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
     if (in->n > (int64_t)UINT32_MAX - 1) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds 2^32-2", (long long)in->n);
@@ -3028,7 +3083,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     DevStats s1 = *ctx->h_st;
     const int64_t n_agg = (int64_t)s1.n_valid - (int64_t)s1.n_late;
     // 3. aggregate, merge into state + emit (table mode: two LDS passes first; direct: every row a record)
-    const bool table = choose_table(ctx, n_agg);
+    const bool table = choose_table(ctx, n_agg, s1.sample_max_run);
     ctx->last_table = table;
     if (table) {
         int64_t n_parts = 0;
@@ -3057,6 +3112,10 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     ctx->last_lon = I.lon;
     record_timings(ctx);
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, n_rows, (const int64_t *)ctx->rows.p, out_memory, out))) return rc;
+    ctx->last_counts[0] = (int64_t)s2.n_state_new;
+    ctx->last_counts[1] = ctx->n_partials_merged;
+    ctx->last_counts[2] = (int64_t)s2.n_touched;
+    ctx->last_counts[3] = table ? 1 : 0;
     // the next batch's aggregation path is chosen from this one's cardinality
     if (n_agg >= (int64_t(1) << 16)) {
         ctx->prev_agg_rows = n_agg;
@@ -3137,7 +3196,7 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     const DevStats s1 = *ctx->h_st;
     const int64_t n_agg = (int64_t)s1.n_valid - (int64_t)s1.n_late;
     // tile partials: table mode aggregates the shard first (one record per key); the direct path sends every row
-    const bool table = choose_table(ctx, n_agg);
+    const bool table = choose_table(ctx, n_agg, s1.sample_max_run);
     ctx->last_table = table;
     int64_t n_records = n_agg;
     if (table && (rc = phase_table(ctx, I, n_agg, &n_records))) return rc;

@@ -104,6 +104,7 @@ SIGNATURES = {
     "hm_selftest_position_statements": (c_i32, [_P(HmPositionDocCfg), c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
                                                 c_vp]),
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
+    "hm_last_counts": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_abi_version": (c_i32, []),
 }
 

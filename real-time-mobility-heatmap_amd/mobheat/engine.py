@@ -190,6 +190,11 @@ class HeatmapEngine:
         return {"ingest": ms[0], "aggregate": ms[1], "merge": ms[2], "emit": ms[3], "dedup": ms[4], "total": ms[5],
                 "partition": ms[6]}
 
+    def last_counts(self):
+        c = (ctypes.c_int64 * 4)()
+        check(self._lib.hm_last_counts(self._ctx, c, 4), self._ctx)
+        return {"state_new": c[0], "partials": c[1], "tiles": c[2], "table_mode": bool(c[3])}
+
     def _result_from_host(self, out, copy=True):
         def arr(p, n, dt):
             if n == 0 or not p:

@@ -100,30 +100,59 @@ def reset_engine():
 
 # ------------------ sinks ------------------
 class MongoSink:
-    """Per-batch MongoClient, like the reference (:156-157, :237)."""
+    """Per-batch connection, like the reference's MongoClient (:156-157, :237).  A plain ``mongodb://host:port`` URI
+    (the reference's default) is written through ``wire.WireMongoSink``: each command's statements leave as one slice
+    of the GPU-encoded buffer.  Any other URI (credentials, TLS, replica sets, options) goes through pymongo."""
 
     def __init__(self, uri=None, db=None):
-        from pymongo import MongoClient
-        self._client = MongoClient(uri or MONGO_URI)
-        self._db = self._client[db or MONGO_DB]
+        from . import wire
+        uri = uri or MONGO_URI
+        self._dbname = db or MONGO_DB
+        self._wire = None
+        self._client = None
+        plain = wire.plain_uri(uri) if wire.wire_enabled() else None
+        if plain is not None:
+            self._wire = wire.WireMongoSink(plain[0], plain[1], self._dbname)
+        else:
+            from pymongo import MongoClient
+            self._client = MongoClient(uri)
+            self._db = self._client[self._dbname]
 
     def bulk_write(self, collection, ops):
         self._db[collection].bulk_write(ops, ordered=False)
 
+    def update_statements(self, collection, buf, offs):
+        """Pre-encoded update statements (bytes buf, offsets[n+1]) in unordered commands of <= BULK_CHUNK."""
+        if self._wire is not None:
+            self._wire.update_statements(collection, buf, offs)
+            return
+        from bson.raw_bson import RawBSONDocument
+        from . import wire
+        o = np.asarray(offs, dtype=np.int64)
+        # pymongo checks a command against maxBsonObjectSize + 16 KiB: split by bytes as well as by count
+        for i, j in wire.chunks(o, 16 * 1024 * 1024 - 64 * 1024, BULK_CHUNK):
+            self.update_raw(collection, [RawBSONDocument(buf[o[k]:o[k + 1]].tobytes()) for k in range(i, j)])
+
     def update_raw(self, collection, statements):
         """One unordered `update` command of pre-encoded statements (RawBSONDocument): the command pymongo's
-        bulk_write(ordered=False) sends for the same UpdateOne ops; write errors raise BulkWriteError like it."""
+        bulk_write(ordered=False) sends for the same UpdateOne ops, with the collection's write concern; write
+        errors raise BulkWriteError like it."""
         from bson.son import SON
-        from pymongo.errors import BulkWriteError
-        res = self._db.command(SON([("update", collection), ("updates", statements), ("ordered", False)]))
-        if res.get("writeErrors") or res.get("writeConcernError"):
-            raise BulkWriteError({"writeErrors": list(res.get("writeErrors", [])),
-                                  "writeConcernErrors": [res["writeConcernError"]] if res.get("writeConcernError") else [],
-                                  "nInserted": 0, "nUpserted": len(res.get("upserted", [])), "nMatched": res.get("n", 0),
-                                  "nModified": res.get("nModified", 0), "nRemoved": 0, "upserted": res.get("upserted", [])})
+        from . import wire
+        cmd = SON([("update", collection), ("updates", statements), ("ordered", False)])
+        try:
+            wc = self._db[collection].write_concern.document
+        except (TypeError, AttributeError, KeyError):
+            wc = None
+        if wc:
+            cmd["writeConcern"] = wc
+        wire.raise_write_errors(self._db.command(cmd))
 
     def close(self):
-        self._client.close()
+        if self._wire is not None:
+            self._wire.close()
+        if self._client is not None:
+            self._client.close()
 
 
 SINK_FACTORY = MongoSink   # tests replace this with an in-memory capture sink
@@ -298,9 +327,14 @@ def _flush(sink, collection, ops):
 
 
 def _flush_statements(sink, collection, buf, offs):
-    """Pre-encoded update statements (hm_encode_tile_updates) in unordered batches of BULK_CHUNK (:191-196)."""
+    """Pre-encoded update statements (hm_encode_tile_updates / hm_encode_position_updates) in unordered batches of
+    BULK_CHUNK (:191-196, :230-235): the sink's update_statements when it has one (MongoSink), else one update_raw
+    per chunk (capture sinks in the tests)."""
+    if hasattr(sink, "update_statements"):
+        sink.update_statements(collection, buf, offs)
+        return
     from bson.raw_bson import RawBSONDocument
-    o = offs.tolist()   # (pymongo encodes RawBSONDocument from bytes only: one copy per statement)
+    o = offs.tolist()
     for i in range(0, len(o) - 1, BULK_CHUNK):
         j = min(i + BULK_CHUNK, len(o) - 1)
         sink.update_raw(collection, [RawBSONDocument(buf[o[k]:o[k + 1]].tobytes()) for k in range(i, j)])

@@ -208,8 +208,9 @@ def test_high_cardinality_res12_two_batches():
 
 
 def test_clustered_city_res9():
-    """C3-shaped batches (Zipf hot spots, res 9): the first batch takes the direct path (no history), the next ones
-    the table mode (few distinct keys, heavily repeated), which must collapse the partials to about the key count."""
+    """C3-shaped batches (Zipf hot spots, res 9): every batch takes the table mode -- the first one because its key
+    sample shows heavy hitters (k_sample_heavy: the hottest key holds ~3% of the rows), the next ones also from the
+    last batch's cardinality -- which must collapse the partials to about the key count."""
     from mobheat import HeatmapEngine, synth
     from oracle.spark_oracle import SparkHeatmapOracle
     eng = HeatmapEngine(h3_res=9)
@@ -219,10 +220,8 @@ def test_clustered_city_res9():
         b["ts_us"] = b["ts_us"] + epoch * 600_000_000
         res, exp = _run(eng, ora, b, epoch)
         assert_batch_equal(res, exp)
-        if epoch == 0:
-            assert res.n_partials == res.n_valid - res.n_late           # direct: one record per aggregated row
-        else:
-            assert res.n_partials <= 4 * len(res.tiles), (res.n_partials, len(res.tiles))   # table mode
+        assert eng.last_counts()["table_mode"]
+        assert res.n_partials <= 4 * len(res.tiles), (res.n_partials, len(res.tiles))
     eng.close()
 
 
@@ -233,6 +232,7 @@ def test_full_size_properties_c2():
     b = synth.c2_global(n=100_000_000)
     eng = HeatmapEngine(h3_res=8)
     res = eng.process_batch(0, **b)
+    assert not eng.last_counts()["table_mode"]                      # uniform keys: no heavy hitter in the sample
     t = res.tiles
     assert res.n_valid == b["lat"].size and res.n_late == 0
     assert int(t.count.sum()) == res.n_valid                       # every valid row lands in exactly one tile

@@ -97,7 +97,7 @@ def test_empty_batch_and_errors():
     buf, offs = eng.encode_tile_updates("ath", 45)
     assert buf.size == 0 and offs.tolist() == [0]
     with pytest.raises(RuntimeError, match="city"):
-        eng.encode_tile_updates("x" * 65, 45)
+        eng.encode_tile_updates("x" * (1 << 20 | 1), 45)   # (a CITY of more than 1 MiB)
     eng.close()
 
 

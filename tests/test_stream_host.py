@@ -251,8 +251,9 @@ def test_statement_batches_and_update_command(monkeypatch):
             cmds.append(bson.decode(bson.encode(cmd)))       # encodable with the raw statements inside
             return DB.reply
 
-    sink = stream.MongoSink.__new__(stream.MongoSink)
+    sink = stream.MongoSink.__new__(stream.MongoSink)   # the pymongo path (a URI with options or credentials)
     sink._db = DB()
+    sink._wire = sink._client = None
     stream._flush_statements(sink, "tiles", buf, offs)
     assert [len(c["updates"]) for c in cmds] == [1000, 1000, 500]
     assert all(list(c) == ["update", "updates", "ordered"] and c["update"] == "tiles" and c["ordered"] is False for c in cmds)
@@ -400,3 +401,81 @@ def test_failed_writes_and_replays_do_not_merge_twice(tmp_path, monkeypatch):
     stream.foreach_batch_func(df, 2)                     # a replay of a merged epoch in the same process
     assert created[-1].epochs == [("loaded", "state-1.npz"), 2] and len(created) == 3
     stream.reset_engine()
+
+
+def test_wire_op_msg_equals_pymongo_and_fake_server():
+    """The wire sink's OP_MSG for a chunk of GPU-encoded statements is byte-identical to the message pymongo builds
+    for the same update command (message._op_msg: section 0 {update, ordered, $db}, section 1 the `updates`
+    sequence); through a fake server on a local socket, chunks of <= 1000 statements arrive intact and write errors
+    raise BulkWriteError like bulk_write (reference heatmap_stream.py:191-196)."""
+    import socket
+    import struct
+    import threading
+    from bson.codec_options import DEFAULT_CODEC_OPTIONS
+    from bson.raw_bson import RawBSONDocument
+    from bson.son import SON
+    from pymongo import message
+    from pymongo.errors import BulkWriteError
+    from mobheat import _lib, wire
+    t = _edge_tiles(np.random.default_rng(6), 2300, 300_000_000, 1759572000_000_000)
+    buf, offs = _lib.tile_statements_selftest(t, "ath", 8, 45, 300_000_000)
+    exp = _reference_statements(t, "ath", 8, 45)
+    docs = [RawBSONDocument(e) for e in exp[:1000]]
+    rid, msg, _, _ = message._op_msg(0, SON([("update", "tiles"), ("updates", docs), ("ordered", False)]), "mobility",
+                                     None, DEFAULT_CODEC_OPTIONS)
+    mine = b"".join(bytes(p) for p in wire.op_msg_parts(rid, wire.command_doc("tiles", "mobility"),
+                                                          memoryview(buf)[:int(offs[1000])]))
+    assert mine == msg
+    assert wire.chunks(offs, 10**9) == [(0, 1000), (1000, 2000), (2000, 2300)]
+    assert wire.chunks(np.array([0, 10, 20, 30, 200]), 25, 1000) == [(0, 2), (2, 3), (3, 4)]
+    assert wire.plain_uri("mongodb://127.0.0.1:27017") == ("127.0.0.1", 27017, None)
+    assert wire.plain_uri("mongodb://u:p@h/db") is None and wire.plain_uri("mongodb://h/?tls=true") is None
+
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    got, fail_on = [], {"chunk": None}
+
+    def serve():
+        c, _ = srv.accept()
+        k = 0
+        while True:
+            h = c.recv(16, socket.MSG_WAITALL)
+            if len(h) < 16:
+                break
+            length, rqid, _, op = struct.unpack("<iiii", h)
+            body = c.recv(length - 16, socket.MSG_WAITALL)
+            clen = struct.unpack_from("<i", body, 5)[0]
+            cmd = bson.decode(body[5:5 + clen])
+            p = 5 + clen
+            assert body[p] == 1
+            slen = struct.unpack_from("<i", body, p + 1)[0]
+            ident_end = body.index(b"\x00", p + 5)
+            assert body[p + 5:ident_end] == b"updates"
+            seq = body[ident_end + 1:p + 1 + slen]
+            n = 0
+            while seq:
+                dl = struct.unpack_from("<i", seq, 0)[0]
+                got.append(seq[:dl])
+                seq = seq[dl:]
+                n += 1
+            assert cmd == {"update": "tiles", "ordered": False, "$db": "mobility"} and n <= 1000
+            reply = {"ok": 1, "n": n}
+            if k == fail_on["chunk"]:
+                reply["writeErrors"] = [{"index": 0, "code": 11000, "errmsg": "E11000 duplicate key"}]
+            rb = bson.encode(reply)
+            c.sendall(struct.pack("<iiiiI", 16 + 5 + len(rb), 99, rqid, 2013, 0) + b"\x00" + rb)
+            k += 1
+        c.close()
+
+    th = threading.Thread(target=serve, daemon=True)
+    th.start()
+    sink = wire.WireMongoSink("127.0.0.1", srv.getsockname()[1], "mobility")
+    sink.update_statements("tiles", buf, offs)
+    assert got == exp
+    fail_on["chunk"] = 3
+    with pytest.raises(BulkWriteError):
+        sink.update_statements("tiles", buf, offs[:11])
+    sink.close()
+    th.join(5)
+    srv.close()
