@@ -1045,10 +1045,13 @@ __global__ __launch_bounds__(AG_THREADS) void k_bin_reduce(const AggRec *__restr
 #endif
 constexpr int MO_THREADS = HM_MO_THREADS;      // partials per chunk (one per lane)
 constexpr int MO_CLAIM = 2 * MO_THREADS;
-#ifndef HM_MO_TAG_BYTES
-#define HM_MO_TAG_BYTES 24576
+#ifndef HM_MO_TAG_MAX
+#define HM_MO_TAG_MAX 90112
 #endif
-constexpr int MO_TAG_BYTES = HM_MO_TAG_BYTES;   // LDS for resident region tags per workgroup
+// LDS for resident region tags per workgroup: dynamic, sized per launch to the regions a bin can receive (the sum
+// over the batch's windows of slots per region, 1 B each) up to MO_TAG_MAX -- 24 KB on the bench (3 windows x 8 K
+// slots: two workgroups per CU), 32 KB for a res-7 window of 2^28 slots, which would otherwise probe through HBM
+constexpr int MO_TAG_MAX = HM_MO_TAG_MAX;
 constexpr int MO_RES_MAX = 16;                   // resident (window, region)s per bin
 
 struct MoShared {
@@ -1071,7 +1074,6 @@ struct MoShared {
     unsigned res_off[MO_RES_MAX];         // byte offset of the region's tags in `tags`
     unsigned res_mask[MO_RES_MAX];        // slots per region - 1
     unsigned res_dirty[MO_RES_MAX];
-    unsigned tags[MO_TAG_BYTES / 4];
 };
 
 template <typename T>
@@ -1175,9 +1177,11 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                                                             const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
                                                             GenDesc *gm, const GenDesc *glist, int n_glist,
                                                             const WInfo *__restrict__ winfo, uint64_t cell_hi,
-                                                            unsigned seq, RowsOut rows, unsigned *bin_cnt, DevStats *st) {
+                                                            unsigned seq, RowsOut rows, unsigned *bin_cnt, DevStats *st,
+                                                            unsigned tag_bytes) {
     constexpr bool rehash = std::is_same<Rec, GrowRec>::value;
     __shared__ MoShared S;
+    extern __shared__ unsigned mo_tags[];   // tag_bytes of resident region tags
     __shared__ WinLds WL;
     __shared__ GenCache C;
     wl_init(WL);
@@ -1203,7 +1207,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                     const unsigned sb = REGION_BITS - g.rbits, smask = (1u << sb) - 1;
                     if (((unsigned)bin & smask) != (window_salt(g.wenc) & smask)) continue;
                     const unsigned slots = (unsigned)g.rmask + 1;
-                    if (nr == MO_RES_MAX || off + slots > (unsigned)MO_TAG_BYTES) continue;
+                    if (nr == MO_RES_MAX || off + slots > tag_bytes) continue;
                     const unsigned long long first = (unsigned long long)((unsigned)bin >> sb) << g.rshift;
                     S.res_we[nr] = g.wenc;
                     S.res_slots[nr] = g.tab + first;
@@ -1223,7 +1227,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
         for (int r = 0; r < nres; r++) {
             const unsigned *src = (const unsigned *)S.res_gtags[r];
             const unsigned w0 = S.res_off[r] >> 2, nw = (S.res_mask[r] + 1) >> 2;
-            for (unsigned q = t; q < nw; q += MO_THREADS) S.tags[w0 + q] = src[q];
+            for (unsigned q = t; q < nw; q += MO_THREADS) mo_tags[w0 + q] = src[q];
         }
         __syncthreads();
         // software pipeline: the next chunk's record is loaded while this chunk is merged
@@ -1266,7 +1270,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                         TileSlot *const sl = base + s;
                         const unsigned long long addr = (unsigned long long)sl;
                         const unsigned bi = off + s, sh = (bi & 3) * 8;
-                        const unsigned b = (__hip_atomic_load(&S.tags[bi >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> sh) & 0xffu;
+                        const unsigned b = (__hip_atomic_load(&mo_tags[bi >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> sh) & 0xffu;
                         if (b == 0 || b == tg) {
                             int x = b == 0 ? -1 : mo_holder(S, addr);
                             bool old_match = false;
@@ -1277,7 +1281,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                                     gslot = sl;
                                     created = b == 0;
                                     if (created) {
-                                        atomicOr(&S.tags[bi >> 2], tg << sh);
+                                        atomicOr(&mo_tags[bi >> 2], tg << sh);
                                         S.res_dirty[r] = 1;
                                     }
                                     done = true;
@@ -1388,7 +1392,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             if (!S.res_dirty[r]) continue;
             unsigned *dst = (unsigned *)S.res_gtags[r];
             const unsigned w0 = S.res_off[r] >> 2, nw = (S.res_mask[r] + 1) >> 2;
-            for (unsigned q = t; q < nw; q += MO_THREADS) dst[q] = S.tags[w0 + q];
+            for (unsigned q = t; q < nw; q += MO_THREADS) dst[q] = mo_tags[w0 + q];
         }
         if (t == 0) { bin_cnt[bin] = S.n_touched; S.n_touched = 0; }
         __syncthreads();
@@ -1618,6 +1622,9 @@ __global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__
 // later rounds skip the fused dedup, which phase_dedup then reruns over the whole batch on a full-size table.
 constexpr unsigned long long DEDUP_FUSED_PROBES = 32;
 constexpr int IG_THREADS = 256;
+#ifndef HM_INGEST_PREFETCH
+#define HM_INGEST_PREFETCH 1
+#endif
 
 // wave-cooperative count: lanes with pred add 1 to cnt[slot] (one LDS add per distinct slot per wave)
 __device__ __forceinline__ void wave_count_slots(bool pred, int slot, unsigned *cnt) {
@@ -1651,9 +1658,41 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     long long tmax = INT64_MIN;
     bool dretry = false;
     int round = 0;
-    for (int64_t base = (int64_t)blockIdx.x * IG_THREADS; base < n; base += (int64_t)gridDim.x * IG_THREADS, round++) {
+    const int64_t gstride = (int64_t)gridDim.x * IG_THREADS;
+#if HM_INGEST_PREFETCH
+    // the next round's columns are loaded while this round computes its cells (software pipelining: the loads'
+    // latency hides behind the fp64 work instead of stalling every round)
+    double nla = 0.0, nlo = 0.0;
+    int64_t nt = 0;
+    unsigned long long nv = EMPTY_VKEY;
+    uint8_t nrv = 1;
+    {
+        const int64_t i0 = (int64_t)blockIdx.x * IG_THREADS + threadIdx.x;
+        if (i0 < n) {
+            nla = __builtin_nontemporal_load(&lat[i0]);
+            nlo = __builtin_nontemporal_load(&lon[i0]);
+            nt = __builtin_nontemporal_load(&ts[i0]);
+            nv = __builtin_nontemporal_load(&vkey[i0]);
+            if (row_valid) nrv = __builtin_nontemporal_load(&row_valid[i0]);
+        }
+    }
+#endif
+    for (int64_t base = (int64_t)blockIdx.x * IG_THREADS; base < n; base += gstride, round++) {
         const int64_t i = base + threadIdx.x;
         const bool in = i < n;
+#if HM_INGEST_PREFETCH
+        const double la = nla, lo = nlo;
+        const int64_t t = nt;
+        const unsigned long long v = nv;
+        const bool rv = nrv != 0;
+        if (i + gstride < n) {
+            nla = __builtin_nontemporal_load(&lat[i + gstride]);
+            nlo = __builtin_nontemporal_load(&lon[i + gstride]);
+            nt = __builtin_nontemporal_load(&ts[i + gstride]);
+            nv = __builtin_nontemporal_load(&vkey[i + gstride]);
+            if (row_valid) nrv = __builtin_nontemporal_load(&row_valid[i + gstride]);
+        }
+#else
         double la = 0.0, lo = 0.0;
         int64_t t = 0;
         unsigned long long v = EMPTY_VKEY;
@@ -1665,6 +1704,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
             v = vkey[i];
             if (row_valid) rv = row_valid[i] != 0;
         }
+#endif
         const bool ok = in && rv && la >= -90.0 && la <= 90.0 && lo >= -180.0 && lo <= 180.0 &&
                         t > INT64_MIN + 2 * tile_us && t < INT64_MAX - 2 * tile_us;
         // dedup: the vkey's home slot is loaded now, its latency hidden behind the cell computation (a plain load:
@@ -2349,10 +2389,18 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles) {
             (rc = ensure(ctx, ctx->s_lat, m * 8)))
             return rc;
     }
-    hipLaunchKernelGGL(k_merge_owned<Rec>, dim3(RP_BINS), dim3(MO_THREADS), 0, ctx->stream, (const Rec *)ctx->parts_sorted.p, n_rows,
+    // resident tags: every window merged into this batch may have a region in a bin
+    unsigned tag_bytes = 0;
+    if (!rehash) {
+        size_t need = 0;
+        for (const auto &g : ctx->gens)
+            if (g.batch_parts) need += size_t(1) << (g.log2cap - (int)g.rbits);
+        tag_bytes = (unsigned)std::min<size_t>((need + 4095) & ~size_t(4095), MO_TAG_MAX);   // (attribute: hm_create)
+    }
+    hipLaunchKernelGGL(k_merge_owned<Rec>, dim3(RP_BINS), dim3(MO_THREADS), tag_bytes, ctx->stream, (const Rec *)ctx->parts_sorted.p, n_rows,
                        (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
                        ctx->n_glist, (const WInfo *)ctx->d_winfo, cell_hi_of(ctx->cfg.h3_res), seq32(ctx), staged_rows(ctx),
-                       (unsigned *)ctx->bin_cnt.p, ctx->d_st);
+                       (unsigned *)ctx->bin_cnt.p, ctx->d_st, tag_bytes);
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
 }
@@ -2911,6 +2959,12 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     };
     if (hipSetDevice(ctx->device) != hipSuccess) { ctx->err = "hipSetDevice"; return fail("create"); }
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { ctx->err = "stream"; return fail("create"); }
+    // k_merge_owned's resident tags live in dynamic LDS of up to MO_TAG_MAX bytes (merge_sorted)
+    if (hipFuncSetAttribute((const void *)k_merge_owned<EventRec>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_merge_owned<SortedRec>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess) {
+        ctx->err = "merge LDS attribute";
+        return fail("create");
+    }
     for (auto &e : ctx->ev)
         if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     H3Tables T = make_tables();
