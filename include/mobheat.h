@@ -44,6 +44,7 @@ extern "C" {
 #define HM_E_NOMEM (-3)     /* device or host allocation failed */
 #define HM_E_OVERFLOW (-4)  /* a device hash table overflowed its probe bound */
 #define HM_E_STATE (-5)     /* call out of order (stage API) */
+#define HM_E_UNSUPPORTED (-6) /* input outside what the device decoder handles (hm_decode_json) */
 
 /* memory kinds for batch pointers */
 #define HM_MEM_HOST 0
@@ -274,6 +275,49 @@ int hm_selftest_position_statements(const hm_position_doc_cfg *cfg, const uint64
  * per phase: index 0 ingest (k_ingest: filter + cells + windows + pre-aggregation + dedup max), 1 reserved
  * (0), 2 merge, 3 emit, 4 dedup (flag + compaction), 5 total, 6 region partition. */
 int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n);
+
+/* ---- Kafka message values -> batch columns (reference heatmap_stream.py:51-61, 88-93) ----
+ * The micro-batch's Kafka values (the producer's JSON records, mbta_to_kafka.py:66-74), back to back with
+ * n + 1 offsets (Arrow binary/string layout; offsets[0] may be > 0), parsed on the device like
+ * from_json(value, schema) in PERMISSIVE mode + to_timestamp(ts) (rules: csrc/json_decode.h): the columns of
+ * hm_batch_in (device memory, valid until the next hm_decode_json on this context) with row_valid = provider,
+ * vehicleId and eventTs non-null, and vkey = provider_code * n_vehicles + vehicle_code from the batch's exact
+ * string dictionaries (code order unspecified; strings as Arrow offsets + UTF-8 bytes in pinned host memory, the
+ * layout hm_encode_position_updates takes).  Records the device decoder does not handle (see json_decode.h) fail
+ * the call with HM_E_UNSUPPORTED; malformed records decode to all-null rows (counted). */
+typedef struct hm_json_in {
+    int64_t n;
+    int32_t memory;            /* HM_MEM_HOST or HM_MEM_DEVICE: where bytes and offsets live */
+    int32_t reserved;
+    const uint8_t *bytes;
+    const int64_t *offsets;    /* n + 1 */
+} hm_json_in;
+typedef struct hm_json_out {
+    hm_batch_in batch;         /* device columns, ready for hm_process_batch */
+    int64_t n_providers;
+    const int64_t *provider_offsets;   /* n_providers + 1 */
+    const uint8_t *provider_bytes;
+    int64_t n_vehicles;
+    const int64_t *vehicle_offsets;    /* n_vehicles + 1 */
+    const uint8_t *vehicle_bytes;
+    int64_t n_malformed;       /* records that decoded to all-null rows (from_json's malformed records) */
+    int64_t n_unsupported;     /* > 0 only with HM_E_UNSUPPORTED */
+} hm_json_out;
+int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out);
+
+/* The distinct 900-s buckets floor(ts_s / 900) of the last hm_process_batch's latest rows, ascending (computed on
+ * the device; *n = count, up to cap written): the buckets whose local offsets hm_encode_position_updates needs. */
+int hm_last_latest_buckets(hm_ctx *ctx, int64_t *bucket_ids, int64_t cap, int64_t *n);
+
+/* Host execution of the record decoder (json_decode.h) on n records (bytes readable up to 16 bytes past the last
+ * record: the decoder reads 16-B windows); scratch (same size as bytes) receives escaped strings' decoded bytes.
+ * Per record: lat, lon, speed (NaN when null), ts_us, bearing, accuracy, the provider / vehicleId spans (absolute
+ * offsets into bytes, or into scratch when the JF_*_ESC flag is set) and the field flags. */
+int hm_selftest_json_records(const uint8_t *bytes, const int64_t *offsets, int64_t n, uint8_t *scratch, double *lat,
+                             double *lon, double *speed, int64_t *ts_us, int32_t *bearing, int32_t *accuracy,
+                             int64_t *p_off, int32_t *p_len, int64_t *v_off, int32_t *v_len, uint32_t *flags);
+/* Host execution of the decoder's decimal -> binary64 conversion: bits[i] = w[i] * 10^q[i] correctly rounded. */
+int hm_selftest_decimal_to_double(const uint64_t *w, const int64_t *q, int64_t n, uint64_t *bits);
 
 /* Counts of the last hm_process_batch (up to n of them): [0] keys created in the tile state, [1] partial records
  * merged (direct path: aggregated rows; table mode: ~ distinct keys), [2] tiles emitted, [3] 1 if table mode ran. */

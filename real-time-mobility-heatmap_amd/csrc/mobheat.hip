@@ -34,6 +34,7 @@
 #include "../../include/mobheat.h"
 #include "kernels.h"
 #include "bson_docs.h"
+#include "json_decode.h"
 
 #define H3T_CONST static const
 #include "h3_tables.inc"
@@ -1846,6 +1847,172 @@ __global__ __launch_bounds__(HS_THREADS) void k_sample_heavy(const uint64_t *__r
 }
 
 // =====================================================================================================
+// K0: Kafka values -> batch columns (row f1: from_json + to_timestamp, heatmap_stream.py:88-93; json_decode.h),
+// one thread per record; then the exact string dictionaries of provider and vehicleId (hash table keyed by a
+// 64-bit string hash, every row verified byte for byte against its slot's representative; a hash collision
+// reruns the dictionary with another seed) and vkey = provider_code * n_vehicles + vehicle_code.
+// =====================================================================================================
+constexpr int64_t SPAN_SCRATCH = INT64_C(1) << 62;   // span offset flag: the decoded bytes are in the scratch buffer
+__global__ __launch_bounds__(256) void k_json_parse(const uint8_t *__restrict__ bytes, const int64_t *__restrict__ offs,
+                                                    int64_t base, int64_t n, uint8_t *__restrict__ scratch,
+                                                    double *__restrict__ lat, double *__restrict__ lon,
+                                                    int64_t *__restrict__ ts, double *__restrict__ speed,
+                                                    uint8_t *__restrict__ sv, uint8_t *__restrict__ rv,
+                                                    int64_t *__restrict__ p_off, int32_t *__restrict__ p_len,
+                                                    int64_t *__restrict__ v_off, int32_t *__restrict__ v_len,
+                                                    unsigned long long *counts) {
+    unsigned long long bad = 0, unsup = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        JsonRow r;
+        parse_record(bytes, offs[i] - base, offs[i + 1] - base, scratch, r);
+        const uint32_t f = r.flags;
+        bad += (f & JF_MALFORMED) != 0;
+        unsup += (f & JF_UNSUPPORTED) != 0;
+        lat[i] = (f & JF_LAT) ? r.lat : __builtin_nan("");
+        lon[i] = (f & JF_LON) ? r.lon : __builtin_nan("");
+        ts[i] = (f & JF_TS) ? r.ts_us : 0;
+        speed[i] = (f & JF_SPEED) ? r.speed : 0.0;
+        sv[i] = (f & JF_SPEED) ? 1 : 0;
+        rv[i] = (f & JF_PROV) && (f & JF_VEH) && (f & JF_TS) ? 1 : 0;
+        p_off[i] = r.p_off | ((f & JF_PROV_ESC) ? SPAN_SCRATCH : 0);
+        p_len[i] = (f & JF_PROV) ? r.p_len : -1;
+        v_off[i] = r.v_off | ((f & JF_VEH_ESC) ? SPAN_SCRATCH : 0);
+        v_len[i] = (f & JF_VEH) ? r.v_len : -1;
+    }
+    bad = wave_sum(bad);
+    unsup = wave_sum(unsup);
+    if (lane_id() == 0) {
+        if (bad) atomicAdd(&counts[0], bad);
+        if (unsup) atomicAdd(&counts[1], unsup);
+    }
+}
+
+__device__ __forceinline__ const uint8_t *span_ptr(const uint8_t *bytes, const uint8_t *scratch, int64_t off) {
+    return (off & SPAN_SCRATCH) ? scratch + (off & ~SPAN_SCRATCH) : bytes + off;
+}
+__device__ __forceinline__ uint64_t str_hash(const uint8_t *s, int n, uint64_t seed) {
+    uint64_t h = mix64(seed ^ ((uint64_t)n * UINT64_C(0x9e3779b97f4a7c15)));
+    for (int k = 0; k < n; k += 8) {
+        uint64_t x = 0;
+        for (int q = 0; q < 8 && k + q < n; q++) x |= (uint64_t)s[k + q] << (8 * q);
+        h = mix64(h ^ x) + UINT64_C(0x632be59bd9b4e019);
+    }
+    return h & ~(UINT64_C(1) << 63);   // (never DICT_EMPTY)
+}
+struct DictSlot {   // cleared to all-ones bytes
+    unsigned long long key;   // str_hash, < 2^63; ~0 = empty
+    unsigned rep;             // the smallest row holding the string
+    unsigned pad;
+};
+constexpr unsigned long long DICT_EMPTY = ~0ull;
+constexpr int DICT_PROBES = 64;
+__global__ __launch_bounds__(256) void k_dict_insert(const uint8_t *__restrict__ bytes, const uint8_t *__restrict__ scratch,
+                                                     const int64_t *__restrict__ off, const int32_t *__restrict__ len,
+                                                     int64_t n, DictSlot *tab, unsigned long long mask, uint64_t seed,
+                                                     unsigned *__restrict__ slot_of, unsigned long long *overflow) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int32_t L = len[i];
+        if (L < 0) { slot_of[i] = ~0u; continue; }
+        const uint64_t h = str_hash(span_ptr(bytes, scratch, off[i]), L, seed);
+        unsigned long long s = mix64(h ^ seed) & mask;
+        unsigned got = ~0u;
+        for (int p = 0; p < DICT_PROBES; p++) {
+            unsigned long long k = __hip_atomic_load(&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k == DICT_EMPTY) k = atomicCAS(&tab[s].key, DICT_EMPTY, (unsigned long long)h);
+            if (k == DICT_EMPTY || k == h) {
+                atomicMin(&tab[s].rep, (unsigned)i);
+                got = (unsigned)s;
+                break;
+            }
+            s = (s + 1) & mask;
+        }
+        slot_of[i] = got;
+        if (got == ~0u) atomicAdd(overflow, 1ull);
+    }
+}
+// every row's bytes against its slot's representative: a mismatch is a 64-bit hash collision
+__global__ __launch_bounds__(256) void k_dict_verify(const uint8_t *__restrict__ bytes, const uint8_t *__restrict__ scratch,
+                                                     const int64_t *__restrict__ off, const int32_t *__restrict__ len,
+                                                     int64_t n, const DictSlot *__restrict__ tab,
+                                                     const unsigned *__restrict__ slot_of, unsigned long long *collide) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const unsigned s = slot_of[i];
+        if (s == ~0u) continue;
+        const unsigned r = tab[s].rep;
+        if (r == (unsigned)i) continue;
+        bool eq = len[r] == len[i];
+        if (eq) {
+            const uint8_t *a = span_ptr(bytes, scratch, off[i]), *b = span_ptr(bytes, scratch, off[r]);
+            for (int k = 0; k < len[i] && eq; k++) eq = a[k] == b[k];
+        }
+        if (!eq) atomicAdd(collide, 1ull);
+    }
+}
+__global__ __launch_bounds__(256) void k_dict_occ(const DictSlot *__restrict__ tab, int64_t cap, uint8_t *__restrict__ occ) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += stride) occ[s] = tab[s].key != DICT_EMPTY;
+}
+// code c = the c-th occupied slot (ascending): code_of_slot, and the code's string length
+__global__ __launch_bounds__(256) void k_dict_codes(const int64_t *__restrict__ slots, const unsigned long long *n_codes,
+                                                    const DictSlot *__restrict__ tab, const int32_t *__restrict__ len,
+                                                    unsigned *__restrict__ code_of_slot, unsigned *__restrict__ clen) {
+    const int64_t m = (int64_t)*n_codes;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < m; c += stride) {
+        const int64_t s = slots[c];
+        code_of_slot[s] = (unsigned)c;
+        clen[c] = (unsigned)len[tab[s].rep];
+    }
+}
+__global__ __launch_bounds__(256) void k_dict_gather(const uint8_t *__restrict__ bytes, const uint8_t *__restrict__ scratch,
+                                                     const int64_t *__restrict__ off, const int32_t *__restrict__ len,
+                                                     const int64_t *__restrict__ slots, const unsigned long long *n_codes,
+                                                     const DictSlot *__restrict__ tab, const unsigned long long *__restrict__ coff,
+                                                     uint8_t *__restrict__ out) {
+    const int64_t m = (int64_t)*n_codes;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < m; c += stride) {
+        const unsigned r = tab[slots[c]].rep;
+        const uint8_t *a = span_ptr(bytes, scratch, off[r]);
+        for (int k = 0; k < len[r]; k++) out[coff[c] + k] = a[k];
+    }
+}
+__global__ __launch_bounds__(256) void k_json_vkey(const uint8_t *__restrict__ rv, const unsigned *__restrict__ pslot,
+                                                   const unsigned *__restrict__ vslot, const unsigned *__restrict__ pcode,
+                                                   const unsigned *__restrict__ vcode, int64_t n, uint64_t n_vehicles,
+                                                   uint64_t *__restrict__ vkey) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        vkey[i] = rv[i] ? (uint64_t)pcode[pslot[i]] * n_vehicles + vcode[vslot[i]] : 0;
+}
+// the distinct 900-s buckets of the latest rows' eventTs (a set of int64, EMPTY = INT64_MIN), compacted into list
+__global__ __launch_bounds__(256) void k_latest_buckets(const int64_t *__restrict__ rows, int64_t m,
+                                                        const int64_t *__restrict__ ts, long long *set, unsigned long long mask,
+                                                        long long *list, unsigned long long *n_list) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
+        const long long b = (long long)floordiv(floordiv(ts[rows[q]], 1000000), 900);
+        unsigned long long s = mix64((uint64_t)b) & mask;
+        for (unsigned long long p = 0; p <= mask; p++) {
+            long long k = __hip_atomic_load(&set[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k == INT64_MIN) {
+                k = atomicCAS((unsigned long long *)&set[s], (unsigned long long)INT64_MIN, (unsigned long long)b);
+                if (k == INT64_MIN) { list[atomicAdd(n_list, 1ull)] = b; break; }
+            }
+            if (k == b) break;
+            s = (s + 1) & mask;
+        }
+    }
+}
+__global__ __launch_bounds__(256) void k_fill_i64(long long *p, int64_t n, long long v) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+// =====================================================================================================
 // ordered compaction of a 0/1 byte array -> indices (deterministic, ascending)
 // =====================================================================================================
 constexpr int CP_THREADS = 256;
@@ -2074,6 +2241,18 @@ struct hm_ctx {
     int64_t prev_agg_rows = 0, prev_keys = 0;   // aggregated rows and distinct keys of the last batch
     bool last_table = false;
     int64_t last_counts[4] = {0, 0, 0, 0};   // hm_last_counts
+    // hm_decode_json (row f1): the values on the device, the decoded columns, the string dictionaries
+    struct Dict {
+        DevBuf tab, slot_of, occ, slots, code_of_slot, clen, coff, cbytes, btot, boff;
+        int64_t last_codes = 0;   // distinct strings of the last batch (sizes the next table: cache-resident)
+        int64_t n_codes = 0;
+        void *h_off = nullptr, *h_bytes = nullptr;   // pinned host copies of the dictionary
+        size_t h_off_cap = 0, h_bytes_cap = 0;
+    };
+    DevBuf jd_bytes, jd_offs, jd_scratch, jd_lat, jd_lon, jd_ts, jd_speed, jd_sv, jd_rv, jd_vkey, jd_poff, jd_plen, jd_voff,
+        jd_vlen;
+    Dict jd_prov, jd_veh;
+    DevBuf lb_set, lb_list;   // hm_last_latest_buckets
     DevBuf keys;                     // k_ingest's event key per row (kernels.h ekey)
     unsigned long long *d_wreg = nullptr, *h_wreg = nullptr;     // the batch's window registry (WREG_SLOTS wenc)
     unsigned long long *d_wcount = nullptr, *h_wcount = nullptr; // aggregated rows per registry slot (census)
@@ -2123,6 +2302,8 @@ constexpr int REGROW_WORD = 251; // records dumped by k_dump_gen
 constexpr int GIVEUP_WORD = 232;
 constexpr int GAPS_WORD = 242;   // 242-243: totals of the gap / donor scans
 constexpr int POSBAD_WORD = 241; // position statements: rows outside the caller's dictionaries
+constexpr int JSON_WORD = 244;   // 244-248: hm_decode_json's malformed / unsupported counts, dictionary overflow /
+                                 // collisions; hm_last_latest_buckets' bucket count
 // (GIVEUP_WORD: k_ingest's fused dedup gave up, a cache line of its own: words 232-239)
 
 #define HIPCHK(ctx, expr)                                                                             \
@@ -3067,9 +3248,18 @@ void hm_destroy(hm_ctx *ctx) {
                       &ctx->rp_btot, &ctx->rp_boff,
                       &ctx->s_cell, &ctx->s_ws, &ctx->s_cnt, &ctx->s_sp, &ctx->s_spn, &ctx->s_lon, &ctx->s_lat, &ctx->bin_cnt, &ctx->bin_off, &ctx->dfused.used, &ctx->dfull.used, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
                       &ctx->o_lon, &ctx->o_lat, &ctx->td_sizes, &ctx->td_off, &ctx->td_btot, &ctx->td_boff, &ctx->td_bytes,
-                      &ctx->td_params, &ctx->gapbuf, &ctx->keys, &ctx->agg_bucket, &ctx->agg_cursor};
+                      &ctx->td_params, &ctx->gapbuf, &ctx->keys, &ctx->agg_bucket, &ctx->agg_cursor,
+                      &ctx->jd_bytes, &ctx->jd_offs, &ctx->jd_scratch, &ctx->jd_lat, &ctx->jd_lon, &ctx->jd_ts, &ctx->jd_speed,
+                      &ctx->jd_sv, &ctx->jd_rv, &ctx->jd_vkey, &ctx->jd_poff, &ctx->jd_plen, &ctx->jd_voff, &ctx->jd_vlen,
+                      &ctx->lb_set, &ctx->lb_list};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
+    for (hm_ctx::Dict *d : {&ctx->jd_prov, &ctx->jd_veh}) {
+        for (DevBuf *b : {&d->tab, &d->slot_of, &d->occ, &d->slots, &d->code_of_slot, &d->clen, &d->coff, &d->cbytes, &d->btot, &d->boff})
+            if (b->p) (void)hipFree(b->p);
+        if (d->h_off) (void)hipHostFree(d->h_off);
+        if (d->h_bytes) (void)hipHostFree(d->h_bytes);
+    }
     for (auto &g : ctx->gens)
         if (!in_arena(ctx, g.tab)) (void)hipFree(g.tab);
     for (auto &pt : ctx->pool)
@@ -3735,6 +3925,254 @@ int hm_encode_position_updates(hm_ctx *ctx, const hm_position_doc_cfg *cfg, int3
         if ((rc = ensure(ctx, ctx->td_bytes, 16))) return rc;
     }
     return statements_out(ctx, n, total, out_memory, bytes, offsets, n_docs);
+}
+
+// ---- Kafka values -> batch columns (row f1; json_decode.h) ----
+__global__ __launch_bounds__(256) void k_check_offsets(const int64_t *__restrict__ offs, int64_t n, int64_t lo, int64_t hi,
+                                                       unsigned long long *bad) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    unsigned long long b = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        b += offs[i] < lo || offs[i] > offs[i + 1] || offs[i + 1] > hi;
+    b = wave_sum(b);
+    if (b && lane_id() == 0) atomicAdd(bad, b);
+}
+
+static int host_pinned(hm_ctx *ctx, void **p, size_t &cap, size_t want) {
+    if (*p && cap >= want) return HM_OK;
+    if (*p) HIPCHK(ctx, hipHostFree(*p));
+    *p = nullptr;
+    cap = std::max<size_t>(want, 4096);
+    HIPCHK(ctx, hipHostMalloc(p, cap, hipHostMallocDefault));
+    return HM_OK;
+}
+
+// the exact dictionary of one string column (spans off/len into bytes or scratch; len -1 = null): slot_of per row,
+// code_of_slot, and the strings (Arrow offsets + bytes) in the Dict's pinned host buffers
+static int dict_build(hm_ctx *ctx, hm_ctx::Dict &d, const uint8_t *bytes, const uint8_t *scratch, const int64_t *off,
+                      const int32_t *len, int64_t n) {
+    int rc;
+    const unsigned long long full = next_pow2((unsigned long long)std::max<int64_t>(2 * n, 1024));
+    unsigned long long cap = d.last_codes > 0 ? next_pow2((unsigned long long)std::max<int64_t>(4 * d.last_codes, 1024))
+                                              : (1ull << 16);
+    cap = std::min(cap, full);
+    uint64_t seed = UINT64_C(0x8f1bbcdcca62c1d6);
+    unsigned long long *words = ctx->d_scratch + JSON_WORD + 2;   // overflow, collisions
+    for (int attempt = 0;; attempt++) {
+        if (attempt == 6) return set_err(ctx, HM_E_OVERFLOW, "string dictionary: repeated hash collisions");
+        if ((rc = ensure(ctx, d.tab, cap * sizeof(DictSlot))) || (rc = ensure(ctx, d.slot_of, std::max<int64_t>(n, 1) * 4)))
+            return rc;
+        HIPCHK(ctx, hipMemsetAsync(d.tab.p, 0xff, cap * sizeof(DictSlot), ctx->stream));
+        HIPCHK(ctx, hipMemsetAsync(words, 0, 16, ctx->stream));
+        hipLaunchKernelGGL(k_dict_insert, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, bytes, scratch, off, len, n,
+                           (DictSlot *)d.tab.p, cap - 1, seed, (unsigned *)d.slot_of.p, words);
+        hipLaunchKernelGGL(k_dict_verify, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, bytes, scratch, off, len, n,
+                           (const DictSlot *)d.tab.p, (const unsigned *)d.slot_of.p, words + 1);
+        HIPCHK(ctx, hipGetLastError());
+        unsigned long long hw[2];
+        HIPCHK(ctx, hipMemcpyAsync(hw, words, 16, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (hw[0]) {   // probes ran out (more distinct strings than the last batch): a full-size table
+            if (cap == full) return set_err(ctx, HM_E_OVERFLOW, "string dictionary table overflow");
+            cap = full;
+            continue;
+        }
+        if (hw[1]) {   // a 64-bit hash collision: another seed
+            seed = mix64(seed + (uint64_t)attempt + 1);
+            continue;
+        }
+        break;
+    }
+    // codes: the occupied slots in ascending order
+    if ((rc = ensure(ctx, d.occ, cap)) || (rc = ensure(ctx, d.slots, cap * 8)) || (rc = ensure(ctx, d.code_of_slot, cap * 4)))
+        return rc;
+    hipLaunchKernelGGL(k_dict_occ, dim3(grid_for((int64_t)cap, 256)), dim3(256), 0, ctx->stream, (const DictSlot *)d.tab.p,
+                       (int64_t)cap, (uint8_t *)d.occ.p);
+    if ((rc = compact_flags(ctx, (const uint8_t *)d.occ.p, (int64_t)cap, (int64_t *)d.slots.p))) return rc;
+    unsigned long long nc = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&nc, ctx->d_scratch + 255, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    const int64_t m = (int64_t)nc;
+    if ((rc = ensure(ctx, d.clen, std::max<int64_t>(m, 1) * 4)) || (rc = ensure(ctx, d.coff, (m + 1) * 8))) return rc;
+    hipLaunchKernelGGL(k_dict_codes, dim3(grid_for(std::max<int64_t>(m, 1), 256)), dim3(256), 0, ctx->stream,
+                       (const int64_t *)d.slots.p, ctx->d_scratch + 255, (const DictSlot *)d.tab.p, len,
+                       (unsigned *)d.code_of_slot.p, (unsigned *)d.clen.p);
+    unsigned long long *coff = (unsigned long long *)d.coff.p;
+    int64_t total = 0;
+    if (m > 0) {
+        const int64_t nb = (m + SC_PER - 1) / SC_PER;
+        if ((rc = ensure(ctx, d.btot, nb * 4)) || (rc = ensure(ctx, d.boff, nb * 8))) return rc;
+        hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, (const unsigned *)d.clen.p, m, coff,
+                           (unsigned *)d.btot.p);
+        hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)d.btot.p, nb,
+                           (unsigned long long *)d.boff.p, coff + m);
+        hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, coff, m, (const unsigned long long *)d.boff.p);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipMemcpyAsync(&total, coff + m, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    } else {
+        HIPCHK(ctx, hipMemsetAsync(coff, 0, 8, ctx->stream));
+    }
+    if ((rc = ensure(ctx, d.cbytes, std::max<int64_t>(total, 1)))) return rc;
+    if (m > 0)
+        hipLaunchKernelGGL(k_dict_gather, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, bytes, scratch, off, len,
+                           (const int64_t *)d.slots.p, ctx->d_scratch + 255, (const DictSlot *)d.tab.p,
+                           (const unsigned long long *)coff, (uint8_t *)d.cbytes.p);
+    HIPCHK(ctx, hipGetLastError());
+    if ((rc = host_pinned(ctx, &d.h_off, d.h_off_cap, (size_t)(m + 1) * 8)) ||
+        (rc = host_pinned(ctx, &d.h_bytes, d.h_bytes_cap, (size_t)std::max<int64_t>(total, 1))))
+        return rc;
+    HIPCHK(ctx, hipMemcpyAsync(d.h_off, coff, (m + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (total) HIPCHK(ctx, hipMemcpyAsync(d.h_bytes, d.cbytes.p, total, hipMemcpyDeviceToHost, ctx->stream));
+    d.n_codes = m;
+    d.last_codes = m;
+    return HM_OK;
+}
+
+int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out) {
+    if (!ctx || !in || !out || in->n < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    const int64_t n = in->n;
+    if (n > (int64_t)UINT32_MAX - 2) return set_err(ctx, HM_E_INVALID, "%lld records exceed 2^32-2", (long long)n);
+    if (n > 0 && (!in->bytes || !in->offsets)) return set_err(ctx, HM_E_INVALID, "bytes and offsets are required");
+    if (in->memory != HM_MEM_HOST && in->memory != HM_MEM_DEVICE) return set_err(ctx, HM_E_INVALID, "bad memory kind");
+    memset(out, 0, sizeof(*out));
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc;
+    const size_t m = (size_t)std::max<int64_t>(n, 1);
+    if ((rc = ensure(ctx, ctx->jd_lat, m * 8)) || (rc = ensure(ctx, ctx->jd_lon, m * 8)) || (rc = ensure(ctx, ctx->jd_ts, m * 8)) ||
+        (rc = ensure(ctx, ctx->jd_speed, m * 8)) || (rc = ensure(ctx, ctx->jd_sv, m)) || (rc = ensure(ctx, ctx->jd_rv, m)) ||
+        (rc = ensure(ctx, ctx->jd_vkey, m * 8)) || (rc = ensure(ctx, ctx->jd_poff, m * 8)) || (rc = ensure(ctx, ctx->jd_plen, m * 4)) ||
+        (rc = ensure(ctx, ctx->jd_voff, m * 8)) || (rc = ensure(ctx, ctx->jd_vlen, m * 4)))
+        return rc;
+    int64_t o0 = 0, on = 0;
+    const uint8_t *dbytes = nullptr;
+    const int64_t *doffs = nullptr;
+    if (n > 0) {
+        if (in->memory == HM_MEM_HOST) {
+            o0 = in->offsets[0];
+            on = in->offsets[n];
+            if (o0 < 0 || on < o0) return set_err(ctx, HM_E_INVALID, "bad offsets");
+            if ((rc = ensure(ctx, ctx->jd_bytes, (size_t)(on - o0) + 16)) || (rc = ensure(ctx, ctx->jd_offs, (size_t)(n + 1) * 8))) return rc;
+            if (on > o0) HIPCHK(ctx, hipMemcpyAsync(ctx->jd_bytes.p, in->bytes + o0, on - o0, hipMemcpyHostToDevice, ctx->stream));
+            HIPCHK(ctx, hipMemcpyAsync(ctx->jd_offs.p, in->offsets, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+            dbytes = (const uint8_t *)ctx->jd_bytes.p;
+            doffs = (const int64_t *)ctx->jd_offs.p;
+        } else {
+            HIPCHK(ctx, hipMemcpyAsync(&o0, in->offsets, 8, hipMemcpyDeviceToHost, ctx->stream));
+            HIPCHK(ctx, hipMemcpyAsync(&on, in->offsets + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+            HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+            if (o0 < 0 || on < o0) return set_err(ctx, HM_E_INVALID, "bad offsets");
+            dbytes = in->bytes + o0;
+            doffs = in->offsets;
+        }
+        // every record inside [o0, on] with non-decreasing offsets (a bad offset would read out of bounds)
+        unsigned long long *w = ctx->d_scratch + JSON_WORD;
+        HIPCHK(ctx, hipMemsetAsync(w, 0, 16, ctx->stream));
+        hipLaunchKernelGGL(k_check_offsets, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, doffs, n, o0, on, w);
+        unsigned long long hb = 0;
+        HIPCHK(ctx, hipMemcpyAsync(&hb, w, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (hb) return set_err(ctx, HM_E_INVALID, "%llu offsets out of order or out of range", hb);
+        if ((rc = ensure(ctx, ctx->jd_scratch, (size_t)(on - o0) + 16))) return rc;
+        hipLaunchKernelGGL(k_json_parse, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, dbytes, doffs, o0, n,
+                           (uint8_t *)ctx->jd_scratch.p, (double *)ctx->jd_lat.p, (double *)ctx->jd_lon.p, (int64_t *)ctx->jd_ts.p,
+                           (double *)ctx->jd_speed.p, (uint8_t *)ctx->jd_sv.p, (uint8_t *)ctx->jd_rv.p, (int64_t *)ctx->jd_poff.p,
+                           (int32_t *)ctx->jd_plen.p, (int64_t *)ctx->jd_voff.p, (int32_t *)ctx->jd_vlen.p, w);
+        HIPCHK(ctx, hipGetLastError());
+        unsigned long long counts[2];
+        HIPCHK(ctx, hipMemcpyAsync(counts, w, 16, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        out->n_malformed = (int64_t)counts[0];
+        out->n_unsupported = (int64_t)counts[1];
+        if (counts[1])
+            return set_err(ctx, HM_E_UNSUPPORTED, "%llu records outside the device decoder (a number of more than 19 significant "
+                           "digits on a rounding boundary, or a float/object/array as a string field)", counts[1]);
+    }
+    const uint8_t *scratch = (const uint8_t *)ctx->jd_scratch.p;
+    if ((rc = dict_build(ctx, ctx->jd_prov, dbytes, scratch, (const int64_t *)ctx->jd_poff.p, (const int32_t *)ctx->jd_plen.p, n)) ||
+        (rc = dict_build(ctx, ctx->jd_veh, dbytes, scratch, (const int64_t *)ctx->jd_voff.p, (const int32_t *)ctx->jd_vlen.p, n)))
+        return rc;
+    const int64_t nv = std::max<int64_t>(ctx->jd_veh.n_codes, 1);
+    if (n > 0)
+        hipLaunchKernelGGL(k_json_vkey, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, (const uint8_t *)ctx->jd_rv.p,
+                           (const unsigned *)ctx->jd_prov.slot_of.p, (const unsigned *)ctx->jd_veh.slot_of.p,
+                           (const unsigned *)ctx->jd_prov.code_of_slot.p, (const unsigned *)ctx->jd_veh.code_of_slot.p, n,
+                           (uint64_t)nv, (uint64_t *)ctx->jd_vkey.p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    hm_batch_in &b = out->batch;
+    b.n = n;
+    b.memory = HM_MEM_DEVICE;
+    b.lat = (const double *)ctx->jd_lat.p;
+    b.lon = (const double *)ctx->jd_lon.p;
+    b.ts_us = (const int64_t *)ctx->jd_ts.p;
+    b.speed = (const double *)ctx->jd_speed.p;
+    b.speed_valid = (const uint8_t *)ctx->jd_sv.p;
+    b.vkey = (const uint64_t *)ctx->jd_vkey.p;
+    b.row_valid = (const uint8_t *)ctx->jd_rv.p;
+    out->n_providers = ctx->jd_prov.n_codes;
+    out->provider_offsets = (const int64_t *)ctx->jd_prov.h_off;
+    out->provider_bytes = (const uint8_t *)ctx->jd_prov.h_bytes;
+    out->n_vehicles = ctx->jd_veh.n_codes;
+    out->vehicle_offsets = (const int64_t *)ctx->jd_veh.h_off;
+    out->vehicle_bytes = (const uint8_t *)ctx->jd_veh.h_bytes;
+    return HM_OK;
+}
+
+int hm_last_latest_buckets(hm_ctx *ctx, int64_t *bucket_ids, int64_t cap, int64_t *n) {
+    if (!ctx || !n || cap < 0 || (cap > 0 && !bucket_ids)) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->last_n_latest < 0) return set_err(ctx, HM_E_STATE, "no hm_process_batch latest rows");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int64_t m = ctx->last_n_latest;
+    *n = 0;
+    if (m == 0) return HM_OK;
+    int rc;
+    const unsigned long long scap = next_pow2((unsigned long long)std::max<int64_t>(2 * m, 1024));
+    if ((rc = ensure(ctx, ctx->lb_set, scap * 8)) || (rc = ensure(ctx, ctx->lb_list, (size_t)m * 8))) return rc;
+    unsigned long long *w = ctx->d_scratch + JSON_WORD + 4;
+    hipLaunchKernelGGL(k_fill_i64, dim3(grid_for((int64_t)scap, 256)), dim3(256), 0, ctx->stream, (long long *)ctx->lb_set.p,
+                       (int64_t)scap, (long long)INT64_MIN);
+    HIPCHK(ctx, hipMemsetAsync(w, 0, 8, ctx->stream));
+    hipLaunchKernelGGL(k_latest_buckets, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, (const int64_t *)ctx->rows.p, m,
+                       ctx->last_ts, (long long *)ctx->lb_set.p, scap - 1, (long long *)ctx->lb_list.p, w);
+    HIPCHK(ctx, hipGetLastError());
+    unsigned long long k = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&k, w, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<int64_t> ids(k);
+    if (k) HIPCHK(ctx, hipMemcpy(ids.data(), ctx->lb_list.p, k * 8, hipMemcpyDeviceToHost));
+    std::sort(ids.begin(), ids.end());
+    *n = (int64_t)k;
+    for (int64_t i = 0; i < (int64_t)k && i < cap; i++) bucket_ids[i] = ids[i];
+    return HM_OK;
+}
+
+int hm_selftest_json_records(const uint8_t *bytes, const int64_t *offsets, int64_t n, uint8_t *scratch, double *lat,
+                             double *lon, double *speed, int64_t *ts_us, int32_t *bearing, int32_t *accuracy,
+                             int64_t *p_off, int32_t *p_len, int64_t *v_off, int32_t *v_len, uint32_t *flags) {
+    if (n < 0 || (n > 0 && (!bytes || !offsets || !scratch))) return HM_E_INVALID;
+    for (int64_t i = 0; i < n; i++) {
+        JsonRow r;
+        parse_record(bytes, offsets[i], offsets[i + 1], scratch, r);
+        lat[i] = r.lat;
+        lon[i] = r.lon;
+        speed[i] = r.speed;
+        ts_us[i] = r.ts_us;
+        bearing[i] = r.bearing;
+        accuracy[i] = r.accuracy;
+        p_off[i] = r.p_off;
+        p_len[i] = r.p_len;
+        v_off[i] = r.v_off;
+        v_len[i] = r.v_len;
+        flags[i] = r.flags;
+    }
+    return HM_OK;
+}
+
+int hm_selftest_decimal_to_double(const uint64_t *w, const int64_t *q, int64_t n, uint64_t *bits) {
+    if (n < 0 || (n > 0 && (!w || !q || !bits))) return HM_E_INVALID;
+    for (int64_t i = 0; i < n; i++) bits[i] = decimal_to_double_bits(q[i], w[i]);
+    return HM_OK;
 }
 
 int hm_device_alloc(int32_t device, int64_t bytes, void **ptr) {

@@ -49,6 +49,16 @@ class HmBatchOut(ctypes.Structure):
     ]
 
 
+class HmJsonIn(ctypes.Structure):
+    _fields_ = [("n", c_i64), ("memory", c_i32), ("reserved", c_i32), ("bytes", c_vp), ("offsets", c_vp)]
+
+
+class HmJsonOut(ctypes.Structure):
+    _fields_ = [("batch", HmBatchIn), ("n_providers", c_i64), ("provider_offsets", c_vp), ("provider_bytes", c_vp),
+                ("n_vehicles", c_i64), ("vehicle_offsets", c_vp), ("vehicle_bytes", c_vp), ("n_malformed", c_i64),
+                ("n_unsupported", c_i64)]
+
+
 class HmStageSizes(ctypes.Structure):
     _fields_ = [("n_tile_partials", c_i64), ("n_cands", c_i64), ("batch_max_event_ms", c_i64),
                 ("n_valid", c_i64), ("n_late", c_i64)]
@@ -105,6 +115,11 @@ SIGNATURES = {
                                                 c_vp]),
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_last_counts": (c_i32, [c_vp, c_vp, c_i32]),
+    "hm_decode_json": (c_i32, [c_vp, _P(HmJsonIn), _P(HmJsonOut)]),
+    "hm_last_latest_buckets": (c_i32, [c_vp, c_vp, c_i64, _P(c_i64)]),
+    "hm_selftest_json_records": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                         c_vp, c_vp]),
+    "hm_selftest_decimal_to_double": (c_i32, [c_vp, c_vp, c_i64, c_vp]),
     "hm_abi_version": (c_i32, []),
 }
 
@@ -239,14 +254,18 @@ def _dictionary(strings):
     return n, offs, raw
 
 
-def time_buckets(ts_us):
-    """The distinct 900-s buckets floor(ts_s / 900) of the rows' eventTs (ascending) and the local-time offset of
-    each (pyspark's naive local datetimes, stream._spark_datetime).  Only the buckets the rows use are looked up, so
-    a batch mixing a 1970 GPS time with current traffic costs two lookups, not 55 years of buckets."""
+def time_buckets(ts_us, bucket_ids=None):
+    """The distinct 900-s buckets floor(ts_s / 900) of the rows' eventTs (ascending; or the given bucket_ids) and the
+    local-time offset of each (pyspark's naive local datetimes, stream._spark_datetime).  Only the buckets the rows
+    use are looked up, so a batch mixing a 1970 GPS time with current traffic costs two lookups, not 55 years of
+    buckets."""
     import calendar
     import datetime as _dt
-    ts_us = np.asarray(ts_us, dtype=np.int64)
-    ids = np.unique(np.floor_divide(np.floor_divide(ts_us, 1_000_000), 900)) if ts_us.size else np.zeros(0, np.int64)
+    if bucket_ids is not None:
+        ids = np.unique(np.asarray(bucket_ids, dtype=np.int64))
+    else:
+        ts_us = np.asarray(ts_us, dtype=np.int64)
+        ids = np.unique(np.floor_divide(np.floor_divide(ts_us, 1_000_000), 900)) if ts_us.size else np.zeros(0, np.int64)
 
     def off(s):
         return calendar.timegm(_dt.datetime.fromtimestamp(s).timetuple()) - s
@@ -256,12 +275,13 @@ def time_buckets(ts_us):
     return np.ascontiguousarray(ids, np.int64), offs
 
 
-def position_doc_cfg(provider_uniques, vehicle_uniques, ts_us):
-    """hm_position_doc_cfg for a batch's string dictionaries (pandas.factorize uniques, the order the vkeys were
-    built in) and the eventTs of its latest rows; the returned tuple keeps the arrays alive."""
-    np_, po, pb = _dictionary(provider_uniques)
-    nv, vo, vb = _dictionary(vehicle_uniques)
-    bi, bo = time_buckets(ts_us)
+def position_doc_cfg(provider_uniques, vehicle_uniques, ts_us, bucket_ids=None):
+    """hm_position_doc_cfg for a batch's string dictionaries (pandas.factorize uniques in the order the vkeys were
+    built, or (n, offsets, bytes) as decode_json returns them) and the eventTs of its latest rows (or their 900-s
+    buckets); the returned tuple keeps the arrays alive."""
+    np_, po, pb = provider_uniques if isinstance(provider_uniques, tuple) else _dictionary(provider_uniques)
+    nv, vo, vb = vehicle_uniques if isinstance(vehicle_uniques, tuple) else _dictionary(vehicle_uniques)
+    bi, bo = time_buckets(ts_us, bucket_ids)
     cfg = HmPositionDocCfg(n_providers=np_, provider_offsets=ptr(po), provider_bytes=ptr(pb), n_vehicles=max(nv, 1),
                            vehicle_offsets=ptr(vo), vehicle_bytes=ptr(vb), n_buckets=bi.size,
                            bucket_ids=ptr(bi) if bi.size else None, bucket_offset_s=ptr(bo) if bo.size else None)
@@ -287,3 +307,57 @@ def position_statements_selftest(provider_uniques, vehicle_uniques, vkey, ts_us,
     check(lib.hm_selftest_position_statements(ctypes.byref(cfg), ptr(vkey), ptr(ts_us), ptr(lat), ptr(lon), n, ptr(buf),
                                               cap, ptr(offs)), None, "hm_selftest_position_statements")
     return buf[:offs[-1]].copy(), offs
+
+
+# ---- Kafka values (row f1) ----
+JF = dict(LAT=1, LON=2, SPEED=4, TS=8, PROV=16, VEH=32, BEARING=64, ACC=128, PROV_ESC=256, VEH_ESC=512,
+          MALFORMED=1 << 16, UNSUPPORTED=1 << 17)   # json_decode.h
+
+
+def pack_values(values):
+    """A list of bytes (Kafka values) -> (bytes uint8 with 16 spare bytes, offsets int64[n+1]) in Arrow's layout."""
+    lens = np.fromiter((len(v) for v in values), dtype=np.int64, count=len(values))
+    offs = np.zeros(len(values) + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    buf = np.zeros(int(offs[-1]) + 16, np.uint8)
+    if len(values):
+        buf[:offs[-1]] = np.frombuffer(b"".join(values), np.uint8)
+    return buf, offs
+
+
+def json_records_selftest(values):
+    """Host execution of the device record decoder (json_decode.h): per-record fields + decoded strings."""
+    lib = load()
+    buf, offs = pack_values(values)
+    n = len(values)
+    scratch = np.zeros_like(buf)
+    o = {k: np.zeros(max(n, 1), dt) for k, dt in (("lat", np.float64), ("lon", np.float64), ("speed", np.float64),
+                                                  ("ts_us", np.int64), ("bearing", np.int32), ("accuracy", np.int32),
+                                                  ("p_off", np.int64), ("p_len", np.int32), ("v_off", np.int64),
+                                                  ("v_len", np.int32), ("flags", np.uint32))}
+    check(lib.hm_selftest_json_records(ptr(buf), ptr(offs), n, ptr(scratch), *[ptr(o[k]) for k in
+                                       ("lat", "lon", "speed", "ts_us", "bearing", "accuracy", "p_off", "p_len", "v_off",
+                                        "v_len", "flags")]), None, "hm_selftest_json_records")
+    o = {k: v[:n] for k, v in o.items()}
+
+    def strs(off, ln, esc_bit, present_bit):
+        out = []
+        for k in range(n):
+            if not o["flags"][k] & present_bit:
+                out.append(None)
+                continue
+            src = scratch if o["flags"][k] & esc_bit else buf
+            out.append(bytes(src[o[off][k]:o[off][k] + o[ln][k]]))
+        return out
+    o["provider"] = strs("p_off", "p_len", JF["PROV_ESC"], JF["PROV"])
+    o["vehicleId"] = strs("v_off", "v_len", JF["VEH_ESC"], JF["VEH"])
+    return o
+
+
+def decimal_to_double_selftest(w, q):
+    lib = load()
+    w = np.ascontiguousarray(w, dtype=np.uint64)
+    q = np.ascontiguousarray(q, dtype=np.int64)
+    out = np.empty(w.size, np.uint64)
+    check(lib.hm_selftest_decimal_to_double(ptr(w), ptr(q), w.size, ptr(out)), None, "hm_selftest_decimal_to_double")
+    return out

@@ -10,8 +10,8 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import (HM_MEM_DEVICE, HM_MEM_HOST, STATE_REC_DTYPE, HmBatchIn, HmBatchOut, HmConfig, HmStateInfo, check,
-                   ptr)
+from ._lib import (HM_MEM_DEVICE, HM_MEM_HOST, STATE_REC_DTYPE, HmBatchIn, HmBatchOut, HmConfig, HmJsonIn, HmJsonOut,
+                   HmStateInfo, check, ptr)
 
 _INFO_FIELDS = [f for f, _ in HmStateInfo._fields_ if f != "reserved"]
 
@@ -30,6 +30,16 @@ class TileRows:
 
     def __len__(self):
         return int(self.cell.size)
+
+
+@dataclass
+class KafkaBatch:
+    """hm_decode_json's result: device columns (batch, valid until the next decode on the engine) and copies of the
+    batch's string dictionaries (vkey = provider_code * n_vehicles + vehicle_code)."""
+    batch: HmBatchIn
+    providers: tuple            # (n, offsets int64[n+1], bytes uint8): Arrow layout, as _lib._dictionary builds
+    vehicles: tuple
+    n_malformed: int
 
 
 @dataclass
@@ -102,6 +112,45 @@ class HeatmapEngine:
               self._ctx, "hm_process_batch")
         return self._result_from_host(out, copy)
 
+    # ---- Kafka values (row f1): JSON decoded on the GPU, then the batch ----
+    def decode_json(self, values, offsets):
+        """The micro-batch's Kafka values (bytes uint8 back to back + offsets int64[n+1], Arrow's binary layout) ->
+        KafkaBatch: from_json(value, schema) + to_timestamp(ts) on the device (reference heatmap_stream.py:88-93)."""
+        buf = np.ascontiguousarray(values, dtype=np.uint8)
+        offs = np.ascontiguousarray(offsets, dtype=np.int64)
+        jin = HmJsonIn(n=offs.size - 1, memory=HM_MEM_HOST, bytes=ptr(buf) if buf.size else None, offsets=ptr(offs))
+        jout = HmJsonOut()
+        check(self._lib.hm_decode_json(self._ctx, ctypes.byref(jin), ctypes.byref(jout)), self._ctx, "hm_decode_json")
+
+        def dictionary(n, po, pb):
+            offs_ = np.ctypeslib.as_array(ctypes.cast(po, ctypes.POINTER(ctypes.c_int64)), shape=(n + 1,)).copy()
+            total = int(offs_[-1])
+            raw = (np.ctypeslib.as_array(ctypes.cast(pb, ctypes.POINTER(ctypes.c_uint8)), shape=(total,)).copy()
+                   if total else np.zeros(1, np.uint8))
+            return n, offs_, raw
+        return KafkaBatch(batch=jout.batch, providers=dictionary(int(jout.n_providers), jout.provider_offsets,
+                                                                  jout.provider_bytes),
+                          vehicles=dictionary(int(jout.n_vehicles), jout.vehicle_offsets, jout.vehicle_bytes),
+                          n_malformed=int(jout.n_malformed))
+
+    def process_kafka(self, epoch_id, values, offsets, copy=True):
+        """decode_json + hm_process_batch on the decoded device columns; (BatchResult, KafkaBatch)."""
+        kb = self.decode_json(values, offsets)
+        out = HmBatchOut()
+        check(self._lib.hm_process_batch(self._ctx, int(epoch_id), ctypes.byref(kb.batch), HM_MEM_HOST, ctypes.byref(out)),
+              self._ctx, "hm_process_batch")
+        return self._result_from_host(out, copy), kb
+
+    def latest_buckets(self):
+        """The distinct 900-s buckets of the last batch's latest rows' eventTs (computed on the device)."""
+        n = ctypes.c_int64()
+        check(self._lib.hm_last_latest_buckets(self._ctx, None, 0, ctypes.byref(n)), self._ctx, "hm_last_latest_buckets")
+        ids = np.zeros(max(n.value, 1), np.int64)
+        if n.value:
+            check(self._lib.hm_last_latest_buckets(self._ctx, ptr(ids), ids.size, ctypes.byref(n)), self._ctx,
+                  "hm_last_latest_buckets")
+        return ids[:n.value]
+
     # ---- device-resident batch (bench / multi-GPU): raw device pointers, results stay on the device ----
     def process_batch_device(self, epoch_id, n, lat, lon, ts_us, speed, speed_valid, vkey, row_valid):
         b = HmBatchIn(n=int(n), memory=HM_MEM_DEVICE, lat=lat, lon=lon, ts_us=ts_us, speed=speed,
@@ -159,12 +208,14 @@ class HeatmapEngine:
                                                ctypes.byref(po), ctypes.byref(nd)), self._ctx, "hm_encode_tile_updates")
         return _host_statements(pb, po, nd, copy)
 
-    def encode_position_updates(self, provider_uniques, vehicle_uniques, latest_ts_us, copy=False):
+    def encode_position_updates(self, provider_uniques, vehicle_uniques, latest_ts_us=None, copy=False):
         """The last batch's latest rows as positions_latest update statements (reference heatmap_stream.py:211-235):
         (bytes uint8, offsets int64[n+1]).  The dictionaries are the batch's factorization its vkeys were built
-        from (vkey = provider_code * n_vehicles + vehicle_code); latest_ts_us = the latest rows' eventTs (their
-        900-s buckets' local offsets are looked up on the host)."""
-        cfg, keep = _lib.position_doc_cfg(provider_uniques, vehicle_uniques, latest_ts_us)
+        from (vkey = provider_code * n_vehicles + vehicle_code): lists of strings, or (n, offsets, bytes) as
+        decode_json returns them.  The local offsets are looked up for the 900-s buckets of latest_ts_us (the
+        latest rows' eventTs), or, when it is None, of the buckets the device finds among the latest rows."""
+        bucket_ids = self.latest_buckets() if latest_ts_us is None else None
+        cfg, keep = _lib.position_doc_cfg(provider_uniques, vehicle_uniques, latest_ts_us, bucket_ids=bucket_ids)
         pb, po, nd = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
         check(self._lib.hm_encode_position_updates(self._ctx, ctypes.byref(cfg), HM_MEM_HOST, ctypes.byref(pb),
                                                    ctypes.byref(po), ctypes.byref(nd)), self._ctx,

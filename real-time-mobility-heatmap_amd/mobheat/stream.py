@@ -219,20 +219,53 @@ def _event_ts_us(t):
         valid = ~np.asarray(col.is_null().to_numpy(zero_copy_only=False), dtype=bool)
         vals = np.asarray(pc.fill_null(col.cast(pa.int64()), 0).to_numpy(zero_copy_only=False), dtype=np.int64)
         return vals, valid
-    # raw ISO-8601 strings: to_timestamp(col("ts")) (reference :92); malformed -> null
+    # raw ISO-8601 strings: to_timestamp(col("ts")) (reference :92); malformed -> null.  Strings with and without a
+    # zone are parsed apart: in one mixed Series pandas applies an offset it saw to the naive strings, where
+    # to_timestamp reads them in the session time zone (UTC, :45)
     import pandas as pd
-    s = pd.to_datetime(t.column("ts").to_pandas(), utc=True, errors="coerce", format="ISO8601")
-    valid = ~s.isna().to_numpy()
-    vals = np.where(valid, s.astype("int64", copy=False).to_numpy() // 1000 if len(s) else np.zeros(0, np.int64), 0)
-    return vals.astype(np.int64), valid
+    raw = t.column("ts").to_pandas()
+    zoned = raw.astype("string").str.strip().str.contains(r"(?:Z|[+-]\d{2}(?::?\d{2})?)$", regex=True).fillna(False).to_numpy(bool)
+    vals = np.zeros(len(raw), np.int64)
+    valid = np.zeros(len(raw), bool)
+    for sel in (zoned, ~zoned):
+        if sel.any():
+            s = pd.to_datetime(raw[sel], utc=True, errors="coerce", format="ISO8601")
+            ok = ~s.isna().to_numpy()
+            valid[sel] = ok
+            vals[sel] = np.where(ok, s.astype("int64", copy=False).to_numpy() // 1000, 0)
+    return vals, valid
+
+
+def kafka_values(t):
+    """The Kafka `value` column of an Arrow table as (bytes uint8, offsets int64[n+1]); a null value (tombstone)
+    is an empty value, which from_json makes an all-null row (heatmap_stream.py:88-91)."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    col = t.column("value")
+    col = col.combine_chunks() if isinstance(col, pa.ChunkedArray) else col
+    if pa.types.is_string(col.type) or pa.types.is_large_string(col.type):
+        col = col.cast(pa.large_binary())
+    elif not pa.types.is_large_binary(col.type):
+        col = col.cast(pa.large_binary())
+    if col.null_count:
+        col = pc.fill_null(col, b"")
+    n = len(col)
+    offs = np.frombuffer(col.buffers()[1], dtype=np.int64, count=n + 1, offset=col.offset * 8)
+    data = col.buffers()[2]
+    raw = np.frombuffer(data, dtype=np.uint8) if data is not None else np.zeros(0, np.uint8)
+    return raw, offs
 
 
 def batch_columns(df):
-    """Extract the SoA buffers the C ABI takes (hm_batch_in) from a micro-batch frame."""
+    """Extract the SoA buffers the C ABI takes (hm_batch_in) from a micro-batch frame.  A frame that carries the
+    raw Kafka `value` column (binary or string: the producer's JSON, mbta_to_kafka.py:66-74) is decoded on the GPU
+    instead (hm_decode_json): then the result is {"kafka": (bytes, offsets), "n": n}."""
     import pandas as pd
     import pyarrow.compute as pc
     t = _to_arrow(df)
     n = t.num_rows
+    if "value" in t.column_names:
+        return {"kafka": kafka_values(t), "n": n}
 
     def f64(name):
         if name not in t.column_names:
@@ -347,8 +380,13 @@ def foreach_batch_func(df, epoch_id: int):
     cols = batch_columns(df)
     eng = get_engine(epoch_id)
     try:
-        res = eng.process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"], cols["speed_valid"],
-                                cols["vkey"], cols["row_valid"], copy=False)
+        if "kafka" in cols:   # raw Kafka values: from_json + to_timestamp on the GPU (row f1)
+            res, kb = eng.process_kafka(epoch_id, *cols["kafka"], copy=False)
+            dicts = (kb.providers, kb.vehicles)
+        else:
+            res = eng.process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"], cols["speed_valid"],
+                                    cols["vkey"], cols["row_valid"], copy=False)
+            dicts = (cols["provider_uniques"], cols["vehicle_uniques"])
     except BaseException:
         reset_engine()   # the state may hold part of the batch: the next attempt rebuilds it from the checkpoint
         raise
@@ -360,10 +398,8 @@ def foreach_batch_func(df, epoch_id: int):
         buf, offs = get_engine().encode_tile_updates(CITY, TTL_MIN)
         _flush_statements(sink, "tiles", buf, offs)
         # ---- 2) latest per (provider, vehicleId) within this micro-batch: statements encoded on the GPU ----
-        rows = res.latest_rows
-        if rows.size:
-            buf, offs = get_engine().encode_position_updates(cols["provider_uniques"], cols["vehicle_uniques"],
-                                                             cols["ts_us"][rows])
+        if res.latest_rows.size:
+            buf, offs = get_engine().encode_position_updates(*dicts)   # (local offsets of the rows' 900-s buckets)
             _flush_statements(sink, "positions_latest", buf, offs)
         if STATE_CHECKPOINT:   # after the writes succeeded: the batch is committed
             save_state_checkpoint(epoch_id)
