@@ -1,7 +1,6 @@
 """GPU: row f1 -- hm_decode_json (from_json + to_timestamp of the Kafka values on the device, reference
 heatmap_stream.py:51-61, 88-93) against the committed fixture and the oracle (Python json + pandas,
 oracle/kafka_oracle.py), and foreach_batch_func fed raw Kafka values against the same batch fed decoded columns."""
-import ctypes
 import json
 import os
 import random
@@ -154,5 +153,16 @@ def test_foreach_batch_func_kafka_values_equal_decoded_frame():
                         "eventTs": ts})
     want = run(dec)
     assert set(got) == {"tiles", "positions_latest"}
-    assert got["tiles"] == want["tiles"] and len(got["tiles"]) > 100
     assert got["positions_latest"] == want["positions_latest"] and len(got["positions_latest"]) > 100
+    # tiles: identical documents, except the last bits of the fp64 averages (the sums' order is not fixed)
+    assert got["tiles"].keys() == want["tiles"].keys() and len(got["tiles"]) > 100
+
+    def close(a, b):
+        return a == b or abs(a - b) <= 1e-12 * max(abs(a), abs(b))
+    for k, g in got["tiles"].items():
+        w = want["tiles"][k]
+        gs, ws = dict(g["u"]["$set"]), dict(w["u"]["$set"])
+        assert close(gs.pop("avgSpeedKmh"), ws.pop("avgSpeedKmh"))
+        gc, wc = gs.pop("centroid")["coordinates"], ws.pop("centroid")["coordinates"]
+        assert close(gc[0], wc[0]) and close(gc[1], wc[1])
+        assert gs == ws and g["q"] == w["q"]
