@@ -129,6 +129,9 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
  * Pointers are in `memory` space (host pointers are copied). Runs on device `device`. */
 int hm_latlng_to_cell(const double *lat, const double *lon, int64_t n, int32_t res, int32_t memory,
                       int32_t device, uint64_t *out);
+/* Inputs of the last hm_latlng_to_cell call on `device` that the fast path handed to the exact path (its near-tie
+ * exceptions; tests check that constructed near-ties exercise it). */
+int64_t hm_latlng_to_cell_last_exact(int32_t device);
 
 /* ---- multi-GPU stage API (one context per GPU/rank; the caller performs the exchanges) ----
  * Record layouts (little endian, packed):
@@ -318,6 +321,14 @@ int hm_selftest_json_records(const uint8_t *bytes, const int64_t *offsets, int64
                              int64_t *p_off, int32_t *p_len, int64_t *v_off, int32_t *v_len, uint32_t *flags);
 /* Host execution of the decoder's decimal -> binary64 conversion: bits[i] = w[i] * 10^q[i] correctly rounded. */
 int hm_selftest_decimal_to_double(const uint64_t *w, const int64_t *q, int64_t n, uint64_t *bits);
+
+/* ---- read side (reference app.py:19-41 h3_boundary_geojson -> h3.cell_to_boundary) ----
+ * cellToBoundary of n cells: vertex k of cell i at lat[10 i + k], lng[10 i + k] (degrees, upstream's vertex order;
+ * unused slots NaN), nverts[i] vertices (5-10; 0 for an invalid index).  memory as hm_latlng_to_cell. */
+int hm_cells_to_boundary(const uint64_t *cells, int64_t n, int32_t memory, int32_t device, double *lat, double *lng,
+                         int32_t *nverts);
+/* Host execution of the same device code (no GPU; the CPU tests compare it with the oracle). */
+int hm_selftest_cells_to_boundary_host(const uint64_t *cells, int64_t n, double *lat, double *lng, int32_t *nverts);
 
 /* Counts of the last hm_process_batch (up to n of them): [0] keys created in the tile state, [1] partial records
  * merged (direct path: aggregated rows; table mode: ~ distinct keys), [2] tiles emitted, [3] 1 if table mode ran. */

@@ -13,8 +13,12 @@
  * x86-64 evaluates them in x87 extended precision exactly like the compiled h3 library does.
  * Compile with -O2 -ffp-contract=off (no FMA contraction; x86-64 SSE2 doubles), link glibc libm.
  *
- * Also restates the inverse (cellToLatLng: _h3ToFaceIjk, _adjustOverageClassII, _faceIjkToGeo) used ONLY
- * to validate the tables by round trip (latLngToCell(cellToLatLng(c)) == c).
+ * Also restates the inverse (cellToLatLng: _h3ToFaceIjk, _adjustOverageClassII, _faceIjkToGeo) used to
+ * validate the tables by round trip (latLngToCell(cellToLatLng(c)) == c), and the read side's cellToBoundary
+ * (reference app.py:19-41 h3_boundary_geojson -> h3.cell_to_boundary; upstream h3Index.c cellToBoundary ->
+ * faceijk.c _faceIjkToCellBoundary / _faceIjkPentToCellBoundary, _faceIjkToVerts, _faceIjkPentToVerts,
+ * _adjustPentVertOverage, _hex2dToGeo with substrate grids; vec2d.c _v2dIntersect (upstream's `float t`),
+ * _v2dAlmostEquals; coordijk.c _ijkToHex2d, _downAp3, _downAp3r), the checker of SURVEY §8f row f4.
  *
  * Parity status: UNPINNED against h3-py (not importable here; the reference ships no fixtures).  Anchors:
  * three public known-answer vectors from upstream READMEs, round-trip and table self-consistency checks.
@@ -498,7 +502,189 @@ void oracle_ld_ops(const double *a, int64_t n, int op, double *out) {
             case 4: out[i] = (double)(x - M_2PI); break;
             case 5: out[i] = (double)(x - M_AP7_ROT_RADS); break;
             case 6: out[i] = (double)(x + M_AP7_ROT_RADS); break;
+            case 7: out[i] = (double)(x * M_SQRT3_2); break;
+            case 8: out[i] = (double)(x * M_RSQRT7); break;
+            case 9: out[i] = (double)(x * M_ONETHIRD); break;
+            case 17: out[i] = (double)(x * M_180_PI); break;
             default: out[i] = NAN;
         }
     }
+}
+
+/* ---------------- read side (row f4): cellToBoundary ---------------- */
+enum { IJ_DIR = 1, KI_DIR = 2, JK_DIR = 3 };
+static int adjacentFaceDir(int from, int to) {   /* upstream's adjacentFaceDir table, from faceNeighbors */
+    if (from == to) return 0;
+    for (int d = 1; d <= 3; d++)
+        if (H3T_faceNeighbors[from][d][0] == to) return d;
+    return -1;
+}
+static void _ijkToHex2d(const CoordIJK *h, Vec2d *v) {
+    int i = h->i - h->k;
+    int j = h->j - h->k;
+    v->x = i - 0.5 * j;
+    v->y = j * M_SQRT3_2;
+}
+static void _downAp3(CoordIJK *ijk) {
+    static const int iv[3] = {2, 0, 1}, jv[3] = {1, 2, 0}, kv[3] = {0, 1, 2};
+    CoordIJK r = {0, 0, 0};
+    _ijkScaleAdd(&r, iv, ijk->i); _ijkScaleAdd(&r, jv, ijk->j); _ijkScaleAdd(&r, kv, ijk->k);
+    *ijk = r;
+    _ijkNormalize(ijk);
+}
+static void _downAp3r(CoordIJK *ijk) {
+    static const int iv[3] = {2, 1, 0}, jv[3] = {0, 2, 1}, kv[3] = {1, 0, 2};
+    CoordIJK r = {0, 0, 0};
+    _ijkScaleAdd(&r, iv, ijk->i); _ijkScaleAdd(&r, jv, ijk->j); _ijkScaleAdd(&r, kv, ijk->k);
+    *ijk = r;
+    _ijkNormalize(ijk);
+}
+static void _hex2dToGeo(const Vec2d *v, int face, int res, int substrate, LatLng *g) {
+    double r = sqrt(v->x * v->x + v->y * v->y);
+    LatLng fc = {H3T_faceCenterGeo[face][0], H3T_faceCenterGeo[face][1]};
+    if (r < EPSILON) { *g = fc; return; }
+    double theta = atan2(v->y, v->x);
+    for (int i = 0; i < res; i++) r *= M_RSQRT7;
+    if (substrate) {
+        r *= M_ONETHIRD;
+        if (isResolutionClassIII(res)) r *= M_RSQRT7;
+    }
+    r *= RES0_U_GNOMONIC;
+    r = atan(r);
+    if (!substrate && isResolutionClassIII(res)) theta = _posAngleRads(theta + M_AP7_ROT_RADS);
+    theta = _posAngleRads(H3T_faceAxesAzRadsCII[face][0] - theta);
+    _geoAzDistanceRads(&fc, theta, r, g);
+}
+static void _v2dIntersect(const Vec2d *p0, const Vec2d *p1, const Vec2d *p2, const Vec2d *p3, Vec2d *inter) {
+    Vec2d s1, s2;
+    s1.x = p1->x - p0->x;
+    s1.y = p1->y - p0->y;
+    s2.x = p3->x - p2->x;
+    s2.y = p3->y - p2->y;
+    float t;
+    t = (s2.x * (p0->y - p2->y) - s2.y * (p0->x - p2->x)) / (-s2.x * s1.y + s1.x * s2.y);
+    inter->x = p0->x + (t * s1.x);
+    inter->y = p0->y + (t * s1.y);
+}
+static int _v2dAlmostEquals(const Vec2d *a, const Vec2d *b) {
+    return fabsf(a->x - b->x) < 1.1920929e-07F && fabsf(a->y - b->y) < 1.1920929e-07F;   /* FLT_EPSILON */
+}
+static void _faceIjkVerts(FaceIJK *fijk, int *res, FaceIJK *verts, int nverts) {
+    static const int vertsCII[6][3] = {{2, 1, 0}, {1, 2, 0}, {0, 2, 1}, {0, 1, 2}, {1, 0, 2}, {2, 0, 1}};
+    static const int vertsCIII[6][3] = {{5, 4, 0}, {1, 5, 0}, {0, 5, 4}, {0, 1, 5}, {4, 0, 5}, {5, 0, 1}};
+    const int (*vs)[3] = isResolutionClassIII(*res) ? vertsCIII : vertsCII;
+    _downAp3(&fijk->coord);
+    _downAp3r(&fijk->coord);
+    if (isResolutionClassIII(*res)) {
+        _downAp7r(&fijk->coord);
+        *res += 1;
+    }
+    for (int v = 0; v < nverts; v++) {
+        verts[v].face = fijk->face;
+        verts[v].coord.i = fijk->coord.i + vs[v][0];
+        verts[v].coord.j = fijk->coord.j + vs[v][1];
+        verts[v].coord.k = fijk->coord.k + vs[v][2];
+        _ijkNormalize(&verts[v].coord);
+    }
+}
+/* the two icosahedron-face edge endpoints of direction dir in a substrate grid of resolution adjRes */
+static void _faceEdge(int adjRes, int dir, Vec2d *e0, Vec2d *e1) {
+    int maxDim = maxDimByCIIres[adjRes];
+    Vec2d v0 = {3.0 * maxDim, 0.0};
+    Vec2d v1 = {-1.5 * maxDim, 3.0 * M_SQRT3_2 * maxDim};
+    Vec2d v2 = {-1.5 * maxDim, -3.0 * M_SQRT3_2 * maxDim};
+    if (dir == IJ_DIR) { *e0 = v0; *e1 = v1; }
+    else if (dir == JK_DIR) { *e0 = v1; *e1 = v2; }
+    else { *e0 = v2; *e1 = v0; }
+}
+static int _faceIjkToCellBoundary(const FaceIJK *h, int res, double *lat, double *lng) {
+    int adjRes = res, n = 0;
+    FaceIJK centerIJK = *h;
+    FaceIJK fijkVerts[6];
+    _faceIjkVerts(&centerIJK, &adjRes, fijkVerts, 6);
+    int lastFace = -1, lastOverage = NO_OVERAGE;
+    for (int vert = 0; vert < 6 + 1; vert++) {
+        int v = vert % 6;
+        FaceIJK fijk = fijkVerts[v];
+        int overage = _adjustOverageClassII(&fijk, adjRes, 0, 1);
+        if (isResolutionClassIII(res) && vert > 0 && fijk.face != lastFace && lastOverage != FACE_EDGE) {
+            int lastV = (v + 5) % 6;
+            Vec2d orig2d0, orig2d1, e0, e1, inter;
+            _ijkToHex2d(&fijkVerts[lastV].coord, &orig2d0);
+            _ijkToHex2d(&fijkVerts[v].coord, &orig2d1);
+            int face2 = (lastFace == centerIJK.face) ? fijk.face : lastFace;
+            _faceEdge(adjRes, adjacentFaceDir(centerIJK.face, face2), &e0, &e1);
+            _v2dIntersect(&orig2d0, &orig2d1, &e0, &e1, &inter);
+            if (!(_v2dAlmostEquals(&orig2d0, &inter) || _v2dAlmostEquals(&orig2d1, &inter))) {
+                LatLng g;
+                _hex2dToGeo(&inter, centerIJK.face, adjRes, 1, &g);
+                lat[n] = radsToDegs(g.lat); lng[n] = radsToDegs(g.lng); n++;
+            }
+        }
+        if (vert < 6) {
+            Vec2d vec;
+            LatLng g;
+            _ijkToHex2d(&fijk.coord, &vec);
+            _hex2dToGeo(&vec, fijk.face, adjRes, 1, &g);
+            lat[n] = radsToDegs(g.lat); lng[n] = radsToDegs(g.lng); n++;
+        }
+        lastFace = fijk.face;
+        lastOverage = overage;
+    }
+    return n;
+}
+static int _faceIjkPentToCellBoundary(const FaceIJK *h, int res, double *lat, double *lng) {
+    int adjRes = res, n = 0;
+    FaceIJK centerIJK = *h;
+    FaceIJK fijkVerts[5];
+    _faceIjkVerts(&centerIJK, &adjRes, fijkVerts, 5);
+    FaceIJK lastFijk = fijkVerts[0];
+    for (int vert = 0; vert < 5 + 1; vert++) {
+        int v = vert % 5;
+        FaceIJK fijk = fijkVerts[v];
+        while (_adjustOverageClassII(&fijk, adjRes, 0, 1) == NEW_FACE) continue;   /* _adjustPentVertOverage */
+        if (isResolutionClassIII(res) && vert > 0) {
+            FaceIJK tmpFijk = fijk;
+            Vec2d orig2d0, orig2d1, e0, e1, inter;
+            _ijkToHex2d(&lastFijk.coord, &orig2d0);
+            int currentToLastDir = adjacentFaceDir(tmpFijk.face, lastFijk.face);
+            const int *o = H3T_faceNeighbors[tmpFijk.face][currentToLastDir];
+            tmpFijk.face = o[0];
+            CoordIJK *ijk = &tmpFijk.coord;
+            for (int i = 0; i < o[4]; i++) _ijkRotate60ccw(ijk);
+            int unitScale = unitScaleByCIIres[adjRes] * 3;
+            ijk->i += o[1] * unitScale; ijk->j += o[2] * unitScale; ijk->k += o[3] * unitScale;
+            _ijkNormalize(ijk);
+            _ijkToHex2d(ijk, &orig2d1);
+            _faceEdge(adjRes, adjacentFaceDir(tmpFijk.face, fijk.face), &e0, &e1);
+            _v2dIntersect(&orig2d0, &orig2d1, &e0, &e1, &inter);
+            LatLng g;
+            _hex2dToGeo(&inter, tmpFijk.face, adjRes, 1, &g);
+            lat[n] = radsToDegs(g.lat); lng[n] = radsToDegs(g.lng); n++;
+        }
+        if (vert < 5) {
+            Vec2d vec;
+            LatLng g;
+            _ijkToHex2d(&fijk.coord, &vec);
+            _hex2dToGeo(&vec, fijk.face, adjRes, 1, &g);
+            lat[n] = radsToDegs(g.lat); lng[n] = radsToDegs(g.lng); n++;
+        }
+        lastFijk = fijk;
+    }
+    return n;
+}
+/* cellToBoundary in degrees (h3-py cell_to_boundary: radsToDegs of each vertex); returns the vertex count, -1 if
+ * h is not a valid cell index */
+int oracle_cell_to_boundary(uint64_t h, double *lat, double *lng) {
+    if (((h >> 59) & 0xf) != 1 || GET_RES(h) > MAX_H3_RES || GET_BC(h) >= H3T_NUM_BASE_CELLS) return -1;
+    FaceIJK fijk;
+    _h3ToFaceIjk(h, &fijk);
+    int res = GET_RES(h);
+    if (H3T_baseCellData[GET_BC(h)][4] && _h3LeadingNonZeroDigit(h) == 0)
+        return _faceIjkPentToCellBoundary(&fijk, res, lat, lng);
+    return _faceIjkToCellBoundary(&fijk, res, lat, lng);
+}
+void oracle_cell_to_boundary_batch(const uint64_t *cells, int64_t n, double *lat, double *lng, int32_t *nverts) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) nverts[i] = oracle_cell_to_boundary(cells[i], lat + 10 * i, lng + 10 * i);
 }

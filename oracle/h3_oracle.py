@@ -1,6 +1,6 @@
 """ORACLE -- test infrastructure only (never imported by the product path).
 
-ctypes wrapper of oracle/libh3oracle.so, the C restatement of H3 v4 latLngToCell / cellToLatLng
+ctypes wrapper of oracle/libh3oracle.so, the C restatement of H3 v4 latLngToCell / cellToLatLng / cellToBoundary
 (see h3_oracle.c for provenance).  Builds the library with `make -C oracle` when it is missing.
 """
 import ctypes
@@ -32,6 +32,8 @@ def load():
         L.oracle_latlng_to_cell_batch.argtypes = [P, P, ctypes.c_int64, ctypes.c_int, P]
         L.oracle_cell_to_latlng_batch.restype = None
         L.oracle_cell_to_latlng_batch.argtypes = [P, ctypes.c_int64, P, P]
+        L.oracle_cell_to_boundary_batch.restype = None
+        L.oracle_cell_to_boundary_batch.argtypes = [P, ctypes.c_int64, P, P, P]
         L.oracle_ld_ops.restype = None
         L.oracle_ld_ops.argtypes = [P, ctypes.c_int64, ctypes.c_int, P]
         _lib = L
@@ -55,6 +57,17 @@ def cell_to_latlng(cells):
     lo = np.empty(cells.size)
     L.oracle_cell_to_latlng_batch(cells.ctypes.data, cells.size, la.ctypes.data, lo.ctypes.data)
     return la, lo
+
+
+def cell_to_boundary(cells):
+    """h3.cell_to_boundary for arrays of cells: (lat [n, 10], lng [n, 10], nverts [n]); nverts -1 = invalid."""
+    L = load()
+    cells = np.ascontiguousarray(cells, dtype=np.uint64)
+    la = np.full((cells.size, 10), np.nan)
+    lo = np.full((cells.size, 10), np.nan)
+    nv = np.zeros(cells.size, np.int32)
+    L.oracle_cell_to_boundary_batch(cells.ctypes.data, cells.size, la.ctypes.data, lo.ctypes.data, nv.ctypes.data)
+    return la, lo, nv
 
 
 def ld_ops(a, op):

@@ -336,6 +336,12 @@ struct H3Tables {
     double fastScale[16];
     int faceIjkBaseCells[20][3][3][3][2];
     int baseCellData[122][7];
+    // cellToBoundary (h3_boundary.h): faceNeighbors[f][dir] = {face, translate i, j, k, ccwRot60} (dir 0 centre,
+    // 1 IJ, 2 KI, 3 JK), adjacentFaceDir[from][to] (0 same face, -1 not adjacent), and the icosahedron-face edge
+    // ordinate (double)(3.0L * M_SQRT3_2 * maxDimByCIIres[r]) of each substrate resolution r
+    int faceNeighbors[20][4][5];
+    signed char adjacentFaceDir[20][20];
+    double edgeY[17];
 };
 
 // _faceIjkToH3 (faceijk.c), res >= 1

@@ -18,8 +18,7 @@ static hm::H3Tables hm_make_tables() {
         T.faceAxesAz0[f] = H3T_faceAxesAzRadsCII[f][0];
         // upstream evaluates cos/sin(p1->lat) per call with the host libm; identical values
         volatile double lat = H3T_faceCenterGeo[f][0];
-        T.faceCosLat[f] = std::cos(lat);
-        T.faceSinLat[f] = std::sin(lat);
+        sincos(lat, &T.faceSinLat[f], &T.faceCosLat[f]);   // (the pair gcc fuses; equal to sin/cos for all 20 here)
         // fast-path gnomonic axes (h3_device.h, latLngToCellFast), in x87 extended precision
         const long double phi = H3T_faceCenterGeo[f][0], lam = H3T_faceCenterGeo[f][1], az0 = H3T_faceAxesAzRadsCII[f][0];
         const long double n[3] = {-sinl(phi) * cosl(lam), -sinl(phi) * sinl(lam), cosl(phi)};
@@ -39,5 +38,20 @@ static hm::H3Tables hm_make_tables() {
     for (int r = 0; r < 16; r++) T.fastScale[r] = (double)((long double)HM_INV_RES0_U_GNOMONIC * powl(sqrtl(7.0L), r));
     memcpy(T.faceIjkBaseCells, H3T_faceIjkBaseCells, sizeof(T.faceIjkBaseCells));
     memcpy(T.baseCellData, H3T_baseCellData, sizeof(T.baseCellData));
+    memcpy(T.faceNeighbors, H3T_faceNeighbors, sizeof(T.faceNeighbors));
+    for (int a = 0; a < 20; a++)
+        for (int b = 0; b < 20; b++) {
+            signed char d = a == b ? 0 : -1;
+            for (int dir = 1; dir <= 3; dir++)
+                if (H3T_faceNeighbors[a][dir][0] == b) d = (signed char)dir;
+            T.adjacentFaceDir[a][b] = d;
+        }
+    const long double sqrt3_2 = 0.8660254037844386467637231707529361834714L;   // M_SQRT3_2
+    for (int r = 0; r < 17; r++) {
+        int m = 2;
+        for (int q = 0; q < r; q += 2) m *= 7;
+        volatile long double three = 3.0L;   // (3.0 * M_SQRT3_2) * maxDim, both in long double, as upstream
+        T.edgeY[r] = (double)((three * sqrt3_2) * (long double)m);
+    }
     return T;
 }

@@ -35,6 +35,8 @@
 #include "kernels.h"
 #include "bson_docs.h"
 #include "json_decode.h"
+#include "h3_boundary.h"
+#include <mutex>
 
 #define H3T_CONST static const
 #include "h3_tables.inc"
@@ -1846,6 +1848,21 @@ __global__ __launch_bounds__(HS_THREADS) void k_sample_heavy(const uint64_t *__r
     if (t == 0) st->sample_max_run = best;
 }
 
+// the read side's cellToBoundary (row f4; h3_boundary.h): up to 10 vertices per cell, lat/lng degrees
+__global__ __launch_bounds__(256) void k_cells_boundary(const uint64_t *__restrict__ cells, int64_t n, double *__restrict__ lat,
+                                                        double *__restrict__ lng, int32_t *__restrict__ nverts) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        double la[10], lo[10];
+        const int nv = cellToBoundaryDeg(cells[i], c_tab, la, lo);
+        nverts[i] = nv;
+        for (int k = 0; k < 10; k++) {
+            lat[10 * i + k] = k < nv ? la[k] : __builtin_nan("");
+            lng[10 * i + k] = k < nv ? lo[k] : __builtin_nan("");
+        }
+    }
+}
+
 // =====================================================================================================
 // K0: Kafka values -> batch columns (row f1: from_json + to_timestamp, heatmap_stream.py:88-93; json_decode.h),
 // one thread per record; then the exact string dictionaries of provider and vehicleId (hash table keyed by a
@@ -3372,48 +3389,130 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     return HM_OK;
 }
 
+// ---- context-free entry points (the standalone UDF and the read side): per-device tables, stream and scratch
+// buffers made once and reused, behind one mutex ----
+struct UdfState {
+    bool ready = false;
+    int64_t last_exact = 0;   // hm_latlng_to_cell: inputs the fast path handed to the exact path (last call)
+    hipStream_t stream = nullptr;
+    DevBuf in0, in1, out0, out1, out2, slow;
+};
+static std::mutex g_udf_mu;
+static UdfState g_udf[64];
+static hipError_t udf_buf(DevBuf &b, size_t bytes) {
+    if (b.bytes >= bytes && b.p) return hipSuccess;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e == hipSuccess) b.bytes = want;
+    return e;
+}
+static int udf_begin(int32_t device, UdfState *&S) {   // (g_udf_mu held)
+    int ndev = 0;
+    if (device < 0 || device >= 64 || hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device) return HM_E_HIP;
+    if (hipSetDevice(device) != hipSuccess) return HM_E_HIP;
+    S = &g_udf[device];
+    if (!S->ready) {
+        H3Tables T = make_tables();
+        if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &T, sizeof(T)) != hipSuccess) return HM_E_HIP;
+        if (hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) != hipSuccess) return HM_E_HIP;
+        S->ready = true;
+    }
+    return HM_OK;
+}
+
 int hm_latlng_to_cell(const double *lat, const double *lon, int64_t n, int32_t res, int32_t memory, int32_t device,
                       uint64_t *out) {
     if (n < 0 || n > (int64_t)UINT32_MAX || res < 0 || res > 15) return HM_E_INVALID;
     if (n == 0) return HM_OK;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device) return HM_E_HIP;
-    if (hipSetDevice(device) != hipSuccess) return HM_E_HIP;
-    static bool tables_loaded[64] = {};
-    if (!tables_loaded[device]) {
-        H3Tables T = make_tables();
-        if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &T, sizeof(T)) != hipSuccess) return HM_E_HIP;
-        tables_loaded[device] = true;
-    }
+    std::lock_guard<std::mutex> lock(g_udf_mu);
+    UdfState *S = nullptr;
+    int rc;
+    if ((rc = udf_begin(device, S))) return rc;
     const double *dlat = lat, *dlon = lon;
     uint64_t *dout = out;
-    void *a = nullptr, *b = nullptr, *c = nullptr, *sl = nullptr;
-    auto cleanup = [&]() {
-        for (void *p : {a, b, c, sl})
-            if (p) (void)hipFree(p);
-    };
     // exception list + its count (last 8 bytes)
-    if (hipMalloc(&sl, n * 4 + 16) != hipSuccess) { cleanup(); return HM_E_NOMEM; }
-    unsigned long long *n_slow = (unsigned long long *)((char *)sl + ((n * 4 + 7) & ~int64_t(7)));
+    if (udf_buf(S->slow, n * 4 + 16) != hipSuccess) return HM_E_NOMEM;
+    unsigned long long *n_slow = (unsigned long long *)((char *)S->slow.p + ((n * 4 + 7) & ~int64_t(7)));
+    hipError_t e = hipSuccess;
     if (memory == HM_MEM_HOST) {
-        if (hipMalloc(&a, n * 8) || hipMalloc(&b, n * 8) || hipMalloc(&c, n * 8)) { cleanup(); return HM_E_NOMEM; }
-        if (hipMemcpy(a, lat, n * 8, hipMemcpyHostToDevice) || hipMemcpy(b, lon, n * 8, hipMemcpyHostToDevice)) { cleanup(); return HM_E_HIP; }
-        dlat = (const double *)a;
-        dlon = (const double *)b;
-        dout = (uint64_t *)c;
+        if (udf_buf(S->in0, n * 8) || udf_buf(S->in1, n * 8) || udf_buf(S->out0, n * 8)) return HM_E_NOMEM;
+        e = hipMemcpyAsync(S->in0.p, lat, n * 8, hipMemcpyHostToDevice, S->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(S->in1.p, lon, n * 8, hipMemcpyHostToDevice, S->stream);
+        dlat = (const double *)S->in0.p;
+        dlon = (const double *)S->in1.p;
+        dout = (uint64_t *)S->out0.p;
     }
-    hipError_t e = hipMemset(n_slow, 0, 8);
+    if (e == hipSuccess) e = hipMemsetAsync(n_slow, 0, 8, S->stream);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_cells, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, 0, dlat, dlon, n, res, dout,
-                           (unsigned int *)sl, n_slow);
-        hipLaunchKernelGGL(k_cells_exact, dim3(256), dim3(256), 0, 0, dlat, dlon, res, dout, (const unsigned int *)sl,
+        hipLaunchKernelGGL(k_cells, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, S->stream, dlat, dlon, n, res, dout,
+                           (unsigned int *)S->slow.p, n_slow);
+        hipLaunchKernelGGL(k_cells_exact, dim3(256), dim3(256), 0, S->stream, dlat, dlon, res, dout, (const unsigned int *)S->slow.p,
                            (const unsigned long long *)n_slow);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e == hipSuccess && memory == HM_MEM_HOST) e = hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost);
-    cleanup();
+    if (e == hipSuccess && memory == HM_MEM_HOST) e = hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, S->stream);
+    unsigned long long ne = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&ne, n_slow, 8, hipMemcpyDeviceToHost, S->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(S->stream);
+    S->last_exact = (int64_t)ne;
     return e == hipSuccess ? HM_OK : HM_E_HIP;
+}
+
+int64_t hm_latlng_to_cell_last_exact(int32_t device) {
+    std::lock_guard<std::mutex> lock(g_udf_mu);
+    return device >= 0 && device < 64 ? g_udf[device].last_exact : -1;
+}
+
+int hm_cells_to_boundary(const uint64_t *cells, int64_t n, int32_t memory, int32_t device, double *lat, double *lng,
+                         int32_t *nverts) {
+    if (n < 0 || n > (int64_t)UINT32_MAX || (n > 0 && (!cells || !lat || !lng || !nverts))) return HM_E_INVALID;
+    if (n == 0) return HM_OK;
+    std::lock_guard<std::mutex> lock(g_udf_mu);
+    UdfState *S = nullptr;
+    int rc;
+    if ((rc = udf_begin(device, S))) return rc;
+    const uint64_t *dcells = cells;
+    double *dlat = lat, *dlng = lng;
+    int32_t *dnv = nverts;
+    hipError_t e = hipSuccess;
+    if (memory == HM_MEM_HOST) {
+        if (udf_buf(S->in0, n * 8) || udf_buf(S->out0, n * 80) || udf_buf(S->out1, n * 80) || udf_buf(S->out2, n * 4))
+            return HM_E_NOMEM;
+        e = hipMemcpyAsync(S->in0.p, cells, n * 8, hipMemcpyHostToDevice, S->stream);
+        dcells = (const uint64_t *)S->in0.p;
+        dlat = (double *)S->out0.p;
+        dlng = (double *)S->out1.p;
+        dnv = (int32_t *)S->out2.p;
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_cells_boundary, dim3(grid_for(n, 256, 256 * 32)), dim3(256), 0, S->stream, dcells, n, dlat, dlng, dnv);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess && memory == HM_MEM_HOST) {
+        e = hipMemcpyAsync(lat, dlat, n * 80, hipMemcpyDeviceToHost, S->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(lng, dlng, n * 80, hipMemcpyDeviceToHost, S->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(nverts, dnv, n * 4, hipMemcpyDeviceToHost, S->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(S->stream);
+    return e == hipSuccess ? HM_OK : HM_E_HIP;
+}
+
+int hm_selftest_cells_to_boundary_host(const uint64_t *cells, int64_t n, double *lat, double *lng, int32_t *nverts) {
+    if (n < 0 || (n > 0 && (!cells || !lat || !lng || !nverts))) return HM_E_INVALID;
+    static const H3Tables T = make_tables();
+    for (int64_t i = 0; i < n; i++) {
+        double la[10], lo[10];
+        const int nv = cellToBoundaryDeg(cells[i], T, la, lo);
+        nverts[i] = nv;
+        for (int k = 0; k < 10; k++) {
+            lat[10 * i + k] = k < nv ? la[k] : NAN;
+            lng[10 * i + k] = k < nv ? lo[k] : NAN;
+        }
+    }
+    return HM_OK;
 }
 
 // ---- multi-GPU stage API ----
@@ -4257,6 +4356,10 @@ int hm_selftest_ld_ops(const double *a, int64_t n, int32_t op, double *out) {
             case 4: r = XADD(x, true, 2PI); break;
             case 5: r = XADD(x, true, AP7_ROT); break;
             case 6: r = XADD(x, false, AP7_ROT); break;
+            case 7: r = XMUL(x, SQRT3_2); break;
+            case 8: r = XMUL(x, RSQRT7); break;
+            case 9: r = XMUL(x, ONETHIRD); break;
+            case 17: r = XMUL(x, 180_PI); break;
             case 10: r = xld_mul(x, HM_LD_PI_180_M, HM_LD_PI_180_E); break;
             case 11: r = xld_mul(x, HM_LD_SQRT7_M, HM_LD_SQRT7_E); break;
             case 12: r = xld_mul(x, HM_LD_RSIN60_M, HM_LD_RSIN60_E); break;

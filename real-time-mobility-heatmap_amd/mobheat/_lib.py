@@ -116,6 +116,9 @@ SIGNATURES = {
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_last_counts": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_decode_json": (c_i32, [c_vp, _P(HmJsonIn), _P(HmJsonOut)]),
+    "hm_latlng_to_cell_last_exact": (c_i64, [c_i32]),
+    "hm_cells_to_boundary": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),
+    "hm_selftest_cells_to_boundary_host": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp]),
     "hm_last_latest_buckets": (c_i32, [c_vp, c_vp, c_i64, _P(c_i64)]),
     "hm_selftest_json_records": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                          c_vp, c_vp]),
@@ -361,3 +364,15 @@ def decimal_to_double_selftest(w, q):
     out = np.empty(w.size, np.uint64)
     check(lib.hm_selftest_decimal_to_double(ptr(w), ptr(q), w.size, ptr(out)), None, "hm_selftest_decimal_to_double")
     return out
+
+
+def cells_to_boundary_host_selftest(cells):
+    """Host execution of the device cellToBoundary: (lat [n, 10], lng [n, 10], nverts [n])."""
+    lib = load()
+    cells = np.ascontiguousarray(cells, dtype=np.uint64)
+    la = np.empty((cells.size, 10))
+    lo = np.empty((cells.size, 10))
+    nv = np.empty(cells.size, np.int32)
+    check(lib.hm_selftest_cells_to_boundary_host(ptr(cells), cells.size, ptr(la), ptr(lo), ptr(nv)), None,
+          "hm_selftest_cells_to_boundary_host")
+    return la, lo, nv

@@ -1,0 +1,103 @@
+"""GPU: row f4 (cellToBoundary, the read side of reference app.py:19-41) against the oracle, and latLngToCell on
+constructed near-ties at every resolution (pentagon centres = icosahedron vertices, icosahedron
+edge midpoints, face centres, cell centres, vertices and edge midpoints, each nudged by 1-8 ulp)."""
+import numpy as np
+import pytest
+
+from mobheat import _lib
+from oracle import h3_oracle
+
+pytestmark = pytest.mark.gpu
+PENTAGON_BASE_CELLS = [4, 14, 24, 38, 49, 58, 63, 72, 83, 97, 107, 117]
+# boundary coordinates: vertex counts exact; coordinates within 1e-12 degrees (~0.1 um on the ground) of the
+# glibc-linked oracle -- the device math library's atan2/atan/asin/sincos may differ from glibc's in the last bit
+BOUNDARY_TOL_DEG = 1e-12
+
+
+def _random_cells(res, n, seed):
+    rng = np.random.default_rng(seed)
+    lat = np.degrees(np.arcsin(rng.uniform(-1, 1, n)))
+    lon = rng.uniform(-180, 180, n)
+    return h3_oracle.latlng_to_cell(lat, lon, res)
+
+
+@pytest.mark.parametrize("res", [0, 1, 2, 5, 7, 8, 9, 12, 15])
+def test_cells_to_boundary_matches_oracle(res):
+    from mobheat import readside
+    cells = _random_cells(res, 100_000, res)
+    base = np.array([(1 << 59) | (res << 52) | (bc << 45) | ((1 << (3 * (15 - res))) - 1) for bc in PENTAGON_BASE_CELLS],
+                    np.uint64)   # the pentagons at this resolution (centre children of the 12 pentagon base cells)
+    cells = np.concatenate([cells, base, np.array([0, 0x8a2a1072b59ffff | (1 << 63)], np.uint64)])
+    la, lo, nv = readside.cells_to_boundary(cells)
+    x, y, z = h3_oracle.cell_to_boundary(cells)
+    z = np.maximum(z, 0)
+    assert np.array_equal(nv, z)
+    m = ~np.isnan(x)
+    assert np.abs(la[m] - x[m]).max() <= BOUNDARY_TOL_DEG and np.abs(lo[m] - y[m]).max() <= BOUNDARY_TOL_DEG
+    exact = float(((la[m] == x[m]) & (lo[m] == y[m])).mean())
+    print(f"res {res}: {cells.size} cells, {exact:.6f} of the vertices bit-identical to the oracle")
+
+
+def test_boundary_geojson_ring_and_collection():
+    import datetime
+    from mobheat import readside
+    ring = readside.h3_boundary_geojson("85283473fffffff")
+    assert len(ring) == 7 and ring[0] == ring[-1]
+    assert abs(ring[0][0] - -121.91508032705622) < 1e-12 and abs(ring[0][1] - 37.271355866731895) < 1e-12
+    ws = datetime.datetime(2025, 10, 4, 10, 20)
+    docs = [{"cellId": "882a1072b5fffff", "count": 3, "avgSpeedKmh": 12.5, "windowStart": ws,
+             "windowEnd": ws + datetime.timedelta(minutes=5)}]
+    fc = readside.tiles_latest_collection(docs)
+    f = fc["features"][0]
+    assert fc["type"] == "FeatureCollection" and f["geometry"]["type"] == "Polygon"
+    assert f["properties"] == {"cellId": "882a1072b5fffff", "count": 3, "avgSpeedKmh": 12.5,
+                               "windowStart": "2025-10-04T10:20:00", "windowEnd": "2025-10-04T10:25:00"}
+
+
+def _nudged(lat, lon, k=8):
+    """every point, and each moved by 1..k ulp up and down in lat, and in lon"""
+    la, lo = [lat], [lon]
+    for s in range(1, k + 1):
+        for sg in (-1, 1):
+            la.append(lat + sg * s * np.spacing(lat))
+            lo.append(lon)
+            la.append(lat)
+            lo.append(lon + sg * s * np.spacing(lon))
+    return np.concatenate(la), np.concatenate(lo)
+
+
+def _near_tie_points(res):
+    pent = np.array([(1 << 59) | (bc << 45) | ((1 << 45) - 1) for bc in PENTAGON_BASE_CELLS], np.uint64)
+    plat, plon = h3_oracle.cell_to_latlng(pent)   # pentagon centres = the icosahedron's vertices
+    v = np.stack([np.cos(np.radians(plat)) * np.cos(np.radians(plon)), np.cos(np.radians(plat)) * np.sin(np.radians(plon)),
+                  np.sin(np.radians(plat))], 1)
+    d = v @ v.T
+    i, j = np.nonzero(np.triu(d > 0.4, 1))          # the 30 icosahedron edges (adjacent vertices)
+    mid = v[i] + v[j]
+    mid /= np.linalg.norm(mid, axis=1, keepdims=True)
+    elat, elon = np.degrees(np.arcsin(mid[:, 2])), np.degrees(np.arctan2(mid[:, 1], mid[:, 0]))
+    cells = _random_cells(res, 300, 1000 + res)
+    clat, clon = h3_oracle.cell_to_latlng(cells)
+    bla, blo, bnv = h3_oracle.cell_to_boundary(cells)
+    vla = np.concatenate([bla[k, :bnv[k]] for k in range(cells.size)])
+    vlo = np.concatenate([blo[k, :bnv[k]] for k in range(cells.size)])
+    mla = np.concatenate([(bla[k, :bnv[k]] + np.roll(bla[k, :bnv[k]], -1)) / 2 for k in range(cells.size)])
+    mlo = np.concatenate([(blo[k, :bnv[k]] + np.roll(blo[k, :bnv[k]], -1)) / 2 for k in range(cells.size)])
+    lat = np.concatenate([plat, elat, clat, vla, mla])
+    lon = np.concatenate([plon, elon, clon, vlo, mlo])
+    return _nudged(lat, lon)
+
+
+@pytest.mark.parametrize("res", range(16))
+def test_latlng_to_cell_constructed_near_ties(res):
+    """the fast path's margin logic where bit-exactness actually breaks: every result equals the oracle, and the
+    exact path ran on some of these inputs"""
+    from mobheat import latlng_to_cell
+    lat, lon = _near_tie_points(res)
+    got = latlng_to_cell(lat, lon, res)
+    n_exact = _lib.load().hm_latlng_to_cell_last_exact(0)
+    exp = h3_oracle.latlng_to_cell(lat, lon, res)
+    ok = (np.abs(lat) <= 90) & (np.abs(lon) <= 180)
+    assert np.array_equal(got[ok], exp[ok])
+    assert n_exact > 0, "no input reached the exact path"
+    print(f"res {res}: {lat.size} near-tie inputs, {n_exact} through the exact path")
