@@ -27,8 +27,7 @@
 #include <stdint.h>
 #include <string.h>
 
-#define H3T_CONST static const
-#include "../real-time-mobility-heatmap_amd/csrc/h3_tables.inc"
+#include <stdio.h>
 
 /* upstream constants.h / coordijk.h (v4) */
 #define M_PI_180 0.0174532925199432957692369076848861271111L
@@ -53,6 +52,9 @@ typedef struct { double x, y, z; } Vec3d;
 typedef struct { double x, y; } Vec2d;
 typedef struct { int i, j, k; } CoordIJK;
 typedef struct { int face; CoordIJK coord; } FaceIJK;
+
+/* the oracle's own tables: primary constants + derived discrete tables (not the product's h3_tables.inc) */
+#include "h3_tables_oracle.h"
 
 enum { CENTER_DIGIT = 0, K_AXES_DIGIT = 1, J_AXES_DIGIT = 2, JK_AXES_DIGIT = 3, I_AXES_DIGIT = 4,
        IK_AXES_DIGIT = 5, IJ_AXES_DIGIT = 6, INVALID_DIGIT = 7 };
@@ -688,3 +690,6 @@ void oracle_cell_to_boundary_batch(const uint64_t *cells, int64_t n, double *lat
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; i++) nverts[i] = oracle_cell_to_boundary(cells[i], lat + 10 * i, lng + 10 * i);
 }
+
+/* derivation of the discrete tables at load (needs the projections above) */
+#include "h3_tables_derive.c"

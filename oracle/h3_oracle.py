@@ -15,7 +15,8 @@ _lib = None
 
 
 def build(force=False):
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "h3_oracle.c")):
+    srcs = ("h3_oracle.c", "h3_tables_oracle.h", "h3_tables_derive.c")
+    if force or not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, s)) for s in srcs):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB
 
@@ -34,6 +35,8 @@ def load():
         L.oracle_cell_to_latlng_batch.argtypes = [P, ctypes.c_int64, P, P]
         L.oracle_cell_to_boundary_batch.restype = None
         L.oracle_cell_to_boundary_batch.argtypes = [P, ctypes.c_int64, P, P, P]
+        L.oracle_tables.restype = ctypes.c_int
+        L.oracle_tables.argtypes = [P, P, P, ctypes.POINTER(ctypes.c_char_p)]
         L.oracle_ld_ops.restype = None
         L.oracle_ld_ops.argtypes = [P, ctypes.c_int64, ctypes.c_int, P]
         _lib = L
@@ -77,3 +80,16 @@ def ld_ops(a, op):
     out = np.empty_like(a)
     L.oracle_ld_ops(a.ctypes.data, a.size, int(op), out.ctypes.data)
     return out
+
+
+def tables():
+    """The oracle's own derived res-0 tables (h3_tables_derive.c): (baseCellData [122, 7], faceIjkBaseCells
+    [20, 3, 3, 3, 2], faceNeighbors [20, 4, 5]); raises if one of the derivation's checks failed."""
+    L = load()
+    bcd = np.zeros((122, 7), np.int32)
+    fib = np.zeros((20, 3, 3, 3, 2), np.int32)
+    fn = np.zeros((20, 4, 5), np.int32)
+    err = ctypes.c_char_p()
+    if L.oracle_tables(bcd.ctypes.data, fib.ctypes.data, fn.ctypes.data, ctypes.byref(err)) != 0:
+        raise RuntimeError("oracle table derivation failed: " + err.value.decode())
+    return bcd, fib, fn

@@ -1361,10 +1361,14 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                 v.slon = oslon + S.sslon[t];
                 if constexpr (rehash) v.touched = p.touched;
                 else v.touched = ((unsigned long long)seq << 32) | krow;
+#ifdef HM_ABL_NOSLOT   // ablation builds only: the state line stores priced by their absence
+                if (created) { created_cnt++; } else if (false) {
+#else
                 if (created) {
                     *gslot = v;
                     created_cnt++;
                 } else {
+#endif
                     gslot->count = v.count;
                     if (ansp) {
                         gslot->nspeed = v.nspeed;
