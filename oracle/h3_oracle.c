@@ -23,6 +23,7 @@
  * Parity status: UNPINNED against h3-py (not importable here; the reference ships no fixtures).  Anchors:
  * three public known-answer vectors from upstream READMEs, round-trip and table self-consistency checks.
  */
+#define _GNU_SOURCE   /* sincos */
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
@@ -74,11 +75,28 @@ static double _posAngleRads(double rads) {
     return tmp;
 }
 
+/* libm-sensitivity probe (tests only, oracle_latlng_to_cell_perturbed): the result of transcendental call site
+ * `pt_site` of latLngToCell's forward path is moved by `pt_ulps` ulps; -1 = off.  Sites: 0 cos(lat), 1 sin(lat),
+ * 2 cos(lng), 3 sin(lng), 4 acos, 5 sin(dlng), 6 cos(dlng), 7 atan2, 8 tan, 9 cos(theta), 10 sin(theta)
+ * (cos/sin of the point's latitude are the same values wherever upstream recomputes them). */
+static __thread int pt_site = -1, pt_ulps = 0;
+static double PT(int site, double x) {
+    if (site != pt_site) return x;
+    for (int u = 0; u < pt_ulps; u++) x = nextafter(x, INFINITY);
+    for (int u = 0; u > pt_ulps; u--) x = nextafter(x, -INFINITY);
+    return x;
+}
+
+/* sin and cos of one argument as one sincos() call: gcc merges upstream's separate calls so (-O1 and up, no fast-math),
+ * and glibc's sincos can differ from its sin/cos in the last bit (their FMA variants) */
 static void _geoToVec3d(const LatLng *geo, Vec3d *v) {
-    double r = cos(geo->lat);
-    v->z = sin(geo->lat);
-    v->x = cos(geo->lng) * r;
-    v->y = sin(geo->lng) * r;
+    double s, c, sg, cg;
+    sincos(geo->lat, &s, &c);
+    sincos(geo->lng, &sg, &cg);
+    double r = PT(0, c);
+    v->z = PT(1, s);
+    v->x = PT(2, cg) * r;
+    v->y = PT(3, sg) * r;
 }
 
 static double _square(double x) { return x * x; }
@@ -103,8 +121,12 @@ static void _geoToClosestFace(const LatLng *g, int *face, double *sqd) {
 }
 
 static double _geoAzimuthRads(const LatLng *p1, const LatLng *p2) {
-    return atan2(cos(p2->lat) * sin(p2->lng - p1->lng),
-                 cos(p1->lat) * sin(p2->lat) - sin(p1->lat) * cos(p2->lat) * cos(p2->lng - p1->lng));
+    double s2, c2, s1, c1, sd, cd;
+    sincos(p2->lat, &s2, &c2);
+    sincos(p2->lng - p1->lng, &sd, &cd);
+    sincos(p1->lat, &s1, &c1);
+    c2 = PT(0, c2);
+    return PT(7, atan2(c2 * PT(5, sd), c1 * PT(1, s2) - s1 * c2 * PT(6, cd)));
 }
 
 static int isResolutionClassIII(int r) { return r % 2; }
@@ -112,7 +134,7 @@ static int isResolutionClassIII(int r) { return r % 2; }
 static void _geoToHex2d(const LatLng *g, int res, int *face, Vec2d *v) {
     double sqd;
     _geoToClosestFace(g, face, &sqd);
-    double r = acos(1 - sqd / 2);
+    double r = PT(4, acos(1 - sqd / 2));
     if (r < EPSILON) {
         v->x = v->y = 0.0;
         return;
@@ -120,11 +142,13 @@ static void _geoToHex2d(const LatLng *g, int res, int *face, Vec2d *v) {
     LatLng fc = {H3T_faceCenterGeo[*face][0], H3T_faceCenterGeo[*face][1]};
     double theta = _posAngleRads(H3T_faceAxesAzRadsCII[*face][0] - _posAngleRads(_geoAzimuthRads(&fc, g)));
     if (isResolutionClassIII(res)) theta = _posAngleRads(theta - M_AP7_ROT_RADS);
-    r = tan(r);
+    r = PT(8, tan(r));
     r *= INV_RES0_U_GNOMONIC;
     for (int i = 0; i < res; i++) r *= M_SQRT7;
-    v->x = r * cos(theta);
-    v->y = r * sin(theta);
+    double st, ct;
+    sincos(theta, &st, &ct);
+    v->x = r * PT(9, ct);
+    v->y = r * PT(10, st);
 }
 
 static void _ijkNormalize(CoordIJK *c) {
@@ -329,6 +353,21 @@ uint64_t oracle_latlng_to_cell(double lat_deg, double lng_deg, int res) {
 void oracle_latlng_to_cell_batch(const double *lat, const double *lng, int64_t n, int res, uint64_t *out) {
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; i++) out[i] = oracle_latlng_to_cell(lat[i], lng[i], res);
+}
+
+/* latLngToCell with the result of one transcendental call site moved by `ulps` ulps (see PT): the answers a libm
+ * differing from this one in the last bits of that function could give.  An input whose cell changes under such a
+ * perturbation is libm-sensitive: h3 itself returns different cells for it on different platforms (glibc's FMA and
+ * non-FMA variants, other libms). */
+void oracle_latlng_to_cell_perturbed_batch(const double *lat, const double *lng, int64_t n, int res, int site, int ulps,
+                                           uint64_t *out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        pt_site = site;
+        pt_ulps = ulps;
+        out[i] = oracle_latlng_to_cell(lat[i], lng[i], res);
+        pt_site = -1;
+    }
 }
 
 /* ---------------- inverse, validation only: cellToLatLng ---------------- */

@@ -31,6 +31,8 @@ def load():
         L.oracle_latlng_to_cell.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int]
         L.oracle_latlng_to_cell_batch.restype = None
         L.oracle_latlng_to_cell_batch.argtypes = [P, P, ctypes.c_int64, ctypes.c_int, P]
+        L.oracle_latlng_to_cell_perturbed_batch.restype = None
+        L.oracle_latlng_to_cell_perturbed_batch.argtypes = [P, P, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
         L.oracle_cell_to_latlng_batch.restype = None
         L.oracle_cell_to_latlng_batch.argtypes = [P, ctypes.c_int64, P, P]
         L.oracle_cell_to_boundary_batch.restype = None
@@ -40,6 +42,7 @@ def load():
         L.oracle_ld_ops.restype = None
         L.oracle_ld_ops.argtypes = [P, ctypes.c_int64, ctypes.c_int, P]
         _lib = L
+        tables()   # the tables are derived at load: fail loudly if a derivation check failed on this host
     return _lib
 
 
@@ -51,6 +54,44 @@ def latlng_to_cell(lat, lon, res):
     out = np.empty(lat.size, dtype=np.uint64)
     L.oracle_latlng_to_cell_batch(lat.ctypes.data, lon.ctypes.data, lat.size, int(res), out.ctypes.data)
     return out
+
+
+N_LIBM_SITES = 11   # transcendental call sites of the forward path (h3_oracle.c PT)
+
+
+def libm_alternatives(lat, lon, res, max_ulps=2):
+    """[k, n] cells of latLngToCell with one transcendental call site's result moved by +-1..max_ulps ulps (k =
+    N_LIBM_SITES * 2 * max_ulps): the cells another libm (last-bit differences) could make h3 return."""
+    L = load()
+    lat = np.ascontiguousarray(lat, dtype=np.float64)
+    lon = np.ascontiguousarray(lon, dtype=np.float64)
+    alts = []
+    for site in range(N_LIBM_SITES):
+        for u in range(1, max_ulps + 1):
+            for sg in (-1, 1):
+                out = np.empty(lat.size, dtype=np.uint64)
+                L.oracle_latlng_to_cell_perturbed_batch(lat.ctypes.data, lon.ctypes.data, lat.size, int(res), site, sg * u,
+                                                       out.ctypes.data)
+                alts.append(out)
+    return np.stack(alts) if alts else np.empty((0, lat.size), np.uint64)
+
+
+NEIGHBOURHOOD_ULPS = (-32, -16, -8, -4, -2, -1, 0, 1, 2, 4, 8, 16, 32)
+
+
+def neighbourhood_cells(lat, lon, res, steps=NEIGHBOURHOOD_ULPS):
+    """[k, n] cells of the inputs moved by (i, j) units in (lat, lon) for i, j in steps (k = len(steps)^2), a unit being
+    one ulp of max(|coordinate|, 45) degrees (7.1e-15 degrees, ~1e-16 rad: the absolute scale of a last-bit error of
+    sin/cos/atan2, whatever the coordinate's own magnitude): the cells whose boundary passes within a few such errors
+    of the point -- where last-bit differences of the libm can land it."""
+    lat = np.asarray(lat, dtype=np.float64)
+    lon = np.asarray(lon, dtype=np.float64)
+    ua, uo = np.spacing(np.maximum(np.abs(lat), 45.0)), np.spacing(np.maximum(np.abs(lon), 45.0))
+    out = []
+    for i in steps:
+        for j in steps:
+            out.append(latlng_to_cell(lat + i * ua, lon + j * uo, res))
+    return np.stack(out)
 
 
 def cell_to_latlng(cells):

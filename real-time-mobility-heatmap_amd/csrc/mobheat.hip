@@ -1086,28 +1086,35 @@ __device__ __forceinline__ T ld_l2(const T *p) {   // bypass the CU's L1 (chunks
 __device__ __forceinline__ unsigned mo_claim_home(unsigned long long addr) {
     return (unsigned)(((addr >> 6) * UINT64_C(0x9e3779b97f4a7c15)) >> 40) & (MO_CLAIM - 1);
 }
-// claim slot `addr` for `lane`: -1 = claimed (entry index in ci), else the lane that already holds it
-__device__ __forceinline__ int mo_claim(MoShared &S, unsigned long long addr, int lane, int &ci) {
+// claim slot `addr` for `lane` in claim set cl: -1 = claimed (entry index in ci), else the lane that already holds it
+__device__ __forceinline__ int mo_claim(unsigned long long *cl, unsigned long long addr, int lane, int &ci) {
     const unsigned long long packed = (addr << 16) | (unsigned)lane;
     unsigned h = mo_claim_home(addr);
     for (int k = 0; k < MO_CLAIM; k++) {
-        const unsigned long long o = atomicCAS(&S.claim[h], 0ull, packed);
+        const unsigned long long o = atomicCAS(&cl[h], 0ull, packed);
         if (o == 0) { ci = (int)h; return -1; }
         if ((o >> 16) == addr) return (int)(o & 0xffff);
         h = (h + 1) & (MO_CLAIM - 1);
     }
     return -2;
 }
-// the lane holding slot `addr` in this chunk, -1 if none
-__device__ __forceinline__ int mo_holder(MoShared &S, unsigned long long addr) {
+// the lane holding slot `addr` in claim set cl, -1 if none
+__device__ __forceinline__ int mo_holder(const unsigned long long *cl, unsigned long long addr) {
     unsigned h = mo_claim_home(addr);
     for (int k = 0; k < MO_CLAIM; k++) {
-        const unsigned long long o = __hip_atomic_load(&S.claim[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const unsigned long long o = __hip_atomic_load(&cl[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (o == 0) return -1;
         if ((o >> 16) == addr) return (int)(o & 0xffff);
         h = (h + 1) & (MO_CLAIM - 1);
     }
     return -1;
+}
+// LDS-only workgroup barrier: orders the workgroup's LDS accesses without draining the waves' outstanding global
+// stores (__syncthreads also waits for every store of the wave to complete)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 // a merge input record, normalised: SortedRec (table mode / stage merge), GrowRec (growth), EventRec (direct path)
 struct MRec {
@@ -1155,24 +1162,34 @@ __device__ __forceinline__ void put_row(const RowsOut &o, int64_t t, uint64_t ce
                                         unsigned long long count, unsigned long long nspeed, double sspeed, double slat,
                                         double slon) {
     const bool null_sp = nspeed == 0;
+    // x / 1.0 == x: a key's first row (count 1) skips the fp64 divisions
+    const double asp = null_sp ? 0.0 : nspeed == 1 ? sspeed : sspeed / (double)nspeed;
+    const double alon = count == 1 ? slon : slon / (double)count, alat = count == 1 ? slat : slat / (double)count;
     if constexpr ((HM_NT_STORES & 2) != 0) {
         __builtin_nontemporal_store(cell, &o.cell[t]);
         __builtin_nontemporal_store(wdec(we), &o.ws[t]);
         __builtin_nontemporal_store((int64_t)count, &o.cnt[t]);
-        __builtin_nontemporal_store(null_sp ? 0.0 : sspeed / (double)nspeed, &o.sp[t]);
+        __builtin_nontemporal_store(asp, &o.sp[t]);
         __builtin_nontemporal_store((uint8_t)null_sp, &o.spnull[t]);
-        __builtin_nontemporal_store(slon / (double)count, &o.lon[t]);
-        __builtin_nontemporal_store(slat / (double)count, &o.lat[t]);
+        __builtin_nontemporal_store(alon, &o.lon[t]);
+        __builtin_nontemporal_store(alat, &o.lat[t]);
     } else {
         o.cell[t] = cell;
         o.ws[t] = wdec(we);
         o.cnt[t] = (int64_t)count;
-        o.sp[t] = null_sp ? 0.0 : sspeed / (double)nspeed;
+        o.sp[t] = asp;
         o.spnull[t] = null_sp;
-        o.lon[t] = slon / (double)count;
-        o.lat[t] = slat / (double)count;
+        o.lon[t] = alon;
+        o.lat[t] = alat;
     }
 }
+
+// a state line's new values (cell and window word are the key's)
+struct MLine {
+    unsigned long long count, nspeed;
+    double sspeed, slat, slon;
+    unsigned long long touched;
+};
 
 // Rec = SortedRec: a batch's partials (partitioned); EventRec: the direct path's rows; GrowRec: growth (rehash)
 template <typename Rec>
@@ -1225,14 +1242,147 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             }
             S.n_res = nr;
         }
-        __syncthreads();
+        lds_barrier();
         const int nres = S.n_res;
-        for (int r = 0; r < nres; r++) {
-            const unsigned *src = (const unsigned *)S.res_gtags[r];
-            const unsigned w0 = S.res_off[r] >> 2, nw = (S.res_mask[r] + 1) >> 2;
-            for (unsigned q = t; q < nw; q += MO_THREADS) mo_tags[w0 + q] = src[q];
+        // the resident regions' tags (16-B words, regions >= 256 slots): every load of a thread in flight together
+        {
+            unsigned tot = 0;
+            for (int r = 0; r < nres; r++) tot += (S.res_mask[r] + 1) >> 4;
+            typedef __attribute__((address_space(1))) const hm_v4u gv4u;   // global loads (the pointers sit in LDS)
+            for (unsigned q0 = t; q0 < tot; q0 += 4 * MO_THREADS) {
+                uint4 v0, v1, v2, v3;
+                unsigned a0 = ~0u, a1 = ~0u, a2 = ~0u, a3 = ~0u;
+                auto fetch = [&](unsigned q, uint4 &v, unsigned &a) __attribute__((always_inline)) {
+                    if (q >= tot) return;
+                    unsigned w = q;
+                    int r = 0;
+                    while (w >= ((S.res_mask[r] + 1) >> 4)) { w -= (S.res_mask[r] + 1) >> 4; r++; }
+                    const hm_v4u x = ((gv4u *)S.res_gtags[r])[w];
+                    v = make_uint4(x.x, x.y, x.z, x.w);
+                    a = (S.res_off[r] >> 4) + w;
+                };
+                fetch(q0, v0, a0);
+                fetch(q0 + MO_THREADS, v1, a1);
+                fetch(q0 + 2 * MO_THREADS, v2, a2);
+                fetch(q0 + 3 * MO_THREADS, v3, a3);
+                if (a0 != ~0u) ((uint4 *)mo_tags)[a0] = v0;
+                if (a1 != ~0u) ((uint4 *)mo_tags)[a1] = v1;
+                if (a2 != ~0u) ((uint4 *)mo_tags)[a2] = v2;
+                if (a3 != ~0u) ((uint4 *)mo_tags)[a3] = v3;
+            }
         }
-        __syncthreads();
+        lds_barrier();
+        // find (and claim) the slot of lane t's key p, or join the lane of this chunk that holds it
+        auto probe = [&](const MRec &p, TileSlot *&gslot, bool &created, int &r, int &ci) __attribute__((always_inline)) {
+            unsigned long long *cl = S.claim;
+            const unsigned long long we = p.we;
+            const uint64_t hk = p.hk;
+            const unsigned tg = tag8(hk);
+            bool done = false;
+            r = -1;
+            for (int q = 0; q < nres; q++)
+                if (S.res_we[q] == we) r = q;
+            if (r >= 0) {
+                const unsigned rmask = S.res_mask[r], off = S.res_off[r];
+                TileSlot *const base = S.res_slots[r];
+                unsigned s = (unsigned)hk & rmask;
+                for (unsigned pr = 0; pr <= rmask && !done; pr++) {
+                    TileSlot *const sl = base + s;
+                    const unsigned long long addr = (unsigned long long)sl;
+                    const unsigned bi = off + s, sh = (bi & 3) * 8;
+                    const unsigned b = (__hip_atomic_load(&mo_tags[bi >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> sh) & 0xffu;
+                    if (b == 0 || b == tg) {
+                        int x = b == 0 ? -1 : mo_holder(cl, addr);
+                        bool old_match = false;
+                        if (b == tg && x < 0) old_match = ld_l2(&sl->cell) == p.cell && ld_l2(&sl->wenc) == we;
+                        if (b == 0 || old_match) {
+                            x = mo_claim(cl, addr, t, ci);
+                            if (x == -1) {
+                                gslot = sl;
+                                created = b == 0;
+                                if (created) {
+                                    atomicOr(&mo_tags[bi >> 2], tg << sh);
+                                    S.res_dirty[r] = 1;
+                                }
+                                done = true;
+                            }
+                        }
+                        if (!done && x >= 0 && S.sc[x] == p.cell && S.sh[x] == hk) {   // same key, this chunk
+                            mo_add_into(S, x, p);
+                            done = true;
+                        }
+                    }
+                    s = (s + 1) & rmask;
+                }
+            } else {
+                const GenDesc *g = gen_lookup(C, gm, we);
+                if (g) {
+                    TileSlot *const tab = g->tab;
+                    const unsigned long long rmask = g->rmask;
+                    unsigned long long sidx = home_slot(*g, hk);
+                    for (unsigned long long pr = 0; pr <= rmask && !done; pr++) {
+                        TileSlot *const sl = &tab[sidx];
+                        const unsigned long long addr = (unsigned long long)sl;
+                        const bool free_here = ld_l2(&sl->wenc) != we;   // never used, or another window's key
+                        if (free_here || ld_l2(&sl->cell) == p.cell) {
+                            const int x = mo_claim(cl, addr, t, ci);
+                            if (x == -1) {
+                                gslot = sl;
+                                created = free_here;
+                                if (created) gen_tags(*g)[sidx] = (uint8_t)tag8(hk);
+                                done = true;
+                            } else if (S.sc[x] == p.cell && S.sh[x] == hk) {
+                                mo_add_into(S, x, p);
+                                done = true;
+                            }
+                        }
+                        sidx = next_slot(sidx, rmask);
+                    }
+                }
+            }
+            if (!done) overflow = true;
+        };
+        // the new state line of a claimed slot (old values read here: the slot's last store is visible) and its
+        // update-mode row index
+        // the slot's current line (all loads of a lane issued together; created slots read nothing)
+        auto old_line = [&](TileSlot *gslot, bool created) __attribute__((always_inline)) -> MLine {
+            MLine o{};
+            if (gslot && !created) {
+                o.touched = ld_l2(&gslot->touched);
+                o.count = ld_l2(&gslot->count);
+                o.nspeed = ld_l2(&gslot->nspeed);
+                o.sspeed = ld_l2(&gslot->sspeed);
+                o.slat = ld_l2(&gslot->slat);
+                o.slon = ld_l2(&gslot->slon);
+            }
+            return o;
+        };
+        auto line_of = [&](const MRec &p, const MLine &o, bool first, unsigned krow) __attribute__((always_inline)) -> MLine {
+            MLine v;
+            const unsigned long long acnt = S.scnt[t], ansp = S.snsp[t];
+            v.count = o.count + acnt;
+            v.nspeed = o.nspeed + ansp;
+            v.sspeed = ansp ? o.sspeed + S.sssp[t] : o.sspeed;
+            v.slat = o.slat + S.sslat[t];
+            v.slon = o.slon + S.sslon[t];
+            if constexpr (rehash) v.touched = p.touched;
+            else v.touched = first ? ((unsigned long long)seq << 32) | krow : o.touched;
+            return v;
+        };
+        // row index of a key's first touch in this batch: one LDS add per wave
+        auto touch_rows = [&](bool first) __attribute__((always_inline)) -> unsigned {
+            const unsigned long long fb = __ballot(first);
+            unsigned tbase = 0;
+            if (lane_id() == 0 && fb) tbase = atomicAdd(&S.n_touched, (unsigned)__popcll(fb));
+            tbase = __shfl(tbase, 0, 64);
+            return tbase + (unsigned)__popcll(fb & ((1ull << lane_id()) - 1));
+        };
+        auto count_created = [&](bool created, int r) __attribute__((always_inline)) {
+            for (int q = 0; q < nres; q++) {
+                const unsigned long long m = __ballot(created && r == q);
+                if (m && lane_id() == 0) atomicAdd(&S.res_new[q], (unsigned)__popcll(m));
+            }
+        };
         // software pipeline: the next chunk's record is loaded while this chunk is merged
         Rec nxt;
         if (b0 + t < b1) nxt = ld_stream(parts + b0 + t);
@@ -1243,166 +1393,69 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             MRec p{};
             if (has) p = mrec_of(nxt, winfo, cell_hi);
             if (i + MO_THREADS < b1) nxt = ld_stream(parts + i + MO_THREADS);
-            const unsigned long long we = p.we;
-            const uint64_t hk = p.hk;
             if (has) {
                 S.sc[t] = p.cell;
-                S.sh[t] = hk;
-                S.sw[t] = we;
+                S.sh[t] = p.hk;
+                S.sw[t] = p.we;
                 S.scnt[t] = p.cnt;
                 S.snsp[t] = p.nsp;
                 S.sssp[t] = p.ssp;
                 S.sslat[t] = p.slat;
                 S.sslon[t] = p.slon;
             }
-            __syncthreads();
+            lds_barrier();
             // 2. find and claim the key's slot, or join the lane that holds it
             TileSlot *gslot = nullptr;
             bool created = false;
             int r = -1, ci = -1;
-            const unsigned tg = tag8(hk);
-            if (has) {
-                bool done = false;
-                for (int q = 0; q < nres; q++)
-                    if (S.res_we[q] == we) r = q;
-                if (r >= 0) {
-                    const unsigned rmask = S.res_mask[r], off = S.res_off[r];
-                    TileSlot *const base = S.res_slots[r];
-                    unsigned s = (unsigned)hk & rmask;
-                    for (unsigned probe = 0; probe <= rmask && !done; probe++) {
-                        TileSlot *const sl = base + s;
-                        const unsigned long long addr = (unsigned long long)sl;
-                        const unsigned bi = off + s, sh = (bi & 3) * 8;
-                        const unsigned b = (__hip_atomic_load(&mo_tags[bi >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> sh) & 0xffu;
-                        if (b == 0 || b == tg) {
-                            int x = b == 0 ? -1 : mo_holder(S, addr);
-                            bool old_match = false;
-                            if (b == tg && x < 0) old_match = ld_l2(&sl->cell) == p.cell && ld_l2(&sl->wenc) == we;
-                            if (b == 0 || old_match) {
-                                x = mo_claim(S, addr, t, ci);
-                                if (x == -1) {
-                                    gslot = sl;
-                                    created = b == 0;
-                                    if (created) {
-                                        atomicOr(&mo_tags[bi >> 2], tg << sh);
-                                        S.res_dirty[r] = 1;
-                                    }
-                                    done = true;
-                                }
-                            }
-                            if (!done && x >= 0 && S.sc[x] == p.cell && S.sh[x] == hk) {   // same key, this chunk
-                                mo_add_into(S, x, p);
-                                done = true;
-                            }
-                        }
-                        s = (s + 1) & rmask;
-                    }
-                } else {
-                    const GenDesc *g = gen_lookup(C, gm, we);
-                    if (g) {
-                        TileSlot *const tab = g->tab;
-                        const unsigned long long rmask = g->rmask;
-                        unsigned long long sidx = home_slot(*g, hk);
-                        for (unsigned long long probe = 0; probe <= rmask && !done; probe++) {
-                            TileSlot *const sl = &tab[sidx];
-                            const unsigned long long addr = (unsigned long long)sl;
-                            const bool free_here = ld_l2(&sl->wenc) != we;   // never used, or another window's key
-                            if (free_here || ld_l2(&sl->cell) == p.cell) {
-                                const int x = mo_claim(S, addr, t, ci);
-                                if (x == -1) {
-                                    gslot = sl;
-                                    created = free_here;
-                                    if (created) gen_tags(*g)[sidx] = (uint8_t)tg;
-                                    done = true;
-                                } else if (S.sc[x] == p.cell && S.sh[x] == hk) {
-                                    mo_add_into(S, x, p);
-                                    done = true;
-                                }
-                            }
-                            sidx = next_slot(sidx, rmask);
-                        }
-                    }
-                }
-                if (!done) overflow = true;
-            }
-            // keys created in the resident regions, one LDS add per region and wave
-            for (int q = 0; q < nres; q++) {
-                const unsigned long long m = __ballot(created && r == q);
-                if (m && lane_id() == 0) atomicAdd(&S.res_new[q], (unsigned)__popcll(m));
-            }
-            __syncthreads();
-            // 3. apply (this workgroup is the only writer of these regions) and write the key's output row
-            unsigned long long ocnt = 0, onsp = 0, tc = 0;
-            double ossp = 0.0, oslat = 0.0, oslon = 0.0;
-            if (gslot && !created) {
-                tc = ld_l2(&gslot->touched);
-                ocnt = ld_l2(&gslot->count);
-                onsp = ld_l2(&gslot->nspeed);
-                ossp = ld_l2(&gslot->sspeed);
-                oslat = ld_l2(&gslot->slat);
-                oslon = ld_l2(&gslot->slon);
-            }
-            const bool retouch = !rehash && gslot && !created && (unsigned)(tc >> 32) == seq;
+            if (has) probe(p, gslot, created, r, ci);
+            count_created(created, r);
+            lds_barrier();
+            // 3. the claimers' new lines (their slots' last stores were drained by an earlier chunk's barrier)
+            MLine v{};
+            const MLine o = old_line(gslot, created);
+            const bool retouch = !rehash && gslot && !created && (unsigned)(o.touched >> 32) == seq;
             const bool first = !rehash && gslot && !retouch;
-            const unsigned long long fb = __ballot(first);
-            unsigned tbase = 0;
-            if (lane_id() == 0 && fb) tbase = atomicAdd(&S.n_touched, (unsigned)__popcll(fb));
-            tbase = __shfl(tbase, 0, 64);
-            const unsigned krow = first ? tbase + (unsigned)__popcll(fb & ((1ull << lane_id()) - 1)) : (unsigned)tc;
+            unsigned krow = touch_rows(first);
+            if (!first) krow = (unsigned)o.touched;
+            if (gslot) v = line_of(p, o, first, krow);
+            // 4. this chunk's stores: the state line (whole) and the key's row
             if (gslot) {
-                const unsigned long long acnt = S.scnt[t], ansp = S.snsp[t];
-                TileSlot v;
-                v.cell = p.cell;
-                v.wenc = we;
-                v.count = ocnt + acnt;
-                v.nspeed = onsp + ansp;
-                v.sspeed = ansp ? ossp + S.sssp[t] : ossp;
-                v.slat = oslat + S.sslat[t];
-                v.slon = oslon + S.sslon[t];
-                if constexpr (rehash) v.touched = p.touched;
-                else v.touched = ((unsigned long long)seq << 32) | krow;
-#ifdef HM_ABL_NOSLOT   // ablation builds only: the state line stores priced by their absence
-                if (created) { created_cnt++; } else if (false) {
-#else
-                if (created) {
-                    *gslot = v;
-                    created_cnt++;
-                } else {
+#ifndef HM_ABL_NOSLOT   // ablation builds only: the state line stores priced by their absence
+                uint4 *d = (uint4 *)gslot;   // the whole 64-B line
+                d[0] = make_uint4((unsigned)p.cell, (unsigned)(p.cell >> 32), (unsigned)p.we, (unsigned)(p.we >> 32));
+                d[1] = make_uint4((unsigned)v.count, (unsigned)(v.count >> 32), (unsigned)v.nspeed, (unsigned)(v.nspeed >> 32));
+                const uint64_t b0s = __builtin_bit_cast(uint64_t, v.sspeed), b1s = __builtin_bit_cast(uint64_t, v.slat);
+                const uint64_t b2s = __builtin_bit_cast(uint64_t, v.slon);
+                d[2] = make_uint4((unsigned)b0s, (unsigned)(b0s >> 32), (unsigned)b1s, (unsigned)(b1s >> 32));
+                d[3] = make_uint4((unsigned)b2s, (unsigned)(b2s >> 32), (unsigned)v.touched, (unsigned)(v.touched >> 32));
 #endif
-                    gslot->count = v.count;
-                    if (ansp) {
-                        gslot->nspeed = v.nspeed;
-                        gslot->sspeed = v.sspeed;
-                    }
-                    gslot->slat = v.slat;
-                    gslot->slon = v.slon;
-                    if (first) gslot->touched = v.touched;
-                }
+                if (created) created_cnt++;
 #ifndef HM_ABL_NOROWS
-                if (!rehash) put_row(rows, b0 + krow, p.cell, we, v.count, v.nspeed, v.sspeed, v.slat, v.slon);
+                if (!rehash) put_row(rows, b0 + krow, p.cell, p.we, v.count, v.nspeed, v.sspeed, v.slat, v.slon);
 #endif
             }
             // created keys of non-resident windows count for their window here (resident ones: res_new); rehash:
             // the host already carries the moved keys
             const bool count_here = created && !rehash && r < 0;
-            if (__ballot(count_here) && !wave_count_windows(count_here, we, 1ull, WL, sink)) overflow = true;
-            // 4. make this chunk's stores visible to the next chunk's probes; release the claims
-#ifndef HM_ABL_NOFENCE
-            __threadfence_block();
-#endif
-            if (ci >= 0) S.claim[ci] = 0;
+            if (__ballot(count_here) && !wave_count_windows(count_here, p.we, 1ull, WL, sink)) overflow = true;
+            // 5. drain this chunk's stores (visible to the next chunk's probes: a full barrier waits for every store of
+            // the wave -- measured: draining them a chunk later instead, deferring the keys the previous chunk wrote,
+            // cost 1.5 ms on the bench and 4.5 ms on the state-read leg); release the claims
             __syncthreads();
+            if (ci >= 0) S.claim[ci] = 0;
         }
-        // 5. write the resident regions' tags back
+        lds_barrier();
+        // 6. write the resident regions' tags back
         if (t < nres && S.res_new[t] && !gmap_add(gm, S.res_we[t], S.res_new[t])) overflow = true;
         for (int r = 0; r < nres; r++) {
             if (!S.res_dirty[r]) continue;
-            unsigned *dst = (unsigned *)S.res_gtags[r];
-            const unsigned w0 = S.res_off[r] >> 2, nw = (S.res_mask[r] + 1) >> 2;
-            for (unsigned q = t; q < nw; q += MO_THREADS) dst[q] = mo_tags[w0 + q];
+            uint4 *dst = (uint4 *)S.res_gtags[r];
+            const unsigned w0 = S.res_off[r] >> 4, nw = (S.res_mask[r] + 1) >> 4;
+            for (unsigned q = t; q < nw; q += MO_THREADS) dst[q] = ((const uint4 *)mo_tags)[w0 + q];
         }
         if (t == 0) { bin_cnt[bin] = S.n_touched; S.n_touched = 0; }
-        __syncthreads();
+        lds_barrier();
     }
     if (!wl_flush(WL, sink)) overflow = true;
     created_cnt = wave_sum(created_cnt);

@@ -377,6 +377,31 @@ def test_ingest_modes_parity(mode, monkeypatch):
     eng.close()
 
 
+def test_direct_merge_keys_repeated_across_chunks(monkeypatch):
+    """k_merge_owned with every key in several consecutive 512-record chunks of its bin (direct path forced: 1.2e7 rows
+    over ~5e5 res-11 keys, ~1.5k rows per bin): a chunk's stores are only drained by the next chunk's full barrier, so
+    a key the previous chunk wrote is deferred behind it (mobheat.hip: k_merge_owned step 4) -- counts and sums must
+    still add up exactly; a second batch in the same window re-reads every key's state."""
+    from mobheat import HeatmapEngine, synth
+    from oracle.spark_oracle import SparkHeatmapOracle
+    monkeypatch.setenv("MOBHEAT_INGEST_MODE", "direct")
+    rng = np.random.default_rng(77)
+    eng = HeatmapEngine(h3_res=11)
+    ora = SparkHeatmapOracle(h3_res=11)
+    minute = 60_000_000
+    for epoch in range(2):
+        n = 12_000_000
+        b = dict(lat=37.9 + rng.uniform(0, 0.3, n), lon=23.6 + rng.uniform(0, 0.3, n),
+                 ts_us=synth.T0 + epoch * minute + rng.integers(0, minute, n), speed=rng.uniform(0, 90, n),
+                 speed_valid=rng.random(n) > 0.1, vkey=rng.integers(0, 5000, n).astype(np.uint64), row_valid=None)
+        res, exp = _run(eng, ora, b, epoch)
+        assert not eng.last_counts()["table_mode"]
+        assert_batch_equal(res, exp)
+        if epoch == 0:
+            assert int(res.tiles.count.sum()) == n
+    eng.close()
+
+
 @pytest.mark.parametrize("arena_mb", [1, 48])
 def test_state_arena_tables(arena_mb):
     """Window tables carved from a create-time arena (state_arena_bytes): a small arena runs out mid-stream and
