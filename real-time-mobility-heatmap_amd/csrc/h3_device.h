@@ -526,6 +526,31 @@ HM_HD void sincos_small(double x, double &s, double &c) {
 
 HM_HD double dmin(double a, double b) { return a < b ? a : b; }
 
+// The generated res-0 tables as compile-time constants (the fast path's closest-face prefilter takes its 60
+// coordinates as instruction literals instead of scalar registers: the kernels' SGPR budget spilled them into
+// VGPR lanes, ~120 v_readlane per round of k_ingest).
+namespace tab {
+#define H3T_CONST constexpr
+#include "h3_tables.inc"
+#undef H3T_CONST
+}  // namespace tab
+
+// closest-face prefilter, branch-free: the best and second-best fp32 dot product over faces F..19 (first face
+// wins ties, as upstream's strict `<`): the same (best, second, face) as the branchy scan
+// `if (d > best) {second = best; best = d; face = f;} else if (d > second) second = d;`
+template <int F>
+HM_HD void closestFaceF32(float fx, float fy, float fz, float &best, float &second, int &face) {
+    constexpr float cx = (float)tab::H3T_faceCenterPoint[F][0];
+    constexpr float cy = (float)tab::H3T_faceCenterPoint[F][1];
+    constexpr float cz = (float)tab::H3T_faceCenterPoint[F][2];
+    const float d = cx * fx + cy * fy + cz * fz;
+    const float lo = best < d ? best : d;
+    second = second < lo ? lo : second;
+    face = d > best ? F : face;
+    best = d > best ? d : best;
+    if constexpr (F + 1 < 20) closestFaceF32<F + 1>(fx, fy, fz, best, second, face);
+}
+
 // The fast path.  Returns false when the caller must use latLngToCellDeg; otherwise `out` is upstream's cell
 // (0 where the reference's UDF returns None).  fc = T.faceCenterPoint, fu = T.fastU[res & 1], or copies of them
 // (k_ingest keeps them in LDS: lane-indexed reads there do not queue behind its outstanding global loads).
@@ -540,13 +565,8 @@ HM_HD bool latLngToCellFastP(double lat_deg, double lng_deg, int res, const H3Ta
     // closest face: fp32 dot products (within ~1e-6 of upstream's fp64 argmin); a lead below 1e-5 -> exact path
     int face = 0;
     {
-        const float fx = (float)px, fy = (float)py, fz = (float)pz;
         float best = -4.0f, second = -4.0f;
-        for (int f = 0; f < 20; ++f) {
-            const float d = T.faceCenterPointF[f][0] * fx + T.faceCenterPointF[f][1] * fy + T.faceCenterPointF[f][2] * fz;
-            if (d > best) { second = best; best = d; face = f; }
-            else if (d > second) second = d;
-        }
+        closestFaceF32<0>((float)px, (float)py, (float)pz, best, second, face);
         if (!(best - second > 1e-5f)) return false;
     }
     const double *c = fc[face];

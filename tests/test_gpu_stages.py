@@ -90,7 +90,7 @@ def _stage_batch(engines, lib, batches_per_rank, epoch):
         latest.append(got.copy())
     for b in bufs:
         b.free()
-    return outs, latest
+    return outs, latest, tcounts, ccounts
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -108,7 +108,7 @@ def test_stage_api_matches_single_shard(world):
         b["ts_us"] = synth.T0 + start * 60_000_000 + rng.integers(0, 9 * 60_000_000, n)
         bounds = [i * n // world for i in range(world + 1)]
         shards = [{k: v[bounds[r]:bounds[r + 1]] for k, v in b.items()} for r in range(world)]
-        outs, latest = _stage_batch(engines, lib, shards, epoch)
+        outs, latest, _, _ = _stage_batch(engines, lib, shards, epoch)
         exp = ora.process_batch(**b)
         got = {}
         for t in outs:
@@ -121,5 +121,94 @@ def test_stage_api_matches_single_shard(world):
         assert all(got[k][0] == o[k][0] and abs(got[k][1] - o[k][1]) <= 1e-9 * abs(o[k][1]) for k in got)
         rows = np.sort(np.concatenate([latest[r] + bounds[r] for r in range(world)]))
         np.testing.assert_array_equal(rows, exp["latest_rows"])
+    for e in engines:
+        e.close()
+
+
+def _check_union(outs, latest, bounds, exp):
+    got = {}
+    for t in outs:
+        for k in range(len(t)):
+            key = (int(t.cell[k]), int(t.window_start_us[k]))
+            assert key not in got, "a key emitted by two owners"
+            got[key] = (int(t.count[k]), float(t.avg_lat[k]), float(t.avg_lon[k]))
+    o = {(x["cell"], x["window_start_us"]): (x["count"], x["avg_lat"], x["avg_lon"]) for x in exp["tiles"]}
+    assert set(got) == set(o)
+    for k, g in got.items():
+        assert g[0] == o[k][0]
+        assert abs(g[1] - o[k][1]) <= 1e-9 * abs(o[k][1]) and abs(g[2] - o[k][2]) <= 1e-9 * abs(o[k][2])
+    rows = np.sort(np.concatenate([latest[r] + bounds[r] for r in range(len(latest))]))
+    np.testing.assert_array_equal(rows, exp["latest_rows"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_stage_api_table_mode_c3(world, monkeypatch, capsys):
+    """C3-shaped shards (Zipf hot spots, res 9) with the table-mode aggregation pinned: every rank sends exactly
+    one 48-B partial per distinct (cell, window) key of its shard (what the exchange carries instead of rows), and
+    the owners' union equals the single-shard oracle over two advancing batches.  Per-rank send counts and bytes
+    are printed (C3's exchange scales with its keys, not with its 1e9 rows)."""
+    monkeypatch.setenv("MOBHEAT_INGEST_MODE", "table")
+    import mobheat
+    from mobheat import synth
+    from mobheat._lib import HM_CAND_REC_BYTES, HM_TILE_REC_BYTES
+    from oracle.spark_oracle import SparkHeatmapOracle
+    lib = mobheat.load()
+    engines = [mobheat.HeatmapEngine(h3_res=9) for _ in range(world)]
+    ora = SparkHeatmapOracle(h3_res=9)
+    n = 400_000
+    log = []
+    for epoch in range(2):
+        b = synth.c3_city(seed=20 + epoch, n=n, hotspots=300, n_vehicles=5000)
+        b["ts_us"] = b["ts_us"] + epoch * 6 * 60_000_000
+        bounds = [i * n // world for i in range(world + 1)]
+        shards = [{k: v[bounds[r]:bounds[r + 1]] for k, v in b.items()} for r in range(world)]
+        outs, latest, tc, cc = _stage_batch(engines, lib, shards, epoch)
+        exp = ora.process_batch(**b)
+        _check_union(outs, latest, bounds, exp)
+        for r in range(world):
+            keys_r = len(SparkHeatmapOracle(h3_res=9).process_batch(**shards[r])["tiles"])
+            # one record per key (a key spills a second one only when an LDS probe or a bucket overflows: rare)
+            assert keys_r <= sum(tc[r]) <= keys_r * 1.02 + 16, (r, sum(tc[r]), keys_r)
+            tb, cb = sum(tc[r]) * HM_TILE_REC_BYTES, sum(cc[r]) * HM_CAND_REC_BYTES
+            log.append((epoch, r, shards[r]["lat"].size, sum(tc[r]), tb, sum(cc[r]), cb))
+            # a rank's tile exchange is bounded by its distinct keys, not by its rows (here ~30 rows per key)
+            assert sum(tc[r]) * 8 <= shards[r]["lat"].size
+    with capsys.disabled():
+        for e, r, rows, nt, tb, nc, cb in log:
+            print(f"\n[c3 table, world {world}] batch {e} rank {r}: {rows} rows -> {nt} tile partials ({tb} B), "
+                  f"{nc} latest candidates ({cb} B); tile bytes per 1e6 rows {tb * 1e6 / rows:.0f}")
+    for e in engines:
+        e.close()
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_stage_api_c5_vehicles_straddle_ranks(world, capsys):
+    """C5-shaped batch: every vehicle's updates are permuted across all ranks and 5% of the vehicles have two rows
+    tied at their max timestamp.  The owner of a vehicle must keep exactly the rows at the global max (both tied
+    rows, whichever ranks they came from) and route them back to their origin ranks; tiles equal the oracle too."""
+    import mobheat
+    from mobheat import synth
+    from mobheat._lib import HM_CAND_REC_BYTES
+    from oracle.spark_oracle import SparkHeatmapOracle
+    lib = mobheat.load()
+    engines = [mobheat.HeatmapEngine(h3_res=9) for _ in range(world)]
+    b = synth.c5_dedup(seed=40 + world, n_vehicles=30_000, updates=12, tie_frac=0.05)
+    n = b["lat"].size
+    bounds = [i * n // world for i in range(world + 1)]
+    shards = [{k: v[bounds[r]:bounds[r + 1]] for k, v in b.items()} for r in range(world)]
+    # every vehicle straddles the ranks (12 updates over `world` shards)
+    owners_per_vehicle = np.zeros(30_000, np.int64)
+    for r in range(world):
+        owners_per_vehicle += np.bincount(shards[r]["vkey"].astype(np.int64), minlength=30_000) > 0
+    assert (owners_per_vehicle >= 2).mean() > 0.99
+    outs, latest, tc, cc = _stage_batch(engines, lib, shards, 0)
+    exp = SparkHeatmapOracle(h3_res=9).process_batch(**b)
+    _check_union(outs, latest, bounds, exp)
+    n_ties = len(exp["latest_rows"]) - 30_000
+    assert n_ties > 1000   # both tied rows of ~5% of the vehicles are kept
+    with capsys.disabled():
+        for r in range(world):
+            print(f"\n[c5, world {world}] rank {r}: {bounds[r + 1] - bounds[r]} rows -> {sum(cc[r])} latest candidates "
+                  f"({sum(cc[r]) * HM_CAND_REC_BYTES} B) to {world} owners {cc[r]}; tile partials {sum(tc[r])}")
     for e in engines:
         e.close()
