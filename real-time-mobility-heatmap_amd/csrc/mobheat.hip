@@ -696,7 +696,12 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_scatter(const uint64_t *__res
 //                writes one partial record per key -> the usual partition + merge.
 // =====================================================================================================
 constexpr int AG_THREADS = 1024;
-constexpr int AG_SLOTS = 3840;                  // 40 B each: 150 KB of LDS, one workgroup per CU
+#ifndef HM_AG_LINEAR
+// 40 B each: 150 KB of LDS, one workgroup per CU.  A prime, so that every double-hashing step visits every slot.
+constexpr int AG_SLOTS = 3833;
+#else
+constexpr int AG_SLOTS = 3840;
+#endif
 constexpr int AG_PER = AG_SLOTS / AG_THREADS + (AG_SLOTS % AG_THREADS != 0);
 constexpr int AG_FLUSH_AT = AG_SLOTS - AG_THREADS;   // a round adds at most AG_THREADS keys
 constexpr int AG_KEEP_MAX = AG_SLOTS / 3;       // aggregates kept resident by a flush
@@ -717,6 +722,17 @@ struct AgTable {
     unsigned long long obase;
 };
 __device__ __forceinline__ unsigned ag_home(uint64_t k) { return (unsigned)(((mix64(k) >> 32) * (uint64_t)AG_SLOTS) >> 32); }
+// Probe sequence: double hashing (step in [1, AG_SLOTS - 1] from other hash bits).  Every round of k_agg ends at a
+// workgroup barrier, so a round lasts as long as its longest probe chain; linear probing's clusters at the table's
+// 70-80% fill before a flush made those chains run to the 64-probe bound (each probe a dependent LDS load).
+__device__ __forceinline__ unsigned ag_step(uint64_t k) {
+#ifndef HM_AG_LINEAR
+    return 1u + (unsigned)(((mix64(k) & 0xffffffffu) * (uint64_t)(AG_SLOTS - 1)) >> 32);
+#else
+    (void)k;
+    return 1u;
+#endif
+}
 __device__ __forceinline__ unsigned ag_bin(uint64_t k) { return (unsigned)mix64(k ^ UINT64_C(0x94d049bb133111eb)) & (AG_BINS - 1); }
 __device__ __forceinline__ unsigned xcc_id() {
     unsigned v;
@@ -737,6 +753,7 @@ __device__ __forceinline__ void ag_clear(AgTable &T) {
 __device__ __forceinline__ bool ag_add(AgTable &T, uint64_t k, unsigned long long c, double ssp, double sla, double slo,
                                        bool &fresh) {
     unsigned h = ag_home(k);
+    const unsigned step = ag_step(k);
     fresh = false;
     for (int p = 0; p < AG_PROBES; p++) {
         unsigned long long cur = __hip_atomic_load(&T.key[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -751,7 +768,8 @@ __device__ __forceinline__ bool ag_add(AgTable &T, uint64_t k, unsigned long lon
             atomicAdd(&T.slon[h], slo);
             return true;
         }
-        h = h + 1 == (unsigned)AG_SLOTS ? 0u : h + 1;
+        h += step;
+        h = h >= (unsigned)AG_SLOTS ? h - (unsigned)AG_SLOTS : h;
     }
     return false;
 }
