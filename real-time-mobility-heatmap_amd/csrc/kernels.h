@@ -102,6 +102,15 @@ struct alignas(32) WInfo {
     unsigned pad[3];
 };
 static_assert(sizeof(WInfo) == 32, "WInfo is 32 B");
+// A direct-mapped image of the batch's WInfo entries (slot & (WI_CACHE - 1)), built by the host next to the per-slot
+// array; the partition and merge kernels copy it into LDS, so that a record's window parameters are an LDS read
+// instead of a dependent global load (slots that collide in the image keep the global lookup).
+constexpr int WI_CACHE = 64;
+constexpr unsigned WI_NONE = 0xffffffffu, WI_CONFLICT = 0xfffffffeu;   // (never a registry slot)
+struct WiCacheImg {
+    unsigned tag[WI_CACHE];   // the registry slot held by the entry, or WI_NONE / WI_CONFLICT
+    WInfo e[WI_CACHE];
+};
 
 // table mode (low cardinality): an aggregate evicted from k_agg's LDS table, bucketed by key hash for k_bin_reduce
 struct alignas(16) AggRec {

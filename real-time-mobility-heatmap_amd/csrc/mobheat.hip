@@ -575,6 +575,23 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict_
 // (window, region) bins, or (multi-GPU) 48-B TilePartials grouped by owner rank.  The histogram reads only the
 // keys; the scatter reads a record's speed/lat/lon only for aggregated rows.
 // =====================================================================================================
+// LDS copy of the host's WInfo image (kernels.h WiCacheImg), stored right after the per-slot array
+struct WiCacheL {
+    unsigned tag[WI_CACHE];
+    WInfo e[WI_CACHE];
+};
+__device__ __forceinline__ void wi_load(WiCacheL &C, const WInfo *winfo) {   // (a barrier must follow)
+    const WiCacheImg *img = (const WiCacheImg *)(winfo + WREG_SLOTS + 1);
+    for (int q = threadIdx.x; q < WI_CACHE; q += blockDim.x) {
+        C.tag[q] = img->tag[q];
+        C.e[q] = img->e[q];
+    }
+}
+__device__ __forceinline__ WInfo wi_get(const WiCacheL &C, const WInfo *winfo, unsigned slot) {
+    const unsigned e = slot & (WI_CACHE - 1);
+    return C.tag[e] == slot ? C.e[e] : winfo[slot];
+}
+
 // the key's radix digit: with nranks > 0 its owner rank, else its (window, region) bin (binp: kernels.h WInfo)
 __device__ __forceinline__ unsigned ev_digit(uint64_t h, unsigned binp, int nranks) {
     if (nranks > 0) return (unsigned)owner_of(h, nranks);
@@ -587,7 +604,9 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_hist(const uint64_t *__restri
                                                        const WInfo *__restrict__ winfo, uint64_t cell_hi, int nranks, int nbins,
                                                        unsigned *__restrict__ H, int64_t ntiles) {
     __shared__ unsigned h[RP_BINS + 1];
+    __shared__ WiCacheL WI;
     for (int d = threadIdx.x; d <= nbins; d += EV_THREADS) h[d] = 0;
+    wi_load(WI, winfo);
     __syncthreads();
     const int64_t t0 = (int64_t)blockIdx.x * tile;
     const int64_t t1 = t0 + tile < n ? t0 + tile : n;
@@ -601,7 +620,7 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_hist(const uint64_t *__restri
         for (int u = 0; u < U; u++) {
             if (b + u * EV_THREADS >= t1) continue;
             if (!k[u]) { gaps++; continue; }
-            const WInfo &wi = winfo[ekey_widx(k[u])];
+            const WInfo wi = wi_get(WI, winfo, ekey_widx(k[u]));
             const uint64_t hh = mix64(((k[u] & CELL_LO) | cell_hi) ^ wi.inner);
             atomicAdd(&h[ev_digit(hh, wi.binp, nranks)], 1u);
         }
@@ -626,7 +645,9 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_scatter(const uint64_t *__res
     constexpr int QO = sizeof(Out) / 16;
     __shared__ unsigned cur[RP_BINS];   // positions < 2^32 - 1 (hm_process_batch checks n)
     __shared__ uint4 stage[(EV_THREADS / 64) * 64 * QO];
+    __shared__ WiCacheL WI;
     for (int d = threadIdx.x; d < nbins; d += EV_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
+    wi_load(WI, winfo);
     __syncthreads();
     const int64_t t0 = (int64_t)blockIdx.x * tile;
     const int64_t t1 = t0 + tile < n ? t0 + tile : n;
@@ -654,7 +675,7 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_scatter(const uint64_t *__res
         unsigned pos = ~0u;   // ~0u: no record
         if (r.k) {
             const uint64_t k = r.k;
-            const WInfo &wi = winfo[ekey_widx(k)];
+            const WInfo wi = wi_get(WI, winfo, ekey_widx(k));
             const uint64_t cell = (k & CELL_LO) | cell_hi;
             const uint64_t hh = mix64(cell ^ wi.inner);
             pos = atomicAdd(&cur[ev_digit(hh, wi.binp, nranks)], 1u);
@@ -695,6 +716,14 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_scatter(const uint64_t *__res
 //  k_bin_reduce  one workgroup per bucket aggregates its evicted entries (a bucket holds 1/256 of the keys) and
 //                writes one partial record per key -> the usual partition + merge.
 // =====================================================================================================
+// LDS-only workgroup barrier: orders the workgroup's LDS accesses without draining the waves' outstanding global
+// loads and stores (__syncthreads' fence also waits for every global access of the wave).  (k_agg keeps
+// __syncthreads: this barrier in its rounds and flushes measured neutral, profiles/r2/abc3c/)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 constexpr int AG_THREADS = 1024;
 #ifndef HM_AG_LINEAR
 // 40 B each: 150 KB of LDS, one workgroup per CU.  A prime, so that every double-hashing step visits every slot.
@@ -933,10 +962,7 @@ __global__ __launch_bounds__(AG_THREADS) void k_agg(const uint64_t *__restrict__
         }
         return r;
     };
-    Row nx = load(b0 + threadIdx.x);
-    for (int64_t c0 = b0; c0 < b1; c0 += AG_THREADS) {
-        const Row r = nx;
-        nx = load(c0 + AG_THREADS + threadIdx.x);
+    auto round_of = [&](const Row &r) __attribute__((always_inline)) {
         const uint64_t k = r.k;
         bool fresh = false;
         if (k) {
@@ -948,6 +974,12 @@ __global__ __launch_bounds__(AG_THREADS) void k_agg(const uint64_t *__restrict__
             ag_flush(T, false, bucket, cursor, cap, wreg, cell_hi, out, st, WL, census, ok);
             FC.occ = T.occ;
         }
+    };
+    Row nx = load(b0 + threadIdx.x);
+    for (int64_t c0 = b0; c0 < b1; c0 += AG_THREADS) {
+        const Row r = nx;
+        nx = load(c0 + AG_THREADS + threadIdx.x);
+        round_of(r);
     }
     ag_flush(T, true, bucket, cursor, cap, wreg, cell_hi, out, st, WL, census, ok);
     __syncthreads();
@@ -1079,7 +1111,6 @@ struct MoShared {
     // this chunk's records by lane; a duplicate key's values are added into its claimer's entry
     unsigned long long sc[MO_THREADS];
     unsigned long long sh[MO_THREADS];
-    unsigned long long sw[MO_THREADS];
     unsigned long long scnt[MO_THREADS];
     unsigned long long snsp[MO_THREADS];
     double sssp[MO_THREADS];
@@ -1127,13 +1158,6 @@ __device__ __forceinline__ int mo_holder(const unsigned long long *cl, unsigned 
     }
     return -1;
 }
-// LDS-only workgroup barrier: orders the workgroup's LDS accesses without draining the waves' outstanding global
-// stores (__syncthreads also waits for every store of the wave to complete)
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 // a merge input record, normalised: SortedRec (table mode / stage merge), GrowRec (growth), EventRec (direct path)
 struct MRec {
     uint64_t cell;
@@ -1150,7 +1174,7 @@ __device__ __forceinline__ MRec mrec_of(const GrowRec &p, const WInfo *, uint64_
     return MRec{p.cell, wenc_of(p.wstart), tile_hash(p.cell, p.wstart), p.count, p.nspeed, p.sspeed, p.slat, p.slon, p.touched};
 }
 __device__ __forceinline__ MRec mrec_of(const EventRec &p, const WInfo *winfo, uint64_t cell_hi) {
-    const WInfo &wi = winfo[ekey_widx(p.key)];
+    const WInfo &wi = winfo[ekey_widx(p.key)];   // (an LDS copy measured no faster here: the chunk loop hides it)
     const uint64_t cell = (p.key & CELL_LO) | cell_hi;
     const bool sv = __builtin_bit_cast(uint64_t, p.speed) != SPEED_NULL_BITS;
     return MRec{cell, wi.wenc, mix64(cell ^ wi.inner), 1ull, sv ? 1ull : 0ull, sv ? p.speed : 0.0, p.lat, p.lon, 0ull};
@@ -1414,7 +1438,6 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             if (has) {
                 S.sc[t] = p.cell;
                 S.sh[t] = p.hk;
-                S.sw[t] = p.we;
                 S.scnt[t] = p.cnt;
                 S.snsp[t] = p.nsp;
                 S.sssp[t] = p.ssp;
@@ -2330,6 +2353,9 @@ struct hm_ctx {
     // aggregation path: direct (event records -> partition -> merge) or table (k_agg + k_bin_reduce, low
     // cardinality); MOBHEAT_INGEST_MODE pins one (0 adaptive, 1 direct, 2 table)
     int ingest_mode = 0;
+    // k_merge_owned's grid: 0 = one workgroup per bin; else that many persistent workgroups looping over the bins
+    // (MOBHEAT_MERGE_GRID, tuning)
+    int merge_grid = 0;
     int64_t prev_agg_rows = 0, prev_keys = 0;   // aggregated rows and distinct keys of the last batch
     bool last_table = false;
     int64_t last_counts[4] = {0, 0, 0, 0};   // hm_last_counts
@@ -2577,17 +2603,20 @@ struct Inputs {   // a batch's device columns
 };
 
 // exclusive scan of the m = (nbins + 1) x ntiles tile histogram rp_H into rp_O (digit-major)
-static int rp_scan(hm_ctx *ctx, int64_t m) {
+// exclusive scan of m u32 counts `in` into u64 offsets `out`
+static int scan_counts(hm_ctx *ctx, const unsigned *in, int64_t m, unsigned long long *out) {
     const int64_t nb = (m + SC_PER - 1) / SC_PER;
     int rc;
     if ((rc = ensure(ctx, ctx->rp_btot, nb * 4)) || (rc = ensure(ctx, ctx->rp_boff, nb * 8))) return rc;
-    hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_H.p, m,
-                       (unsigned long long *)ctx->rp_O.p, (unsigned *)ctx->rp_btot.p);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(nb), dim3(1024), 0, ctx->stream, in, m, out, (unsigned *)ctx->rp_btot.p);
     hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->rp_btot.p, nb,
                        (unsigned long long *)ctx->rp_boff.p, ctx->d_scratch + 254);
-    hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, (unsigned long long *)ctx->rp_O.p, m,
+    hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, out, m,
                        (const unsigned long long *)ctx->rp_boff.p);
     return HM_OK;
+}
+static int rp_scan(hm_ctx *ctx, int64_t m) {
+    return scan_counts(ctx, (const unsigned *)ctx->rp_H.p, m, (unsigned long long *)ctx->rp_O.p);
 }
 
 // radix partition of n partial records into RP_BINS bins (one per (window, region)); the sorted copy goes to
@@ -2670,7 +2699,8 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles) {
             if (g.batch_parts) need += size_t(1) << (g.log2cap - (int)g.rbits);
         tag_bytes = (unsigned)std::min<size_t>((need + 4095) & ~size_t(4095), MO_TAG_MAX);   // (attribute: hm_create)
     }
-    hipLaunchKernelGGL(k_merge_owned<Rec>, dim3(RP_BINS), dim3(MO_THREADS), tag_bytes, ctx->stream, (const Rec *)ctx->parts_sorted.p, n_rows,
+    const int grid = ctx->merge_grid > 0 ? std::min(ctx->merge_grid, RP_BINS) : RP_BINS;
+    hipLaunchKernelGGL(k_merge_owned<Rec>, dim3(grid), dim3(MO_THREADS), tag_bytes, ctx->stream, (const Rec *)ctx->parts_sorted.p, n_rows,
                        (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
                        ctx->n_glist, (const WInfo *)ctx->d_winfo, cell_hi_of(ctx->cfg.h3_res), seq32(ctx), staged_rows(ctx),
                        (unsigned *)ctx->bin_cnt.p, ctx->d_st, tag_bytes);
@@ -2731,6 +2761,20 @@ static int winfo_upload(hm_ctx *ctx, bool with_bins) {
     if (hi >= lo)
         HIPCHK(ctx, hipMemcpyAsync(ctx->d_winfo + lo, h + lo, (size_t)(hi - lo + 1) * sizeof(WInfo), hipMemcpyHostToDevice,
                                    ctx->stream));
+    // the direct-mapped image the kernels keep in LDS (kernels.h WiCacheImg)
+    WiCacheImg *img = (WiCacheImg *)(h + WREG_SLOTS + 1);
+    for (int e = 0; e < WI_CACHE; e++) img->tag[e] = WI_NONE;
+    for (int w = lo; w <= hi; w++) {
+        if (!ctx->h_wreg[w]) continue;
+        const int e = w & (WI_CACHE - 1);
+        if (img->tag[e] == WI_NONE) {
+            img->tag[e] = (unsigned)w;
+            img->e[e] = h[w];
+        } else {
+            img->tag[e] = WI_CONFLICT;   // (both slots keep the global lookup)
+        }
+    }
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_winfo + WREG_SLOTS + 1, img, sizeof(WiCacheImg), hipMemcpyHostToDevice, ctx->stream));
     return HM_OK;
 }
 
@@ -3262,12 +3306,14 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     }
     // MOBHEAT_INGEST_MODE=direct|table pins the aggregation path (tests); default: adaptive
     if (const char *m = getenv("MOBHEAT_INGEST_MODE")) ctx->ingest_mode = !strcmp(m, "direct") ? 1 : !strcmp(m, "table") ? 2 : 0;
+    if (const char *m = getenv("MOBHEAT_MERGE_GRID")) ctx->merge_grid = std::max(0, atoi(m));
     if (hipMalloc(&ctx->d_wreg, (WREG_SLOTS + 1) * 8) != hipSuccess || hipMalloc(&ctx->d_wcount, (WREG_SLOTS + 1) * 8) != hipSuccess ||
         hipHostMalloc(&ctx->h_wreg, (WREG_SLOTS + 1) * 8, hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc(&ctx->h_wcount, (WREG_SLOTS + 1) * 8, hipHostMallocDefault) != hipSuccess ||
-        hipMalloc(&ctx->d_winfo, (WREG_SLOTS + 1) * sizeof(WInfo)) != hipSuccess ||
-        hipHostMalloc(&ctx->h_winfo, (WREG_SLOTS + 1) * sizeof(WInfo), hipHostMallocDefault) != hipSuccess ||
-        hipMemset(ctx->d_winfo, 0, (WREG_SLOTS + 1) * sizeof(WInfo)) != hipSuccess) {
+        hipMalloc(&ctx->d_winfo, (WREG_SLOTS + 1) * sizeof(WInfo) + sizeof(WiCacheImg)) != hipSuccess ||
+        hipHostMalloc(&ctx->h_winfo, (WREG_SLOTS + 1) * sizeof(WInfo) + sizeof(WiCacheImg), hipHostMallocDefault) != hipSuccess ||
+        hipMemset(ctx->d_winfo, 0, (WREG_SLOTS + 1) * sizeof(WInfo)) != hipSuccess ||
+        hipMemset(ctx->d_winfo + WREG_SLOTS + 1, 0xff, sizeof(WiCacheImg)) != hipSuccess) {
         ctx->err = "window registry alloc";
         return fail("create");
     }

@@ -44,8 +44,8 @@ class KafkaBatch:
 
 @dataclass
 class BatchResult:
-    tiles: TileRows
-    latest_rows: np.ndarray     # int64 row indices of the in-batch latest positions (ties included)
+    tiles: TileRows             # None when the rows stayed on the device (rows_on_device=True)
+    latest_rows: np.ndarray     # int64 row indices of the in-batch latest positions (ties included); None likewise
     n_in: int
     n_valid: int
     n_late: int
@@ -54,6 +54,8 @@ class BatchResult:
     watermark_ms: int
     late_watermark_ms: int
     n_partials: int = 0         # partial records merged (direct path: aggregated rows; table mode: ~ distinct keys)
+    n_tiles: int = 0
+    n_latest: int = 0
 
 
 def _u8(a, n):
@@ -94,10 +96,12 @@ class HeatmapEngine:
 
     # ---- host-memory batch (the foreach_batch_func path) ----
     def process_batch(self, epoch_id, lat, lon, ts_us, speed=None, speed_valid=None, vkey=None, row_valid=None,
-                      copy=True):
+                      copy=True, rows_on_device=False):
         """One micro-batch from host columns (the foreach_batch_func path).  copy=False returns views of the
         library's pinned output buffers, valid until the next call on this engine (a 1e8-tile batch's outputs are
-        ~5 GB: copying them costs about as much as the whole GPU pipeline and both PCIe transfers)."""
+        ~5 GB: copying them costs about as much as the whole GPU pipeline and both PCIe transfers).
+        rows_on_device=True leaves the tile rows and latest rows on the device (tiles / latest_rows None, the counts
+        in n_tiles / n_latest): what the writer needs, since it encodes the statements from the device rows."""
         n = int(np.asarray(lat).size)
         lat = np.ascontiguousarray(lat, dtype=np.float64)
         lon = np.ascontiguousarray(lon, dtype=np.float64)
@@ -108,9 +112,10 @@ class HeatmapEngine:
         b = HmBatchIn(n=n, memory=HM_MEM_HOST, lat=ptr(lat), lon=ptr(lon), ts_us=ptr(ts_us), speed=ptr(speed),
                       speed_valid=ptr(_u8(speed_valid, n)), vkey=ptr(vkey), row_valid=ptr(_u8(row_valid, n)))
         out = HmBatchOut()
-        check(self._lib.hm_process_batch(self._ctx, int(epoch_id), ctypes.byref(b), HM_MEM_HOST, ctypes.byref(out)),
+        mem = HM_MEM_DEVICE if rows_on_device else HM_MEM_HOST
+        check(self._lib.hm_process_batch(self._ctx, int(epoch_id), ctypes.byref(b), mem, ctypes.byref(out)),
               self._ctx, "hm_process_batch")
-        return self._result_from_host(out, copy)
+        return self._result_counts(out) if rows_on_device else self._result_from_host(out, copy)
 
     # ---- Kafka values (row f1): JSON decoded on the GPU, then the batch ----
     def decode_json(self, values, offsets):
@@ -133,13 +138,14 @@ class HeatmapEngine:
                           vehicles=dictionary(int(jout.n_vehicles), jout.vehicle_offsets, jout.vehicle_bytes),
                           n_malformed=int(jout.n_malformed))
 
-    def process_kafka(self, epoch_id, values, offsets, copy=True):
+    def process_kafka(self, epoch_id, values, offsets, copy=True, rows_on_device=False):
         """decode_json + hm_process_batch on the decoded device columns; (BatchResult, KafkaBatch)."""
         kb = self.decode_json(values, offsets)
         out = HmBatchOut()
-        check(self._lib.hm_process_batch(self._ctx, int(epoch_id), ctypes.byref(kb.batch), HM_MEM_HOST, ctypes.byref(out)),
+        mem = HM_MEM_DEVICE if rows_on_device else HM_MEM_HOST
+        check(self._lib.hm_process_batch(self._ctx, int(epoch_id), ctypes.byref(kb.batch), mem, ctypes.byref(out)),
               self._ctx, "hm_process_batch")
-        return self._result_from_host(out, copy), kb
+        return (self._result_counts(out) if rows_on_device else self._result_from_host(out, copy)), kb
 
     def latest_buckets(self):
         """The distinct 900-s buckets of the last batch's latest rows' eventTs (computed on the device)."""
@@ -262,7 +268,16 @@ class HeatmapEngine:
                            n_in=int(out.n_in), n_valid=int(out.n_valid), n_late=int(out.n_late),
                            n_state=int(out.n_state), batch_max_event_ms=int(out.batch_max_event_ms),
                            watermark_ms=int(out.watermark_ms), late_watermark_ms=int(out.late_watermark_ms),
-                           n_partials=int(out.n_partials))
+                           n_partials=int(out.n_partials), n_tiles=nt, n_latest=int(out.n_latest))
+
+    @staticmethod
+    def _result_counts(out):
+        """The statistics of a batch whose rows stayed on the device (HM_MEM_DEVICE outputs)."""
+        return BatchResult(tiles=None, latest_rows=None, n_in=int(out.n_in), n_valid=int(out.n_valid),
+                           n_late=int(out.n_late), n_state=int(out.n_state),
+                           batch_max_event_ms=int(out.batch_max_event_ms), watermark_ms=int(out.watermark_ms),
+                           late_watermark_ms=int(out.late_watermark_ms), n_partials=int(out.n_partials),
+                           n_tiles=int(out.n_tiles), n_latest=int(out.n_latest))
 
 
 def _host_statements(pb, po, nd, copy):

@@ -380,12 +380,13 @@ def foreach_batch_func(df, epoch_id: int):
     cols = batch_columns(df)
     eng = get_engine(epoch_id)
     try:
+        # (the tile and latest rows stay on the device: the statements are encoded there from them)
         if "kafka" in cols:   # raw Kafka values: from_json + to_timestamp on the GPU (row f1)
-            res, kb = eng.process_kafka(epoch_id, *cols["kafka"], copy=False)
+            res, kb = eng.process_kafka(epoch_id, *cols["kafka"], rows_on_device=True)
             dicts = (kb.providers, kb.vehicles)
         else:
             res = eng.process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"], cols["speed_valid"],
-                                    cols["vkey"], cols["row_valid"], copy=False)
+                                    cols["vkey"], cols["row_valid"], rows_on_device=True)
             dicts = (cols["provider_uniques"], cols["vehicle_uniques"])
     except BaseException:
         reset_engine()   # the state may hold part of the batch: the next attempt rebuilds it from the checkpoint
@@ -398,7 +399,7 @@ def foreach_batch_func(df, epoch_id: int):
         buf, offs = get_engine().encode_tile_updates(CITY, TTL_MIN)
         _flush_statements(sink, "tiles", buf, offs)
         # ---- 2) latest per (provider, vehicleId) within this micro-batch: statements encoded on the GPU ----
-        if res.latest_rows.size:
+        if res.n_latest:
             buf, offs = get_engine().encode_position_updates(*dicts)   # (local offsets of the rows' 900-s buckets)
             _flush_statements(sink, "positions_latest", buf, offs)
         if STATE_CHECKPOINT:   # after the writes succeeded: the batch is committed

@@ -359,6 +359,7 @@ def test_failed_writes_and_replays_do_not_merge_twice(tmp_path, monkeypatch):
 
             class R:
                 latest_rows = np.zeros(0, np.int64)
+                n_latest = 0
             return R()
 
         def encode_tile_updates(self, city, ttl):

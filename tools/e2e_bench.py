@@ -8,7 +8,15 @@ memory and in page-locked memory (hipHostRegister through torch's pin_memory), b
 bench.py reports.  It is the PCIe-inclusive figure DESIGN.md §7 quotes; bench.py's `value` stays device-resident.
 
 usage: python tools/e2e_bench.py [--events 100000000] [--steps 4]   (one JSON line)
+       python tools/e2e_bench.py --foreach [--events 10000000]
+         foreach_batch_func end to end: C1 (10k events, the reference's Boston batch) and a
+         uniform batch of --events events (~that many tiles at res 8), as pandas frames, written through the wire
+         sink to a loopback server that acknowledges every OP_MSG (no MongoDB on the box: the server only reads the
+         bytes and replies ok, so the time is the writer's own: frame decode, GPU path, statements, sends).
 """
+import socket
+import struct
+import threading
 import argparse
 import json
 import os
@@ -24,11 +32,101 @@ T0 = 1759572000 * 1_000_000
 SPAN = 15 * 60_000_000
 
 
+class LoopbackMongo:
+    """A TCP server on 127.0.0.1 that answers every OP_MSG with {ok: 1} (counts messages and bytes)."""
+
+    def __init__(self):
+        import bson
+        self._ok = bson.encode({"ok": 1.0})
+        self.srv = socket.socket()
+        self.srv.bind(("127.0.0.1", 0))
+        self.srv.listen(8)
+        self.port = self.srv.getsockname()[1]
+        self.messages = 0
+        self.bytes = 0
+        threading.Thread(target=self._serve, daemon=True).start()
+
+    def _serve(self):
+        while True:
+            try:
+                c, _ = self.srv.accept()
+            except OSError:
+                return
+            threading.Thread(target=self._conn, args=(c,), daemon=True).start()
+
+    def _conn(self, c):
+        def exact(n):
+            buf = bytearray(n)
+            v = memoryview(buf)
+            got = 0
+            while got < n:
+                k = c.recv_into(v[got:], n - got)
+                if not k:
+                    raise EOFError
+                got += k
+            return buf
+        try:
+            while True:
+                length, rid, _, _ = struct.unpack("<iiii", exact(16))
+                exact(length - 16)
+                self.messages += 1
+                self.bytes += length
+                body = struct.pack("<I", 0) + b"\x00" + self._ok
+                c.sendall(struct.pack("<iiii", 16 + len(body), 0, rid, 2013) + body)
+        except (EOFError, OSError):
+            c.close()
+
+
+def foreach_mode(a):
+    import pandas as pd
+    from mobheat import stream, synth
+    srv = LoopbackMongo()
+    stream.MONGO_URI = f"mongodb://127.0.0.1:{srv.port}"
+    stream.STATE_CHECKPOINT = False
+    out = {"what": "foreach_batch_func(df, epoch) end to end: pandas frame -> columns -> GPU path (rows stay on the "
+                   "device) -> tile and position statements encoded on the GPU -> OP_MSG frames over TCP to a "
+                   "loopback server that acknowledges each; median of the timed batches"}
+    cases = [("c1", synth.c1_boston(seed=0)), ("uniform", None)]
+    for name, b in cases:
+        n = 10_000 if b is not None else a.events
+        if b is None:
+            rng = np.random.default_rng(3)
+            b = dict(lat=np.degrees(np.arcsin(rng.uniform(-1, 1, n))), lon=rng.uniform(-180, 180, n),
+                     ts_us=T0 + rng.integers(0, 60_000_000, n), speed=rng.uniform(0, 80, n),
+                     speed_valid=rng.random(n) >= 0.15, vkey=rng.integers(0, 50_000, n).astype(np.uint64),
+                     row_valid=np.ones(n, bool))
+        sp = b["speed"].astype(float).copy()
+        sp[~b["speed_valid"]] = np.nan
+        frames = []
+        for s in range(a.steps + 1):
+            df = pd.DataFrame({"provider": "mbta", "vehicleId": pd.Series(b["vkey"]).map("v{:05d}".format),
+                               "lat": b["lat"], "lon": b["lon"], "speedKmh": pd.Series(sp).astype(object).where(b["speed_valid"], None),
+                               "eventTs": pd.to_datetime(b["ts_us"] + s * 60_000_000, unit="us")})
+            frames.append(df)
+        stream.reset_engine()
+        times = []
+        m0, b0 = srv.messages, srv.bytes
+        for s, df in enumerate(frames):
+            t = time.perf_counter()
+            stream.foreach_batch_func(df, s)
+            if s >= 1:
+                times.append(time.perf_counter() - t)
+        ms = 1e3 * float(np.median(times))
+        out[name] = {"events": n, "ms_per_batch": round(ms, 2), "events_per_s": n / (ms * 1e-3),
+                     "messages_per_batch": (srv.messages - m0) / len(frames),
+                     "wire_bytes_per_batch": (srv.bytes - b0) / len(frames)}
+    stream.reset_engine()
+    print(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--events", type=int, default=100_000_000)
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--foreach", action="store_true")
     a = ap.parse_args()
+    if a.foreach:
+        return foreach_mode(a)
     import torch
     import mobheat
     n = a.events
@@ -43,20 +141,26 @@ def main():
         eng = mobheat.HeatmapEngine(h3_res=8, batch_capacity_hint=n)
         ts0 = cols["ts_us"].copy()
         times, tiles = [], 0
-        for s in range(a.steps + 2):
-            cols["ts_us"][:] = ts0 + s * SPAN
-            t = time.perf_counter()
-            res = eng.process_batch(s, **cols, copy=False)
-            dt = time.perf_counter() - t
-            if s >= 2:
-                times.append(dt)
-                tiles = len(res.tiles)
+        for rows_on_device in (False, True):
+            times, tiles = [], 0
+            for s in range(a.steps + 2):
+                cols["ts_us"][:] = ts0 + (s + (a.steps + 2) * rows_on_device) * SPAN
+                t = time.perf_counter()
+                res = eng.process_batch(s + (a.steps + 2) * rows_on_device, **cols, copy=False,
+                                        rows_on_device=rows_on_device)
+                dt = time.perf_counter() - t
+                if s >= 2:
+                    times.append(dt)
+                    tiles = res.n_tiles
+            ms = 1e3 * float(np.median(times))
+            key = mode + ("_rows_on_device" if rows_on_device else "")
+            out[key] = {"ms_per_batch": round(ms, 1), "events_per_s": n / (ms * 1e-3), "tiles_per_batch": tiles,
+                        "bytes_out": 0 if rows_on_device else tiles * 49 + int(res.n_latest) * 8}
         eng.close()
-        ms = 1e3 * float(np.median(times))
-        out[mode] = {"ms_per_batch": round(ms, 1), "events_per_s": n / (ms * 1e-3), "tiles_per_batch": tiles,
-                     "bytes_out": tiles * 49 + int(res.latest_rows.size) * 8}
     out["what"] = ("hm_process_batch with host inputs and host outputs (H2D of the 42-B/event columns, the hot "
-                   "path, D2H of the tiles and latest rows), median of the timed batches")
+                   "path, D2H of the tiles and latest rows), median of the timed batches; *_rows_on_device: the same "
+                   "with the rows left on the device, as foreach_batch_func now runs it (the statements are encoded "
+                   "from the device rows)")
     print(json.dumps(out))
 
 
