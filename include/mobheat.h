@@ -331,7 +331,8 @@ int hm_cells_to_boundary(const uint64_t *cells, int64_t n, int32_t memory, int32
 int hm_selftest_cells_to_boundary_host(const uint64_t *cells, int64_t n, double *lat, double *lng, int32_t *nverts);
 
 /* Counts of the last hm_process_batch (up to n of them): [0] keys created in the tile state, [1] partial records
- * merged (direct path: aggregated rows; table mode: ~ distinct keys), [2] tiles emitted, [3] 1 if table mode ran. */
+ * merged (direct path: aggregated rows; table mode: ~ distinct keys), [2] tiles emitted, [3] 1 if table mode ran,
+ * [4] table mode: aggregates evicted from k_agg's LDS tables into its buckets. */
 int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n);
 
 /* HM_ABI_VERSION the library was built with (callers check it before hm_create). */

@@ -2358,7 +2358,8 @@ struct hm_ctx {
     int merge_grid = 0;
     int64_t prev_agg_rows = 0, prev_keys = 0;   // aggregated rows and distinct keys of the last batch
     bool last_table = false;
-    int64_t last_counts[4] = {0, 0, 0, 0};   // hm_last_counts
+    int64_t last_counts[5] = {0, 0, 0, 0, 0};   // hm_last_counts
+    int64_t table_evicted = 0;                   // table mode: aggregates k_agg evicted into its buckets (last batch)
     // hm_decode_json (row f1): the values on the device, the decoded columns, the string dictionaries
     struct Dict {
         DevBuf tab, slot_of, occ, slots, code_of_slot, clen, coff, cbytes, btot, boff;
@@ -3029,6 +3030,7 @@ static int phase_table(hm_ctx *ctx, const Inputs &I, int64_t n_agg, int64_t *n_p
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "more than %d windows in one batch", GMAP_SLOTS);
     *n_parts = (int64_t)ctx->h_st->n_partials;
+    ctx->table_evicted = (int64_t)ctx->h_st->n_evicted;
     // the next table batch's sub-bucket capacity: twice this batch's fullest one (shrinks slowly)
     unsigned long long mx = 0;
     for (unsigned long long c : ctx->h_agg_cursor) mx = std::max(mx, c);
@@ -3441,7 +3443,7 @@ int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n) {
 
 int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n) {
     if (!ctx || !c) return HM_E_INVALID;
-    for (int i = 0; i < n && i < 4; i++) c[i] = ctx->last_counts[i];
+    for (int i = 0; i < n && i < 5; i++) c[i] = ctx->last_counts[i];
     return HM_OK;
 }
 
@@ -3498,6 +3500,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     ctx->last_counts[1] = ctx->n_partials_merged;
     ctx->last_counts[2] = (int64_t)s2.n_touched;
     ctx->last_counts[3] = table ? 1 : 0;
+    ctx->last_counts[4] = table ? ctx->table_evicted : 0;
     // the next batch's aggregation path is chosen from this one's cardinality
     if (n_agg >= (int64_t(1) << 16)) {
         ctx->prev_agg_rows = n_agg;

@@ -248,9 +248,9 @@ class HeatmapEngine:
                 "partition": ms[6]}
 
     def last_counts(self):
-        c = (ctypes.c_int64 * 4)()
-        check(self._lib.hm_last_counts(self._ctx, c, 4), self._ctx)
-        return {"state_new": c[0], "partials": c[1], "tiles": c[2], "table_mode": bool(c[3])}
+        c = (ctypes.c_int64 * 5)()
+        check(self._lib.hm_last_counts(self._ctx, c, 5), self._ctx)
+        return {"state_new": c[0], "partials": c[1], "tiles": c[2], "table_mode": bool(c[3]), "evicted": c[4]}
 
     def _result_from_host(self, out, copy=True):
         def arr(p, n, dt):

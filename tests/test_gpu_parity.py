@@ -256,6 +256,43 @@ def test_full_size_properties_c2():
     eng.close()
 
 
+def test_rows_on_device_same_statements():
+    """rows_on_device=True (what foreach_batch_func uses: the rows stay on the device and the statements are encoded
+    from them) gives the same counts and byte-identical tile and position statements as the host-output path, over
+    two batches that update the same windows."""
+    import mobheat
+    from mobheat import synth
+    a, b = mobheat.HeatmapEngine(h3_res=9), mobheat.HeatmapEngine(h3_res=9)
+    for epoch in range(2):
+        x = synth.c1_boston(seed=30 + epoch, n=50_000)
+        x["ts_us"] = x["ts_us"] + epoch * 30_000_000
+        ra = a.process_batch(epoch, **x)
+        rb = b.process_batch(epoch, **x, rows_on_device=True)
+        assert rb.tiles is None and rb.latest_rows is None
+        assert (rb.n_tiles, rb.n_latest) == (len(ra.tiles), ra.latest_rows.size)
+        assert (rb.n_valid, rb.n_late, rb.n_state, rb.watermark_ms) == (ra.n_valid, ra.n_late, ra.n_state, ra.watermark_ms)
+        ba, oa = a.encode_tile_updates("ath", 30)
+        bb, ob = b.encode_tile_updates("ath", 30)
+        # (tile order and the last bits of the fp64 sums may differ between two engines: compare by _id)
+        import bson
+
+        def docs(buf, offs):
+            out = {}
+            for k in range(offs.size - 1):
+                d = bson.decode(bytes(buf[offs[k]:offs[k + 1]]))
+                out[d["q"]["_id"]] = d["u"]["$set"]
+            return out
+        da, db = docs(ba, oa), docs(bb, ob)
+        assert da.keys() == db.keys() and len(da) == rb.n_tiles
+        for k, u in da.items():
+            v = db[k]
+            assert u.keys() == v.keys() and u["count"] == v["count"] and u["staleAt"] == v["staleAt"]
+            assert u["avgSpeedKmh"] == pytest.approx(v["avgSpeedKmh"], rel=1e-12, abs=1e-12)
+            assert u["centroid"]["coordinates"] == pytest.approx(v["centroid"]["coordinates"], rel=1e-12)
+    a.close()
+    b.close()
+
+
 def test_foreach_batch_func_capture_sink():
     """The drop-in boundary end to end: a micro-batch frame in, the reference's UpdateOne ops out."""
     import pandas as pd

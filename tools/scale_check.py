@@ -157,7 +157,8 @@ def run_c3(dev, scale):
         assert nt < n // 20, "C3 keys should repeat heavily"
         tm = eng.last_timings()
         report["batches"].append({"ms": round(dt * 1e3, 1), "events_per_s": n / dt, "tiles": nt,
-                                  "partials": int(out.n_partials), "kernel_ms": {k: round(v, 2) for k, v in tm.items()}})
+                                  "partials": int(out.n_partials), "evicted": int(eng.last_counts()["evicted"]),
+                                  "kernel_ms": {k: round(v, 2) for k, v in tm.items()}})
         if b >= 4:
             rates.append(n / dt)
     report["steady_events_per_s"] = float(np.median(rates))
