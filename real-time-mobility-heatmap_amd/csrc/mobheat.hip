@@ -587,9 +587,27 @@ __device__ __forceinline__ void wi_load(WiCacheL &C, const WInfo *winfo) {   // 
         C.e[q] = img->e[q];
     }
 }
+// Before a software-pipelined loop (the next round's columns loaded while this round computes): wait for the first
+// round's loads.  Without it the compiler's wait-count pass merges, at the loop header, the preheader's pending loads
+// into the registers the loop's back edge fills by copies, and then waits inside every round until only a few loads
+// are in flight -- i.e. for the next round's prefetch too (the vector memory counter retires in order).
+__device__ __forceinline__ void preheader_wait() { __builtin_amdgcn_s_waitcnt(0); }
+
+// A miss reads the registry in HBM and waits for it inside the miss branch (relaxed atomic loads: a plain load would
+// be folded with the LDS read into one flat load of a selected address, whose wait -- vmcnt(0) after every row --
+// also waited for the next round's prefetched columns).
 __device__ __forceinline__ WInfo wi_get(const WiCacheL &C, const WInfo *winfo, unsigned slot) {
     const unsigned e = slot & (WI_CACHE - 1);
-    return C.tag[e] == slot ? C.e[e] : winfo[slot];
+    WInfo w = C.e[e];
+    if (C.tag[e] != slot) {
+        static_assert(sizeof(WInfo) % 8 == 0, "WInfo: 8-B words");
+        const unsigned long long *g = (const unsigned long long *)&winfo[slot];
+        unsigned long long *d = (unsigned long long *)&w;
+#pragma unroll
+        for (int q = 0; q < (int)(sizeof(WInfo) / 8); q++) d[q] = __hip_atomic_load(&g[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0);
+    }
+    return w;
 }
 
 // the key's radix digit: with nranks > 0 its owner rank, else its (window, region) bin (binp: kernels.h WInfo)
@@ -669,6 +687,7 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_scatter(const uint64_t *__res
     };
     int64_t i0 = t0 + (int64_t)(threadIdx.x >> 6) * 64;
     Row nx = load(i0 + ln);
+    preheader_wait();
     for (; i0 < t1; i0 += EV_THREADS) {
         const Row r = nx;
         nx = load(i0 + EV_THREADS + ln);
@@ -949,7 +968,10 @@ __global__ __launch_bounds__(AG_THREADS) void k_agg(const uint64_t *__restrict__
     const int64_t b0 = (int64_t)blockIdx.x * span;
     const int64_t b1 = b0 + span < n ? b0 + span : n;
     FreshCount FC(fresh_ctr);
-    // a row's columns, loaded one round ahead (the round's loads are in flight while the previous one aggregates)
+    // a row's columns, loaded one round ahead (the round's loads are in flight while the previous one aggregates).
+    // (Measured on C3: keeping the validity byte raw and waiting for the first round before the loop -- so that no
+    // round waits for the next round's loads -- made k_agg 0.3 ms slower, profiles/r2/ab1/: its rounds are not
+    // load-bound, its flushes are.)
     struct Row { uint64_t k; double sp, la, lo; bool sv; };
     auto load = [&](int64_t i) {
         Row r{0, 0.0, 0.0, 0.0, false};
@@ -1749,14 +1771,17 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     __shared__ WinCacheL WC;
     __shared__ double Fc[20][3], Fu[20][2][3];   // the fast path's per-face tables (res parity): LDS reads
     __shared__ unsigned dskip;                    // the fused dedup has given up (*dgiveup) -- skip it
+    __shared__ long long tmax_l[IG_THREADS];      // per-thread max ts (an LDS max per row instead of 2 live registers)
     for (int k = threadIdx.x; k < 60; k += IG_THREADS) (&Fc[0][0])[k] = (&c_tab.faceCenterPoint[0][0])[k];
     for (int k = threadIdx.x; k < 120; k += IG_THREADS) (&Fu[0][0][0])[k] = (&c_tab.fastU[res & 1][0][0][0])[k];
     wc_init(WC);
     if (threadIdx.x == 0) dskip = 0;
     __syncthreads();
     const int64_t tile_us = wdiv.d;
-    unsigned long long nvalid = 0, nlate = 0, bad = 0, wover = 0;
-    long long tmax = INT64_MIN;
+    // per-thread counters in 32 bits (a thread sees at most n / gstride < 2^32 rows): fewer registers live across
+    // the cell computation, whose peak spilled the prefetched columns
+    unsigned nvalid = 0, nlate = 0, bad = 0, wover = 0;
+    tmax_l[threadIdx.x] = INT64_MIN;
     bool dretry = false;
     int round = 0;
     const int64_t gstride = (int64_t)gridDim.x * IG_THREADS;
@@ -1827,7 +1852,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
             fl = late ? (F_VALID | F_LATE) : (F_VALID | F_AGG);
             nvalid++;
             nlate += late;
-            tmax = t > tmax ? t : tmax;
+            atomicMax(&tmax_l[threadIdx.x], (long long)t);
             if (!late) {
                 widx = wc_lookup(WC, wreg, wq, wenc_of(ws), wslot);
                 if (widx < 0) { wover++; fl = F_VALID; }   // registry full: the batch fails (hm_process_batch)
@@ -1881,18 +1906,16 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     __syncthreads();
     for (int q = threadIdx.x; q < WC_SLOTS; q += IG_THREADS)
         if (WC.cnt[q]) atomicAdd(&wcount[(WC.e[q] & 0xfff) - 1], (unsigned long long)WC.cnt[q]);
-    nvalid = wave_sum(nvalid);
-    nlate = wave_sum(nlate);
-    bad = wave_sum(bad);
-    wover = wave_sum(wover);
-    tmax = wave_max(tmax);
+    const unsigned long long wvalid = wave_sum((unsigned long long)nvalid), wlate = wave_sum((unsigned long long)nlate);
+    const unsigned long long wbad = wave_sum((unsigned long long)bad), wwover = wave_sum((unsigned long long)wover);
+    const long long tmax = wave_max(tmax_l[threadIdx.x]);
     const unsigned long long rt = __ballot(dretry);
     if (lane_id() == 0) {
-        if (nvalid) atomicAdd(&st->n_valid, nvalid);
-        if (nlate) atomicAdd(&st->n_late, nlate);
+        if (wvalid) atomicAdd(&st->n_valid, wvalid);
+        if (wlate) atomicAdd(&st->n_late, wlate);
         if (tmax != INT64_MIN) atomicMax(&st->max_ts_ms, (long long)(tmax / 1000));   // trunc(max) = max(trunc)
-        if (bad) atomicAdd(&st->bad_vkey, bad);
-        if (wover) atomicAdd(&st->win_overflow, wover);
+        if (wbad) atomicAdd(&st->bad_vkey, wbad);
+        if (wwover) atomicAdd(&st->win_overflow, wwover);
         if (rt) atomicAdd(&st->dedup_retry, 1ull);
     }
 }
