@@ -752,7 +752,13 @@ constexpr int AG_SLOTS = 3840;
 #endif
 constexpr int AG_PER = AG_SLOTS / AG_THREADS + (AG_SLOTS % AG_THREADS != 0);
 constexpr int AG_FLUSH_AT = AG_SLOTS - AG_THREADS;   // a round adds at most AG_THREADS keys
-constexpr int AG_KEEP_MAX = AG_SLOTS / 3;       // aggregates kept resident by a flush
+#ifndef HM_AG_KEEP_DIV
+#define HM_AG_KEEP_DIV 8
+#endif
+// aggregates kept resident by a flush.  Fewer kept = more room per flush = fewer flushes, which cost more than the
+// extra evicted aggregates (C3 shard, profiles/r2/abk*/: keep 1/2 -> k_agg + k_bin_reduce 6.4 ms, 1/3 -> 4.9,
+// 1/5 -> 4.35, 1/8 -> 4.0, 1/12 and 1/24 -> 4.0; evicted aggregates 30.1M / 33.7M / 37.5M / 40.1M / 41.9M / 44.1M)
+constexpr int AG_KEEP_MAX = AG_SLOTS / HM_AG_KEEP_DIV;
 constexpr int AG_PROBES = 64;
 constexpr int AG_BINS = 256, AG_SUB = 8;        // buckets x sub-buckets (XCD)
 struct AgTable {
