@@ -751,7 +751,14 @@ constexpr int AG_SLOTS = 3833;
 constexpr int AG_SLOTS = 3840;
 #endif
 constexpr int AG_PER = AG_SLOTS / AG_THREADS + (AG_SLOTS % AG_THREADS != 0);
-constexpr int AG_FLUSH_AT = AG_SLOTS - AG_THREADS;   // a round adds at most AG_THREADS keys
+#ifndef HM_AG_HEADROOM
+#define HM_AG_HEADROOM 640
+#endif
+// flush when fewer than HM_AG_HEADROOM slots are free.  A round adds at most AG_THREADS keys, ~360 on C3; when one
+// adds more than the headroom, probes fail and those rows go out as partial records (exact, just not pre-aggregated).
+// C3 shard (profiles/r2/abh/): headroom 1024 -> k_agg + k_bin_reduce 4.01 ms, 640 -> 3.89 ms (~200 such partials
+// per batch), 400 -> 4.1 ms (13k)
+constexpr int AG_FLUSH_AT = AG_SLOTS - HM_AG_HEADROOM;
 #ifndef HM_AG_KEEP_DIV
 #define HM_AG_KEEP_DIV 8
 #endif
@@ -864,8 +871,13 @@ __device__ void ag_flush(AgTable &T, bool final, AggRec *__restrict__ bucket, un
         if (s < AG_SLOTS && T.key[s]) {
             const unsigned c = (unsigned)T.cnt[s];
             lg[q] = min(31 - __clz(c), 15);
-            atomicAdd(&T.hist[lg[q]], 1u);
         }
+        // the keep threshold reads hist[1..15] only (singletons always go): no atomics for the many count-1
+        // entries, and the count-2/3 class (the next most common) counted per wave -- every lane adding into one
+        // LDS word serialises the wave
+        const unsigned long long m1 = __ballot(lg[q] == 1);
+        if (m1 && lane_id() == 0) atomicAdd(&T.hist[1], (unsigned)__popcll(m1));
+        if (lg[q] >= 2) atomicAdd(&T.hist[lg[q]], 1u);
     }
     __syncthreads();
     if (t == 0) {   // keep the entries with count >= 2^kf, at most AG_KEEP_MAX of them (kf >= 1: singletons go)
