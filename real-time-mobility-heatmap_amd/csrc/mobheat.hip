@@ -1137,6 +1137,9 @@ __global__ __launch_bounds__(AG_THREADS) void k_bin_reduce(const AggRec *__restr
 #define HM_MO_THREADS 512
 #endif
 constexpr int MO_THREADS = HM_MO_THREADS;      // partials per chunk (one per lane)
+#ifndef HM_MO_COOP_LINES
+#define HM_MO_COOP_LINES 1
+#endif
 constexpr int MO_CLAIM = 2 * MO_THREADS;
 #ifndef HM_MO_TAG_MAX
 #define HM_MO_TAG_MAX 90112
@@ -1501,16 +1504,52 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             if (!first) krow = (unsigned)o.touched;
             if (gslot) v = line_of(p, o, first, krow);
             // 4. this chunk's stores: the state line (whole) and the key's row
-            if (gslot) {
 #ifndef HM_ABL_NOSLOT   // ablation builds only: the state line stores priced by their absence
-                uint4 *d = (uint4 *)gslot;   // the whole 64-B line
-                d[0] = make_uint4((unsigned)p.cell, (unsigned)(p.cell >> 32), (unsigned)p.we, (unsigned)(p.we >> 32));
-                d[1] = make_uint4((unsigned)v.count, (unsigned)(v.count >> 32), (unsigned)v.nspeed, (unsigned)(v.nspeed >> 32));
+            {
                 const uint64_t b0s = __builtin_bit_cast(uint64_t, v.sspeed), b1s = __builtin_bit_cast(uint64_t, v.slat);
                 const uint64_t b2s = __builtin_bit_cast(uint64_t, v.slon);
-                d[2] = make_uint4((unsigned)b0s, (unsigned)(b0s >> 32), (unsigned)b1s, (unsigned)(b1s >> 32));
-                d[3] = make_uint4((unsigned)b2s, (unsigned)(b2s >> 32), (unsigned)v.touched, (unsigned)(v.touched >> 32));
+                const uint4 q0 = make_uint4((unsigned)p.cell, (unsigned)(p.cell >> 32), (unsigned)p.we, (unsigned)(p.we >> 32));
+                const uint4 q1 = make_uint4((unsigned)v.count, (unsigned)(v.count >> 32), (unsigned)v.nspeed, (unsigned)(v.nspeed >> 32));
+                const uint4 q2 = make_uint4((unsigned)b0s, (unsigned)(b0s >> 32), (unsigned)b1s, (unsigned)(b1s >> 32));
+                const uint4 q3 = make_uint4((unsigned)b2s, (unsigned)(b2s >> 32), (unsigned)v.touched, (unsigned)(v.touched >> 32));
+#if HM_MO_COOP_LINES
+                // whole lines per store instruction: in round k, the wave's lanes 16k..16k+15 put their lines in LDS
+                // (the wave's slices of S.sc / S.sh, unused after the probe), then lane L stores part L & 3 of line
+                // 16k + L / 4 -- each 16-B store instruction writes 16 whole 64-B lines instead of a quarter of 64
+                // (each lane's own line: four instructions, each touching 64 different lines)
+                uint4 *xa = (uint4 *)&S.sc[t & ~63], *xb = (uint4 *)&S.sh[t & ~63];
+                const int ln = lane_id();
+                const unsigned long long ga = (unsigned long long)gslot;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if ((ln >> 4) == k) {
+                        const int e = (ln & 15) * 2;
+                        xa[e] = q0;
+                        xa[e + 1] = q1;
+                        xb[e] = q2;
+                        xb[e + 1] = q3;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    const int src = k * 16 + (ln >> 2), part = ln & 3;
+                    const unsigned long long sa = __shfl(ga, src, 64);
+                    const uint4 val = ((part < 2) ? xa : xb)[(src & 15) * 2 + (part & 1)];
+                    if (sa) ((uint4 *)sa)[part] = val;
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                }
+#else
+                if (gslot) {
+                    uint4 *d = (uint4 *)gslot;   // the whole 64-B line
+                    d[0] = q0;
+                    d[1] = q1;
+                    d[2] = q2;
+                    d[3] = q3;
+                }
 #endif
+            }
+#endif
+            if (gslot) {
                 if (created) created_cnt++;
 #ifndef HM_ABL_NOROWS
                 if (!rehash) put_row(rows, b0 + krow, p.cell, p.we, v.count, v.nspeed, v.sspeed, v.slat, v.slon);
