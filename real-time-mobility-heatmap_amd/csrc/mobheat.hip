@@ -1173,8 +1173,13 @@ struct MoShared {
 
 template <typename T>
 __device__ __forceinline__ T ld_l2(const T *p) {   // bypass the CU's L1 (chunks of one workgroup re-read slots)
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (a global-address-space access: the slot pointers come from LDS, and as generic pointers every access became a
+    // flat instruction, which also counts on lgkmcnt -- so each later LDS wait waited for it to complete)
+    return __hip_atomic_load((__attribute__((address_space(1))) const T *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+typedef __attribute__((address_space(1))) const hm_v4u g_cv4u;
+typedef __attribute__((address_space(1))) hm_v4u g_v4u;
+__device__ __forceinline__ void st_g16(void *p, uint4 v) { *(g_v4u *)p = hm_v4u{v.x, v.y, v.z, v.w}; }   // global 16-B store
 __device__ __forceinline__ unsigned mo_claim_home(unsigned long long addr) {
     return (unsigned)(((addr >> 6) * UINT64_C(0x9e3779b97f4a7c15)) >> 40) & (MO_CLAIM - 1);
 }
@@ -1414,7 +1419,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                             if (x == -1) {
                                 gslot = sl;
                                 created = free_here;
-                                if (created) gen_tags(*g)[sidx] = (uint8_t)tag8(hk);
+                                if (created) ((__attribute__((address_space(1))) uint8_t *)gen_tags(*g))[sidx] = (uint8_t)tag8(hk);
                                 done = true;
                             } else if (S.sc[x] == p.cell && S.sh[x] == hk) {
                                 mo_add_into(S, x, p);
@@ -1432,6 +1437,40 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
         // the slot's current line (all loads of a lane issued together; created slots read nothing)
         auto old_line = [&](TileSlot *gslot, bool created) __attribute__((always_inline)) -> MLine {
             MLine o{};
+#if HM_MO_COOP_LINES
+            // whole lines per load instruction (the mirror of step 4's stores): in round k, lane L loads part L & 3 of
+            // the line of lane 16k + L / 4 (16-B non-temporal loads: L2-served, like ld_l2) into the wave's LDS slice,
+            // and lanes 16k..16k+15 take their lines from there.  Every lane of the wave runs it (shuffles).
+            const bool need = gslot && !created;
+            if (__ballot(need)) {
+                uint4 *xa = (uint4 *)&S.sc[t & ~63], *xb = (uint4 *)&S.sh[t & ~63];
+                const int ln = lane_id();
+                const unsigned long long ga = need ? (unsigned long long)gslot : 0ull;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int src = k * 16 + (ln >> 2), part = ln & 3;
+                    const unsigned long long sa = __shfl(ga, src, 64);
+                    if (sa) {
+                        const hm_v4u x = __builtin_nontemporal_load((g_cv4u *)sa + part);
+                        ((part < 2) ? xa : xb)[(src & 15) * 2 + (part & 1)] = make_uint4(x.x, x.y, x.z, x.w);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    if (need && (ln >> 4) == k) {
+                        const int e = (ln & 15) * 2;
+                        const uint4 q1 = xa[e + 1], q2 = xb[e], q3 = xb[e + 1];   // (part 0: cell, window)
+                        o.count = (unsigned long long)q1.x | ((unsigned long long)q1.y << 32);
+                        o.nspeed = (unsigned long long)q1.z | ((unsigned long long)q1.w << 32);
+                        o.sspeed = __builtin_bit_cast(double, (unsigned long long)q2.x | ((unsigned long long)q2.y << 32));
+                        o.slat = __builtin_bit_cast(double, (unsigned long long)q2.z | ((unsigned long long)q2.w << 32));
+                        o.slon = __builtin_bit_cast(double, (unsigned long long)q3.x | ((unsigned long long)q3.y << 32));
+                        o.touched = (unsigned long long)q3.z | ((unsigned long long)q3.w << 32);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                }
+            }
+#else
             if (gslot && !created) {
                 o.touched = ld_l2(&gslot->touched);
                 o.count = ld_l2(&gslot->count);
@@ -1440,6 +1479,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                 o.slat = ld_l2(&gslot->slat);
                 o.slon = ld_l2(&gslot->slon);
             }
+#endif
             return o;
         };
         auto line_of = [&](const MRec &p, const MLine &o, bool first, unsigned krow) __attribute__((always_inline)) -> MLine {
@@ -1534,7 +1574,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                     const int src = k * 16 + (ln >> 2), part = ln & 3;
                     const unsigned long long sa = __shfl(ga, src, 64);
                     const uint4 val = ((part < 2) ? xa : xb)[(src & 15) * 2 + (part & 1)];
-                    if (sa) ((uint4 *)sa)[part] = val;
+                    if (sa) st_g16((uint4 *)sa + part, val);
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 }
@@ -1572,7 +1612,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             if (!S.res_dirty[r]) continue;
             uint4 *dst = (uint4 *)S.res_gtags[r];
             const unsigned w0 = S.res_off[r] >> 4, nw = (S.res_mask[r] + 1) >> 4;
-            for (unsigned q = t; q < nw; q += MO_THREADS) dst[q] = ((const uint4 *)mo_tags)[w0 + q];
+            for (unsigned q = t; q < nw; q += MO_THREADS) st_g16(dst + q, ((const uint4 *)mo_tags)[w0 + q]);
         }
         if (t == 0) { bin_cnt[bin] = S.n_touched; S.n_touched = 0; }
         lds_barrier();
