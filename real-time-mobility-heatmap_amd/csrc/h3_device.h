@@ -344,8 +344,16 @@ struct H3Tables {
     double edgeY[17];
 };
 
-// _faceIjkToH3 (faceijk.c), res >= 1
-HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const H3Tables &T) {
+// the two tables _faceIjkToH3 reads (k_ingest keeps a copy in LDS)
+struct H3BaseTables {
+    int faceIjkBaseCells[20][3][3][3][2];
+    int baseCellData[122][7];
+};
+
+// _faceIjkToH3 (faceijk.c), res >= 1.  TT: any table holding faceIjkBaseCells and baseCellData (H3Tables, or the
+// LDS copy k_ingest keeps: lane-indexed reads there do not wait behind the vector loads in flight)
+template <typename TT>
+HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const TT &T) {
     uint64_t h = UINT64_C(0x00001fffffffffff) | (UINT64_C(1) << 59) | ((uint64_t)res << 52);
     if (res == 0) {
         if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
@@ -554,8 +562,9 @@ HM_HD void closestFaceF32(float fx, float fy, float fz, float &best, float &seco
 // The fast path.  Returns false when the caller must use latLngToCellDeg; otherwise `out` is upstream's cell
 // (0 where the reference's UDF returns None).  fc = T.faceCenterPoint, fu = T.fastU[res & 1], or copies of them
 // (k_ingest keeps them in LDS: lane-indexed reads there do not queue behind its outstanding global loads).
+template <typename TT = H3Tables>
 HM_HD bool latLngToCellFastP(double lat_deg, double lng_deg, int res, const H3Tables &T, const double (*fc)[3],
-                             const double (*fu)[2][3], uint64_t &out) {
+                             const double (*fu)[2][3], uint64_t &out, const TT *bt = nullptr) {
     out = 0;
     if (!(lat_deg >= -90.0 && lat_deg <= 90.0 && lng_deg >= -180.0 && lng_deg <= 180.0)) return true;
     double sl, cl, sg, cg;
@@ -631,7 +640,7 @@ HM_HD bool latLngToCellFastP(double lat_deg, double lng_deg, int res, const H3Ta
         h.j = -1 * h.j;
     }
     ijkNormalize(h);
-    out = faceIjkToH3(face, h, res, T);
+    out = bt ? faceIjkToH3(face, h, res, *bt) : faceIjkToH3(face, h, res, T);
     return true;
 }
 HM_HD bool latLngToCellFast(double lat_deg, double lng_deg, int res, const H3Tables &T, uint64_t &out) {

@@ -1845,6 +1845,10 @@ constexpr int IG_THREADS = 256;
 #ifndef HM_INGEST_PREFETCH
 #define HM_INGEST_PREFETCH 1
 #endif
+#ifndef HM_INGEST_TLATE
+#define HM_INGEST_TLATE 1
+#endif
+__device__ const uint8_t g_one_byte = 1;   // k_ingest's row validity when the batch has no validity column
 
 // wave-cooperative count: lanes with pred add 1 to cnt[slot] (one LDS add per distinct slot per wave)
 __device__ __forceinline__ void wave_count_slots(bool pred, int slot, unsigned *cnt) {
@@ -1871,6 +1875,11 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     __shared__ long long tmax_l[IG_THREADS];      // per-thread max ts (an LDS max per row instead of 2 live registers)
     for (int k = threadIdx.x; k < 60; k += IG_THREADS) (&Fc[0][0])[k] = (&c_tab.faceCenterPoint[0][0])[k];
     for (int k = threadIdx.x; k < 120; k += IG_THREADS) (&Fu[0][0][0])[k] = (&c_tab.fastU[res & 1][0][0][0])[k];
+    // _faceIjkToH3's base-cell tables in LDS (7.7 KB): from __constant__ memory they were lane-indexed vector loads
+    // at the end of every cell, each with a full wait that also waited for the next round's prefetched columns
+    __shared__ H3BaseTables BT;
+    for (int k = threadIdx.x; k < 20 * 27 * 2; k += IG_THREADS) (&BT.faceIjkBaseCells[0][0][0][0][0])[k] = (&c_tab.faceIjkBaseCells[0][0][0][0][0])[k];
+    for (int k = threadIdx.x; k < 122 * 7; k += IG_THREADS) (&BT.baseCellData[0][0])[k] = (&c_tab.baseCellData[0][0])[k];
     wc_init(WC);
     if (threadIdx.x == 0) dskip = 0;
     __syncthreads();
@@ -1894,7 +1903,9 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         if (i0 < n) {
             nla = __builtin_nontemporal_load(&lat[i0]);
             nlo = __builtin_nontemporal_load(&lon[i0]);
+#if !HM_INGEST_TLATE
             nt = __builtin_nontemporal_load(&ts[i0]);
+#endif
             nv = __builtin_nontemporal_load(&vkey[i0]);
             if (row_valid) nrv = __builtin_nontemporal_load(&row_valid[i0]);
         }
@@ -1905,9 +1916,29 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         const bool in = i < n;
 #if HM_INGEST_PREFETCH
         const double la = nla, lo = nlo;
+#if HM_INGEST_TLATE
+        // ts is not prefetched: it is loaded now and first used after the cell, whose computation hides the load
+        // (prefetched, the next round's ts was the register the cell computation's peak spilled -- a spill that
+        // waited for every prefetched load mid-round)
+        const int64_t t = in ? __builtin_nontemporal_load(&ts[i]) : 0;
+        (void)nt;
+#else
         const int64_t t = nt;
+#endif
         const unsigned long long v = nv;
         const bool rv = nrv != 0;
+#if HM_INGEST_TLATE
+        {
+            // unconditional (the row clamped to the last one; a row past n is never used): a conditional load keeps
+            // the old value on the other path, and that register copy waited for every load in flight
+            const int64_t j = i + gstride < n ? i + gstride : n - 1;
+            nla = __builtin_nontemporal_load(&lat[j]);
+            nlo = __builtin_nontemporal_load(&lon[j]);
+            nv = __builtin_nontemporal_load(&vkey[j]);
+            nrv = __builtin_nontemporal_load(   // (no branch: see above; global, not flat: a flat load's wait is a full one)
+                (__attribute__((address_space(1))) const uint8_t *)(row_valid ? &row_valid[j] : &g_one_byte));
+        }
+#else
         if (i + gstride < n) {
             nla = __builtin_nontemporal_load(&lat[i + gstride]);
             nlo = __builtin_nontemporal_load(&lon[i + gstride]);
@@ -1915,6 +1946,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
             nv = __builtin_nontemporal_load(&vkey[i + gstride]);
             if (row_valid) nrv = __builtin_nontemporal_load(&row_valid[i + gstride]);
         }
+#endif
 #else
         double la = 0.0, lo = 0.0;
         int64_t t = 0;
@@ -1928,8 +1960,22 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
             if (row_valid) rv = row_valid[i] != 0;
         }
 #endif
-        const bool ok = in && rv && la >= -90.0 && la <= 90.0 && lo >= -180.0 && lo <= 180.0 &&
-                        t > INT64_MIN + 2 * tile_us && t < INT64_MAX - 2 * tile_us;
+#if HM_INGEST_TLATE
+        // the cell of every row in range, before the ts- and validity-dependent tests (late, invalid or
+        // out-of-range-ts rows waste their cell): nothing loaded this round is waited for before the cell
+        const bool geo0 = in && la >= -90.0 && la <= 90.0 && lo >= -180.0 && lo <= 180.0;
+        bool exc = false;
+        uint64_t cell = EMPTY_CELL;
+#ifdef HM_ABL_NOCELL
+        if (geo0) cell = mix64(__builtin_bit_cast(uint64_t, la) ^ mix64(__builtin_bit_cast(uint64_t, lo)));
+#else
+        if (geo0) exc = !latLngToCellFastP(la, lo, res, c_tab, Fc, Fu, cell, &BT);
+#endif
+        const bool geo = geo0 && rv;
+#else
+        const bool geo = in && rv && la >= -90.0 && la <= 90.0 && lo >= -180.0 && lo <= 180.0;
+#endif
+        const bool ok = geo && t > INT64_MIN + 2 * tile_us && t < INT64_MAX - 2 * tile_us;
         // dedup: the vkey's home slot is loaded now, its latency hidden behind the cell computation (a plain load:
         // a stale copy can only show the slot empty or its max lower, both of which the atomics below correct)
 #ifdef HM_ABL_NODEDUP
@@ -1956,12 +2002,16 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
             }
         }
         // cell of the aggregated rows; margin exceptions go to k_ingest_exact (exact path), which fills their key
+#if HM_INGEST_TLATE
+        exc = exc && (fl & F_AGG) != 0;
+#else
         bool exc = false;
         uint64_t cell = EMPTY_CELL;
 #ifdef HM_ABL_NOCELL   // ablation builds (tools/ablate_ingest.sh): a hash stands in for the cell
         if (fl & F_AGG) cell = mix64(__builtin_bit_cast(uint64_t, la) ^ mix64(__builtin_bit_cast(uint64_t, lo)));
 #else
-        if (fl & F_AGG) exc = !latLngToCellFastP(la, lo, res, c_tab, Fc, Fu, cell);
+        if (fl & F_AGG) exc = !latLngToCellFastP(la, lo, res, c_tab, Fc, Fu, cell, &BT);
+#endif
 #endif
         {
             const unsigned long long pos = wave_append(exc, n_slow);
