@@ -113,14 +113,14 @@ def cpu_baseline(sample, res):
                       f"{dt:.1f} s"}
 
 
-def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank):
+def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, arena_bytes=0):
     """Warmup + exactly K timed steps (barrier + synchronize on both sides, max over ranks); per-stage HIP-event
     times (the library's events on its own stream) and algorithmic bytes of the timed steps."""
     import mobheat
     from mobheat.distributed import LibStages, ShardedHeatmap
     total_steps = args.warmup + args.steps
     data = gen_batch(n, total_steps, seed=seed, dev=dev, span_us=span_us, advance_us=advance_us)
-    eng = mobheat.HeatmapEngine(h3_res=res, device=local, batch_capacity_hint=n)
+    eng = mobheat.HeatmapEngine(h3_res=res, device=local, batch_capacity_hint=n, state_arena_bytes=arena_bytes)
     sharded = ShardedHeatmap(LibStages(eng), dev) if world > 1 else None
 
     def step(s):
@@ -246,7 +246,10 @@ def main():
         # holds 1 minute of event time and the stream advances 1 minute per step, so consecutive batches update the
         # same open windows and the merge reads existing state lines.  res 7 (configs[1]'s resolution): 1e8 events
         # per minute re-touch most of a window's keys from its second batch on.
-        B = run_leg(args, n, 7, 60_000_000, 60_000_000, 2, dev, local, world, rank)
+        # (its windows' tables come from a state arena reserved at create: a new window's multi-GB table allocated by
+        # hipMalloc inside a timed step right after the first leg freed its memory took seconds on some boxes,
+        # profiles/r2/abgl/, profiles/r2/abpfl/ -- ~400 B per event covers the three windows the leg touches)
+        B = run_leg(args, n, 7, 60_000_000, 60_000_000, 2, dev, local, world, rank, arena_bytes=400 * n)
         bms = B["elapsed"] / K * 1e3
         bb = sum(B["kb"].values())
         out["state_read_leg"] = {
