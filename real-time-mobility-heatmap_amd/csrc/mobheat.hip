@@ -1140,9 +1140,6 @@ constexpr int MO_THREADS = HM_MO_THREADS;      // partials per chunk (one per la
 #ifndef HM_MO_COOP_LINES
 #define HM_MO_COOP_LINES 1
 #endif
-#ifndef HM_MO_PF_LATE
-#define HM_MO_PF_LATE 0
-#endif
 constexpr int MO_CLAIM = 2 * MO_THREADS;
 #ifndef HM_MO_TAG_MAX
 #define HM_MO_TAG_MAX 90112
@@ -1520,9 +1517,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             const bool has = i < b1;
             MRec p{};
             if (has) p = mrec_of(nxt, winfo, cell_hi);
-#if !HM_MO_PF_LATE
             if (i + MO_THREADS < b1) nxt = ld_stream(parts + i + MO_THREADS);
-#endif
             if (has) {
                 S.sc[t] = p.cell;
                 S.sh[t] = p.hk;
@@ -1548,12 +1543,6 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             unsigned krow = touch_rows(first);
             if (!first) krow = (unsigned)o.touched;
             if (gslot) v = line_of(p, o, first, krow);
-#if HM_MO_PF_LATE
-            // the next chunk's record, loaded after this chunk's own loads (the probe's tag checks, the old lines):
-            // issued at the chunk's start, every wait of those dependent loads also waited for it (the counter retires
-            // in order); here it overlaps the stores and their drain.  Unconditional (clamped): no register copy.
-            nxt = ld_stream(parts + (i + MO_THREADS < b1 ? i + MO_THREADS : b1 - 1));
-#endif
             // 4. this chunk's stores: the state line (whole) and the key's row
 #ifndef HM_ABL_NOSLOT   // ablation builds only: the state line stores priced by their absence
             {
