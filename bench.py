@@ -241,6 +241,7 @@ def main():
                    "table_mode": c["table_mode"]},
         "roofline": roof,
     }
+    B = None
     if world == 1 and not args.no_state_leg:
         # second leg: the state-read regime of the reference's ~2-s trigger (README.md:134-135) -- each micro-batch
         # holds 1 minute of event time and the stream advances 1 minute per step, so consecutive batches update the
@@ -262,6 +263,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.res)
     if rank == 0:
         print("per-step ms (host wall, rank 0): " + " ".join(f"{x:.1f}" for x in A["step_ms"]), file=sys.stderr, flush=True)
+        if B is not None:
+            print("state-read leg per-step ms: " + " ".join(f"{x:.1f}" for x in B["step_ms"]), file=sys.stderr, flush=True)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
