@@ -247,9 +247,9 @@ def main():
         # holds 1 minute of event time and the stream advances 1 minute per step, so consecutive batches update the
         # same open windows and the merge reads existing state lines.  res 7 (configs[1]'s resolution): 1e8 events
         # per minute re-touch most of a window's keys from its second batch on.
-        # (its windows' tables come from a state arena reserved at create: a new window's multi-GB table allocated by
-        # hipMalloc inside a timed step right after the first leg freed its memory took seconds on some boxes,
-        # profiles/r2/abgl/, profiles/r2/abpfl/ -- ~400 B per event covers the three windows the leg touches)
+        # (its windows' tables come from a state arena reserved at create, ~400 B per event for the three windows the
+        # leg touches, so that no multi-GB table is allocated inside a timed step; the leg's occasional out-of-kernel
+        # stall, DESIGN.md section 7, is not this -- it persisted with the arena)
         B = run_leg(args, n, 7, 60_000_000, 60_000_000, 2, dev, local, world, rank, arena_bytes=400 * n)
         bms = B["elapsed"] / K * 1e3
         bb = sum(B["kb"].values())
