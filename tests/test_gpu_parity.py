@@ -140,6 +140,32 @@ def test_multi_batch_watermark_and_eviction():
     eng.close()
 
 
+def test_state_read_regime_matches_oracle():
+    """The bench's state_read_leg in small: the same points every batch, each batch one minute later, so batches 2-5
+    of a 5-minute window update every existing key (the merge's whole-line loads of existing state, rows rewritten),
+    then a new window.  Dense enough (res 3: 41k cells for 2e5 points) that keys repeat within a batch and chunk."""
+    from mobheat import HeatmapEngine
+    from oracle.spark_oracle import SparkHeatmapOracle
+    rng = np.random.default_rng(29)
+    n = 200_000
+    lat = np.degrees(np.arcsin(rng.uniform(-1.0, 1.0, n)))
+    lon = rng.uniform(-180.0, 180.0, n)
+    base = 1_759_572_000_000_000 + rng.integers(0, 60_000_000, n)
+    speed = rng.uniform(0, 90, n)
+    sv = rng.random(n) > 0.1
+    vkey = rng.integers(0, 5000, n).astype(np.uint64)
+    rv = np.ones(n, bool)
+    eng = HeatmapEngine(h3_res=3)
+    ora = SparkHeatmapOracle(h3_res=3)
+    for epoch in range(7):
+        b = dict(lat=lat, lon=lon, ts_us=base + epoch * 60_000_000, speed=speed, speed_valid=sv, vkey=vkey, row_valid=rv)
+        res, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res, exp)
+        if 0 < epoch < 5:
+            assert eng.last_counts()["state_new"] == 0, "an existing key was created again"
+    eng.close()
+
+
 def test_edge_semantics_batch():
     """Filter edges (+-90/+-180 inclusive, NaN, inf, null rows), window boundaries, negative timestamps,
     null and NaN speeds, duplicate vehicles with tied maxima."""
