@@ -176,8 +176,8 @@ int hm_memcpy(void *dst, const void *src, int64_t bytes, int32_t kind); /* 0 H2D
 int hm_selftest_ld_ops(const double *a, int64_t n, int32_t op, double *out);
 /* floor(t[i] / d) by k_ingest's invariant-divisor multiply (kernels.h FloorDiv), executed on the host */
 int hm_selftest_floor_div(const int64_t *t, int64_t n, int64_t d, int64_t *out);
-/* Host-side execution of the device latLngToCell code path (for debugging without a GPU; uses host libm
- * for the transcendental functions, so it is NOT the device numerics). */
+/* Host-side execution of the device latLngToCell exact path (upstream's sequence with glibc's transcendentals as
+ * restated in csrc/glibc_libm.h: the same numerics as k_ingest_exact / k_cells_exact). */
 int hm_selftest_latlng_to_cell_host(const double *lat, const double *lon, int64_t n, int32_t res,
                                     uint64_t *out);
 /* Host-side execution of the kernels' fast path (latLngToCellFast: direct gnomonic projection with a margin
@@ -185,6 +185,12 @@ int hm_selftest_latlng_to_cell_host(const double *lat, const double *lon, int64_
  * exact path was taken (may be NULL). */
 int hm_selftest_latlng_to_cell_fast_host(const double *lat, const double *lon, int64_t n, int32_t res,
                                          uint64_t *out, uint8_t *fell_back);
+/* glibc 2.35's sincos / acos / atan2 / tan as the exact path restates them (csrc/glibc_libm.h; what the
+ * reference's h3 calls through the host libm, heatmap_stream.py:65-75): fn 0 sincos(a) -> out = sin, out2 = cos;
+ * 1 acos(a); 2 atan2(a, b); 3 tan(a).  _host runs the code on the CPU, _device on GPU `device` (host arrays). */
+int hm_selftest_glibc_libm_host(int32_t fn, const double *a, const double *b, int64_t n, double *out, double *out2);
+int hm_selftest_glibc_libm_device(int32_t fn, const double *a, const double *b, int64_t n, double *out, double *out2,
+                                  int32_t device);
 
 /* Tile-state checkpoint (Spark's state store version after an epoch, heatmap_stream.py:37,244).
  * One record per live (cellId, windowStart) key: the cumulative aggregates the next batches build on.

@@ -80,6 +80,10 @@ static double _posAngleRads(double rads) {
  * 2 cos(lng), 3 sin(lng), 4 acos, 5 sin(dlng), 6 cos(dlng), 7 atan2, 8 tan, 9 cos(theta), 10 sin(theta)
  * (cos/sin of the point's latitude are the same values wherever upstream recomputes them). */
 static __thread int pt_site = -1, pt_ulps = 0;
+/* argument capture (tests only, oracle_latlng_to_cell_args_batch): the arguments of the forward path's glibc calls --
+ * 0 sincos(lat), 1 sincos(lng), 2 acos, 3 sincos(dlng), 4/5 atan2 (y, x), 6 tan, 7 sincos(theta) */
+static __thread double *arg_cap = 0;
+#define CAP(site, x) (arg_cap ? (arg_cap[site] = (x)) : (x))
 static double PT(int site, double x) {
     if (site != pt_site) return x;
     for (int u = 0; u < pt_ulps; u++) x = nextafter(x, INFINITY);
@@ -91,8 +95,8 @@ static double PT(int site, double x) {
  * and glibc's sincos can differ from its sin/cos in the last bit (their FMA variants) */
 static void _geoToVec3d(const LatLng *geo, Vec3d *v) {
     double s, c, sg, cg;
-    sincos(geo->lat, &s, &c);
-    sincos(geo->lng, &sg, &cg);
+    sincos(CAP(0, geo->lat), &s, &c);
+    sincos(CAP(1, geo->lng), &sg, &cg);
     double r = PT(0, c);
     v->z = PT(1, s);
     v->x = PT(2, cg) * r;
@@ -123,10 +127,10 @@ static void _geoToClosestFace(const LatLng *g, int *face, double *sqd) {
 static double _geoAzimuthRads(const LatLng *p1, const LatLng *p2) {
     double s2, c2, s1, c1, sd, cd;
     sincos(p2->lat, &s2, &c2);
-    sincos(p2->lng - p1->lng, &sd, &cd);
+    sincos(CAP(3, p2->lng - p1->lng), &sd, &cd);
     sincos(p1->lat, &s1, &c1);
     c2 = PT(0, c2);
-    return PT(7, atan2(c2 * PT(5, sd), c1 * PT(1, s2) - s1 * c2 * PT(6, cd)));
+    return PT(7, atan2(CAP(4, c2 * PT(5, sd)), CAP(5, c1 * PT(1, s2) - s1 * c2 * PT(6, cd))));
 }
 
 static int isResolutionClassIII(int r) { return r % 2; }
@@ -134,7 +138,7 @@ static int isResolutionClassIII(int r) { return r % 2; }
 static void _geoToHex2d(const LatLng *g, int res, int *face, Vec2d *v) {
     double sqd;
     _geoToClosestFace(g, face, &sqd);
-    double r = PT(4, acos(1 - sqd / 2));
+    double r = PT(4, acos(CAP(2, 1 - sqd / 2)));
     if (r < EPSILON) {
         v->x = v->y = 0.0;
         return;
@@ -142,11 +146,11 @@ static void _geoToHex2d(const LatLng *g, int res, int *face, Vec2d *v) {
     LatLng fc = {H3T_faceCenterGeo[*face][0], H3T_faceCenterGeo[*face][1]};
     double theta = _posAngleRads(H3T_faceAxesAzRadsCII[*face][0] - _posAngleRads(_geoAzimuthRads(&fc, g)));
     if (isResolutionClassIII(res)) theta = _posAngleRads(theta - M_AP7_ROT_RADS);
-    r = PT(8, tan(r));
+    r = PT(8, tan(CAP(6, r)));
     r *= INV_RES0_U_GNOMONIC;
     for (int i = 0; i < res; i++) r *= M_SQRT7;
     double st, ct;
-    sincos(theta, &st, &ct);
+    sincos(CAP(7, theta), &st, &ct);
     v->x = r * PT(9, ct);
     v->y = r * PT(10, st);
 }
@@ -355,6 +359,17 @@ void oracle_latlng_to_cell_batch(const double *lat, const double *lng, int64_t n
     for (int64_t i = 0; i < n; i++) out[i] = oracle_latlng_to_cell(lat[i], lng[i], res);
 }
 
+/* the arguments latLngToCell hands glibc for each point (8 per point, NaN where a call is not reached; see CAP) */
+void oracle_latlng_to_cell_args_batch(const double *lat, const double *lng, int64_t n, int res, double *args) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        for (int k = 0; k < 8; k++) args[8 * i + k] = NAN;
+        arg_cap = args + 8 * i;
+        oracle_latlng_to_cell(lat[i], lng[i], res);
+        arg_cap = 0;
+    }
+}
+
 /* latLngToCell with the result of one transcendental call site moved by `ulps` ulps (see PT): the answers a libm
  * differing from this one in the last bits of that function could give.  An input whose cell changes under such a
  * perturbation is libm-sensitive: h3 itself returns different cells for it on different platforms (glibc's FMA and
@@ -367,6 +382,23 @@ void oracle_latlng_to_cell_perturbed_batch(const double *lat, const double *lng,
         pt_ulps = ulps;
         out[i] = oracle_latlng_to_cell(lat[i], lng[i], res);
         pt_site = -1;
+    }
+}
+
+/* glibc's own sincos / acos / atan2 / tan, called through this process's libm (the reference's h3 calls them so):
+ * the checker of the product's restatement of those routines (csrc/glibc_libm.h).  fn as hm_selftest_glibc_libm_host. */
+void oracle_libm_batch(int fn, const double *a, const double *b, int64_t n, double *out, double *out2) {
+    /* through a pointer: gcc would otherwise fold this sincos() into separate sin() and cos() calls here, and
+     * glibc's (FMA) sin/cos differ from its sincos in the last bit for ~0.1% of arguments */
+    void (*volatile libm_sincos)(double, double *, double *) = sincos;
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        switch (fn) {
+            case 0: libm_sincos(a[i], &out[i], &out2[i]); break;
+            case 1: out[i] = acos(a[i]); break;
+            case 2: out[i] = atan2(a[i], b[i]); break;
+            default: out[i] = tan(a[i]); break;
+        }
     }
 }
 

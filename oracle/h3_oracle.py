@@ -39,6 +39,10 @@ def load():
         L.oracle_cell_to_boundary_batch.argtypes = [P, ctypes.c_int64, P, P, P]
         L.oracle_tables.restype = ctypes.c_int
         L.oracle_tables.argtypes = [P, P, P, ctypes.POINTER(ctypes.c_char_p)]
+        L.oracle_latlng_to_cell_args_batch.restype = None
+        L.oracle_latlng_to_cell_args_batch.argtypes = [P, P, ctypes.c_int64, ctypes.c_int, P]
+        L.oracle_libm_batch.restype = None
+        L.oracle_libm_batch.argtypes = [ctypes.c_int, P, P, ctypes.c_int64, P, P]
         L.oracle_ld_ops.restype = None
         L.oracle_ld_ops.argtypes = [P, ctypes.c_int64, ctypes.c_int, P]
         _lib = L
@@ -53,6 +57,32 @@ def latlng_to_cell(lat, lon, res):
     lon = np.ascontiguousarray(lon, dtype=np.float64)
     out = np.empty(lat.size, dtype=np.uint64)
     L.oracle_latlng_to_cell_batch(lat.ctypes.data, lon.ctypes.data, lat.size, int(res), out.ctypes.data)
+    return out
+
+
+LIBM_FNS = {"sincos": 0, "acos": 1, "atan2": 2, "tan": 3}
+
+
+def libm(fn, a, b=None):
+    """glibc's sincos (-> (sin, cos)), acos, atan2(a, b) or tan of each element, through this process's libm."""
+    L = load()
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = None if b is None else np.ascontiguousarray(b, dtype=np.float64)
+    out = np.empty(a.size)
+    out2 = np.empty(a.size) if fn == "sincos" else None
+    L.oracle_libm_batch(LIBM_FNS[fn], a.ctypes.data, None if b is None else b.ctypes.data, a.size, out.ctypes.data,
+                        None if out2 is None else out2.ctypes.data)
+    return (out, out2) if fn == "sincos" else out
+
+
+def latlng_to_cell_args(lat, lon, res):
+    """The arguments latLngToCell passes to glibc for each point: (n, 8) array -- sincos(lat), sincos(lng), acos,
+    sincos(dlng), atan2 y, atan2 x, tan, sincos(theta); NaN where the call is not reached."""
+    L = load()
+    lat = np.ascontiguousarray(lat, dtype=np.float64)
+    lon = np.ascontiguousarray(lon, dtype=np.float64)
+    out = np.empty((lat.size, 8))
+    L.oracle_latlng_to_cell_args_batch(lat.ctypes.data, lon.ctypes.data, lat.size, int(res), out.ctypes.data)
     return out
 
 

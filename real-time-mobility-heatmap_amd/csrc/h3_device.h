@@ -12,13 +12,16 @@
 //  * every fp64 expression keeps upstream's operation order and is compiled with -ffp-contract=off
 //    (no v_fma_f64 contraction: x86-64 h3 builds have none).
 //  * sin/cos of the face-centre latitudes are precomputed on the host with the same libm the reference
-//    uses (glibc) and uploaded; the per-event sin/cos/acos/atan2/tan use the device math library.
+//    uses (glibc) and uploaded; the exact path's per-event sincos/acos/atan2/tan are glibc 2.35's own routines
+//    restated for the device (glibc_libm.h), so even knife-edge inputs get the glibc-linked reference's bits.
 //
 // Functions are __host__ __device__ so the same code can be executed on the CPU by the self-test entry
 // points (where the transcendental calls resolve to the host libm).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "glibc_libm.h"
 
 #define HM_HD __host__ __device__ __forceinline__
 
@@ -342,6 +345,8 @@ struct H3Tables {
     int faceNeighbors[20][4][5];
     signed char adjacentFaceDir[20][20];
     double edgeY[17];
+    // glibc's sincos/acos/atan2/tan tables (glibc_libm.h): the device copy for c_tab, the host copy for self-tests
+    const glm::Tables *glm;
 };
 
 // the two tables _faceIjkToH3 reads (k_ingest keeps a copy in LDS)
@@ -434,10 +439,11 @@ HM_HD uint64_t latLngToCellDeg(double lat_deg, double lng_deg, int res, const H3
     double glat = XMUL(lat_deg, PI_180);
     double glng = XMUL(lng_deg, PI_180);
     // _geoToVec3d
-    // sincos: the same reduction and polynomials as separate sin and cos (device math library and glibc)
+    // glibc's sincos (gcc fuses upstream's sin/cos pairs; glibc_libm.h)
+    const glm::Tables &G = *T.glm;
     double clat, slat, clng, slng;
-    sincos(glat, &slat, &clat);
-    sincos(glng, &slng, &clng);
+    glm::sincos(glat, slat, clat, G);
+    glm::sincos(glng, slng, clng, G);
     double vz = slat;
     double vx = clng * clat;
     double vy = slng * clat;
@@ -464,26 +470,26 @@ HM_HD uint64_t latLngToCellDeg(double lat_deg, double lng_deg, int res, const H3
         }
     }
     // _geoToHex2d
-    double r = acos(1 - sqd / 2);
+    double r = glm::acos(1 - sqd / 2, G);
     double hx, hy;
     if (xld_lt(r, HM_LD_EPSILON_M, HM_LD_EPSILON_E)) {
         hx = hy = 0.0;
     } else {
         double dlng = glng - T.faceCenterGeo[face][1];
         double sd, cd;
-        sincos(dlng, &sd, &cd);
+        glm::sincos(dlng, sd, cd, G);
         double num = clat * sd;
         double t1 = T.faceCosLat[face] * slat;
         double t2 = T.faceSinLat[face] * clat;
         t2 = t2 * cd;
-        double az = atan2(num, t1 - t2);
+        double az = glm::atan2(num, t1 - t2, G);
         double theta = posAngleRads(T.faceAxesAz0[face] - posAngleRads(az));
         if (res & 1) theta = posAngleRads(XADD(theta, true, AP7_ROT));
-        r = tan(r);
+        r = glm::tan(r, G);
         r *= HM_INV_RES0_U_GNOMONIC;
         for (int i = 0; i < res; i++) r = XMUL(r, SQRT7);
         double st, ct;
-        sincos(theta, &st, &ct);
+        glm::sincos(theta, st, ct, G);
         hx = r * ct;
         hy = r * st;
     }

@@ -5,8 +5,12 @@
 
 #include "h3_device.h"
 
+// glibc's sincos/acos/atan2/tan tables (glibc_libm.inc), host copy (the device copy is mobheat.hip's g_glm)
+static const hm::glm::Tables hm_glm_host = {GLM_TABLE_INIT};
+
 static hm::H3Tables hm_make_tables() {
     hm::H3Tables T;
+    T.glm = &hm_glm_host;
     const long double ap7 = 0.333473172251832115336090755351601070065900389L;   // M_AP7_ROT_RADS
     for (int f = 0; f < 20; f++) {
         T.faceCenterGeo[f][0] = H3T_faceCenterGeo[f][0];

@@ -44,9 +44,20 @@
 using namespace hm;
 
 __constant__ H3Tables c_tab;
+// glibc's sincos/acos/atan2/tan tables for the exact path (glibc_libm.h); c_tab.glm points here
+__device__ const glm::Tables g_glm = {GLM_TABLE_INIT};
 
 #include "h3_tables_host.h"
 static H3Tables make_tables() { return hm_make_tables(); }
+// c_tab of the current device, its glibc table pointer aimed at the device copy
+static hipError_t upload_tables() {
+    H3Tables T = make_tables();
+    void *g = nullptr;
+    hipError_t e = hipGetSymbolAddress(&g, HIP_SYMBOL(g_glm));
+    if (e != hipSuccess) return e;
+    T.glm = (const glm::Tables *)g;
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &T, sizeof(T));
+}
 
 // =====================================================================================================
 // wave helpers
@@ -3456,8 +3467,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     }
     for (auto &e : ctx->ev)
         if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
-    H3Tables T = make_tables();
-    if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &T, sizeof(T)) != hipSuccess) { ctx->err = "tables"; return fail("create"); }
+    if (upload_tables() != hipSuccess) { ctx->err = "tables"; return fail("create"); }
     {
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_ingest, IG_THREADS, 0) != hipSuccess ||
@@ -3709,8 +3719,7 @@ static int udf_begin(int32_t device, UdfState *&S) {   // (g_udf_mu held)
     if (hipSetDevice(device) != hipSuccess) return HM_E_HIP;
     S = &g_udf[device];
     if (!S->ready) {
-        H3Tables T = make_tables();
-        if (hipMemcpyToSymbol(HIP_SYMBOL(c_tab), &T, sizeof(T)) != hipSuccess) return HM_E_HIP;
+        if (upload_tables() != hipSuccess) return HM_E_HIP;
         if (hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) != hipSuccess) return HM_E_HIP;
         S->ready = true;
     }
@@ -4692,6 +4701,60 @@ int hm_selftest_latlng_to_cell_fast_host(const double *lat, const double *lon, i
         if (fell_back) fell_back[i] = !ok;
     }
     return HM_OK;
+}
+
+// glibc's sincos / acos / atan2 / tan as restated in glibc_libm.h (fn 0 sincos: out = sin, out2 = cos; 1 acos(a);
+// 2 atan2(a, b); 3 tan(a)), executed on the host and on the GPU (test entry points; tests/test_glibc_libm.py)
+static int glm_check(int32_t fn, const double *a, const double *b, int64_t n, double *out, double *out2) {
+    if (!a || !out || n < 0 || fn < 0 || fn > 3 || (fn == 0 && !out2) || (fn == 2 && !b)) return HM_E_INVALID;
+    return HM_OK;
+}
+HM_HD void glm_eval(int32_t fn, int64_t i, const double *a, const double *b, double *out, double *out2,
+                    const glm::Tables &G) {
+    switch (fn) {
+        case 0: glm::sincos(a[i], out[i], out2[i], G); break;
+        case 1: out[i] = glm::acos(a[i], G); break;
+        case 2: out[i] = glm::atan2(a[i], b[i], G); break;
+        default: out[i] = glm::tan(a[i], G); break;
+    }
+}
+__global__ __launch_bounds__(256) void k_glibc_libm(int32_t fn, const double *a, const double *b, int64_t n,
+                                                    double *out, double *out2) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        glm_eval(fn, i, a, b, out, out2, g_glm);
+}
+
+int hm_selftest_glibc_libm_host(int32_t fn, const double *a, const double *b, int64_t n, double *out, double *out2) {
+    if (int e = glm_check(fn, a, b, n, out, out2)) return e;
+    for (int64_t i = 0; i < n; i++) glm_eval(fn, i, a, b, out, out2, hm_glm_host);
+    return HM_OK;
+}
+
+int hm_selftest_glibc_libm_device(int32_t fn, const double *a, const double *b, int64_t n, double *out, double *out2,
+                                  int32_t device) {
+    if (int e = glm_check(fn, a, b, n, out, out2)) return e;
+    int ndev = 0;
+    if (device < 0 || hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev || hipSetDevice(device) != hipSuccess)
+        return HM_E_HIP;
+    if (n == 0) return HM_OK;
+    const size_t B = (size_t)n * sizeof(double);
+    double *d[4] = {nullptr, nullptr, nullptr, nullptr};
+    int rc = HM_OK;
+    for (int k = 0; k < 4 && rc == HM_OK; k++)
+        if (hipMalloc((void **)&d[k], B) != hipSuccess) rc = HM_E_NOMEM;
+    if (rc == HM_OK && (hipMemcpy(d[0], a, B, hipMemcpyHostToDevice) != hipSuccess ||
+                        (b && hipMemcpy(d[1], b, B, hipMemcpyHostToDevice) != hipSuccess)))
+        rc = HM_E_HIP;
+    if (rc == HM_OK) {
+        hipLaunchKernelGGL(k_glibc_libm, dim3(grid_for(n, 256)), dim3(256), 0, 0, fn, d[0], d[1], n, d[2], d[3]);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+            hipMemcpy(out, d[2], B, hipMemcpyDeviceToHost) != hipSuccess ||
+            (fn == 0 && hipMemcpy(out2, d[3], B, hipMemcpyDeviceToHost) != hipSuccess))
+            rc = HM_E_HIP;
+    }
+    for (double *p : d)
+        if (p) (void)hipFree(p);
+    return rc;
 }
 
 }  // extern "C"

@@ -104,6 +104,8 @@ SIGNATURES = {
     "hm_selftest_floor_div": (c_i32, [c_vp, c_i64, c_i64, c_vp]),
     "hm_selftest_latlng_to_cell_host": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp]),
     "hm_selftest_latlng_to_cell_fast_host": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "hm_selftest_glibc_libm_host": (c_i32, [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "hm_selftest_glibc_libm_device": (c_i32, [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32]),
     "hm_state_export": (c_i32, [c_vp, _P(HmStateInfo), c_vp, c_i64]),
     "hm_state_import": (c_i32, [c_vp, _P(HmStateInfo), c_vp]),
     "hm_last_windows": (c_i32, [c_vp, c_vp, c_i64, _P(c_i64)]),
@@ -183,13 +185,32 @@ def floor_div_selftest(t, d):
 
 
 def latlng_to_cell_host_selftest(lat, lon, res):
-    """Host execution of the device latLngToCell code (host libm transcendentals) -- debugging aid only."""
+    """Host execution of the device exact latLngToCell path (glibc's routines as restated in glibc_libm.h)."""
     lib = load()
     lat = np.ascontiguousarray(lat, dtype=np.float64)
     lon = np.ascontiguousarray(lon, dtype=np.float64)
     out = np.empty(lat.size, dtype=np.uint64)
     check(lib.hm_selftest_latlng_to_cell_host(ptr(lat), ptr(lon), lat.size, res, ptr(out)))
     return out
+
+
+GLIBC_FNS = {"sincos": 0, "acos": 1, "atan2": 2, "tan": 3}
+
+
+def glibc_libm_selftest(fn, a, b=None, device=None):
+    """glibc's sincos (-> (sin, cos)) / acos / atan2(a, b) / tan as csrc/glibc_libm.h restates them, executed on the
+    host (device=None) or on GPU `device`."""
+    lib = load()
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = None if b is None else np.ascontiguousarray(b, dtype=np.float64)
+    out = np.empty(a.size)
+    out2 = np.empty(a.size) if fn == "sincos" else None
+    args = (GLIBC_FNS[fn], ptr(a), None if b is None else ptr(b), a.size, ptr(out), None if out2 is None else ptr(out2))
+    if device is None:
+        check(lib.hm_selftest_glibc_libm_host(*args))
+    else:
+        check(lib.hm_selftest_glibc_libm_device(*args, int(device)))
+    return (out, out2) if fn == "sincos" else out
 
 
 def latlng_to_cell_fast_host_selftest(lat, lon, res):
