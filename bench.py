@@ -41,30 +41,35 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 # Algorithmic HBM bytes of each stage, from the batch's counts (hm_last_counts): n events, R partial
 # records merged (direct path: one per aggregated row), T tiles emitted, E of them keys that existed before the batch
-# (their 64-B state line is read).
+# (their 64-B state line is read); multi-GPU (stage API): S records this rank sent, R the records it merged as owner.
 #   direct path   ingest 42/event (lat, lon, ts, vkey 8 each + row_valid 1 read; flags 1 + event key 8 written)
 #                 partition 16/event (k_ev_hist and k_ev_scatter read the key) + 65/record (speed, speed_valid,
 #                           lat, lon read: 33; the 32-B EventRec written)
 #                 merge 32/record read + 113/tile (64-B state line + 49-B row written) + 64/pre-existing key read
 #                 emit 98/gap (a 49-B row moved into a gap; gaps = R - T), dedup 20/event
+#   multi-GPU     send (the sender's partition by owner) 16/event + 65/sent record (8-B key + 24-B payload written)
+#                 partition (the owner's) 88/received record: census 8 + histogram 8 read, key 8 + payload 24 read,
+#                           the 32-B EventRec written
 #   table mode    aggregate 41/event + 48/record, partition 160/record (48 + 48 read, 64 written), merge 64/record
 #                 read + 113/tile + 64/pre-existing key
-def stage_bytes(n, c):
+def stage_bytes(n, c, world=1):
     R, T = c["partials"], c["tiles"]
     E = max(T - c["state_new"], 0)
-    b = {"ingest": 42 * n, "dedup": 20 * n, "emit": 98 * max(R - T, 0)}
+    b = {"ingest": 42 * n, "dedup": 20 * n, "emit": 98 * max(R - T, 0), "send": 0}
     if c["table_mode"]:
         b.update(aggregate=41 * n + 48 * R, partition=160 * R, merge=64 * R + 113 * T + 64 * E)
+    elif world > 1:
+        b.update(aggregate=0, send=16 * n + 65 * c["sent"], partition=88 * R, merge=32 * R + 113 * T + 64 * E)
     else:
         b.update(aggregate=0, partition=16 * n + 65 * R, merge=32 * R + 113 * T + 64 * E)
     return b
 
 
-STAGES = ["ingest", "aggregate", "partition", "merge", "emit", "dedup"]
+STAGES = ["ingest", "aggregate", "send", "partition", "merge", "emit", "dedup"]
 # HBM traffic per dispatch of every kernel and k_ingest's VALU instruction mix per event of this workload, counted by
 # rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r2/kernel_pmc.json).
 PMC_FILE = os.path.join(ROOT, "profiles", "r2", "kernel_pmc.json")
-STAGE_KERNELS = {"ingest": ["k_ingest"], "aggregate": ["k_agg", "k_bin_reduce"],
+STAGE_KERNELS = {"ingest": ["k_ingest"], "aggregate": ["k_agg", "k_bin_reduce"], "send": ["k_ev_hist", "k_ev_scatter"],
                  "partition": ["k_ev_hist", "k_ev_scatter"], "merge": ["k_merge_owned"], "emit": ["k_fill_gaps"],
                  "dedup": ["k_dedup_flag"]}
 
@@ -150,7 +155,7 @@ def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, ar
         counts = eng.last_counts()
         for k in STAGES:
             kt[k] += max(tm[k], 0.0)
-        for k, v in stage_bytes(n, counts).items():
+        for k, v in stage_bytes(n, counts, world).items():
             kb[k] += v
     torch.cuda.synchronize()
     if world > 1:
@@ -224,7 +229,7 @@ def main():
                                "fp64_flops_per_event": pmc["fp64_flops_per_event"]}
     step_bytes = sum(kb.values())
     roof.update({"kernel_ms": {k: round(v, 3) for k, v in avg_ms.items()}, "algorithmic_bytes_per_launch": kb[dom],
-                 "units_per_launch": {"events": n, "records": c["partials"], "tiles": c["tiles"]},
+                 "units_per_launch": {"events": n, "records": c["partials"], "tiles": c["tiles"], "sent": c["sent"]},
                  # the whole step: every stage's algorithmic bytes / the step's wall time / 8 TB/s
                  "step": {"algorithmic_bytes": step_bytes, "ms": ms_step,
                           "achieved_gbs": step_bytes / (ms_step * 1e-3) / 1e9,
@@ -238,6 +243,7 @@ def main():
                                f"15 min of event time (3 windows) per step, advancing 15 min per step; H3 res {args.res}",
                    "events_per_step_per_gpu": n, "h3_res": args.res, "parallelism": f"dp{world}",
                    "tiles_emitted_last_step": c["tiles"], "partials_last_step": c["partials"],
+                   "records_sent_last_step": c["sent"],
                    "table_mode": c["table_mode"]},
         "roofline": roof,
     }

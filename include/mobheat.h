@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 8
+#define HM_ABI_VERSION 9
 
 /* error codes */
 #define HM_OK 0
@@ -134,35 +134,50 @@ int hm_latlng_to_cell(const double *lat, const double *lon, int64_t n, int32_t r
 int64_t hm_latlng_to_cell_last_exact(int32_t device);
 
 /* ---- multi-GPU stage API (one context per GPU/rank; the caller performs the exchanges) ----
- * Record layouts (little endian, packed):
- *   tile partial  (48 B): u64 cell, i64 window_start_us, u32 count, u32 n_speed, f64 sum_speed,
- *                         f64 sum_lat, f64 sum_lon  (three 16-B parts; the owner rank and state region are
- *                         functions of (cell, window_start), recomputed by every consumer)
- *   latest cand.  (32 B): u64 vkey, i64 ts_us, i64 row, i64 origin_rank
- * All exchange buffers are caller-owned device memory (e.g. torch tensors handed to RCCL), sized in records.
- * 1. hm_stage_local: snap + filter + window + local pre-aggregation + local latest candidates; both record
- *    kinds are written grouped by owner rank = hash(key) % nranks into the caller's send buffers (capacity
- *    >= in->n records each is always enough) with per-destination counts (host arrays of nranks entries).
- * 2. caller: exchange counts and records (all_to_all), allreduce(max) of batch_max_event_ms.
- * 3. hm_stage_merge: merges the received tile partials into this rank's persistent state, emits the tiles
- *    this rank owns, reduces the received candidates to winners, and writes the winners' row indices grouped
- *    by origin rank into winner_send_buf (capacity >= n_cand_recv) with per-origin counts.
- * 4. caller: exchange winners back; hm_stage_finish takes the received winners (rows of this rank). */
+ * Replaces Spark's shuffle of the groupBy and of the latest-position join (heatmap_stream.py:44,112-133,198-207).
+ * Per micro-batch:
+ * 1. hm_stage_ingest: snap + filter + window + late test + this rank's latest-position max; writes this rank's
+ *    summary (HM_STAGE_SUMMARY_WORDS int64 words, host memory) for the caller to all-gather.
+ * 2. hm_stage_send(all ranks' summaries, [nranks][HM_STAGE_SUMMARY_WORDS], rank-major): every rank derives the
+ *    same batch-wide decisions from them -- the global max event time (the watermark's input, :107), the
+ *    aggregation path and the batch's global window registry -- and writes its records grouped by owner rank
+ *    (a function of the key's hash) into the caller's send buffers, with per-destination counts (host arrays of
+ *    nranks entries):
+ *      direct path (sizes.table_mode == 0): one record per aggregated row, 32 B on the wire, as two streams:
+ *        tile stream    8 B per row: the cell's low 52 bits | (1 + the window's global registry slot) << 52
+ *        payload stream 24 B per row: speed bits (null = 0x7ff0000000000001, NaN canonical), f64 lat, f64 lon
+ *      table mode (sizes.table_mode == 1, low-cardinality batches): the tile stream holds 48-B tile partials,
+ *        one per key of the rank's shard: u64 cell, i64 window_start_us, u32 count, u32 n_speed, f64 sum_speed,
+ *        f64 sum_lat, f64 sum_lon; the payload stream is unused;
+ *      latest candidates, 32 B: u64 vkey, i64 ts_us, i64 row, i64 origin_rank.
+ *    Capacities are in records; tile_send_buf >= 48 B and payload_send_buf >= 24 B per event of the rank's batch,
+ *    cand_send_buf >= 32 B per event are always enough.
+ * 3. caller: all_to_all of the three streams (record counts per destination as returned).
+ * 4. hm_stage_merge: the owner merges the received tile records into the persistent state it owns, emits the
+ *    tiles it owns, reduces the received candidates to winners, and writes the winners' row indices grouped by
+ *    origin rank into winner_send_buf (capacity >= n_cand_recv) with per-origin counts.
+ * 5. caller: exchange winners back; hm_stage_finish takes the received winners (rows of this rank). */
+#define HM_STAGE_SUMMARY_WORDS 8200
 #define HM_TILE_REC_BYTES 48
+#define HM_TILE_KEY_BYTES 8
+#define HM_TILE_PAYLOAD_BYTES 24
 #define HM_CAND_REC_BYTES 32
 typedef struct hm_stage_sizes {
-    int64_t n_tile_partials;      /* total tile partial records produced locally */
-    int64_t n_cands;              /* total latest candidates produced locally */
-    int64_t batch_max_event_ms;   /* local max, to be allreduced by the caller */
-    int64_t n_valid, n_late;
+    int64_t table_mode;                  /* the batch's aggregation path (the same on every rank) */
+    int64_t n_tile_records;              /* tile records this rank sent */
+    int64_t n_cands;                     /* latest candidates this rank sent */
+    int64_t global_batch_max_event_ms;   /* max over all ranks */
+    int64_t n_valid, n_late;             /* this rank's rows */
 } hm_stage_sizes;
 
-int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t nranks, int32_t rank,
-                   void *tile_send_buf, int64_t tile_send_cap, int64_t *tile_send_counts,
-                   void *cand_send_buf, int64_t cand_send_cap, int64_t *cand_send_counts, hm_stage_sizes *sizes);
-int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, const void *cand_recv_dev,
-                   int64_t n_cand_recv, int64_t global_batch_max_event_ms, int32_t out_memory,
-                   hm_batch_out *out, void *winner_send_buf, int64_t winner_send_cap, int64_t *winner_send_counts);
+int hm_stage_ingest(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t nranks, int32_t rank,
+                    int64_t *summary);
+int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *tile_send_buf, void *payload_send_buf,
+                  int64_t tile_send_cap, int64_t *tile_send_counts, void *cand_send_buf, int64_t cand_send_cap,
+                  int64_t *cand_send_counts, hm_stage_sizes *sizes);
+int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, const void *payload_recv_dev, int64_t n_tile_recv,
+                   const void *cand_recv_dev, int64_t n_cand_recv, int32_t out_memory, hm_batch_out *out,
+                   void *winner_send_buf, int64_t winner_send_cap, int64_t *winner_send_counts);
 int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_recv, int32_t out_memory,
                     hm_batch_out *out);
 
@@ -280,9 +295,10 @@ int hm_selftest_position_statements(const hm_position_doc_cfg *cfg, const uint64
                                     const double *lat, const double *lon, int64_t n, uint8_t *bytes, int64_t cap,
                                     int64_t *offsets);
 
-/* Timing of the last hm_process_batch / stage call on the library's stream (HIP events), milliseconds
- * per phase: index 0 ingest (k_ingest: filter + cells + windows + pre-aggregation + dedup max), 1 reserved
- * (0), 2 merge, 3 emit, 4 dedup (flag + compaction), 5 total, 6 region partition. */
+/* Timing of the last hm_process_batch / stage batch on the library's stream (HIP events), milliseconds
+ * per phase: index 0 ingest (k_ingest: filter + cells + windows + event keys + latest max), 1 table-mode
+ * aggregation (k_agg + k_bin_reduce), 2 merge, 3 emit, 4 dedup (flag + compaction), 5 total, 6 (window, region)
+ * partition, 7 stage API: the sender's partition by owner rank. */
 int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n);
 
 /* ---- Kafka message values -> batch columns (reference heatmap_stream.py:51-61, 88-93) ----
@@ -336,9 +352,10 @@ int hm_cells_to_boundary(const uint64_t *cells, int64_t n, int32_t memory, int32
 /* Host execution of the same device code (no GPU; the CPU tests compare it with the oracle). */
 int hm_selftest_cells_to_boundary_host(const uint64_t *cells, int64_t n, double *lat, double *lng, int32_t *nverts);
 
-/* Counts of the last hm_process_batch (up to n of them): [0] keys created in the tile state, [1] partial records
- * merged (direct path: aggregated rows; table mode: ~ distinct keys), [2] tiles emitted, [3] 1 if table mode ran,
- * [4] table mode: aggregates evicted from k_agg's LDS tables into its buckets. */
+/* Counts of the last hm_process_batch / stage batch (up to n of them): [0] keys created in the tile state, [1] partial
+ * records merged (direct path: aggregated rows; table mode: ~ distinct keys; stage API: the records this rank
+ * received as owner), [2] tiles emitted, [3] 1 if table mode ran, [4] table mode: aggregates evicted from k_agg's
+ * LDS tables into its buckets, [5] stage API: tile records this rank sent. */
 int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n);
 
 /* HM_ABI_VERSION the library was built with (callers check it before hm_create). */

@@ -99,7 +99,8 @@ struct alignas(32) WInfo {
     unsigned long long wenc;   // window start ^ 2^63
     uint64_t inner;            // mix64(windowStart + golden): tile_hash(cell, ws) = mix64(cell ^ inner)
     unsigned binp;             // radix bin parameters: (REGION_BITS - rbits) << 24 | (window salt & smask)
-    unsigned pad[3];
+    unsigned gslot;            // multi-GPU sender: the window's slot in the batch's global registry
+    unsigned pad[2];
 };
 static_assert(sizeof(WInfo) == 32, "WInfo is 32 B");
 // A direct-mapped image of the batch's WInfo entries (slot & (WI_CACHE - 1)), built by the host next to the per-slot

@@ -660,20 +660,34 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_hist(const uint64_t *__restri
     for (int d = threadIdx.x; d <= nbins; d += EV_THREADS) H[(int64_t)d * ntiles + blockIdx.x] = h[d];
 }
 
+// the direct path's multi-GPU wire format (hm_stage_send): a key stream (8 B per row: the cell's low 52 bits | 1 + the
+// batch's GLOBAL window slot << 52) and a payload stream (24 B: speed bits as in EventRec, lat, lon), both grouped by
+// owner rank; the owner partitions them into EventRecs (k_ev_scatter with payload_in)
+struct WireKey {
+    uint64_t key;
+};
+constexpr int WIRE_PAYLOAD_WORDS = 3;
+
 // Per wave and round, 64 rows: each lane takes its row's digit and position (LDS cursor) and builds its record in
 // LDS; then the wave writes the 64 records as rounds of 16-B parts, consecutive lanes covering consecutive parts of
-// one record (whole 32-B sectors / 48-B records at random places).  Out = EventRec (the direct path) or TilePartial
-// (the owner partition of hm_stage_local: count 1, window start from the registry).
+// one record (whole 32-B sectors at random places).
+//   Out = EventRec: the direct path's (window, region) bins; the row's speed/lat/lon come from the batch's columns,
+//         or (payload_in, the multi-GPU owner) from the received payload stream;
+//   Out = WireKey:  grouped by owner rank into the caller's key and payload streams (payload_out), the key's window
+//         slot rewritten from the rank's registry to the batch's global registry (WInfo.gslot).
 template <typename Out>
 __global__ __launch_bounds__(EV_THREADS) void k_ev_scatter(const uint64_t *__restrict__ keys, int64_t n, int64_t tile,
                                                           const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
                                                           const double *__restrict__ lat, const double *__restrict__ lon,
+                                                          const uint64_t *__restrict__ payload_in,
                                                           const WInfo *__restrict__ winfo, uint64_t cell_hi, int nranks, int nbins,
                                                           const unsigned long long *__restrict__ O, int64_t ntiles,
-                                                          Out *__restrict__ dst) {
-    constexpr int QO = sizeof(Out) / 16;
+                                                          Out *__restrict__ dst, uint64_t *__restrict__ payload_out) {
+    constexpr bool wire = std::is_same<Out, WireKey>::value;
+    static_assert(wire || std::is_same<Out, EventRec>::value, "k_ev_scatter output");
+    constexpr int QO = wire ? 1 : sizeof(Out) / 16;
     __shared__ unsigned cur[RP_BINS];   // positions < 2^32 - 1 (hm_process_batch checks n)
-    __shared__ uint4 stage[(EV_THREADS / 64) * 64 * QO];
+    __shared__ uint4 stage[wire ? 1 : (EV_THREADS / 64) * 64 * QO];
     __shared__ WiCacheL WI;
     for (int d = threadIdx.x; d < nbins; d += EV_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
     wi_load(WI, winfo);
@@ -681,18 +695,26 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_scatter(const uint64_t *__res
     const int64_t t0 = (int64_t)blockIdx.x * tile;
     const int64_t t1 = t0 + tile < n ? t0 + tile : n;
     uint4 *__restrict__ d4 = (uint4 *)dst;
-    uint4 *ws = stage + (threadIdx.x >> 6) * 64 * QO;
+    uint4 *ws = stage + (wire ? 0 : (threadIdx.x >> 6) * 64 * QO);
     const int ln = lane_id();
-    // a row's columns, loaded one round ahead (every load of a round is issued before the first is used)
-    struct Row { uint64_t k; double sp, la, lo; uint8_t sv; };
+    // a row's columns, loaded one round ahead (every load of a round is issued before the first is used); sv = 2:
+    // the speed word is already encoded (payload stream)
+    struct Row { uint64_t k, sp; double la, lo; uint8_t sv; };
     auto load = [&](int64_t i) {
-        Row r{0, 0.0, 0.0, 0.0, 0};
+        Row r{0, 0, 0.0, 0.0, 0};
         if (i < t1) {
             r.k = __builtin_nontemporal_load(&keys[i]);
-            r.sp = speed ? __builtin_nontemporal_load(&speed[i]) : 0.0;
-            r.sv = speed ? (speed_valid ? __builtin_nontemporal_load(&speed_valid[i]) : (uint8_t)1) : (uint8_t)0;
-            r.la = __builtin_nontemporal_load(&lat[i]);
-            r.lo = __builtin_nontemporal_load(&lon[i]);
+            if (payload_in) {
+                r.sp = __builtin_nontemporal_load(&payload_in[i * WIRE_PAYLOAD_WORDS]);
+                r.la = __builtin_bit_cast(double, __builtin_nontemporal_load(&payload_in[i * WIRE_PAYLOAD_WORDS + 1]));
+                r.lo = __builtin_bit_cast(double, __builtin_nontemporal_load(&payload_in[i * WIRE_PAYLOAD_WORDS + 2]));
+                r.sv = 2;
+            } else {
+                r.sp = speed ? __builtin_bit_cast(uint64_t, __builtin_nontemporal_load(&speed[i])) : 0;
+                r.sv = speed ? (speed_valid ? __builtin_nontemporal_load(&speed_valid[i]) : (uint8_t)1) : (uint8_t)0;
+                r.la = __builtin_nontemporal_load(&lat[i]);
+                r.lo = __builtin_nontemporal_load(&lon[i]);
+            }
         }
         return r;
     };
@@ -709,30 +731,54 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_scatter(const uint64_t *__res
             const uint64_t cell = (k & CELL_LO) | cell_hi;
             const uint64_t hh = mix64(cell ^ wi.inner);
             pos = atomicAdd(&cur[ev_digit(hh, wi.binp, nranks)], 1u);
-            const bool sv = r.sv != 0;
-            const double sp = sv ? r.sp : 0.0;
+            const double sp = __builtin_bit_cast(double, r.sp);
+            const uint64_t spb = r.sv == 2 ? r.sp : r.sv == 0 ? SPEED_NULL_BITS : sp != sp ? CANON_NAN_BITS : r.sp;
             const uint64_t lab = __builtin_bit_cast(uint64_t, r.la), lob = __builtin_bit_cast(uint64_t, r.lo);
-            if constexpr (std::is_same<Out, EventRec>::value) {
-                const uint64_t spb = !sv ? SPEED_NULL_BITS : sp != sp ? CANON_NAN_BITS : __builtin_bit_cast(uint64_t, sp);
+            if constexpr (wire) {
+                // few digits (owner ranks): a wave's rows land in a few contiguous runs, written lane by lane
+                dst[pos].key = ekey_make(k, wi.gslot);
+                payload_out[(int64_t)pos * WIRE_PAYLOAD_WORDS + 0] = spb;
+                payload_out[(int64_t)pos * WIRE_PAYLOAD_WORDS + 1] = lab;
+                payload_out[(int64_t)pos * WIRE_PAYLOAD_WORDS + 2] = lob;
+            } else {
                 ws[ln * 2 + 0] = make_uint4((unsigned)k, (unsigned)(k >> 32), (unsigned)spb, (unsigned)(spb >> 32));
                 ws[ln * 2 + 1] = make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32));
-            } else {
-                static_assert(std::is_same<Out, TilePartial>::value, "k_ev_scatter output");
-                const uint64_t w = (uint64_t)wdec(wi.wenc), spb = __builtin_bit_cast(uint64_t, sp);
-                ws[ln * 3 + 0] = make_uint4((unsigned)cell, (unsigned)(cell >> 32), (unsigned)w, (unsigned)(w >> 32));
-                ws[ln * 3 + 1] = make_uint4(1u, sv ? 1u : 0u, (unsigned)spb, (unsigned)(spb >> 32));
-                ws[ln * 3 + 2] = make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32));
             }
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        for (int q = 0; q < QO; q++) {
-            const int idx = q * 64 + ln, rec = idx / QO, part = idx % QO;
-            const unsigned p = __shfl(pos, rec, 64);
-            if (p != ~0u) d4[(int64_t)p * QO + part] = ws[idx];
+        if constexpr (!wire) {
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            for (int q = 0; q < QO; q++) {
+                const int idx = q * 64 + ln, rec = idx / QO, part = idx % QO;
+                const unsigned p = __shfl(pos, rec, 64);
+                if (p != ~0u) d4[(int64_t)p * QO + part] = ws[idx];
+            }
+            __builtin_amdgcn_wave_barrier();
         }
-        __builtin_amdgcn_wave_barrier();
     }
+}
+
+// the multi-GPU owner's census: received direct-path records per global window slot (sizes the window tables)
+struct SlotSink {
+    unsigned long long *cnt;   // WREG_SLOTS counters
+    __device__ bool add(unsigned long long id, unsigned long long c) const {
+        atomicAdd(&cnt[id - 1], c);
+        return true;
+    }
+};
+__global__ __launch_bounds__(256) void k_key_census(const uint64_t *__restrict__ keys, int64_t n, unsigned long long *cnt) {
+    __shared__ WinLds WL;
+    wl_init(WL);
+    __syncthreads();
+    const SlotSink sink{cnt};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+        const int64_t i = base + threadIdx.x;
+        const uint64_t k = i < n ? __builtin_nontemporal_load(&keys[i]) : 0;
+        wave_count_windows(k != 0, (unsigned long long)ekey_widx(k) + 1, 1ull, WL, sink);
+    }
+    __syncthreads();
+    wl_flush(WL, sink);
 }
 
 // =====================================================================================================
@@ -2483,13 +2529,21 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+struct Inputs {   // a batch's device columns
+    const double *lat, *lon, *sp;
+    const int64_t *ts;
+    const uint8_t *sv, *rv;
+    const uint64_t *vk;
+    int64_t n;
+};
+
 struct hm_ctx {
     hm_config cfg;
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    hipEvent_t ev[8] = {};
-    double timings[7] = {0, 0, 0, 0, 0, 0, 0};
+    hipEvent_t ev[11] = {};
+    double timings[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // per-event
     DevBuf in_lat, in_lon, in_ts, in_speed, in_sv, in_vkey, in_rv;
     DevBuf cell, wstart, flags, win, rows, block_counts, block_offs;
@@ -2539,7 +2593,7 @@ struct hm_ctx {
     int merge_grid = 0;
     int64_t prev_agg_rows = 0, prev_keys = 0;   // aggregated rows and distinct keys of the last batch
     bool last_table = false;
-    int64_t last_counts[5] = {0, 0, 0, 0, 0};   // hm_last_counts
+    int64_t last_counts[6] = {0, 0, 0, 0, 0, 0};   // hm_last_counts
     int64_t table_evicted = 0;                   // table mode: aggregates k_agg evicted into its buckets (last batch)
     // hm_decode_json (row f1): the values on the device, the decoded columns, the string dictionaries
     struct Dict {
@@ -2583,12 +2637,20 @@ struct hm_ctx {
     DevBuf td_sizes, td_off, td_btot, td_boff, td_bytes, td_params;
     void *h_td_bytes = nullptr, *h_td_off = nullptr;
     size_t h_td_bytes_cap = 0, h_td_off_cap = 0;
-    // stage API state
+    // stage API state (hm_stage_ingest -> hm_stage_send -> hm_stage_merge -> hm_stage_finish)
     int stage = 0;
+    bool staged = false;                               // the last batch ran through the stage API
     int nranks = 1, rank = 0;
     int64_t stage_n_in = 0;
     int64_t stage_agg_rows = 0;
     hm_stage_sizes stage_sizes{};
+    Inputs stage_I{};                                  // the batch's device columns (valid until hm_stage_send)
+    DevStats stage_s1{};                               // this rank's ingest statistics
+    bool stage_table = false;                          // the batch's aggregation path (the same on every rank)
+    int64_t stage_gmax_ms = INT64_MIN;                 // the batch's max event time over all ranks
+    int64_t stage_sent = 0;                            // tile records this rank sent
+    std::vector<unsigned long long> stage_gwreg;       // the batch's global window registry (WREG_SLOTS wenc)
+    std::vector<unsigned> stage_gslot;                 // this rank's registry slot -> global slot
 };
 
 static std::string g_create_err;
@@ -2776,14 +2838,6 @@ static int gens_upload(hm_ctx *ctx) {
     return HM_OK;
 }
 
-struct Inputs {   // a batch's device columns
-    const double *lat, *lon, *sp;
-    const int64_t *ts;
-    const uint8_t *sv, *rv;
-    const uint64_t *vk;
-    int64_t n;
-};
-
 // exclusive scan of the m = (nbins + 1) x ntiles tile histogram rp_H into rp_O (digit-major)
 // exclusive scan of m u32 counts `in` into u64 offsets `out`
 static int scan_counts(hm_ctx *ctx, const unsigned *in, int64_t m, unsigned long long *out) {
@@ -2825,12 +2879,13 @@ static int partition(hm_ctx *ctx, const In *parts, int64_t n, int64_t &ntiles, i
     return HM_OK;
 }
 
-// the direct path's partition: the batch's n event keys -> EventRecs in (window, region) bins (parts_sorted), or
-// with nranks > 0 TilePartials grouped by owner rank into dst; rows without a key fall into digit nbins (dropped)
+// the direct path's partition: n event keys with the batch's columns (I) or, on a multi-GPU owner, the received payload
+// stream -> EventRecs in (window, region) bins (parts_sorted); or with nranks > 0 the wire streams grouped by owner rank
+// (dst = key stream, payload_out); rows without a key fall into digit nbins (dropped)
 template <typename Out>
-static int ev_partition(hm_ctx *ctx, const Inputs &I, int64_t &ntiles, int nranks = 0, Out *dst = nullptr) {
+static int ev_partition(hm_ctx *ctx, const uint64_t *keys, int64_t n, const Inputs *I, const uint64_t *payload_in,
+                        int64_t &ntiles, int nranks = 0, Out *dst = nullptr, uint64_t *payload_out = nullptr) {
     const int nbins = nranks > 0 ? nranks : RP_BINS;
-    const int64_t n = I.n;
     const int64_t tile = rp_tile_for(n);
     ntiles = std::max<int64_t>((n + tile - 1) / tile, 1);
     const int64_t m = (int64_t)(nbins + 1) * ntiles;
@@ -2838,12 +2893,13 @@ static int ev_partition(hm_ctx *ctx, const Inputs &I, int64_t &ntiles, int nrank
     if (!dst && (rc = ensure(ctx, ctx->parts_sorted, std::max<int64_t>(n, 1) * sizeof(Out)))) return rc;
     if ((rc = ensure(ctx, ctx->rp_H, m * 4)) || (rc = ensure(ctx, ctx->rp_O, m * 8))) return rc;
     const uint64_t ch = cell_hi_of(ctx->cfg.h3_res);
-    hipLaunchKernelGGL(k_ev_hist, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, (const uint64_t *)ctx->keys.p, n, tile,
-                       (const WInfo *)ctx->d_winfo, ch, nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles);
+    hipLaunchKernelGGL(k_ev_hist, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, (const WInfo *)ctx->d_winfo, ch,
+                       nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles);
     if ((rc = rp_scan(ctx, m))) return rc;
-    hipLaunchKernelGGL(k_ev_scatter<Out>, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, (const uint64_t *)ctx->keys.p, n, tile,
-                       I.sp, I.sv, I.lat, I.lon, (const WInfo *)ctx->d_winfo, ch, nranks, nbins,
-                       (const unsigned long long *)ctx->rp_O.p, ntiles, dst ? dst : (Out *)ctx->parts_sorted.p);
+    hipLaunchKernelGGL(k_ev_scatter<Out>, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, I ? I->sp : nullptr,
+                       I ? I->sv : nullptr, I ? I->lat : nullptr, I ? I->lon : nullptr, payload_in, (const WInfo *)ctx->d_winfo,
+                       ch, nranks, nbins, (const unsigned long long *)ctx->rp_O.p, ntiles, dst ? dst : (Out *)ctx->parts_sorted.p,
+                       payload_out);
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
 }
@@ -2928,6 +2984,7 @@ static int winfo_upload(hm_ctx *ctx, bool with_bins) {
         memset(&x, 0, sizeof x);
         x.wenc = we;
         x.inner = window_inner(wdec(we));
+        x.gslot = ctx->stage_gslot.empty() ? (unsigned)w : ctx->stage_gslot[w];
         if (with_bins) {
             unsigned rbits = 0;
             bool found = false;
@@ -3330,7 +3387,7 @@ static int merge_events(hm_ctx *ctx, const Inputs &I, int64_t n_rec) {
     if ((rc = gens_prepare(ctx, census)) || (rc = winfo_upload(ctx, true))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
     int64_t ntiles;
-    if ((rc = ev_partition<EventRec>(ctx, I, ntiles))) return rc;
+    if ((rc = ev_partition<EventRec>(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, nullptr, ntiles))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
     if ((rc = merge_sorted<EventRec>(ctx, I.n, ntiles))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
@@ -3420,13 +3477,14 @@ static void record_timings(hm_ctx *ctx) {
     float t;
     auto el = [&](int a, int b) -> double { return hipEventElapsedTime(&t, ctx->ev[a], ctx->ev[b]) == hipSuccess ? t : -1.0; };
     ctx->timings[0] = el(0, 1);
-    ctx->timings[1] = el(1, 2);
+    ctx->timings[1] = ctx->staged ? el(10, 2) : el(1, 2);   // (stage API: table mode runs in hm_stage_send)
     ctx->timings[2] = el(3, 4);
     ctx->timings[3] = el(4, 5);
     ctx->timings[4] = el(5, 6);
     ctx->timings[5] = el(0, 6);
     ctx->timings[2] = el(7, 4);   // merge proper
     ctx->timings[6] = el(3, 7);   // partition by table region
+    ctx->timings[7] = el(8, 9);   // multi-GPU sender: partition by owner rank
     (void)hipGetLastError();      // (an event a path did not record: its timing reads -1, no sticky error)
 }
 
@@ -3617,13 +3675,13 @@ const char *hm_last_error(const hm_ctx *ctx) { return ctx ? ctx->err.c_str() : g
 
 int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n) {
     if (!ctx || !ms) return HM_E_INVALID;
-    for (int i = 0; i < n && i < 7; i++) ms[i] = ctx->timings[i];
+    for (int i = 0; i < n && i < 8; i++) ms[i] = ctx->timings[i];
     return HM_OK;
 }
 
 int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n) {
     if (!ctx || !c) return HM_E_INVALID;
-    for (int i = 0; i < n && i < 5; i++) c[i] = ctx->last_counts[i];
+    for (int i = 0; i < n && i < 6; i++) c[i] = ctx->last_counts[i];
     return HM_OK;
 }
 
@@ -3636,6 +3694,8 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     memset(out, 0, sizeof(*out));
     ctx->epoch = epoch_id;
     ctx->last_n_latest = -1;
+    ctx->staged = false;
+    ctx->stage = 0;
     int rc;
     // 1. evict with this batch's eviction watermark happened at the end of the previous batch (see below)
     int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
@@ -3681,6 +3741,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     ctx->last_counts[2] = (int64_t)s2.n_touched;
     ctx->last_counts[3] = table ? 1 : 0;
     ctx->last_counts[4] = table ? ctx->table_evicted : 0;
+    ctx->last_counts[5] = 0;
     // the next batch's aggregation path is chosen from this one's cardinality
     if (n_agg >= (int64_t(1) << 16)) {
         ctx->prev_agg_rows = n_agg;
@@ -3819,32 +3880,120 @@ int hm_selftest_cells_to_boundary_host(const uint64_t *cells, int64_t n, double 
 }
 
 // ---- multi-GPU stage API ----
-int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t nranks, int32_t rank, void *tile_send_buf,
-                   int64_t tile_send_cap, int64_t *tile_send_counts, void *cand_send_buf, int64_t cand_send_cap,
-                   int64_t *cand_send_counts, hm_stage_sizes *sizes) {
-    if (!ctx || !in || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks || !tile_send_counts || !cand_send_counts ||
-        (in->n > 0 && (!tile_send_buf || !cand_send_buf)))
+// summary words of one rank (HM_STAGE_SUMMARY_WORDS int64, all-gathered by the caller between ingest and send)
+enum : int {
+    SW_N_IN = 0, SW_VALID, SW_LATE, SW_AGG, SW_MAX_MS, SW_SAMPLE_RUN, SW_PREV_AGG, SW_PREV_KEYS, SW_NWIN, SW_RESERVED,
+    SW_WIN0   // then n_windows pairs (registry slot, wenc)
+};
+static_assert(SW_WIN0 + 2 * WREG_SLOTS <= HM_STAGE_SUMMARY_WORDS, "summary layout");
+
+int hm_stage_ingest(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t nranks, int32_t rank, int64_t *summary) {
+    if (!ctx || !in || !summary || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks)
         return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
-    if (in->n > (int64_t)UINT32_MAX) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds 2^32-1", (long long)in->n);
+    if (in->n > (int64_t)UINT32_MAX - 1) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds 2^32-2", (long long)in->n);
     if (in->n > 0 && (!in->lat || !in->lon || !in->ts_us || !in->vkey))
         return set_err(ctx, HM_E_INVALID, "lat, lon, ts_us and vkey are required");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc;
+    ctx->stage = 0;
     ctx->epoch = epoch_id;
     ctx->last_n_latest = -1;   // (hm_encode_position_updates: single-context batches only)
     ctx->nranks = nranks;
     ctx->rank = rank;
-    int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
+    const int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
     Inputs I;
     I.n = in->n;
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
     if ((rc = phase_local(ctx, I, late_wm))) return rc;
     const DevStats s1 = *ctx->h_st;
+    ctx->stage_I = I;
+    ctx->stage_s1 = s1;
+    ctx->staged = true;
+    memset(summary, 0, HM_STAGE_SUMMARY_WORDS * sizeof(int64_t));
+    summary[SW_N_IN] = I.n;
+    summary[SW_VALID] = (int64_t)s1.n_valid;
+    summary[SW_LATE] = (int64_t)s1.n_late;
+    summary[SW_AGG] = (int64_t)s1.n_valid - (int64_t)s1.n_late;
+    summary[SW_MAX_MS] = s1.max_ts_ms;
+    summary[SW_SAMPLE_RUN] = (int64_t)s1.sample_max_run;
+    summary[SW_PREV_AGG] = ctx->prev_agg_rows;
+    summary[SW_PREV_KEYS] = ctx->prev_keys;
+    int64_t nw = 0;
+    for (int w = 0; w < WREG_SLOTS; w++)
+        if (ctx->h_wreg[w] && ctx->h_wcount[w]) {
+            summary[SW_WIN0 + 2 * nw] = w;
+            summary[SW_WIN0 + 2 * nw + 1] = (int64_t)ctx->h_wreg[w];
+            nw++;
+        }
+    summary[SW_NWIN] = nw;
+    ctx->stage_n_in = I.n;
+    ctx->stage = 1;
+    return HM_OK;
+}
+
+// The batch-wide decisions every rank derives identically from all ranks' summaries: the global max event time (the
+// watermark's input), the aggregation path, and the global window registry (k_ingest's hashing -- slot wq mod
+// WREG_SLOTS, linear probing -- over the union of the ranks' windows in ascending order).
+static int stage_decide(hm_ctx *ctx, const int64_t *sums) {
+    const int W = ctx->nranks;
+    int64_t gmax = INT64_MIN, min_agg = INT64_MAX, prev_agg = 0, prev_keys = 0;
+    unsigned long long max_run = 0;
+    std::vector<unsigned long long> wins;
+    for (int r = 0; r < W; r++) {
+        const int64_t *S = sums + (size_t)r * HM_STAGE_SUMMARY_WORDS;
+        gmax = std::max(gmax, S[SW_MAX_MS]);
+        min_agg = std::min(min_agg, S[SW_AGG]);
+        max_run = std::max(max_run, (unsigned long long)S[SW_SAMPLE_RUN]);
+        prev_agg += S[SW_PREV_AGG];
+        prev_keys += S[SW_PREV_KEYS];
+        if (S[SW_NWIN] < 0 || S[SW_NWIN] > WREG_SLOTS) return set_err(ctx, HM_E_INVALID, "summary of rank %d is malformed", r);
+        for (int64_t k = 0; k < S[SW_NWIN]; k++) wins.push_back((unsigned long long)S[SW_WIN0 + 2 * k + 1]);
+    }
+    std::sort(wins.begin(), wins.end());
+    wins.erase(std::unique(wins.begin(), wins.end()), wins.end());
+    ctx->stage_gwreg.assign(WREG_SLOTS, 0ull);
+    for (unsigned long long we : wins) {
+        const int64_t wq = wdec(we) / ctx->cfg.tile_us;   // (window starts are multiples of tile_us)
+        unsigned h = (unsigned)((uint64_t)wq % (uint64_t)WREG_SLOTS);
+        int p = 0;
+        for (; p < WREG_SLOTS && ctx->stage_gwreg[h]; p++) h = h + 1 == (unsigned)WREG_SLOTS ? 0u : h + 1;
+        if (p == WREG_SLOTS)
+            return set_err(ctx, HM_E_OVERFLOW, "more than %d distinct windows in one micro-batch over all ranks", WREG_SLOTS);
+        ctx->stage_gwreg[h] = we;
+    }
+    ctx->stage_gmax_ms = gmax;
+    // aggregation path: the single-context rule (choose_table) on batch-wide numbers -- table mode when a rank's key
+    // sample shows heavy hitters, or when the last batch's keys were few and repeated a lot on every rank
+    bool table;
+    if (ctx->ingest_mode) table = ctx->ingest_mode == 2;
+    else if (min_agg < (int64_t(1) << 16)) table = false;
+    else if (max_run >= (unsigned long long)(HS_SAMPLE / 256)) table = true;
+    else table = prev_keys > 0 && prev_keys <= (int64_t)AG_BINS * (AG_SLOTS / 2) && prev_agg >= 8 * (int64_t)W * prev_keys;
+    ctx->stage_table = table;
+    return HM_OK;
+}
+
+int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *tile_send_buf, void *payload_send_buf, int64_t tile_send_cap,
+                  int64_t *tile_send_counts, void *cand_send_buf, int64_t cand_send_cap, int64_t *cand_send_counts,
+                  hm_stage_sizes *sizes) {
+    if (!ctx || !summaries || !tile_send_counts || !cand_send_counts)
+        return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->stage != 1) return set_err(ctx, HM_E_STATE, "hm_stage_send before hm_stage_ingest");
+    const Inputs &I = ctx->stage_I;
+    if (I.n > 0 && (!tile_send_buf || !payload_send_buf || !cand_send_buf))
+        return set_err(ctx, HM_E_INVALID, "send buffers are required");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc;
+    const int W = ctx->nranks;
+    if (summaries[(size_t)ctx->rank * HM_STAGE_SUMMARY_WORDS + SW_N_IN] != I.n)
+        return set_err(ctx, HM_E_INVALID, "summaries[rank] is not this rank's summary");
+    if ((rc = stage_decide(ctx, summaries))) return rc;
+    const DevStats &s1 = ctx->stage_s1;
     const int64_t n_agg = (int64_t)s1.n_valid - (int64_t)s1.n_late;
-    // tile partials: table mode aggregates the shard first (one record per key); the direct path sends every row
-    const bool table = choose_table(ctx, n_agg, s1.sample_max_run);
+    const bool table = ctx->stage_table;
     ctx->last_table = table;
     int64_t n_records = n_agg;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[10], ctx->stream));
     if (table && (rc = phase_table(ctx, I, n_agg, &n_records))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     ctx->census_ready = false;   // (the owner counts what it receives)
@@ -3852,13 +4001,13 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     if ((rc = phase_dedup(ctx, &I, nullptr, I.n, s1.dedup_retry != 0))) return rc;
     if ((rc = ensure(ctx, ctx->cands, std::max<int64_t>(I.n, 1) * sizeof(Cand)))) return rc;
     hipLaunchKernelGGL(k_make_cands, dim3(grid_for(std::max<int64_t>(I.n, 1), 256)), dim3(256), 0, ctx->stream,
-                       (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, I.vk, I.ts, rank, (Cand *)ctx->cands.p);
+                       (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, I.vk, I.ts, ctx->rank, (Cand *)ctx->cands.p);
     HIPCHK(ctx, hipGetLastError());
-    // partition both record kinds by owner rank: candidates by counts + cursors here, tile partials below
+    // partition both record kinds by owner rank: candidates by counts + cursors here, tile records below
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch, 0, 128 * 8, ctx->stream));
-    int gb = grid_for(std::max<int64_t>(I.n, 1), 256);
+    const int gb = grid_for(std::max<int64_t>(I.n, 1), 256);
     hipLaunchKernelGGL(k_part_count<Cand>, dim3(gb), dim3(256), 0, ctx->stream, (const Cand *)ctx->cands.p, ctx->d_scratch + 255,
-                       nranks, ctx->d_scratch + 64);
+                       W, ctx->d_scratch + 64);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 256 * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
@@ -3867,69 +4016,113 @@ int hm_stage_local(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t
     if (ctx->h_st->bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved");
     ctx->dedup_seen = (int64_t)ctx->h_scratch[ctx->dlast->used_word];
     if (n_records > tile_send_cap || (int64_t)ctx->h_scratch[255] > cand_send_cap)
-        return set_err(ctx, HM_E_INVALID, "send buffer too small (%lld tiles, %llu candidates)", (long long)n_records,
+        return set_err(ctx, HM_E_INVALID, "send buffer too small (%lld tile records, %llu candidates)", (long long)n_records,
                        ctx->h_scratch[255]);
     // candidates: exclusive offsets -> cursors
     unsigned long long cur[128];
     unsigned long long acc = 0;
-    for (int r = 0; r < nranks; r++) { cur[64 + r] = acc; cand_send_counts[r] = (int64_t)ctx->h_scratch[64 + r]; acc += ctx->h_scratch[64 + r]; }
+    for (int r = 0; r < W; r++) { cur[64 + r] = acc; cand_send_counts[r] = (int64_t)ctx->h_scratch[64 + r]; acc += ctx->h_scratch[64 + r]; }
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_scratch + 64, cur + 64, 64 * 8, hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(k_part_scatter<Cand>, dim3(gb), dim3(256), 0, ctx->stream, (const Cand *)ctx->cands.p, ctx->d_scratch + 255,
-                       nranks, ctx->d_scratch + 64, (Cand *)cand_send_buf);
+                       W, ctx->d_scratch + 64, (Cand *)cand_send_buf);
     HIPCHK(ctx, hipGetLastError());
-    // tile partials: the radix partition with the owner rank as the digit, straight into the send buffer
+    // tile records: the radix partition with the owner rank as the digit, straight into the send streams
+    HIPCHK(ctx, hipEventRecord(ctx->ev[8], ctx->stream));
     if (n_records > 0) {
         int64_t ntiles;
         if (table) {
-            if ((rc = partition<TilePartial, TilePartial>(ctx, (const TilePartial *)ctx->partials.p, n_records, ntiles, nranks,
+            if ((rc = partition<TilePartial, TilePartial>(ctx, (const TilePartial *)ctx->partials.p, n_records, ntiles, W,
                                                           (TilePartial *)tile_send_buf)))
                 return rc;
         } else {
-            if ((rc = winfo_upload(ctx, false)) ||
-                (rc = ev_partition<TilePartial>(ctx, I, ntiles, nranks, (TilePartial *)tile_send_buf)))
+            // this rank's registry slots -> the batch's global slots (WInfo.gslot), keys rewritten by the scatter
+            ctx->stage_gslot.assign(WREG_SLOTS, 0u);
+            for (int w = 0; w < WREG_SLOTS; w++) {
+                const unsigned long long we = ctx->h_wreg[w];
+                if (!we) continue;
+                const auto it = std::find(ctx->stage_gwreg.begin(), ctx->stage_gwreg.end(), we);
+                if (it == ctx->stage_gwreg.end() && ctx->h_wcount[w])
+                    return set_err(ctx, HM_E_STATE, "a window of this rank is missing from the global registry");
+                ctx->stage_gslot[w] = (unsigned)(it - ctx->stage_gwreg.begin());
+            }
+            rc = winfo_upload(ctx, false);
+            ctx->stage_gslot.clear();
+            if (rc || (rc = ev_partition<WireKey>(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, nullptr, ntiles, W,
+                                                  (WireKey *)tile_send_buf, (uint64_t *)payload_send_buf)))
                 return rc;
         }
         hipLaunchKernelGGL(k_digit_starts, dim3(1), dim3(128), 0, ctx->stream, (const unsigned long long *)ctx->rp_O.p, ntiles,
-                           nranks + 1, ctx->d_scratch);
+                           W + 1, ctx->d_scratch);
         HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, (nranks + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, (W + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
     }
+    HIPCHK(ctx, hipEventRecord(ctx->ev[9], ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    for (int r = 0; r < nranks; r++) {
+    for (int r = 0; r < W; r++) {
         const int64_t start = n_records > 0 ? (int64_t)ctx->h_scratch[r] : 0;
-        const int64_t end = n_records > 0 ? (int64_t)ctx->h_scratch[r + 1] : 0;   // [nranks]: the gaps' digit
+        const int64_t end = n_records > 0 ? (int64_t)ctx->h_scratch[r + 1] : 0;   // [W]: the gaps' digit
         tile_send_counts[r] = end - start;
     }
     ctx->stage_agg_rows = n_agg;
-    if (sizes) {
-        sizes->n_tile_partials = n_records;
-        sizes->n_cands = 0;
-        for (int r = 0; r < nranks; r++) sizes->n_cands += cand_send_counts[r];
-        sizes->batch_max_event_ms = s1.max_ts_ms;
-        sizes->n_valid = (int64_t)s1.n_valid;
-        sizes->n_late = (int64_t)s1.n_late;
-    }
-    ctx->stage_sizes.n_tile_partials = n_records;
-    ctx->stage_sizes.batch_max_event_ms = s1.max_ts_ms;
-    ctx->stage_sizes.n_valid = (int64_t)s1.n_valid;
-    ctx->stage_sizes.n_late = (int64_t)s1.n_late;
-    ctx->stage_n_in = I.n;
-    ctx->stage = 1;
+    ctx->stage_sent = n_records;
+    hm_stage_sizes z{};
+    z.table_mode = table ? 1 : 0;
+    z.n_tile_records = n_records;
+    for (int r = 0; r < W; r++) z.n_cands += cand_send_counts[r];
+    z.global_batch_max_event_ms = ctx->stage_gmax_ms;
+    z.n_valid = (int64_t)s1.n_valid;
+    z.n_late = (int64_t)s1.n_late;
+    ctx->stage_sizes = z;
+    if (sizes) *sizes = z;
+    ctx->stage = 2;
     return HM_OK;
 }
 
-int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, const void *cand_recv_dev, int64_t n_cand_recv,
-                   int64_t global_batch_max_event_ms, int32_t out_memory, hm_batch_out *out, void *winner_send_buf,
-                   int64_t winner_send_cap, int64_t *winner_send_counts) {
+// the multi-GPU owner's direct path: the received key + payload streams (n rows of all ranks) -> census per global
+// window -> window tables -> (window, region) partition into EventRecs -> merge -> rows
+static int merge_received_events(hm_ctx *ctx, const uint64_t *keys, const uint64_t *payload, int64_t n) {
+    int rc;
+    ctx->n_partials_merged = n;
+    if ((rc = merge_begin(ctx, n))) return rc;
+    if (n == 0) return merge_nothing(ctx);
+    memcpy(ctx->h_wreg, ctx->stage_gwreg.data(), WREG_SLOTS * sizeof(unsigned long long));
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_wcount, 0, (WREG_SLOTS + 1) * 8, ctx->stream));
+    hipLaunchKernelGGL(k_key_census, dim3(grid_for(n, 256, 256 * 8)), dim3(256), 0, ctx->stream, keys, n, ctx->d_wcount);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_wcount, ctx->d_wcount, WREG_SLOTS * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    for (int w = 0; w < WREG_SLOTS; w++)
+        if (ctx->h_wcount[w] && !ctx->h_wreg[w]) return set_err(ctx, HM_E_INVALID, "received a record of an unknown window slot");
+    std::vector<WinCount> census;
+    census_of_registry(ctx, census);
+    if ((rc = gens_prepare(ctx, census)) || (rc = winfo_upload(ctx, true))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    int64_t ntiles;
+    if ((rc = ev_partition<EventRec>(ctx, keys, n, nullptr, payload, ntiles))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
+    if ((rc = merge_sorted<EventRec>(ctx, n, ntiles))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+    if ((rc = rows_densify(ctx, ntiles))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+    return HM_OK;
+}
+
+int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, const void *payload_recv_dev, int64_t n_tile_recv,
+                   const void *cand_recv_dev, int64_t n_cand_recv, int32_t out_memory, hm_batch_out *out,
+                   void *winner_send_buf, int64_t winner_send_cap, int64_t *winner_send_counts) {
     if (!ctx || !out || !winner_send_counts || n_tile_recv < 0 || n_cand_recv < 0 || winner_send_cap < n_cand_recv ||
-        (n_cand_recv > 0 && !winner_send_buf))
+        (n_cand_recv > 0 && (!winner_send_buf || !cand_recv_dev)) || (n_tile_recv > 0 && !tile_recv_dev))
         return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
-    if (ctx->stage != 1) return set_err(ctx, HM_E_STATE, "hm_stage_merge before hm_stage_local");
+    if (ctx->stage != 2) return set_err(ctx, HM_E_STATE, "hm_stage_merge before hm_stage_send");
+    if (!ctx->stage_table && n_tile_recv > 0 && !payload_recv_dev)
+        return set_err(ctx, HM_E_INVALID, "the direct path needs the received payload stream");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc;
     memset(out, 0, sizeof(*out));
-    int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
-    if ((rc = merge_partials(ctx, (const TilePartial *)tile_recv_dev, n_tile_recv))) return rc;
+    const int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
+    if (ctx->stage_table) rc = merge_partials(ctx, (const TilePartial *)tile_recv_dev, n_tile_recv);
+    else rc = merge_received_events(ctx, (const uint64_t *)tile_recv_dev, (const uint64_t *)payload_recv_dev, n_tile_recv);
+    if (rc) return rc;
     // owner-side dedup over received candidates
     if ((rc = phase_dedup(ctx, nullptr, (const Cand *)cand_recv_dev, n_cand_recv, true))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch, 0, 128 * 8, ctx->stream));
@@ -3956,7 +4149,14 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, 
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     record_timings(ctx);
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, 0, nullptr, out_memory, out))) return rc;
-    if (ctx->stage_agg_rows >= (int64_t(1) << 16)) {   // this rank's share of the keys stands in for the shard's
+    // hm_last_counts: this rank's share of the batch (state keys created, records merged, tiles emitted, path)
+    ctx->last_counts[0] = (int64_t)s2.n_state_new;
+    ctx->last_counts[1] = n_tile_recv;
+    ctx->last_counts[2] = (int64_t)s2.n_touched;
+    ctx->last_counts[3] = ctx->stage_table ? 1 : 0;
+    ctx->last_counts[4] = ctx->stage_table ? ctx->table_evicted : 0;
+    ctx->last_counts[5] = ctx->stage_sent;
+    if (ctx->stage_agg_rows >= (int64_t(1) << 16)) {   // this rank's rows and owned keys (summed over ranks next batch)
         ctx->prev_agg_rows = ctx->stage_agg_rows;
         ctx->prev_keys = (int64_t)s2.n_touched;
     }
@@ -3964,16 +4164,16 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, int64_t n_tile_recv, 
     DevStats sf{};
     sf.n_valid = ctx->stage_sizes.n_valid;
     sf.n_late = ctx->stage_sizes.n_late;
-    sf.max_ts_ms = global_batch_max_event_ms;
+    sf.max_ts_ms = ctx->stage_gmax_ms;
     fill_stats(ctx, out, ctx->stage_n_in, sf, late_wm);
-    advance_watermark(ctx, global_batch_max_event_ms);
-    ctx->stage = 2;
+    advance_watermark(ctx, ctx->stage_gmax_ms);
+    ctx->stage = 3;
     return HM_OK;
 }
 
 int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_recv, int32_t out_memory, hm_batch_out *out) {
     if (!ctx || !out || n_winner_recv < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
-    if (ctx->stage != 2) return set_err(ctx, HM_E_STATE, "hm_stage_finish before hm_stage_merge");
+    if (ctx->stage != 3) return set_err(ctx, HM_E_STATE, "hm_stage_finish before hm_stage_merge");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc;
     out->n_latest = n_winner_recv;

@@ -14,10 +14,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MOBHEAT_LIB: load another build of the same ABI (kernel variants under csrc/variants/ for tuning runs)
 LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
 
-HM_ABI_VERSION = 8
+HM_ABI_VERSION = 9
 HM_MEM_HOST = 0
 HM_MEM_DEVICE = 1
-HM_TILE_REC_BYTES = 48
+HM_STAGE_SUMMARY_WORDS = 8200
+HM_TILE_REC_BYTES = 48       # table mode's tile partial
+HM_TILE_KEY_BYTES = 8        # direct path: key stream
+HM_TILE_PAYLOAD_BYTES = 24   # direct path: payload stream
 HM_CAND_REC_BYTES = 32
 
 c_i32, c_i64, c_u64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double, ctypes.c_void_p
@@ -60,7 +63,7 @@ class HmJsonOut(ctypes.Structure):
 
 
 class HmStageSizes(ctypes.Structure):
-    _fields_ = [("n_tile_partials", c_i64), ("n_cands", c_i64), ("batch_max_event_ms", c_i64),
+    _fields_ = [("table_mode", c_i64), ("n_tile_records", c_i64), ("n_cands", c_i64), ("global_batch_max_event_ms", c_i64),
                 ("n_valid", c_i64), ("n_late", c_i64)]
 
 
@@ -93,9 +96,9 @@ SIGNATURES = {
     "hm_last_error": (ctypes.c_char_p, [c_vp]),
     "hm_process_batch": (c_i32, [c_vp, c_i64, _P(HmBatchIn), c_i32, _P(HmBatchOut)]),
     "hm_latlng_to_cell": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp]),
-    "hm_stage_local": (c_i32, [c_vp, c_i64, _P(HmBatchIn), c_i32, c_i32, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp,
-                               _P(HmStageSizes)]),
-    "hm_stage_merge": (c_i32, [c_vp, c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, _P(HmBatchOut), c_vp, c_i64, c_vp]),
+    "hm_stage_ingest": (c_i32, [c_vp, c_i64, _P(HmBatchIn), c_i32, c_i32, c_vp]),
+    "hm_stage_send": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, _P(HmStageSizes)]),
+    "hm_stage_merge": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, _P(HmBatchOut), c_vp, c_i64, c_vp]),
     "hm_stage_finish": (c_i32, [c_vp, c_vp, c_i64, c_i32, _P(HmBatchOut)]),
     "hm_device_alloc": (c_i32, [c_i32, c_i64, _P(c_vp)]),
     "hm_device_free": (c_i32, [c_i32, c_vp]),

@@ -1,89 +1,158 @@
 """Multi-GPU hot path: one process per GPU, torch.distributed (backend "nccl" = RCCL over xGMI).
 
 Replaces Spark's shuffle of the two aggregations (spark.sql.shuffle.partitions = 4, reference
-heatmap_stream.py:44): every rank snaps and pre-aggregates its own shard of the micro-batch, then ONE
-all-to-all per record kind routes
+heatmap_stream.py:44).  Per micro-batch every rank snaps its own shard of the events (hm_stage_ingest), then
 
-  * tile partials  (48-B records: cell, windowStart, count, n_speed, sum speed/lat/lon) to owner rank
-    hash(cell, windowStart) % world, which merges them into the persistent state it owns and emits them;
-  * latest-position candidates (32-B records: vkey, ts, row, origin rank) to owner hash(vkey) % world,
-    which keeps the rows tied at the global max and routes the winning row indices back to their origin;
+  1. all_gather of the ranks' summaries (counts, max event time, window registry: ~64 KB per rank), from which
+     every rank derives the same batch-wide decisions -- the watermark's input (:107), the aggregation path, the
+     batch's global window registry;
+  2. hm_stage_send writes the records grouped by owner rank:
+       * direct path: one 32-B record per aggregated row, as a key stream (8 B) and a payload stream (24 B), owner
+         = hash(cell, windowStart) % world -- the owner merges them into the persistent state it owns and emits them;
+       * table mode (low cardinality): one 48-B tile partial per key of the shard;
+       * latest-position candidates (32 B: vkey, ts, row, origin rank) to owner hash(vkey) % world, which keeps the
+         rows tied at the global max and routes the winning row indices back to their origin;
+  3. ONE all_to_all of every stream's per-destination counts, then one all_to_all per stream;
+  4. hm_stage_merge on the owner, the winners' all_to_all back, hm_stage_finish.
 
-plus an all-reduce(max) of the batch's max event time (the watermark's input, :107).  Ownership is a pure
-function of the key, so the persistent state never moves between batches.  The exchange buffers are torch
-tensors handed to RCCL directly; the library writes/reads them through plain device pointers.
+Ownership is a pure function of the key, so the persistent state never moves between batches.  The exchange buffers
+are torch tensors handed to RCCL directly; the library writes/reads them through plain device pointers.
 """
 import ctypes
+from collections import namedtuple
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
 from . import _lib
-from ._lib import HM_CAND_REC_BYTES, HM_MEM_DEVICE, HM_MEM_HOST, HM_TILE_REC_BYTES, HmBatchIn, HmBatchOut, HmStageSizes, check
+from ._lib import (HM_CAND_REC_BYTES, HM_MEM_DEVICE, HM_STAGE_SUMMARY_WORDS, HM_TILE_KEY_BYTES, HM_TILE_PAYLOAD_BYTES,
+                   HM_TILE_REC_BYTES, HmBatchIn, HmBatchOut, HmStageSizes, check)
+
+# one record stream of an exchange: buf (uint8 tensor), counts[r] records for rank r, rec_bytes per record
+Stream = namedtuple("Stream", "name buf counts rec_bytes")
+
+# summary word layout (csrc/mobheat.hip SW_*)
+SW_N_IN, SW_VALID, SW_LATE, SW_AGG, SW_MAX_MS, SW_SAMPLE_RUN, SW_PREV_AGG, SW_PREV_KEYS, SW_NWIN = range(9)
+SW_WIN0 = 10
+WREG_SLOTS = 4095
 
 
-def exchange(send, send_counts, rec_bytes, device):
-    """all_to_all of variable-size record runs; send_counts[r] records go to rank r. Returns (recv, counts),
-    recv a uint8 tensor.  The payload moves as 8-byte words (records are 48, 32 or 8 bytes): a rank's share at
-    1e8 events per GPU is several GB, past 2^31 single-byte elements."""
+def all_gather_summaries(summary, device):
+    """all_gather of every rank's int64[HM_STAGE_SUMMARY_WORDS] summary -> host array [world, words]."""
     world = dist.get_world_size()
-    assert rec_bytes % 8 == 0
-    w = rec_bytes // 8
-    sc = torch.tensor(send_counts, dtype=torch.int64, device=device)
+    t = torch.from_numpy(np.ascontiguousarray(summary, dtype=np.int64)).to(device)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return torch.stack(out).cpu().numpy()
+
+
+def exchange(streams, device):
+    """all_to_all of several variable-size record streams: one all_to_all of all the per-destination counts (the
+    batch's single host synchronization of the exchange), then one all_to_all per stream.  Payloads move as 8-byte
+    words (record sizes are multiples of 8): a rank's share at 1e8 events per GPU is several GB, past 2^31
+    single-byte elements.  Returns [(recv uint8 tensor, recv_counts per source)] in stream order."""
+    world = dist.get_world_size()
+    k = len(streams)
+    sc = torch.tensor([[s.counts[r] for s in streams] for r in range(world)], dtype=torch.int64, device=device)
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc)
-    recv_counts = rc.cpu().tolist()
-    nrecv = int(sum(recv_counts))
-    recv = torch.empty(max(nrecv * w, 2), dtype=torch.int64, device=device)
-    nsend = int(sum(send_counts))
-    dist.all_to_all_single(recv[: nrecv * w], send[: nsend * rec_bytes].view(torch.int64),
-                           [c * w for c in recv_counts], [c * w for c in send_counts])
-    assert len(recv_counts) == world
-    return recv.view(torch.uint8), recv_counts
+    rcounts = rc.cpu().tolist()
+    out = []
+    for j, s in enumerate(streams):
+        assert s.rec_bytes % 8 == 0 and len(s.counts) == world
+        w = s.rec_bytes // 8
+        recv_counts = [int(rcounts[r][j]) for r in range(world)]
+        nrecv, nsend = sum(recv_counts), int(sum(s.counts))
+        recv = torch.empty(max(nrecv * w, 2), dtype=torch.int64, device=device)
+        dist.all_to_all_single(recv[: nrecv * w], s.buf[: nsend * s.rec_bytes].view(torch.int64),
+                               [c * w for c in recv_counts], [int(c) * w for c in s.counts])
+        out.append((recv.view(torch.uint8), recv_counts))
+    assert len(out) == k
+    return out
+
+
+def global_window_registry(summaries, tile_us):
+    """Python twin of the library's stage_decide registry: the union of the ranks' windows in ascending order,
+    hashed like k_ingest's registry (slot = window quotient mod WREG_SLOTS, linear probing).  Returns wenc per slot."""
+    wins = set()
+    for S in summaries:
+        n = int(S[SW_NWIN])
+        wins.update(int(x) & (2 ** 64 - 1) for x in S[SW_WIN0 + 1: SW_WIN0 + 2 * n: 2])
+    reg = [0] * WREG_SLOTS
+    for we in sorted(wins):
+        u = we ^ (1 << 63)
+        start = u - (1 << 64) if u >= (1 << 63) else u
+        h = ((start // tile_us) % (1 << 64)) % WREG_SLOTS   # (C: (uint64_t)wq % WREG_SLOTS)
+        for _ in range(WREG_SLOTS):
+            if not reg[h]:
+                break
+            h = (h + 1) % WREG_SLOTS
+        else:
+            raise OverflowError("more than 4095 windows in one micro-batch")
+        reg[h] = we
+    return reg
 
 
 class LibStages:
-    """The library's stage API (hm_stage_local / hm_stage_merge / hm_stage_finish) on torch device buffers."""
+    """The library's stage API (hm_stage_ingest / send / merge / finish) on torch device buffers."""
 
     def __init__(self, engine):
         self.engine = engine
         self.lib = _lib.load()
         self.dev = torch.device("cuda", engine.device)
-        self._tile_send = self._cand_send = self._winner_send = None
+        self._bufs = {}
+        self._summary = np.zeros(HM_STAGE_SUMMARY_WORDS, np.int64)
 
     def _buf(self, name, nbytes):
-        b = getattr(self, name)
+        b = self._bufs.get(name)
         if b is None or b.numel() < nbytes:
             b = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=self.dev)
-            setattr(self, name, b)
+            self._bufs[name] = b
         return b
 
-    def local(self, epoch, batch, world, rank):
-        n = int(batch["n"])
-        tile_send = self._buf("_tile_send", n * HM_TILE_REC_BYTES)
-        cand_send = self._buf("_cand_send", n * HM_CAND_REC_BYTES)
-        tc = (ctypes.c_int64 * world)()
-        cc = (ctypes.c_int64 * world)()
-        sizes = HmStageSizes()
+    def ingest(self, epoch, batch, world, rank):
+        self.world = world
+        self._n = n = int(batch["n"])
         b = HmBatchIn(n=n, memory=HM_MEM_DEVICE, lat=batch["lat"], lon=batch["lon"], ts_us=batch["ts_us"],
                       speed=batch.get("speed"), speed_valid=batch.get("speed_valid"), vkey=batch["vkey"],
                       row_valid=batch.get("row_valid"))
         ctx = self.engine._ctx
-        check(self.lib.hm_stage_local(ctx, int(epoch), ctypes.byref(b), world, rank, tile_send.data_ptr(), n, tc,
-                                      cand_send.data_ptr(), n, cc, ctypes.byref(sizes)), ctx, "hm_stage_local")
-        return tile_send, list(tc), cand_send, list(cc), int(sizes.batch_max_event_ms)
+        check(self.lib.hm_stage_ingest(ctx, int(epoch), ctypes.byref(b), world, rank, self._summary.ctypes.data), ctx,
+              "hm_stage_ingest")
+        return self._summary
 
-    def merge(self, tile_recv, n_tile, cand_recv, n_cand, global_max_ms, out_memory):
-        world = dist.get_world_size()
-        winner_send = self._buf("_winner_send", max(n_cand, 1) * 8)
+    def send(self, summaries):
+        world, n = self.world, self._n
+        summaries = np.ascontiguousarray(summaries, dtype=np.int64)
+        tile = self._buf("tile", n * HM_TILE_REC_BYTES)
+        pay = self._buf("payload", n * HM_TILE_PAYLOAD_BYTES)
+        cand = self._buf("cand", n * HM_CAND_REC_BYTES)
+        tc, cc = (ctypes.c_int64 * world)(), (ctypes.c_int64 * world)()
+        sizes = HmStageSizes()
+        ctx = self.engine._ctx
+        check(self.lib.hm_stage_send(ctx, summaries.ctypes.data, tile.data_ptr(), pay.data_ptr(), n, tc, cand.data_ptr(),
+                                     n, cc, ctypes.byref(sizes)), ctx, "hm_stage_send")
+        self.table_mode = bool(sizes.table_mode)
+        if self.table_mode:
+            return [Stream("tile", tile, list(tc), HM_TILE_REC_BYTES), Stream("cand", cand, list(cc), HM_CAND_REC_BYTES)]
+        return [Stream("tile", tile, list(tc), HM_TILE_KEY_BYTES), Stream("payload", pay, list(tc), HM_TILE_PAYLOAD_BYTES),
+                Stream("cand", cand, list(cc), HM_CAND_REC_BYTES)]
+
+    def merge(self, recv, out_memory):
+        world = self.world
+        (tile_recv, trc) = recv[0]
+        pay_recv = None if self.table_mode else recv[1][0]
+        cand_recv, crc = recv[-1]
+        n_tile, n_cand = int(sum(trc)), int(sum(crc))
+        winner_send = self._buf("winner", max(n_cand, 1) * 8)
         wc = (ctypes.c_int64 * world)()
         out = HmBatchOut()
         ctx = self.engine._ctx
-        check(self.lib.hm_stage_merge(ctx, tile_recv.data_ptr(), n_tile, cand_recv.data_ptr(), n_cand, global_max_ms,
-                                      out_memory, ctypes.byref(out), winner_send.data_ptr(), max(n_cand, 1), wc),
-              ctx, "hm_stage_merge")
-        return out, winner_send, list(wc)
+        check(self.lib.hm_stage_merge(ctx, tile_recv.data_ptr(), None if pay_recv is None else pay_recv.data_ptr(), n_tile,
+                                      cand_recv.data_ptr(), n_cand, out_memory, ctypes.byref(out), winner_send.data_ptr(),
+                                      max(n_cand, 1), wc), ctx, "hm_stage_merge")
+        return out, Stream("winner", winner_send, list(wc), 8)
 
     def finish(self, winner_recv, n_winner, out_memory, out):
         ctx = self.engine._ctx
@@ -93,32 +162,30 @@ class LibStages:
 
 
 class ShardedHeatmap:
-    """One rank of the sharded hot path. ``stages`` provides local / merge / finish (LibStages on GPUs)."""
+    """One rank of the sharded hot path. ``stages`` provides ingest / send / merge / finish (LibStages on GPUs)."""
 
     def __init__(self, stages, device):
         self.stages = stages
         self.device = device
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
-        # the last batch's receive buffers: with out_memory=HM_MEM_DEVICE, out.latest_row points into winner_recv
-        # (hm_stage_finish), so they stay alive until the next process_batch call
+        # the last batch's receive buffers: with out_memory=HM_MEM_DEVICE, out.latest_row points into the winners'
+        # receive buffer (hm_stage_finish), so they stay alive until the next process_batch call
         self._recv = None
 
     def process_batch(self, epoch, batch, out_memory=HM_MEM_DEVICE, sync=None):
+        # the library reads the received buffers on its own stream: RCCL's (torch's current stream) must be done
         sync = sync or (lambda: torch.cuda.current_stream(self.device).synchronize()
                         if self.device.type == "cuda" else None)
-        tile_send, tcounts, cand_send, ccounts, local_max = self.stages.local(epoch, batch, self.world, self.rank)
-        tile_recv, trc = exchange(tile_send, tcounts, HM_TILE_REC_BYTES, self.device)
-        cand_recv, crc = exchange(cand_send, ccounts, HM_CAND_REC_BYTES, self.device)
-        m = torch.tensor([local_max], dtype=torch.int64, device=self.device)
-        dist.all_reduce(m, op=dist.ReduceOp.MAX)
-        global_max = int(m.item())
+        summary = self.stages.ingest(epoch, batch, self.world, self.rank)
+        summaries = all_gather_summaries(summary, self.device)
+        streams = self.stages.send(summaries)
+        recv = exchange(streams, self.device)
         sync()
-        out, winner_send, wcounts = self.stages.merge(tile_recv, int(sum(trc)), cand_recv, int(sum(crc)), global_max,
-                                                      out_memory)
-        winner_recv, wrc = exchange(winner_send, wcounts, 8, self.device)
+        out, winners = self.stages.merge(recv, out_memory)
+        [(winner_recv, wrc)] = exchange([winners], self.device)
         sync()
-        self._recv = (tile_recv, cand_recv, winner_recv)
+        self._recv = (recv, winner_recv)
         return self.stages.finish(winner_recv, int(sum(wrc)), out_memory, out)
 
 

@@ -242,15 +242,16 @@ class HeatmapEngine:
         return pb.value, po.value, nd.value
 
     def last_timings(self):
-        ms = (ctypes.c_double * 7)()
-        check(self._lib.hm_last_timings(self._ctx, ms, 7), self._ctx)
+        ms = (ctypes.c_double * 8)()
+        check(self._lib.hm_last_timings(self._ctx, ms, 8), self._ctx)
         return {"ingest": ms[0], "aggregate": ms[1], "merge": ms[2], "emit": ms[3], "dedup": ms[4], "total": ms[5],
-                "partition": ms[6]}
+                "partition": ms[6], "send": ms[7]}
 
     def last_counts(self):
-        c = (ctypes.c_int64 * 5)()
-        check(self._lib.hm_last_counts(self._ctx, c, 5), self._ctx)
-        return {"state_new": c[0], "partials": c[1], "tiles": c[2], "table_mode": bool(c[3]), "evicted": c[4]}
+        c = (ctypes.c_int64 * 6)()
+        check(self._lib.hm_last_counts(self._ctx, c, 6), self._ctx)
+        return {"state_new": c[0], "partials": c[1], "tiles": c[2], "table_mode": bool(c[3]), "evicted": c[4],
+                "sent": c[5]}
 
     def _result_from_host(self, out, copy=True):
         def arr(p, n, dt):

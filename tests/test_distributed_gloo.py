@@ -1,11 +1,13 @@
-"""CPU, world_size 2 over gloo: the sharded path (mobheat.distributed.ShardedHeatmap) -- local stage,
-all-to-all of tile partials and latest candidates by owner rank, all-reduce(max) of the batch max event time,
-owner merge, winners routed back -- must produce exactly the single-shard result.
+"""CPU, world_size 2 over gloo: the sharded path (mobheat.distributed.ShardedHeatmap) -- ingest, all_gather of the
+ranks' summaries, the batch-wide decisions (global window registry, max event time), the owner-grouped record streams
+(direct path: 8-B keys + 24-B payloads; table mode: 48-B tile partials; 32-B latest candidates), one all_to_all of
+every stream's counts then one per stream, owner merge, winners routed back -- must produce exactly the single-shard
+result.
 
-The stages here are a numpy restatement of hm_stage_local / hm_stage_merge / hm_stage_finish built on the
-oracle (test-only stand-in for the GPU); the orchestration, record layouts, owner functions and exchange
-code under test are the product's.  tests/test_gpu_stages.py runs the same decomposition through the HIP
-library on one GPU.
+The stages here are a numpy restatement of hm_stage_ingest / send / merge / finish built on the oracle (test-only
+stand-in for the GPU) that writes the library's wire formats; the orchestration, exchange code, owner functions and
+the global registry rule (distributed.global_window_registry, the twin of the library's) are the product's.
+tests/test_gpu_stages.py runs the same protocol through the HIP library on one GPU.
 """
 import os
 import socket
@@ -18,44 +20,91 @@ import torch.multiprocessing as mp
 
 TILE_DT = np.dtype([("cell", "<u8"), ("ws", "<i8"), ("count", "<u4"), ("nsp", "<u4"), ("ssp", "<f8"), ("slat", "<f8"),
                     ("slon", "<f8")])   # HM_TILE_REC_BYTES = 48
+PAY_DT = np.dtype([("sp", "<u8"), ("lat", "<f8"), ("lon", "<f8")])   # HM_TILE_PAYLOAD_BYTES = 24
 CAND_DT = np.dtype([("vkey", "<u8"), ("ts", "<i8"), ("row", "<i8"), ("origin", "<i8")])
+CELL_LO = (1 << 52) - 1
+SPEED_NULL = 0x7FF0000000000001
+I64_MIN = np.iinfo(np.int64).min
+
+
+def _wenc(ws):
+    return (np.asarray(ws, np.int64).view(np.uint64) ^ np.uint64(1 << 63))
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()) if a.size else torch.zeros(8, dtype=torch.uint8)
 
 
 class OracleStages:
-    def __init__(self, res, tile_us=300_000_000, delay_ms=600_000):
+    def __init__(self, res, table=False, tile_us=300_000_000, delay_ms=600_000):
         from oracle.spark_oracle import SparkHeatmapOracle
         self.o = SparkHeatmapOracle(h3_res=res, tile_us=tile_us, watermark_delay_ms=delay_ms)
         self.res = res
+        self.table = table
 
-    def local(self, epoch, b, world, rank):
-        from mobheat.distributed import _owner as owner_of, tile_hash, vkey_owner
+    def ingest(self, epoch, b, world, rank):
+        from mobheat import _lib
+        from mobheat.distributed import SW_AGG, SW_MAX_MS, SW_N_IN, SW_NWIN, SW_VALID, SW_WIN0
         from oracle import h3_oracle
         o = self.o
+        self.b, self.world, self.rank = b, world, rank
         valid = o.valid_mask(b["lat"], b["lon"], b["ts_us"], b["row_valid"])
         ts = b["ts_us"]
         ws = ts - np.mod(ts, o.tile)
         late = valid & (ws + o.tile <= o.wm_prev * 1000)
-        agg = np.nonzero(valid & ~late)[0]
-        cells = h3_oracle.latlng_to_cell(b["lat"][agg], b["lon"][agg], self.res)
-        recs = np.zeros(0, TILE_DT)
-        if agg.size:
-            keys = np.rec.fromarrays([cells, ws[agg]], names="c,w")
-            uq, inv = np.unique(keys, return_inverse=True)
-            inv = inv.ravel()
-            sv = b["speed_valid"][agg]
-            recs = np.zeros(uq.size, TILE_DT)
-            recs["cell"], recs["ws"] = uq["c"], uq["w"]
-            recs["count"] = np.bincount(inv, minlength=uq.size)
-            recs["nsp"] = np.bincount(inv, weights=sv.astype(float), minlength=uq.size)
-            recs["ssp"] = np.bincount(inv[sv], weights=b["speed"][agg][sv], minlength=uq.size)
-            recs["slat"] = np.bincount(inv, weights=b["lat"][agg], minlength=uq.size)
-            recs["slon"] = np.bincount(inv, weights=b["lon"][agg], minlength=uq.size)
-        own = owner_of(tile_hash(recs["cell"], recs["ws"]), world)
+        self.valid = valid
+        self.agg = agg = np.nonzero(valid & ~late)[0]
+        self.cells = h3_oracle.latlng_to_cell(b["lat"][agg], b["lon"][agg], self.res)
+        self.ws = ws[agg]
+        v = np.nonzero(valid)[0]
+        S = np.zeros(_lib.HM_STAGE_SUMMARY_WORDS, np.int64)
+        S[SW_N_IN], S[SW_VALID], S[SW_AGG] = ts.size, v.size, agg.size
+        S[SW_MAX_MS] = int(np.max(np.floor_divide(ts[v], 1000))) if v.size else I64_MIN
+        wins = np.unique(self.ws)
+        S[SW_NWIN] = wins.size
+        S[SW_WIN0: SW_WIN0 + 2 * wins.size: 2] = np.arange(wins.size)          # this rank's slots
+        S[SW_WIN0 + 1: SW_WIN0 + 2 * wins.size: 2] = _wenc(wins).view(np.int64)
+        return S
+
+    def send(self, summaries):
+        from mobheat.distributed import SW_MAX_MS, Stream, global_window_registry, tile_hash, vkey_owner
+        from mobheat.distributed import _owner as owner_of
+        o, b, world, rank = self.o, self.b, self.world, self.rank
+        self.gmax = int(max(S[SW_MAX_MS] for S in summaries))
+        self.reg = global_window_registry(summaries, o.tile)
+        gslot = {we: i for i, we in enumerate(self.reg) if we}
+        agg, cells, ws = self.agg, self.cells, self.ws
+        own = owner_of(tile_hash(cells, ws), world)
         order = np.argsort(own, kind="stable")
         tcounts = np.bincount(own, minlength=world).tolist()
-        tile_send = torch.from_numpy(recs[order].view(np.uint8).copy())
+        if self.table:
+            recs = np.zeros(0, TILE_DT)
+            if agg.size:
+                keys = np.rec.fromarrays([cells, ws], names="c,w")
+                uq, inv = np.unique(keys, return_inverse=True)
+                inv = inv.ravel()
+                sv = b["speed_valid"][agg]
+                recs = np.zeros(uq.size, TILE_DT)
+                recs["cell"], recs["ws"] = uq["c"], uq["w"]
+                recs["count"] = np.bincount(inv, minlength=uq.size)
+                recs["nsp"] = np.bincount(inv, weights=sv.astype(float), minlength=uq.size)
+                recs["ssp"] = np.bincount(inv[sv], weights=b["speed"][agg][sv], minlength=uq.size)
+                recs["slat"] = np.bincount(inv, weights=b["lat"][agg], minlength=uq.size)
+                recs["slon"] = np.bincount(inv, weights=b["lon"][agg], minlength=uq.size)
+            own = owner_of(tile_hash(recs["cell"], recs["ws"]), world)
+            order = np.argsort(own, kind="stable")
+            streams = [Stream("tile", _t(recs[order]), np.bincount(own, minlength=world).tolist(), 48)]
+        else:
+            key = (cells & np.uint64(CELL_LO)) | (np.array([gslot[int(w)] + 1 for w in _wenc(ws)], np.uint64) << np.uint64(52))
+            pay = np.zeros(agg.size, PAY_DT)
+            sv, sp = b["speed_valid"][agg], b["speed"][agg]
+            bits = np.where(np.isnan(sp), np.uint64(0x7FF8000000000000), sp.view(np.uint64))
+            pay["sp"] = np.where(sv, bits, np.uint64(SPEED_NULL))
+            pay["lat"], pay["lon"] = b["lat"][agg], b["lon"][agg]
+            streams = [Stream("tile", _t(key[order]), tcounts, 8), Stream("payload", _t(pay[order]), tcounts, 24)]
         # local latest candidates: rows tied at the local max of their vehicle
-        v = np.nonzero(valid)[0]
+        v = np.nonzero(self.valid)[0]
+        ts = b["ts_us"]
         cands = np.zeros(0, CAND_DT)
         if v.size:
             vk, tv = b["vkey"][v], ts[v]
@@ -67,15 +116,28 @@ class OracleStages:
             cands["vkey"], cands["ts"], cands["row"], cands["origin"] = vk[win], tv[win], v[win], rank
         cown = vkey_owner(cands["vkey"], world)
         corder = np.argsort(cown, kind="stable")
-        ccounts = np.bincount(cown, minlength=world).tolist()
-        cand_send = torch.from_numpy(cands[corder].view(np.uint8).copy())
-        bmax = int(np.max(np.where(ts[v] >= 0, ts[v] // 1000, -((-ts[v]) // 1000)))) if v.size else np.iinfo(np.int64).min
-        return (tile_send if tile_send.numel() else torch.zeros(1, dtype=torch.uint8), tcounts,
-                cand_send if cand_send.numel() else torch.zeros(1, dtype=torch.uint8), ccounts, bmax)
+        return streams + [Stream("cand", _t(cands[corder]), np.bincount(cown, minlength=world).tolist(), 32)]
 
-    def merge(self, tile_recv, n_tile, cand_recv, n_cand, global_max, out_memory):
+    def merge(self, recv, out_memory):
+        from mobheat.distributed import Stream
         o = self.o
-        recs = tile_recv.numpy()[: n_tile * TILE_DT.itemsize].view(TILE_DT)
+        if self.table:
+            (tb, trc) = recv[0]
+            recs = tb.numpy()[: sum(trc) * 48].view(TILE_DT)
+        else:
+            (kb, trc), (pb, _) = recv[0], recv[1]
+            n = sum(trc)
+            key = kb.numpy()[: n * 8].view(np.uint64)
+            pay = pb.numpy()[: n * 24].view(PAY_DT)
+            wenc = np.array(self.reg, np.uint64)[(key >> np.uint64(52)).astype(np.int64) - 1]
+            recs = np.zeros(n, TILE_DT)
+            recs["cell"] = (key & np.uint64(CELL_LO)) | np.uint64((1 << 59) | (self.res << 52))
+            recs["ws"] = (wenc ^ np.uint64(1 << 63)).view(np.int64)
+            recs["count"] = 1
+            null = pay["sp"] == np.uint64(SPEED_NULL)
+            recs["nsp"] = ~null
+            recs["ssp"] = np.where(null, 0.0, pay["sp"].view(np.float64))
+            recs["slat"], recs["slon"] = pay["lat"], pay["lon"]
         touched = []
         for r in recs:
             k = (int(r["cell"]), int(r["ws"]))
@@ -90,10 +152,11 @@ class OracleStages:
             tiles[k] = (c, None if nsp == 0 else ssp / nsp, slo / c, sla / c)
         for k in [k for k in o.state if k[1] + o.tile <= o.wm_cur * 1000]:
             del o.state[k]
-        nxt = o.wm_cur if global_max == np.iinfo(np.int64).min else max(o.wm_cur, global_max - o.delay)
+        nxt = o.wm_cur if self.gmax == I64_MIN else max(o.wm_cur, self.gmax - o.delay)
         o.wm_prev, o.wm_cur = o.wm_cur, nxt
-        cands = cand_recv.numpy()[: n_cand * CAND_DT.itemsize].view(CAND_DT)
-        world = dist.get_world_size()
+        cand_recv, crc = recv[-1]
+        cands = cand_recv.numpy()[: sum(crc) * 32].view(CAND_DT)
+        world = self.world
         rows_by_origin = [[] for _ in range(world)]
         if cands.size:
             srt = np.lexsort((cands["ts"], cands["vkey"]))
@@ -103,21 +166,19 @@ class OracleStages:
             win = srt[cands["ts"][srt] == cands["ts"][srt][last][grp]]
             for w in win:
                 rows_by_origin[int(cands["origin"][w])].append(int(cands["row"][w]))
-        wcounts = [len(x) for x in rows_by_origin]
         flat = np.array([r for x in rows_by_origin for r in x], np.int64)
-        send = torch.from_numpy(flat.view(np.uint8).copy()) if flat.size else torch.zeros(1, dtype=torch.uint8)
-        return {"tiles": tiles}, send, wcounts
+        return {"tiles": tiles}, Stream("winner", _t(flat), [len(x) for x in rows_by_origin], 8)
 
     def finish(self, winner_recv, n, out_memory, out):
         out["latest"] = np.sort(winner_recv.numpy()[: n * 8].view(np.int64))
         return out
 
 
-def _worker(rank, world, port, batches, res, q):
+def _worker(rank, world, port, batches, res, table, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from mobheat.distributed import ShardedHeatmap
-    sh = ShardedHeatmap(OracleStages(res), torch.device("cpu"))
+    sh = ShardedHeatmap(OracleStages(res, table=table), torch.device("cpu"))
     results = []
     for e, b in enumerate(batches):
         n = b["lat"].size
@@ -139,7 +200,8 @@ def _free_port():
     return p
 
 
-def test_sharded_equals_single_shard(oracle_h3):
+@pytest.mark.parametrize("table", [False, True])
+def test_sharded_equals_single_shard(oracle_h3, table):
     from mobheat import synth
     from oracle.spark_oracle import SparkHeatmapOracle
     rng = np.random.default_rng(5)
@@ -158,7 +220,7 @@ def test_sharded_equals_single_shard(oracle_h3):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, batches, 8, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, batches, 8, table, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=300) for _ in range(world))

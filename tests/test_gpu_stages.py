@@ -1,8 +1,11 @@
-"""GPU: the multi-GPU stage API (hm_stage_local / hm_stage_merge / hm_stage_finish) through the HIP library,
-with W contexts ("virtual ranks") on one device and the all-to-all done on the host.  The union of the owners'
-outputs must equal the single-shard result (oracle), batch after batch (state ownership is stable).
+"""GPU: the multi-GPU stage API (hm_stage_ingest / send / merge / finish) through the HIP library, with W contexts
+("virtual ranks") on one device and the exchanges routed on the host, plus the product's ShardedHeatmap driver over
+two gloo processes sharing the GPU (RCCL needs one GPU per rank).  The union of the owners' outputs must equal the
+single-shard result (oracle), batch after batch (state ownership is stable).
 """
 import ctypes
+import os
+import socket
 
 import numpy as np
 import pytest
@@ -33,50 +36,70 @@ class DevBuf:
 
 
 def _stage_batch(engines, lib, batches_per_rank, epoch):
-    from mobheat._lib import HM_CAND_REC_BYTES, HM_MEM_HOST, HM_TILE_REC_BYTES, HmBatchIn, HmBatchOut, HmStageSizes, check
+    """One micro-batch through the stage API of W contexts, exchanges routed on the host.  Returns the owners' tiles,
+    each rank's latest rows, per-rank tile/candidate send counts and whether table mode ran."""
+    from mobheat._lib import (HM_CAND_REC_BYTES, HM_MEM_HOST, HM_STAGE_SUMMARY_WORDS, HM_TILE_KEY_BYTES,
+                              HM_TILE_PAYLOAD_BYTES, HM_TILE_REC_BYTES, HmBatchIn, HmBatchOut, HmStageSizes, check)
     W = len(engines)
-    sends, tcounts, ccounts, maxes, bufs = [], [], [], [], []
+    bufs, keep = [], []
+    summaries = np.zeros((W, HM_STAGE_SUMMARY_WORDS), np.int64)
     for r, (eng, b) in enumerate(zip(engines, batches_per_rank)):
         n = b["lat"].size
-        tb, cb = DevBuf(lib, n * HM_TILE_REC_BYTES), DevBuf(lib, n * HM_CAND_REC_BYTES)
-        bufs += [tb, cb]
+        k = {kk: np.ascontiguousarray(v) for kk, v in b.items()}
+        k["sv"], k["rv"] = k["speed_valid"].astype(np.uint8), k["row_valid"].astype(np.uint8)
+        keep.append(k)
+        bi = HmBatchIn(n=n, memory=HM_MEM_HOST, lat=k["lat"].ctypes.data, lon=k["lon"].ctypes.data,
+                       ts_us=k["ts_us"].ctypes.data, speed=k["speed"].ctypes.data, speed_valid=k["sv"].ctypes.data,
+                       vkey=k["vkey"].ctypes.data, row_valid=k["rv"].ctypes.data)
+        check(lib.hm_stage_ingest(eng._ctx, epoch, ctypes.byref(bi), W, r, summaries[r].ctypes.data), eng._ctx)
+    sends, tcounts, ccounts, table = [], [], [], None
+    for r, (eng, b) in enumerate(zip(engines, batches_per_rank)):
+        n = b["lat"].size
+        tb, pb, cb = DevBuf(lib, n * HM_TILE_REC_BYTES), DevBuf(lib, n * HM_TILE_PAYLOAD_BYTES), DevBuf(lib, n * HM_CAND_REC_BYTES)
+        bufs += [tb, pb, cb]
         tc, cc = (ctypes.c_int64 * W)(), (ctypes.c_int64 * W)()
         sz = HmStageSizes()
-        keep = {k: np.ascontiguousarray(v) for k, v in b.items()}
-        sv = keep["speed_valid"].astype(np.uint8)
-        rv = keep["row_valid"].astype(np.uint8)
-        bi = HmBatchIn(n=n, memory=HM_MEM_HOST, lat=keep["lat"].ctypes.data, lon=keep["lon"].ctypes.data,
-                       ts_us=keep["ts_us"].ctypes.data, speed=keep["speed"].ctypes.data, speed_valid=sv.ctypes.data,
-                       vkey=keep["vkey"].ctypes.data, row_valid=rv.ctypes.data)
-        check(lib.hm_stage_local(eng._ctx, epoch, ctypes.byref(bi), W, r, tb.p, n, tc, cb.p, n, cc, ctypes.byref(sz)),
-              eng._ctx)
-        tcounts.append(list(tc)); ccounts.append(list(cc)); maxes.append(sz.batch_max_event_ms)
-        sends.append((tb.get(sum(tc) * HM_TILE_REC_BYTES), cb.get(sum(cc) * HM_CAND_REC_BYTES)))
-    gmax = max(maxes)
+        check(lib.hm_stage_send(eng._ctx, summaries.ctypes.data, tb.p, pb.p, n, tc, cb.p, n, cc, ctypes.byref(sz)), eng._ctx)
+        assert table is None or table == bool(sz.table_mode), "ranks disagree on the aggregation path"
+        table = bool(sz.table_mode)
+        assert sz.global_batch_max_event_ms == max(summaries[:, 4])
+        tcounts.append(list(tc)); ccounts.append(list(cc))
+        if not table:   # one 32-B wire record (8-B key + 24-B payload) per aggregated row of the rank
+            assert sum(tc) == summaries[r][3] == sz.n_tile_records
+        trec = HM_TILE_REC_BYTES if table else HM_TILE_KEY_BYTES
+        sends.append((tb.get(sum(tc) * trec), None if table else pb.get(sum(tc) * HM_TILE_PAYLOAD_BYTES),
+                      cb.get(sum(cc) * HM_CAND_REC_BYTES)))
 
     def route(r, kind, rec):
         parts = []
         for s in range(W):
-            cnt = (tcounts if kind == 0 else ccounts)[s]
+            cnt = (ccounts if kind == 2 else tcounts)[s]
             off = sum(cnt[:r]) * rec
             parts.append(sends[s][kind][off: off + cnt[r] * rec])
-        return np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+        return np.concatenate(parts)
 
     outs, wsends, wcounts = [], [], []
     for r, eng in enumerate(engines):
-        trecv, crecv = route(r, 0, HM_TILE_REC_BYTES), route(r, 1, HM_CAND_REC_BYTES)
+        trec = HM_TILE_REC_BYTES if table else HM_TILE_KEY_BYTES
+        trecv, crecv = route(r, 0, trec), route(r, 2, HM_CAND_REC_BYTES)
+        precv = None if table else route(r, 1, HM_TILE_PAYLOAD_BYTES)
         tb, cb, wb = DevBuf(lib, trecv.nbytes), DevBuf(lib, crecv.nbytes), DevBuf(lib, max(crecv.nbytes // 4, 8))
-        bufs += [tb, cb, wb]
+        pb = DevBuf(lib, 16 if table else precv.nbytes)
+        bufs += [tb, pb, cb, wb]
         tb.put(trecv); cb.put(crecv)
+        if not table:
+            pb.put(precv)
         nc = crecv.nbytes // HM_CAND_REC_BYTES
         out = HmBatchOut()
         wc = (ctypes.c_int64 * W)()
-        check(lib.hm_stage_merge(eng._ctx, tb.p, trecv.nbytes // HM_TILE_REC_BYTES, cb.p, nc, gmax, HM_MEM_HOST,
+        check(lib.hm_stage_merge(eng._ctx, tb.p, None if table else pb.p, trecv.nbytes // trec, cb.p, nc, HM_MEM_HOST,
                                  ctypes.byref(out), wb.p, max(nc, 1), wc), eng._ctx)
         res = eng._result_from_host(out)
         outs.append(res.tiles)
         wcounts.append(list(wc))
         wsends.append(wb.get(sum(wc) * 8).view(np.int64))
+        c = eng.last_counts()
+        assert c["partials"] == trecv.nbytes // trec and c["tiles"] == len(res.tiles) and c["sent"] == sum(tcounts[r])
     latest = []
     for r, eng in enumerate(engines):
         rows = np.concatenate([wsends[s][sum(wcounts[s][:r]): sum(wcounts[s][:r + 1])] for s in range(W)])
@@ -90,11 +113,15 @@ def _stage_batch(engines, lib, batches_per_rank, epoch):
         latest.append(got.copy())
     for b in bufs:
         b.free()
-    return outs, latest, tcounts, ccounts
+    return outs, latest, tcounts, ccounts, table
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_stage_api_matches_single_shard(world):
+@pytest.mark.parametrize("world,mode", [(2, "direct"), (3, "direct"), (2, "table")])
+def test_stage_api_matches_single_shard(world, mode, monkeypatch):
+    """Both aggregation paths pinned, four batches (one empty): on the direct path every aggregated row crosses as a
+    32-B record (8-B key with the batch's global window slot + 24-B payload) and the owner partitions them into the
+    same 32-B EventRecs the single-GPU merge uses."""
+    monkeypatch.setenv("MOBHEAT_INGEST_MODE", mode)
     import mobheat
     from mobheat import synth
     from oracle.spark_oracle import SparkHeatmapOracle
@@ -108,7 +135,7 @@ def test_stage_api_matches_single_shard(world):
         b["ts_us"] = synth.T0 + start * 60_000_000 + rng.integers(0, 9 * 60_000_000, n)
         bounds = [i * n // world for i in range(world + 1)]
         shards = [{k: v[bounds[r]:bounds[r + 1]] for k, v in b.items()} for r in range(world)]
-        outs, latest, _, _ = _stage_batch(engines, lib, shards, epoch)
+        outs, latest, _, _, _ = _stage_batch(engines, lib, shards, epoch)
         exp = ora.process_batch(**b)
         got = {}
         for t in outs:
@@ -162,7 +189,8 @@ def test_stage_api_table_mode_c3(world, monkeypatch, capsys):
         b["ts_us"] = b["ts_us"] + epoch * 6 * 60_000_000
         bounds = [i * n // world for i in range(world + 1)]
         shards = [{k: v[bounds[r]:bounds[r + 1]] for k, v in b.items()} for r in range(world)]
-        outs, latest, tc, cc = _stage_batch(engines, lib, shards, epoch)
+        outs, latest, tc, cc, table = _stage_batch(engines, lib, shards, epoch)
+        assert table
         exp = ora.process_batch(**b)
         _check_union(outs, latest, bounds, exp)
         for r in range(world):
@@ -201,7 +229,7 @@ def test_stage_api_c5_vehicles_straddle_ranks(world, capsys):
     for r in range(world):
         owners_per_vehicle += np.bincount(shards[r]["vkey"].astype(np.int64), minlength=30_000) > 0
     assert (owners_per_vehicle >= 2).mean() > 0.99
-    outs, latest, tc, cc = _stage_batch(engines, lib, shards, 0)
+    outs, latest, tc, cc, _ = _stage_batch(engines, lib, shards, 0)
     exp = SparkHeatmapOracle(h3_res=9).process_batch(**b)
     _check_union(outs, latest, bounds, exp)
     n_ties = len(exp["latest_rows"]) - 30_000
@@ -212,3 +240,92 @@ def test_stage_api_c5_vehicles_straddle_ranks(world, capsys):
                   f"({sum(cc[r]) * HM_CAND_REC_BYTES} B) to {world} owners {cc[r]}; tile partials {sum(tc[r])}")
     for e in engines:
         e.close()
+
+
+def _free_port():
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    p = so.getsockname()[1]
+    so.close()
+    return p
+
+
+def _batches_for_dist():
+    from mobheat import synth
+    rng = np.random.default_rng(77)
+    out = []
+    for start, n in ((0, 200_000), (7, 200_000), (0, 0), (20, 150_000)):
+        b = synth.c2_global(seed=start + 3, n=max(n, 1))
+        b = {k: v[:n] for k, v in b.items()}
+        b["ts_us"] = synth.T0 + start * 60_000_000 + rng.integers(0, 9 * 60_000_000, n)
+        out.append(b)
+    return out
+
+
+def _dist_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import mobheat
+    from mobheat._lib import HM_MEM_HOST
+    from mobheat.distributed import LibStages, ShardedHeatmap
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    eng = mobheat.HeatmapEngine(h3_res=8, device=0)
+    sh = ShardedHeatmap(LibStages(eng), dev)
+    res = []
+    for e, b in enumerate(_batches_for_dist()):
+        n = b["lat"].size
+        lo, hi = rank * n // world, (rank + 1) * n // world
+        cols = {}
+        for k, v in b.items():
+            a = np.ascontiguousarray(v[lo:hi])
+            a = a.view(np.int64) if a.dtype == np.uint64 else a.astype(np.uint8) if a.dtype == bool else a
+            cols[k] = torch.from_numpy(a).to(dev)
+        ptrs = dict(n=hi - lo, **{k: v.data_ptr() for k, v in cols.items()})
+        out = sh.process_batch(e, ptrs, out_memory=HM_MEM_HOST)
+        r = eng._result_from_host(out)
+        t = r.tiles
+        tiles = {(int(t.cell[k]), int(t.window_start_us[k])): (int(t.count[k]), float(t.avg_lat[k])) for k in range(len(t))}
+        res.append((tiles, (np.asarray(r.latest_rows) + lo).tolist(), eng.last_counts()))
+        torch.cuda.synchronize()
+    q.put((rank, res))
+    dist.barrier()
+    eng.close()
+    dist.destroy_process_group()
+
+
+def test_sharded_driver_two_processes_gloo_on_gpu():
+    """The product's driver (mobheat.distributed: summaries all_gather, one counts all_to_all, the key/payload/candidate
+    streams, winners back) over two processes that share the GPU, gloo moving the device tensors: every batch's union
+    of the owners' tiles and latest rows equals the single-shard oracle, and hm_last_counts reports each rank's share
+    (the bench's N>1 line prices its roofline on them)."""
+    import torch.multiprocessing as mp
+    from oracle.spark_oracle import SparkHeatmapOracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dist_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ora = SparkHeatmapOracle(h3_res=8)
+    for e, b in enumerate(_batches_for_dist()):
+        exp = ora.process_batch(**b)
+        tiles = {}
+        for r in range(world):
+            assert not set(got[r][e][0]) & set(tiles), "a key emitted by two owners"
+            tiles.update(got[r][e][0])
+        o = {(x["cell"], x["window_start_us"]): (x["count"], x["avg_lat"]) for x in exp["tiles"]}
+        assert set(tiles) == set(o)
+        assert all(tiles[k][0] == o[k][0] and abs(tiles[k][1] - o[k][1]) <= 1e-9 * abs(o[k][1]) for k in tiles)
+        assert sorted(got[0][e][1] + got[1][e][1]) == exp["latest_rows"].tolist()
+        counts = [got[r][e][2] for r in range(world)]
+        assert sum(c["tiles"] for c in counts) == len(o)
+        assert sum(c["partials"] for c in counts) == sum(c["sent"] for c in counts)
+        if b["lat"].size:
+            assert all(c["tiles"] > 0 and c["partials"] > 0 for c in counts)

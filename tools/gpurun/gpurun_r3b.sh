@@ -1,0 +1,11 @@
+# Round 3: GPU tests (new: glibc restatement, bit-exact near ties, stage API v2 + two-process driver), the default
+# bench, then bench.py's N=2 path rehearsed on one GPU (two gloo ranks; RCCL refuses two ranks on one device).
+set -o pipefail
+O=gpurun_out/${TAG:-r3b}
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -rf > $O/gpu_tests.log 2>&1 && \
+timeout -k 10 600 python3 bench.py ${BENCH_ARGS:-} > $O/bench.log 2>&1 && \
+MOBHEAT_DIST_BACKEND=gloo timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+  bench.py --gpus 2 --steps 4 --warmup 2 --events ${EVENTS:-20000000} > $O/bench_n2.log 2>&1
+rc=$?; echo "done rc=$rc"; exit $rc
