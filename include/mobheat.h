@@ -235,6 +235,11 @@ typedef struct hm_state_info {
 /* Fills *info; with recs != NULL also writes info->n_keys records to recs (host memory, cap records:
  * HM_E_INVALID if cap < n_keys). Call once with recs = NULL for the size. Not between stage calls. */
 int hm_state_export(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs, int64_t cap);
+/* Incremental checkpoint (Spark's state store delta files): the records of the keys the last batch touched (their
+ * cumulative values), *n_out of them (recs = NULL: count only); info as hm_state_export (n_keys = all live keys).  The
+ * state after that batch = the last-written record of every key of an older full export followed by the deltas of the
+ * batches since, keeping keys whose window end > info->prev_watermark_ms * 1000. */
+int hm_state_export_touched(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs, int64_t cap, int64_t *n_out);
 /* Restores an exported state into a context that has processed no batch (HM_E_STATE otherwise); the
  * config fields of info must equal the context's (HM_E_INVALID). recs: info->n_keys distinct keys, host memory. */
 int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *recs);
@@ -357,6 +362,9 @@ int hm_selftest_cells_to_boundary_host(const uint64_t *cells, int64_t n, double 
  * received as owner), [2] tiles emitted, [3] 1 if table mode ran, [4] table mode: aggregates evicted from k_agg's
  * LDS tables into its buckets, [5] stage API: tile records this rank sent. */
 int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n);
+/* Version of the persistent tile state: incremented when a batch starts merging into it (hm_process_batch,
+ * hm_stage_merge, growth).  A call that failed without changing it left the state as it was (-1: ctx NULL). */
+int64_t hm_state_version(const hm_ctx *ctx);
 
 /* HM_ABI_VERSION the library was built with (callers check it before hm_create). */
 int32_t hm_abi_version(void);

@@ -351,7 +351,9 @@ __global__ __launch_bounds__(256) void k_census(const TilePartial *__restrict__ 
 
 // growth: the live keys of one window's old table as partial records (aux = the key's touched word), to be
 // merged into its new table by k_merge_owned in rehash mode
-__global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, GrowRec *__restrict__ out, unsigned long long *n_out) {
+// (only_seq != 0: only the keys whose touched word carries that batch sequence -- an incremental checkpoint)
+__global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, GrowRec *__restrict__ out, unsigned long long *n_out,
+                                                  unsigned only_seq = 0) {
     const unsigned long long cap = (g.rmask + 1) << g.rbits;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < (int64_t)cap; base += stride) {
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, GrowRec *__restrict
         GrowRec p;
         if (i < (int64_t)cap) {
             const TileSlot sl = g.tab[i];
-            live = sl.wenc == g.wenc;
+            live = sl.wenc == g.wenc && (only_seq == 0 || (unsigned)(sl.touched >> 32) == only_seq);
             p.cell = sl.cell;
             p.wstart = wdec(sl.wenc);
             p.count = sl.count;
@@ -3679,6 +3681,9 @@ int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n) {
     return HM_OK;
 }
 
+// the state's version: bumped when a batch's merge begins (a failed call that left it unchanged did not touch the state)
+int64_t hm_state_version(const hm_ctx *ctx) { return ctx ? (int64_t)ctx->seq : -1; }
+
 int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n) {
     if (!ctx || !c) return HM_E_INVALID;
     for (int i = 0; i < n && i < 6; i++) c[i] = ctx->last_counts[i];
@@ -4209,6 +4214,31 @@ static void state_info_of(const hm_ctx *ctx, hm_state_info *info, int64_t n_keys
     info->h3_res = ctx->cfg.h3_res;
 }
 
+// every live window's keys (only_seq != 0: those the batch with that sequence touched) into recs[0, n)
+static int state_dump(hm_ctx *ctx, hm_state_rec *recs, int64_t n, unsigned only_seq) {
+    int rc;
+    if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(n, 1) * sizeof(GrowRec)))) return rc;
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
+    for (const auto &g : ctx->gens) {
+        GenDesc d{};
+        d.wenc = g.wenc;
+        d.tab = g.tab;
+        d.rbits = g.rbits;
+        d.rshift = (unsigned)g.log2cap - g.rbits;
+        d.rmask = (UINT64_C(1) << d.rshift) - 1;
+        hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
+                           (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD, only_seq);
+    }
+    HIPCHK(ctx, hipGetLastError());
+    unsigned long long dumped = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&dumped, ctx->d_scratch + REGROW_WORD, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if ((int64_t)dumped != n) return set_err(ctx, HM_E_STATE, "state dump found %llu keys, expected %lld", dumped, (long long)n);
+    if (n > 0) HIPCHK(ctx, hipMemcpy(recs, ctx->parts_regrow.p, n * sizeof(GrowRec), hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; i++) recs[i].reserved = 0;
+    return HM_OK;
+}
+
 int hm_state_export(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs, int64_t cap) {
     static_assert(sizeof(hm_state_rec) == sizeof(GrowRec), "hm_state_rec mirrors GrowRec");
     if (!ctx || !info) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
@@ -4219,26 +4249,45 @@ int hm_state_export(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs, int64_
     state_info_of(ctx, info, n);
     if (!recs) return HM_OK;
     if (cap < n) return set_err(ctx, HM_E_INVALID, "state of %lld keys does not fit %lld records", (long long)n, (long long)cap);
-    if (n == 0) return HM_OK;
-    int rc;
-    if ((rc = ensure(ctx, ctx->parts_regrow, n * sizeof(GrowRec)))) return rc;
-    HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
-    for (const auto &g : ctx->gens) {
-        GenDesc d{};
-        d.wenc = g.wenc;
-        d.tab = g.tab;
-        d.rbits = g.rbits;
-        d.rshift = (unsigned)g.log2cap - g.rbits;
-        d.rmask = (UINT64_C(1) << d.rshift) - 1;
-        hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
-                           (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD);
+    return n == 0 ? HM_OK : state_dump(ctx, recs, n, 0);
+}
+
+// Incremental checkpoint (Spark's state store writes a delta file per version): the keys the last batch touched, with
+// their cumulative values; together with an older full export and the deltas between, the state after this batch is
+// the last-written record of every key whose window end > info.prev_watermark_ms (the batch's eviction watermark).
+int hm_state_export_touched(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs, int64_t cap, int64_t *n_out) {
+    if (!ctx || !info || !n_out) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->stage != 0) return set_err(ctx, HM_E_STATE, "hm_state_export_touched between stage calls");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int64_t live = 0;
+    for (const auto &g : ctx->gens) live += g.keys;
+    state_info_of(ctx, info, live);
+    // the last batch's touched keys that are still live (a touched key of an evicted window went with its table)
+    int64_t n = 0;
+    if (ctx->seq > 0 && !ctx->gens.empty()) {
+        int rc;
+        if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(live, 1) * sizeof(GrowRec)))) return rc;
+        HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
+        for (const auto &g : ctx->gens) {
+            GenDesc d{};
+            d.wenc = g.wenc;
+            d.tab = g.tab;
+            d.rbits = g.rbits;
+            d.rshift = (unsigned)g.log2cap - g.rbits;
+            d.rmask = (UINT64_C(1) << d.rshift) - 1;
+            hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
+                               (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD, seq32(ctx));
+        }
+        HIPCHK(ctx, hipGetLastError());
+        unsigned long long dumped = 0;
+        HIPCHK(ctx, hipMemcpyAsync(&dumped, ctx->d_scratch + REGROW_WORD, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        n = (int64_t)dumped;
     }
-    HIPCHK(ctx, hipGetLastError());
-    unsigned long long dumped = 0;
-    HIPCHK(ctx, hipMemcpyAsync(&dumped, ctx->d_scratch + REGROW_WORD, 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    if ((int64_t)dumped != n) return set_err(ctx, HM_E_STATE, "state dump found %llu keys, expected %lld", dumped, (long long)n);
-    HIPCHK(ctx, hipMemcpy(recs, ctx->parts_regrow.p, n * sizeof(GrowRec), hipMemcpyDeviceToHost));
+    *n_out = n;
+    if (!recs) return HM_OK;
+    if (cap < n) return set_err(ctx, HM_E_INVALID, "%lld touched keys do not fit %lld records", (long long)n, (long long)cap);
+    if (n > 0) HIPCHK(ctx, hipMemcpy(recs, ctx->parts_regrow.p, n * sizeof(GrowRec), hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < n; i++) recs[i].reserved = 0;
     return HM_OK;
 }

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE,
 HM_ABI_VERSION = 9
 HM_MEM_HOST = 0
 HM_MEM_DEVICE = 1
+HM_E_INVALID, HM_E_HIP, HM_E_NOMEM, HM_E_OVERFLOW, HM_E_STATE, HM_E_UNSUPPORTED = -1, -2, -3, -4, -5, -6
 HM_STAGE_SUMMARY_WORDS = 8200
 HM_TILE_REC_BYTES = 48       # table mode's tile partial
 HM_TILE_KEY_BYTES = 8        # direct path: key stream
@@ -110,6 +111,8 @@ SIGNATURES = {
     "hm_selftest_glibc_libm_host": (c_i32, [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "hm_selftest_glibc_libm_device": (c_i32, [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32]),
     "hm_state_export": (c_i32, [c_vp, _P(HmStateInfo), c_vp, c_i64]),
+    "hm_state_export_touched": (c_i32, [c_vp, _P(HmStateInfo), c_vp, c_i64, c_vp]),
+    "hm_state_version": (c_i64, [c_vp]),
     "hm_state_import": (c_i32, [c_vp, _P(HmStateInfo), c_vp]),
     "hm_last_windows": (c_i32, [c_vp, c_vp, c_i64, _P(c_i64)]),
     "hm_encode_tile_updates": (c_i32, [c_vp, _P(HmTileDocCfg), c_i32, _P(c_vp), _P(c_vp), _P(c_i64)]),
@@ -153,11 +156,19 @@ def load():
     return lib
 
 
+class MobheatError(RuntimeError):
+    """A failed library call: `code` is the C-ABI error code (HM_E_*)."""
+
+    def __init__(self, msg, code):
+        super().__init__(msg)
+        self.code = code
+
+
 def check(rc, ctx=None, what="mobheat"):
     if rc < 0:
         lib = load()
         msg = lib.hm_last_error(ctx)
-        raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+        raise MobheatError(f"{what} failed ({rc}): {msg.decode() if msg else ''}", rc)
     return rc
 
 

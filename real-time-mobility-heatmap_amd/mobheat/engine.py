@@ -179,6 +179,24 @@ class HeatmapEngine:
                   "hm_state_export")
         return {f: int(getattr(info, f)) for f in _INFO_FIELDS}, recs
 
+    def state_version(self):
+        """Bumped whenever a batch starts merging into the persistent state (a failed call that left it unchanged did
+        not touch the state)."""
+        return int(self._lib.hm_state_version(self._ctx))
+
+    def export_state_delta(self):
+        """(info dict, records) of the keys the last batch touched: an incremental checkpoint (see merge_state)."""
+        info = HmStateInfo()
+        n = ctypes.c_int64()
+        check(self._lib.hm_state_export_touched(self._ctx, ctypes.byref(info), None, 0, ctypes.byref(n)), self._ctx,
+              "hm_state_export_touched")
+        recs = np.zeros(int(n.value), STATE_REC_DTYPE)
+        if recs.size:
+            check(self._lib.hm_state_export_touched(self._ctx, ctypes.byref(info), ptr(recs), recs.size, ctypes.byref(n)),
+                  self._ctx, "hm_state_export_touched")
+            recs = recs[: int(n.value)]
+        return {f: int(getattr(info, f)) for f in _INFO_FIELDS}, recs
+
     def import_state(self, info, recs):
         """Restore an exported state into this engine (which must not have processed a batch yet)."""
         recs = np.ascontiguousarray(recs, dtype=STATE_REC_DTYPE)
@@ -289,6 +307,28 @@ def _host_statements(pb, po, nd, copy):
     buf = (np.ctypeslib.as_array(ctypes.cast(pb, ctypes.POINTER(ctypes.c_uint8)), shape=(total,))
            if total else np.zeros(0, np.uint8))
     return (buf.copy(), offs.copy()) if copy else (buf, offs)
+
+
+def merge_state(base, deltas):
+    """The state after the last of `deltas` from a full export `base` and the incremental exports of the batches since,
+    in order (each an (info, recs) pair): the last-written record of every (cell, windowStart) key, keeping the keys
+    whose window outlives the last batch's eviction watermark (hm_state_export_touched).  Returns (info, recs)."""
+    info, recs = base
+    parts = [recs] + [d[1] for d in deltas]
+    if deltas:
+        info = deltas[-1][0]
+    allr = np.concatenate(parts) if len(parts) > 1 else recs
+    if allr.size:
+        # last occurrence of each key wins: reverse, stable unique on (cell, window_start), map back
+        rev = allr[::-1]
+        key = np.empty(rev.size, dtype=[("c", "<u8"), ("w", "<i8")])
+        key["c"], key["w"] = rev["cell"], rev["window_start_us"]
+        _, first = np.unique(key, return_index=True)
+        allr = rev[np.sort(first)]
+        tile_us = int(info["tile_us"])
+        allr = allr[allr["window_start_us"] + tile_us > int(info["prev_watermark_ms"]) * 1000]
+    info = dict(info, n_keys=int(allr.size))
+    return info, np.ascontiguousarray(allr)
 
 
 def save_state_file(path, info, recs):

@@ -32,15 +32,18 @@ TTL_MIN = int(os.getenv("TTL_MINUTES", "45"))
 WATERMARK_DELAY_MS = 10 * 60 * 1000          # withWatermark("eventTs", "10 minutes"), :107
 BULK_CHUNK = 1000                              # :191, :230
 DEVICE = int(os.getenv("MOBHEAT_DEVICE", os.getenv("LOCAL_RANK", "0")))
-# Spark keeps the aggregation state under checkpointLocation (:37, :244); the GPU state is checkpointed beside it
-# (CHECKPOINT_DIR/mobheat-state/state-<epoch>.npz) after each committed batch.  On by default whenever CHECKPOINT is
-# set (the reference always restores its state from there); MOBHEAT_STATE_CHECKPOINT=0/1 overrides.
+# Spark keeps the aggregation state under checkpointLocation, default /tmp/heatmap-checkpoint (:37, :244), and always
+# restores it from there; the GPU state is checkpointed beside it (CHECKPOINT_DIR/mobheat-state) after each committed
+# batch, like Spark's HDFS state store: a delta file per batch (the keys the batch touched) and a full snapshot every
+# STATE_FULL_EVERY batches (spark.sql.streaming.stateStore.minDeltasForSnapshot = 10).  MOBHEAT_STATE_CHECKPOINT=0
+# turns it off.
 CHECKPOINT_DIR = os.getenv("CHECKPOINT", "/tmp/heatmap-checkpoint")
-STATE_CHECKPOINT = os.getenv("MOBHEAT_STATE_CHECKPOINT", "1" if "CHECKPOINT" in os.environ else "0") == "1"
-STATE_KEEP = 2     # the newest two: an epoch replayed after a crash between our save and Spark's commit log
+STATE_CHECKPOINT = os.getenv("MOBHEAT_STATE_CHECKPOINT", "1") == "1"
+STATE_FULL_EVERY = int(os.getenv("MOBHEAT_STATE_FULL_EVERY", "10"))
 
 _ENGINE = None
-_LAST_EPOCH = None   # the last epoch merged into _ENGINE's state (a replay of it must not be merged twice)
+_LAST_EPOCH = None   # the last epoch committed (merged and written) from _ENGINE's state
+_PENDING = None      # (epoch, result, dictionaries): a batch merged into _ENGINE's state whose writes did not complete
 
 
 def _state_dir():
@@ -48,18 +51,35 @@ def _state_dir():
 
 
 def _checkpoints():
-    """[(epoch, path)] of the saved states, oldest first."""
+    """[(epoch, kind, path)] of the saved states, oldest first; kind "full" (state-<epoch>.npz) or "delta"."""
     d = _state_dir()
     if not os.path.isdir(d):
         return []
     out = []
     for name in os.listdir(d):
-        if name.startswith("state-") and name.endswith(".npz"):
-            try:
-                out.append((int(name[6:-4]), os.path.join(d, name)))
-            except ValueError:
-                pass
+        for prefix, kind in (("state-", "full"), ("delta-", "delta")):
+            if name.startswith(prefix) and name.endswith(".npz"):
+                try:
+                    out.append((int(name[len(prefix):-4]), kind, os.path.join(d, name)))
+                except ValueError:
+                    pass
     return sorted(out)
+
+
+def restore_state(eng, epoch_id):
+    """Load the state after the newest checkpointed epoch older than `epoch_id` into a fresh engine: the newest full
+    snapshot before it and the deltas of the epochs since (merged on the host, engine.merge_state).  Returns that
+    epoch or None."""
+    from .engine import load_state_file, merge_state
+    cps = [c for c in _checkpoints() if c[0] < int(epoch_id)]
+    fulls = [c for c in cps if c[1] == "full"]
+    if not fulls:
+        return None
+    f = fulls[-1]
+    deltas = [c for c in cps if c[1] == "delta" and c[0] > f[0]]
+    info, recs = merge_state(load_state_file(f[2]), [load_state_file(d[2]) for d in deltas])
+    eng.import_state(info, recs)
+    return deltas[-1][0] if deltas else f[0]
 
 
 def get_engine(epoch_id=None):
@@ -74,28 +94,42 @@ def get_engine(epoch_id=None):
         eng = HeatmapEngine(h3_res=H3_RES, tile_minutes=TILE_MIN, watermark_delay_ms=WATERMARK_DELAY_MS,
                             device=DEVICE)
         if STATE_CHECKPOINT and epoch_id is not None:
-            older = [(e, p) for e, p in _checkpoints() if e < int(epoch_id)]
-            if older:
-                eng.load_state(older[-1][1])
+            restore_state(eng, epoch_id)
         _ENGINE = eng
     return _ENGINE
 
 
 def save_state_checkpoint(epoch_id):
-    """Write the engine's state after `epoch_id` and keep the newest STATE_KEEP checkpoints."""
+    """Checkpoint the engine's state after `epoch_id`: a full snapshot when none exists or STATE_FULL_EVERY deltas
+    followed the newest one, else the batch's delta; keeps the files from the second-newest snapshot on (a replay of
+    an epoch whose save became a snapshot restores from the one before)."""
+    from .engine import save_state_file
     os.makedirs(_state_dir(), exist_ok=True)
-    get_engine().save_state(os.path.join(_state_dir(), f"state-{int(epoch_id)}.npz"))
-    for _, p in _checkpoints()[:-STATE_KEEP]:
-        os.remove(p)
+    cps = [c for c in _checkpoints() if c[0] < int(epoch_id)]
+    fulls = [c for c in cps if c[1] == "full"]
+    since = [c for c in cps if c[1] == "delta" and fulls and c[0] > fulls[-1][0]]
+    eng = get_engine()
+    if not fulls or len(since) >= STATE_FULL_EVERY:
+        eng.save_state(os.path.join(_state_dir(), f"state-{int(epoch_id)}.npz"))
+    else:
+        info, recs = eng.export_state_delta()
+        save_state_file(os.path.join(_state_dir(), f"delta-{int(epoch_id)}.npz"), info, recs)
+    cps = _checkpoints()
+    fulls = [c for c in cps if c[1] == "full"]
+    if len(fulls) > 2:
+        for e, _, p in cps:
+            if e < fulls[-2][0]:
+                os.remove(p)
 
 
 def reset_engine():
-    """Drop the persistent state (a new streaming query, or a batch that failed after its merge)."""
-    global _ENGINE, _LAST_EPOCH
+    """Drop the persistent state (a new streaming query, or a batch that failed after its merge began)."""
+    global _ENGINE, _LAST_EPOCH, _PENDING
     if _ENGINE is not None:
         _ENGINE.close()
     _ENGINE = None
     _LAST_EPOCH = None
+    _PENDING = None
 
 
 # ------------------ sinks ------------------
@@ -118,8 +152,15 @@ class MongoSink:
             self._client = MongoClient(uri)
             self._db = self._client[self._dbname]
 
+    def _pymongo_db(self):
+        if getattr(self, "_db", None) is None:   # (the wire path writes the encoded statements; pymongo the rest)
+            from pymongo import MongoClient
+            self._client = MongoClient(f"mongodb://{self._wire.host}:{self._wire.port}")
+            self._db = self._client[self._dbname]
+        return self._db
+
     def bulk_write(self, collection, ops):
-        self._db[collection].bulk_write(ops, ordered=False)
+        self._pymongo_db()[collection].bulk_write(ops, ordered=False)
 
     def update_statements(self, collection, buf, offs):
         """Pre-encoded update statements (bytes buf, offsets[n+1]) in unordered commands of <= BULK_CHUNK."""
@@ -140,13 +181,14 @@ class MongoSink:
         from bson.son import SON
         from . import wire
         cmd = SON([("update", collection), ("updates", statements), ("ordered", False)])
+        db = self._pymongo_db()
         try:
-            wc = self._db[collection].write_concern.document
+            wc = db[collection].write_concern.document
         except (TypeError, AttributeError, KeyError):
             wc = None
         if wc:
             cmd["writeConcern"] = wc
-        wire.raise_write_errors(self._db.command(cmd))
+        wire.raise_write_errors(db.command(cmd))
 
     def close(self):
         if self._wire is not None:
@@ -224,7 +266,9 @@ def _event_ts_us(t):
     # to_timestamp reads them in the session time zone (UTC, :45)
     import pandas as pd
     raw = t.column("ts").to_pandas()
-    zoned = raw.astype("string").str.strip().str.contains(r"(?:Z|[+-]\d{2}(?::?\d{2})?)$", regex=True).fillna(False).to_numpy(bool)
+    # (a zone only after a time component: the day of a date-only '2024-01-15' is no offset)
+    zoned = raw.astype("string").str.strip().str.contains(r"[T ]\d{2}:\d{2}.*(?:Z|[+-]\d{2}(?::?\d{2})?)$",
+                                                          regex=True).fillna(False).to_numpy(bool)
     vals = np.zeros(len(raw), np.int64)
     valid = np.zeros(len(raw), bool)
     for sel in (zoned, ~zoned):
@@ -374,41 +418,64 @@ def _flush_statements(sink, collection, buf, offs):
 
 
 # ------------------ the drop-in boundary ------------------
-def foreach_batch_func(df, epoch_id: int):
-    """Runs on each micro-batch (reference heatmap_stream.py:150): tiles + latest positions -> MongoDB."""
-    global _LAST_EPOCH
-    cols = batch_columns(df)
-    eng = get_engine(epoch_id)
-    try:
-        # (the tile and latest rows stay on the device: the statements are encoded there from them)
-        if "kafka" in cols:   # raw Kafka values: from_json + to_timestamp on the GPU (row f1)
+def _process(eng, epoch_id, cols):
+    """Merge the batch into the engine's state; (result, the string dictionaries of its vkeys)."""
+    from . import _lib
+    # (the tile and latest rows stay on the device: the statements are encoded there from them)
+    if "kafka" in cols:   # raw Kafka values: from_json + to_timestamp on the GPU (row f1)
+        try:
             res, kb = eng.process_kafka(epoch_id, *cols["kafka"], rows_on_device=True)
-            dicts = (kb.providers, kb.vehicles)
-        else:
-            res = eng.process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"], cols["speed_valid"],
-                                    cols["vkey"], cols["row_valid"], rows_on_device=True)
-            dicts = (cols["provider_uniques"], cols["vehicle_uniques"])
-    except BaseException:
-        reset_engine()   # the state may hold part of the batch: the next attempt rebuilds it from the checkpoint
-        raise
-    _LAST_EPOCH = int(epoch_id)
-    committed = False
+            return res, (kb.providers, kb.vehicles)
+        except RuntimeError as e:
+            if getattr(e, "code", None) != _lib.HM_E_UNSUPPORTED:
+                raise
+        # a record outside the device decoder's scope: decode the batch on the host (kafka_host) -- one such record
+        # must not stop the stream (Spark would replay the same offsets into the same failure)
+        from . import kafka_host
+        cols = batch_columns(kafka_host.decode_table(*cols["kafka"]))
+    res = eng.process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"], cols["speed_valid"],
+                            cols["vkey"], cols["row_valid"], rows_on_device=True)
+    return res, (cols["provider_uniques"], cols["vehicle_uniques"])
+
+
+def foreach_batch_func(df, epoch_id: int):
+    """Runs on each micro-batch (reference heatmap_stream.py:150): tiles + latest positions -> MongoDB.
+
+    Failures keep the reference's semantics (the exception fails the batch and Spark re-runs the epoch) without
+    losing state: a batch that fails before its merge leaves the state untouched (hm_state_version); one that fails
+    during the merge drops the state, which the retry rebuilds from the checkpoints; one whose writes fail keeps the
+    merged state and, when Spark re-runs that epoch, writes the same documents again without merging twice."""
+    global _LAST_EPOCH, _PENDING
+    epoch = int(epoch_id)
+    if _PENDING is not None and _PENDING[0] == epoch and _ENGINE is not None:
+        res, dicts = _PENDING[1], _PENDING[2]   # the replay of the epoch whose writes failed: its state is in place
+    else:
+        if _PENDING is not None:   # another epoch while one is uncommitted: that merge never committed
+            reset_engine()
+        cols = batch_columns(df)
+        eng = get_engine(epoch)
+        v0 = eng.state_version()
+        try:
+            res, dicts = _process(eng, epoch, cols)
+        except BaseException:
+            if _ENGINE is not None and _ENGINE.state_version() != v0:
+                reset_engine()   # the merge began: the state may hold part of the batch
+            raise
+        _PENDING = (epoch, res, dicts)
+    eng = get_engine()
     sink = SINK_FACTORY()
     try:
         # ---- 1) Upsert tiles (TTL via staleAt): the UpdateOne statements, BSON-encoded on the GPU ----
-        buf, offs = get_engine().encode_tile_updates(CITY, TTL_MIN)
+        buf, offs = eng.encode_tile_updates(CITY, TTL_MIN)
         _flush_statements(sink, "tiles", buf, offs)
         # ---- 2) latest per (provider, vehicleId) within this micro-batch: statements encoded on the GPU ----
         if res.n_latest:
-            buf, offs = get_engine().encode_position_updates(*dicts)   # (local offsets of the rows' 900-s buckets)
+            buf, offs = eng.encode_position_updates(*dicts)   # (local offsets of the rows' 900-s buckets)
             _flush_statements(sink, "positions_latest", buf, offs)
         if STATE_CHECKPOINT:   # after the writes succeeded: the batch is committed
-            save_state_checkpoint(epoch_id)
-        committed = True
+            save_state_checkpoint(epoch)
     finally:
         sink.close()
-        if not committed:
-            # the writes (or the checkpoint) failed and Spark will re-run this epoch: drop the state that already
-            # holds it, so the retry starts from the checkpoint of the epoch before (or empty without checkpoints)
-            reset_engine()
+    _PENDING = None
+    _LAST_EPOCH = epoch
     return res

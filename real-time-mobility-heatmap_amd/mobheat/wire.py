@@ -79,6 +79,7 @@ class WireMongoSink:
 
     def __init__(self, host, port, db, timeout=60.0):
         self.db = db
+        self.host, self.port = host, port
         self._sock = socket.create_connection((host, port), timeout=timeout)
         self._sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         self._rid = 1

@@ -31,3 +31,16 @@ def oracle_h3():
 def mobheat_lib():
     import mobheat
     return mobheat.load()
+
+
+@pytest.fixture(autouse=True)
+def _state_checkpoint_dir(tmp_path, monkeypatch):
+    """foreach_batch_func checkpoints its state by default (reference heatmap_stream.py:37,244): every test gets its
+    own checkpoint directory, so that no test resumes from another's files."""
+    d = str(tmp_path / "heatmap-checkpoint")
+    monkeypatch.setenv("CHECKPOINT", d)
+    try:
+        from mobheat import stream
+    except Exception:   # (the package is not importable in this environment: nothing to redirect)
+        return
+    monkeypatch.setattr(stream, "CHECKPOINT_DIR", d)

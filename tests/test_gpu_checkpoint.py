@@ -146,10 +146,38 @@ def test_import_errors():
     a.close()
 
 
-def test_foreach_batch_func_restart_replays_epoch(tmp_path, monkeypatch):
-    """foreach_batch_func with MOBHEAT_STATE_CHECKPOINT: a restart (new engine) resumes from the newest checkpoint
-    older than the incoming epoch -- also when that epoch itself was already checkpointed (crash before Spark's
-    commit log) -- and emits the same documents as the uninterrupted stream."""
+def test_incremental_checkpoint_equals_full_export():
+    """hm_state_export_touched after every batch (Spark's per-version delta files): a full export of batch 0 merged
+    with the deltas since (engine.merge_state: last write wins, windows evicted by the watermark dropped) equals the
+    full export after every later batch, record for record (cumulative counts and fp64 sums bit for bit)."""
+    from mobheat import HeatmapEngine
+    from mobheat.engine import merge_state
+    eng = HeatmapEngine(h3_res=9)
+    base, deltas = None, []
+
+    def keyed(recs):
+        o = np.lexsort((recs["window_start_us"], recs["cell"]))
+        return recs[o]
+    for e, b in enumerate(_batches(seed=37)):
+        eng.process_batch(e, **b)
+        if base is None:
+            base = eng.export_state()
+            continue
+        deltas.append(eng.export_state_delta())
+        info, recs = merge_state(base, deltas)
+        finfo, frecs = eng.export_state()
+        assert info == finfo, e
+        assert keyed(recs).tobytes() == keyed(frecs).tobytes(), e
+    assert sum(d[1].size for d in deltas) > 0
+    eng.close()
+
+
+@pytest.mark.parametrize("full_every", [10, 2])
+def test_foreach_batch_func_restart_replays_epoch(tmp_path, monkeypatch, full_every):
+    """foreach_batch_func with its default state checkpoints (a full snapshot, then per-batch deltas): a restart (new
+    engine) resumes from the state after the newest checkpointed epoch older than the incoming one -- also when that
+    epoch itself was already checkpointed (crash before Spark's commit log) -- and emits the same documents as the
+    uninterrupted stream."""
     import pandas as pd
     from mobheat import stream
 
@@ -176,6 +204,7 @@ def test_foreach_batch_func_restart_replays_epoch(tmp_path, monkeypatch):
     monkeypatch.setattr(stream, "SINK_FACTORY", Capture)
     monkeypatch.setattr(stream, "CHECKPOINT_DIR", str(tmp_path))
     monkeypatch.setattr(stream, "STATE_CHECKPOINT", True)
+    monkeypatch.setattr(stream, "STATE_FULL_EVERY", full_every)
 
     def run(epochs):
         out = []
@@ -191,9 +220,55 @@ def test_foreach_batch_func_restart_replays_epoch(tmp_path, monkeypatch):
     ref = run(range(5))
     monkeypatch.setattr(stream, "STATE_CHECKPOINT", True)
     stream.reset_engine()
-    got = run(range(3))                                    # epochs 0..2 committed, checkpoints 1 and 2 kept
-    assert [e for e, _ in stream._checkpoints()] == [1, 2]
+    got = run(range(3))                                    # epochs 0..2 committed: a snapshot, then deltas
+    assert [(e, k) for e, k, _ in stream._checkpoints()] == [(0, "full"), (1, "delta"), (2, "delta")]
     stream.reset_engine()                                  # restart; Spark replays epoch 2 (its commit was lost)
     got += run([2, 3, 4])
     stream.reset_engine()
     assert got[:3] == ref[:3] and got[3:] == ref[2:]
+
+
+def test_foreach_batch_func_failed_writes_without_checkpoints(monkeypatch):
+    """Checkpoints off: a batch whose writes fail keeps its merged GPU state, and Spark's re-run of the epoch writes the
+    same documents again without merging the batch twice -- the stream then continues exactly like an uninterrupted
+    one (one transient Mongo error no longer discards the tile state)."""
+    import pandas as pd
+    from mobheat import stream
+
+    class Capture:
+        ops = []
+        fail = False
+
+        def update_raw(self, coll, stmts):
+            import bson
+            if Capture.fail:
+                raise IOError("mongo down")
+            Capture.ops.extend((coll, d["q"]["_id"], d["u"]) for d in (bson.decode(st.raw) for st in stmts))
+
+        def close(self):
+            pass
+
+    raw = _batches(seed=36)
+    bs = [pd.DataFrame({"provider": ["p"] * len(b["lat"]), "vehicleId": [f"v{int(v)}" for v in b["vkey"]],
+                        "lat": b["lat"], "lon": b["lon"], "speedKmh": np.where(b["speed_valid"], b["speed"], np.nan),
+                        "eventTs": pd.to_datetime(b["ts_us"], unit="us")}) for b in (raw[0], raw[1], raw[3], raw[4])]
+    monkeypatch.setattr(stream, "SINK_FACTORY", Capture)
+    monkeypatch.setattr(stream, "STATE_CHECKPOINT", False)
+
+    def run(plan):
+        out = []
+        for e, fail in plan:
+            Capture.ops, Capture.fail = [], fail
+            if fail:
+                with pytest.raises(IOError):
+                    stream.foreach_batch_func(bs[e], e)
+                continue
+            stream.foreach_batch_func(bs[e], e)
+            out.append(sorted((c, i, d["$set"].get("count"), str(d["$set"].get("ts"))) for c, i, d in Capture.ops))
+        return out
+    stream.reset_engine()
+    ref = run([(0, False), (1, False), (2, False), (3, False)])
+    stream.reset_engine()
+    got = run([(0, False), (1, True), (1, True), (1, False), (2, False), (3, False)])
+    stream.reset_engine()
+    assert got == ref

@@ -166,3 +166,44 @@ def test_foreach_batch_func_kafka_values_equal_decoded_frame():
         gc, wc = gs.pop("centroid")["coordinates"], ws.pop("centroid")["coordinates"]
         assert close(gc[0], wc[0]) and close(gc[1], wc[1])
         assert gs == ws and g["q"] == w["q"]
+
+
+def test_foreach_batch_func_kafka_values_with_unsupported_records():
+    """A batch holding records outside the device decoder's scope (a number as vehicleId, an object as provider) no
+    longer fails (hm_decode_json's HM_E_UNSUPPORTED -> the host decode of mobheat.kafka_host): it writes the documents
+    of the same batch decoded on the host, the odd records' strings being their JSON text as Spark stores them."""
+    import numpy as np
+    import pandas as pd
+    from mobheat import kafka_host, stream
+    rng = random.Random(19)
+    vals = _producer_values(rng, 5_000, 300) + [
+        b'{"provider":"mbta","vehicleId":1.5,"lat":42.3,"lon":-71.1,"speedKmh":10,"ts":"2025-10-04T10:22:05Z"}',
+        b'{"provider":{"a":1},"vehicleId":"v","lat":42.31,"lon":-71.11,"ts":"2025-10-04T10:22:05Z"}']
+
+    def run(df):
+        ops = {}
+
+        class Capture:
+            def update_raw(self, coll, stmts):
+                import bson
+                for st in stmts:
+                    d = bson.decode(st.raw)
+                    ops.setdefault(coll, {})[d["q"]["_id"]] = d
+
+            def close(self):
+                pass
+        stream.reset_engine()
+        stream.SINK_FACTORY = Capture
+        try:
+            stream.foreach_batch_func(df, 0)
+        finally:
+            stream.SINK_FACTORY = stream.MongoSink
+            stream.reset_engine()
+        return ops
+
+    got = run(pd.DataFrame({"value": vals}))
+    offs = np.cumsum([0] + [len(v) for v in vals])
+    want = run(kafka_host.decode_table(np.frombuffer(b"".join(vals), np.uint8), offs))
+    assert got["positions_latest"] == want["positions_latest"]
+    assert "mbta|1.5" in got["positions_latest"] and '{"a":1}|v' in got["positions_latest"]
+    assert got["tiles"].keys() == want["tiles"].keys() and len(got["tiles"]) > 100

@@ -152,3 +152,46 @@ def test_jackson_only_non_numeric_tokens(tok, val):
     o = _lib.json_records_selftest([('{"provider":"p","vehicleId":"v","lat":%s,"lon":1,"ts":"2025-10-04"}' % tok).encode()])
     assert o["flags"][0] & F["LAT"] and not o["flags"][0] & F["MALFORMED"]
     assert (math.isnan(val) and math.isnan(o["lat"][0])) or o["lat"][0] == val
+
+
+def _table_columns(t):
+    """kafka_host.decode_table's Arrow table -> the fixture's column form"""
+    lat = np.array([np.nan if v is None else v for v in t.column("lat").to_pylist()], np.float64)
+    lon = np.array([np.nan if v is None else v for v in t.column("lon").to_pylist()], np.float64)
+    spl = t.column("speedKmh").to_pylist()
+    ts = t.column("eventTs").cast("int64").to_pylist()
+    prov = [None if v is None else v.encode("utf-8") for v in t.column("provider").to_pylist()]
+    veh = [None if v is None else v.encode("utf-8") for v in t.column("vehicleId").to_pylist()]
+    return dict(lat=lat, lon=lon, speed=np.array([0.0 if v is None else v for v in spl]),
+                speed_valid=np.array([v is not None for v in spl]), ts_us=np.array([0 if v is None else v for v in ts]),
+                ts_valid=np.array([v is not None for v in ts]), provider=prov, vehicleId=veh)
+
+
+def test_host_fallback_decodes_the_fixture_like_the_device():
+    """mobheat.kafka_host (the product's host decode for batches with records outside the device decoder's scope)
+    gives every fixture record the columns the device decoder and the oracle give it."""
+    from mobheat import kafka_host
+    values, z = _golden()
+    offs = np.cumsum([0] + [len(v) for v in values])
+    c = _table_columns(kafka_host.decode_table(np.frombuffer(b"".join(values), np.uint8), offs))
+    for k in ("lat", "lon", "speed"):
+        assert _same_f64(c[k], z[k]).all(), k
+    assert np.array_equal(c["speed_valid"], z["speed_valid"]) and np.array_equal(c["ts_valid"], z["ts_valid"])
+    assert np.array_equal(np.where(c["ts_valid"], c["ts_us"], 0), np.where(z["ts_valid"], z["ts_us"], 0))
+    assert c["provider"] == _strings(z["provider_present"], z["provider_bytes"], z["provider_len"])
+    assert c["vehicleId"] == _strings(z["vehicle_present"], z["vehicle_bytes"], z["vehicle_len"])
+
+
+def test_host_fallback_writes_non_string_values_as_jackson_text():
+    """The records the device flags (a number or an object in a StringType field) become that value's JSON text as
+    Spark's JacksonParser stores it (copyCurrentStructure: compact JSON, Double.toString for floating point)."""
+    from mobheat import kafka_host
+    z = np.load(os.path.join(HERE, "golden", "kafka_values.npz"))
+    ub, uo = z["unsupported_bytes"].tobytes(), z["unsupported_offsets"]
+    recs = [kafka_host.decode_record(ub[uo[i]:uo[i + 1]]) for i in range(uo.size - 1)]
+    assert recs[0]["vehicleId"] == "1.5" and recs[1]["provider"] == '{"a":1}'
+    for v, want in ((1e10, "1.0E10"), (123456.0, "123456.0"), (1e-4, "1.0E-4"), (0.001, "0.001"), (-2.5e-7, "-2.5E-7"),
+                    (12345678.9, "1.23456789E7"), (9999999.0, "9999999.0"), (-0.0, "-0.0"), (100.0, "100.0")):
+        assert kafka_host.java_double(v) == want, v
+    r = kafka_host.decode_record(b'{"provider":[1,2.5,"x",null,true],"vehicleId":{"k":{"z":-3}},"lat":1,"lon":2,"ts":"2025-10-04"}')
+    assert r["provider"] == '[1,2.5,"x",null,true]' and r["vehicleId"] == '{"k":{"z":-3}}'

@@ -135,8 +135,10 @@ def test_iso_ts_strings_parse_like_to_timestamp():
 
 def test_state_checkpoint_files_and_resume_choice(tmp_path, monkeypatch):
     """CPU: the state checkpoint's file format round-trips (plain arrays, no pickles) and a restarted engine
-    resumes from the newest checkpoint OLDER than the incoming epoch (Spark re-runs the first uncommitted epoch
-    on the state of the one before it, reference heatmap_stream.py:37,244)."""
+    resumes from the state after the newest checkpointed epoch OLDER than the incoming one (Spark re-runs the first
+    uncommitted epoch on the state of the one before it, reference heatmap_stream.py:37,244): the newest full
+    snapshot before it plus the deltas since, the last-written record of each key winning and windows evicted by the
+    last delta's watermark dropped (engine.merge_state)."""
     from mobheat import engine as eng_mod
     from mobheat._lib import STATE_REC_DTYPE
     recs = np.zeros(3, STATE_REC_DTYPE)
@@ -150,14 +152,14 @@ def test_state_checkpoint_files_and_resume_choice(tmp_path, monkeypatch):
     assert info2 == info
     np.testing.assert_array_equal(recs2.view(np.uint8), recs.view(np.uint8))
 
-    loaded = []
+    imported = []
 
     class FakeEngine:
         def __init__(self, **kw):
             pass
 
-        def load_state(self, path):
-            loaded.append(os.path.basename(path))
+        def import_state(self, info, recs):
+            imported.append((info, {(int(r["cell"]), int(r["window_start_us"])): int(r["count"]) for r in recs}))
 
         def close(self):
             pass
@@ -166,15 +168,35 @@ def test_state_checkpoint_files_and_resume_choice(tmp_path, monkeypatch):
     monkeypatch.setattr(stream, "CHECKPOINT_DIR", str(tmp_path))
     monkeypatch.setattr(stream, "STATE_CHECKPOINT", True)
     os.makedirs(stream._state_dir())
-    for e in (3, 4, 12):
-        open(os.path.join(stream._state_dir(), f"state-{e}.npz"), "wb").close()
+    T = 300_000_000
+    w0, w1 = 100 * T, 101 * T
+
+    def write(kind, epoch, keys, prev_wm_ms=0):
+        r = np.zeros(len(keys), STATE_REC_DTYPE)
+        for k, (c, w, n) in enumerate(keys):
+            r[k]["cell"], r[k]["window_start_us"], r[k]["count"] = c, w, n
+        inf = dict(info, epoch_id=epoch, n_keys=len(keys), prev_watermark_ms=prev_wm_ms)
+        eng_mod.save_state_file(os.path.join(stream._state_dir(), f"{kind}-{epoch}.npz"), inf, r)
+
+    write("state", 3, [(1, w0, 1), (2, w0, 1)])
+    write("delta", 4, [(2, w0, 5), (9, w1, 1)])
+    write("delta", 5, [(1, w0, 7)])
+    write("delta", 6, [(3, w1, 2)], prev_wm_ms=(w0 + T) // 1000)   # window w0 evicted by batch 6's watermark
+    write("state", 12, [(4, w1, 4)])
+    write("delta", 13, [(4, w1, 6), (5, w1, 1)])
     open(os.path.join(stream._state_dir(), "state-x.npz"), "wb").close()
-    assert [e for e, _ in stream._checkpoints()] == [3, 4, 12]
-    for epoch, want in ((13, "state-12.npz"), (12, "state-4.npz"), (5, "state-4.npz"), (4, "state-3.npz"), (3, None)):
+    assert [(e, k) for e, k, _ in stream._checkpoints()] == [(3, "full"), (4, "delta"), (5, "delta"), (6, "delta"),
+                                                             (12, "full"), (13, "delta")]
+    cases = [(14, {(4, w1): 6, (5, w1): 1}), (13, {(4, w1): 4}), (12, {(3, w1): 2, (9, w1): 1}),
+             (6, {(1, w0): 7, (2, w0): 5, (9, w1): 1}), (5, {(1, w0): 1, (2, w0): 5, (9, w1): 1}),
+             (4, {(1, w0): 1, (2, w0): 1}), (3, None)]
+    for epoch, want in cases:
         stream.reset_engine()
-        loaded.clear()
+        imported.clear()
         stream.get_engine(epoch)
-        assert loaded == ([want] if want else [])
+        assert (imported[0][1] if imported else None) == want, epoch
+        if imported:
+            assert imported[0][0]["n_keys"] == len(want)
     stream.reset_engine()
 
 
@@ -339,21 +361,38 @@ def test_position_encoder_wide_time_span(tz):
         time.tzset()
 
 
-def test_failed_writes_and_replays_do_not_merge_twice(tmp_path, monkeypatch):
-    """CPU, host logic of foreach_batch_func: a batch whose Mongo writes fail must not leave its rows in the
-    state (Spark re-runs the epoch: reference heatmap_stream.py:192-235 raise, :249), and an epoch the live engine
-    already merged is re-run on the state of the epoch before it, not on top of itself."""
+@pytest.mark.parametrize("checkpoint", [True, False])
+def test_failed_writes_and_replays_do_not_merge_twice(tmp_path, monkeypatch, checkpoint):
+    """CPU, host logic of foreach_batch_func (reference heatmap_stream.py:150-249: an exception fails the batch and
+    Spark re-runs the epoch), with and without state checkpoints:
+      * a batch whose Mongo writes fail keeps its merged state; the re-run of that epoch writes the same documents
+        again without merging twice;
+      * an error before the merge (the state version unchanged: a decode error, a bad argument) keeps the engine;
+      * an error after the merge began drops the state; the retry rebuilds it from the checkpoints;
+      * an epoch the live engine already committed is re-run on the state of the epoch before it."""
+    from mobheat import engine as eng_mod
+    from mobheat._lib import STATE_REC_DTYPE
     created, merged = [], []
+    mode = {"fail_write": False, "fail_before": False, "fail_during": False}
 
     class FakeEngine:
         def __init__(self, **kw):
             self.epochs = []
+            self.version = 0
             created.append(self)
 
-        def load_state(self, path):
-            self.epochs.append(("loaded", os.path.basename(path)))
+        def state_version(self):
+            return self.version
+
+        def import_state(self, info, recs):
+            self.epochs.append(("restored", int(info["epoch_id"])))
 
         def process_batch(self, epoch_id, *a, **kw):
+            if mode["fail_before"]:
+                raise RuntimeError("bad input")
+            self.version += 1
+            if mode["fail_during"]:
+                raise RuntimeError("device fault")
             self.epochs.append(epoch_id)
             merged.append(epoch_id)
 
@@ -366,18 +405,26 @@ def test_failed_writes_and_replays_do_not_merge_twice(tmp_path, monkeypatch):
             doc = np.frombuffer(bson.encode({"q": {"_id": "x"}}), np.uint8)
             return doc, np.array([0, doc.size], np.int64)
 
+        def _info(self):
+            return dict(epoch_id=self.epochs[-1] if self.epochs and isinstance(self.epochs[-1], int) else -1, n_keys=0,
+                        watermark_ms=0, prev_watermark_ms=0, tile_us=300_000_000, watermark_delay_ms=600_000, h3_res=8)
+
         def save_state(self, path):
-            open(path, "wb").close()
+            eng_mod.save_state_file(path, self._info(), np.zeros(0, STATE_REC_DTYPE))
+
+        def export_state_delta(self):
+            return self._info(), np.zeros(0, STATE_REC_DTYPE)
 
         def close(self):
             pass
 
-    fail = {"on": False}
+    writes = []
 
     class Sink:
         def update_raw(self, coll, statements):
-            if fail["on"]:
+            if mode["fail_write"]:
                 raise IOError("mongo down")
+            writes.append(coll)
 
         def close(self):
             pass
@@ -385,22 +432,45 @@ def test_failed_writes_and_replays_do_not_merge_twice(tmp_path, monkeypatch):
     monkeypatch.setattr(stream, "HeatmapEngine", FakeEngine)
     monkeypatch.setattr(stream, "SINK_FACTORY", Sink)
     monkeypatch.setattr(stream, "CHECKPOINT_DIR", str(tmp_path))
-    monkeypatch.setattr(stream, "STATE_CHECKPOINT", True)
+    monkeypatch.setattr(stream, "STATE_CHECKPOINT", checkpoint)
     df = pd.DataFrame({"provider": ["p"], "vehicleId": ["v"], "lat": [1.0], "lon": [2.0], "speedKmh": [3.0],
                        "eventTs": pd.to_datetime([1759572000], unit="s")})
     stream.reset_engine()
     stream.foreach_batch_func(df, 0)
     stream.foreach_batch_func(df, 1)
     assert len(created) == 1 and created[0].epochs == [0, 1]
-    fail["on"] = True
+    # writes fail: the merged state stays, the re-run writes again without a second merge
+    mode["fail_write"] = True
     with pytest.raises(IOError):
         stream.foreach_batch_func(df, 2)
-    assert stream._ENGINE is None                        # the state holding epoch 2 was dropped
-    fail["on"] = False
-    stream.foreach_batch_func(df, 2)                     # the retry: a new engine from the checkpoint of epoch 1
-    assert created[-1].epochs == [("loaded", "state-1.npz"), 2]
-    stream.foreach_batch_func(df, 2)                     # a replay of a merged epoch in the same process
-    assert created[-1].epochs == [("loaded", "state-1.npz"), 2] and len(created) == 3
+    assert stream._ENGINE is created[0] and merged == [0, 1, 2]
+    mode["fail_write"] = False
+    n_w = len(writes)
+    stream.foreach_batch_func(df, 2)
+    assert merged == [0, 1, 2] and len(created) == 1 and len(writes) == n_w + 1
+    # an error before the merge keeps the engine
+    mode["fail_before"] = True
+    with pytest.raises(RuntimeError):
+        stream.foreach_batch_func(df, 3)
+    assert stream._ENGINE is created[0]
+    mode["fail_before"] = False
+    stream.foreach_batch_func(df, 3)
+    assert created[0].epochs == [0, 1, 2, 3] and len(created) == 1
+    # an error during the merge drops the state; the retry rebuilds it
+    mode["fail_during"] = True
+    with pytest.raises(RuntimeError):
+        stream.foreach_batch_func(df, 4)
+    assert stream._ENGINE is None
+    mode["fail_during"] = False
+    stream.foreach_batch_func(df, 4)
+    assert len(created) == 2
+    assert created[1].epochs == ([("restored", 3), 4] if checkpoint else [4])
+    # a replay of a committed epoch in the same process: the state of the epoch before it, then the batch once
+    stream.foreach_batch_func(df, 4)
+    assert len(created) == 3 and created[2].epochs == ([("restored", 3), 4] if checkpoint else [4])
+    if checkpoint:
+        kinds = [(e, k) for e, k, _ in stream._checkpoints()]
+        assert kinds[0] == (0, "full") and all(k == "delta" for _, k in kinds[1:])
     stream.reset_engine()
 
 
