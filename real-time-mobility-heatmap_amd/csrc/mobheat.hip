@@ -45,7 +45,7 @@ using namespace hm;
 
 __constant__ H3Tables c_tab;
 // glibc's sincos/acos/atan2/tan tables for the exact path (glibc_libm.h); c_tab.glm points here
-__device__ const glm::Tables g_glm = {GLM_TABLE_INIT};
+__device__ glm::Tables g_glm = {GLM_TABLE_INIT};   // (not const: a const namespace-scope symbol has internal linkage, which hipGetSymbolAddress cannot resolve)
 
 #include "h3_tables_host.h"
 static H3Tables make_tables() { return hm_make_tables(); }
@@ -2595,7 +2595,8 @@ struct hm_ctx {
     int merge_grid = 0;
     int64_t prev_agg_rows = 0, prev_keys = 0;   // aggregated rows and distinct keys of the last batch
     bool last_table = false;
-    int64_t last_counts[6] = {0, 0, 0, 0, 0, 0};   // hm_last_counts
+    int64_t last_counts[6] = {0, 0, 0, 0, 0, 0};   // hm_last_counts [0, 6) ([6], [7]: n_allocs, n_frees)
+    int64_t n_allocs = 0, n_frees = 0;             // device + pinned-host allocations / frees since create
     int64_t table_evicted = 0;                   // table mode: aggregates k_agg evicted into its buckets (last batch)
     // hm_decode_json (row f1): the values on the device, the decoded columns, the string dictionaries
     struct Dict {
@@ -2696,9 +2697,10 @@ static double wall_ms() {
     clock_gettime(CLOCK_MONOTONIC, &t);
     return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
 }
-static hipError_t dev_malloc(void **p, size_t bytes, const char *what) {
+static hipError_t dev_malloc(hm_ctx *ctx, void **p, size_t bytes, const char *what) {
     const double t0 = g_trace ? wall_ms() : 0;
     const hipError_t e = hipMalloc(p, bytes);
+    ctx->n_allocs++;
     if (g_trace) fprintf(stderr, "[mobheat] hipMalloc %-12s %10.3f GB %8.1f ms\n", what, bytes / 1e9, wall_ms() - t0);
     return e;
 }
@@ -2708,12 +2710,13 @@ static int ensure(hm_ctx *ctx, DevBuf &b, size_t bytes) {
     if (b.p) {
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         HIPCHK(ctx, hipFree(b.p));
+        ctx->n_frees++;
         b.p = nullptr;
         b.bytes = 0;
     }
     size_t want = std::max<size_t>(bytes, 256);
     want = (want + 4095) & ~(size_t)4095;
-    if (dev_malloc(&b.p, want, "buffer") != hipSuccess) {
+    if (dev_malloc(ctx, &b.p, want, "buffer") != hipSuccess) {
         (void)hipGetLastError();
         return set_err(ctx, HM_E_NOMEM, "hipMalloc(%zu) failed", want);
     }
@@ -2788,13 +2791,14 @@ static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **
         ctx->arena_used += (bytes + 255) & ~(size_t)255;
         return HM_OK;
     }
-    if (dev_malloc((void **)&t, bytes, "state table") != hipSuccess) {
+    if (dev_malloc(ctx, (void **)&t, bytes, "state table") != hipSuccess) {
         (void)hipGetLastError();
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         std::vector<std::pair<TileSlot *, int>> keep;
         for (auto &pt : ctx->pool)
-            if (in_arena(ctx, pt.first)) keep.push_back(pt); else (void)hipFree(pt.first);
+            if (in_arena(ctx, pt.first)) keep.push_back(pt); else { (void)hipFree(pt.first); ctx->n_frees++; }
         ctx->pool.swap(keep);
+        ctx->n_allocs++;
         if (hipMalloc(&t, bytes) != hipSuccess) {
             (void)hipGetLastError();
             return set_err(ctx, HM_E_NOMEM, "state table of 2^%d slots: out of device memory", log2cap);
@@ -2812,6 +2816,7 @@ static void table_release(hm_ctx *ctx, TileSlot *t, int log2cap) {
     for (size_t i = 0; own > 8 && i < ctx->pool.size();) {
         if (in_arena(ctx, ctx->pool[i].first)) { i++; continue; }
         (void)hipFree(ctx->pool[i].first);
+        ctx->n_frees++;
         ctx->pool.erase(ctx->pool.begin() + i);
         own--;
     }
@@ -3118,9 +3123,10 @@ static int dedup_prepare(hm_ctx *ctx, hm_ctx::DedupTable &d, int64_t n_keys, boo
     if (d.tab) {
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         HIPCHK(ctx, hipFree(d.tab));
+        ctx->n_frees++;
         d.tab = nullptr;
     }
-    if (dev_malloc((void **)&d.tab, want * sizeof(DedupSlot), "dedup table") != hipSuccess) {
+    if (dev_malloc(ctx, (void **)&d.tab, want * sizeof(DedupSlot), "dedup table") != hipSuccess) {
         (void)hipGetLastError();
         return set_err(ctx, HM_E_NOMEM, "dedup table alloc failed");
     }
@@ -3178,8 +3184,9 @@ static int stage_inputs(hm_ctx *ctx, const hm_batch_in *in, const double **lat, 
 
 static int ensure_host(hm_ctx *ctx, void **p, size_t &cap_el, size_t want_el, size_t el) {
     (void)cap_el;
-    if (*p) HIPCHK(ctx, hipHostFree(*p));
+    if (*p) { HIPCHK(ctx, hipHostFree(*p)); ctx->n_frees++; }
     *p = nullptr;
+    ctx->n_allocs++;
     HIPCHK(ctx, hipHostMalloc(p, std::max<size_t>(want_el, 1) * el, hipHostMallocDefault));
     return HM_OK;
 }
@@ -3596,7 +3603,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     }
     if (cfg->state_arena_bytes > 0) {
         ctx->arena_bytes = (size_t)cfg->state_arena_bytes & ~(size_t)255;
-        if (dev_malloc((void **)&ctx->arena, ctx->arena_bytes, "state arena") != hipSuccess) {
+        if (dev_malloc(ctx, (void **)&ctx->arena, ctx->arena_bytes, "state arena") != hipSuccess) {
             (void)hipGetLastError();
             ctx->arena = nullptr;
             ctx->err = "state arena: out of device memory";
@@ -3687,6 +3694,8 @@ int64_t hm_state_version(const hm_ctx *ctx) { return ctx ? (int64_t)ctx->seq : -
 int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n) {
     if (!ctx || !c) return HM_E_INVALID;
     for (int i = 0; i < n && i < 6; i++) c[i] = ctx->last_counts[i];
+    if (n > 6) c[6] = ctx->n_allocs;
+    if (n > 7) c[7] = ctx->n_frees;
     return HM_OK;
 }
 
@@ -4591,9 +4600,10 @@ __global__ __launch_bounds__(256) void k_check_offsets(const int64_t *__restrict
 
 static int host_pinned(hm_ctx *ctx, void **p, size_t &cap, size_t want) {
     if (*p && cap >= want) return HM_OK;
-    if (*p) HIPCHK(ctx, hipHostFree(*p));
+    if (*p) { HIPCHK(ctx, hipHostFree(*p)); ctx->n_frees++; }
     *p = nullptr;
     cap = std::max<size_t>(want, 4096);
+    ctx->n_allocs++;
     HIPCHK(ctx, hipHostMalloc(p, cap, hipHostMallocDefault));
     return HM_OK;
 }

@@ -266,10 +266,10 @@ class HeatmapEngine:
                 "partition": ms[6], "send": ms[7]}
 
     def last_counts(self):
-        c = (ctypes.c_int64 * 6)()
-        check(self._lib.hm_last_counts(self._ctx, c, 6), self._ctx)
+        c = (ctypes.c_int64 * 8)()
+        check(self._lib.hm_last_counts(self._ctx, c, 8), self._ctx)
         return {"state_new": c[0], "partials": c[1], "tiles": c[2], "table_mode": bool(c[3]), "evicted": c[4],
-                "sent": c[5]}
+                "sent": c[5], "allocs": c[6], "frees": c[7]}
 
     def _result_from_host(self, out, copy=True):
         def arr(p, n, dt):

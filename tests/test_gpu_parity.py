@@ -166,6 +166,36 @@ def test_state_read_regime_matches_oracle():
     eng.close()
 
 
+def test_steady_state_batches_allocate_nothing():
+    """The state-read regime with window growth, 30 one-minute batches at res 7 (half the points repeat, half are new
+    each minute, so a window's table grows during its life): after the first windows have been evicted, no batch
+    allocates or frees device or pinned memory (a hipMalloc/hipFree inside a step stalls it --
+    released window tables are pooled, the buffers only grow), and every batch still equals the oracle."""
+    from mobheat import HeatmapEngine
+    from oracle.spark_oracle import SparkHeatmapOracle
+    rng = np.random.default_rng(41)
+    n = 200_000
+    lat0 = np.degrees(np.arcsin(rng.uniform(-1.0, 1.0, n // 2)))
+    lon0 = rng.uniform(-180.0, 180.0, n // 2)
+    eng = HeatmapEngine(h3_res=7)
+    ora = SparkHeatmapOracle(h3_res=7)
+    counts = []
+    for epoch in range(30):
+        lat = np.concatenate([lat0, np.degrees(np.arcsin(rng.uniform(-1.0, 1.0, n // 2)))])
+        lon = np.concatenate([lon0, rng.uniform(-180.0, 180.0, n // 2)])
+        b = dict(lat=lat, lon=lon, ts_us=1_759_572_000_000_000 + epoch * 60_000_000 + rng.integers(0, 60_000_000, n),
+                 speed=rng.uniform(0, 90, n), speed_valid=rng.random(n) > 0.1,
+                 vkey=rng.integers(0, 5000, n).astype(np.uint64), row_valid=np.ones(n, bool))
+        res, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res, exp)
+        c = eng.last_counts()
+        counts.append((c["allocs"], c["frees"]))
+    steady = counts[16:]
+    assert all(x == steady[0] for x in steady), counts
+    print(f"allocations/frees since create after each batch: {counts}")
+    eng.close()
+
+
 def test_edge_semantics_batch():
     """Filter edges (+-90/+-180 inclusive, NaN, inf, null rows), window boundaries, negative timestamps,
     null and NaN speeds, duplicate vehicles with tied maxima."""
