@@ -2707,6 +2707,10 @@ static hipError_t dev_malloc(hm_ctx *ctx, void **p, size_t bytes, const char *wh
 
 static int ensure(hm_ctx *ctx, DevBuf &b, size_t bytes) {
     if (b.bytes >= bytes && b.p) return HM_OK;
+    size_t want = std::max<size_t>(bytes, 256);
+    // a regrowth takes 1.5x headroom: a size that creeps up over a window's life (the census of a growing window,
+    // its regrow records) then reallocates O(log) times instead of in every batch that grows it
+    if (b.p) want = std::max(want, b.bytes + b.bytes / 2);
     if (b.p) {
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         HIPCHK(ctx, hipFree(b.p));
@@ -2714,11 +2718,15 @@ static int ensure(hm_ctx *ctx, DevBuf &b, size_t bytes) {
         b.p = nullptr;
         b.bytes = 0;
     }
-    size_t want = std::max<size_t>(bytes, 256);
     want = (want + 4095) & ~(size_t)4095;
     if (dev_malloc(ctx, &b.p, want, "buffer") != hipSuccess) {
         (void)hipGetLastError();
-        return set_err(ctx, HM_E_NOMEM, "hipMalloc(%zu) failed", want);
+        want = (std::max<size_t>(bytes, 256) + 4095) & ~(size_t)4095;   // without the headroom
+        if (dev_malloc(ctx, &b.p, want, "buffer") != hipSuccess) {
+            (void)hipGetLastError();
+            b.p = nullptr;
+            return set_err(ctx, HM_E_NOMEM, "hipMalloc(%zu) failed", want);
+        }
     }
     b.bytes = want;
     return HM_OK;
@@ -2763,14 +2771,14 @@ static bool in_arena(const hm_ctx *ctx, const void *p) {
     return ctx->arena && (const uint8_t *)p >= ctx->arena && (const uint8_t *)p < ctx->arena + ctx->arena_bytes;
 }
 
-// A table of >= 2^log2cap slots: the smallest pooled table of 2^log2cap or 2^(log2cap+1) slots (not cleared: see
+// A table of >= 2^log2cap slots: the smallest pooled table of 2^log2cap .. 2^(log2cap+2) slots (not cleared: see
 // kernels.h; a window whose key count sits near a power of two must not miss the pool and pay a multi-GB hipMalloc
 // every batch), else a new one zeroed once.  log2cap and rbits return the table's actual geometry.
 static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **out) {
     int best = -1;
     for (size_t i = 0; i < ctx->pool.size(); i++) {
         const int l = ctx->pool[i].second;
-        if (l >= log2cap && l <= log2cap + 1 && (best < 0 || l < ctx->pool[best].second)) best = (int)i;
+        if (l >= log2cap && l <= log2cap + 2 && (best < 0 || l < ctx->pool[best].second)) best = (int)i;
     }
     if (best >= 0) {
         *out = ctx->pool[best].first;
@@ -3182,6 +3190,9 @@ static int stage_inputs(hm_ctx *ctx, const hm_batch_in *in, const double **lat, 
     return HM_OK;
 }
 
+// pinned host capacity for `need` elements, grown with 1.5x headroom (output row counts creep up as windows fill)
+static size_t host_cap_for(size_t cap, size_t need) { return std::max<size_t>({need, cap + cap / 2, 1024}); }
+
 static int ensure_host(hm_ctx *ctx, void **p, size_t &cap_el, size_t want_el, size_t el) {
     (void)cap_el;
     if (*p) { HIPCHK(ctx, hipHostFree(*p)); ctx->n_frees++; }
@@ -3424,7 +3435,7 @@ static int finish_outputs(hm_ctx *ctx, int64_t n_tiles, int64_t n_rows, const in
     }
     int rc;
     if ((size_t)n_tiles > ctx->h_tiles_cap || !ctx->h_cell) {
-        size_t want = std::max<size_t>((size_t)n_tiles, 1024);
+        size_t want = host_cap_for(ctx->h_cell ? ctx->h_tiles_cap : 0, (size_t)n_tiles);
         size_t dummy = 0;
         if ((rc = ensure_host(ctx, &ctx->h_cell, dummy, want, 8)) || (rc = ensure_host(ctx, &ctx->h_ws, dummy, want, 8)) ||
             (rc = ensure_host(ctx, &ctx->h_cnt, dummy, want, 8)) || (rc = ensure_host(ctx, &ctx->h_sp, dummy, want, 8)) ||
@@ -3434,7 +3445,7 @@ static int finish_outputs(hm_ctx *ctx, int64_t n_tiles, int64_t n_rows, const in
         ctx->h_tiles_cap = want;
     }
     if ((size_t)n_rows > ctx->h_rows_cap || !ctx->h_rows) {
-        size_t want = std::max<size_t>((size_t)n_rows, 1024), dummy = 0;
+        size_t want = host_cap_for(ctx->h_rows ? ctx->h_rows_cap : 0, (size_t)n_rows), dummy = 0;
         if ((rc = ensure_host(ctx, &ctx->h_rows, dummy, want, 8))) return rc;
         ctx->h_rows_cap = want;
     }
@@ -4195,7 +4206,7 @@ int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_r
         out->latest_row = (const int64_t *)winner_recv_dev;
     } else {
         if ((size_t)n_winner_recv > ctx->h_rows_cap || !ctx->h_rows) {
-            size_t want = std::max<size_t>((size_t)n_winner_recv, 1024), dummy = 0;
+            size_t want = host_cap_for(ctx->h_rows ? ctx->h_rows_cap : 0, (size_t)n_winner_recv), dummy = 0;
             if ((rc = ensure_host(ctx, &ctx->h_rows, dummy, want, 8))) return rc;
             ctx->h_rows_cap = want;
         }
@@ -4601,8 +4612,8 @@ __global__ __launch_bounds__(256) void k_check_offsets(const int64_t *__restrict
 static int host_pinned(hm_ctx *ctx, void **p, size_t &cap, size_t want) {
     if (*p && cap >= want) return HM_OK;
     if (*p) { HIPCHK(ctx, hipHostFree(*p)); ctx->n_frees++; }
+    cap = *p ? host_cap_for(cap, want) : std::max<size_t>(want, 4096);
     *p = nullptr;
-    cap = std::max<size_t>(want, 4096);
     ctx->n_allocs++;
     HIPCHK(ctx, hipHostMalloc(p, cap, hipHostMallocDefault));
     return HM_OK;

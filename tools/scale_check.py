@@ -17,7 +17,9 @@ checked through size-independent properties (the oracle cannot run these sizes):
       key emitted twice, tiles per batch << events; eight batches, the steady-state rate is the median of the
       last four (the first ones allocate window tables sized by their partial counts until the pool holds them).
 
-usage: python tools/scale_check.py [--config c3|c4|c5|all] [--scale 1.0]   (prints one JSON line per config)
+  C2  configs[1] at its own resolution 7: 1e8 uniform events in one batch (run_c2).
+
+usage: python tools/scale_check.py [--config c2|c3|c4|c5|all] [--scale 1.0]   (prints one JSON line per config)
 """
 import argparse
 import json
@@ -116,6 +118,46 @@ def run_c4(dev, scale):
     return report
 
 
+def run_c2(dev, scale, res=7):
+    """configs[1]: 1e8 events uniform on the sphere at res 7 (its own resolution), 50k vehicles, 15 min (3 windows),
+    one batch.  Checks: counts add up to the valid rows, no key emitted twice, window starts in the batch's 15 min,
+    one latest row per vehicle (no ties by construction: distinct timestamps per vehicle are not forced, so the
+    check is that every latest row carries its vehicle's max and every vehicle has one)."""
+    import mobheat
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    n = int(100_000_000 * scale)
+    d = dict(lat=torch.rad2deg(torch.asin(torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 2 - 1)),
+             lon=torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 360 - 180,
+             ts=T0 + torch.randint(0, 15 * MIN_US, (n,), generator=g, device=dev, dtype=torch.int64),
+             speed=torch.rand(n, generator=g, device=dev, dtype=torch.float64) * 80,
+             sv=(torch.rand(n, generator=g, device=dev) >= 0.1).to(torch.uint8),
+             vkey=torch.randint(0, 50_000, (n,), generator=g, device=dev, dtype=torch.int64),
+             rv=torch.ones(n, dtype=torch.uint8, device=dev))
+    eng = mobheat.HeatmapEngine(h3_res=res, device=dev.index or 0, batch_capacity_hint=n)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    out = eng.process_batch_device(0, **ptrs(d, n))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    nt = int(out.n_tiles)
+    cell = dev_array(out.cell, nt, torch.int64, dev)
+    ws = dev_array(out.window_start_us, nt, torch.int64, dev)
+    cnt = dev_array(out.count, nt, torch.int64, dev)
+    assert no_duplicate_keys(cell, ws), "a key emitted twice"
+    assert int(cnt.sum()) == int(out.n_valid) == n, "counts do not add up to the rows"
+    assert bool(((ws >= T0) & (ws < T0 + 15 * MIN_US)).all()), "window start outside the batch's 15 minutes"
+    rows = dev_array(out.latest_row, int(out.n_latest), torch.int64, dev)
+    v = d["vkey"][rows]
+    vmax = torch.full((50_000,), -2**63, dtype=torch.int64, device=dev).scatter_reduce(0, d["vkey"], d["ts"], reduce="amax")
+    assert bool((d["ts"][rows] == vmax[v]).all()), "a latest row does not carry its vehicle's max ts"
+    assert int(torch.unique(v).numel()) == int((vmax > -2**63).sum()), "a vehicle without a latest row"
+    tm = eng.last_timings()
+    eng.close()
+    return {"config": f"C2 (res {res})", "events": n, "ms": round(dt * 1e3, 1), "events_per_s": n / dt, "tiles": nt,
+            "latest_rows": int(out.n_latest), "kernel_ms": {k: round(x, 2) for k, x in tm.items()}, "ok": True}
+
+
 def run_c3(dev, scale):
     import mobheat
     g = torch.Generator(device=dev)
@@ -212,13 +254,13 @@ def run_c5(dev, scale):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="all", choices=["c3", "c4", "c5", "all"])
+    ap.add_argument("--config", default="all", choices=["c2", "c3", "c4", "c5", "all"])
     ap.add_argument("--scale", type=float, default=1.0)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    for c in (["c3", "c4", "c5"] if a.config == "all" else [a.config]):
-        r = {"c3": run_c3, "c4": run_c4, "c5": run_c5}[c](dev, a.scale)
+    for c in (["c2", "c3", "c4", "c5"] if a.config == "all" else [a.config]):
+        r = {"c2": run_c2, "c3": run_c3, "c4": run_c4, "c5": run_c5}[c](dev, a.scale)
         print(json.dumps(r), flush=True)
         torch.cuda.empty_cache()
 
