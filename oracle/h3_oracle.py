@@ -15,7 +15,7 @@ _lib = None
 
 
 def build(force=False):
-    srcs = ("h3_oracle.c", "h3_tables_oracle.h", "h3_tables_derive.c")
+    srcs = ("h3_oracle.c", "h3_tables_oracle.h", "h3_tables_derive.c", "heatmap_cpu.c")
     if force or not os.path.exists(LIB) or any(os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, s)) for s in srcs):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB
