@@ -1923,7 +1923,7 @@ __device__ __forceinline__ void wave_count_slots(bool pred, int slot, unsigned *
 
 __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     const double *__restrict__ lat, const double *__restrict__ lon, const int64_t *__restrict__ ts,
-    const uint8_t *__restrict__ row_valid, const uint64_t *__restrict__ vkey, int64_t n, int res, FloorDiv wdiv,
+    const uint8_t *__restrict__ row_valid, const uint64_t *__restrict__ vkey, int64_t i_begin, int64_t n, int res, FloorDiv wdiv,
     int64_t late_end_us, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ keys_out, DedupSlot *dtab,
     unsigned long long dmask, unsigned int *dused, unsigned long long *n_dused, unsigned int *__restrict__ slow,
     unsigned long long *n_slow, unsigned long long *dgiveup, unsigned long long *wreg, unsigned long long *wcount,
@@ -1958,7 +1958,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     unsigned long long nv = EMPTY_VKEY;
     uint8_t nrv = 1;
     {
-        const int64_t i0 = (int64_t)blockIdx.x * IG_THREADS + threadIdx.x;
+        const int64_t i0 = i_begin + (int64_t)blockIdx.x * IG_THREADS + threadIdx.x;
         if (i0 < n) {
             nla = __builtin_nontemporal_load(&lat[i0]);
             nlo = __builtin_nontemporal_load(&lon[i0]);
@@ -1970,7 +1970,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         }
     }
 #endif
-    for (int64_t base = (int64_t)blockIdx.x * IG_THREADS; base < n; base += gstride, round++) {
+    for (int64_t base = i_begin + (int64_t)blockIdx.x * IG_THREADS; base < n; base += gstride, round++) {
         const int64_t i = base + threadIdx.x;
         const bool in = i < n;
 #if HM_INGEST_PREFETCH
@@ -2545,6 +2545,14 @@ struct hm_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     hipEvent_t ev[11] = {};
+    // host inputs: their copies run on copy_stream in row chunks, k_ingest on each chunk as soon as it has arrived
+    // (stage_inputs records the sources, phase_local issues copies and launches)
+    static constexpr int H2D_CHUNKS = 16;
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t h2d_ev[H2D_CHUNKS] = {};
+    struct H2D { const void *src; void *dst; size_t el; };
+    H2D h2d[7] = {};
+    int n_h2d = 0;
     double timings[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // per-event
     DevBuf in_lat, in_lon, in_ts, in_speed, in_sv, in_vkey, in_rv;
@@ -3180,11 +3188,12 @@ static int stage_inputs(hm_ctx *ctx, const hm_batch_in *in, const double **lat, 
         {&ctx->in_sv, in->speed_valid, 1, (const void **)sv}, {&ctx->in_vkey, in->vkey, 8, (const void **)vk},
         {&ctx->in_rv, in->row_valid, 1, (const void **)rv},
     };
+    ctx->n_h2d = 0;
     for (auto &it : items) {
         if (!it.src) { *it.dst = nullptr; continue; }
         int rc = ensure(ctx, *it.b, n * it.el);
         if (rc) return rc;
-        HIPCHK(ctx, hipMemcpyAsync(it.b->p, it.src, n * it.el, hipMemcpyHostToDevice, ctx->stream));
+        ctx->h2d[ctx->n_h2d++] = hm_ctx::H2D{it.src, it.b->p, it.el};   // copied by phase_local, chunk by chunk
         *it.dst = it.b->p;
     }
     return HM_OK;
@@ -3220,12 +3229,32 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
     HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->max_ts_ms, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
     if (n > 0) {
-        const int blocks = (int)std::min<int64_t>((n + IG_THREADS - 1) / IG_THREADS, ctx->ingest_grid);
-        hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(IG_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.vk, n,
-                           ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
-                           (uint64_t *)ctx->keys.p, ctx->dfused.tab, ctx->dfused.cap - 1, (unsigned int *)ctx->dfused.used.p,
-                           ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
-                           ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st);
+        // host inputs: row chunks copied on copy_stream, each chunk's k_ingest launched behind its copy (the copies
+        // of later chunks overlap the ingest of earlier ones); device inputs: one launch
+        const int nch = ctx->n_h2d ? (int)std::min<int64_t>(hm_ctx::H2D_CHUNKS, std::max<int64_t>(1, n >> 22)) : 1;
+        if (ctx->n_h2d) {
+            HIPCHK(ctx, hipEventRecord(ctx->h2d_ev[0], ctx->stream));   // (buffers free: the last batch is done)
+            HIPCHK(ctx, hipStreamWaitEvent(ctx->copy_stream, ctx->h2d_ev[0], 0));
+        }
+        for (int c = 0; c < nch; c++) {
+            const int64_t a = n * c / nch, b = n * (c + 1) / nch;
+            if (ctx->n_h2d) {
+                for (int q = 0; q < ctx->n_h2d; q++) {
+                    const hm_ctx::H2D &h = ctx->h2d[q];
+                    HIPCHK(ctx, hipMemcpyAsync((uint8_t *)h.dst + a * h.el, (const uint8_t *)h.src + a * h.el, (b - a) * h.el,
+                                               hipMemcpyHostToDevice, ctx->copy_stream));
+                }
+                HIPCHK(ctx, hipEventRecord(ctx->h2d_ev[c], ctx->copy_stream));
+                HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->h2d_ev[c], 0));
+            }
+            const int blocks = (int)std::min<int64_t>((b - a + IG_THREADS - 1) / IG_THREADS, ctx->ingest_grid);
+            hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(IG_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.vk, a, b,
+                               ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
+                               (uint64_t *)ctx->keys.p, ctx->dfused.tab, ctx->dfused.cap - 1, (unsigned int *)ctx->dfused.used.p,
+                               ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
+                               ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st);
+        }
+        ctx->n_h2d = 0;
         hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, ctx->cfg.h3_res,
                            (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, (uint64_t *)ctx->keys.p);
         hipLaunchKernelGGL(k_sample_heavy, dim3(1), dim3(HS_THREADS), 0, ctx->stream, (const uint64_t *)ctx->keys.p, n, ctx->d_st);
@@ -3536,7 +3565,10 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         return HM_E_HIP;
     };
     if (hipSetDevice(ctx->device) != hipSuccess) { ctx->err = "hipSetDevice"; return fail("create"); }
-    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { ctx->err = "stream"; return fail("create"); }
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess) { ctx->err = "stream"; return fail("create"); }
+    for (auto &e : ctx->h2d_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     // k_merge_owned's resident tags live in dynamic LDS of up to MO_TAG_MAX bytes (merge_sorted)
     if (hipFuncSetAttribute((const void *)k_merge_owned<EventRec>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
         hipFuncSetAttribute((const void *)k_merge_owned<SortedRec>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess) {
@@ -3687,6 +3719,9 @@ void hm_destroy(hm_ctx *ctx) {
     if (ctx->h_scratch) (void)hipHostFree(ctx->h_scratch);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto &e : ctx->h2d_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -8,6 +8,9 @@ memory and in page-locked memory (hipHostRegister through torch's pin_memory), b
 bench.py reports.  It is the PCIe-inclusive figure DESIGN.md §7 quotes; bench.py's `value` stays device-resident.
 
 usage: python tools/e2e_bench.py [--events 100000000] [--steps 4]   (one JSON line)
+       python tools/e2e_bench.py --kafka [--events 10000000]
+         foreach_batch_func on the raw Kafka `value` column (the producer's JSON records, mbta_to_kafka.py:66-74,
+         decoded on the GPU by hm_decode_json) end to end through the same loopback wire sink
        python tools/e2e_bench.py --foreach [--events 10000000]
          foreach_batch_func end to end: C1 (10k events, the reference's Boston batch) and a
          uniform batch of --events events (~that many tiles at res 8), as pandas frames, written through the wire
@@ -119,14 +122,78 @@ def foreach_mode(a):
     print(json.dumps(out))
 
 
+def producer_values(n, seed=5, n_vehicles=50_000, unique=1_000_000):
+    """n producer records (json.dumps of mbta_to_kafka.py:66-74's message) as Arrow binary (bytes, offsets): `unique`
+    records made by json.dumps, repeated to n with copy c's minute digit set to c % 10 (so the copies fall into
+    later minutes and windows)."""
+    rng = np.random.default_rng(seed)
+    m = min(n, unique)
+    lat = np.degrees(np.arcsin(rng.uniform(-1, 1, m)))
+    lon = rng.uniform(-180, 180, m)
+    sp = rng.uniform(0, 80, m)
+    nul = rng.random(m) < 0.1
+    veh = rng.integers(0, n_vehicles, m)
+    sec = rng.integers(0, 60, m)
+    vals = [json.dumps({"provider": "opensky", "vehicleId": f"v{veh[k]:06d}", "lat": float(lat[k]), "lon": float(lon[k]),
+                        "speedKmh": None if nul[k] else float(sp[k]), "bearing": 90, "accuracyM": None,
+                        "ts": f"2025-10-04T10:0{0}:{s:02d}Z"}).encode()
+            for k, s in enumerate(sec.tolist())]
+    lens = np.array([len(v) for v in vals], np.int64)
+    one = np.frombuffer(b"".join(vals), np.uint8)
+    reps = (n + m - 1) // m
+    buf = np.tile(one, reps)
+    lens_all = np.tile(lens, reps)[:n]
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(lens_all, out=offs[1:])
+    buf = buf[:offs[-1]].copy()
+    ends = offs[1:]
+    copy = np.arange(n) // m
+    buf[ends - 7] = ord("0") + (copy % 10)   # the minute's last digit: ...T10:0M:SSZ"}
+    return buf, offs
+
+
+def kafka_mode(a):
+    import pyarrow as pa
+    from mobheat import stream
+    srv = LoopbackMongo()
+    stream.MONGO_URI = f"mongodb://127.0.0.1:{srv.port}"
+    n = a.events
+    t = time.perf_counter()
+    buf, offs = producer_values(n)
+    gen_s = time.perf_counter() - t
+    table = pa.table({"value": pa.Array.from_buffers(pa.binary(), n, [None, pa.py_buffer(offs.astype(np.int32)),
+                                                                       pa.py_buffer(buf)])})
+    stream.reset_engine()
+    times = []
+    m0, b0 = srv.messages, srv.bytes
+    for s in range(a.steps + 1):
+        t = time.perf_counter()
+        stream.foreach_batch_func(table, s)
+        if s >= 1:
+            times.append(time.perf_counter() - t)
+    ms = 1e3 * float(np.median(times))
+    stream.reset_engine()
+    print(json.dumps({"what": "foreach_batch_func(df, epoch) on the raw Kafka value column (producer JSON records, "
+                              "hm_decode_json on the GPU) -> GPU path -> statements encoded on the GPU -> OP_MSG frames "
+                              "to a loopback server that acknowledges each; the same batch every epoch (its windows are "
+                              "re-touched, as in the reference's ~2-s trigger); median of the timed batches",
+                      "events": n, "value_bytes": int(offs[-1]), "ms_per_batch": round(ms, 1),
+                      "events_per_s": n / (ms * 1e-3), "batch_ms": [round(1e3 * x, 1) for x in times],
+                      "messages_per_batch": (srv.messages - m0) / (a.steps + 1),
+                      "wire_bytes_per_batch": (srv.bytes - b0) / (a.steps + 1), "generate_s": round(gen_s, 1)}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--events", type=int, default=100_000_000)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--foreach", action="store_true")
+    ap.add_argument("--kafka", action="store_true")
     a = ap.parse_args()
     if a.foreach:
         return foreach_mode(a)
+    if a.kafka:
+        return kafka_mode(a)
     import torch
     import mobheat
     n = a.events
