@@ -65,6 +65,11 @@ def stage_bytes(n, c, world=1):
     return b
 
 
+def s8d(n, c, ms):
+    b = 42 * n + (56 + 2 * 56) * c["tiles"]
+    return {"bytes": b, "ms": ms, "achieved_gbs": b / (ms * 1e-3) / 1e9, "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 STAGES = ["ingest", "aggregate", "send", "partition", "merge", "emit", "dedup"]
 # HBM traffic per dispatch of every kernel and k_ingest's VALU instruction mix per event of this workload, counted by
 # rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r2/kernel_pmc.json).
@@ -246,7 +251,10 @@ def main():
                  # the whole step: every stage's algorithmic bytes / the step's wall time / 8 TB/s
                  "step": {"algorithmic_bytes": step_bytes, "ms": ms_step,
                           "achieved_gbs": step_bytes / (ms_step * 1e-3) / 1e9,
-                          "frac": step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS}})
+                          "frac": step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                 # SURVEY.md section 8(d)'s own bytes for the step, independent of this build's intermediates: 42 B per
+                 # event in, 56 B per emitted tile, 2 x 56 B per touched state group (read + write)
+                 "step_s8d": s8d(n, c, ms_step)})
     value = world * n * K / elapsed
     out = {
         "metric": METRIC, "value": value, "unit": "events/s", "n_gpus": world, "steps": K, "warmup": args.warmup,
@@ -277,7 +285,7 @@ def main():
             "workload": f"{n:,} events/step uniform on the sphere, 1 min of event time per step, advancing 1 min per step",
             "kernel_ms": {k: round(v, 3) for k, v in B["kt"].items()},
             "tiles_last_step": B["counts"]["tiles"], "state_keys_created_last_step": B["counts"]["state_new"],
-            "step_frac": bb / (bms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+            "step_frac": bb / (bms * 1e-3) / 1e9 / HBM_PEAK_GBS, "step_s8d": s8d(n, B["counts"], bms)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.res)
     if rank == 0:
