@@ -20,6 +20,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "glibc_libm.h"
 
@@ -324,6 +325,24 @@ HM_HD uint64_t rotatePent60ccw(uint64_t h, int res) {
     if (leadingNonZeroDigit(h, res) == 1) h = rotate60(h, false);
     return h;
 }
+// m (0..5) ccw 60-degree rotations of every digit in one step.  In digit bits (i = 4, j = 2, k = 1), two rotations
+// (1->4, 2->1, 4->2, ...) move the planes: i' = k, j' = i, k' = j; three (1->6, 5->2, ...) complement every digit
+// other than 0 and 7; so m rotations = the planes moved (2m mod 3) times, complemented when m is odd.  Branch-free
+// (m varies by lane): replaces up to five data-dependent applications of rotate60.
+HM_HD uint64_t rotate60k(uint64_t h, int m) {
+    const uint64_t K = h & HM_DIG_LO, J = (h >> 1) & HM_DIG_LO, I = (h >> 2) & HM_DIG_LO;
+    const int pr = (2 * m) % 3;
+    const uint64_t ni = pr == 0 ? I : pr == 1 ? K : J;
+    const uint64_t nj = pr == 0 ? J : pr == 1 ? I : K;
+    const uint64_t nk = pr == 0 ? K : pr == 1 ? J : I;
+    uint64_t d = (ni << 2) | (nj << 1) | nk;
+    const uint64_t nf = (m & 1) ? (I | J | K) & ~(I & J & K) : 0;   // digits 1..6
+    d ^= nf | (nf << 1) | (nf << 2);
+    return (h & ~HM_DIG_MASK) | d;
+}
+// position of a leading digit in the cycle a pentagon's rotations visit (5 -> 4 -> 6 -> 2 -> 3 -> 5: the deleted K
+// digit is skipped), 3 bits per digit value; 0 for the digits 0, 1 and 7
+constexpr uint32_t HM_PENT_CYCLE_POS = (3u << 6) | (4u << 9) | (1u << 12) | (0u << 15) | (2u << 18);
 
 // Tables the kernels read (device: __constant__ copies; host self-test: static copies).
 struct H3Tables {
@@ -370,26 +389,35 @@ HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const TT &T) {
     // (dx, dy) in {-1,0,1}^2 (7 when it is not a unit vector; cf. _unitIjkToDigit).
     int x = ijk.i - ijk.k, y = ijk.j - ijk.k;
     uint64_t digits = 0;
-    for (int r = res - 1; r >= 0; r--) {
+    // one aperture-7 step up: resolution r + 1's digit; Class III (r even): _upAp7, centre child by _downAp7
+    // (i -> (3,0,1), j -> (1,3,0)); Class II: _upAp7r, centre child by _downAp7r (i -> (3,1,0), j -> (0,3,1))
+    auto up = [&](int r, auto cls3) __attribute__((always_inline)) {
         int px, py, cx, cy;
-        if ((r + 1) & 1) {  // Class III: _upAp7, centre child by _downAp7 (i -> (3,0,1), j -> (1,3,0))
+        if constexpr (decltype(cls3)::value) {
             px = round_div7(3 * x - y);
             py = round_div7(x + 2 * y);
             cx = 2 * px + py;
             cy = 3 * py - px;
-        } else {            // Class II: _upAp7r, centre child by _downAp7r (i -> (3,1,0), j -> (0,3,1))
+        } else {
             px = round_div7(2 * x + y);
             py = round_div7(3 * y - x);
             cx = 3 * px - py;
             cy = px + 2 * py;
         }
         const int dx = x - cx, dy = y - cy;
-        uint64_t digit = 7;
+        uint32_t digit = 7;
         if ((unsigned)(dx + 1) <= 2u && (unsigned)(dy + 1) <= 2u)
             digit = (0x69d0bd9u >> (3 * ((dx + 1) * 3 + (dy + 1)))) & 7u;
-        digits |= digit << ((14 - r) * 3);   // resolution r + 1
+        digits |= (uint64_t)digit << ((14 - r) * 3);
         x = px;
         y = py;
+    };
+    // the classes alternate: pairs (odd r: Class II, then r - 1: Class III) with no class branch per digit
+    int r = res - 1;
+    if (!(r & 1)) up(r--, std::true_type{});
+    for (; r >= 1; r -= 2) {
+        up(r, std::false_type{});
+        up(r - 1, std::true_type{});
     }
     h = (h & ~(HM_DIG_MASK & ~((UINT64_C(1) << (3 * (15 - res))) - 1))) | digits;
     ijk.i = x;
@@ -400,17 +428,25 @@ HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const TT &T) {
     int baseCell = T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][0];
     int numRots = T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][1];
     h |= (uint64_t)baseCell << 45;
+    // the rotations as one count m of 60-degree ccw steps, applied once (rotate60k).  Hexagon: numRots.  Pentagon
+    // (upstream: a leading K digit is first rotated out, cw on the base cell's cw-offset faces, then numRots
+    // _h3RotatePent60ccw, each of which takes one extra step when it lands on a leading K): from the leading digit's
+    // position q in the cycle 5 -> 4 -> 6 -> 2 -> 3, numRots steps pass the deleted K (q + numRots) / 5 times
+    // (numRots <= 5, q <= 4).  Equal to rotatePent60ccw applied numRots times (test_device_numerics_host).
+    int m = numRots;
     if (T.baseCellData[baseCell][4]) {
-        if (leadingNonZeroDigit(h, res) == 1)
-            h = rotate60(h, T.baseCellData[baseCell][5] == face || T.baseCellData[baseCell][6] == face);
-        for (int i = 0; i < numRots; i++) h = rotatePent60ccw(h, res);
-    } else {
-        // numRots ccw rotations of a hexagon's digits: the same as 6 - numRots cw ones; take the shorter way
-        const bool cw = numRots > 3;
-        const int k = cw ? 6 - numRots : numRots;
-        for (int i = 0; i < k; i++) h = rotate60(h, cw);
+        int lead = leadingNonZeroDigit(h, res);
+        int m0 = 0;
+        if (lead == 1) {
+            const bool cw = T.baseCellData[baseCell][5] == face || T.baseCellData[baseCell][6] == face;
+            m0 = cw ? 5 : 1;
+            lead = cw ? 3 : 5;
+        }
+        const int q = (int)((HM_PENT_CYCLE_POS >> (3 * lead)) & 7u);
+        m = m0 + numRots + (q + numRots) / 5;
+        m = m >= 6 ? m - 6 : m;
     }
-    return h;
+    return rotate60k(h, m);
 }
 
 // squared distance from face f's centre, upstream's operation order (_geoToClosestFace)
@@ -570,7 +606,7 @@ HM_HD void closestFaceF32(float fx, float fy, float fz, float &best, float &seco
 // (k_ingest keeps them in LDS: lane-indexed reads there do not queue behind its outstanding global loads).
 template <typename TT = H3Tables>
 HM_HD bool latLngToCellFastP(double lat_deg, double lng_deg, int res, const H3Tables &T, const double (*fc)[3],
-                             const double (*fu)[2][3], uint64_t &out, const TT *bt = nullptr) {
+                             const double (*fu)[2][3], uint64_t &out, const TT &bt) {
     out = 0;
     if (!(lat_deg >= -90.0 && lat_deg <= 90.0 && lng_deg >= -180.0 && lng_deg <= 180.0)) return true;
     double sl, cl, sg, cg;
@@ -596,7 +632,15 @@ HM_HD bool latLngToCellFastP(double lat_deg, double lng_deg, int res, const H3Ta
     const double a1 = __builtin_fabs(vx), a2 = __builtin_fabs(vy);
     const double M = a1 + a2;
     const double eps = 0x1p-52;
-    const double tau0 = M * ((4.0 / sqd + 2.0) + res + 128.0) * eps + S * 32.0 * eps;
+    // an upper bound of M ((4 / sqd + 2) + res + 128) eps + S 32 eps: 4 / sqd from an fp32 reciprocal (relative
+    // error < 3e-7, inflated by 2^-20) instead of an fp64 division, and res bounded by 15 (a loop-invariant
+    // (double)res was the register the cell computation's peak spilled to scratch, reloaded with a full wait)
+#ifdef __HIP_DEVICE_COMPILE__
+    const double rq = (double)__builtin_amdgcn_rcpf((float)sqd) * (1.0 + 0x1p-20);
+#else
+    const double rq = (double)(1.0f / (float)sqd) * (1.0 + 0x1p-20);
+#endif
+    const double tau0 = M * (4.0 * rq + 145.0) * eps + S * 32.0 * eps;
 #ifndef HM_FAST_TAU_SCALE
 #define HM_FAST_TAU_SCALE 8.0
 #endif
@@ -646,11 +690,12 @@ HM_HD bool latLngToCellFastP(double lat_deg, double lng_deg, int res, const H3Ta
         h.j = -1 * h.j;
     }
     ijkNormalize(h);
-    out = bt ? faceIjkToH3(face, h, res, *bt) : faceIjkToH3(face, h, res, T);
+    out = faceIjkToH3(face, h, res, bt);   // (bt: a reference -- as a pointer tested for null, both variants were
+                                           // compiled, since an LDS variable's generic address may be 0)
     return true;
 }
 HM_HD bool latLngToCellFast(double lat_deg, double lng_deg, int res, const H3Tables &T, uint64_t &out) {
-    return latLngToCellFastP(lat_deg, lng_deg, res, T, T.faceCenterPoint, T.fastU[res & 1], out);
+    return latLngToCellFastP(lat_deg, lng_deg, res, T, T.faceCenterPoint, T.fastU[res & 1], out, T);
 }
 
 }  // namespace hm

@@ -2028,7 +2028,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
 #ifdef HM_ABL_NOCELL
         if (geo0) cell = mix64(__builtin_bit_cast(uint64_t, la) ^ mix64(__builtin_bit_cast(uint64_t, lo)));
 #else
-        if (geo0) exc = !latLngToCellFastP(la, lo, res, c_tab, Fc, Fu, cell, &BT);
+        if (geo0) exc = !latLngToCellFastP(la, lo, res, c_tab, Fc, Fu, cell, BT);
 #endif
         const bool geo = geo0 && rv;
 #else
@@ -2069,7 +2069,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
 #ifdef HM_ABL_NOCELL   // ablation builds (tools/ablate_ingest.sh): a hash stands in for the cell
         if (fl & F_AGG) cell = mix64(__builtin_bit_cast(uint64_t, la) ^ mix64(__builtin_bit_cast(uint64_t, lo)));
 #else
-        if (fl & F_AGG) exc = !latLngToCellFastP(la, lo, res, c_tab, Fc, Fu, cell, &BT);
+        if (fl & F_AGG) exc = !latLngToCellFastP(la, lo, res, c_tab, Fc, Fu, cell, BT);
 #endif
 #endif
         {
