@@ -576,29 +576,42 @@ HM_HD void sincos_small(double x, double &s, double &c) {
 
 HM_HD double dmin(double a, double b) { return a < b ? a : b; }
 
-// The generated res-0 tables as compile-time constants (the fast path's closest-face prefilter takes its 60
-// coordinates as instruction literals instead of scalar registers: the kernels' SGPR budget spilled them into
-// VGPR lanes, ~120 v_readlane per round of k_ingest).
-namespace tab {
-#define H3T_CONST constexpr
-#include "h3_tables.inc"
-#undef H3T_CONST
-}  // namespace tab
-
-// closest-face prefilter, branch-free: the best and second-best fp32 dot product over faces F..19 (first face
-// wins ties, as upstream's strict `<`): the same (best, second, face) as the branchy scan
-// `if (d > best) {second = best; best = d; face = f;} else if (d > second) second = d;`
-template <int F>
-HM_HD void closestFaceF32(float fx, float fy, float fz, float &best, float &second, int &face) {
-    constexpr float cx = (float)tab::H3T_faceCenterPoint[F][0];
-    constexpr float cy = (float)tab::H3T_faceCenterPoint[F][1];
-    constexpr float cz = (float)tab::H3T_faceCenterPoint[F][2];
-    const float d = cx * fx + cy * fy + cz * fz;
-    const float lo = best < d ? best : d;
-    second = second < lo ? lo : second;
-    face = d > best ? F : face;
-    best = d > best ? d : best;
-    if constexpr (F + 1 < 20) closestFaceF32<F + 1>(fx, fy, fz, best, second, face);
+#include "face_dodeca.inc"
+// Closest face from the dodecahedron's symmetry (tools/gen_face_dodeca.py): R takes H3's face centres onto the
+// canonical dodecahedron -- (+-1, +-1, +-1) and the cyclic permutations of (0, +-1/phi, +-phi), over sqrt(3) -- so
+// with q = R p and a, b, c = |q.x|, |q.y|, |q.z| the best vertex of each family is the one whose signs match q's
+// (a + b + c; b/phi + c phi; a/phi + b phi; a phi + c/phi) and a family's runner-up flips the sign of its smaller term.
+// The closest face and its lead over the runner-up follow from these eight values (values in units of sqrt(3) times
+// the dot product).  Equal, up to fp32 rounding, to the argmax and lead over the 20 fp32 dot products; the lead test
+// (> 1e-5 in dot-product units, else the exact path) absorbs the difference.  ~45 VALU instead of ~160 for the 20
+// products, no memory access.
+HM_HD bool closestFaceDodeca(float px, float py, float pz, int &face) {
+    constexpr float R[3][3] = {{H3T_DODECA_R0}, {H3T_DODECA_R1}, {H3T_DODECA_R2}};
+    constexpr float P = 1.6180339887498949f, IP = 0.61803398874989490f;
+    const float qx = R[0][0] * px + R[0][1] * py + R[0][2] * pz;
+    const float qy = R[1][0] * px + R[1][1] * py + R[1][2] * pz;
+    const float qz = R[2][0] * px + R[2][1] * py + R[2][2] * pz;
+    const float a = __builtin_fabsf(qx), b = __builtin_fabsf(qy), c = __builtin_fabsf(qz);
+    const unsigned nx = qx < 0.0f, ny = qy < 0.0f, nz = qz < 0.0f;
+    const float ba = b * IP, cb = c * P, aa = a * IP, bb = b * P, ac = a * P, cc = c * IP;
+    const float f0 = (a + b) + c, f1 = ba + cb, f2 = aa + bb, f3 = ac + cc;
+    const float m0 = a < b ? a : b;
+    const float s0 = f0 - 2.0f * (m0 < c ? m0 : c), s1 = f1 - 2.0f * (ba < cb ? ba : cb);
+    const float s2 = f2 - 2.0f * (aa < bb ? aa : bb), s3 = f3 - 2.0f * (ac < cc ? ac : cc);
+    // the winner (first family on ties) and the best of the others' firsts and its own runner-up
+    float best = f0, second = s0;
+    unsigned idx = 4 * nx + 2 * ny + nz;
+    auto take = [&](float f, float s, unsigned i) __attribute__((always_inline)) {
+        const bool w = f > best;
+        second = w ? (best > s ? best : s) : (second > f ? second : f);
+        idx = w ? i : idx;
+        best = w ? f : best;
+    };
+    take(f1, s1, 8 + 3 * (2 * ny + nz));
+    take(f2, s2, 9 + 3 * (2 * nx + ny));
+    take(f3, s3, 10 + 3 * (2 * nx + nz));
+    face = (int)((idx < 12 ? H3T_DODECA_FACE_LO >> (5 * idx) : H3T_DODECA_FACE_HI >> (5 * (idx - 12))) & 31u);
+    return best - second > 1e-5f * 1.7320508f;
 }
 
 // The fast path.  Returns false when the caller must use latLngToCellDeg; otherwise `out` is upstream's cell
@@ -615,11 +628,7 @@ HM_HD bool latLngToCellFastP(double lat_deg, double lng_deg, int res, const H3Ta
     const double px = cg * cl, py = sg * cl, pz = sl;
     // closest face: fp32 dot products (within ~1e-6 of upstream's fp64 argmin); a lead below 1e-5 -> exact path
     int face = 0;
-    {
-        float best = -4.0f, second = -4.0f;
-        closestFaceF32<0>((float)px, (float)py, (float)pz, best, second, face);
-        if (!(best - second > 1e-5f)) return false;
-    }
+    if (!closestFaceDodeca((float)px, (float)py, (float)pz, face)) return false;
     const double *c = fc[face];
     const double pc = fma(px, c[0], fma(py, c[1], pz * c[2]));
     const double sqd = 2.0 - 2.0 * pc;
