@@ -163,12 +163,15 @@ def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, ar
     kt = {k: 0.0 for k in STAGES}
     kb = {k: 0.0 for k in STAGES}
     step_ms = []
+    host = []   # per step: the library call's host side (wall, syncs, allocations; single GPU)
     counts = None
     t0 = time.perf_counter()
     for s in range(args.warmup, total_steps):
         ts0 = time.perf_counter()
         step(s)
         step_ms.append((time.perf_counter() - ts0) * 1e3)
+        if sharded is None:
+            host.append(eng.last_host_timings())
         tm = eng.last_timings()
         counts = eng.last_counts()
         for k in STAGES:
@@ -189,7 +192,17 @@ def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, ar
     torch.cuda.empty_cache()
     K = args.steps
     return dict(elapsed=elapsed, step_ms=step_ms, kt={k: v / K for k, v in kt.items()},
-                kb={k: v / K for k, v in kb.items()}, counts=counts)
+                kb={k: v / K for k, v in kb.items()}, counts=counts, host=host)
+
+
+def slowest_step(leg):
+    """the slowest timed step: its wall ms and the library call's host side (where a step's time outside the
+    kernels went: stream synchronizations -- the longest one and its library source line -- and allocations)"""
+    if not leg["host"]:
+        return None
+    i = max(range(len(leg["step_ms"])), key=lambda k: leg["step_ms"][k])
+    return dict(step=i, wall_ms=round(leg["step_ms"][i], 3), **{k: (round(v, 3) if isinstance(v, float) else v)
+                                                               for k, v in leg["host"][i].items()})
 
 
 def main():
@@ -267,6 +280,7 @@ def main():
                    "records_sent_last_step": c["sent"],
                    "table_mode": c["table_mode"]},
         "roofline": roof,
+        "slowest_step": slowest_step(A),
     }
     B = None
     if world == 1 and not args.no_state_leg:
@@ -285,7 +299,8 @@ def main():
             "workload": f"{n:,} events/step uniform on the sphere, 1 min of event time per step, advancing 1 min per step",
             "kernel_ms": {k: round(v, 3) for k, v in B["kt"].items()},
             "tiles_last_step": B["counts"]["tiles"], "state_keys_created_last_step": B["counts"]["state_new"],
-            "step_frac": bb / (bms * 1e-3) / 1e9 / HBM_PEAK_GBS, "step_s8d": s8d(n, B["counts"], bms)}
+            "step_frac": bb / (bms * 1e-3) / 1e9 / HBM_PEAK_GBS, "step_s8d": s8d(n, B["counts"], bms),
+            "slowest_step": slowest_step(B)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.res)
     if rank == 0:

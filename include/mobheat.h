@@ -303,7 +303,9 @@ int hm_selftest_position_statements(const hm_position_doc_cfg *cfg, const uint64
 /* Timing of the last hm_process_batch / stage batch on the library's stream (HIP events), milliseconds
  * per phase: index 0 ingest (k_ingest: filter + cells + windows + event keys + latest max), 1 table-mode
  * aggregation (k_agg + k_bin_reduce), 2 merge, 3 emit, 4 dedup (flag + compaction), 5 total, 6 (window, region)
- * partition, 7 stage API: the sender's partition by owner rank. */
+ * partition, 7 stage API: the sender's partition by owner rank.  Host side of the last hm_process_batch (wall
+ * clock): 8 the call, 9 blocked in stream synchronizations, 10 in device/pinned allocations and frees, 11 the
+ * longest single synchronization, 12 its source line in the library, 13 allocations + frees made. */
 int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n);
 
 /* ---- Kafka message values -> batch columns (reference heatmap_stream.py:51-61, 88-93) ----

@@ -36,6 +36,7 @@
 #include "bson_docs.h"
 #include "json_decode.h"
 #include "h3_boundary.h"
+#include <chrono>
 #include <mutex>
 
 #define H3T_CONST static const
@@ -760,6 +761,110 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_scatter(const uint64_t *__res
     }
 }
 
+// Out = EventRec (the direct path's (window, region) bins; the single-GPU partition and the multi-GPU owner's): the same
+// rows and records as k_ev_scatter above, with no wait for the stores or the next round's loads inside the loop.
+// Rounds alternate between two register sets (no loop-carried copy: a register copy of a pending load waits for it);
+// every load is unconditional (the row clamped into the tile, absent columns read from one-element device constants,
+// the payload stream chosen at compile time), and every lane stores a record each round -- a row without a key goes
+// to the gap digit after every bin (counted by k_ev_hist; never read by the merge), a lane past the tile to the slack
+// records after the n-th (ensured by ev_partition) -- so the stores are unconditional too: the wait before a round's
+// rows only waits for them, not for the previous round's stores (measured before: a vmcnt(0) at the loop latch and
+// one after the prefetch, i.e. every round waited for its own stores and the next round's loads).
+__device__ const double g_zero_double = 0.0;
+__device__ const uint8_t g_zero_byte = 0;
+__device__ const uint8_t g_one_byte = 1;   // (also k_ingest's row validity when the batch has no validity column)
+typedef __attribute__((address_space(1))) const hm_v4u g_cv4u;
+typedef __attribute__((address_space(1))) hm_v4u g_v4u;
+__device__ __forceinline__ void st_g16(void *p, uint4 v) { *(g_v4u *)p = hm_v4u{v.x, v.y, v.z, v.w}; }   // global 16-B store
+template <bool kPayload>
+__global__ __launch_bounds__(EV_THREADS) void k_ev_scatter_rec(const uint64_t *__restrict__ keys, int64_t n, int64_t tile,
+                                                              const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
+                                                              const double *__restrict__ lat, const double *__restrict__ lon,
+                                                              const uint64_t *__restrict__ payload_in,
+                                                              const WInfo *__restrict__ winfo, uint64_t cell_hi, int nbins,
+                                                              const unsigned long long *__restrict__ O, int64_t ntiles,
+                                                              EventRec *__restrict__ dst) {
+    __shared__ unsigned cur[RP_BINS + 1];   // the bins' cursors and the gap digit's (positions < 2^32 - 1)
+    __shared__ uint4 stage[(EV_THREADS / 64) * 64 * 2];
+    __shared__ WiCacheL WI;
+    for (int d = threadIdx.x; d <= nbins; d += EV_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
+    wi_load(WI, winfo);
+    __syncthreads();
+    const int64_t t0 = (int64_t)blockIdx.x * tile;
+    const int64_t t1 = t0 + tile < n ? t0 + tile : n;
+    typedef __attribute__((address_space(1))) const double gcd;
+    typedef __attribute__((address_space(1))) const uint8_t gcu8;
+    typedef __attribute__((address_space(1))) const uint64_t gcu64;
+    uint4 *__restrict__ d4 = (uint4 *)dst;
+    uint4 *ws = stage + (threadIdx.x >> 6) * 64 * 2;
+    const int ln = lane_id();
+    struct Row { uint64_t k, sp; double la, lo; unsigned sv; bool in; };
+    auto load = [&](int64_t i) __attribute__((always_inline)) {
+        Row r;
+        r.in = i < t1;
+        const int64_t j = r.in ? i : t1 - 1;
+        r.k = __builtin_nontemporal_load((gcu64 *)&keys[j]);
+        if constexpr (kPayload) {
+            r.sp = __builtin_nontemporal_load((gcu64 *)&payload_in[j * WIRE_PAYLOAD_WORDS]);
+            r.la = __builtin_bit_cast(double, __builtin_nontemporal_load((gcu64 *)&payload_in[j * WIRE_PAYLOAD_WORDS + 1]));
+            r.lo = __builtin_bit_cast(double, __builtin_nontemporal_load((gcu64 *)&payload_in[j * WIRE_PAYLOAD_WORDS + 2]));
+            r.sv = 2;
+        } else {
+            r.sp = __builtin_bit_cast(uint64_t, __builtin_nontemporal_load((gcd *)(speed ? &speed[j] : &g_zero_double)));
+            r.sv = __builtin_nontemporal_load((gcu8 *)(speed_valid ? &speed_valid[j] : speed ? &g_one_byte : &g_zero_byte));
+            r.la = __builtin_nontemporal_load((gcd *)&lat[j]);
+            r.lo = __builtin_nontemporal_load((gcd *)&lon[j]);
+        }
+        return r;
+    };
+    auto put = [&](const Row &r) __attribute__((always_inline)) {
+        const uint64_t k = r.in ? r.k : 0;
+        unsigned pos;
+        if (k) {
+            const WInfo wi = wi_get(WI, winfo, ekey_widx(k));
+            const uint64_t hh = mix64(((k & CELL_LO) | cell_hi) ^ wi.inner);
+            pos = atomicAdd(&cur[ev_digit(hh, wi.binp, 0)], 1u);
+        }
+        // rows without a key: the gap digit (one LDS add per wave); lanes past the tile: the slack after record n
+        const unsigned long long gm = __ballot(r.in && !k);
+        if (gm) {
+            const int leader = __ffsll((long long)gm) - 1;
+            unsigned gb = 0;
+            if (ln == leader) gb = atomicAdd(&cur[nbins], (unsigned)__popcll(gm));
+            gb = __shfl(gb, leader, 64);
+            if (r.in && !k) pos = gb + (unsigned)__popcll(gm & ((UINT64_C(1) << ln) - 1));
+        }
+        if (!r.in) pos = (unsigned)n + (unsigned)ln;
+        const uint64_t spb = kPayload ? r.sp : r.sv == 0 ? SPEED_NULL_BITS
+                                                        : __builtin_bit_cast(double, r.sp) != __builtin_bit_cast(double, r.sp) ? CANON_NAN_BITS : r.sp;
+        const uint64_t lab = __builtin_bit_cast(uint64_t, r.la), lob = __builtin_bit_cast(uint64_t, r.lo);
+        ws[ln * 2 + 0] = make_uint4((unsigned)k, (unsigned)(k >> 32), (unsigned)spb, (unsigned)(spb >> 32));
+        ws[ln * 2 + 1] = make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32));
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const int idx = q * 64 + ln, rec = idx >> 1, part = idx & 1;
+            const unsigned p = __shfl(pos, rec, 64);
+            st_g16(&d4[(int64_t)p * 2 + part], ws[idx]);
+        }
+        __builtin_amdgcn_wave_barrier();
+    };
+    int64_t i0 = t0 + (int64_t)(threadIdx.x >> 6) * 64;
+    if (i0 >= t1) return;
+    Row a = load(i0 + ln);
+    preheader_wait();
+    for (;;) {
+        const Row b = load(i0 + EV_THREADS + ln);
+        put(a);
+        if (i0 + EV_THREADS >= t1) break;
+        a = load(i0 + 2 * EV_THREADS + ln);
+        put(b);
+        i0 += 2 * EV_THREADS;
+        if (i0 >= t1) break;
+    }
+}
+
 // the multi-GPU owner's census: received direct-path records per global window slot (sizes the window tables)
 struct SlotSink {
     unsigned long long *cnt;   // WREG_SLOTS counters
@@ -1236,9 +1341,6 @@ __device__ __forceinline__ T ld_l2(const T *p) {   // bypass the CU's L1 (chunks
     // flat instruction, which also counts on lgkmcnt -- so each later LDS wait waited for it to complete)
     return __hip_atomic_load((__attribute__((address_space(1))) const T *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-typedef __attribute__((address_space(1))) const hm_v4u g_cv4u;
-typedef __attribute__((address_space(1))) hm_v4u g_v4u;
-__device__ __forceinline__ void st_g16(void *p, uint4 v) { *(g_v4u *)p = hm_v4u{v.x, v.y, v.z, v.w}; }   // global 16-B store
 __device__ __forceinline__ unsigned mo_claim_home(unsigned long long addr) {
     return (unsigned)(((addr >> 6) * UINT64_C(0x9e3779b97f4a7c15)) >> 40) & (MO_CLAIM - 1);
 }
@@ -1907,7 +2009,6 @@ constexpr int IG_THREADS = 256;
 #ifndef HM_INGEST_TLATE
 #define HM_INGEST_TLATE 1
 #endif
-__device__ const uint8_t g_one_byte = 1;   // k_ingest's row validity when the batch has no validity column
 
 // wave-cooperative count: lanes with pred add 1 to cnt[slot] (one LDS add per distinct slot per wave)
 __device__ __forceinline__ void wave_count_slots(bool pred, int slot, unsigned *cnt) {
@@ -2554,6 +2655,10 @@ struct hm_ctx {
     H2D h2d[7] = {};
     int n_h2d = 0;
     double timings[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // host side of the last batch call (hm_last_timings [8, 14)): wall ms of the call, ms blocked in stream
+    // synchronizations, ms in device/pinned allocations and frees, the longest single synchronization and its source
+    // line, allocations + frees made
+    double host_ms[6] = {0, 0, 0, 0, 0, 0};
     // per-event
     DevBuf in_lat, in_lon, in_ts, in_speed, in_sv, in_vkey, in_rv;
     DevBuf cell, wstart, flags, win, rows, block_counts, block_offs;
@@ -2688,6 +2793,31 @@ constexpr int JSON_WORD = 244;   // 244-248: hm_decode_json's malformed / unsupp
         }                                                                                             \
     } while (0)
 
+static double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+// hipStreamSynchronize on the context's stream, timed into host_ms (site: the caller's source line)
+static hipError_t ctx_sync(hm_ctx *ctx, int site) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const hipError_t e = hipStreamSynchronize(ctx->stream);
+    const double ms = ms_since(t0);
+    ctx->host_ms[1] += ms;
+    if (ms > ctx->host_ms[3]) { ctx->host_ms[3] = ms; ctx->host_ms[4] = site; }
+    return e;
+}
+static void host_batch_begin(hm_ctx *ctx) { for (double &x : ctx->host_ms) x = 0; }
+struct BatchClock {   // the call's wall time into host_ms[0] on every return path
+    hm_ctx *ctx;
+    std::chrono::steady_clock::time_point t0;
+    explicit BatchClock(hm_ctx *c) : ctx(c), t0(std::chrono::steady_clock::now()) {}
+    ~BatchClock() { ctx->host_ms[0] = ms_since(t0); }
+};
+struct AllocTimer {   // times a device/pinned allocation or free into host_ms[2]
+    hm_ctx *ctx;
+    std::chrono::steady_clock::time_point t0;
+    explicit AllocTimer(hm_ctx *c) : ctx(c), t0(std::chrono::steady_clock::now()) {}
+    ~AllocTimer() { ctx->host_ms[2] += ms_since(t0); ctx->host_ms[5] += 1; }
+};
 static int set_err(hm_ctx *ctx, int code, const char *fmt, ...) {
     char buf[512];
     va_list ap;
@@ -2707,6 +2837,7 @@ static double wall_ms() {
 }
 static hipError_t dev_malloc(hm_ctx *ctx, void **p, size_t bytes, const char *what) {
     const double t0 = g_trace ? wall_ms() : 0;
+    AllocTimer at_(ctx);
     const hipError_t e = hipMalloc(p, bytes);
     ctx->n_allocs++;
     if (g_trace) fprintf(stderr, "[mobheat] hipMalloc %-12s %10.3f GB %8.1f ms\n", what, bytes / 1e9, wall_ms() - t0);
@@ -2720,8 +2851,8 @@ static int ensure(hm_ctx *ctx, DevBuf &b, size_t bytes) {
     // its regrow records) then reallocates O(log) times instead of in every batch that grows it
     if (b.p) want = std::max(want, b.bytes + b.bytes / 2);
     if (b.p) {
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        HIPCHK(ctx, hipFree(b.p));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+        { AllocTimer at_(ctx); HIPCHK(ctx, hipFree(b.p)); }
         ctx->n_frees++;
         b.p = nullptr;
         b.bytes = 0;
@@ -2809,10 +2940,10 @@ static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **
     }
     if (dev_malloc(ctx, (void **)&t, bytes, "state table") != hipSuccess) {
         (void)hipGetLastError();
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         std::vector<std::pair<TileSlot *, int>> keep;
         for (auto &pt : ctx->pool)
-            if (in_arena(ctx, pt.first)) keep.push_back(pt); else { (void)hipFree(pt.first); ctx->n_frees++; }
+            if (in_arena(ctx, pt.first)) keep.push_back(pt); else { AllocTimer at_(ctx); (void)hipFree(pt.first); ctx->n_frees++; }
         ctx->pool.swap(keep);
         ctx->n_allocs++;
         if (hipMalloc(&t, bytes) != hipSuccess) {
@@ -2831,7 +2962,7 @@ static void table_release(hm_ctx *ctx, TileSlot *t, int log2cap) {
     for (auto &pt : ctx->pool) own += !in_arena(ctx, pt.first);
     for (size_t i = 0; own > 8 && i < ctx->pool.size();) {
         if (in_arena(ctx, ctx->pool[i].first)) { i++; continue; }
-        (void)hipFree(ctx->pool[i].first);
+        { AllocTimer at_(ctx); (void)hipFree(ctx->pool[i].first); }
         ctx->n_frees++;
         ctx->pool.erase(ctx->pool.begin() + i);
         own--;
@@ -2913,16 +3044,29 @@ static int ev_partition(hm_ctx *ctx, const uint64_t *keys, int64_t n, const Inpu
     ntiles = std::max<int64_t>((n + tile - 1) / tile, 1);
     const int64_t m = (int64_t)(nbins + 1) * ntiles;
     int rc;
-    if (!dst && (rc = ensure(ctx, ctx->parts_sorted, std::max<int64_t>(n, 1) * sizeof(Out)))) return rc;
+    // (+ 64 slack records: k_ev_scatter_rec's lanes past a tile store there)
+    if (!dst && (rc = ensure(ctx, ctx->parts_sorted, (std::max<int64_t>(n, 1) + 64) * sizeof(Out)))) return rc;
     if ((rc = ensure(ctx, ctx->rp_H, m * 4)) || (rc = ensure(ctx, ctx->rp_O, m * 8))) return rc;
     const uint64_t ch = cell_hi_of(ctx->cfg.h3_res);
     hipLaunchKernelGGL(k_ev_hist, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, (const WInfo *)ctx->d_winfo, ch,
                        nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles);
     if ((rc = rp_scan(ctx, m))) return rc;
-    hipLaunchKernelGGL(k_ev_scatter<Out>, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, I ? I->sp : nullptr,
-                       I ? I->sv : nullptr, I ? I->lat : nullptr, I ? I->lon : nullptr, payload_in, (const WInfo *)ctx->d_winfo,
-                       ch, nranks, nbins, (const unsigned long long *)ctx->rp_O.p, ntiles, dst ? dst : (Out *)ctx->parts_sorted.p,
-                       payload_out);
+    if constexpr (std::is_same<Out, EventRec>::value) {
+        if (nranks != 0 || dst) return set_err(ctx, HM_E_STATE, "ev_partition: EventRecs go to the context's bins");
+        if (payload_in)
+            hipLaunchKernelGGL(k_ev_scatter_rec<true>, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, nullptr,
+                               nullptr, nullptr, nullptr, payload_in, (const WInfo *)ctx->d_winfo, ch, nbins,
+                               (const unsigned long long *)ctx->rp_O.p, ntiles, (EventRec *)ctx->parts_sorted.p);
+        else
+            hipLaunchKernelGGL(k_ev_scatter_rec<false>, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, I->sp, I->sv,
+                               I->lat, I->lon, nullptr, (const WInfo *)ctx->d_winfo, ch, nbins,
+                               (const unsigned long long *)ctx->rp_O.p, ntiles, (EventRec *)ctx->parts_sorted.p);
+    } else {
+        hipLaunchKernelGGL(k_ev_scatter<Out>, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, I ? I->sp : nullptr,
+                           I ? I->sv : nullptr, I ? I->lat : nullptr, I ? I->lon : nullptr, payload_in,
+                           (const WInfo *)ctx->d_winfo, ch, nranks, nbins, (const unsigned long long *)ctx->rp_O.p, ntiles,
+                           dst ? dst : (Out *)ctx->parts_sorted.p, payload_out);
+    }
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
 }
@@ -2979,7 +3123,7 @@ static int census_of_partials(hm_ctx *ctx, const TilePartial *parts, int64_t n, 
     ctx->census_ready = false;
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_cmap, ctx->d_cmap, GMAP_SLOTS * sizeof(WinCount), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "more than %d windows in one batch", GMAP_SLOTS);
     census.clear();
     for (int q = 0; q < GMAP_SLOTS; q++)
@@ -2997,7 +3141,7 @@ static void census_of_registry(const hm_ctx *ctx, std::vector<WinCount> &census)
 // WInfo of every registry slot in use (after gens_prepare when with_bins: the radix bin parameters need the
 // window's table geometry)
 static int winfo_upload(hm_ctx *ctx, bool with_bins) {
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));   // (h_winfo is reused: the previous upload must be done)
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));   // (h_winfo is reused: the previous upload must be done)
     WInfo *h = ctx->h_winfo;
     int lo = WREG_SLOTS, hi = -1;
     for (int w = 0; w < WREG_SLOTS; w++) {
@@ -3093,7 +3237,7 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census) {
         int64_t ntiles;
         if ((rc = partition<GrowRec, GrowRec>(ctx, (const GrowRec *)ctx->parts_regrow.p, moved, ntiles))) return rc;
         if ((rc = merge_sorted<GrowRec>(ctx, moved, ntiles))) return rc;
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         for (const auto &g : old) table_release(ctx, g.tab, g.log2cap);
     }
     return HM_OK;
@@ -3103,7 +3247,7 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census) {
 // released whole (their rows are late from now on); n_state = keys of the live windows.
 static int state_account(hm_ctx *ctx, int64_t evict_wm_ms) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_gmap, ctx->d_gmap, GMAP_SLOTS * sizeof(GenDesc), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     const int64_t dead_end_us = evict_wm_ms * 1000;
     int64_t live = 0;
     std::vector<hm_ctx::Gen> keep;
@@ -3137,8 +3281,8 @@ static int dedup_prepare(hm_ctx *ctx, hm_ctx::DedupTable &d, int64_t n_keys, boo
     // (a 2 MB fused table stays in every XCD's L2, an 8 MB one does not: k_ingest 6.9 -> 28 ms on the bench)
     if (d.tab && d.cap >= want && (!shrink || d.cap <= 2 * want)) return HM_OK;
     if (d.tab) {
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        HIPCHK(ctx, hipFree(d.tab));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+        { AllocTimer at_(ctx); HIPCHK(ctx, hipFree(d.tab)); }
         ctx->n_frees++;
         d.tab = nullptr;
     }
@@ -3204,6 +3348,7 @@ static size_t host_cap_for(size_t cap, size_t need) { return std::max<size_t>({n
 
 static int ensure_host(hm_ctx *ctx, void **p, size_t &cap_el, size_t want_el, size_t el) {
     (void)cap_el;
+    AllocTimer at_(ctx);
     if (*p) { HIPCHK(ctx, hipHostFree(*p)); ctx->n_frees++; }
     *p = nullptr;
     ctx->n_allocs++;
@@ -3266,7 +3411,7 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_wreg, ctx->d_wreg, WREG_SLOTS * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_wcount, ctx->d_wcount, WREG_SLOTS * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     if (ctx->h_st->win_overflow)
         return set_err(ctx, HM_E_OVERFLOW, "more than %d distinct windows in one micro-batch (%llu rows)", WREG_SLOTS,
                        ctx->h_st->win_overflow);
@@ -3314,7 +3459,7 @@ static int phase_table(hm_ctx *ctx, const Inputs &I, int64_t n_agg, int64_t *n_p
     ctx->h_agg_cursor.resize(nsub);
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_agg_cursor.data(), ctx->agg_cursor.p, (size_t)nsub * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "more than %d windows in one batch", GMAP_SLOTS);
     *n_parts = (int64_t)ctx->h_st->n_partials;
     ctx->table_evicted = (int64_t)ctx->h_st->n_evicted;
@@ -3488,7 +3633,7 @@ static int finish_outputs(hm_ctx *ctx, int64_t n_tiles, int64_t n_rows, const in
         HIPCHK(ctx, hipMemcpyAsync(ctx->h_lat, ctx->o_lat.p, n_tiles * 8, hipMemcpyDeviceToHost, ctx->stream));
     }
     if (n_rows > 0) HIPCHK(ctx, hipMemcpyAsync(ctx->h_rows, rows_dev, n_rows * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     out->cell = (const uint64_t *)ctx->h_cell;
     out->window_start_us = (const int64_t *)ctx->h_ws;
     out->count = (const int64_t *)ctx->h_cnt;
@@ -3731,6 +3876,7 @@ const char *hm_last_error(const hm_ctx *ctx) { return ctx ? ctx->err.c_str() : g
 int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n) {
     if (!ctx || !ms) return HM_E_INVALID;
     for (int i = 0; i < n && i < 8; i++) ms[i] = ctx->timings[i];
+    for (int i = 8; i < n && i < 14; i++) ms[i] = ctx->host_ms[i - 8];
     return HM_OK;
 }
 
@@ -3751,6 +3897,8 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if (in->n > 0 && (!in->lat || !in->lon || !in->ts_us || !in->vkey))
         return set_err(ctx, HM_E_INVALID, "lat, lon, ts_us and vkey are required");
     HIPCHK(ctx, hipSetDevice(ctx->device));
+    host_batch_begin(ctx);
+    const BatchClock clock_(ctx);
     memset(out, 0, sizeof(*out));
     ctx->epoch = epoch_id;
     ctx->last_n_latest = -1;
@@ -3783,7 +3931,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 256 * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     ctx->dedup_seen = (int64_t)ctx->h_scratch[ctx->dlast->used_word];   // distinct vkeys of this batch
     DevStats s2 = *ctx->h_st;
     if (s2.overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
@@ -4071,7 +4219,7 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *tile_send_buf, vo
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 256 * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     if (ctx->h_st->bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved");
     ctx->dedup_seen = (int64_t)ctx->h_scratch[ctx->dlast->used_word];
@@ -4117,7 +4265,7 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *tile_send_buf, vo
         HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, (W + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[9], ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     for (int r = 0; r < W; r++) {
         const int64_t start = n_records > 0 ? (int64_t)ctx->h_scratch[r] : 0;
         const int64_t end = n_records > 0 ? (int64_t)ctx->h_scratch[r + 1] : 0;   // [W]: the gaps' digit
@@ -4150,7 +4298,7 @@ static int merge_received_events(hm_ctx *ctx, const uint64_t *keys, const uint64
     hipLaunchKernelGGL(k_key_census, dim3(grid_for(n, 256, 256 * 8)), dim3(256), 0, ctx->stream, keys, n, ctx->d_wcount);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_wcount, ctx->d_wcount, WREG_SLOTS * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     for (int w = 0; w < WREG_SLOTS; w++)
         if (ctx->h_wcount[w] && !ctx->h_wreg[w]) return set_err(ctx, HM_E_INVALID, "received a record of an unknown window slot");
     std::vector<WinCount> census;
@@ -4193,7 +4341,7 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, const void *payload_r
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 256 * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     DevStats s2 = *ctx->h_st;
     if (s2.overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     unsigned long long cur[64];
@@ -4206,7 +4354,7 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, const void *payload_r
                            (int64_t *)winner_send_buf, 1);
         HIPCHK(ctx, hipGetLastError());
     }
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     record_timings(ctx);
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, 0, nullptr, out_memory, out))) return rc;
     // hm_last_counts: this rank's share of the batch (state keys created, records merged, tiles emitted, path)
@@ -4247,7 +4395,7 @@ int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_r
         }
         if (n_winner_recv > 0)
             HIPCHK(ctx, hipMemcpyAsync(ctx->h_rows, winner_recv_dev, n_winner_recv * 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         std::sort((int64_t *)ctx->h_rows, (int64_t *)ctx->h_rows + n_winner_recv);
         out->latest_row = (const int64_t *)ctx->h_rows;
     }
@@ -4287,7 +4435,7 @@ static int state_dump(hm_ctx *ctx, hm_state_rec *recs, int64_t n, unsigned only_
     HIPCHK(ctx, hipGetLastError());
     unsigned long long dumped = 0;
     HIPCHK(ctx, hipMemcpyAsync(&dumped, ctx->d_scratch + REGROW_WORD, 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     if ((int64_t)dumped != n) return set_err(ctx, HM_E_STATE, "state dump found %llu keys, expected %lld", dumped, (long long)n);
     if (n > 0) HIPCHK(ctx, hipMemcpy(recs, ctx->parts_regrow.p, n * sizeof(GrowRec), hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < n; i++) recs[i].reserved = 0;
@@ -4336,7 +4484,7 @@ int hm_state_export_touched(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs
         HIPCHK(ctx, hipGetLastError());
         unsigned long long dumped = 0;
         HIPCHK(ctx, hipMemcpyAsync(&dumped, ctx->d_scratch + REGROW_WORD, 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         n = (int64_t)dumped;
     }
     *n_out = n;
@@ -4399,7 +4547,7 @@ int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *
         if ((rc = partition<GrowRec, GrowRec>(ctx, (const GrowRec *)ctx->parts_regrow.p, n, ntiles))) return rc;
         if ((rc = merge_sorted<GrowRec>(ctx, n, ntiles))) return rc;
         HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow while restoring the state");
     }
     ctx->state_size = n;
@@ -4432,7 +4580,7 @@ static int statements_out(hm_ctx *ctx, int64_t n, int64_t total, int32_t out_mem
     unsigned long long *off = (unsigned long long *)ctx->td_off.p;
     *n_docs = n;
     if (out_memory == HM_MEM_DEVICE) {
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         *bytes = (const uint8_t *)ctx->td_bytes.p;
         *offsets = (const int64_t *)ctx->td_off.p;
         return HM_OK;
@@ -4450,7 +4598,7 @@ static int statements_out(hm_ctx *ctx, int64_t n, int64_t total, int32_t out_mem
     }
     if (total) HIPCHK(ctx, hipMemcpyAsync(ctx->h_td_bytes, ctx->td_bytes.p, total, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_td_off, off, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     *bytes = (const uint8_t *)ctx->h_td_bytes;
     *offsets = (const int64_t *)ctx->h_td_off;
     return HM_OK;
@@ -4515,7 +4663,7 @@ int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_
         hipLaunchKernelGGL(k_scan_add, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, off, n, (const unsigned long long *)ctx->td_boff.p);
         HIPCHK(ctx, hipGetLastError());
         HIPCHK(ctx, hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         if ((rc = ensure(ctx, ctx->td_bytes, total + 16))) return rc;
         // LDS staging sized by the longest statement this city/resolution can produce (int64 count, 16 hex
         // digits): occupancy is bounded by it (~400 B per statement -> 3 workgroups per CU)
@@ -4619,7 +4767,7 @@ int hm_encode_position_updates(hm_ctx *ctx, const hm_position_doc_cfg *cfg, int3
         unsigned long long hb[2] = {0, 0};
         HIPCHK(ctx, hipMemcpyAsync(&hb[0], off + n, 8, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipMemcpyAsync(&hb[1], ctx->d_scratch + POSBAD_WORD, 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         if (hb[1]) return set_err(ctx, HM_E_INVALID, "%llu latest rows outside the provider/vehicle dictionaries or time buckets", hb[1]);
         total = (int64_t)hb[0];
         if ((rc = ensure(ctx, ctx->td_bytes, total + 16))) return rc;
@@ -4646,6 +4794,7 @@ __global__ __launch_bounds__(256) void k_check_offsets(const int64_t *__restrict
 
 static int host_pinned(hm_ctx *ctx, void **p, size_t &cap, size_t want) {
     if (*p && cap >= want) return HM_OK;
+    AllocTimer at_(ctx);
     if (*p) { HIPCHK(ctx, hipHostFree(*p)); ctx->n_frees++; }
     cap = *p ? host_cap_for(cap, want) : std::max<size_t>(want, 4096);
     *p = nullptr;
@@ -4678,7 +4827,7 @@ static int dict_build(hm_ctx *ctx, hm_ctx::Dict &d, const uint8_t *bytes, const 
         HIPCHK(ctx, hipGetLastError());
         unsigned long long hw[2];
         HIPCHK(ctx, hipMemcpyAsync(hw, words, 16, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         if (hw[0]) {   // probes ran out (more distinct strings than the last batch): a full-size table
             if (cap == full) return set_err(ctx, HM_E_OVERFLOW, "string dictionary table overflow");
             cap = full;
@@ -4698,7 +4847,7 @@ static int dict_build(hm_ctx *ctx, hm_ctx::Dict &d, const uint8_t *bytes, const 
     if ((rc = compact_flags(ctx, (const uint8_t *)d.occ.p, (int64_t)cap, (int64_t *)d.slots.p))) return rc;
     unsigned long long nc = 0;
     HIPCHK(ctx, hipMemcpyAsync(&nc, ctx->d_scratch + 255, 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     const int64_t m = (int64_t)nc;
     if ((rc = ensure(ctx, d.clen, std::max<int64_t>(m, 1) * 4)) || (rc = ensure(ctx, d.coff, (m + 1) * 8))) return rc;
     hipLaunchKernelGGL(k_dict_codes, dim3(grid_for(std::max<int64_t>(m, 1), 256)), dim3(256), 0, ctx->stream,
@@ -4716,7 +4865,7 @@ static int dict_build(hm_ctx *ctx, hm_ctx::Dict &d, const uint8_t *bytes, const 
         hipLaunchKernelGGL(k_scan_add, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, coff, m, (const unsigned long long *)d.boff.p);
         HIPCHK(ctx, hipGetLastError());
         HIPCHK(ctx, hipMemcpyAsync(&total, coff + m, 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     } else {
         HIPCHK(ctx, hipMemsetAsync(coff, 0, 8, ctx->stream));
     }
@@ -4767,7 +4916,7 @@ int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out) {
         } else {
             HIPCHK(ctx, hipMemcpyAsync(&o0, in->offsets, 8, hipMemcpyDeviceToHost, ctx->stream));
             HIPCHK(ctx, hipMemcpyAsync(&on, in->offsets + n, 8, hipMemcpyDeviceToHost, ctx->stream));
-            HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+            HIPCHK(ctx, ctx_sync(ctx, __LINE__));
             if (o0 < 0 || on < o0) return set_err(ctx, HM_E_INVALID, "bad offsets");
             dbytes = in->bytes + o0;
             doffs = in->offsets;
@@ -4778,7 +4927,7 @@ int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out) {
         hipLaunchKernelGGL(k_check_offsets, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, doffs, n, o0, on, w);
         unsigned long long hb = 0;
         HIPCHK(ctx, hipMemcpyAsync(&hb, w, 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         if (hb) return set_err(ctx, HM_E_INVALID, "%llu offsets out of order or out of range", hb);
         if ((rc = ensure(ctx, ctx->jd_scratch, (size_t)(on - o0) + 16))) return rc;
         hipLaunchKernelGGL(k_json_parse, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, dbytes, doffs, o0, n,
@@ -4788,7 +4937,7 @@ int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out) {
         HIPCHK(ctx, hipGetLastError());
         unsigned long long counts[2];
         HIPCHK(ctx, hipMemcpyAsync(counts, w, 16, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         out->n_malformed = (int64_t)counts[0];
         out->n_unsupported = (int64_t)counts[1];
         if (counts[1])
@@ -4806,7 +4955,7 @@ int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out) {
                            (const unsigned *)ctx->jd_prov.code_of_slot.p, (const unsigned *)ctx->jd_veh.code_of_slot.p, n,
                            (uint64_t)nv, (uint64_t *)ctx->jd_vkey.p);
     HIPCHK(ctx, hipGetLastError());
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     hm_batch_in &b = out->batch;
     b.n = n;
     b.memory = HM_MEM_DEVICE;
@@ -4845,7 +4994,7 @@ int hm_last_latest_buckets(hm_ctx *ctx, int64_t *bucket_ids, int64_t cap, int64_
     HIPCHK(ctx, hipGetLastError());
     unsigned long long k = 0;
     HIPCHK(ctx, hipMemcpyAsync(&k, w, 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     std::vector<int64_t> ids(k);
     if (k) HIPCHK(ctx, hipMemcpy(ids.data(), ctx->lb_list.p, k * 8, hipMemcpyDeviceToHost));
     std::sort(ids.begin(), ids.end());

@@ -265,6 +265,14 @@ class HeatmapEngine:
         return {"ingest": ms[0], "aggregate": ms[1], "merge": ms[2], "emit": ms[3], "dedup": ms[4], "total": ms[5],
                 "partition": ms[6], "send": ms[7]}
 
+    def last_host_timings(self):
+        """Host side of the last process_batch (ms): the call, stream synchronizations, allocations + frees, the
+        longest synchronization and its library source line, allocations + frees made."""
+        ms = (ctypes.c_double * 14)()
+        check(self._lib.hm_last_timings(self._ctx, ms, 14), self._ctx)
+        return {"call": ms[8], "sync": ms[9], "alloc": ms[10], "max_sync": ms[11], "max_sync_line": int(ms[12]),
+                "allocs_frees": int(ms[13])}
+
     def last_counts(self):
         c = (ctypes.c_int64 * 8)()
         check(self._lib.hm_last_counts(self._ctx, c, 8), self._ctx)
