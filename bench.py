@@ -72,10 +72,10 @@ def s8d(n, c, ms):
 
 STAGES = ["ingest", "aggregate", "send", "partition", "merge", "emit", "dedup"]
 # HBM traffic per dispatch of every kernel and k_ingest's VALU instruction mix per event of this workload, counted by
-# rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r2/kernel_pmc.json).
-PMC_FILE = os.path.join(ROOT, "profiles", "r2", "kernel_pmc.json")
+# rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r3/kernel_pmc.json).
+PMC_FILE = os.path.join(ROOT, "profiles", "r3", "kernel_pmc.json")
 STAGE_KERNELS = {"ingest": ["k_ingest"], "aggregate": ["k_agg", "k_bin_reduce"], "send": ["k_ev_hist", "k_ev_scatter"],
-                 "partition": ["k_ev_hist", "k_ev_scatter"], "merge": ["k_merge_owned"], "emit": ["k_fill_gaps"],
+                 "partition": ["k_ev_hist", "k_ev_scatter_rec"], "merge": ["k_merge_owned"], "emit": ["k_fill_gaps"],
                  "dedup": ["k_dedup_flag"]}
 
 

@@ -1304,7 +1304,10 @@ constexpr int MO_THREADS = HM_MO_THREADS;      // partials per chunk (one per la
 #ifndef HM_MO_COOP_LINES
 #define HM_MO_COOP_LINES 1
 #endif
-constexpr int MO_CLAIM = 2 * MO_THREADS;
+#ifndef HM_MO_CLAIM_MULT
+#define HM_MO_CLAIM_MULT 4
+#endif
+constexpr int MO_CLAIM = HM_MO_CLAIM_MULT * MO_THREADS;   // claim-set entries (load <= 1 / HM_MO_CLAIM_MULT)
 #ifndef HM_MO_TAG_MAX
 #define HM_MO_TAG_MAX 90112
 #endif
@@ -1364,6 +1367,32 @@ __device__ __forceinline__ int mo_holder(const unsigned long long *cl, unsigned 
         if (o == 0) return -1;
         if ((o >> 16) == addr) return (int)(o & 0xffff);
         h = (h + 1) & (MO_CLAIM - 1);
+    }
+    return -1;
+}
+// The resident-only merge keys its claims by the slot's tag index (< 2^17: MO_TAG_MAX) instead of its address, so an
+// entry is 32 bits -- ((tag index + 1) << 9) | claimer lane -- and the same LDS holds twice the entries (load <= 1/8).
+constexpr int MO_CLAIM32 = 2 * MO_CLAIM;
+static_assert(MO_TAG_MAX < (1 << 17) && MO_THREADS <= 512, "32-bit claim entries");
+__device__ __forceinline__ unsigned mo_claim_home32(unsigned key) { return (key * 0x9e3779b1u) >> (32 - __builtin_ctz(MO_CLAIM32)); }
+__device__ __forceinline__ int mo_claim32(unsigned *cl, unsigned key, int lane, int &ci) {
+    const unsigned packed = ((key + 1) << 9) | (unsigned)lane;
+    unsigned h = mo_claim_home32(key);
+    for (int k = 0; k < MO_CLAIM32; k++) {
+        const unsigned o = atomicCAS(&cl[h], 0u, packed);
+        if (o == 0) { ci = (int)h; return -1; }
+        if ((o >> 9) == key + 1) return (int)(o & 511u);
+        h = (h + 1) & (MO_CLAIM32 - 1);
+    }
+    return -2;
+}
+__device__ __forceinline__ int mo_holder32(const unsigned *cl, unsigned key) {
+    unsigned h = mo_claim_home32(key);
+    for (int k = 0; k < MO_CLAIM32; k++) {
+        const unsigned o = __hip_atomic_load(&cl[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (o == 0) return -1;
+        if ((o >> 9) == key + 1) return (int)(o & 511u);
+        h = (h + 1) & (MO_CLAIM32 - 1);
     }
     return -1;
 }
@@ -1442,8 +1471,10 @@ struct MLine {
     unsigned long long touched;
 };
 
-// Rec = SortedRec: a batch's partials (partitioned); EventRec: the direct path's rows; GrowRec: growth (rehash)
-template <typename Rec>
+// Rec = SortedRec: a batch's partials (partitioned); EventRec: the direct path's rows; GrowRec: growth (rehash).
+// kResident: the host found every window of the batch resident in every bin (merge_sorted), so the variant carries
+// no HBM-probing fallback (less code, fewer live registers); a record outside the resident windows sets overflow.
+template <typename Rec, bool kResident = false>
 __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restrict__ parts, int64_t n,
                                                             const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
                                                             GenDesc *gm, const GenDesc *glist, int n_glist,
@@ -1537,17 +1568,38 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                 const unsigned rmask = S.res_mask[r], off = S.res_off[r];
                 TileSlot *const base = S.res_slots[r];
                 unsigned s = (unsigned)hk & rmask;
-                for (unsigned pr = 0; pr <= rmask && !done; pr++) {
+                // Tags scanned 8 at a time (one 8-B LDS read): only slots whose tag is empty or this key's are visited
+                // one by one, so a wave's loop runs its lanes' longest count of such slots, not of probed slots.
+                // (regions are >= 256 slots and start at multiples of their size: a word never crosses a region)
+                const unsigned long long tgv = (unsigned long long)tg * UINT64_C(0x0101010101010101);
+                const unsigned long long *tags64 = (const unsigned long long *)mo_tags;
+                for (unsigned scanned = 0; scanned <= rmask && !done;) {
+                    const unsigned bw = off + s, p0 = bw & 7;
+                    const unsigned long long word = __hip_atomic_load(&tags64[bw >> 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    // high bit of each byte that is 0 (exact per byte: no borrow between bytes), or equal to tg
+                    constexpr unsigned long long LO7 = UINT64_C(0x7f7f7f7f7f7f7f7f);
+                    const unsigned long long y = word ^ tgv;
+                    unsigned long long cand = ~(((word & LO7) + LO7) | word | LO7) | ~(((y & LO7) + LO7) | y | LO7);
+                    cand &= ~UINT64_C(0) << (8 * p0);
+                    if (!cand) {   // no candidate in the rest of the word: the next word
+                        scanned += 8 - p0;
+                        s = (s + 8 - p0) & rmask;
+                        continue;
+                    }
+                    const unsigned pos = (unsigned)__builtin_ctzll(cand) >> 3;
+                    scanned += pos - p0 + 1;
+                    s = (s + pos - p0) & rmask;
                     TileSlot *const sl = base + s;
                     const unsigned long long addr = (unsigned long long)sl;
                     const unsigned bi = off + s, sh = (bi & 3) * 8;
-                    const unsigned b = (__hip_atomic_load(&mo_tags[bi >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> sh) & 0xffu;
-                    if (b == 0 || b == tg) {
-                        int x = b == 0 ? -1 : mo_holder(cl, addr);
+                    const unsigned b = (unsigned)(word >> (8 * pos)) & 0xffu;
+                    {
+                        unsigned *const cl32 = (unsigned *)cl;
+                        int x = b == 0 ? -1 : kResident ? mo_holder32(cl32, bi) : mo_holder(cl, addr);
                         bool old_match = false;
                         if (b == tg && x < 0) old_match = ld_l2(&sl->cell) == p.cell && ld_l2(&sl->wenc) == we;
                         if (b == 0 || old_match) {
-                            x = mo_claim(cl, addr, t, ci);
+                            x = kResident ? mo_claim32(cl32, bi, t, ci) : mo_claim(cl, addr, t, ci);
                             if (x == -1) {
                                 gslot = sl;
                                 created = b == 0;
@@ -1565,7 +1617,7 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
                     }
                     s = (s + 1) & rmask;
                 }
-            } else {
+            } else if constexpr (!kResident) {
                 const GenDesc *g = gen_lookup(C, gm, we);
                 if (g) {
                     TileSlot *const tab = g->tab;
@@ -1758,13 +1810,18 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             }
             // created keys of non-resident windows count for their window here (resident ones: res_new); rehash:
             // the host already carries the moved keys
-            const bool count_here = created && !rehash && r < 0;
-            if (__ballot(count_here) && !wave_count_windows(count_here, p.we, 1ull, WL, sink)) overflow = true;
+            if constexpr (!kResident) {
+                const bool count_here = created && !rehash && r < 0;
+                if (__ballot(count_here) && !wave_count_windows(count_here, p.we, 1ull, WL, sink)) overflow = true;
+            }
             // 5. drain this chunk's stores (visible to the next chunk's probes: a full barrier waits for every store of
             // the wave -- measured: draining them a chunk later instead, deferring the keys the previous chunk wrote,
             // cost 1.5 ms on the bench and 4.5 ms on the state-read leg); release the claims
             __syncthreads();
-            if (ci >= 0) S.claim[ci] = 0;
+            if (ci >= 0) {
+                if constexpr (kResident) ((unsigned *)S.claim)[ci] = 0u;
+                else S.claim[ci] = 0;
+            }
         }
         lds_barrier();
         // 6. write the resident regions' tags back
@@ -3105,10 +3162,28 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles) {
         tag_bytes = (unsigned)std::min<size_t>((need + 4095) & ~size_t(4095), MO_TAG_MAX);   // (attribute: hm_create)
     }
     const int grid = ctx->merge_grid > 0 ? std::min(ctx->merge_grid, RP_BINS) : RP_BINS;
-    hipLaunchKernelGGL(k_merge_owned<Rec>, dim3(grid), dim3(MO_THREADS), tag_bytes, ctx->stream, (const Rec *)ctx->parts_sorted.p, n_rows,
-                       (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
-                       ctx->n_glist, (const WInfo *)ctx->d_winfo, cell_hi_of(ctx->cfg.h3_res), seq32(ctx), staged_rows(ctx),
-                       (unsigned *)ctx->bin_cnt.p, ctx->d_st, tag_bytes);
+    // every window of the batch resident in every bin (their regions' tags fit together): the variant without the
+    // HBM-probing fallback
+    bool resident = false;
+    if (!rehash) {
+        size_t need = 0;
+        int nwin = 0;
+        for (const auto &g : ctx->gens)
+            if (g.batch_parts) { need += size_t(1) << (g.log2cap - (int)g.rbits); nwin++; }
+        resident = need <= tag_bytes && nwin <= MO_RES_MAX && ctx->n_glist <= GC_MAX;
+    }
+    auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(MO_THREADS), tag_bytes, ctx->stream, (const Rec *)ctx->parts_sorted.p, n_rows,
+                           (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
+                           ctx->n_glist, (const WInfo *)ctx->d_winfo, cell_hi_of(ctx->cfg.h3_res), seq32(ctx), staged_rows(ctx),
+                           (unsigned *)ctx->bin_cnt.p, ctx->d_st, tag_bytes);
+    };
+    if constexpr (!rehash) {
+        if (resident) launch(k_merge_owned<Rec, true>);
+        else launch(k_merge_owned<Rec, false>);
+    } else {
+        launch(k_merge_owned<Rec, false>);
+    }
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
 }
@@ -3715,8 +3790,10 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     for (auto &e : ctx->h2d_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     // k_merge_owned's resident tags live in dynamic LDS of up to MO_TAG_MAX bytes (merge_sorted)
-    if (hipFuncSetAttribute((const void *)k_merge_owned<EventRec>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
-        hipFuncSetAttribute((const void *)k_merge_owned<SortedRec>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess) {
+    if (hipFuncSetAttribute((const void *)k_merge_owned<EventRec, false>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_merge_owned<EventRec, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_merge_owned<SortedRec, false>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_merge_owned<SortedRec, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess) {
         ctx->err = "merge LDS attribute";
         return fail("create");
     }

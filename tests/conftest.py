@@ -20,6 +20,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP library on the device)")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_gpu_first(request):
+    """In a GPU run, initialise torch's HIP runtime before the first test runs the library: torch ships its own copy of
+    libamdhip64, and a test that first touches torch's device only after the library's runtime has been working (a
+    subset such as tests/test_gpu_full_size.py after the stage tests) failed its torch init with 'No HIP GPUs are
+    available'."""
+    if "gpu" in (request.config.getoption("-m") or "") and "not gpu" not in (request.config.getoption("-m") or ""):
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+
+
 @pytest.fixture(scope="session")
 def oracle_h3():
     from oracle import h3_oracle

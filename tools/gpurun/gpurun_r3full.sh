@@ -1,0 +1,19 @@
+# Full GPU pass (round 3): parity tests, smoke, kernel-trace stats of the bench and of the C3 shard, PMC passes of the
+# bench's first leg -> profiles/r3/kernel_pmc.json (bench.py's roofline traffic), then the bench with its CPU baseline.
+set -o pipefail
+O=gpurun_out/${TAG:-r3f}
+mkdir -p $O
+export TMPDIR=/tmp
+P="python3 bench.py --steps 2 --warmup 2 --no-cpu-baseline --no-state-leg"
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -rf > $O/gpu_tests.log 2>&1 && \
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 6 --warmup 3 --no-cpu-baseline > $O/prof.log 2>&1 && \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o run -- python3 tools/scale_check.py --config c3 > $O/prof_c3.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 -d $O/pmc_f64 -o run --output-format csv -- $P > $O/pmc_f64.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVES SQ_BUSY_CU_CYCLES SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d $O/pmc_sq -o run --output-format csv -- $P > $O/pmc_sq.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- $P > $O/pmc_fetch.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- $P > $O/pmc_write.log 2>&1 && \
+python3 tools/ingest_pmc.py --res 8 --events 100000000 --out $O/kernel_pmc.json $O/pmc_f64 $O/pmc_sq $O/pmc_fetch $O/pmc_write > $O/ingest_pmc.log 2>&1 && \
+mkdir -p profiles/r3 && cp $O/kernel_pmc.json profiles/r3/kernel_pmc.json && \
+timeout -k 10 600 python3 bench.py > $O/bench.log 2>&1
+rc=$?; echo "done rc=$rc"; exit $rc
