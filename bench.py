@@ -202,7 +202,8 @@ def slowest_step(leg):
         return None
     i = max(range(len(leg["step_ms"])), key=lambda k: leg["step_ms"][k])
     return dict(step=i, wall_ms=round(leg["step_ms"][i], 3), **{k: (round(v, 3) if isinstance(v, float) else v)
-                                                               for k, v in leg["host"][i].items()})
+                                                               for k, v in leg["host"][i].items()},
+                allocs_frees_per_step=[h["allocs_frees"] for h in leg["host"]])
 
 
 def main():

@@ -1304,8 +1304,13 @@ constexpr int MO_THREADS = HM_MO_THREADS;      // partials per chunk (one per la
 #ifndef HM_MO_COOP_LINES
 #define HM_MO_COOP_LINES 1
 #endif
+#ifndef HM_MO_EARLY_LINES
+#define HM_MO_EARLY_LINES 1
+#endif
+// claim-set entries per record of a chunk (the resident-only merge: 2x as many 32-bit entries; 2 + the early old-line
+// scratch fit the same LDS as 4 without it)
 #ifndef HM_MO_CLAIM_MULT
-#define HM_MO_CLAIM_MULT 4
+#define HM_MO_CLAIM_MULT (HM_MO_EARLY_LINES ? 2 : 4)
 #endif
 constexpr int MO_CLAIM = HM_MO_CLAIM_MULT * MO_THREADS;   // claim-set entries (load <= 1 / HM_MO_CLAIM_MULT)
 #ifndef HM_MO_TAG_MAX
@@ -1336,6 +1341,9 @@ struct MoShared {
     unsigned res_off[MO_RES_MAX];         // byte offset of the region's tags in `tags`
     unsigned res_mask[MO_RES_MAX];        // slots per region - 1
     unsigned res_dirty[MO_RES_MAX];
+#if HM_MO_EARLY_LINES
+    uint4 xline[MO_THREADS / 64][64];     // per wave: one round of the cooperative old-line loads (16 lines)
+#endif
 };
 
 template <typename T>
@@ -1656,7 +1664,13 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             // and lanes 16k..16k+15 take their lines from there.  Every lane of the wave runs it (shuffles).
             const bool need = gslot && !created;
             if (__ballot(need)) {
+#if HM_MO_EARLY_LINES
+                // (its own scratch: the lines are loaded before the barrier, while other waves' joiners still read
+                // this wave's staged keys in S.sc / S.sh)
+                uint4 *xa = &S.xline[t >> 6][0], *xb = &S.xline[t >> 6][32];
+#else
                 uint4 *xa = (uint4 *)&S.sc[t & ~63], *xb = (uint4 *)&S.sh[t & ~63];
+#endif
                 const int ln = lane_id();
                 const unsigned long long ga = need ? (unsigned long long)gslot : 0ull;
 #pragma unroll
@@ -1747,10 +1761,17 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             int r = -1, ci = -1;
             if (has) probe(p, gslot, created, r, ci);
             count_created(created, r);
-            lds_barrier();
-            // 3. the claimers' new lines (their slots' last stores were drained by an earlier chunk's barrier)
-            MLine v{};
+#if HM_MO_EARLY_LINES
+            // 3a. the claimed existing lines, loaded before the barrier (their slots' last stores were drained by an
+            // earlier chunk's barrier, and no store of this chunk precedes step 4): the round trip overlaps the wait
             const MLine o = old_line(gslot, created);
+            lds_barrier();
+#else
+            lds_barrier();
+            const MLine o = old_line(gslot, created);
+#endif
+            // 3. the claimers' new lines
+            MLine v{};
             const bool retouch = !rehash && gslot && !created && (unsigned)(o.touched >> 32) == seq;
             const bool first = !rehash && gslot && !retouch;
             unsigned krow = touch_rows(first);

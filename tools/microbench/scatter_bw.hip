@@ -1,8 +1,9 @@
 // Random 32-B record scatter on MI355X: the write pattern of the direct path's partition (k_ev_scatter_rec) without
 // its compute.  n records of 32 B, two lanes per record (16-B stores), three destination patterns:
 //   seq     record i -> slot i (coalesced: the HBM write roofline of the same bytes)
-//   binned  record i -> bin b = hash(i) mod 8192, slot = b * (n / 8192) + i / 8192 (each bin's slots fill in order, as
-//           the partition's per-bin cursors do; consecutive records of a wave land in ~64 different bins)
+//   binned  record i -> bin b = hash(i) mod B, slot = b * (n / B) + i / B (each bin's slots fill in order, as the
+//           partition's per-bin cursors do; consecutive records of a wave land in ~64 different bins), for
+//           B = 8192 (the partition's bins) down to 64
 //   random  record i -> slot (i * odd) mod n (no locality at all)
 // Build: hipcc --offload-arch=gfx950 -O3 -o scatter_bw scatter_bw.hip      Run: ./scatter_bw [n]
 #include <hip/hip_runtime.h>
@@ -14,15 +15,15 @@ __device__ __forceinline__ uint64_t mixh(uint64_t x) {
     x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33; return x;
 }
 template <int MODE>
-__global__ __launch_bounds__(512) void k_scatter(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n) {
-    const int64_t nb = n / 8192;
+__global__ __launch_bounds__(512) void k_scatter(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n, int bins) {
+    const int64_t nb = n / bins;
     for (int64_t base = (int64_t)blockIdx.x * 512; base < 2 * n; base += (int64_t)gridDim.x * 512) {
         const int64_t j = base + threadIdx.x;   // 16-B part j of record j / 2
         if (j >= 2 * n) continue;
         const int64_t i = j >> 1;
         int64_t p;
         if (MODE == 0) p = i;
-        else if (MODE == 1) p = (int64_t)(mixh((uint64_t)i) & 8191) * nb + (i / 8192) % nb;
+        else if (MODE == 1) p = (int64_t)(mixh((uint64_t)i) & (uint64_t)(bins - 1)) * nb + (i / bins) % nb;
         else p = (int64_t)(((uint64_t)i * 0x9e3779b97f4a7c15ULL) % (uint64_t)n);
         dst[p * 2 + (j & 1)] = src[j];
     }
@@ -36,19 +37,24 @@ int main(int argc, char **argv) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const char *names[3] = {"seq", "binned", "random"};
-    for (int rep = 0; rep < 3; rep++)
-        for (int m = 0; m < 3; m++) {
-            hipEventRecord(a);
-            if (m == 0) hipLaunchKernelGGL(k_scatter<0>, dim3(8192), dim3(512), 0, 0, src, dst, n);
-            if (m == 1) hipLaunchKernelGGL(k_scatter<1>, dim3(8192), dim3(512), 0, 0, src, dst, n);
-            if (m == 2) hipLaunchKernelGGL(k_scatter<2>, dim3(8192), dim3(512), 0, 0, src, dst, n);
-            hipEventRecord(b);
-            hipEventSynchronize(b);
-            float ms;
-            hipEventElapsedTime(&ms, a, b);
-            printf("rep %d %-7s %lld records: %.3f ms  %.2f GB/s written (+ %.2f GB/s read)\n", rep, names[m], (long long)n, ms,
-                   n * 32 / (ms * 1e-3) / 1e9, n * 32 / (ms * 1e-3) / 1e9);
+    auto run = [&](int m, int bins) {
+        hipEventRecord(a);
+        if (m == 0) hipLaunchKernelGGL(k_scatter<0>, dim3(8192), dim3(512), 0, 0, src, dst, n, bins);
+        if (m == 1) hipLaunchKernelGGL(k_scatter<1>, dim3(8192), dim3(512), 0, 0, src, dst, n, bins);
+        if (m == 2) hipLaunchKernelGGL(k_scatter<2>, dim3(8192), dim3(512), 0, 0, src, dst, n, bins);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        return ms;
+    };
+    for (int rep = 0; rep < 2; rep++) {
+        printf("rep %d seq     %.3f ms\n", rep, run(0, 8192));
+        for (int bins = 8192; bins >= 64; bins /= 2) {
+            const float ms = run(1, bins);
+            printf("rep %d binned %5d bins %.3f ms  %.2f GB/s written\n", rep, bins, ms, n * 32 / (ms * 1e-3) / 1e9);
         }
+        printf("rep %d random  %.3f ms\n", rep, run(2, 8192));
+    }
     return 0;
 }
