@@ -289,10 +289,12 @@ def main():
         # holds 1 minute of event time and the stream advances 1 minute per step, so consecutive batches update the
         # same open windows and the merge reads existing state lines.  res 7 (configs[1]'s resolution): 1e8 events
         # per minute re-touch most of a window's keys from its second batch on.
-        # (its windows' tables come from a state arena reserved at create, ~400 B per event for the three windows the
-        # leg touches, so that no multi-GB table is allocated inside a timed step; the leg's occasional out-of-kernel
-        # stall, DESIGN.md section 7, is not this -- it persisted with the arena)
-        B = run_leg(args, n, 7, 60_000_000, 60_000_000, 2, dev, local, world, rank, arena_bytes=400 * n)
+        # (its windows' tables come from a state arena reserved at create, so that no multi-GB table is allocated
+        # inside a timed step: a window's table grows to 2^28 slots (17.4 GB) once its minutes have touched more than
+        # 67M cells, and the leg holds up to three such tables plus the smaller ones it grew from -- ~700 B per event.
+        # Round 3's per-step host timing found the leg's occasional multi-second stall in the step that allocated, with
+        # 400 B per event, the table the arena no longer covered)
+        B = run_leg(args, n, 7, 60_000_000, 60_000_000, 2, dev, local, world, rank, arena_bytes=700 * n)
         bms = B["elapsed"] / K * 1e3
         bb = sum(B["kb"].values())
         out["state_read_leg"] = {

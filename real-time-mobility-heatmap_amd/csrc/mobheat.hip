@@ -1307,6 +1307,10 @@ constexpr int MO_THREADS = HM_MO_THREADS;      // partials per chunk (one per la
 #ifndef HM_MO_EARLY_LINES
 #define HM_MO_EARLY_LINES 1
 #endif
+// the resident-only merge's wave-cooperative probe (needs the early-lines scratch)
+#ifndef HM_MO_COOP_PROBE
+#define HM_MO_COOP_PROBE HM_MO_EARLY_LINES
+#endif
 // claim-set entries per record of a chunk (the resident-only merge: 2x as many 32-bit entries; 2 + the early old-line
 // scratch fit the same LDS as 4 without it)
 #ifndef HM_MO_CLAIM_MULT
@@ -1425,6 +1429,13 @@ __device__ __forceinline__ MRec mrec_of(const EventRec &p, const WInfo *winfo, u
     const bool sv = __builtin_bit_cast(uint64_t, p.speed) != SPEED_NULL_BITS;
     return MRec{cell, wi.wenc, mix64(cell ^ wi.inner), 1ull, sv ? 1ull : 0ull, sv ? p.speed : 0.0, p.lat, p.lon, 0ull};
 }
+// the same from the LDS image of the batch's window parameters (the partition's WiCacheL)
+__device__ __forceinline__ MRec mrec_of_wi(const EventRec &p, const WiCacheL &WI, const WInfo *winfo, uint64_t cell_hi) {
+    const WInfo wi = wi_get(WI, winfo, ekey_widx(p.key));
+    const uint64_t cell = (p.key & CELL_LO) | cell_hi;
+    const bool sv = __builtin_bit_cast(uint64_t, p.speed) != SPEED_NULL_BITS;
+    return MRec{cell, wi.wenc, mix64(cell ^ wi.inner), 1ull, sv ? 1ull : 0ull, sv ? p.speed : 0.0, p.lat, p.lon, 0ull};
+}
 // a duplicate of lane x's key: add this record's values into x's staging entry
 __device__ __forceinline__ void mo_add_into(MoShared &S, int x, const MRec &p) {
     atomicAdd(&S.scnt[x], p.cnt);
@@ -1451,8 +1462,12 @@ __device__ __forceinline__ void put_row(const RowsOut &o, int64_t t, uint64_t ce
                                         double slon) {
     const bool null_sp = nspeed == 0;
     // x / 1.0 == x: a key's first row (count 1) skips the fp64 divisions
-    const double asp = null_sp ? 0.0 : nspeed == 1 ? sspeed : sspeed / (double)nspeed;
-    const double alon = count == 1 ? slon : slon / (double)count, alat = count == 1 ? slat : slat / (double)count;
+    double asp = null_sp ? 0.0 : sspeed, alon = slon, alat = slat;
+    if (count != 1) {   // (a branch: a wave whose keys all have one row skips the three fp64 divisions)
+        if (!null_sp && nspeed != 1) asp = sspeed / (double)nspeed;
+        alon = slon / (double)count;
+        alat = slat / (double)count;
+    }
     if constexpr ((HM_NT_STORES & 2) != 0) {
         __builtin_nontemporal_store(cell, &o.cell[t]);
         __builtin_nontemporal_store(wdec(we), &o.ws[t]);
@@ -1482,8 +1497,12 @@ struct MLine {
 // Rec = SortedRec: a batch's partials (partitioned); EventRec: the direct path's rows; GrowRec: growth (rehash).
 // kResident: the host found every window of the batch resident in every bin (merge_sorted), so the variant carries
 // no HBM-probing fallback (less code, fewer live registers); a record outside the resident windows sets overflow.
-template <typename Rec, bool kResident = false>
-__global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restrict__ parts, int64_t n,
+// kCoop (resident only): the wave-cooperative probe (probe_coop) -- chosen when the last batch re-touched mostly
+// existing keys (their lines then cost one cooperative round trip); a batch of mostly new keys runs the per-lane probe,
+// which carries less machinery per probed slot (bench leg: 3.72-3.81 vs 4.03-4.11 ms; state-read leg: 6.86-6.89 vs
+// 6.22-6.30 ms, profiles/r3/r3ab9/)
+template <typename Rec, bool kResident = false, bool kCoop = false>
+__global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_merge_owned(const Rec *__restrict__ parts, int64_t n,
                                                             const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
                                                             GenDesc *gm, const GenDesc *glist, int n_glist,
                                                             const WInfo *__restrict__ winfo, uint64_t cell_hi,
@@ -1494,6 +1513,12 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
     extern __shared__ unsigned mo_tags[];   // tag_bytes of resident region tags
     __shared__ WinLds WL;
     __shared__ GenCache C;
+#ifndef HM_MO_WI_LDS
+#define HM_MO_WI_LDS 1
+#endif
+    constexpr bool kWi = HM_MO_WI_LDS && std::is_same<Rec, EventRec>::value;
+    __shared__ std::conditional_t<kWi, WiCacheL, char> WI;   // EventRec: the window parameters' LDS image
+    if constexpr (kWi) wi_load(WI, winfo);
     wl_init(WL);
     gc_load(C, glist, n_glist);
     const GenSink sink{gm};
@@ -1653,11 +1678,131 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             }
             if (!done) overflow = true;
         };
+#if HM_MO_COOP_PROBE
+        // The resident-only merge's probe, wave-cooperative: each round every lane still probing scans its region's
+        // tags to its next candidate slot (empty or its tag); the lanes whose candidate holds an older key of the same
+        // tag then load those lines TOGETHER, whole (lane L loads part L & 3 of the line of lane 16k + L / 4, 16 lines
+        // per 16-B instruction, through the wave's LDS scratch), compare the key and keep the line: one round trip per
+        // existing key, and no second load of the line after the barrier.
+        auto probe_coop = [&](const MRec &p, bool has, TileSlot *&gslot, bool &created, int &r, int &ci, MLine &pre,
+                              bool &preloaded) __attribute__((always_inline)) {
+            unsigned *const cl32 = (unsigned *)S.claim;
+            const unsigned long long we = p.we;
+            const uint64_t hk = p.hk;
+            const unsigned tg = tag8(hk);
+            r = -1;
+            if (has)
+                for (int q = 0; q < nres; q++)
+                    if (S.res_we[q] == we) r = q;
+            bool done = !has || r < 0, lost = has && r < 0;
+            unsigned rmask = 0, off = 0, s = 0, scanned = 0;
+            TileSlot *base = nullptr;
+            if (r >= 0) {
+                rmask = S.res_mask[r];
+                off = S.res_off[r];
+                base = S.res_slots[r];
+                s = (unsigned)hk & rmask;
+            }
+            const unsigned long long tgv = (unsigned long long)tg * UINT64_C(0x0101010101010101);
+            const unsigned long long *tags64 = (const unsigned long long *)mo_tags;
+            uint4 *xa = &S.xline[t >> 6][0], *xb = &S.xline[t >> 6][32];
+            const int ln = lane_id();
+            while (__ballot(!done)) {
+                // 1. this lane's next candidate slot
+                unsigned b = 0;
+                bool found = false;
+                if (!done) {
+                    while (scanned <= rmask) {
+                        const unsigned bw = off + s, p0 = bw & 7;
+                        const unsigned long long word = __hip_atomic_load(&tags64[bw >> 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        constexpr unsigned long long LO7 = UINT64_C(0x7f7f7f7f7f7f7f7f);
+                        const unsigned long long y = word ^ tgv;
+                        unsigned long long cand = ~(((word & LO7) + LO7) | word | LO7) | ~(((y & LO7) + LO7) | y | LO7);
+                        cand &= ~UINT64_C(0) << (8 * p0);
+                        if (!cand) {
+                            scanned += 8 - p0;
+                            s = (s + 8 - p0) & rmask;
+                            continue;
+                        }
+                        const unsigned pos = (unsigned)__builtin_ctzll(cand) >> 3;
+                        scanned += pos - p0 + 1;
+                        s = (s + pos - p0) & rmask;
+                        b = (unsigned)(word >> (8 * pos)) & 0xffu;
+                        found = true;
+                        break;
+                    }
+                    if (!found) { done = true; lost = true; }   // the region is full
+                }
+                const unsigned bi = off + s;
+                TileSlot *const sl = base + s;
+                // 2. a tag-matching slot: claimed in this chunk (its holder), else its line from HBM, loaded together
+                int x = -1;
+                if (found && b != 0) x = mo_holder32(cl32, bi);
+                const bool need = found && b == tg && x < 0;
+                hm_v4u q0{}, q1{}, q2{}, q3{};
+                const unsigned long long ga = need ? (unsigned long long)sl : 0ull;
+                const unsigned long long needm = __ballot(need);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    if (!((needm >> (16 * k)) & 0xffffull)) continue;   // (wave-uniform)
+                    const int src = k * 16 + (ln >> 2), part = ln & 3;
+                    const unsigned long long sa = __shfl(ga, src, 64);
+                    if (sa) {
+                        const hm_v4u v = __builtin_nontemporal_load((g_cv4u *)sa + part);
+                        ((part < 2) ? xa : xb)[(src & 15) * 2 + (part & 1)] = make_uint4(v.x, v.y, v.z, v.w);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    if (need && (ln >> 4) == k) {
+                        const int e = (ln & 15) * 2;
+                        const uint4 a0 = xa[e], a1 = xa[e + 1], a2 = xb[e], a3 = xb[e + 1];
+                        q0 = hm_v4u{a0.x, a0.y, a0.z, a0.w};
+                        q1 = hm_v4u{a1.x, a1.y, a1.z, a1.w};
+                        q2 = hm_v4u{a2.x, a2.y, a2.z, a2.w};
+                        q3 = hm_v4u{a3.x, a3.y, a3.z, a3.w};
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                }
+                const bool old_match = need && ((unsigned long long)q0.x | ((unsigned long long)q0.y << 32)) == p.cell &&
+                                       ((unsigned long long)q0.z | ((unsigned long long)q0.w << 32)) == we;
+                // 3. claim an empty slot or the key's own
+                if (found && (b == 0 || old_match)) {
+                    x = mo_claim32(cl32, bi, t, ci);
+                    if (x == -1) {
+                        gslot = sl;
+                        created = b == 0;
+                        if (created) {
+                            atomicOr(&mo_tags[bi >> 2], tg << ((bi & 3) * 8));
+                            S.res_dirty[r] = 1;
+                        } else {
+                            pre.count = (unsigned long long)q1.x | ((unsigned long long)q1.y << 32);
+                            pre.nspeed = (unsigned long long)q1.z | ((unsigned long long)q1.w << 32);
+                            pre.sspeed = __builtin_bit_cast(double, (unsigned long long)q2.x | ((unsigned long long)q2.y << 32));
+                            pre.slat = __builtin_bit_cast(double, (unsigned long long)q2.z | ((unsigned long long)q2.w << 32));
+                            pre.slon = __builtin_bit_cast(double, (unsigned long long)q3.x | ((unsigned long long)q3.y << 32));
+                            pre.touched = (unsigned long long)q3.z | ((unsigned long long)q3.w << 32);
+                            preloaded = true;
+                        }
+                        done = true;
+                    }
+                }
+                if (found && !done && x >= 0 && S.sc[x] == p.cell && S.sh[x] == hk) {   // same key, this chunk
+                    mo_add_into(S, x, p);
+                    done = true;
+                }
+                if (found && !done) s = (s + 1) & rmask;
+            }
+            if (lost) overflow = true;
+        };
+#endif
         // the new state line of a claimed slot (old values read here: the slot's last store is visible) and its
         // update-mode row index
         // the slot's current line (all loads of a lane issued together; created slots read nothing)
-        auto old_line = [&](TileSlot *gslot, bool created) __attribute__((always_inline)) -> MLine {
+        auto old_line = [&](TileSlot *gslot, bool created, const MLine &pre, bool preloaded) __attribute__((always_inline)) -> MLine {
             MLine o{};
+            if (preloaded) o = pre;
+            created = created || preloaded;   // (the probe loaded it: nothing to load here)
 #if HM_MO_COOP_LINES
             // whole lines per load instruction (the mirror of step 4's stores): in round k, lane L loads part L & 3 of
             // the line of lane 16k + L / 4 (16-B non-temporal loads: L2-served, like ld_l2) into the wave's LDS slice,
@@ -1743,7 +1888,11 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             const int64_t i = c0 + t;
             const bool has = i < b1;
             MRec p{};
-            if (has) p = mrec_of(nxt, winfo, cell_hi);
+            if constexpr (kWi) {
+                if (has) p = mrec_of_wi(nxt, WI, winfo, cell_hi);
+            } else {
+                if (has) p = mrec_of(nxt, winfo, cell_hi);
+            }
             if (i + MO_THREADS < b1) nxt = ld_stream(parts + i + MO_THREADS);
             if (has) {
                 S.sc[t] = p.cell;
@@ -1757,18 +1906,24 @@ __global__ __launch_bounds__(MO_THREADS) void k_merge_owned(const Rec *__restric
             lds_barrier();
             // 2. find and claim the key's slot, or join the lane that holds it
             TileSlot *gslot = nullptr;
-            bool created = false;
+            bool created = false, preloaded = false;
             int r = -1, ci = -1;
+            MLine pre{};
+#if HM_MO_COOP_PROBE
+            if constexpr (kResident && kCoop) probe_coop(p, has, gslot, created, r, ci, pre, preloaded);
+            else if (has) probe(p, gslot, created, r, ci);
+#else
             if (has) probe(p, gslot, created, r, ci);
+#endif
             count_created(created, r);
 #if HM_MO_EARLY_LINES
             // 3a. the claimed existing lines, loaded before the barrier (their slots' last stores were drained by an
             // earlier chunk's barrier, and no store of this chunk precedes step 4): the round trip overlaps the wait
-            const MLine o = old_line(gslot, created);
+            const MLine o = old_line(gslot, created, pre, preloaded);
             lds_barrier();
 #else
             lds_barrier();
-            const MLine o = old_line(gslot, created);
+            const MLine o = old_line(gslot, created, pre, preloaded);
 #endif
             // 3. the claimers' new lines
             MLine v{};
@@ -2728,6 +2883,12 @@ struct hm_ctx {
     // (stage_inputs records the sources, phase_local issues copies and launches)
     static constexpr int H2D_CHUNKS = 16;
     hipStream_t copy_stream = nullptr;
+    // hm_process_batch's dedup (flag + compaction) runs on side_stream while the main stream partitions and merges:
+    // the two bind on different units (the dedup streams flags and probes a cache-resident table; the partition is
+    // write-pattern bound, the merge instruction-issue bound)
+    hipStream_t side_stream = nullptr;
+    hipEvent_t side_ev[3] = {};
+    bool dedup_side = false;
     hipEvent_t h2d_ev[H2D_CHUNKS] = {};
     struct H2D { const void *src; void *dst; size_t el; };
     H2D h2d[7] = {};
@@ -2785,6 +2946,7 @@ struct hm_ctx {
     // (MOBHEAT_MERGE_GRID, tuning)
     int merge_grid = 0;
     int64_t prev_agg_rows = 0, prev_keys = 0;   // aggregated rows and distinct keys of the last batch
+    bool merge_coop = false;   // the last batch's keys were mostly existing ones: the merge's cooperative probe
     bool last_table = false;
     int64_t last_counts[6] = {0, 0, 0, 0, 0, 0};   // hm_last_counts [0, 6) ([6], [7]: n_allocs, n_frees)
     int64_t n_allocs = 0, n_frees = 0;             // device + pinned-host allocations / frees since create
@@ -3200,7 +3362,8 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles) {
                            (unsigned *)ctx->bin_cnt.p, ctx->d_st, tag_bytes);
     };
     if constexpr (!rehash) {
-        if (resident) launch(k_merge_owned<Rec, true>);
+        if (resident && ctx->merge_coop) launch(k_merge_owned<Rec, true, true>);
+        else if (resident) launch(k_merge_owned<Rec, true>);
         else launch(k_merge_owned<Rec, false>);
     } else {
         launch(k_merge_owned<Rec, false>);
@@ -3399,16 +3562,16 @@ static int64_t dedup_fused_keys(const hm_ctx *ctx, int64_t n) {
 }
 
 // ordered compaction of byte flags -> int64 indices into ctx->rows; count into d_scratch[255]
-static int compact_flags(hm_ctx *ctx, const uint8_t *f, int64_t n, int64_t *out) {
+static int compact_flags(hm_ctx *ctx, const uint8_t *f, int64_t n, int64_t *out, hipStream_t st) {
     int64_t nb = (n + CP_TILE - 1) / CP_TILE;
     if (nb < 1) nb = 1;
     int rc;
     if ((rc = ensure(ctx, ctx->block_counts, nb * sizeof(unsigned)))) return rc;
     if ((rc = ensure(ctx, ctx->block_offs, nb * sizeof(unsigned long long)))) return rc;
-    hipLaunchKernelGGL(k_cp_count, dim3(nb), dim3(CP_THREADS), 0, ctx->stream, f, n, (unsigned *)ctx->block_counts.p);
-    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->block_counts.p, nb,
+    hipLaunchKernelGGL(k_cp_count, dim3(nb), dim3(CP_THREADS), 0, st, f, n, (unsigned *)ctx->block_counts.p);
+    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, st, (const unsigned *)ctx->block_counts.p, nb,
                        (unsigned long long *)ctx->block_offs.p, ctx->d_scratch + 255);
-    hipLaunchKernelGGL(k_cp_write, dim3(nb), dim3(CP_THREADS), 0, ctx->stream, f, n,
+    hipLaunchKernelGGL(k_cp_write, dim3(nb), dim3(CP_THREADS), 0, st, f, n,
                        (const unsigned long long *)ctx->block_offs.p, out);
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
@@ -3570,9 +3733,11 @@ static int phase_table(hm_ctx *ctx, const Inputs &I, int64_t n_agg, int64_t *n_p
 
 // Dedup over the batch's rows (I != nullptr; the per-vkey max came from k_ingest unless its probes gave up:
 // `rerun_max`) or over received candidates; result: ctx->rows indices, count in d_scratch[255].
-static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t n, bool rerun_max) {
+static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t n, bool rerun_max,
+                       hipStream_t st = nullptr) {
     int rc;
     const bool need_max = cands != nullptr || rerun_max;
+    if (!st) st = ctx->stream;
     hm_ctx::DedupTable &d = need_max ? ctx->dfull : ctx->dfused;
     if (need_max && (rc = dedup_prepare(ctx, d, n, false))) return rc;
     ctx->dlast = &d;
@@ -3580,18 +3745,18 @@ static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t 
         return rc;
     if (n > 0) {
         if (need_max) {
-            hipLaunchKernelGGL(k_dedup_max, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, I ? I->vk : nullptr,
+            hipLaunchKernelGGL(k_dedup_max, dim3(grid_for(n, 256)), dim3(256), 0, st, I ? I->vk : nullptr,
                                I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, d.tab, d.cap - 1,
                                (unsigned int *)d.used.p, ctx->d_scratch + d.used_word, ctx->d_st);
             d.dirty = true;
         }
-        hipLaunchKernelGGL(k_dedup_flag, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, I ? I->vk : nullptr,
+        hipLaunchKernelGGL(k_dedup_flag, dim3(grid_for(n, 256)), dim3(256), 0, st, I ? I->vk : nullptr,
                            I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, d.tab, d.cap - 1,
                            (uint8_t *)ctx->win.p, !need_max);
         HIPCHK(ctx, hipGetLastError());
-        if ((rc = compact_flags(ctx, (const uint8_t *)ctx->win.p, n, (int64_t *)ctx->rows.p))) return rc;
+        if ((rc = compact_flags(ctx, (const uint8_t *)ctx->win.p, n, (int64_t *)ctx->rows.p, st))) return rc;
     } else {
-        HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + 255, 0, 8, ctx->stream));
+        HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + 255, 0, 8, st));
     }
     return HM_OK;
 }
@@ -3771,6 +3936,8 @@ static void record_timings(hm_ctx *ctx) {
     ctx->timings[2] = el(3, 4);
     ctx->timings[3] = el(4, 5);
     ctx->timings[4] = el(5, 6);
+    if (ctx->dedup_side && !ctx->staged)   // (concurrent with the merge path: its own span on the side stream)
+        ctx->timings[4] = hipEventElapsedTime(&t, ctx->side_ev[1], ctx->side_ev[2]) == hipSuccess ? t : -1.0;
     ctx->timings[5] = el(0, 6);
     ctx->timings[2] = el(7, 4);   // merge proper
     ctx->timings[6] = el(3, 7);   // partition by table region
@@ -3807,12 +3974,17 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     };
     if (hipSetDevice(ctx->device) != hipSuccess) { ctx->err = "hipSetDevice"; return fail("create"); }
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess) { ctx->err = "stream"; return fail("create"); }
+        hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking) != hipSuccess) { ctx->err = "stream"; return fail("create"); }
+    for (auto &e : ctx->side_ev)
+        if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     for (auto &e : ctx->h2d_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     // k_merge_owned's resident tags live in dynamic LDS of up to MO_TAG_MAX bytes (merge_sorted)
     if (hipFuncSetAttribute((const void *)k_merge_owned<EventRec, false>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
         hipFuncSetAttribute((const void *)k_merge_owned<EventRec, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_merge_owned<EventRec, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_merge_owned<SortedRec, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
         hipFuncSetAttribute((const void *)k_merge_owned<SortedRec, false>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
         hipFuncSetAttribute((const void *)k_merge_owned<SortedRec, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess) {
         ctx->err = "merge LDS attribute";
@@ -3965,6 +4137,9 @@ void hm_destroy(hm_ctx *ctx) {
     for (auto &e : ctx->h2d_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+    if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);
+    for (auto &e : ctx->side_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -4012,9 +4187,20 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if ((rc = phase_local(ctx, I, late_wm))) return rc;
     DevStats s1 = *ctx->h_st;
     const int64_t n_agg = (int64_t)s1.n_valid - (int64_t)s1.n_late;
-    // 3. aggregate, merge into state + emit (table mode: two LDS passes first; direct: every row a record)
+    // the aggregation path of this batch (table mode: two LDS passes first; direct: every row a record)
     const bool table = choose_table(ctx, n_agg, s1.sample_max_run);
     ctx->last_table = table;
+    // 4. dedup over the batch's valid rows -- on the side stream, concurrently with step 3 (the rerun of the max on a
+    // full table, after the fused one gave up, prepares that table on the main stream: it stays there)
+    ctx->dedup_side = s1.dedup_retry == 0;
+    if (ctx->dedup_side) {
+        HIPCHK(ctx, hipEventRecord(ctx->side_ev[0], ctx->stream));
+        HIPCHK(ctx, hipStreamWaitEvent(ctx->side_stream, ctx->side_ev[0], 0));
+        HIPCHK(ctx, hipEventRecord(ctx->side_ev[1], ctx->side_stream));
+        if ((rc = phase_dedup(ctx, &I, nullptr, I.n, false, ctx->side_stream))) return rc;
+        HIPCHK(ctx, hipEventRecord(ctx->side_ev[2], ctx->side_stream));
+    }
+    // 3. aggregate, merge into state + emit (table mode: two LDS passes first; direct: every row a record)
     if (table) {
         int64_t n_parts = 0;
         if ((rc = phase_table(ctx, I, n_agg, &n_parts))) return rc;
@@ -4024,8 +4210,11 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
         HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
         if ((rc = merge_events(ctx, I, n_agg))) return rc;
     }
-    // 4. dedup over the batch's valid rows
-    if ((rc = phase_dedup(ctx, &I, nullptr, I.n, s1.dedup_retry != 0))) return rc;
+    if (!ctx->dedup_side) {
+        if ((rc = phase_dedup(ctx, &I, nullptr, I.n, true))) return rc;
+    } else {
+        HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[2], 0));
+    }
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 256 * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -4052,6 +4241,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if (n_agg >= (int64_t(1) << 16)) {
         ctx->prev_agg_rows = n_agg;
         ctx->prev_keys = (int64_t)s2.n_touched;
+        ctx->merge_coop = s2.n_touched > 0 && 2 * s2.n_state_new < s2.n_touched;
     }
     // 5. eviction after emission with this batch's watermark (lazy: see hm_ctx), then advance the watermark
     if ((rc = state_account(ctx, ctx->wm_cur))) return rc;
@@ -4465,6 +4655,7 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, const void *payload_r
     if (ctx->stage_agg_rows >= (int64_t(1) << 16)) {   // this rank's rows and owned keys (summed over ranks next batch)
         ctx->prev_agg_rows = ctx->stage_agg_rows;
         ctx->prev_keys = (int64_t)s2.n_touched;
+        ctx->merge_coop = s2.n_touched > 0 && 2 * s2.n_state_new < s2.n_touched;
     }
     if ((rc = state_account(ctx, ctx->wm_cur))) return rc;
     DevStats sf{};
@@ -4942,7 +5133,7 @@ static int dict_build(hm_ctx *ctx, hm_ctx::Dict &d, const uint8_t *bytes, const 
         return rc;
     hipLaunchKernelGGL(k_dict_occ, dim3(grid_for((int64_t)cap, 256)), dim3(256), 0, ctx->stream, (const DictSlot *)d.tab.p,
                        (int64_t)cap, (uint8_t *)d.occ.p);
-    if ((rc = compact_flags(ctx, (const uint8_t *)d.occ.p, (int64_t)cap, (int64_t *)d.slots.p))) return rc;
+    if ((rc = compact_flags(ctx, (const uint8_t *)d.occ.p, (int64_t)cap, (int64_t *)d.slots.p, ctx->stream))) return rc;
     unsigned long long nc = 0;
     HIPCHK(ctx, hipMemcpyAsync(&nc, ctx->d_scratch + 255, 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, ctx_sync(ctx, __LINE__));
