@@ -574,7 +574,8 @@ HM_HD void sincos_small(double x, double &s, double &c) {
     c = ((k + 1) & 2) ? -b : b;
 }
 
-HM_HD double dmin(double a, double b) { return a < b ? a : b; }
+// (v_min_f64: one instruction instead of a compare and two selects; the margins it takes are never NaN)
+HM_HD double dmin(double a, double b) { return __builtin_fmin(a, b); }
 
 #include "face_dodeca.inc"
 // Closest face from the dodecahedron's symmetry (tools/gen_face_dodeca.py): R takes H3's face centres onto the

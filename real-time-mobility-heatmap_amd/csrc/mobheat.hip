@@ -1513,8 +1513,8 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     extern __shared__ unsigned mo_tags[];   // tag_bytes of resident region tags
     __shared__ WinLds WL;
     __shared__ GenCache C;
-#ifndef HM_MO_WI_LDS
-#define HM_MO_WI_LDS 1
+#ifndef HM_MO_WI_LDS   // (off: the image's LDS cost the state-read leg's merge ~1 ms, profiles/r3/r3ab11)
+#define HM_MO_WI_LDS 0
 #endif
     constexpr bool kWi = HM_MO_WI_LDS && std::is_same<Rec, EventRec>::value;
     __shared__ std::conditional_t<kWi, WiCacheL, char> WI;   // EventRec: the window parameters' LDS image

@@ -15,5 +15,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc_fetch -o r
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- $P > $O/pmc_write.log 2>&1 && \
 python3 tools/ingest_pmc.py --res 8 --events 100000000 --out $O/kernel_pmc.json $O/pmc_f64 $O/pmc_sq $O/pmc_fetch $O/pmc_write > $O/ingest_pmc.log 2>&1 && \
 mkdir -p profiles/r3 && cp $O/kernel_pmc.json profiles/r3/kernel_pmc.json && \
-timeout -k 10 600 python3 bench.py > $O/bench.log 2>&1
+timeout -k 10 600 python3 bench.py > $O/bench.log 2>&1 && \
+timeout -k 10 120 ./tools/microbench/scatter_bw > $O/scatter_bw.log 2>&1
 rc=$?; echo "done rc=$rc"; exit $rc
