@@ -2029,6 +2029,22 @@ __global__ __launch_bounds__(256) void k_zero16(uint4 *__restrict__ p, int64_t n
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) p[i] = make_uint4(0u, 0u, 0u, 0u);
 }
+
+// the start of a batch in one launch (was six memsets and a copy): the batch statistics (max ts / min window start
+// at their identities), the fast-path exception and dedup give-up words, the window registry and its census
+__global__ __launch_bounds__(256) void k_batch_reset(unsigned long long *__restrict__ st, unsigned long long *__restrict__ slow_word,
+                                                     unsigned long long *__restrict__ giveup_word, unsigned long long *__restrict__ wreg2,
+                                                     int n_wreg2) {
+    static_assert(sizeof(DevStats) % 8 == 0 && offsetof(DevStats, min_wstart) == offsetof(DevStats, max_ts_ms) + 8, "DevStats");
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_wreg2) wreg2[i] = 0;
+    if (i < (int)(sizeof(DevStats) / 8)) {
+        const int mx = (int)(offsetof(DevStats, max_ts_ms) / 8);
+        st[i] = i == mx ? (unsigned long long)INT64_MIN : i == mx + 1 ? (unsigned long long)INT64_MAX : 0ull;
+    }
+    if (i == 0) { *slow_word = 0; *giveup_word = 0; }
+}
+
 // In-place densification of the per-bin row segments: bin b's merged rows are [s_b, s_b + c_b) of the staging
 // arrays (s_b = the bin's first partial, c_b its touched keys), so the rows [0, T) (T = sum c_b) are dense except
 // for the gaps left by keys with several partials; each gap below T takes one row from above T (gap i <- the i-th
@@ -2473,38 +2489,41 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
 }
 
 // Heavy hitters in the batch's event keys, for the choice of the aggregation path when the last batch says nothing
-// (the first batch, or a sudden change of the data): HS_SAMPLE keys at an even stride, bitonic-sorted in LDS, the
-// longest run of equal keys -> DevStats.sample_max_run.  A key holding a few % of the rows would put that share of the
+// (the first batch, or a sudden change of the data): HS_SAMPLE keys at an even stride, the largest
+// multiplicity among them -> DevStats.sample_max_run.  A key holding a few % of the rows would put that share of the
 // batch through one merge workgroup (one bin) on the direct path; table mode aggregates it in LDS first.
-constexpr int HS_SAMPLE = 4096, HS_THREADS = 1024;
+constexpr int HS_SAMPLE = 4096, HS_THREADS = 1024, HS_SLOTS = 2 * HS_SAMPLE;
+// (the multiplicities counted in an LDS hash table at load <= 1/2: was a bitonic sort of the sample, 78 barriers)
 __global__ __launch_bounds__(HS_THREADS) void k_sample_heavy(const uint64_t *__restrict__ keys, int64_t n, DevStats *st) {
-    __shared__ unsigned long long k[HS_SAMPLE];
+    __shared__ unsigned long long k[HS_SLOTS];
+    __shared__ unsigned c[HS_SLOTS];
     __shared__ unsigned best;
     const int t = threadIdx.x;
     const int64_t stride = n / HS_SAMPLE > 0 ? n / HS_SAMPLE : 1;
-    for (int q = t; q < HS_SAMPLE; q += HS_THREADS) {
-        const int64_t i = (int64_t)q * stride;
-        const uint64_t v = i < n ? keys[i] : 0;
-        k[q] = v ? v : ~0ull;   // rows without a key sort last and are not counted
+    constexpr int PER = HS_SAMPLE / HS_THREADS;
+    uint64_t v[PER];
+#pragma unroll
+    for (int u = 0; u < PER; u++) {   // every load in flight before the table is cleared
+        const int64_t i = (int64_t)(t + u * HS_THREADS) * stride;
+        v[u] = i < n ? keys[i] : 0;
     }
+    for (int q = t; q < HS_SLOTS; q += HS_THREADS) { k[q] = 0; c[q] = 0; }
     if (t == 0) best = 0;
     __syncthreads();
-    for (int size = 2; size <= HS_SAMPLE; size <<= 1)
-        for (int stride2 = size >> 1; stride2 > 0; stride2 >>= 1) {
-            for (int q = t; q < HS_SAMPLE / 2; q += HS_THREADS) {
-                const int lo = 2 * q - (q & (stride2 - 1)), hi = lo + stride2;
-                const bool up = (lo & size) == 0;
-                const unsigned long long a = k[lo], b = k[hi];
-                if ((a > b) == up) { k[lo] = b; k[hi] = a; }
-            }
-            __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+        if (!v[u]) continue;   // rows without a key are not counted
+        unsigned h = (unsigned)mix64(v[u]) & (HS_SLOTS - 1);
+        for (;;) {   // (at most HS_SAMPLE keys in 2 x as many slots: an empty or matching slot is always found)
+            const unsigned long long prev = atomicCAS(&k[h], 0ull, (unsigned long long)v[u]);
+            if (prev == 0 || prev == v[u]) { atomicAdd(&c[h], 1u); break; }
+            h = (h + 1) & (HS_SLOTS - 1);
         }
-    for (int q = t; q < HS_SAMPLE; q += HS_THREADS) {
-        if (k[q] == ~0ull || (q > 0 && k[q - 1] == k[q])) continue;   // q starts a run of a real key
-        int e = q + 1;
-        while (e < HS_SAMPLE && k[e] == k[q]) e++;
-        atomicMax(&best, (unsigned)(e - q));
     }
+    __syncthreads();
+    unsigned m = 0;
+    for (int q = t; q < HS_SLOTS; q += HS_THREADS) m = c[q] > m ? c[q] : m;
+    atomicMax(&best, m);
     __syncthreads();
     if (t == 0) st->sample_max_run = best;
 }
@@ -2887,7 +2906,7 @@ struct hm_ctx {
     // the two bind on different units (the dedup streams flags and probes a cache-resident table; the partition is
     // write-pattern bound, the merge instruction-issue bound)
     hipStream_t side_stream = nullptr;
-    hipEvent_t side_ev[3] = {};
+    hipEvent_t side_ev[4] = {};   // [3]: the pooled tables' tags cleared (table_release)
     bool dedup_side = false;
     hipEvent_t h2d_ev[H2D_CHUNKS] = {};
     struct H2D { const void *src; void *dst; size_t el; };
@@ -2913,6 +2932,7 @@ struct hm_ctx {
     uint8_t *arena = nullptr;
     size_t arena_bytes = 0, arena_used = 0;
     GenDesc *d_gmap = nullptr, *h_gmap = nullptr;   // device map window -> table (host mirror)
+    bool gmap_ready = false;                         // h_gmap holds the device map after this batch's merge
     GenDesc *d_glist = nullptr, *h_glist = nullptr; // the same descriptors as a dense list (kernels' LDS cache)
     int n_glist = 0;
     bool census_ready = false;                      // k_ingest filled d_cmap for this batch's partials
@@ -2967,6 +2987,7 @@ struct hm_ctx {
     unsigned long long *d_wreg = nullptr, *h_wreg = nullptr;     // the batch's window registry (WREG_SLOTS wenc)
     unsigned long long *d_wcount = nullptr, *h_wcount = nullptr; // aggregated rows per registry slot (census)
     WInfo *d_winfo = nullptr, *h_winfo = nullptr;   // per registry slot: window parameters of the direct path
+    hipEvent_t winfo_ev = nullptr;                    // recorded after the last upload from h_winfo
     DevBuf agg_bucket, agg_cursor;   // table mode: k_agg's buckets (AG_BINS x AG_SUB x cap AggRecs) + fill cursors
     unsigned agg_cap = 0;            // AggRecs per sub-bucket
     std::vector<unsigned long long> h_agg_cursor;
@@ -3164,11 +3185,8 @@ static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **
         log2cap = ctx->pool[best].second;
         rbits = (unsigned)std::min(RP_BITS, log2cap - REGION_MIN_BITS);
         ctx->pool.erase(ctx->pool.begin() + best);
-        // the slots keep the previous window's keys (never matched: other wenc), the tags start empty
-        const int64_t n16 = (int64_t(1) << log2cap) / 16;   // (2^log2cap >= 1024 tag bytes, 64-B aligned)
-        hipLaunchKernelGGL(k_zero16, dim3(grid_for(n16, 256, 256 * 32)), dim3(256), 0, ctx->stream,
-                           (uint4 *)(*out + (size_t(1) << log2cap)), n16);
-        HIPCHK(ctx, hipGetLastError());
+        // the slots keep the previous window's keys (never matched: other wenc), the tags were cleared at release
+        HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[3], 0));
         return HM_OK;
     }
     const size_t bytes = (size_t(1) << log2cap) * (sizeof(TileSlot) + 1);   // slots, then one tag byte per slot
@@ -3181,6 +3199,7 @@ static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **
     if (dev_malloc(ctx, (void **)&t, bytes, "state table") != hipSuccess) {
         (void)hipGetLastError();
         HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->side_stream));   // (pooled tags being cleared: table_release)
         std::vector<std::pair<TileSlot *, int>> keep;
         for (auto &pt : ctx->pool)
             if (in_arena(ctx, pt.first)) keep.push_back(pt); else { AllocTimer at_(ctx); (void)hipFree(pt.first); ctx->n_frees++; }
@@ -3195,22 +3214,34 @@ static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **
     *out = t;
     return HM_OK;
 }
-// (the stream must have drained every kernel that reads the table)
-static void table_release(hm_ctx *ctx, TileSlot *t, int log2cap) {
+// (the stream must have drained every kernel that reads the table).  The table's tags are cleared at once on the
+// side stream -- behind the main stream's work so far, concurrent with the next batch's first kernels (k_ingest does
+// not use the HBM bandwidth) -- and table_acquire waits for that (side_ev[3]).
+static int table_release(hm_ctx *ctx, TileSlot *t, int log2cap) {
+    const int64_t n16 = (int64_t(1) << log2cap) / 16;   // (2^log2cap >= 1024 tag bytes, 64-B aligned)
+    HIPCHK(ctx, hipEventRecord(ctx->side_ev[0], ctx->stream));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->side_stream, ctx->side_ev[0], 0));
+    hipLaunchKernelGGL(k_zero16, dim3(grid_for(n16, 256, 256 * 32)), dim3(256), 0, ctx->side_stream,
+                       (uint4 *)(t + (size_t(1) << log2cap)), n16);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventRecord(ctx->side_ev[3], ctx->side_stream));
     ctx->pool.emplace_back(t, log2cap);
     size_t own = 0;   // pooled tables of our own allocations (arena tables stay pooled)
     for (auto &pt : ctx->pool) own += !in_arena(ctx, pt.first);
     for (size_t i = 0; own > 8 && i < ctx->pool.size();) {
         if (in_arena(ctx, ctx->pool[i].first)) { i++; continue; }
+        HIPCHK(ctx, hipStreamSynchronize(ctx->side_stream));   // (its tags may still be being cleared)
         { AllocTimer at_(ctx); (void)hipFree(ctx->pool[i].first); }
         ctx->n_frees++;
         ctx->pool.erase(ctx->pool.begin() + i);
         own--;
     }
+    return HM_OK;
 }
 
 static int gens_upload(hm_ctx *ctx) {
     memset(ctx->h_gmap, 0, GMAP_SLOTS * sizeof(GenDesc));
+    ctx->gmap_ready = false;   // (h_gmap is the upload's staging now)
     for (const auto &g : ctx->gens) {
         unsigned h = (unsigned)(mix64(g.wenc) & (GMAP_SLOTS - 1));
         while (ctx->h_gmap[h].wenc) h = (h + 1) & (GMAP_SLOTS - 1);
@@ -3400,7 +3431,7 @@ static void census_of_registry(const hm_ctx *ctx, std::vector<WinCount> &census)
 // WInfo of every registry slot in use (after gens_prepare when with_bins: the radix bin parameters need the
 // window's table geometry)
 static int winfo_upload(hm_ctx *ctx, bool with_bins) {
-    HIPCHK(ctx, ctx_sync(ctx, __LINE__));   // (h_winfo is reused: the previous upload must be done)
+    HIPCHK(ctx, hipEventSynchronize(ctx->winfo_ev));   // (h_winfo is reused: the previous upload must be done)
     WInfo *h = ctx->h_winfo;
     int lo = WREG_SLOTS, hi = -1;
     for (int w = 0; w < WREG_SLOTS; w++) {
@@ -3440,6 +3471,7 @@ static int winfo_upload(hm_ctx *ctx, bool with_bins) {
         }
     }
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_winfo + WREG_SLOTS + 1, img, sizeof(WiCacheImg), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipEventRecord(ctx->winfo_ev, ctx->stream));
     return HM_OK;
 }
 
@@ -3497,7 +3529,8 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census) {
         if ((rc = partition<GrowRec, GrowRec>(ctx, (const GrowRec *)ctx->parts_regrow.p, moved, ntiles))) return rc;
         if ((rc = merge_sorted<GrowRec>(ctx, moved, ntiles))) return rc;
         HIPCHK(ctx, ctx_sync(ctx, __LINE__));
-        for (const auto &g : old) table_release(ctx, g.tab, g.log2cap);
+        for (const auto &g : old)
+            if ((rc = table_release(ctx, g.tab, g.log2cap))) return rc;
     }
     return HM_OK;
 }
@@ -3505,8 +3538,11 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census) {
 // After a batch: every window's key count from the device; windows whose end <= the eviction watermark are
 // released whole (their rows are late from now on); n_state = keys of the live windows.
 static int state_account(hm_ctx *ctx, int64_t evict_wm_ms) {
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_gmap, ctx->d_gmap, GMAP_SLOTS * sizeof(GenDesc), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+    if (!ctx->gmap_ready) {
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_gmap, ctx->d_gmap, GMAP_SLOTS * sizeof(GenDesc), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+    }
+    ctx->gmap_ready = false;
     const int64_t dead_end_us = evict_wm_ms * 1000;
     int64_t live = 0;
     std::vector<hm_ctx::Gen> keep;
@@ -3515,7 +3551,7 @@ static int state_account(hm_ctx *ctx, int64_t evict_wm_ms) {
         for (int p = 0; p < GMAP_SLOTS && ctx->h_gmap[h].wenc; p++, h = (h + 1) & (GMAP_SLOTS - 1))
             if (ctx->h_gmap[h].wenc == g.wenc) { g.keys = (int64_t)ctx->h_gmap[h].count; break; }
         if (wdec(g.wenc) + ctx->cfg.tile_us <= dead_end_us) {
-            table_release(ctx, g.tab, g.log2cap);
+            if (int rc = table_release(ctx, g.tab, g.log2cap)) return rc;
         } else {
             live += g.keys;
             keep.push_back(g);
@@ -3624,13 +3660,12 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
         (rc = ensure(ctx, ctx->keys, n * 8)) || (rc = ensure(ctx, ctx->slow, n * sizeof(unsigned int))))
         return rc;
     if ((rc = dedup_prepare(ctx, ctx->dfused, dedup_fused_keys(ctx, n), true))) return rc;
-    HIPCHK(ctx, hipMemsetAsync(ctx->d_st, 0, sizeof(DevStats), ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + SLOW_WORD, 0, 8, ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + GIVEUP_WORD, 0, 8, ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(ctx->d_wreg, 0, (WREG_SLOTS + 1) * 8, ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(ctx->d_wcount, 0, (WREG_SLOTS + 1) * 8, ctx->stream));
-    long long init[2] = {INT64_MIN, INT64_MAX};
-    HIPCHK(ctx, hipMemcpyAsync(&ctx->d_st->max_ts_ms, init, sizeof(init), hipMemcpyHostToDevice, ctx->stream));
+    {
+        const int nw = 2 * (WREG_SLOTS + 1);   // d_wreg and d_wcount: one allocation (hm_create)
+        hipLaunchKernelGGL(k_batch_reset, dim3((nw + 255) / 256), dim3(256), 0, ctx->stream, (unsigned long long *)ctx->d_st,
+                           ctx->d_scratch + SLOW_WORD, ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, nw);
+        HIPCHK(ctx, hipGetLastError());
+    }
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
     if (n > 0) {
         // host inputs: row chunks copied on copy_stream, each chunk's k_ingest launched behind its copy (the copies
@@ -3668,8 +3703,7 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
     // the batch statistics and the registry with its census, read back together
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_wreg, ctx->d_wreg, WREG_SLOTS * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_wcount, ctx->d_wcount, WREG_SLOTS * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_wreg, ctx->d_wreg, 2 * (WREG_SLOTS + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));   // (+ h_wcount)
     HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     if (ctx->h_st->win_overflow)
         return set_err(ctx, HM_E_OVERFLOW, "more than %d distinct windows in one micro-batch (%llu rows)", WREG_SLOTS,
@@ -3799,8 +3833,8 @@ static int rows_densify(hm_ctx *ctx, int64_t ntiles) {
 }
 
 static int merge_begin(hm_ctx *ctx, int64_t n_rows) {
-    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_touched, 0, 8, ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_state_new, 0, 8, ctx->stream));
+    static_assert(offsetof(DevStats, n_state_new) == offsetof(DevStats, n_touched) + 8, "DevStats");
+    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_touched, 0, 16, ctx->stream));   // (+ n_state_new)
     HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
     ctx->seq++;
     ctx->batch_windows.clear();
@@ -3978,6 +4012,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking) != hipSuccess) { ctx->err = "stream"; return fail("create"); }
     for (auto &e : ctx->side_ev)
         if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
+    if (hipEventCreateWithFlags(&ctx->winfo_ev, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     for (auto &e : ctx->h2d_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     // k_merge_owned's resident tags live in dynamic LDS of up to MO_TAG_MAX bytes (merge_sorted)
@@ -4014,9 +4049,10 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     // MOBHEAT_INGEST_MODE=direct|table pins the aggregation path (tests); default: adaptive
     if (const char *m = getenv("MOBHEAT_INGEST_MODE")) ctx->ingest_mode = !strcmp(m, "direct") ? 1 : !strcmp(m, "table") ? 2 : 0;
     if (const char *m = getenv("MOBHEAT_MERGE_GRID")) ctx->merge_grid = std::max(0, atoi(m));
-    if (hipMalloc(&ctx->d_wreg, (WREG_SLOTS + 1) * 8) != hipSuccess || hipMalloc(&ctx->d_wcount, (WREG_SLOTS + 1) * 8) != hipSuccess ||
-        hipHostMalloc(&ctx->h_wreg, (WREG_SLOTS + 1) * 8, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(&ctx->h_wcount, (WREG_SLOTS + 1) * 8, hipHostMallocDefault) != hipSuccess ||
+    // the registry and its census side by side (one reset, one readback per batch)
+    if (hipMalloc(&ctx->d_wreg, 2 * (WREG_SLOTS + 1) * 8) != hipSuccess || !(ctx->d_wcount = ctx->d_wreg + WREG_SLOTS + 1) ||
+        hipHostMalloc(&ctx->h_wreg, 2 * (WREG_SLOTS + 1) * 8, hipHostMallocDefault) != hipSuccess ||
+        !(ctx->h_wcount = ctx->h_wreg + WREG_SLOTS + 1) ||
         hipMalloc(&ctx->d_winfo, (WREG_SLOTS + 1) * sizeof(WInfo) + sizeof(WiCacheImg)) != hipSuccess ||
         hipHostMalloc(&ctx->h_winfo, (WREG_SLOTS + 1) * sizeof(WInfo) + sizeof(WiCacheImg), hipHostMallocDefault) != hipSuccess ||
         hipMemset(ctx->d_winfo, 0, (WREG_SLOTS + 1) * sizeof(WInfo)) != hipSuccess ||
@@ -4075,8 +4111,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         int L = ilog2(next_pow2((uint64_t)std::max<int64_t>(2 * cfg->state_capacity_hint, 1024)));
         unsigned rb = 0;
         TileSlot *t = nullptr;
-        if (table_acquire(ctx, L, rb, &t)) return fail("create");
-        table_release(ctx, t, L);
+        if (table_acquire(ctx, L, rb, &t) || table_release(ctx, t, L)) return fail("create");
     }
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) { ctx->err = "sync"; return fail("create"); }
     *out = ctx;
@@ -4087,6 +4122,7 @@ void hm_destroy(hm_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
     DevBuf *bufs[] = {&ctx->in_lat, &ctx->in_lon, &ctx->in_ts, &ctx->in_speed, &ctx->in_sv, &ctx->in_vkey, &ctx->in_rv,
                       &ctx->cell, &ctx->wstart, &ctx->flags, &ctx->win, &ctx->rows, &ctx->block_counts, &ctx->block_offs,
                       &ctx->partials, &ctx->cands, &ctx->slow, &ctx->parts_sorted, &ctx->parts_regrow, &ctx->rp_H, &ctx->rp_O,
@@ -4110,10 +4146,8 @@ void hm_destroy(hm_ctx *ctx) {
     for (auto &pt : ctx->pool)
         if (!in_arena(ctx, pt.first)) (void)hipFree(pt.first);
     if (ctx->arena) (void)hipFree(ctx->arena);
-    if (ctx->d_wreg) (void)hipFree(ctx->d_wreg);
-    if (ctx->d_wcount) (void)hipFree(ctx->d_wcount);
+    if (ctx->d_wreg) (void)hipFree(ctx->d_wreg);   // (d_wcount / h_wcount: inside these)
     if (ctx->h_wreg) (void)hipHostFree(ctx->h_wreg);
-    if (ctx->h_wcount) (void)hipHostFree(ctx->h_wcount);
     if (ctx->d_winfo) (void)hipFree(ctx->d_winfo);
     if (ctx->h_winfo) (void)hipHostFree(ctx->h_winfo);
     if (ctx->d_gmap) (void)hipFree(ctx->d_gmap);
@@ -4140,6 +4174,7 @@ void hm_destroy(hm_ctx *ctx) {
     if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);
     for (auto &e : ctx->side_ev)
         if (e) (void)hipEventDestroy(e);
+    if (ctx->winfo_ev) (void)hipEventDestroy(ctx->winfo_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -4164,6 +4199,51 @@ int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n) {
     return HM_OK;
 }
 
+#ifdef HM_EXP_OVERLAP
+// experiment build only (tools/gpurun/gpurun_r3ov.sh): after a direct-path batch, k_ingest (into scratch keys) and
+// k_ev_scatter_rec (the batch's own records again) timed alone and on two streams together
+static void exp_overlap(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
+    static DevBuf ek, ef;
+    const int64_t n = I.n;
+    if (n <= 0 || ensure(ctx, ek, n * 8) || ensure(ctx, ef, n)) return;
+    const int64_t tile = rp_tile_for(n), ntiles = std::max<int64_t>((n + tile - 1) / tile, 1);
+    hipEvent_t e[4];
+    for (auto &x : e) hipEventCreate(&x);
+    auto ingest = [&](hipStream_t st) {
+        hipMemsetAsync(ctx->d_scratch + SLOW_WORD, 0, 8, st);
+        const int blocks = (int)std::min<int64_t>((n + IG_THREADS - 1) / IG_THREADS, ctx->ingest_grid);
+        hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(IG_THREADS), 0, st, I.lat, I.lon, I.ts, I.rv, I.vk, (int64_t)0, n,
+                           ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ef.p,
+                           (uint64_t *)ek.p, ctx->dfused.tab, ctx->dfused.cap - 1, (unsigned int *)ctx->dfused.used.p,
+                           ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
+                           ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st);
+    };
+    auto scatter = [&](hipStream_t st) {
+        hipLaunchKernelGGL(k_ev_scatter_rec<false>, dim3(ntiles), dim3(EV_THREADS), 0, st, (const uint64_t *)ctx->keys.p, n, tile,
+                           I.sp, I.sv, I.lat, I.lon, nullptr, (const WInfo *)ctx->d_winfo, cell_hi_of(ctx->cfg.h3_res), RP_BINS,
+                           (const unsigned long long *)ctx->rp_O.p, ntiles, (EventRec *)ctx->parts_sorted.p);
+    };
+    for (int rep = 0; rep < 3; rep++) {
+        float ms[3];
+        hipEventRecord(e[0], ctx->stream); ingest(ctx->stream); hipEventRecord(e[1], ctx->stream);
+        hipStreamSynchronize(ctx->stream); hipEventElapsedTime(&ms[0], e[0], e[1]);
+        hipEventRecord(e[0], ctx->stream); scatter(ctx->stream); hipEventRecord(e[1], ctx->stream);
+        hipStreamSynchronize(ctx->stream); hipEventElapsedTime(&ms[1], e[0], e[1]);
+        hipEventRecord(e[0], ctx->stream);
+        hipStreamWaitEvent(ctx->side_stream, e[0], 0);
+        ingest(ctx->stream);
+        scatter(ctx->side_stream);
+        hipEventRecord(e[2], ctx->side_stream);
+        hipStreamWaitEvent(ctx->stream, e[2], 0);
+        hipEventRecord(e[1], ctx->stream);
+        hipStreamSynchronize(ctx->stream); hipEventElapsedTime(&ms[2], e[0], e[1]);
+        fprintf(stderr, "exp_overlap ingest %.3f scatter %.3f both %.3f ms (sum %.3f)\n", ms[0], ms[1], ms[2], ms[0] + ms[1]);
+    }
+    for (auto &x : e) hipEventDestroy(x);
+    ctx->dfused.dirty = true;
+}
+#endif
+
 int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t out_memory, hm_batch_out *out) {
     if (!ctx || !in || !out || in->n < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
     if (in->n > (int64_t)UINT32_MAX - 1) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds 2^32-2", (long long)in->n);
@@ -4173,6 +4253,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     host_batch_begin(ctx);
     const BatchClock clock_(ctx);
     memset(out, 0, sizeof(*out));
+    ctx->gmap_ready = false;
     ctx->epoch = epoch_id;
     ctx->last_n_latest = -1;
     ctx->staged = false;
@@ -4193,12 +4274,9 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     // 4. dedup over the batch's valid rows -- on the side stream, concurrently with step 3 (the rerun of the max on a
     // full table, after the fused one gave up, prepares that table on the main stream: it stays there)
     ctx->dedup_side = s1.dedup_retry == 0;
-    if (ctx->dedup_side) {
+    if (ctx->dedup_side) {   // (launched after the merge path's kernels: those are the critical path)
         HIPCHK(ctx, hipEventRecord(ctx->side_ev[0], ctx->stream));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->side_stream, ctx->side_ev[0], 0));
-        HIPCHK(ctx, hipEventRecord(ctx->side_ev[1], ctx->side_stream));
-        if ((rc = phase_dedup(ctx, &I, nullptr, I.n, false, ctx->side_stream))) return rc;
-        HIPCHK(ctx, hipEventRecord(ctx->side_ev[2], ctx->side_stream));
     }
     // 3. aggregate, merge into state + emit (table mode: two LDS passes first; direct: every row a record)
     if (table) {
@@ -4213,12 +4291,18 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if (!ctx->dedup_side) {
         if ((rc = phase_dedup(ctx, &I, nullptr, I.n, true))) return rc;
     } else {
+        HIPCHK(ctx, hipEventRecord(ctx->side_ev[1], ctx->side_stream));
+        if ((rc = phase_dedup(ctx, &I, nullptr, I.n, false, ctx->side_stream))) return rc;
+        HIPCHK(ctx, hipEventRecord(ctx->side_ev[2], ctx->side_stream));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[2], 0));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 256 * 8, hipMemcpyDeviceToHost, ctx->stream));
+    // (the window map's key counts for state_account, read back in the same wait)
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_gmap, ctx->d_gmap, GMAP_SLOTS * sizeof(GenDesc), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+    ctx->gmap_ready = true;
     ctx->dedup_seen = (int64_t)ctx->h_scratch[ctx->dlast->used_word];   // distinct vkeys of this batch
     DevStats s2 = *ctx->h_st;
     if (s2.overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
@@ -4247,6 +4331,9 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if ((rc = state_account(ctx, ctx->wm_cur))) return rc;
     fill_stats(ctx, out, in->n, s1, late_wm);
     advance_watermark(ctx, s1.max_ts_ms);
+#ifdef HM_EXP_OVERLAP
+    if (!table && getenv("MOBHEAT_EXP_OVERLAP")) exp_overlap(ctx, I, late_wm);
+#endif
     return HM_OK;
 }
 
