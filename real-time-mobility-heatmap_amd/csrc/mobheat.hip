@@ -2917,6 +2917,8 @@ struct hm_ctx {
     // write-pattern bound, the merge instruction-issue bound)
     hipStream_t side_stream = nullptr;
     hipEvent_t side_ev[4] = {};   // [3]: the pooled tables' tags cleared (table_release)
+    hipEvent_t hist_ev = nullptr;   // the direct path's k_ev_hist launched (the side-stream dedup starts behind it)
+    const struct Inputs *side_dedup_in = nullptr;   // the batch whose side-stream dedup ev_partition launches
     bool dedup_side = false;
     hipEvent_t h2d_ev[H2D_CHUNKS] = {};
     struct H2D { const void *src; void *dst; size_t el; };
@@ -3317,6 +3319,16 @@ static int partition(hm_ctx *ctx, const In *parts, int64_t n, int64_t &ntiles, i
 // the direct path's partition: n event keys with the batch's columns (I) or, on a multi-GPU owner, the received payload
 // stream -> EventRecs in (window, region) bins (parts_sorted); or with nranks > 0 the wire streams grouped by owner rank
 // (dst = key stream, payload_out); rows without a key fall into digit nbins (dropped)
+static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t n, bool rerun_max, hipStream_t st);
+// the batch's dedup on the side stream (hm_process_batch): side_ev[1] / [2] bracket it
+static int launch_side_dedup(hm_ctx *ctx, const Inputs *I) {
+    int rc;
+    HIPCHK(ctx, hipEventRecord(ctx->side_ev[1], ctx->side_stream));
+    if ((rc = phase_dedup(ctx, I, nullptr, I->n, false, ctx->side_stream))) return rc;
+    HIPCHK(ctx, hipEventRecord(ctx->side_ev[2], ctx->side_stream));
+    return HM_OK;
+}
+
 template <typename Out>
 static int ev_partition(hm_ctx *ctx, const uint64_t *keys, int64_t n, const Inputs *I, const uint64_t *payload_in,
                         int64_t &ntiles, int nranks = 0, Out *dst = nullptr, uint64_t *payload_out = nullptr) {
@@ -3331,6 +3343,13 @@ static int ev_partition(hm_ctx *ctx, const uint64_t *keys, int64_t n, const Inpu
     const uint64_t ch = cell_hi_of(ctx->cfg.h3_res);
     hipLaunchKernelGGL(k_ev_hist, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, (const WInfo *)ctx->d_winfo, ch,
                        nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles);
+    if (ctx->side_dedup_in) {   // the batch's dedup, behind the histogram (both read HBM at full rate)
+        HIPCHK(ctx, hipEventRecord(ctx->hist_ev, ctx->stream));
+        HIPCHK(ctx, hipStreamWaitEvent(ctx->side_stream, ctx->hist_ev, 0));
+        const Inputs *di = ctx->side_dedup_in;
+        ctx->side_dedup_in = nullptr;
+        if ((rc = launch_side_dedup(ctx, di))) return rc;
+    }
     if ((rc = rp_scan(ctx, m))) return rc;
     if constexpr (std::is_same<Out, EventRec>::value) {
         if (nranks != 0 || dst) return set_err(ctx, HM_E_STATE, "ev_partition: EventRecs go to the context's bins");
@@ -4022,7 +4041,8 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking) != hipSuccess) { ctx->err = "stream"; return fail("create"); }
     for (auto &e : ctx->side_ev)
         if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
-    if (hipEventCreateWithFlags(&ctx->winfo_ev, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
+    if (hipEventCreateWithFlags(&ctx->winfo_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->hist_ev, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     for (auto &e : ctx->h2d_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     // k_merge_owned's resident tags live in dynamic LDS of up to MO_TAG_MAX bytes (merge_sorted)
@@ -4185,6 +4205,7 @@ void hm_destroy(hm_ctx *ctx) {
     for (auto &e : ctx->side_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->winfo_ev) (void)hipEventDestroy(ctx->winfo_ev);
+    if (ctx->hist_ev) (void)hipEventDestroy(ctx->hist_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -4286,12 +4307,16 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     ctx->dedup_side = s1.dedup_retry == 0;
     // (launched here, ahead of the partition: 1-3% faster on the bench than launched after the merge path's kernels,
     // and ~5% faster than overlapping the merge only -- profiles/r3/r3ab12/)
+    ctx->side_dedup_in = nullptr;
     if (ctx->dedup_side) {
         HIPCHK(ctx, hipEventRecord(ctx->side_ev[0], ctx->stream));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->side_stream, ctx->side_ev[0], 0));
-        HIPCHK(ctx, hipEventRecord(ctx->side_ev[1], ctx->side_stream));
-        if ((rc = phase_dedup(ctx, &I, nullptr, I.n, false, ctx->side_stream))) return rc;
-        HIPCHK(ctx, hipEventRecord(ctx->side_ev[2], ctx->side_stream));
+#ifdef HM_DEDUP_AFTER_HIST
+        if (!table) ctx->side_dedup_in = &I;   // (launched by ev_partition, behind k_ev_hist)
+        else if ((rc = launch_side_dedup(ctx, &I))) return rc;
+#else
+        if ((rc = launch_side_dedup(ctx, &I))) return rc;
+#endif
     }
     // 3. aggregate, merge into state + emit (table mode: two LDS passes first; direct: every row a record)
     if (table) {
@@ -4306,6 +4331,10 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if (!ctx->dedup_side) {
         if ((rc = phase_dedup(ctx, &I, nullptr, I.n, true))) return rc;
     } else {
+        if (ctx->side_dedup_in) {   // (no partition ran: nothing aggregated)
+            ctx->side_dedup_in = nullptr;
+            if ((rc = launch_side_dedup(ctx, &I))) return rc;
+        }
         HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[2], 0));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
