@@ -794,8 +794,13 @@ __device__ const uint8_t g_one_byte = 1;   // (also k_ingest's row validity when
 typedef __attribute__((address_space(1))) const hm_v4u g_cv4u;
 typedef __attribute__((address_space(1))) hm_v4u g_v4u;
 __device__ __forceinline__ void st_g16(void *p, uint4 v) { *(g_v4u *)p = hm_v4u{v.x, v.y, v.z, v.w}; }   // global 16-B store
+// workgroup size of k_ev_scatter_rec (its LDS: the 8193 cursors + a 32-B record per lane)
+#ifndef HM_SR_THREADS
+#define HM_SR_THREADS 512
+#endif
+constexpr int SR_THREADS = HM_SR_THREADS;
 template <bool kPayload>
-__global__ __launch_bounds__(EV_THREADS) void k_ev_scatter_rec(const uint64_t *__restrict__ keys, int64_t n, int64_t tile,
+__global__ __launch_bounds__(SR_THREADS) void k_ev_scatter_rec(const uint64_t *__restrict__ keys, int64_t n, int64_t tile,
                                                               const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
                                                               const double *__restrict__ lat, const double *__restrict__ lon,
                                                               const uint64_t *__restrict__ payload_in,
@@ -803,9 +808,9 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_scatter_rec(const uint64_t *_
                                                               const unsigned long long *__restrict__ O, int64_t ntiles,
                                                               EventRec *__restrict__ dst) {
     __shared__ unsigned cur[RP_BINS + 1];   // the bins' cursors and the gap digit's (positions < 2^32 - 1)
-    __shared__ uint4 stage[(EV_THREADS / 64) * 64 * 2];
+    __shared__ uint4 stage[(SR_THREADS / 64) * 64 * 2];
     __shared__ WiCacheL WI;
-    for (int d = threadIdx.x; d <= nbins; d += EV_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
+    for (int d = threadIdx.x; d <= nbins; d += SR_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
     wi_load(WI, winfo);
     __syncthreads();
     const int64_t t0 = (int64_t)blockIdx.x * tile;
@@ -873,12 +878,12 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_scatter_rec(const uint64_t *_
     Row a = load(i0 + ln);
     preheader_wait();
     for (;;) {
-        const Row b = load(i0 + EV_THREADS + ln);
+        const Row b = load(i0 + SR_THREADS + ln);
         put(a);
-        if (i0 + EV_THREADS >= t1) break;
-        a = load(i0 + 2 * EV_THREADS + ln);
+        if (i0 + SR_THREADS >= t1) break;
+        a = load(i0 + 2 * SR_THREADS + ln);
         put(b);
-        i0 += 2 * EV_THREADS;
+        i0 += 2 * SR_THREADS;
         if (i0 >= t1) break;
     }
 }
@@ -2917,8 +2922,6 @@ struct hm_ctx {
     // write-pattern bound, the merge instruction-issue bound)
     hipStream_t side_stream = nullptr;
     hipEvent_t side_ev[4] = {};   // [3]: the pooled tables' tags cleared (table_release)
-    hipEvent_t hist_ev = nullptr;   // the direct path's k_ev_hist launched (the side-stream dedup starts behind it)
-    const struct Inputs *side_dedup_in = nullptr;   // the batch whose side-stream dedup ev_partition launches
     bool dedup_side = false;
     hipEvent_t h2d_ev[H2D_CHUNKS] = {};
     struct H2D { const void *src; void *dst; size_t el; };
@@ -3343,22 +3346,15 @@ static int ev_partition(hm_ctx *ctx, const uint64_t *keys, int64_t n, const Inpu
     const uint64_t ch = cell_hi_of(ctx->cfg.h3_res);
     hipLaunchKernelGGL(k_ev_hist, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, (const WInfo *)ctx->d_winfo, ch,
                        nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles);
-    if (ctx->side_dedup_in) {   // the batch's dedup, behind the histogram (both read HBM at full rate)
-        HIPCHK(ctx, hipEventRecord(ctx->hist_ev, ctx->stream));
-        HIPCHK(ctx, hipStreamWaitEvent(ctx->side_stream, ctx->hist_ev, 0));
-        const Inputs *di = ctx->side_dedup_in;
-        ctx->side_dedup_in = nullptr;
-        if ((rc = launch_side_dedup(ctx, di))) return rc;
-    }
     if ((rc = rp_scan(ctx, m))) return rc;
     if constexpr (std::is_same<Out, EventRec>::value) {
         if (nranks != 0 || dst) return set_err(ctx, HM_E_STATE, "ev_partition: EventRecs go to the context's bins");
         if (payload_in)
-            hipLaunchKernelGGL(k_ev_scatter_rec<true>, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, nullptr,
+            hipLaunchKernelGGL(k_ev_scatter_rec<true>, dim3(ntiles), dim3(SR_THREADS), 0, ctx->stream, keys, n, tile, nullptr,
                                nullptr, nullptr, nullptr, payload_in, (const WInfo *)ctx->d_winfo, ch, nbins,
                                (const unsigned long long *)ctx->rp_O.p, ntiles, (EventRec *)ctx->parts_sorted.p);
         else
-            hipLaunchKernelGGL(k_ev_scatter_rec<false>, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, I->sp, I->sv,
+            hipLaunchKernelGGL(k_ev_scatter_rec<false>, dim3(ntiles), dim3(SR_THREADS), 0, ctx->stream, keys, n, tile, I->sp, I->sv,
                                I->lat, I->lon, nullptr, (const WInfo *)ctx->d_winfo, ch, nbins,
                                (const unsigned long long *)ctx->rp_O.p, ntiles, (EventRec *)ctx->parts_sorted.p);
     } else {
@@ -4041,8 +4037,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking) != hipSuccess) { ctx->err = "stream"; return fail("create"); }
     for (auto &e : ctx->side_ev)
         if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
-    if (hipEventCreateWithFlags(&ctx->winfo_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->hist_ev, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
+    if (hipEventCreateWithFlags(&ctx->winfo_ev, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     for (auto &e : ctx->h2d_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     // k_merge_owned's resident tags live in dynamic LDS of up to MO_TAG_MAX bytes (merge_sorted)
@@ -4205,7 +4200,6 @@ void hm_destroy(hm_ctx *ctx) {
     for (auto &e : ctx->side_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->winfo_ev) (void)hipEventDestroy(ctx->winfo_ev);
-    if (ctx->hist_ev) (void)hipEventDestroy(ctx->hist_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -4250,7 +4244,7 @@ static void exp_overlap(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
                            ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st);
     };
     auto scatter = [&](hipStream_t st) {
-        hipLaunchKernelGGL(k_ev_scatter_rec<false>, dim3(ntiles), dim3(EV_THREADS), 0, st, (const uint64_t *)ctx->keys.p, n, tile,
+        hipLaunchKernelGGL(k_ev_scatter_rec<false>, dim3(ntiles), dim3(SR_THREADS), 0, st, (const uint64_t *)ctx->keys.p, n, tile,
                            I.sp, I.sv, I.lat, I.lon, nullptr, (const WInfo *)ctx->d_winfo, cell_hi_of(ctx->cfg.h3_res), RP_BINS,
                            (const unsigned long long *)ctx->rp_O.p, ntiles, (EventRec *)ctx->parts_sorted.p);
     };
@@ -4306,17 +4300,11 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     // full table, after the fused one gave up, prepares that table on the main stream: it stays there)
     ctx->dedup_side = s1.dedup_retry == 0;
     // (launched here, ahead of the partition: 1-3% faster on the bench than launched after the merge path's kernels,
-    // and ~5% faster than overlapping the merge only -- profiles/r3/r3ab12/)
-    ctx->side_dedup_in = nullptr;
+    // ~5% faster than overlapping the merge only, 2-4% faster than behind k_ev_hist -- profiles/r3/r3ab12/, r3ab13/)
     if (ctx->dedup_side) {
         HIPCHK(ctx, hipEventRecord(ctx->side_ev[0], ctx->stream));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->side_stream, ctx->side_ev[0], 0));
-#ifdef HM_DEDUP_AFTER_HIST
-        if (!table) ctx->side_dedup_in = &I;   // (launched by ev_partition, behind k_ev_hist)
-        else if ((rc = launch_side_dedup(ctx, &I))) return rc;
-#else
         if ((rc = launch_side_dedup(ctx, &I))) return rc;
-#endif
     }
     // 3. aggregate, merge into state + emit (table mode: two LDS passes first; direct: every row a record)
     if (table) {
@@ -4331,10 +4319,6 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if (!ctx->dedup_side) {
         if ((rc = phase_dedup(ctx, &I, nullptr, I.n, true))) return rc;
     } else {
-        if (ctx->side_dedup_in) {   // (no partition ran: nothing aggregated)
-            ctx->side_dedup_in = nullptr;
-            if ((rc = launch_side_dedup(ctx, &I))) return rc;
-        }
         HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[2], 0));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
