@@ -3051,7 +3051,8 @@ static std::string g_create_err;
 // 255: result count of the last ordered compaction
 constexpr int DUSED_WORD = 253;
 constexpr int FULL_USED_WORD = 240;   // used-slot count of the full dedup table
-constexpr int SLOW_WORD = 252;   // number of k_ingest fast-path exceptions of the current batch
+constexpr int SLOW_WORD = 252;
+constexpr size_t REG_BLOCK_BYTES = 2 * (WREG_SLOTS + 1) * 8 + sizeof(DevStats);   // d_wreg | d_wcount | d_st (hm_create)   // number of k_ingest fast-path exceptions of the current batch
 constexpr int REGROW_WORD = 251; // records dumped by k_dump_gen
 constexpr int GIVEUP_WORD = 232;
 constexpr int GAPS_WORD = 242;   // 242-243: totals of the gap / donor scans
@@ -3727,8 +3728,7 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
     // the batch statistics and the registry with its census, read back together
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_wreg, ctx->d_wreg, 2 * (WREG_SLOTS + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));   // (+ h_wcount)
+    HIPCHK(ctx, hipMemcpyAsync(ctx->h_wreg, ctx->d_wreg, REG_BLOCK_BYTES, hipMemcpyDeviceToHost, ctx->stream));   // (+ h_wcount, h_st)
     HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     if (ctx->h_st->win_overflow)
         return set_err(ctx, HM_E_OVERFLOW, "more than %d distinct windows in one micro-batch (%llu rows)", WREG_SLOTS,
@@ -3857,10 +3857,13 @@ static int rows_densify(hm_ctx *ctx, int64_t ntiles) {
     return HM_OK;
 }
 
-static int merge_begin(hm_ctx *ctx, int64_t n_rows) {
+// counters_zero: the merge's counters are still as k_batch_reset left them (the direct path, right after phase_local)
+static int merge_begin(hm_ctx *ctx, int64_t n_rows, bool counters_zero = false) {
     static_assert(offsetof(DevStats, n_state_new) == offsetof(DevStats, n_touched) + 8, "DevStats");
-    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_touched, 0, 16, ctx->stream));   // (+ n_state_new)
-    HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
+    if (!counters_zero) {
+        HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->n_touched, 0, 16, ctx->stream));   // (+ n_state_new)
+        HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));
+    }
     ctx->seq++;
     ctx->batch_windows.clear();
     return ensure_outputs(ctx, n_rows);
@@ -3894,7 +3897,8 @@ static int merge_partials(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts
 static int merge_events(hm_ctx *ctx, const Inputs &I, int64_t n_rec) {
     int rc;
     ctx->n_partials_merged = n_rec;
-    if ((rc = merge_begin(ctx, I.n))) return rc;
+    if ((rc = merge_begin(ctx, I.n, true))) return rc;   // (only k_ingest, k_sample_heavy and the side stream's
+                                                          // k_dedup_flag ran since k_batch_reset: none counts these)
     if (n_rec == 0) return merge_nothing(ctx);
     std::vector<WinCount> census;
     census_of_registry(ctx, census);
@@ -4074,10 +4078,11 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     // MOBHEAT_INGEST_MODE=direct|table pins the aggregation path (tests); default: adaptive
     if (const char *m = getenv("MOBHEAT_INGEST_MODE")) ctx->ingest_mode = !strcmp(m, "direct") ? 1 : !strcmp(m, "table") ? 2 : 0;
     if (const char *m = getenv("MOBHEAT_MERGE_GRID")) ctx->merge_grid = std::max(0, atoi(m));
-    // the registry and its census side by side (one reset, one readback per batch)
-    if (hipMalloc(&ctx->d_wreg, 2 * (WREG_SLOTS + 1) * 8) != hipSuccess || !(ctx->d_wcount = ctx->d_wreg + WREG_SLOTS + 1) ||
-        hipHostMalloc(&ctx->h_wreg, 2 * (WREG_SLOTS + 1) * 8, hipHostMallocDefault) != hipSuccess ||
-        !(ctx->h_wcount = ctx->h_wreg + WREG_SLOTS + 1) ||
+    // the registry, its census and the batch statistics side by side (one reset, one readback after k_ingest)
+    if (hipMalloc(&ctx->d_wreg, REG_BLOCK_BYTES) != hipSuccess || !(ctx->d_wcount = ctx->d_wreg + WREG_SLOTS + 1) ||
+        !(ctx->d_st = (DevStats *)(ctx->d_wreg + 2 * (WREG_SLOTS + 1))) ||
+        hipHostMalloc(&ctx->h_wreg, REG_BLOCK_BYTES, hipHostMallocDefault) != hipSuccess ||
+        !(ctx->h_wcount = ctx->h_wreg + WREG_SLOTS + 1) || !(ctx->h_st = (DevStats *)(ctx->h_wreg + 2 * (WREG_SLOTS + 1))) ||
         hipMalloc(&ctx->d_winfo, (WREG_SLOTS + 1) * sizeof(WInfo) + sizeof(WiCacheImg)) != hipSuccess ||
         hipHostMalloc(&ctx->h_winfo, (WREG_SLOTS + 1) * sizeof(WInfo) + sizeof(WiCacheImg), hipHostMallocDefault) != hipSuccess ||
         hipMemset(ctx->d_winfo, 0, (WREG_SLOTS + 1) * sizeof(WInfo)) != hipSuccess ||
@@ -4085,8 +4090,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         ctx->err = "window registry alloc";
         return fail("create");
     }
-    if (hipMalloc(&ctx->d_st, sizeof(DevStats)) != hipSuccess || hipHostMalloc(&ctx->h_st, sizeof(DevStats)) != hipSuccess ||
-        hipMalloc(&ctx->d_scratch, 256 * 8) != hipSuccess || hipHostMalloc(&ctx->h_scratch, 256 * 8) != hipSuccess) {
+    if (hipMalloc(&ctx->d_scratch, 256 * 8) != hipSuccess || hipHostMalloc(&ctx->h_scratch, 256 * 8) != hipSuccess) {
         ctx->err = "stats alloc";
         return fail("create");
     }
@@ -4171,7 +4175,7 @@ void hm_destroy(hm_ctx *ctx) {
     for (auto &pt : ctx->pool)
         if (!in_arena(ctx, pt.first)) (void)hipFree(pt.first);
     if (ctx->arena) (void)hipFree(ctx->arena);
-    if (ctx->d_wreg) (void)hipFree(ctx->d_wreg);   // (d_wcount / h_wcount: inside these)
+    if (ctx->d_wreg) (void)hipFree(ctx->d_wreg);   // (d_wcount, d_st / h_wcount, h_st: inside these)
     if (ctx->h_wreg) (void)hipHostFree(ctx->h_wreg);
     if (ctx->d_winfo) (void)hipFree(ctx->d_winfo);
     if (ctx->h_winfo) (void)hipHostFree(ctx->h_winfo);
@@ -4187,8 +4191,6 @@ void hm_destroy(hm_ctx *ctx) {
                      ctx->h_td_bytes, ctx->h_td_off};
     for (void *p : hbufs)
         if (p) (void)hipHostFree(p);
-    if (ctx->d_st) (void)hipFree(ctx->d_st);
-    if (ctx->h_st) (void)hipHostFree(ctx->h_st);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->h_scratch) (void)hipHostFree(ctx->h_scratch);
     for (auto &e : ctx->ev)

@@ -16,5 +16,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc_write -o r
 python3 tools/ingest_pmc.py --res 8 --events 100000000 --out $O/kernel_pmc.json $O/pmc_f64 $O/pmc_sq $O/pmc_fetch $O/pmc_write > $O/ingest_pmc.log 2>&1 && \
 mkdir -p profiles/r3 && cp $O/kernel_pmc.json profiles/r3/kernel_pmc.json && \
 timeout -k 10 600 python3 bench.py > $O/bench.log 2>&1 && \
-timeout -k 10 120 ./tools/microbench/scatter_bw > $O/scatter_bw.log 2>&1
+timeout -k 10 120 ./tools/microbench/scatter_bw > $O/scatter_bw.log 2>&1 && \
+MOBHEAT_DIST_BACKEND=gloo timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+  bench.py --gpus 2 --steps 4 --warmup 2 --events 20000000 > $O/bench_n2.log 2>&1 && \
+timeout -k 10 120 python3 bench.py --gpus 1 --steps 4 --warmup 2 --events 20000000 --no-cpu-baseline --no-state-leg > $O/bench_n1_small.log 2>&1
 rc=$?; echo "done rc=$rc"; exit $rc
