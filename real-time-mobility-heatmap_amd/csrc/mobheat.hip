@@ -2093,12 +2093,18 @@ __global__ __launch_bounds__(256) void k_fill_gaps(RowsOut r, const unsigned lon
         const unsigned ng = g[b];
         if (!ng) continue;
         const unsigned long long dst0 = O[(int64_t)b * ntiles] + cnt[b], g0 = goff[b];
+        int lo = -1;   // the donor bin: the last bin with voff <= i
         for (unsigned k = threadIdx.x; k < ng; k += blockDim.x) {
             const unsigned long long i = g0 + k;
-            int lo = 0, hi = nbins;   // last bin with voff <= i
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (voff[mid] <= i) lo = mid; else hi = mid;
+            if (lo < 0) {   // a thread's first row: binary search (13 dependent loads)
+                lo = 0;
+                int hi = nbins;
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (voff[mid] <= i) lo = mid; else hi = mid;
+                }
+            } else {        // i grows by blockDim.x per row: the donor bin moves forward a few bins at most
+                while (lo + 1 < nbins && voff[lo + 1] <= i) lo++;
             }
             const unsigned long long sb = O[(int64_t)lo * ntiles];
             const int64_t src = (int64_t)((sb > T ? sb : T) + (i - voff[lo])), dst = (int64_t)(dst0 + k);
