@@ -43,12 +43,13 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9
 # records merged (direct path: one per aggregated row), T tiles emitted, E of them keys that existed before the batch
 # (their 64-B state line is read); multi-GPU (stage API): S records this rank sent, R the records it merged as owner.
 #   direct path   ingest 42/event (lat, lon, ts, vkey 8 each + row_valid 1 read; flags 1 + event key 8 written)
-#                 partition 16/event (k_ev_hist and k_ev_scatter read the key) + 65/record (speed, speed_valid,
-#                           lat, lon read: 33; the 32-B EventRec written)
+#                 partition 16/event (k_ev_hist and k_ev_scatter read the key) + 57/record (speed, speed_valid,
+#                           lat, lon read: 25; the 32-B EventRec written)
 #                 merge 32/record read + 113/tile (64-B state line + 49-B row written) + 64/pre-existing key read
 #                 emit 98/gap (a 49-B row moved into a gap; gaps = R - T), dedup 20/event
-#   multi-GPU     send (the sender's partition by owner) 16/event + 65/sent record (8-B key + 24-B payload written)
-#                 partition (the owner's) 88/received record: census 8 + histogram 8 read, key 8 + payload 24 read,
+#   multi-GPU     send (the sender's partition by owner) 16/event + 57/sent record (speed, speed_valid, lat, lon
+#                           read: 25; 8-B key + 24-B payload written)
+#                 partition (the owner's) 80/received record: census 8 + histogram 8 read, key 8 + payload 24 read,
 #                           the 32-B EventRec written
 #   table mode    aggregate 41/event + 48/record, partition 160/record (48 + 48 read, 64 written), merge 64/record
 #                 read + 113/tile + 64/pre-existing key
@@ -59,9 +60,9 @@ def stage_bytes(n, c, world=1):
     if c["table_mode"]:
         b.update(aggregate=41 * n + 48 * R, partition=160 * R, merge=64 * R + 113 * T + 64 * E)
     elif world > 1:
-        b.update(aggregate=0, send=16 * n + 65 * c["sent"], partition=88 * R, merge=32 * R + 113 * T + 64 * E)
+        b.update(aggregate=0, send=16 * n + 57 * c["sent"], partition=80 * R, merge=32 * R + 113 * T + 64 * E)
     else:
-        b.update(aggregate=0, partition=16 * n + 65 * R, merge=32 * R + 113 * T + 64 * E)
+        b.update(aggregate=0, partition=16 * n + 57 * R, merge=32 * R + 113 * T + 64 * E)
     return b
 
 
@@ -78,6 +79,12 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r3", "kernel_pmc.json")
 STAGE_KERNELS = {"ingest": ["k_ingest"], "aggregate": ["k_agg", "k_bin_reduce"], "send": ["k_ev_hist", "k_ev_scatter"],
                  "partition": ["k_ev_hist", "k_ev_scatter_rec"], "merge": ["k_merge_owned"], "emit": ["k_fill_gaps"],
                  "dedup": ["k_dedup_flag"]}
+
+
+def dominant_stage(avg_ms):
+    """The stage the roofline prices: the longest of the serial stages on the main stream (the dedup runs on a side
+    stream, concurrently with the partition and merge: its time is a span shared with them, not a stage of the step)."""
+    return max((k for k in STAGES if k not in CONCURRENT_STAGES), key=lambda k: avg_ms[k])
 
 
 def ingest_pmc(res, n, world):
@@ -241,9 +248,7 @@ def main():
     ms_step = elapsed / K * 1e3
     # Roofline of the dominant stage by time, priced on HBM (the metric's "% HBM peak"), with the PMC-counted
     # traffic of its kernels when the PMC file was taken on this exact workload (tools/ingest_pmc.py).
-    # (the dedup runs on a side stream, concurrently with the partition and merge: its time is a span shared with
-    # them, not a stage of the step -- so it is not a candidate)
-    dom = max((k for k in STAGES if k not in CONCURRENT_STAGES), key=lambda k: avg_ms[k])
+    dom = dominant_stage(avg_ms)
     gbs = kb[dom] / (avg_ms[dom] * 1e-3) / 1e9 if avg_ms[dom] > 0 else 0.0
     roof = {"bound": "hbm", "kernel": dom, "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": gbs / HBM_PEAK_GBS, "traffic": None}
