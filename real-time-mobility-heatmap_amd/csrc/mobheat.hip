@@ -794,6 +794,11 @@ __device__ const uint8_t g_one_byte = 1;   // (also k_ingest's row validity when
 typedef __attribute__((address_space(1))) const hm_v4u g_cv4u;
 typedef __attribute__((address_space(1))) hm_v4u g_v4u;
 __device__ __forceinline__ void st_g16(void *p, uint4 v) { *(g_v4u *)p = hm_v4u{v.x, v.y, v.z, v.w}; }   // global 16-B store
+// k_ev_scatter_rec's record stores (HM_NT_STORES bit 3: non-temporal, A/B builds)
+__device__ __forceinline__ void st_g16_rec(void *p, uint4 v) {
+    if constexpr ((HM_NT_STORES & 8) != 0) __builtin_nontemporal_store(hm_v4u{v.x, v.y, v.z, v.w}, (g_v4u *)p);
+    else st_g16(p, v);
+}
 // workgroup size of k_ev_scatter_rec (its LDS: the 8193 cursors + a 32-B record per lane)
 #ifndef HM_SR_THREADS
 #define HM_SR_THREADS 512
@@ -869,7 +874,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_ev_scatter_rec(const uint64_t *_
         for (int q = 0; q < 2; q++) {
             const int idx = q * 64 + ln, rec = idx >> 1, part = idx & 1;
             const unsigned p = __shfl(pos, rec, 64);
-            st_g16(&d4[(int64_t)p * 2 + part], ws[idx]);
+            st_g16_rec(&d4[(int64_t)p * 2 + part], ws[idx]);
         }
         __builtin_amdgcn_wave_barrier();
     };
