@@ -133,6 +133,17 @@ def test_iso_ts_strings_parse_like_to_timestamp():
     assert c["row_valid"].tolist() == [True, False]
 
 
+def test_iso_ts_date_only_and_mixed_zones():
+    """A date-only string is midnight (UTC session), not a string with a '-15'-style zone; naive, Z and +hh:mm
+    strings in one frame each parse on their own (the zone test only after a time component)."""
+    df = pd.DataFrame({"provider": ["p"] * 4, "vehicleId": ["v", "w", "x", "y"], "lat": [1.0] * 4, "lon": [1.0] * 4,
+                       "speedKmh": [1.0] * 4,
+                       "ts": ["2025-09-26T12:45:10Z", "2025-09-26", "2025-09-26T12:45:10+02:00", "2025-09-26T12:45:10"]})
+    c = stream.batch_columns(df)
+    assert c["ts_us"].tolist() == [1758890710_000_000, 1758844800_000_000, 1758883510_000_000, 1758890710_000_000]
+    assert c["row_valid"].tolist() == [True] * 4
+
+
 def test_state_checkpoint_files_and_resume_choice(tmp_path, monkeypatch):
     """CPU: the state checkpoint's file format round-trips (plain arrays, no pickles) and a restarted engine
     resumes from the state after the newest checkpointed epoch OLDER than the incoming one (Spark re-runs the first
