@@ -18,6 +18,11 @@
 // NaN, which no caller produces.
 // The whole file must be compiled with -ffp-contract=off (the Makefile does): the non-fma expressions are separate
 // roundings, as in glibc's code.
+//
+// License: the routines below are a restatement (a derived work) of the GNU C Library's dbl-64 sources (s_sin.c,
+// s_sincos.c, e_asin.c, e_atan2.c, s_tan.c, s_atan.c and their tables: IBM Accurate Mathematical Library, Copyright
+// (C) 2001-2022 Free Software Foundation, Inc.), which are licensed under the GNU Lesser General Public License 2.1 or
+// later.  This file and glibc_libm.inc are distributed under the same license; see NOTICE at the repository root.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

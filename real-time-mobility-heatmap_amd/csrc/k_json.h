@@ -1,0 +1,169 @@
+// Kafka values -> batch columns (from_json + to_timestamp, heatmap_stream.py:88-93) and the string dictionaries.
+// Part of the single translation unit mobheat.hip (included there in dependency order; not compiled alone).
+#pragma once
+
+// =====================================================================================================
+// K0: Kafka values -> batch columns (row f1: from_json + to_timestamp, heatmap_stream.py:88-93; json_decode.h),
+// one thread per record; then the exact string dictionaries of provider and vehicleId (hash table keyed by a
+// 64-bit string hash, every row verified byte for byte against its slot's representative; a hash collision
+// reruns the dictionary with another seed) and vkey = provider_code * n_vehicles + vehicle_code.
+// =====================================================================================================
+constexpr int64_t SPAN_SCRATCH = INT64_C(1) << 62;   // span offset flag: the decoded bytes are in the scratch buffer
+__global__ __launch_bounds__(256) void k_json_parse(const uint8_t *__restrict__ bytes, const int64_t *__restrict__ offs,
+                                                    int64_t base, int64_t n, uint8_t *__restrict__ scratch,
+                                                    double *__restrict__ lat, double *__restrict__ lon,
+                                                    int64_t *__restrict__ ts, double *__restrict__ speed,
+                                                    uint8_t *__restrict__ sv, uint8_t *__restrict__ rv,
+                                                    int64_t *__restrict__ p_off, int32_t *__restrict__ p_len,
+                                                    int64_t *__restrict__ v_off, int32_t *__restrict__ v_len,
+                                                    unsigned long long *counts) {
+    unsigned long long bad = 0, unsup = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        JsonRow r;
+        parse_record(bytes, offs[i] - base, offs[i + 1] - base, scratch, r);
+        const uint32_t f = r.flags;
+        bad += (f & JF_MALFORMED) != 0;
+        unsup += (f & JF_UNSUPPORTED) != 0;
+        lat[i] = (f & JF_LAT) ? r.lat : __builtin_nan("");
+        lon[i] = (f & JF_LON) ? r.lon : __builtin_nan("");
+        ts[i] = (f & JF_TS) ? r.ts_us : 0;
+        speed[i] = (f & JF_SPEED) ? r.speed : 0.0;
+        sv[i] = (f & JF_SPEED) ? 1 : 0;
+        rv[i] = (f & JF_PROV) && (f & JF_VEH) && (f & JF_TS) ? 1 : 0;
+        p_off[i] = r.p_off | ((f & JF_PROV_ESC) ? SPAN_SCRATCH : 0);
+        p_len[i] = (f & JF_PROV) ? r.p_len : -1;
+        v_off[i] = r.v_off | ((f & JF_VEH_ESC) ? SPAN_SCRATCH : 0);
+        v_len[i] = (f & JF_VEH) ? r.v_len : -1;
+    }
+    bad = wave_sum(bad);
+    unsup = wave_sum(unsup);
+    if (lane_id() == 0) {
+        if (bad) atomicAdd(&counts[0], bad);
+        if (unsup) atomicAdd(&counts[1], unsup);
+    }
+}
+
+__device__ __forceinline__ const uint8_t *span_ptr(const uint8_t *bytes, const uint8_t *scratch, int64_t off) {
+    return (off & SPAN_SCRATCH) ? scratch + (off & ~SPAN_SCRATCH) : bytes + off;
+}
+__device__ __forceinline__ uint64_t str_hash(const uint8_t *s, int n, uint64_t seed) {
+    uint64_t h = mix64(seed ^ ((uint64_t)n * UINT64_C(0x9e3779b97f4a7c15)));
+    for (int k = 0; k < n; k += 8) {
+        uint64_t x = 0;
+        for (int q = 0; q < 8 && k + q < n; q++) x |= (uint64_t)s[k + q] << (8 * q);
+        h = mix64(h ^ x) + UINT64_C(0x632be59bd9b4e019);
+    }
+    return h & ~(UINT64_C(1) << 63);   // (never DICT_EMPTY)
+}
+struct DictSlot {   // cleared to all-ones bytes
+    unsigned long long key;   // str_hash, < 2^63; ~0 = empty
+    unsigned rep;             // the smallest row holding the string
+    unsigned pad;
+};
+constexpr unsigned long long DICT_EMPTY = ~0ull;
+constexpr int DICT_PROBES = 64;
+__global__ __launch_bounds__(256) void k_dict_insert(const uint8_t *__restrict__ bytes, const uint8_t *__restrict__ scratch,
+                                                     const int64_t *__restrict__ off, const int32_t *__restrict__ len,
+                                                     int64_t n, DictSlot *tab, unsigned long long mask, uint64_t seed,
+                                                     unsigned *__restrict__ slot_of, unsigned long long *overflow) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int32_t L = len[i];
+        if (L < 0) { slot_of[i] = ~0u; continue; }
+        const uint64_t h = str_hash(span_ptr(bytes, scratch, off[i]), L, seed);
+        unsigned long long s = mix64(h ^ seed) & mask;
+        unsigned got = ~0u;
+        for (int p = 0; p < DICT_PROBES; p++) {
+            unsigned long long k = __hip_atomic_load(&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k == DICT_EMPTY) k = atomicCAS(&tab[s].key, DICT_EMPTY, (unsigned long long)h);
+            if (k == DICT_EMPTY || k == h) {
+                atomicMin(&tab[s].rep, (unsigned)i);
+                got = (unsigned)s;
+                break;
+            }
+            s = (s + 1) & mask;
+        }
+        slot_of[i] = got;
+        if (got == ~0u) atomicAdd(overflow, 1ull);
+    }
+}
+// every row's bytes against its slot's representative: a mismatch is a 64-bit hash collision
+__global__ __launch_bounds__(256) void k_dict_verify(const uint8_t *__restrict__ bytes, const uint8_t *__restrict__ scratch,
+                                                     const int64_t *__restrict__ off, const int32_t *__restrict__ len,
+                                                     int64_t n, const DictSlot *__restrict__ tab,
+                                                     const unsigned *__restrict__ slot_of, unsigned long long *collide) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const unsigned s = slot_of[i];
+        if (s == ~0u) continue;
+        const unsigned r = tab[s].rep;
+        if (r == (unsigned)i) continue;
+        bool eq = len[r] == len[i];
+        if (eq) {
+            const uint8_t *a = span_ptr(bytes, scratch, off[i]), *b = span_ptr(bytes, scratch, off[r]);
+            for (int k = 0; k < len[i] && eq; k++) eq = a[k] == b[k];
+        }
+        if (!eq) atomicAdd(collide, 1ull);
+    }
+}
+__global__ __launch_bounds__(256) void k_dict_occ(const DictSlot *__restrict__ tab, int64_t cap, uint8_t *__restrict__ occ) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += stride) occ[s] = tab[s].key != DICT_EMPTY;
+}
+// code c = the c-th occupied slot (ascending): code_of_slot, and the code's string length
+__global__ __launch_bounds__(256) void k_dict_codes(const int64_t *__restrict__ slots, const unsigned long long *n_codes,
+                                                    const DictSlot *__restrict__ tab, const int32_t *__restrict__ len,
+                                                    unsigned *__restrict__ code_of_slot, unsigned *__restrict__ clen) {
+    const int64_t m = (int64_t)*n_codes;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < m; c += stride) {
+        const int64_t s = slots[c];
+        code_of_slot[s] = (unsigned)c;
+        clen[c] = (unsigned)len[tab[s].rep];
+    }
+}
+__global__ __launch_bounds__(256) void k_dict_gather(const uint8_t *__restrict__ bytes, const uint8_t *__restrict__ scratch,
+                                                     const int64_t *__restrict__ off, const int32_t *__restrict__ len,
+                                                     const int64_t *__restrict__ slots, const unsigned long long *n_codes,
+                                                     const DictSlot *__restrict__ tab, const unsigned long long *__restrict__ coff,
+                                                     uint8_t *__restrict__ out) {
+    const int64_t m = (int64_t)*n_codes;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < m; c += stride) {
+        const unsigned r = tab[slots[c]].rep;
+        const uint8_t *a = span_ptr(bytes, scratch, off[r]);
+        for (int k = 0; k < len[r]; k++) out[coff[c] + k] = a[k];
+    }
+}
+__global__ __launch_bounds__(256) void k_json_vkey(const uint8_t *__restrict__ rv, const unsigned *__restrict__ pslot,
+                                                   const unsigned *__restrict__ vslot, const unsigned *__restrict__ pcode,
+                                                   const unsigned *__restrict__ vcode, int64_t n, uint64_t n_vehicles,
+                                                   uint64_t *__restrict__ vkey) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        vkey[i] = rv[i] ? (uint64_t)pcode[pslot[i]] * n_vehicles + vcode[vslot[i]] : 0;
+}
+// the distinct 900-s buckets of the latest rows' eventTs (a set of int64, EMPTY = INT64_MIN), compacted into list
+__global__ __launch_bounds__(256) void k_latest_buckets(const int64_t *__restrict__ rows, int64_t m,
+                                                        const int64_t *__restrict__ ts, long long *set, unsigned long long mask,
+                                                        long long *list, unsigned long long *n_list) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += stride) {
+        const long long b = (long long)floordiv(floordiv(ts[rows[q]], 1000000), 900);
+        unsigned long long s = mix64((uint64_t)b) & mask;
+        for (unsigned long long p = 0; p <= mask; p++) {
+            long long k = __hip_atomic_load(&set[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k == INT64_MIN) {
+                k = atomicCAS((unsigned long long *)&set[s], (unsigned long long)INT64_MIN, (unsigned long long)b);
+                if (k == INT64_MIN) { list[atomicAdd(n_list, 1ull)] = b; break; }
+            }
+            if (k == b) break;
+            s = (s + 1) & mask;
+        }
+    }
+}
+__global__ __launch_bounds__(256) void k_fill_i64(long long *p, int64_t n, long long v) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}

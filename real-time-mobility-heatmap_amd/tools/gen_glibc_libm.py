@@ -111,7 +111,10 @@ def main():
              f" * sha256 {hashlib.sha256(b).hexdigest()}.",
              " * Constants and tables of sincos (generic dbl-64), __ieee754_acos_fma, __ieee754_atan2_fma and __tan_fma;",
              " * csrc/glibc_libm.h restates the routines.  Names follow glibc's sources (usncs.h, e_asin.c, e_atan2.c,",
-             " * s_tan.c, root.tbl); a trailing N marks a constant the machine code subtracts (its negation). */"]
+             " * s_tan.c, root.tbl); a trailing N marks a constant the machine code subtracts (its negation).",
+             " * The values are data of the GNU C Library (sysdeps/ieee754/dbl-64, IBM Accurate Mathematical Library),",
+             " * Copyright (C) 2001-2022 Free Software Foundation, Inc., licensed under the GNU Lesser General Public",
+             " * License 2.1 or later; see NOTICE at the repository root. */"]
     for n, a in SCALARS:
         lines.append(f"#define GLM_{n} {dbl(b, a).hex()}  /* libm+0x{a:x} */")
     lines.append("#define GLM_TABLE_INIT \\")
