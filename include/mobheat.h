@@ -156,7 +156,11 @@ int64_t hm_latlng_to_cell_last_exact(int32_t device);
  * 4. hm_stage_merge: the owner merges the received tile records into the persistent state it owns, emits the
  *    tiles it owns, reduces the received candidates to winners, and writes the winners' row indices grouped by
  *    origin rank into winner_send_buf (capacity >= n_cand_recv) with per-origin counts.
- * 5. caller: exchange winners back; hm_stage_finish takes the received winners (rows of this rank). */
+ * 5. caller: exchange winners back; hm_stage_finish takes the received winners (rows of this rank).
+ * After hm_stage_merge the owner's tiles can be encoded (hm_last_windows, hm_encode_tile_updates); after hm_stage_finish
+ * the rank's latest rows can (hm_last_latest_buckets, hm_encode_position_updates, with the batch's dictionaries): every
+ * rank writes the statements of what it owns, so no statement crosses the exchange.  A device caller keeps its input
+ * buffers until then. */
 #define HM_STAGE_SUMMARY_WORDS 8200
 #define HM_TILE_REC_BYTES 48
 #define HM_TILE_KEY_BYTES 8
@@ -272,8 +276,8 @@ int hm_encode_tile_updates(hm_ctx *ctx, const hm_tile_doc_cfg *cfg, int32_t out_
  * from the batch's dictionaries (the vkey the caller passed = provider_code * n_vehicles + vehicle_code; string k
  * of a dictionary = bytes[offsets[k], offsets[k+1]), UTF-8); ts is the naive local datetime of eventTs, with the
  * local UTC offset of the row's 900-s bucket floor(ts_s / 900): bucket_offset_s[k] for bucket_ids[k] (the distinct
- * buckets of the latest rows, strictly ascending; a row whose bucket is absent fails the call). Not after stage
- * calls (HM_E_STATE). Outputs as hm_encode_tile_updates. */
+ * buckets of the latest rows, strictly ascending; a row whose bucket is absent fails the call). After the stage API:
+ * this rank's latest rows (hm_stage_finish). Outputs as hm_encode_tile_updates. */
 typedef struct hm_position_doc_cfg {
     int64_t n_providers;
     const int64_t *provider_offsets;   /* n_providers + 1 */

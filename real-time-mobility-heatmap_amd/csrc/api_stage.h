@@ -13,14 +13,14 @@ static_assert(SW_WIN0 + 2 * WREG_SLOTS <= HM_STAGE_SUMMARY_WORDS, "summary layou
 int hm_stage_ingest(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t nranks, int32_t rank, int64_t *summary) {
     if (!ctx || !in || !summary || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks)
         return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
-    if (in->n > (int64_t)UINT32_MAX - 1) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds 2^32-2", (long long)in->n);
+    if (in->n > MAX_BATCH_ROWS) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds %lld", (long long)in->n, (long long)MAX_BATCH_ROWS);
     if (in->n > 0 && (!in->lat || !in->lon || !in->ts_us || !in->vkey))
         return set_err(ctx, HM_E_INVALID, "lat, lon, ts_us and vkey are required");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc;
     ctx->stage = 0;
     ctx->epoch = epoch_id;
-    ctx->last_n_latest = -1;   // (hm_encode_position_updates: single-context batches only)
+    ctx->last_n_latest = -1;   // (set again by hm_stage_finish: this rank's latest rows)
     ctx->nranks = nranks;
     ctx->rank = rank;
     const int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
@@ -205,6 +205,7 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *tile_send_buf, vo
 // window -> window tables -> (window, region) partition into EventRecs -> merge -> rows
 static int merge_received_events(hm_ctx *ctx, const uint64_t *keys, const uint64_t *payload, int64_t n) {
     int rc;
+    if (n > MAX_BATCH_ROWS) return set_err(ctx, HM_E_INVALID, "%lld received records exceed %lld", (long long)n, (long long)MAX_BATCH_ROWS);
     ctx->n_partials_merged = n;
     if ((rc = merge_begin(ctx, n))) return rc;
     if (n == 0) return merge_nothing(ctx);
@@ -301,8 +302,19 @@ int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_r
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc;
     out->n_latest = n_winner_recv;
+    // the rank's latest rows into the context (library-owned like hm_process_batch's), so that the positions sink
+    // (hm_encode_position_updates, hm_last_latest_buckets) encodes this rank's winners from its own columns: the
+    // origin rank writes the positions_latest statements of the rows it holds (heatmap_stream.py:209-235)
+    if ((rc = ensure(ctx, ctx->rows, std::max<int64_t>(n_winner_recv, 1) * 8))) return rc;
+    if (n_winner_recv > 0)
+        HIPCHK(ctx, hipMemcpyAsync(ctx->rows.p, winner_recv_dev, n_winner_recv * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    ctx->last_n_latest = n_winner_recv;
+    ctx->last_vk = ctx->stage_I.vk;
+    ctx->last_ts = ctx->stage_I.ts;
+    ctx->last_lat = ctx->stage_I.lat;
+    ctx->last_lon = ctx->stage_I.lon;
     if (out_memory == HM_MEM_DEVICE) {
-        out->latest_row = (const int64_t *)winner_recv_dev;
+        out->latest_row = (const int64_t *)ctx->rows.p;
     } else {
         if ((size_t)n_winner_recv > ctx->h_rows_cap || !ctx->h_rows) {
             size_t want = host_cap_for(ctx->h_rows ? ctx->h_rows_cap : 0, (size_t)n_winner_recv), dummy = 0;

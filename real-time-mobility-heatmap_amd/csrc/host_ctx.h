@@ -132,7 +132,8 @@ struct hm_ctx {
     int64_t epoch = -1;
     // tile update statements (hm_encode_tile_updates): the last batch's emitted tiles and their windows
     int64_t last_n_tiles = 0;
-    int64_t last_n_latest = -1;   // the last hm_process_batch's latest rows (ctx->rows) and its input columns
+    int64_t last_n_latest = -1;   // the last batch's latest rows (ctx->rows) and its input columns (hm_process_batch,
+                                  // or hm_stage_finish: the rank's own rows)
     const uint64_t *last_vk = nullptr;
     const int64_t *last_ts = nullptr;
     const double *last_lat = nullptr, *last_lon = nullptr;
@@ -147,7 +148,8 @@ struct hm_ctx {
     int64_t stage_n_in = 0;
     int64_t stage_agg_rows = 0;
     hm_stage_sizes stage_sizes{};
-    Inputs stage_I{};                                  // the batch's device columns (valid until hm_stage_send)
+    Inputs stage_I{};                                  // the batch's device columns (the caller's device buffers
+                                                       // or the context's copies: valid until the next batch)
     DevStats stage_s1{};                               // this rank's ingest statistics
     bool stage_table = false;                          // the batch's aggregation path (the same on every rank)
     int64_t stage_gmax_ms = INT64_MIN;                 // the batch's max event time over all ranks
@@ -157,6 +159,9 @@ struct hm_ctx {
 };
 
 static std::string g_create_err;
+// rows of one batch (and records of one stage merge): positions are 32-bit, and k_ev_scatter_rec's lanes past a tile
+// store to the 64 slack records after the n-th (a bound of 2^32 - 2 let those slack positions wrap)
+constexpr int64_t MAX_BATCH_ROWS = (int64_t)UINT32_MAX - 66;
 // d_scratch word layout: [0,64) tile partition counts/cursors, [64,128) candidate counts/cursors,
 // DUSED_WORD: used-slot count of the persistent dedup table (survives until the table is cleared),
 // 255: result count of the last ordered compaction

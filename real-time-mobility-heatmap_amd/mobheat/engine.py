@@ -339,11 +339,14 @@ def merge_state(base, deltas):
     return info, np.ascontiguousarray(allr)
 
 
-def save_state_file(path, info, recs):
+def save_state_file(path, info, recs, meta=None):
+    """info + records written atomically to `path` (.npz of plain arrays, no pickles); `meta` (a str: the checkpoint
+    chain record, mobheat.checkpoint) is stored beside them."""
     import os
     tmp = f"{path}.tmp{os.getpid()}"
+    extra = {} if meta is None else {"meta": np.array(meta)}
     with open(tmp, "wb") as f:
-        np.savez(f, info=np.array([info[k] for k in _INFO_FIELDS], np.int64), recs=recs)
+        np.savez(f, info=np.array([info[k] for k in _INFO_FIELDS], np.int64), recs=recs, **extra)
         f.flush()
         os.fsync(f.fileno())
     os.replace(tmp, path)

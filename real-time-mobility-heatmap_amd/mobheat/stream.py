@@ -44,82 +44,68 @@ STATE_FULL_EVERY = int(os.getenv("MOBHEAT_STATE_FULL_EVERY", "10"))
 _ENGINE = None
 _LAST_EPOCH = None   # the last epoch committed (merged and written) from _ENGINE's state
 _PENDING = None      # (epoch, result, dictionaries): a batch merged into _ENGINE's state whose writes did not complete
+_LINEAGE = None      # the checkpoint chain _ENGINE's state continues (mobheat.checkpoint)
 
 
 def _state_dir():
     return os.path.join(CHECKPOINT_DIR, "mobheat-state")
 
 
+def _store(rank=0, world=1):
+    from .checkpoint import StateCheckpoints
+    return StateCheckpoints(_state_dir(), rank, world)
+
+
 def _checkpoints():
-    """[(epoch, kind, path)] of the saved states, oldest first; kind "full" (state-<epoch>.npz) or "delta"."""
-    d = _state_dir()
-    if not os.path.isdir(d):
-        return []
-    out = []
-    for name in os.listdir(d):
-        for prefix, kind in (("state-", "full"), ("delta-", "delta")):
-            if name.startswith(prefix) and name.endswith(".npz"):
-                try:
-                    out.append((int(name[len(prefix):-4]), kind, os.path.join(d, name)))
-                except ValueError:
-                    pass
-    return sorted(out)
+    """[(epoch, kind, path)] of this stream's (rank 0 of 1) saved states, oldest first; kind "full" or "delta"."""
+    return [(e.epoch, e.kind, e.path) for e in _store().scan() if e.rank == 0 and e.world == 1]
 
 
 def restore_state(eng, epoch_id):
-    """Load the state after the newest checkpointed epoch older than `epoch_id` into a fresh engine: the newest full
-    snapshot before it and the deltas of the epochs since (merged on the host, engine.merge_state).  Returns that
-    epoch or None."""
-    from .engine import load_state_file, merge_state
-    cps = [c for c in _checkpoints() if c[0] < int(epoch_id)]
-    fulls = [c for c in cps if c[1] == "full"]
-    if not fulls:
+    """Load the state after the newest checkpointed epoch older than `epoch_id` into a fresh engine: the newest epoch
+    at which an unbroken chain (snapshot + deltas, one lineage) ends for every rank of the world that wrote it
+    (mobheat.checkpoint; a multi-GPU stream's chains are merged: one GPU owns every key).  Returns that epoch or None
+    (a fresh lineage then starts)."""
+    global _LINEAGE
+    from .checkpoint import new_lineage
+    st = _store()
+    pt = st.restore_point(int(epoch_id))
+    if pt is None:
+        _LINEAGE = new_lineage()
         return None
-    f = fulls[-1]
-    deltas = [c for c in cps if c[1] == "delta" and c[0] > f[0]]
-    info, recs = merge_state(load_state_file(f[2]), [load_state_file(d[2]) for d in deltas])
+    info, recs = st.load(pt)
     eng.import_state(info, recs)
-    return deltas[-1][0] if deltas else f[0]
+    _LINEAGE = pt.lineage
+    return pt.epoch
 
 
 def get_engine(epoch_id=None):
     """The process's engine; a new one resumes from the newest state checkpoint older than `epoch_id` (Spark
     re-runs the first uncommitted epoch on the state of the one before it)."""
-    global _ENGINE, _LAST_EPOCH
+    global _ENGINE, _LAST_EPOCH, _LINEAGE
     if _ENGINE is not None and epoch_id is not None and _LAST_EPOCH is not None and int(epoch_id) <= _LAST_EPOCH:
         # Spark re-runs an epoch this engine already merged (the query restarted in this process): rebuild the state
         # of the epoch before it instead of merging the batch a second time
         reset_engine()
     if _ENGINE is None:
+        from .checkpoint import new_lineage
         eng = HeatmapEngine(h3_res=H3_RES, tile_minutes=TILE_MIN, watermark_delay_ms=WATERMARK_DELAY_MS,
                             device=DEVICE)
         if STATE_CHECKPOINT and epoch_id is not None:
             restore_state(eng, epoch_id)
+        else:
+            _LINEAGE = new_lineage()
         _ENGINE = eng
     return _ENGINE
 
 
 def save_state_checkpoint(epoch_id):
-    """Checkpoint the engine's state after `epoch_id`: a full snapshot when none exists or STATE_FULL_EVERY deltas
-    followed the newest one, else the batch's delta; keeps the files from the second-newest snapshot on (a replay of
-    an epoch whose save became a snapshot restores from the one before)."""
-    from .engine import save_state_file
-    os.makedirs(_state_dir(), exist_ok=True)
-    cps = [c for c in _checkpoints() if c[0] < int(epoch_id)]
-    fulls = [c for c in cps if c[1] == "full"]
-    since = [c for c in cps if c[1] == "delta" and fulls and c[0] > fulls[-1][0]]
-    eng = get_engine()
-    if not fulls or len(since) >= STATE_FULL_EVERY:
-        eng.save_state(os.path.join(_state_dir(), f"state-{int(epoch_id)}.npz"))
-    else:
-        info, recs = eng.export_state_delta()
-        save_state_file(os.path.join(_state_dir(), f"delta-{int(epoch_id)}.npz"), info, recs)
-    cps = _checkpoints()
-    fulls = [c for c in cps if c[1] == "full"]
-    if len(fulls) > 2:
-        for e, _, p in cps:
-            if e < fulls[-2][0]:
-                os.remove(p)
+    """Checkpoint the engine's state after committed epoch `epoch_id` into its chain (mobheat.checkpoint): a full
+    snapshot when the chain has none or STATE_FULL_EVERY deltas followed the newest one, else the batch's delta; files
+    of epochs >= epoch_id (an abandoned lineage) are deleted first, and the chain keeps its newest two snapshots."""
+    st = _store()
+    st.save(epoch_id, get_engine(), _LINEAGE, STATE_FULL_EVERY)
+    st.prune_other_worlds(_LINEAGE)
 
 
 def reset_engine():

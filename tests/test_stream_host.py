@@ -5,6 +5,7 @@ Expected documents are written out literally from reference heatmap_stream.py:16
 encoded as UTC milliseconds, sub-millisecond digits dropped -- SURVEY.md App. A.7).
 """
 import datetime
+import json
 import os
 
 import bson
@@ -182,19 +183,21 @@ def test_state_checkpoint_files_and_resume_choice(tmp_path, monkeypatch):
     T = 300_000_000
     w0, w1 = 100 * T, 101 * T
 
-    def write(kind, epoch, keys, prev_wm_ms=0):
+    def write(kind, epoch, keys, prev_wm_ms=0, prev=-1, base=None, lineage="A"):
         r = np.zeros(len(keys), STATE_REC_DTYPE)
         for k, (c, w, n) in enumerate(keys):
             r[k]["cell"], r[k]["window_start_us"], r[k]["count"] = c, w, n
         inf = dict(info, epoch_id=epoch, n_keys=len(keys), prev_watermark_ms=prev_wm_ms)
-        eng_mod.save_state_file(os.path.join(stream._state_dir(), f"{kind}-{epoch}.npz"), inf, r)
+        meta = json.dumps({"lineage": lineage, "base": epoch if base is None else base, "prev": prev})
+        name = f"{kind}-{epoch}.r0of1.npz"
+        eng_mod.save_state_file(os.path.join(stream._state_dir(), name), inf, r, meta=meta)
 
     write("state", 3, [(1, w0, 1), (2, w0, 1)])
-    write("delta", 4, [(2, w0, 5), (9, w1, 1)])
-    write("delta", 5, [(1, w0, 7)])
-    write("delta", 6, [(3, w1, 2)], prev_wm_ms=(w0 + T) // 1000)   # window w0 evicted by batch 6's watermark
+    write("delta", 4, [(2, w0, 5), (9, w1, 1)], prev=3, base=3)
+    write("delta", 5, [(1, w0, 7)], prev=4, base=3)
+    write("delta", 6, [(3, w1, 2)], prev_wm_ms=(w0 + T) // 1000, prev=5, base=3)   # w0 evicted by batch 6's watermark
     write("state", 12, [(4, w1, 4)])
-    write("delta", 13, [(4, w1, 6), (5, w1, 1)])
+    write("delta", 13, [(4, w1, 6), (5, w1, 1)], prev=12, base=12)
     open(os.path.join(stream._state_dir(), "state-x.npz"), "wb").close()
     assert [(e, k) for e, k, _ in stream._checkpoints()] == [(3, "full"), (4, "delta"), (5, "delta"), (6, "delta"),
                                                              (12, "full"), (13, "delta")]
@@ -209,6 +212,127 @@ def test_state_checkpoint_files_and_resume_choice(tmp_path, monkeypatch):
         if imported:
             assert imported[0][0]["n_keys"] == len(want)
     stream.reset_engine()
+
+
+def test_state_checkpoint_chains_lineage_and_pruning(tmp_path, monkeypatch):
+    """CPU: the checkpoint chains (mobheat.checkpoint).  (1) Saves with a snapshot every 2 deltas keep only
+    the files from the second-newest snapshot on, and a restart before every epoch restores exactly the state after the
+    epoch before it.  (2) A delta whose link is missing, or one of another lineage, is never merged: the restore falls
+    back to the newest complete chain, and warns when none exists.  (3) A fresh stream over an older stream's files
+    (epochs restarting at 0) deletes them at its first save, so their higher epochs are never resumed."""
+    import warnings
+
+    from mobheat import checkpoint as ck
+    from mobheat._lib import STATE_REC_DTYPE
+
+    class FakeEngine:
+        """A state of {key: count}: export_state = every key, export_state_delta = the keys the last batch touched."""
+        info = dict(epoch_id=0, n_keys=0, watermark_ms=0, prev_watermark_ms=0, tile_us=300_000_000,
+                    watermark_delay_ms=600_000, h3_res=8)
+
+        def __init__(self, state=None):
+            self.state, self.touched = dict(state or {}), set()
+
+        def batch(self, epoch):
+            self.touched = {epoch % 5, 100 + epoch}
+            for k in self.touched:
+                self.state[k] = self.state.get(k, 0) + epoch + 1
+
+        def _recs(self, keys):
+            r = np.zeros(len(keys), STATE_REC_DTYPE)
+            for i, k in enumerate(sorted(keys)):
+                r[i]["cell"], r[i]["window_start_us"], r[i]["count"] = k, 0, self.state[k]
+            return dict(self.info, n_keys=len(keys)), r
+
+        def export_state(self):
+            return self._recs(self.state)
+
+        def export_state_delta(self):
+            return self._recs(self.touched)
+
+    root = str(tmp_path / "st")
+    st = ck.StateCheckpoints(root)
+    eng, lineage, history = FakeEngine(), ck.new_lineage(), {}
+    for epoch in range(9):
+        eng.batch(epoch)
+        kinds = st.save(epoch, eng, lineage, full_every=2)
+        history[epoch] = dict(eng.state)
+        assert kinds == ("full" if epoch % 3 == 0 else "delta"), epoch
+        files = [(e.epoch, e.kind) for e in st.scan()]
+        fulls = [e for e, k in files if k == "full"]
+        assert fulls == sorted(fulls)[-2:] and files[0][0] == fulls[0], (epoch, files)   # from the 2nd-newest snapshot
+    for before in range(4, 10):
+        pt = st.restore_point(before)
+        assert pt.epoch == before - 1 and pt.lineage == lineage and pt.world == 1
+        info, recs = st.load(pt)
+        assert {int(r["cell"]): int(r["count"]) for r in recs} == history[before - 1] and info["n_keys"] == recs.size
+    # (2) a broken link: delete delta 7 -> epoch 8's chain is broken, the restore before 9 uses the chain ending at 6
+    os.remove(st.path("delta", 7))
+    assert st.restore_point(9).epoch == 6
+    # a foreign lineage's newer snapshot + delta (an abandoned stream's leftovers in the directory) are not mixed in:
+    # only a complete chain of one lineage counts, the newest wins (here the foreign one, complete on its own)
+    foreign = FakeEngine({1: 111})
+    foreign.touched = {1}
+    st2 = ck.StateCheckpoints(root)
+    info, r = foreign.export_state()
+    from mobheat import engine as eng_mod
+    eng_mod.save_state_file(st2.path("full", 20), info, r, meta=json.dumps({"lineage": "B", "base": 20, "prev": -1}))
+    eng_mod.save_state_file(st2.path("delta", 21), info, r, meta=json.dumps({"lineage": "C", "base": 20, "prev": 20}))
+    pt = st2.restore_point(22)
+    assert pt.epoch == 20 and pt.lineage == "B"   # delta 21 names another lineage: its chain is broken
+    # (3) a fresh stream (epochs from 0 again) deletes the older files at its first save: no later restore sees them
+    fresh, lin2 = FakeEngine(), ck.new_lineage()
+    fresh.batch(0)
+    st2.save(0, fresh, lin2, full_every=2)
+    assert [(e.epoch, e.kind) for e in st2.scan()] == [(0, "full")]
+    pt = st2.restore_point(30)
+    assert pt.epoch == 0 and pt.lineage == lin2
+    # files exist but no complete chain: a warning, and an empty start
+    os.remove(st2.path("full", 0))
+    eng_mod.save_state_file(st2.path("delta", 5), info, r, meta=json.dumps({"lineage": lin2, "base": 4, "prev": 4}))
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert st2.restore_point(9) is None
+    assert any("no complete chain" in str(x.message) for x in w)
+
+
+def test_state_checkpoint_reshard(tmp_path):
+    """CPU: a 3-rank stream's chains restored into 1 and into 2 ranks: each new rank keeps the keys it owns
+    (distributed.tile_owner), and the union over the new ranks is the old state exactly."""
+    from mobheat import checkpoint as ck
+    from mobheat import engine as eng_mod
+    from mobheat._lib import STATE_REC_DTYPE
+    from mobheat.distributed import tile_owner
+    rng = np.random.default_rng(3)
+    cells = rng.integers(1, 2 ** 60, 3000).astype(np.uint64)
+    ws = (rng.integers(0, 4, 3000) * 300_000_000).astype(np.int64)
+    info = dict(epoch_id=5, n_keys=0, watermark_ms=0, prev_watermark_ms=0, tile_us=300_000_000,
+                watermark_delay_ms=600_000, h3_res=8)
+    old_owner = tile_owner(cells, ws, 3)
+    root = str(tmp_path / "st")
+    for r in range(3):
+        sel = old_owner == r
+        recs = np.zeros(int(sel.sum()), STATE_REC_DTYPE)
+        recs["cell"], recs["window_start_us"], recs["count"] = cells[sel], ws[sel], np.arange(sel.sum()) + 1
+        st = ck.StateCheckpoints(root, r, 3)
+        os.makedirs(root, exist_ok=True)
+        eng_mod.save_state_file(st.path("full", 5), dict(info, n_keys=recs.size), recs,
+                                meta=json.dumps({"lineage": "L", "base": 5, "prev": -1}))
+    everything = None
+    for world in (1, 2):
+        got = []
+        for r in range(world):
+            st = ck.StateCheckpoints(root, r, world)
+            pt = st.restore_point(6)
+            assert pt == ck.RestorePoint(5, 3, "L")
+            _, recs = st.load(pt, owner=lambda c, w: tile_owner(c, w, world) == r)
+            assert (tile_owner(recs["cell"], recs["window_start_us"], world) == r).all()
+            got.append(recs)
+        u = np.sort(np.concatenate(got), order=["cell", "window_start_us"])
+        assert u.size == 3000
+        if everything is None:
+            everything = u
+        np.testing.assert_array_equal(u.view(np.uint8), everything.view(np.uint8))
 
 
 def _reference_statements(tiles, city, h3_res, ttl_min):
