@@ -32,32 +32,54 @@ from ._lib import (HM_CAND_REC_BYTES, HM_MEM_DEVICE, HM_STAGE_SUMMARY_WORDS, HM_
 # one record stream of an exchange: buf (uint8 tensor), counts[r] records for rank r, rec_bytes per record
 Stream = namedtuple("Stream", "name buf counts rec_bytes")
 
-# summary word layout (csrc/mobheat.hip SW_*)
-SW_N_IN, SW_VALID, SW_LATE, SW_AGG, SW_MAX_MS, SW_SAMPLE_RUN, SW_PREV_AGG, SW_PREV_KEYS, SW_NWIN = range(9)
+# summary word layout (csrc/api_stage.h SW_*); word 9 (SW_RESERVED in the library, which ignores it) carries the
+# rank's status: nonzero when its stage failed, so that every rank leaves the batch at the same collective
+SW_N_IN, SW_VALID, SW_LATE, SW_AGG, SW_MAX_MS, SW_SAMPLE_RUN, SW_PREV_AGG, SW_PREV_KEYS, SW_NWIN, SW_STATUS = range(10)
 SW_WIN0 = 10
 WREG_SLOTS = 4095
+MAX_STREAMS = 3   # record streams of one exchange (direct path: key, payload, candidates)
 
 
-def all_gather_summaries(summary, device):
-    """all_gather of every rank's int64[HM_STAGE_SUMMARY_WORDS] summary -> host array [world, words]."""
+class PeerFailed(RuntimeError):
+    """Another rank's stage failed: this rank left the batch at the same collective (its own state is as a failed
+    batch leaves it; the caller resets or replays)."""
+
+
+def all_gather_summaries(summary, device, status=0):
+    """all_gather of every rank's int64[HM_STAGE_SUMMARY_WORDS] summary -> host array [world, words]; `status` != 0
+    (this rank's ingest failed) makes every rank raise PeerFailed after the collective."""
     world = dist.get_world_size()
-    t = torch.from_numpy(np.ascontiguousarray(summary, dtype=np.int64)).to(device)
+    summary = np.array(summary, dtype=np.int64)
+    summary[SW_STATUS] = status
+    t = torch.from_numpy(summary).to(device)
     out = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(out, t)
-    return torch.stack(out).cpu().numpy()
+    S = torch.stack(out).cpu().numpy()
+    if status == 0 and (S[:, SW_STATUS] != 0).any():
+        raise PeerFailed(f"rank(s) {np.nonzero(S[:, SW_STATUS])[0].tolist()} failed the batch's ingest")
+    return S
 
 
-def exchange(streams, device):
+def exchange(streams, device, status=0):
     """all_to_all of several variable-size record streams: one all_to_all of all the per-destination counts (the
-    batch's single host synchronization of the exchange), then one all_to_all per stream.  Payloads move as 8-byte
-    words (record sizes are multiples of 8): a rank's share at 1e8 events per GPU is several GB, past 2^31
-    single-byte elements.  Returns [(recv uint8 tensor, recv_counts per source)] in stream order."""
+    batch's single host synchronization of the exchange; it also carries each rank's status: a rank whose stage failed
+    sends status != 0 and no streams, and every rank raises PeerFailed before the payloads move), then one all_to_all
+    per stream.  Payloads move as 8-byte words (record sizes are multiples of 8): a rank's share at 1e8 events per GPU
+    is several GB, past 2^31 single-byte elements.  Returns [(recv uint8 tensor, recv_counts per source)] in stream
+    order."""
     world = dist.get_world_size()
     k = len(streams)
-    sc = torch.tensor([[s.counts[r] for s in streams] for r in range(world)], dtype=torch.int64, device=device)
+    assert k <= MAX_STREAMS
+    cnt = [[(streams[j].counts[r] if j < k else 0) for j in range(MAX_STREAMS)] + [status] for r in range(world)]
+    sc = torch.tensor(cnt, dtype=torch.int64, device=device)
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc)
     rcounts = rc.cpu().tolist()
+    bad = [r for r in range(world) if rcounts[r][MAX_STREAMS]]
+    if bad and status == 0:
+        raise PeerFailed(f"rank(s) {bad} failed the batch's stage before the exchange")
+    if status:
+        return []
     out = []
     for j, s in enumerate(streams):
         assert s.rec_bytes % 8 == 0 and len(s.counts) == world
@@ -112,9 +134,11 @@ class LibStages:
         return b
 
     def ingest(self, epoch, batch, world, rank):
+        """batch: n and the column pointers (device memory, or host memory with batch["memory"] = HM_MEM_HOST: the
+        library copies them, sharded.py's per-rank slices of the micro-batch)."""
         self.world = world
         self._n = n = int(batch["n"])
-        b = HmBatchIn(n=n, memory=HM_MEM_DEVICE, lat=batch["lat"], lon=batch["lon"], ts_us=batch["ts_us"],
+        b = HmBatchIn(n=n, memory=int(batch.get("memory", HM_MEM_DEVICE)), lat=batch["lat"], lon=batch["lon"], ts_us=batch["ts_us"],
                       speed=batch.get("speed"), speed_valid=batch.get("speed_valid"), vkey=batch["vkey"],
                       row_valid=batch.get("row_valid"))
         ctx = self.engine._ctx
@@ -174,15 +198,32 @@ class ShardedHeatmap:
         self._recv = None
 
     def process_batch(self, epoch, batch, out_memory=HM_MEM_DEVICE, sync=None):
+        """One micro-batch on this rank.  A stage that raises on one rank makes every rank leave at the next
+        collective (the failed rank re-raises its error, the others PeerFailed), so no rank waits on a collective its
+        peers never reach."""
         # the library reads the received buffers on its own stream: RCCL's (torch's current stream) must be done
         sync = sync or (lambda: torch.cuda.current_stream(self.device).synchronize()
                         if self.device.type == "cuda" else None)
-        summary = self.stages.ingest(epoch, batch, self.world, self.rank)
-        summaries = all_gather_summaries(summary, self.device)
-        streams = self.stages.send(summaries)
+        err = None
+        try:
+            summary = self.stages.ingest(epoch, batch, self.world, self.rank)
+        except Exception as e:
+            err, summary = e, np.zeros(HM_STAGE_SUMMARY_WORDS, np.int64)
+        summaries = all_gather_summaries(summary, self.device, status=1 if err else 0)
+        if err:
+            raise err
+        try:
+            streams = self.stages.send(summaries)
+        except Exception as e:
+            exchange([], self.device, status=1)
+            raise e
         recv = exchange(streams, self.device)
         sync()
-        out, winners = self.stages.merge(recv, out_memory)
+        try:
+            out, winners = self.stages.merge(recv, out_memory)
+        except Exception as e:
+            exchange([], self.device, status=1)
+            raise e
         [(winner_recv, wrc)] = exchange([winners], self.device)
         sync()
         self._recv = (recv, winner_recv)

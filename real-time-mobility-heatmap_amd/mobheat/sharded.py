@@ -1,0 +1,408 @@
+"""The multi-GPU hot path behind the reference's boundary: foreach_batch_func(df, epoch_id) with MOBHEAT_GPUS=N.
+
+The reference hands each micro-batch to ``foreach_batch_func`` on the Spark driver, once per epoch, sequentially
+(heatmap_stream.py:150,245), and writes the tiles and positions_latest documents from there (:159-235).  With N GPUs
+the driver process runs rank 0 and N-1 persistent worker processes run ranks 1..N-1, one GPU each, joined by
+torch.distributed (backend "nccl" = RCCL over xGMI; MOBHEAT_DIST_BACKEND=gloo rehearses several ranks on one GPU).
+Workers are started with a fresh spawn (never an exec of a process that touched the GPU).  Per micro-batch:
+
+  1. the driver extracts the batch's columns (stream.batch_columns; raw Kafka values are decoded on rank 0's GPU) and
+     its string dictionaries into one POSIX shared-memory region, and tells every rank its contiguous share;
+  2. every rank runs the sharded stages (distributed.ShardedHeatmap over the library's stage API, its share copied
+     to its GPU by the library): snap, windows and latest-position maxima locally, the owner-keyed all-to-all, the
+     owner merge into the state it owns;
+  3. every rank encodes, on its GPU, the update statements of what it owns -- the tiles of its keys
+     (hm_encode_tile_updates) and the positions of the latest rows it holds (hm_encode_position_updates) -- so no
+     statement crosses the exchange; workers hand theirs back through shared memory;
+  4. the driver writes them through the sink, tiles first, as the reference does (one connection per batch, unordered
+     bulks of 1000);
+  5. after the writes succeeded (the batch is committed) every rank checkpoints its own state (mobheat.checkpoint:
+     per-rank chains; a restore into another GPU count re-partitions the keys by owner).
+
+A failure on any rank fails the batch (every rank leaves at the same collective, distributed.PeerFailed); a failure
+after a merge began resets every rank's state, which the replayed epoch restores from the checkpoints.
+"""
+import atexit
+import os
+import socket
+import traceback
+
+import numpy as np
+
+from . import _lib
+from ._lib import HM_MEM_DEVICE, HM_MEM_HOST
+
+COLS = ("lat", "lon", "ts_us", "speed", "speed_valid", "vkey", "row_valid")
+_DT = {"lat": np.float64, "lon": np.float64, "ts_us": np.int64, "speed": np.float64, "speed_valid": np.uint8,
+       "vkey": np.uint64, "row_valid": np.uint8}
+
+
+# ------------------ shared memory ------------------
+class ShmArena:
+    """A growable POSIX shared-memory region holding named arrays (64-B aligned); put() returns the manifest a reader
+    maps them with (shm_views)."""
+
+    def __init__(self):
+        self.shm = None
+
+    def put(self, arrays):
+        layout, off = [], 0
+        arrays = {k: np.ascontiguousarray(v) for k, v in arrays.items()}
+        for name, a in arrays.items():
+            layout.append((name, a.dtype.str, a.shape, off))
+            off += (a.nbytes + 63) & ~63
+        self._ensure(max(off, 64))
+        for (name, dt, shp, o) in layout:
+            a = arrays[name]
+            if a.nbytes:
+                np.ndarray(a.shape, a.dtype, buffer=self.shm.buf, offset=o)[...] = a
+        return self.shm.name, layout
+
+    def _ensure(self, nbytes):
+        from multiprocessing import shared_memory
+        if self.shm is not None and self.shm.size >= nbytes:
+            return
+        old = self.shm
+        self.shm = shared_memory.SharedMemory(create=True, size=int(nbytes + nbytes // 4 + (1 << 20)))
+        if old is not None:
+            old.close()
+            old.unlink()
+
+    def close(self):
+        if self.shm is not None:
+            self.shm.close()
+            try:
+                self.shm.unlink()
+            except FileNotFoundError:
+                pass
+            self.shm = None
+
+
+_ATTACHED = {}
+
+
+def shm_views(name, layout, slot="in"):
+    """{name: array view} of a manifest in another process's region (attachments are cached).  (The spawned ranks share
+    the driver's resource tracker, whose registry is a set: attaching adds nothing, and the region's creator
+    unregisters it when it unlinks it.)"""
+    from multiprocessing import shared_memory
+    cur = _ATTACHED.get(slot)   # (slot: the writer -- its previous region is gone once it grew into a new one)
+    if cur is None or cur.name != name:
+        if cur is not None:
+            cur.close()
+        cur = _ATTACHED[slot] = shared_memory.SharedMemory(name=name)
+    shm = cur
+    return {n: np.ndarray(shp, np.dtype(dt), buffer=shm.buf, offset=o) for n, dt, shp, o in layout}
+
+
+def dictionary_arrays(uniques):
+    """A batch's string dictionary as (n, offsets, bytes) arrays (Arrow layout), whatever form it came in."""
+    if isinstance(uniques, tuple):
+        return uniques
+    return _lib._dictionary(uniques)
+
+
+# ------------------ one rank ------------------
+class RankRunner:
+    """One rank of the sharded writer: its engine (restored from the checkpoints when it starts), the stage pipeline,
+    the statements of what it owns, its checkpoint chain."""
+
+    def __init__(self, rank, world, device, cfg):
+        import torch
+        from .checkpoint import StateCheckpoints
+        self.rank, self.world, self.cfg = rank, world, cfg
+        self.device_index = device
+        self.device = torch.device("cuda", device) if device is not None else torch.device("cpu")
+        self.began = False
+        self.engine = None
+        self.sharded = None
+        self.lineage = None
+        self.store = StateCheckpoints(os.path.join(cfg["checkpoint_dir"], "mobheat-state"), rank, world)
+        self.out = ShmArena()
+
+    def reset(self):
+        if self.engine is not None:
+            self.engine.close()
+        self.engine = self.sharded = None
+
+    def _start(self, restore):
+        from .distributed import LibStages, ShardedHeatmap, tile_owner
+        from .engine import HeatmapEngine
+        c = self.cfg
+        eng = HeatmapEngine(h3_res=c["h3_res"], tile_minutes=c["tile_minutes"], watermark_delay_ms=c["delay_ms"],
+                            device=self.device_index)
+        kind, val = restore
+        if kind == "point":
+            info, recs = self.store.load(val, owner=lambda cl, ws: tile_owner(cl, ws, self.world) == self.rank)
+            eng.import_state(info, recs)
+            self.lineage = val.lineage
+        else:
+            self.lineage = val
+        self.engine = eng
+        self.sharded = ShardedHeatmap(LibStages(eng), self.device)
+
+    def run(self, epoch, views, lo, hi, restore):
+        """Rank's share [lo, hi) of the batch in `views` (host arrays, the whole batch): the sharded stages, then the
+        statements of the tiles it owns and of the latest rows it holds.  Returns (stats, tiles, positions) with the
+        statements as (bytes, offsets) views of the engine's pinned buffers."""
+        if self.engine is None:
+            self._start(restore)
+        eng = self.engine
+        self.began = False
+        v0 = eng.state_version()
+        try:
+            return self._run(eng, epoch, views, lo, hi)
+        finally:
+            self.began = eng.state_version() != v0
+
+    def _run(self, eng, epoch, views, lo, hi):
+        n = hi - lo
+        batch = {"n": n, "memory": HM_MEM_HOST}
+        for k in COLS:
+            a = views[k]
+            batch[k] = a.ctypes.data + lo * a.itemsize if a.size else None
+        out = self.sharded.process_batch(epoch, batch, out_memory=HM_MEM_DEVICE)
+        c = self.cfg
+        tiles = eng.encode_tile_updates(c["city"], c["ttl_min"])
+        positions = None
+        if out.n_latest:
+            prov = (int(views["prov_n"][0]), views["prov_offs"], views["prov_bytes"])
+            veh = (int(views["veh_n"][0]), views["veh_offs"], views["veh_bytes"])
+            positions = eng.encode_position_updates(prov, veh)
+        stats = dict(n_in=int(out.n_in), n_valid=int(out.n_valid), n_late=int(out.n_late), n_state=int(out.n_state),
+                     n_tiles=int(out.n_tiles), n_latest=int(out.n_latest), watermark_ms=int(out.watermark_ms),
+                     batch_max_event_ms=int(out.batch_max_event_ms), late_watermark_ms=int(out.late_watermark_ms),
+                     n_partials=int(out.n_partials), counts=eng.last_counts())
+        return stats, tiles, positions
+
+    def commit(self, epoch):
+        if self.cfg["checkpoint"] and self.engine is not None:
+            self.store.save(epoch, self.engine, self.lineage, self.cfg["full_every"])
+
+    def export_out(self, tiles, positions):
+        """A worker's statements into its shared-memory region: (name, layout)."""
+        arrs = {"tb": tiles[0], "to": tiles[1]}
+        if positions is not None:
+            arrs.update(pb=positions[0], po=positions[1])
+        return self.out.put(arrs)
+
+
+def _runner_class(cfg):
+    """RankRunner, or the class cfg["runner"] names ("module:Class": the CPU tests' oracle-backed rank)."""
+    name = cfg.get("runner")
+    if not name:
+        return RankRunner
+    import importlib
+    mod, cls = name.split(":")
+    return getattr(importlib.import_module(mod), cls)
+
+
+def _init_group(rank, world, port, backend, device):
+    import torch
+    import torch.distributed as dist
+    if device is not None:
+        torch.cuda.set_device(device)
+    kw = {"device_id": torch.device("cuda", device)} if backend == "nccl" else {}
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world, **kw)
+
+
+def _worker_main(rank, world, port, conn, cfg):
+    """A worker rank's loop: ("batch", ...) -> ("ok", stats, out manifest) | ("err", repr, traceback);
+    ("commit", epoch), ("reset",), ("close",)."""
+    import torch.distributed as dist
+    device = cfg["devices"][rank]
+    try:
+        _init_group(rank, world, port, cfg["backend"], device)
+        runner = _runner_class(cfg)(rank, world, device, cfg)
+    except Exception as e:   # (the driver's init_process_group times out; report why)
+        conn.send(("err", repr(e), traceback.format_exc()))
+        return
+    conn.send(("ready",))
+    while True:
+        msg = conn.recv()
+        op = msg[0]
+        try:
+            if op == "batch":
+                _, epoch, name, layout, lo, hi, restore = msg
+                stats, tiles, positions = runner.run(epoch, shm_views(name, layout), lo, hi, restore)
+                conn.send(("ok", stats, runner.export_out(tiles, positions)))
+            elif op == "commit":
+                runner.commit(msg[1])
+                conn.send(("ok",))
+            elif op == "reset":
+                runner.reset()
+                conn.send(("ok",))
+            elif op == "close":
+                break
+        except Exception as e:
+            conn.send(("err", repr(e), traceback.format_exc(), type(e).__name__, getattr(runner, "began", False)))
+    runner.reset()
+    runner.out.close()
+    try:
+        dist.destroy_process_group()
+    except Exception:
+        pass
+    conn.send(("closed",))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class ShardedStream:
+    """The driver's side: rank 0 in this process, ranks 1..world-1 in spawned workers."""
+
+    def __init__(self, world, cfg):
+        import torch
+        import torch.distributed as dist
+        import torch.multiprocessing as mp
+        if dist.is_available() and dist.is_initialized():
+            raise RuntimeError("MOBHEAT_GPUS > 1 starts its own process group: this process already has one")
+        self.world = int(world)
+        ndev = max(torch.cuda.device_count(), 1)
+        cfg = dict(cfg)
+        if cfg.get("cpu"):   # (the CPU tests: ranks without a GPU, gloo on host tensors)
+            cfg["devices"] = [None] * self.world
+        else:
+            cfg["devices"] = [int(d) for d in cfg.get("devices") or [r % ndev for r in range(self.world)]]
+        self.cfg = cfg
+        port = _free_port()
+        ctx = mp.get_context("spawn")
+        self.conns, self.procs = [], []
+        for r in range(1, self.world):
+            parent, child = ctx.Pipe()
+            p = ctx.Process(target=_worker_main, args=(r, self.world, port, child, cfg), daemon=True)
+            p.start()
+            self.conns.append(parent)
+            self.procs.append(p)
+        _init_group(0, self.world, port, cfg["backend"], cfg["devices"][0])
+        for c in self.conns:
+            m = c.recv()
+            if m[0] != "ready":
+                raise RuntimeError(f"mobheat worker failed to start: {m[1]}\n{m[2]}")
+        self.runner = _runner_class(cfg)(0, self.world, cfg["devices"][0], cfg)
+        self.inputs = ShmArena()
+        self.restore = None   # the restore point the ranks start from (set when they (re)start)
+        self.last = None      # the last batch's per-rank statements (views) and stats
+        self.closed = False
+        atexit.register(self.close)
+
+    # ---- one micro-batch ----
+    def _restore_point(self, epoch):
+        from .checkpoint import new_lineage
+        pt = self.runner.store.restore_point(int(epoch)) if self.cfg["checkpoint"] and epoch is not None else None
+        return ("point", pt) if pt is not None else ("fresh", new_lineage())
+
+    def rank0_engine(self, epoch):
+        """Rank 0's engine, started (restored) now if it is not yet (the Kafka decode runs on it before the batch)."""
+        if self.restore is None:
+            self.restore = self._restore_point(epoch)
+        if self.runner.engine is None:
+            self.runner._start(self.restore)
+        return self.runner.engine
+
+    def process(self, epoch, cols, dicts):
+        """Run one micro-batch on every rank; returns the per-rank stats.  Raises (every rank's state reset when a merge
+        may have begun) if any rank failed."""
+        from .distributed import PeerFailed
+        n = int(cols["n"])
+        arrays = {k: np.ascontiguousarray(cols[k] if cols.get(k) is not None else np.zeros(n), dtype=_DT[k]) for k in COLS}
+        if cols.get("speed") is None:   # (no speed column: all null)
+            arrays["speed_valid"] = np.zeros(n, np.uint8)
+        pn, po, pb = dictionary_arrays(dicts[0])
+        vn, vo, vb = dictionary_arrays(dicts[1])
+        arrays.update(prov_n=np.array([pn], np.int64), prov_offs=po, prov_bytes=pb, veh_n=np.array([vn], np.int64),
+                      veh_offs=vo, veh_bytes=vb)
+        name, layout = self.inputs.put(arrays)
+        views = {k: np.ndarray(shp, np.dtype(d), buffer=self.inputs.shm.buf, offset=o) for k, d, shp, o in layout}
+        bounds = [r * n // self.world for r in range(self.world + 1)]
+        if self.restore is None:   # (the ranks (re)start from the newest checkpoint before this epoch)
+            self.restore = self._restore_point(epoch)
+        for r, c in enumerate(self.conns, start=1):
+            c.send(("batch", int(epoch), name, layout, bounds[r], bounds[r + 1], self.restore))
+        err0 = res0 = None
+        try:
+            res0 = self.runner.run(int(epoch), views, bounds[0], bounds[1], self.restore)
+        except Exception as e:
+            err0 = e
+        replies = [c.recv() for c in self.conns]
+        errs = [(0, err0)] if err0 is not None else []
+        began = err0 is not None and getattr(self.runner, "began", False)
+        for r, m in enumerate(replies, start=1):
+            if m[0] != "ok":
+                errs.append((r, RuntimeError(f"rank {r}: {m[1]}\n{m[2]}")))
+                began = began or bool(m[4])
+        if errs:
+            # a merge began on some rank: every rank's state is dropped (the replayed epoch restores it from the
+            # checkpoints); a batch that failed before any merge leaves every state as it was
+            if began:
+                self.reset()
+            first = next((e for _, e in errs if not isinstance(e, PeerFailed) and "PeerFailed" not in str(e)), errs[0][1])
+            raise first
+        stats0, tiles0, pos0 = res0
+        per_rank = [(stats0, tiles0, pos0)]
+        for m in replies:
+            v = shm_views(*m[2], slot=f"out{len(per_rank)}")
+            per_rank.append((m[1], (v["tb"], v["to"]), (v["pb"], v["po"]) if "pb" in v else None))
+        self.last = per_rank
+        return per_rank
+
+    def commit(self, epoch):
+        """Checkpoint every rank's state after the committed epoch (rank 0 last; then the files of an older world size
+        are dropped once every rank of this one holds a snapshot)."""
+        for c in self.conns:
+            c.send(("commit", int(epoch)))
+        err = None
+        try:
+            self.runner.commit(epoch)
+        except Exception as e:
+            err = e
+        for r, c in enumerate(self.conns, start=1):
+            m = c.recv()
+            if m[0] != "ok" and err is None:
+                err = RuntimeError(f"rank {r} checkpoint: {m[1]}")
+        if err is not None:
+            raise err
+        if self.cfg["checkpoint"] and self.runner.lineage is not None:
+            self.runner.store.prune_other_worlds(self.runner.lineage)
+
+    def reset(self):
+        """Drop every rank's state (the next batch restores from the checkpoints)."""
+        for c in self.conns:
+            c.send(("reset",))
+        self.runner.reset()
+        for c in self.conns:
+            c.recv()
+        self.last = None
+        self.restore = None
+
+    def close(self):
+        if self.closed:
+            return
+        self.closed = True
+        import torch.distributed as dist
+        for c in self.conns:
+            try:
+                c.send(("close",))
+            except Exception:
+                pass
+        self.runner.reset()
+        for c, p in zip(self.conns, self.procs):
+            try:
+                if c.poll(60):
+                    c.recv()
+            except Exception:
+                pass
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+        try:
+            dist.destroy_process_group()
+        except Exception:
+            pass
+        self.inputs.close()
+        self.runner.out.close()

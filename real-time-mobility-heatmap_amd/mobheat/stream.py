@@ -38,6 +38,10 @@ DEVICE = int(os.getenv("MOBHEAT_DEVICE", os.getenv("LOCAL_RANK", "0")))
 # STATE_FULL_EVERY batches (spark.sql.streaming.stateStore.minDeltasForSnapshot = 10).  MOBHEAT_STATE_CHECKPOINT=0
 # turns it off.
 CHECKPOINT_DIR = os.getenv("CHECKPOINT", "/tmp/heatmap-checkpoint")
+# MOBHEAT_GPUS=N > 1: the batch is sharded over N GPUs of this node (mobheat.sharded: this process runs rank 0, N-1
+# spawned workers the others; torch.distributed over RCCL, or MOBHEAT_DIST_BACKEND=gloo to rehearse on one GPU)
+N_GPUS = int(os.getenv("MOBHEAT_GPUS", "1"))
+DIST_BACKEND = os.getenv("MOBHEAT_DIST_BACKEND", "nccl")
 STATE_CHECKPOINT = os.getenv("MOBHEAT_STATE_CHECKPOINT", "1") == "1"
 STATE_FULL_EVERY = int(os.getenv("MOBHEAT_STATE_FULL_EVERY", "10"))
 
@@ -114,6 +118,34 @@ def reset_engine():
     if _ENGINE is not None:
         _ENGINE.close()
     _ENGINE = None
+    _LAST_EPOCH = None
+    _PENDING = None
+    if _SHARDED is not None:
+        _SHARDED.reset()
+
+
+_SHARDED = None   # mobheat.sharded.ShardedStream when N_GPUS > 1
+SHARDED_EXTRA = {}   # more ShardedStream config (the CPU tests: {"cpu": True, "runner": "module:Class"})
+
+
+def get_sharded():
+    """The process's sharded writer (N_GPUS ranks; started at the first batch)."""
+    global _SHARDED
+    if _SHARDED is None:
+        from .sharded import ShardedStream
+        _SHARDED = ShardedStream(N_GPUS, dict(h3_res=H3_RES, tile_minutes=TILE_MIN, delay_ms=WATERMARK_DELAY_MS,
+                                              city=CITY, ttl_min=TTL_MIN, checkpoint_dir=CHECKPOINT_DIR,
+                                              checkpoint=STATE_CHECKPOINT, full_every=STATE_FULL_EVERY,
+                                              backend=DIST_BACKEND, **SHARDED_EXTRA))
+    return _SHARDED
+
+
+def close_sharded():
+    """Stop the sharded writer's workers and its process group (a new query, or the end of the process)."""
+    global _SHARDED, _LAST_EPOCH, _PENDING
+    if _SHARDED is not None:
+        _SHARDED.close()
+    _SHARDED = None
     _LAST_EPOCH = None
     _PENDING = None
 
@@ -424,6 +456,77 @@ def _process(eng, epoch_id, cols):
     return res, (cols["provider_uniques"], cols["vehicle_uniques"])
 
 
+def _kafka_host_columns(eng, values, offsets):
+    """Raw Kafka values decoded on `eng`'s GPU (hm_decode_json) and copied to host columns: the sharded writer hands
+    every rank its share from host memory (the batch-wide string dictionaries keep the vkeys consistent across ranks)."""
+    from . import _lib
+    try:
+        kb = eng.decode_json(values, offsets)
+    except RuntimeError as e:
+        if getattr(e, "code", None) != _lib.HM_E_UNSUPPORTED:
+            raise
+        from . import kafka_host
+        cols = batch_columns(kafka_host.decode_table(values, offsets))
+        return cols, (cols["provider_uniques"], cols["vehicle_uniques"])
+    b = kb.batch
+    n = int(b.n)
+    lib = _lib.load()
+
+    def d2h(p, dt):
+        a = np.empty(n, dt)
+        if n:
+            _lib.check(lib.hm_memcpy(a.ctypes.data, p, a.nbytes, 1), None, "hm_memcpy")
+        return a
+    cols = dict(n=n, lat=d2h(b.lat, np.float64), lon=d2h(b.lon, np.float64), ts_us=d2h(b.ts_us, np.int64),
+                speed=d2h(b.speed, np.float64), speed_valid=d2h(b.speed_valid, np.uint8), vkey=d2h(b.vkey, np.uint64),
+                row_valid=d2h(b.row_valid, np.uint8))
+    return cols, (kb.providers, kb.vehicles)
+
+
+def _foreach_sharded(df, epoch):
+    """foreach_batch_func over N_GPUS ranks (mobheat.sharded): every rank merges the keys it owns and encodes the
+    statements of its tiles and of its latest rows; they are written here, tiles first (:159-235), and every rank
+    checkpoints after the writes succeeded.  Replay and failure semantics as the single-GPU path."""
+    global _LAST_EPOCH, _PENDING
+    from .engine import BatchResult
+    sh = get_sharded()
+    if _PENDING is not None and _PENDING[0] == epoch and sh.last is not None:
+        per_rank = sh.last   # the replay of the epoch whose writes failed: every rank's state is in place
+    else:
+        if _PENDING is not None or (_LAST_EPOCH is not None and epoch <= _LAST_EPOCH):
+            # another epoch while one is uncommitted, or a committed epoch re-run: every rank restores the state of
+            # the epoch before it from the checkpoints
+            sh.reset()
+            _LAST_EPOCH = None
+        _PENDING = None
+        cols = batch_columns(df)
+        if "kafka" in cols:
+            cols, dicts = _kafka_host_columns(sh.rank0_engine(epoch), *cols["kafka"])
+        else:
+            dicts = (cols["provider_uniques"], cols["vehicle_uniques"])
+        per_rank = sh.process(epoch, cols, dicts)
+        _PENDING = (epoch, per_rank, None)
+    sink = SINK_FACTORY()
+    try:
+        for _, tiles, _ in per_rank:
+            _flush_statements(sink, "tiles", *tiles)
+        for _, _, pos in per_rank:
+            if pos is not None:
+                _flush_statements(sink, "positions_latest", *pos)
+        if STATE_CHECKPOINT:
+            sh.commit(epoch)
+    finally:
+        sink.close()
+    _PENDING = None
+    _LAST_EPOCH = epoch
+    st = [x[0] for x in per_rank]
+    tot = lambda k: sum(int(x[k]) for x in st)   # noqa: E731
+    return BatchResult(tiles=None, latest_rows=None, n_in=tot("n_in"), n_valid=tot("n_valid"), n_late=tot("n_late"),
+                       n_state=tot("n_state"), batch_max_event_ms=int(st[0]["batch_max_event_ms"]),
+                       watermark_ms=int(st[0]["watermark_ms"]), late_watermark_ms=int(st[0]["late_watermark_ms"]),
+                       n_partials=tot("n_partials"), n_tiles=tot("n_tiles"), n_latest=tot("n_latest"))
+
+
 def foreach_batch_func(df, epoch_id: int):
     """Runs on each micro-batch (reference heatmap_stream.py:150): tiles + latest positions -> MongoDB.
 
@@ -433,6 +536,8 @@ def foreach_batch_func(df, epoch_id: int):
     merged state and, when Spark re-runs that epoch, writes the same documents again without merging twice."""
     global _LAST_EPOCH, _PENDING
     epoch = int(epoch_id)
+    if N_GPUS > 1:
+        return _foreach_sharded(df, epoch)
     if _PENDING is not None and _PENDING[0] == epoch and _ENGINE is not None:
         res, dicts = _PENDING[1], _PENDING[2]   # the replay of the epoch whose writes failed: its state is in place
     else:

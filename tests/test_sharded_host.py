@@ -1,0 +1,105 @@
+"""CPU, world_size 2 over gloo: the sharded writer behind foreach_batch_func (mobheat.sharded, MOBHEAT_GPUS = 2;
+reference heatmap_stream.py:150,159-235,244-245) -- a spawned worker rank, the batch's columns and string dictionaries
+handed over in shared memory, every rank encoding the statements of what it owns, the driver writing them tiles first,
+commits after the writes, and Spark's replay of a batch whose writes failed.
+
+The ranks' stages are the oracle restatement (tests/sharded_fake.OracleRunner over test_distributed_gloo.OracleStages)
+and their statements come from the library's host-executed encoders, so the written statements must equal those of
+the single-shard oracle run through the same encoders, byte for byte (dyadic inputs: every fp64 sum is exact).
+tests/test_gpu_sharded_stream.py runs the same writer on the GPU through the HIP library.
+"""
+import numpy as np
+import pandas as pd
+import pytest
+
+from mobheat import stream
+
+
+class Capture:
+    log = []
+    fail = False
+
+    def __init__(self):
+        self.cur = {"tiles": [], "positions_latest": []}
+        Capture.log.append(self.cur)
+
+    def update_raw(self, collection, statements):
+        if Capture.fail:
+            raise IOError("mongo down")
+        self.cur[collection].extend(bytes(s.raw) for s in statements)
+
+    def close(self):
+        pass
+
+
+def _frames(n_batches=3, n=3000, seed=2):
+    rng = np.random.default_rng(seed)
+    out = []
+    for b in range(n_batches):
+        lat = 42.0 + rng.integers(0, 1 << 8, n) / 1024.0
+        lon = -71.25 + rng.integers(0, 1 << 8, n) / 1024.0
+        speed = pd.array(rng.integers(0, 160, n) * 0.5, dtype="Float64")
+        speed[rng.random(n) < 0.1] = pd.NA
+        ts = 1759572000 + b * 240 + rng.integers(0, 360, n)
+        ts[: n // 30] = ts[n // 30: 2 * (n // 30)]
+        veh = rng.integers(0, 300, n)
+        out.append(pd.DataFrame({"provider": np.where(veh % 5 == 0, "mbta", "opensky"),
+                                 "vehicleId": [f"v{v}" for v in veh], "lat": lat, "lon": lon, "speedKmh": speed,
+                                 "eventTs": pd.to_datetime(ts, unit="s", utc=True)}))
+    return out
+
+
+def _expected(frames):
+    """The single-shard oracle through the same host encoders: per batch, sorted tile and position statements."""
+    from mobheat import _lib
+    from oracle.spark_oracle import SparkHeatmapOracle
+    from sharded_fake import statements_of_tiles
+    ora = SparkHeatmapOracle(h3_res=stream.H3_RES, tile_us=stream.TILE_MIN * 60_000_000)
+    cfg = dict(city=stream.CITY, h3_res=stream.H3_RES, ttl_min=stream.TTL_MIN, tile_minutes=stream.TILE_MIN)
+    out = []
+    for df in frames:
+        c = stream.batch_columns(df)
+        e = ora.process_batch(c["lat"], c["lon"], c["ts_us"], c["speed"], c["speed_valid"], c["vkey"], c["row_valid"])
+        tb, to = statements_of_tiles({(t["cell"], t["window_start_us"]): (t["count"], t["avg_speed"], t["avg_lon"],
+                                                                         t["avg_lat"]) for t in e["tiles"]}, cfg)
+        r = e["latest_rows"]
+        pb, po = _lib.position_statements_selftest(c["provider_uniques"], c["vehicle_uniques"], c["vkey"][r],
+                                                   c["ts_us"][r], c["lat"][r], c["lon"][r])
+        out.append({"tiles": sorted(bytes(tb[to[k]:to[k + 1]]) for k in range(to.size - 1)),
+                    "positions_latest": sorted(bytes(pb[po[k]:po[k + 1]]) for k in range(po.size - 1))})
+    return out
+
+
+def test_sharded_writer_world2_gloo(tmp_path, monkeypatch, oracle_h3):
+    from sharded_fake import OracleRunner
+    frames = _frames()
+    exp = _expected(frames)
+    monkeypatch.setattr(stream, "SINK_FACTORY", Capture)
+    monkeypatch.setattr(stream, "N_GPUS", 2)
+    monkeypatch.setattr(stream, "DIST_BACKEND", "gloo")
+    monkeypatch.setattr(stream, "STATE_CHECKPOINT", True)
+    monkeypatch.setattr(stream, "SHARDED_EXTRA", {"cpu": True, "runner": "sharded_fake:OracleRunner"})
+    stream.close_sharded()
+    Capture.log.clear()
+    OracleRunner.commits.clear()
+    try:
+        stream.foreach_batch_func(frames[0], 0)
+        stream.foreach_batch_func(frames[1], 1)
+        # the writes of batch 2 fail: nothing is committed; Spark re-runs epoch 2 and the same statements are written
+        # without a second merge (the oracle's state would double-count the batch)
+        Capture.fail = True
+        with pytest.raises(IOError):
+            stream.foreach_batch_func(frames[2], 2)
+        Capture.fail = False
+        res = stream.foreach_batch_func(frames[2], 2)
+    finally:
+        Capture.fail = False
+        stream.close_sharded()
+    written = [c for c in Capture.log if c["tiles"] or c["positions_latest"]]
+    assert len(written) == 3
+    for e in range(3):
+        for coll in ("tiles", "positions_latest"):
+            assert sorted(written[e][coll]) == exp[e][coll], (e, coll)
+    assert len(exp[2]["tiles"]) > 100 and res.n_tiles == len(exp[2]["tiles"])
+    # (rank 0's commits are recorded here; the worker's in its own process) epochs 0, 1 and 2 once, after the writes
+    assert OracleRunner.commits == [(0, 0), (0, 1), (0, 2)]
