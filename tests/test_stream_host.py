@@ -544,8 +544,8 @@ def test_failed_writes_and_replays_do_not_merge_twice(tmp_path, monkeypatch, che
             return dict(epoch_id=self.epochs[-1] if self.epochs and isinstance(self.epochs[-1], int) else -1, n_keys=0,
                         watermark_ms=0, prev_watermark_ms=0, tile_us=300_000_000, watermark_delay_ms=600_000, h3_res=8)
 
-        def save_state(self, path):
-            eng_mod.save_state_file(path, self._info(), np.zeros(0, STATE_REC_DTYPE))
+        def export_state(self):
+            return self._info(), np.zeros(0, STATE_REC_DTYPE)
 
         def export_state_delta(self):
             return self._info(), np.zeros(0, STATE_REC_DTYPE)
