@@ -367,7 +367,8 @@ int hm_selftest_cells_to_boundary_host(const uint64_t *cells, int64_t n, double 
  * records merged (direct path: aggregated rows; table mode: ~ distinct keys; stage API: the records this rank
  * received as owner), [2] tiles emitted, [3] 1 if table mode ran, [4] table mode: aggregates evicted from k_agg's
  * LDS tables into its buckets, [5] stage API: tile records this rank sent, [6] device + pinned-host allocations and
- * [7] frees the context made since hm_create (steady-state batches make none: tests/test_gpu_parity.py). */
+ * [7] frees the context made since hm_create (steady-state batches make none: tests/test_gpu_parity.py), [8] 1 if the
+ * direct path's rows were binned by the ingest itself (no separate partition pass). */
 int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n);
 /* Version of the persistent tile state: incremented when a batch starts merging into it (hm_process_batch,
  * hm_stage_merge, growth).  A call that failed without changing it left the state as it was (-1: ctx NULL). */

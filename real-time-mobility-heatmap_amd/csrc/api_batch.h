@@ -49,9 +49,10 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     for (auto &e : ctx->ev)
         if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     if (upload_tables() != hipSuccess) { ctx->err = "tables"; return fail("create"); }
-    {
+    for (int variant = 0; variant < 2; variant++) {
+        const void *kern = variant ? (const void *)k_ingest<true> : (const void *)k_ingest<false>;
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)k_ingest, IG_THREADS, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, IG_THREADS, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) {
             ctx->err = "occupancy query";
             return fail("create");
@@ -60,15 +61,18 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         // boundaries: SGPR counts 81-112); k_ingest is persistent, so an extra block per CU would only run once
         // a resident one finished.  Bound it by the LDS each block takes.
         hipFuncAttributes fa{};
-        if (hipFuncGetAttributes(&fa, (const void *)k_ingest) == hipSuccess && fa.sharedSizeBytes > 0)
+        if (hipFuncGetAttributes(&fa, kern) == hipSuccess && fa.sharedSizeBytes > 0)
             per_cu = std::min<int>(per_cu, (int)(163840 / fa.sharedSizeBytes));
         if (getenv("MOBHEAT_DEBUG"))
-            fprintf(stderr, "mobheat: k_ingest %d blocks/CU x %d CUs (LDS %zu B)\n", per_cu, cus, fa.sharedSizeBytes);
-        ctx->ingest_grid = std::max(1, per_cu) * std::max(1, cus);
+            fprintf(stderr, "mobheat: k_ingest<%d> %d blocks/CU x %d CUs (LDS %zu B, %d VGPRs)\n", variant, per_cu, cus,
+                    fa.sharedSizeBytes, fa.numRegs);
+        (variant ? ctx->ingest_grid_bin : ctx->ingest_grid) = std::max(1, per_cu) * std::max(1, cus);
         ctx->n_cus = std::max(1, cus);
     }
-    // MOBHEAT_INGEST_MODE=direct|table pins the aggregation path (tests); default: adaptive
-    if (const char *m = getenv("MOBHEAT_INGEST_MODE")) ctx->ingest_mode = !strcmp(m, "direct") ? 1 : !strcmp(m, "table") ? 2 : 0;
+    // MOBHEAT_INGEST_MODE=direct|table|binned pins the aggregation path (tests): the direct path with its partition
+    // pass, table mode, or the direct path binned in k_ingest at any batch size; default: adaptive
+    if (const char *m = getenv("MOBHEAT_INGEST_MODE"))
+        ctx->ingest_mode = !strcmp(m, "direct") ? 1 : !strcmp(m, "table") ? 2 : !strcmp(m, "binned") ? 3 : 0;
     if (const char *m = getenv("MOBHEAT_MERGE_GRID")) ctx->merge_grid = std::max(0, atoi(m));
     // the registry, its census and the batch statistics side by side (one reset, one readback after k_ingest)
     if (hipMalloc(&ctx->d_wreg, REG_BLOCK_BYTES) != hipSuccess || !(ctx->d_wcount = ctx->d_wreg + WREG_SLOTS + 1) ||
@@ -82,7 +86,8 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         ctx->err = "window registry alloc";
         return fail("create");
     }
-    if (hipMalloc(&ctx->d_scratch, 256 * 8) != hipSuccess || hipHostMalloc(&ctx->h_scratch, 256 * 8) != hipSuccess) {
+    if (hipMalloc(&ctx->d_scratch, 256 * 8) != hipSuccess || hipHostMalloc(&ctx->h_scratch, 256 * 8) != hipSuccess ||
+        hipHostMalloc(&ctx->h_bincur, (RP_BINS + 1) * 4, hipHostMallocDefault) != hipSuccess) {
         ctx->err = "stats alloc";
         return fail("create");
     }
@@ -150,7 +155,7 @@ void hm_destroy(hm_ctx *ctx) {
                       &ctx->rp_btot, &ctx->rp_boff,
                       &ctx->s_cell, &ctx->s_ws, &ctx->s_cnt, &ctx->s_sp, &ctx->s_spn, &ctx->s_lon, &ctx->s_lat, &ctx->bin_cnt, &ctx->bin_off, &ctx->dfused.used, &ctx->dfull.used, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
                       &ctx->o_lon, &ctx->o_lat, &ctx->td_sizes, &ctx->td_off, &ctx->td_btot, &ctx->td_boff, &ctx->td_bytes,
-                      &ctx->td_params, &ctx->gapbuf, &ctx->keys, &ctx->agg_bucket, &ctx->agg_cursor,
+                      &ctx->td_params, &ctx->gapbuf, &ctx->keys, &ctx->bin_cur, &ctx->agg_bucket, &ctx->agg_cursor,
                       &ctx->jd_bytes, &ctx->jd_offs, &ctx->jd_scratch, &ctx->jd_lat, &ctx->jd_lon, &ctx->jd_ts, &ctx->jd_speed,
                       &ctx->jd_sv, &ctx->jd_rv, &ctx->jd_vkey, &ctx->jd_poff, &ctx->jd_plen, &ctx->jd_voff, &ctx->jd_vlen,
                       &ctx->lb_set, &ctx->lb_list};
@@ -185,6 +190,7 @@ void hm_destroy(hm_ctx *ctx) {
         if (p) (void)hipHostFree(p);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->h_scratch) (void)hipHostFree(ctx->h_scratch);
+    if (ctx->h_bincur) (void)hipHostFree(ctx->h_bincur);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto &e : ctx->h2d_ev)
@@ -215,6 +221,7 @@ int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n) {
     for (int i = 0; i < n && i < 6; i++) c[i] = ctx->last_counts[i];
     if (n > 6) c[6] = ctx->n_allocs;
     if (n > 7) c[7] = ctx->n_frees;
+    if (n > 8) c[8] = ctx->last_binned;
     return HM_OK;
 }
 
@@ -240,7 +247,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     I.n = in->n;
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
     // 2. snap + window registry + event keys
-    if ((rc = phase_local(ctx, I, late_wm))) return rc;
+    if ((rc = phase_local(ctx, I, late_wm, true))) return rc;
     DevStats s1 = *ctx->h_st;
     const int64_t n_agg = (int64_t)s1.n_valid - (int64_t)s1.n_late;
     // the aggregation path of this batch (table mode: two LDS passes first; direct: every row a record)
@@ -296,6 +303,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     ctx->last_counts[3] = table ? 1 : 0;
     ctx->last_counts[4] = table ? ctx->table_evicted : 0;
     ctx->last_counts[5] = 0;
+    ctx->last_binned = !table && ctx->binned ? 1 : 0;
     // the next batch's aggregation path is chosen from this one's cardinality
     if (n_agg >= (int64_t(1) << 16)) {
         ctx->prev_agg_rows = n_agg;

@@ -280,6 +280,7 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, const void *payload_r
     ctx->last_counts[3] = ctx->stage_table ? 1 : 0;
     ctx->last_counts[4] = ctx->stage_table ? ctx->table_evicted : 0;
     ctx->last_counts[5] = ctx->stage_sent;
+    ctx->last_binned = 0;
     if (ctx->stage_agg_rows >= (int64_t(1) << 16)) {   // this rank's rows and owned keys (summed over ranks next batch)
         ctx->prev_agg_rows = ctx->stage_agg_rows;
         ctx->prev_keys = (int64_t)s2.n_touched;

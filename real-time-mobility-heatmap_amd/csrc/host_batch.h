@@ -3,18 +3,48 @@
 #pragma once
 
 // ---- batch phases shared by the single-GPU and stage paths ----
-// k_ingest + k_ingest_exact: flags, event keys, the window registry and its census, dedup max, batch statistics
-static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
+// Fused binning (k_ingest<true>) for a direct-path batch of at least BIN_MIN_ROWS rows: the last batch's numbers did
+// not ask for table mode (the choice is made before the ingest here; a key sample that then shows heavy hitters still
+// switches the batch to table mode, the binned records unused).  MOBHEAT_INGEST_MODE=direct pins the separate
+// partition, =binned the fused one at any size.
+constexpr int64_t BIN_MIN_ROWS = int64_t(1) << 22;
+static bool prev_says_table(const hm_ctx *ctx) {
+    return ctx->prev_keys > 0 && ctx->prev_keys <= (int64_t)AG_BINS * (AG_SLOTS / 2) && ctx->prev_agg_rows >= 8 * ctx->prev_keys;
+}
+static bool choose_binned(const hm_ctx *ctx, int64_t n) {
+    if (ctx->ingest_mode) return ctx->ingest_mode == 3;
+    return n >= BIN_MIN_ROWS && !prev_says_table(ctx);
+}
+// records per bin slab for n rows: the rows spread over the RP_BINS bins by a hash (binomial counts, ~sqrt(n / RP_BINS)
+// wide), so the mean + 25% + 256 overflows only on skewed keys (then the batch re-partitions from its keys)
+// (clustered keys -- a key's rows share its bin -- widen that; the last binned batch's fullest bin / mean, `skew`, with
+// 10% room, covers a stream whose clustering is steady)
+static unsigned slab_cap_for(int64_t n, double skew) {
+    const int64_t m = (n + RP_BINS - 1) / RP_BINS;
+    const int64_t c = std::max<int64_t>(m + m / 4 + 256, (int64_t)(skew * 1.1 * (double)m) + 256);
+    return (unsigned)std::min<int64_t>((c + 1) & ~int64_t(1), (int64_t)UINT32_MAX / 2);   // (even: 64-B aligned slabs)
+}
+
+// k_ingest + k_ingest_exact: flags, event keys, the window registry and its census, dedup max, batch statistics;
+// allow_bin: the batch may bin its rows in k_ingest (hm_process_batch; not the stage API)
+static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool allow_bin = false) {
     int64_t n = I.n;
     int rc;
     if ((rc = ensure(ctx, ctx->flags, n)) || (rc = ensure(ctx, ctx->win, n)) || (rc = ensure(ctx, ctx->rows, n * 8)) ||
         (rc = ensure(ctx, ctx->keys, n * 8)) || (rc = ensure(ctx, ctx->slow, n * sizeof(unsigned int))))
         return rc;
     if ((rc = dedup_prepare(ctx, ctx->dfused, dedup_fused_keys(ctx, n), true))) return rc;
+    const bool bin = allow_bin && n > 0 && choose_binned(ctx, n);
+    ctx->slab_cap = bin ? slab_cap_for(n, ctx->bin_skew) : 0;
+    ctx->binned = false;
+    if ((rc = ensure(ctx, ctx->bin_cur, (RP_BINS + 1) * 4))) return rc;
+    // (+ 64 slack records: k_ev_scatter_rec's, when a slab overflows and the batch is re-partitioned)
+    if (bin && (rc = ensure(ctx, ctx->parts_sorted, ((size_t)RP_BINS * ctx->slab_cap + 64) * sizeof(EventRec)))) return rc;
     {
         const int nw = 2 * (WREG_SLOTS + 1);   // d_wreg and d_wcount: one allocation (hm_create)
         hipLaunchKernelGGL(k_batch_reset, dim3((nw + 255) / 256), dim3(256), 0, ctx->stream, (unsigned long long *)ctx->d_st,
-                           ctx->d_scratch + SLOW_WORD, ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, nw);
+                           ctx->d_scratch + SLOW_WORD, ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, nw, (unsigned *)ctx->bin_cur.p,
+                           RP_BINS + 1);
         HIPCHK(ctx, hipGetLastError());
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
@@ -37,16 +67,20 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
                 HIPCHK(ctx, hipEventRecord(ctx->h2d_ev[c], ctx->copy_stream));
                 HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->h2d_ev[c], 0));
             }
-            const int blocks = (int)std::min<int64_t>((b - a + IG_THREADS - 1) / IG_THREADS, ctx->ingest_grid);
-            hipLaunchKernelGGL(k_ingest, dim3(blocks), dim3(IG_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.vk, a, b,
+            const int blocks = (int)std::min<int64_t>((b - a + IG_THREADS - 1) / IG_THREADS, bin ? ctx->ingest_grid_bin : ctx->ingest_grid);
+            auto kern = bin ? k_ingest<true> : k_ingest<false>;
+            hipLaunchKernelGGL(kern, dim3(blocks), dim3(IG_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.vk, a, b,
                                ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
                                (uint64_t *)ctx->keys.p, ctx->dfused.tab, ctx->dfused.cap - 1, (unsigned int *)ctx->dfused.used.p,
                                ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
-                               ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st);
+                               ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st, I.sp, I.sv,
+                               (unsigned *)ctx->bin_cur.p, bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap);
         }
         ctx->n_h2d = 0;
         hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, ctx->cfg.h3_res,
-                           (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, (uint64_t *)ctx->keys.p);
+                           (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, (uint64_t *)ctx->keys.p, I.sp, I.sv,
+                           (const unsigned long long *)ctx->d_wreg, (unsigned *)ctx->bin_cur.p,
+                           bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap, ctx->d_st);
         hipLaunchKernelGGL(k_sample_heavy, dim3(1), dim3(HS_THREADS), 0, ctx->stream, (const uint64_t *)ctx->keys.p, n, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
         ctx->dfused.dirty = true;
@@ -54,10 +88,17 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms) {
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
     // the batch statistics and the registry with its census, read back together
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_wreg, ctx->d_wreg, REG_BLOCK_BYTES, hipMemcpyDeviceToHost, ctx->stream));   // (+ h_wcount, h_st)
+    if (bin) HIPCHK(ctx, hipMemcpyAsync(ctx->h_bincur, ctx->bin_cur.p, RP_BINS * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+    if (bin) {   // the fullest bin against the mean: the next batch's slab room
+        unsigned long long tot = 0, mx = 0;
+        for (int b = 0; b < RP_BINS; b++) { tot += ctx->h_bincur[b]; mx = std::max<unsigned long long>(mx, ctx->h_bincur[b]); }
+        if (tot) ctx->bin_skew = std::max(1.0, (double)mx * RP_BINS / (double)tot);
+    }
     if (ctx->h_st->win_overflow)
         return set_err(ctx, HM_E_OVERFLOW, "more than %d distinct windows in one micro-batch (%llu rows)", WREG_SLOTS,
                        ctx->h_st->win_overflow);
+    ctx->binned = bin && ctx->h_st->bin_overflow == 0;
     return HM_OK;
 }
 
@@ -68,7 +109,7 @@ static bool choose_table(const hm_ctx *ctx, int64_t n_agg, unsigned long long sa
     if (ctx->ingest_mode) return ctx->ingest_mode == 2;
     if (n_agg < (int64_t(1) << 16)) return false;
     if (sample_max_run >= (unsigned long long)(HS_SAMPLE / 256)) return true;
-    return ctx->prev_keys > 0 && ctx->prev_keys <= (int64_t)AG_BINS * (AG_SLOTS / 2) && ctx->prev_agg_rows >= 8 * ctx->prev_keys;
+    return prev_says_table(ctx);
 }
 
 // table mode: k_agg + k_bin_reduce -> one partial record per key of the batch (ctx->partials, count *n_parts),
@@ -227,12 +268,20 @@ static int merge_events(hm_ctx *ctx, const Inputs &I, int64_t n_rec) {
     if (n_rec == 0) return merge_nothing(ctx);
     std::vector<WinCount> census;
     census_of_registry(ctx, census);
-    if ((rc = gens_prepare(ctx, census)) || (rc = winfo_upload(ctx, true))) return rc;
+    // binned in k_ingest: every window's table gets 2^REGION_BITS regions (a row's bin is its region), and the bins'
+    // row offsets are the exclusive scan of their cursors -- no partition pass over the keys and columns
+    const bool binned = ctx->binned;
+    if ((rc = gens_prepare(ctx, census, binned ? REGION_BITS + REGION_MIN_BITS : 0)) || (rc = winfo_upload(ctx, true))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
-    int64_t ntiles;
-    if ((rc = ev_partition<EventRec>(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, nullptr, ntiles))) return rc;
+    int64_t ntiles = 1;
+    if (binned) {
+        if ((rc = ensure(ctx, ctx->rp_O, (RP_BINS + 1) * 8))) return rc;
+        if ((rc = scan_counts(ctx, (const unsigned *)ctx->bin_cur.p, RP_BINS + 1, (unsigned long long *)ctx->rp_O.p))) return rc;
+    } else if ((rc = ev_partition<EventRec>(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, nullptr, ntiles))) {
+        return rc;
+    }
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
-    if ((rc = merge_sorted<EventRec>(ctx, I.n, ntiles))) return rc;
+    if ((rc = merge_sorted<EventRec>(ctx, I.n, ntiles, binned ? ctx->slab_cap : 0))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
     if ((rc = rows_densify(ctx, ntiles))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));

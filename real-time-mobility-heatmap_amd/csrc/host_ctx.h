@@ -84,6 +84,8 @@ struct hm_ctx {
     int64_t dedup_seen = 0;
     int64_t n_partials_merged = 0;   // partial records of the last merge (hm_batch_out.n_partials)
     int ingest_grid = 0;             // k_ingest's persistent grid: resident workgroups per CU x CUs
+    int ingest_grid_bin = 0;         // the same for k_ingest<true> (fused binning)
+    int64_t last_binned = 0;         // hm_last_counts [8]: the last batch was binned in k_ingest
     int n_cus = 0;
     // aggregation path: direct (event records -> partition -> merge) or table (k_agg + k_bin_reduce, low
     // cardinality); MOBHEAT_INGEST_MODE pins one (0 adaptive, 1 direct, 2 table)
@@ -110,6 +112,13 @@ struct hm_ctx {
     Dict jd_prov, jd_veh;
     DevBuf lb_set, lb_list;   // hm_last_latest_buckets
     DevBuf keys;                     // k_ingest's event key per row (kernels.h ekey)
+    // k_ingest's fused binning (large direct-path batches): the bins' cursors (RP_BINS + 1 u32: the last stays 0, so
+    // that their exclusive scan ends with the total) and the slab capacity; the slabs are parts_sorted
+    DevBuf bin_cur;
+    unsigned slab_cap = 0;           // records per bin slab of this batch (0: not binned in k_ingest)
+    unsigned *h_bincur = nullptr;    // the cursors read back (pinned): the fullest bin sizes the next batch's slabs
+    double bin_skew = 1.0;           // the last binned batch's fullest bin / mean bin
+    bool binned = false;             // this batch's rows are in their bins (k_ingest<true>, no slab overflowed)
     unsigned long long *d_wreg = nullptr, *h_wreg = nullptr;     // the batch's window registry (WREG_SLOTS wenc)
     unsigned long long *d_wcount = nullptr, *h_wcount = nullptr; // aggregated rows per registry slot (census)
     WInfo *d_winfo = nullptr, *h_winfo = nullptr;   // per registry slot: window parameters of the direct path
@@ -497,7 +506,7 @@ static unsigned seq32(const hm_ctx *ctx) { return (unsigned)(ctx->seq % 0xffffff
 
 // merge the partitioned records (ctx->parts_sorted) of n_rows staging rows
 template <typename Rec>
-static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles) {
+static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t slab = 0) {
     constexpr bool rehash = std::is_same<Rec, GrowRec>::value;
     int rc;
     if ((rc = ensure(ctx, ctx->bin_cnt, RP_BINS * 4)) || (rc = ensure(ctx, ctx->bin_off, RP_BINS * 8)))
@@ -529,7 +538,7 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles) {
         resident = need <= tag_bytes && nwin <= MO_RES_MAX && ctx->n_glist <= GC_MAX;
     }
     auto launch = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(MO_THREADS), tag_bytes, ctx->stream, (const Rec *)ctx->parts_sorted.p, n_rows,
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(MO_THREADS), tag_bytes, ctx->stream, (const Rec *)ctx->parts_sorted.p, slab,
                            (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
                            ctx->n_glist, (const WInfo *)ctx->d_winfo, cell_hi_of(ctx->cfg.h3_res), seq32(ctx), staged_rows(ctx),
                            (unsigned *)ctx->bin_cnt.p, ctx->d_st, tag_bytes);
@@ -620,7 +629,9 @@ static int winfo_upload(hm_ctx *ctx, bool with_bins) {
 // Give every window of the census a table large enough for its keys after this batch (new windows: a new table;
 // windows that would pass load 1/2: a larger table, filled by dumping the old one and merging the dump in rehash
 // mode); upload the window map.
-static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census) {
+// min_log2: every window's table at least 2^min_log2 slots (fused binning: 2^(REGION_BITS + REGION_MIN_BITS), so that
+// each has 2^REGION_BITS regions and a row's bin, chosen before the census, is its region)
+static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census, int min_log2 = 0) {
     std::vector<hm_ctx::Gen> old;   // tables being replaced by larger ones
     int rc;
     for (auto &g : ctx->gens) g.batch_parts = 0;
@@ -631,14 +642,14 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census) {
         int L;
         unsigned rb;
         if (it == ctx->gens.end()) {
-            gen_geometry(ctx, c, c, 0, L, rb);
+            gen_geometry(ctx, c, c, min_log2, L, rb);
             TileSlot *t = nullptr;
             if ((rc = table_acquire(ctx, L, rb, &t))) return rc;
             ctx->gens.push_back({w.wenc, t, L, rb, 0, c});
             continue;
         }
-        if (std::min(it->keys + c, h3_cells_at(ctx->cfg.h3_res)) * 2 > (int64_t(1) << it->log2cap)) {
-            gen_geometry(ctx, it->keys + c, c, it->log2cap + 1, L, rb);
+        if (std::min(it->keys + c, h3_cells_at(ctx->cfg.h3_res)) * 2 > (int64_t(1) << it->log2cap) || it->log2cap < min_log2) {
+            gen_geometry(ctx, it->keys + c, c, std::max(it->log2cap + 1, min_log2), L, rb);
             TileSlot *t = nullptr;
             if ((rc = table_acquire(ctx, L, rb, &t))) return rc;
             old.push_back(*it);

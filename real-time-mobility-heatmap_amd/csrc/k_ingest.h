@@ -63,13 +63,20 @@ __device__ __forceinline__ void wave_count_slots(bool pred, int slot, unsigned *
     }
 }
 
+// kBin: the direct path's (window, region) binning fused in (hm_process_batch, large batches): every aggregated row's
+// 32-B EventRec goes straight to its bin's slab -- bin = the key hash's region field (every window of such a batch
+// has 2^REGION_BITS regions, so region = bin, kernels.h) at slab b * slab_cap + a returned atomic on the bin's
+// cursor -- instead of a later histogram + scatter pass over the keys and columns.  A bin past slab_cap counts in
+// DevStats.bin_overflow and the host partitions the batch from its keys instead.
+template <bool kBin>
 __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     const double *__restrict__ lat, const double *__restrict__ lon, const int64_t *__restrict__ ts,
     const uint8_t *__restrict__ row_valid, const uint64_t *__restrict__ vkey, int64_t i_begin, int64_t n, int res, FloorDiv wdiv,
     int64_t late_end_us, uint8_t *__restrict__ flags_out, uint64_t *__restrict__ keys_out, DedupSlot *dtab,
     unsigned long long dmask, unsigned int *dused, unsigned long long *n_dused, unsigned int *__restrict__ slow,
     unsigned long long *n_slow, unsigned long long *dgiveup, unsigned long long *wreg, unsigned long long *wcount,
-    DevStats *st) {
+    DevStats *st, const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid, unsigned *__restrict__ bin_cur,
+    EventRec *__restrict__ slabs, unsigned slab_cap) {
     __shared__ WinCacheL WC;
     __shared__ double Fc[20][3], Fu[20][2][3];   // the fast path's per-face tables (res parity): LDS reads
     __shared__ unsigned dskip;                    // the fused dedup has given up (*dgiveup) -- skip it
@@ -87,7 +94,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     const int64_t tile_us = wdiv.d;
     // per-thread counters in 32 bits (a thread sees at most n / gstride < 2^32 rows): fewer registers live across
     // the cell computation, whose peak spilled the prefetched columns
-    unsigned nvalid = 0, nlate = 0, bad = 0, wover = 0;
+    unsigned nvalid = 0, nlate = 0, bad = 0, wover = 0, binover = 0;
     tmax_l[threadIdx.x] = INT64_MIN;
     bool dretry = false;
     int round = 0;
@@ -116,6 +123,16 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         // waited for every prefetched load mid-round)
         const int64_t t = in ? __builtin_nontemporal_load(&ts[i]) : 0;
         (void)nt;
+        // kBin: the row's speed the same way (first used after the cell); absent columns read one-element constants
+        uint64_t spb = 0;
+        uint8_t svb = 0;
+        if constexpr (kBin) {
+            typedef __attribute__((address_space(1))) const uint64_t gcu64;
+            typedef __attribute__((address_space(1))) const uint8_t gcu8;
+            const int64_t j = in ? i : n - 1;
+            spb = __builtin_nontemporal_load((gcu64 *)(speed ? (const uint64_t *)&speed[j] : (const uint64_t *)&g_zero_double));
+            svb = __builtin_nontemporal_load((gcu8 *)(speed_valid ? &speed_valid[j] : speed ? &g_one_byte : &g_zero_byte));
+        }
         const unsigned long long v = nv;
         const bool rv = nrv != 0;
         {
@@ -144,9 +161,10 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         if (dd) d0 = dtab[dh0];
         uint8_t fl = 0;
         int widx = -1, wslot = -1;
+        int64_t ws = 0;
         if (ok) {
             const int64_t wq = floor_div(t, wdiv);   // tumbling window: floor(t / tile) (Spark TimeWindowing)
-            const int64_t ws = wq * tile_us;
+            ws = wq * tile_us;
             const bool late = (ws + tile_us) <= late_end_us;
             fl = late ? (F_VALID | F_LATE) : (F_VALID | F_AGG);
             nvalid++;
@@ -182,9 +200,28 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
             }
         }
         const bool agg = (fl & F_AGG) != 0;
+        const uint64_t key = agg ? ekey_make(exc ? 0 : cell, (unsigned)widx) : 0;
         if (in) {
             flags_out[i] = fl | (cand ? F_CAND : 0);
-            keys_out[i] = agg ? ekey_make(exc ? 0 : cell, (unsigned)widx) : 0;
+            keys_out[i] = key;
+        }
+        if constexpr (kBin) {
+            // the row's EventRec into its bin (exceptions: k_ingest_exact, once their cell is known)
+            if (agg && !exc) {
+                const uint64_t h = mix64(cell ^ window_inner(ws));
+                const unsigned b = region_field(h);
+                const unsigned p = atomicAdd(&bin_cur[b], 1u);
+                if (p < slab_cap) {
+                    const uint64_t sp = svb == 0 ? SPEED_NULL_BITS
+                                                 : __builtin_bit_cast(double, spb) != __builtin_bit_cast(double, spb) ? CANON_NAN_BITS : spb;
+                    const uint64_t lab = __builtin_bit_cast(uint64_t, la), lob = __builtin_bit_cast(uint64_t, lo);
+                    uint4 *d = (uint4 *)&slabs[(size_t)b * slab_cap + p];
+                    st_g16(d, make_uint4((unsigned)key, (unsigned)(key >> 32), (unsigned)sp, (unsigned)(sp >> 32)));
+                    st_g16(d + 1, make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32)));
+                } else {
+                    binover++;
+                }
+            }
         }
         const unsigned long long pos = wave_append(claimed, n_dused);
         if (claimed) dused[pos] = (unsigned int)dh;
@@ -201,6 +238,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         if (WC.cnt[q]) atomicAdd(&wcount[(WC.e[q] & 0xfff) - 1], (unsigned long long)WC.cnt[q]);
     const unsigned long long wvalid = wave_sum((unsigned long long)nvalid), wlate = wave_sum((unsigned long long)nlate);
     const unsigned long long wbad = wave_sum((unsigned long long)bad), wwover = wave_sum((unsigned long long)wover);
+    const unsigned long long wbinover = kBin ? wave_sum((unsigned long long)binover) : 0ull;
     const long long tmax = wave_max(tmax_l[threadIdx.x]);
     const unsigned long long rt = __ballot(dretry);
     if (lane_id() == 0) {
@@ -210,18 +248,38 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         if (wbad) atomicAdd(&st->bad_vkey, wbad);
         if (wwover) atomicAdd(&st->win_overflow, wwover);
         if (rt) atomicAdd(&st->dedup_retry, 1ull);
+        if (wbinover) atomicAdd(&st->bin_overflow, wbinover);
     }
 }
 
 // exceptions of k_ingest's fast path: upstream's exact sequence; the cell bits go into the row's key (k_ingest
-// wrote its window slot)
+// wrote its window slot); with slabs (k_ingest<true>) the row's EventRec into its bin as k_ingest does
 __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__ lat, const double *__restrict__ lon, int res,
                                                       const unsigned int *__restrict__ slow, const unsigned long long *n_slow,
-                                                      uint64_t *__restrict__ keys) {
+                                                      uint64_t *__restrict__ keys, const double *__restrict__ speed,
+                                                      const uint8_t *__restrict__ speed_valid, const unsigned long long *wreg,
+                                                      unsigned *__restrict__ bin_cur, EventRec *__restrict__ slabs, unsigned slab_cap,
+                                                      DevStats *st) {
     const int64_t m = (int64_t)*n_slow;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (int64_t)gridDim.x * blockDim.x) {
         const unsigned i = slow[q];
-        keys[i] |= latLngToCellDeg(lat[i], lon[i], res, c_tab) & CELL_LO;
+        const uint64_t cell = latLngToCellDeg(lat[i], lon[i], res, c_tab);
+        const uint64_t key = keys[i] | (cell & CELL_LO);
+        keys[i] = key;
+        if (slabs) {
+            const uint64_t h = mix64(cell ^ window_inner(wdec(wreg[ekey_widx(key)])));
+            const unsigned b = region_field(h);
+            const unsigned p = atomicAdd(&bin_cur[b], 1u);
+            if (p >= slab_cap) { atomicAdd(&st->bin_overflow, 1ull); continue; }
+            const bool sv = speed && (!speed_valid || speed_valid[i]);
+            const double sp = sv ? speed[i] : 0.0;
+            EventRec r;
+            r.key = key;
+            r.speed = __builtin_bit_cast(double, !sv ? SPEED_NULL_BITS : sp != sp ? CANON_NAN_BITS : __builtin_bit_cast(uint64_t, sp));
+            r.lat = lat[i];
+            r.lon = lon[i];
+            slabs[(size_t)b * slab_cap + p] = r;
+        }
     }
 }
 

@@ -235,7 +235,7 @@ struct MLine {
 // which carries less machinery per probed slot (bench leg: 3.72-3.81 vs 4.03-4.11 ms; state-read leg: 6.86-6.89 vs
 // 6.22-6.30 ms, profiles/r3/r3ab9/)
 template <typename Rec, bool kResident = false, bool kCoop = false>
-__global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_merge_owned(const Rec *__restrict__ parts, int64_t n,
+__global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_merge_owned(const Rec *__restrict__ parts, int64_t slab,
                                                             const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
                                                             GenDesc *gm, const GenDesc *glist, int n_glist,
                                                             const WInfo *__restrict__ winfo, uint64_t cell_hi,
@@ -592,7 +592,10 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         };
         // software pipeline: the next chunk's record is loaded while this chunk is merged
         Rec nxt;
-        if (b0 + t < b1) nxt = ld_stream(parts + b0 + t);
+        // the bin's records: [b0, b1) of the partitioned array, or (slab != 0: k_ingest's fused binning) the first
+        // b1 - b0 records of the bin's slab; either way row k of the bin goes to b0 + k
+        const Rec *__restrict__ bp = slab ? parts + ((int64_t)bin * slab - b0) : parts;
+        if (b0 + t < b1) nxt = ld_stream(bp + b0 + t);
         for (int64_t c0 = b0; c0 < b1; c0 += MO_THREADS) {
             // 1. stage this chunk's records in LDS
             const int64_t i = c0 + t;
@@ -600,7 +603,7 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             MRec p{};
             if (has) p = mrec_of(nxt, winfo, cell_hi);   // (the window parameters from an LDS image cost the state-read
                                                          // leg's merge ~1 ms, profiles/r3/r3ab11: a global load)
-            if (i + MO_THREADS < b1) nxt = ld_stream(parts + i + MO_THREADS);
+            if (i + MO_THREADS < b1) nxt = ld_stream(bp + i + MO_THREADS);
             if (has) {
                 S.sc[t] = p.cell;
                 S.sh[t] = p.hk;
@@ -718,10 +721,11 @@ __global__ __launch_bounds__(256) void k_zero16(uint4 *__restrict__ p, int64_t n
 // at their identities), the fast-path exception and dedup give-up words, the window registry and its census
 __global__ __launch_bounds__(256) void k_batch_reset(unsigned long long *__restrict__ st, unsigned long long *__restrict__ slow_word,
                                                      unsigned long long *__restrict__ giveup_word, unsigned long long *__restrict__ wreg2,
-                                                     int n_wreg2) {
+                                                     int n_wreg2, unsigned *__restrict__ bin_cur, int n_bin) {
     static_assert(sizeof(DevStats) % 8 == 0 && offsetof(DevStats, min_wstart) == offsetof(DevStats, max_ts_ms) + 8, "DevStats");
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n_wreg2) wreg2[i] = 0;
+    if (i < n_bin) bin_cur[i] = 0;
     if (i < (int)(sizeof(DevStats) / 8)) {
         const int mx = (int)(offsetof(DevStats, max_ts_ms) / 8);
         st[i] = i == mx ? (unsigned long long)INT64_MIN : i == mx + 1 ? (unsigned long long)INT64_MAX : 0ull;

@@ -197,6 +197,7 @@ struct DevStats {
     unsigned long long agg_spill;   // table mode: aggregates that did not fit a bucket (sent as partial records)
     unsigned long long n_evicted;   // table mode: aggregates k_agg evicted into the buckets
     unsigned long long sample_max_run;   // k_sample_heavy: occurrences of the most frequent key in a key sample
+    unsigned long long bin_overflow;     // k_ingest<true>: rows whose bin slab was full (the batch re-partitions)
 };
 
 HM_HD uint64_t mix64(uint64_t x) {

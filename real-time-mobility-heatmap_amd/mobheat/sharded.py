@@ -23,8 +23,11 @@ A failure on any rank fails the batch (every rank leaves at the same collective,
 after a merge began resets every rank's state, which the replayed epoch restores from the checkpoints.
 """
 import atexit
+import datetime
 import os
 import socket
+import sys
+import time
 import traceback
 
 import numpy as np
@@ -33,6 +36,16 @@ from . import _lib
 from ._lib import HM_MEM_DEVICE, HM_MEM_HOST
 
 COLS = ("lat", "lon", "ts_us", "speed", "speed_valid", "vkey", "row_valid")
+# MOBHEAT_SHARDED_TRACE=1: every rank's protocol steps to stderr (a hung rank names its step)
+_TRACE = os.environ.get("MOBHEAT_SHARDED_TRACE") == "1"
+# seconds a rank waits for its peers at a rendezvous or a reply before the batch fails (a dead rank must not hang the
+# stream: a worker that died shows up as a timeout here)
+TIMEOUT_S = float(os.environ.get("MOBHEAT_SHARDED_TIMEOUT", "600"))
+
+
+def _trace(rank, msg):
+    if _TRACE:
+        print(f"[mobheat r{rank} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 _DT = {"lat": np.float64, "lon": np.float64, "ts_us": np.int64, "speed": np.float64, "speed_valid": np.uint8,
        "vkey": np.uint64, "row_valid": np.uint8}
 
@@ -161,7 +174,9 @@ class RankRunner:
         for k in COLS:
             a = views[k]
             batch[k] = a.ctypes.data + lo * a.itemsize if a.size else None
+        _trace(self.rank, f"batch {epoch}: {n} rows")
         out = self.sharded.process_batch(epoch, batch, out_memory=HM_MEM_DEVICE)
+        _trace(self.rank, f"batch {epoch}: merged, {int(out.n_tiles)} tiles, {int(out.n_latest)} latest rows")
         c = self.cfg
         tiles = eng.encode_tile_updates(c["city"], c["ttl_min"])
         positions = None
@@ -203,7 +218,10 @@ def _init_group(rank, world, port, backend, device):
     if device is not None:
         torch.cuda.set_device(device)
     kw = {"device_id": torch.device("cuda", device)} if backend == "nccl" else {}
-    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world, **kw)
+    _trace(rank, f"init_process_group {backend} port {port} device {device}")
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=TIMEOUT_S), **kw)
+    _trace(rank, "process group up")
 
 
 def _worker_main(rank, world, port, conn, cfg):
@@ -221,6 +239,7 @@ def _worker_main(rank, world, port, conn, cfg):
     while True:
         msg = conn.recv()
         op = msg[0]
+        _trace(rank, f"op {op}")
         try:
             if op == "batch":
                 _, epoch, name, layout, lo, hi, restore = msg
@@ -280,8 +299,8 @@ class ShardedStream:
             self.conns.append(parent)
             self.procs.append(p)
         _init_group(0, self.world, port, cfg["backend"], cfg["devices"][0])
-        for c in self.conns:
-            m = c.recv()
+        for r, c in enumerate(self.conns, start=1):
+            m = self._recv(c, r)
             if m[0] != "ready":
                 raise RuntimeError(f"mobheat worker failed to start: {m[1]}\n{m[2]}")
         self.runner = _runner_class(cfg)(0, self.world, cfg["devices"][0], cfg)
@@ -329,7 +348,7 @@ class ShardedStream:
             res0 = self.runner.run(int(epoch), views, bounds[0], bounds[1], self.restore)
         except Exception as e:
             err0 = e
-        replies = [c.recv() for c in self.conns]
+        replies = [self._recv(c, r) for r, c in enumerate(self.conns, start=1)]
         errs = [(0, err0)] if err0 is not None else []
         began = err0 is not None and getattr(self.runner, "began", False)
         for r, m in enumerate(replies, start=1):
@@ -362,7 +381,7 @@ class ShardedStream:
         except Exception as e:
             err = e
         for r, c in enumerate(self.conns, start=1):
-            m = c.recv()
+            m = self._recv(c, r)
             if m[0] != "ok" and err is None:
                 err = RuntimeError(f"rank {r} checkpoint: {m[1]}")
         if err is not None:
@@ -370,13 +389,24 @@ class ShardedStream:
         if self.cfg["checkpoint"] and self.runner.lineage is not None:
             self.runner.store.prune_other_worlds(self.runner.lineage)
 
+    def _recv(self, c, r):
+        """A worker's reply, or RuntimeError when it died or did not answer within TIMEOUT_S."""
+        p = self.procs[r - 1]
+        t0 = time.monotonic()
+        while not c.poll(1.0):
+            if not p.is_alive():
+                raise RuntimeError(f"mobheat worker rank {r} died (exit code {p.exitcode})")
+            if time.monotonic() - t0 > TIMEOUT_S:
+                raise RuntimeError(f"mobheat worker rank {r} did not answer within {TIMEOUT_S:.0f} s")
+        return c.recv()
+
     def reset(self):
         """Drop every rank's state (the next batch restores from the checkpoints)."""
         for c in self.conns:
             c.send(("reset",))
         self.runner.reset()
-        for c in self.conns:
-            c.recv()
+        for r, c in enumerate(self.conns, start=1):
+            self._recv(c, r)
         self.last = None
         self.restore = None
 

@@ -447,16 +447,18 @@ def test_window_tables_growth_many_windows_and_reuse():
     eng.close()
 
 
-@pytest.mark.parametrize("mode", ["direct", "table"])
+@pytest.mark.parametrize("mode", ["direct", "table", "binned"])
 def test_ingest_modes_parity(mode, monkeypatch):
-    """The two aggregation paths pinned (MOBHEAT_INGEST_MODE): direct (every aggregated row a 32-B record through
-    the partition and merge) and table (k_agg's LDS table with hot-key retention + k_bin_reduce, picked adaptively
-    for low-cardinality batches) give the oracle's results on a multi-batch stream with late rows, ties, nulls, an
-    empty batch, many windows and few hot keys."""
+    """The aggregation paths pinned (MOBHEAT_INGEST_MODE): direct (every aggregated row a 32-B record through the
+    partition and merge), binned (the same records written into their bins by k_ingest itself; a batch whose hot keys
+    overflow a bin's slab falls back to the partition) and table (k_agg's LDS table with hot-key retention +
+    k_bin_reduce, picked adaptively for low-cardinality batches) give the oracle's results on a multi-batch stream with
+    late rows, ties, nulls, an empty batch, many windows and few hot keys."""
     from mobheat import HeatmapEngine, synth
     from oracle.spark_oracle import SparkHeatmapOracle
     monkeypatch.setenv("MOBHEAT_INGEST_MODE", mode)
     rng = np.random.default_rng(31)
+    binned = []
     eng = HeatmapEngine(h3_res=10)
     ora = SparkHeatmapOracle(h3_res=10)
     minute = 60_000_000
@@ -471,17 +473,21 @@ def test_ingest_modes_parity(mode, monkeypatch):
                  vkey=rng.integers(0, 700, n).astype(np.uint64), row_valid=rng.random(n) > 0.01)
         res, exp = _run(eng, ora, b, epoch)
         assert_batch_equal(res, exp)
+        binned.append(eng.last_counts()["binned"])
+    if mode == "binned":   # (uniform batches binned by the ingest; the hot-key batches overflowed and re-partitioned)
+        assert binned == [True, False, False, True, True, False], binned
     eng.close()
 
 
-def test_direct_merge_keys_repeated_across_chunks(monkeypatch):
+@pytest.mark.parametrize("mode", ["direct", "binned"])
+def test_direct_merge_keys_repeated_across_chunks(mode, monkeypatch):
     """k_merge_owned with every key in several consecutive 512-record chunks of its bin (direct path forced: 1.2e7 rows
     over ~5e5 res-11 keys, ~1.5k rows per bin): a chunk's stores are only drained by the next chunk's full barrier, so
     a key the previous chunk wrote is deferred behind it (mobheat.hip: k_merge_owned step 4) -- counts and sums must
     still add up exactly; a second batch in the same window re-reads every key's state."""
     from mobheat import HeatmapEngine, synth
     from oracle.spark_oracle import SparkHeatmapOracle
-    monkeypatch.setenv("MOBHEAT_INGEST_MODE", "direct")
+    monkeypatch.setenv("MOBHEAT_INGEST_MODE", mode)
     rng = np.random.default_rng(77)
     eng = HeatmapEngine(h3_res=11)
     ora = SparkHeatmapOracle(h3_res=11)
