@@ -45,6 +45,9 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9
 #   direct path   ingest 42/event (lat, lon, ts, vkey 8 each + row_valid 1 read; flags 1 + event key 8 written)
 #                 partition 16/event (k_ev_hist and k_ev_scatter read the key) + 57/record (speed, speed_valid,
 #                           lat, lon read: 25; the 32-B EventRec written)
+#   binned        (the direct path's records written by k_ingest itself, hm_last_counts "binned") ingest 51/event (+ speed
+#                 and speed_valid read) + 32/record (the EventRec written into its bin); partition 0 (a scan of the
+#                 8192 bin counts)
 #                 merge 32/record read + 113/tile (64-B state line + 49-B row written) + 64/pre-existing key read
 #                 emit 98/gap (a 49-B row moved into a gap; gaps = R - T), dedup 20/event
 #   multi-GPU     send (the sender's partition by owner) 16/event + 57/sent record (speed, speed_valid, lat, lon
@@ -59,6 +62,8 @@ def stage_bytes(n, c, world=1):
     b = {"ingest": 42 * n, "dedup": 20 * n, "emit": 98 * max(R - T, 0), "send": 0}
     if c["table_mode"]:
         b.update(aggregate=41 * n + 48 * R, partition=160 * R, merge=64 * R + 113 * T + 64 * E)
+    elif c.get("binned"):
+        b.update(ingest=51 * n + 32 * R, aggregate=0, partition=0, merge=32 * R + 113 * T + 64 * E)
     elif world > 1:
         b.update(aggregate=0, send=16 * n + 57 * c["sent"], partition=80 * R, merge=32 * R + 113 * T + 64 * E)
     else:
@@ -286,6 +291,10 @@ def main():
         "config": {"workload": f"C2-shaped global batch: {n:,} events/step/GPU uniform on the sphere, 50k vehicles, "
                                f"15 min of event time (3 windows) per step, advancing 15 min per step; H3 res {args.res}",
                    "events_per_step_per_gpu": n, "h3_res": args.res, "parallelism": f"dp{world}",
+                   # the process group the exchange ran on, as torch.distributed reports it (None: one GPU, no exchange)
+                   "dist_backend": dist.get_backend() if world > 1 else None,
+                   "dist_world_size": dist.get_world_size() if world > 1 else 1,
+                   "binned_in_ingest": bool(c.get("binned")),
                    "tiles_emitted_last_step": c["tiles"], "partials_last_step": c["partials"],
                    "records_sent_last_step": c["sent"],
                    "table_mode": c["table_mode"]},

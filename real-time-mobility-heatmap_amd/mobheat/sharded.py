@@ -192,7 +192,9 @@ class RankRunner:
 
     def commit(self, epoch):
         if self.cfg["checkpoint"] and self.engine is not None:
-            self.store.save(epoch, self.engine, self.lineage, self.cfg["full_every"])
+            _trace(self.rank, f"checkpoint {epoch}")
+            kind = self.store.save(epoch, self.engine, self.lineage, self.cfg["full_every"])
+            _trace(self.rank, f"checkpoint {epoch}: {kind} written")
 
     def export_out(self, tiles, positions):
         """A worker's statements into its shared-memory region: (name, layout)."""
@@ -229,6 +231,9 @@ def _worker_main(rank, world, port, conn, cfg):
     ("commit", epoch), ("reset",), ("close",)."""
     import torch.distributed as dist
     device = cfg["devices"][rank]
+    if _TRACE:   # (a hung worker prints where it is)
+        import faulthandler
+        faulthandler.dump_traceback_later(100, repeat=True)
     try:
         _init_group(rank, world, port, cfg["backend"], device)
         runner = _runner_class(cfg)(rank, world, device, cfg)
@@ -257,11 +262,13 @@ def _worker_main(rank, world, port, conn, cfg):
             conn.send(("err", repr(e), traceback.format_exc(), type(e).__name__, getattr(runner, "began", False)))
     runner.reset()
     runner.out.close()
+    _trace(rank, "closing")
+    conn.send(("closed",))
     try:
         dist.destroy_process_group()
     except Exception:
         pass
-    conn.send(("closed",))
+    _trace(rank, "closed")
 
 
 def _free_port():
@@ -373,6 +380,7 @@ class ShardedStream:
     def commit(self, epoch):
         """Checkpoint every rank's state after the committed epoch (rank 0 last; then the files of an older world size
         are dropped once every rank of this one holds a snapshot)."""
+        _trace(0, f"commit {epoch}")
         for c in self.conns:
             c.send(("commit", int(epoch)))
         err = None
@@ -414,6 +422,7 @@ class ShardedStream:
         if self.closed:
             return
         self.closed = True
+        _trace(0, "close")
         import torch.distributed as dist
         for c in self.conns:
             try:
@@ -430,9 +439,11 @@ class ShardedStream:
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
+        _trace(0, "workers joined")
         try:
             dist.destroy_process_group()
         except Exception:
             pass
         self.inputs.close()
         self.runner.out.close()
+        _trace(0, "closed")

@@ -67,6 +67,8 @@ def _run(stream, frames, epochs):
     Capture.log.clear()
     for e in epochs:
         stream.foreach_batch_func(frames[e], e)
+        print(f"[test] epoch {e}: {len(Capture.log[-1]['tiles'])} tile statements, "
+              f"{len(Capture.log[-1]['positions_latest'])} positions", flush=True)
     return [dict(c) for c in Capture.log]
 
 

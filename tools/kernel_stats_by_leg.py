@@ -18,7 +18,8 @@ def main(path, steps_a):
     leg = 0
     for r in rows:
         name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "")
-        if name == "k_ingest":
+        base = re.sub(r"<.*", "", name)   # (k_ingest<true> / <false>: one kernel for the leg boundary)
+        if base == "k_ingest":
             ingests += 1
             if ingests == steps_a + 1:
                 leg = 1
