@@ -131,7 +131,9 @@ class RankRunner:
         self.sharded = None
         self.lineage = None
         self.store = StateCheckpoints(os.path.join(cfg["checkpoint_dir"], "mobheat-state"), rank, world)
-        self.out = ShmArena()
+        # the rank's statements, copied out of the engine's pinned buffers (each encode reuses them) into shared
+        # memory the driver reads: tiles, positions
+        self.out_t, self.out_p = ShmArena(), ShmArena()
 
     def reset(self):
         if self.engine is not None:
@@ -156,8 +158,8 @@ class RankRunner:
 
     def run(self, epoch, views, lo, hi, restore):
         """Rank's share [lo, hi) of the batch in `views` (host arrays, the whole batch): the sharded stages, then the
-        statements of the tiles it owns and of the latest rows it holds.  Returns (stats, tiles, positions) with the
-        statements as (bytes, offsets) views of the engine's pinned buffers."""
+        statements of the tiles it owns and of the latest rows it holds.  Returns (stats, tiles, positions), the
+        statements as the manifests of the rank's shared-memory regions (positions None when it holds no latest row)."""
         if self.engine is None:
             self._start(restore)
         eng = self.engine
@@ -178,12 +180,14 @@ class RankRunner:
         out = self.sharded.process_batch(epoch, batch, out_memory=HM_MEM_DEVICE)
         _trace(self.rank, f"batch {epoch}: merged, {int(out.n_tiles)} tiles, {int(out.n_latest)} latest rows")
         c = self.cfg
-        tiles = eng.encode_tile_updates(c["city"], c["ttl_min"])
+        tb, to = eng.encode_tile_updates(c["city"], c["ttl_min"])   # (views: copied before the next encode)
+        tiles = self.out_t.put({"b": tb, "o": to})
         positions = None
         if out.n_latest:
             prov = (int(views["prov_n"][0]), views["prov_offs"], views["prov_bytes"])
             veh = (int(views["veh_n"][0]), views["veh_offs"], views["veh_bytes"])
-            positions = eng.encode_position_updates(prov, veh)
+            pb, po = eng.encode_position_updates(prov, veh)
+            positions = self.out_p.put({"b": pb, "o": po})
         stats = dict(n_in=int(out.n_in), n_valid=int(out.n_valid), n_late=int(out.n_late), n_state=int(out.n_state),
                      n_tiles=int(out.n_tiles), n_latest=int(out.n_latest), watermark_ms=int(out.watermark_ms),
                      batch_max_event_ms=int(out.batch_max_event_ms), late_watermark_ms=int(out.late_watermark_ms),
@@ -196,12 +200,6 @@ class RankRunner:
             kind = self.store.save(epoch, self.engine, self.lineage, self.cfg["full_every"])
             _trace(self.rank, f"checkpoint {epoch}: {kind} written")
 
-    def export_out(self, tiles, positions):
-        """A worker's statements into its shared-memory region: (name, layout)."""
-        arrs = {"tb": tiles[0], "to": tiles[1]}
-        if positions is not None:
-            arrs.update(pb=positions[0], po=positions[1])
-        return self.out.put(arrs)
 
 
 def _runner_class(cfg):
@@ -249,7 +247,7 @@ def _worker_main(rank, world, port, conn, cfg):
             if op == "batch":
                 _, epoch, name, layout, lo, hi, restore = msg
                 stats, tiles, positions = runner.run(epoch, shm_views(name, layout), lo, hi, restore)
-                conn.send(("ok", stats, runner.export_out(tiles, positions)))
+                conn.send(("ok", stats, tiles, positions))
             elif op == "commit":
                 runner.commit(msg[1])
                 conn.send(("ok",))
@@ -261,7 +259,8 @@ def _worker_main(rank, world, port, conn, cfg):
         except Exception as e:
             conn.send(("err", repr(e), traceback.format_exc(), type(e).__name__, getattr(runner, "began", False)))
     runner.reset()
-    runner.out.close()
+    runner.out_t.close()
+    runner.out_p.close()
     _trace(rank, "closing")
     conn.send(("closed",))
     try:
@@ -369,13 +368,21 @@ class ShardedStream:
                 self.reset()
             first = next((e for _, e in errs if not isinstance(e, PeerFailed) and "PeerFailed" not in str(e)), errs[0][1])
             raise first
-        stats0, tiles0, pos0 = res0
-        per_rank = [(stats0, tiles0, pos0)]
-        for m in replies:
-            v = shm_views(*m[2], slot=f"out{len(per_rank)}")
-            per_rank.append((m[1], (v["tb"], v["to"]), (v["pb"], v["po"]) if "pb" in v else None))
+        per_rank = []
+        for r, (stats, tiles, pos) in enumerate([res0] + [m[1:4] for m in replies]):
+            per_rank.append((stats, self._views(r, tiles, "t"), self._views(r, pos, "p")))
         self.last = per_rank
         return per_rank
+
+    def _views(self, r, manifest, kind):
+        if manifest is None:
+            return None
+        if r == 0:
+            arena = self.runner.out_t if kind == "t" else self.runner.out_p
+            v = {k: np.ndarray(shp, np.dtype(d), buffer=arena.shm.buf, offset=o) for k, d, shp, o in manifest[1]}
+        else:
+            v = shm_views(*manifest, slot=f"{kind}{r}")
+        return v["b"], v["o"]
 
     def commit(self, epoch):
         """Checkpoint every rank's state after the committed epoch (rank 0 last; then the files of an older world size
@@ -445,5 +452,6 @@ class ShardedStream:
         except Exception:
             pass
         self.inputs.close()
-        self.runner.out.close()
+        self.runner.out_t.close()
+        self.runner.out_p.close()
         _trace(0, "closed")

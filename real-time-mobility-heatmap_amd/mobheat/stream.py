@@ -220,6 +220,7 @@ SINK_FACTORY = MongoSink   # tests replace this with an in-memory capture sink
 
 # ------------------ batch columns ------------------
 def _pandas_to_arrow(pdf):
+    import pandas as pd
     """A pandas frame as Arrow WITHOUT pandas' NaN -> null mapping on float columns: a NaN speedKmh (Spark's JSON reader
     accepts NaN tokens, SURVEY App. A.2) must stay NaN so that avg(speedKmh) is NaN (App. A.4), while a missing value
     (None in an object column, pd.NA in a nullable column) is null."""
@@ -227,7 +228,11 @@ def _pandas_to_arrow(pdf):
     cols = {}
     for name in pdf.columns:
         c = pdf[name]
-        if c.dtype.kind == "f":            # numpy float: NaN is a value, there is no null
+        if isinstance(c.dtype, pd.api.extensions.ExtensionDtype) and hasattr(c.array, "__arrow_array__"):
+            # nullable extension arrays (Float64, Int64, string, ...): their mask is the null set -- pd.NA -> null, a
+            # NaN in a Float64 column stays NaN (pyarrow's __arrow_array__ protocol keeps the two apart)
+            cols[str(name)] = pa.array(c.array)
+        elif c.dtype.kind == "f":          # numpy float: NaN is a value, there is no null
             cols[str(name)] = pa.array(c.to_numpy(), from_pandas=False)
         elif c.dtype == object:            # None -> null, float('nan') -> NaN
             try:

@@ -35,17 +35,19 @@ class OracleRunner(RankRunner):
         out = self.sharded.process_batch(epoch, b, sync=lambda: None)
         c = self.cfg
         tb, to = statements_of_tiles(out["tiles"], c)
+        tiles = self.out_t.put({"b": tb, "o": to})
         rows = np.asarray(out["latest"], np.int64) + lo
         pos = None
         if rows.size:
             prov = (int(views["prov_n"][0]), views["prov_offs"], views["prov_bytes"])
             veh = (int(views["veh_n"][0]), views["veh_offs"], views["veh_bytes"])
-            pos = _lib.position_statements_selftest(prov, veh, views["vkey"][rows], views["ts_us"][rows],
-                                                    views["lat"][rows], views["lon"][rows])
+            pb, po = _lib.position_statements_selftest(prov, veh, views["vkey"][rows], views["ts_us"][rows],
+                                                       views["lat"][rows], views["lon"][rows])
+            pos = self.out_p.put({"b": pb, "o": po})
         o = self.sharded.stages.o
         stats = dict(n_in=n, n_valid=0, n_late=0, n_state=len(o.state), n_tiles=len(out["tiles"]), n_latest=int(rows.size),
                      watermark_ms=int(o.wm_cur), batch_max_event_ms=0, late_watermark_ms=0, n_partials=0)
-        return stats, (tb, to), pos
+        return stats, tiles, pos
 
     def commit(self, epoch):
         OracleRunner.commits.append((self.rank, int(epoch)))

@@ -82,6 +82,19 @@ def _set(monkeypatch, stream, tmp_path, world, tag):
     stream.reset_engine()
 
 
+def _assert_same_statements(got, ref, what):
+    """Equal multisets of statements; on a difference, the first few differing documents (decoded) in the message
+    (pytest's own diff of two long byte lists takes minutes)."""
+    import bson
+    g, r = sorted(got), sorted(ref)
+    if g == r:
+        return
+    gs, rs = set(g), set(r)
+    only_g, only_r = [bson.decode(x) for x in g if x not in rs][:3], [bson.decode(x) for x in r if x not in gs][:3]
+    raise AssertionError(f"{what}: {len(g)} vs {len(r)} statements, {len(gs - rs)} differ; "
+                         f"sharded only: {only_g}; single only: {only_r}")
+
+
 def _docs(stmts):
     import bson
     out = {}
@@ -122,8 +135,7 @@ def test_sharded_foreach_batch_func_writes_single_gpu_statements(world, tmp_path
     got = _run(stream, frames, range(5))
     for e in range(5):
         for coll in ("tiles", "positions_latest"):
-            assert len(got[e][coll]) == len(ref[e][coll]), (e, coll)
-            assert sorted(got[e][coll]) == sorted(ref[e][coll]), (e, coll)
+            _assert_same_statements(got[e][coll], ref[e][coll], f"epoch {e} {coll}")
         assert len(ref[e]["tiles"]) > 1000 and len(ref[e]["positions_latest"]) > 1500
     # cut after batch 2: a new process (workers and state gone) resumes at epoch 3 from the checkpoints
     for world2 in (world, 3 if world != 3 else 2):
@@ -134,7 +146,7 @@ def test_sharded_foreach_batch_func_writes_single_gpu_statements(world, tmp_path
         rest = _run(stream, frames, range(3, 5))
         for k, e in enumerate(range(3, 5)):
             for coll in ("tiles", "positions_latest"):
-                assert sorted(rest[k][coll]) == sorted(ref[e][coll]), (world2, e, coll)
+                _assert_same_statements(rest[k][coll], ref[e][coll], f"resumed into {world2} ranks, epoch {e} {coll}")
     stream.close_sharded()
 
 

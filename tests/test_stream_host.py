@@ -685,3 +685,20 @@ def test_wire_op_msg_equals_pymongo_and_fake_server():
     sink.close()
     th.join(5)
     srv.close()
+
+
+def test_batch_columns_nullable_float_keeps_nulls_apart_from_nan():
+    """A pandas nullable Float64 speedKmh column: pd.NA is a null speed (not counted by avg, Spark's null) and a NaN is
+    a NaN value (propagates into avg), as Spark's JSON reader gives them.  (Round 4: NA became NaN
+    through to_numpy(), turning every avgSpeedKmh of a tile with a missing speed into NaN.)"""
+    sp = pd.arrays.FloatingArray(np.array([1.5, 0.0, np.nan, 4.0]), np.array([False, True, False, False]))
+    df = pd.DataFrame({"provider": ["p"] * 4, "vehicleId": ["a", "b", "c", "d"], "lat": [1.0] * 4, "lon": [2.0] * 4,
+                       "speedKmh": sp, "eventTs": pd.to_datetime([1759572000] * 4, unit="s")})
+    c = stream.batch_columns(df)
+    assert c["speed_valid"].tolist() == [True, False, True, True]
+    assert c["speed"][0] == 1.5 and np.isnan(c["speed"][2]) and c["speed"][3] == 4.0
+    # nullable integer and string columns too (mask = null)
+    df2 = df.assign(lat=pd.array([1, None, 3, 4], dtype="Int64"), vehicleId=pd.array(["a", None, "c", "d"], dtype="string"))
+    c2 = stream.batch_columns(df2)
+    assert np.isnan(c2["lat"][1]) and c2["lat"][2] == 3.0
+    assert c2["row_valid"].tolist() == [True, False, True, True]
