@@ -186,6 +186,7 @@ int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_r
                     hm_batch_out *out);
 
 /* device helpers for the caller's exchange buffers */
+int hm_device_memory(int32_t device, int64_t *free_bytes, int64_t *total_bytes);   /* (sizes a state arena) */
 int hm_device_alloc(int32_t device, int64_t bytes, void **ptr);
 int hm_device_free(int32_t device, void *ptr);
 int hm_memcpy(void *dst, const void *src, int64_t bytes, int32_t kind); /* 0 H2D 1 D2H 2 D2D */

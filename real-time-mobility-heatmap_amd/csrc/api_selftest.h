@@ -30,6 +30,19 @@ int hm_selftest_decimal_to_double(const uint64_t *w, const int64_t *q, int64_t n
     return HM_OK;
 }
 
+int hm_device_memory(int32_t device, int64_t *free_bytes, int64_t *total_bytes) {
+    if (!free_bytes || !total_bytes) return HM_E_INVALID;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev || hipSetDevice(device) != hipSuccess) {
+        (void)hipGetLastError();
+        return HM_E_HIP;
+    }
+    size_t f = 0, t = 0;
+    if (hipMemGetInfo(&f, &t) != hipSuccess) return HM_E_HIP;
+    *free_bytes = (int64_t)f;
+    *total_bytes = (int64_t)t;
+    return HM_OK;
+}
 int hm_device_alloc(int32_t device, int64_t bytes, void **ptr) {
     if (!ptr || bytes < 0) return HM_E_INVALID;
     if (hipSetDevice(device) != hipSuccess) return HM_E_HIP;

@@ -149,19 +149,17 @@ class StateCheckpoints:
 
     # ---- save ----
     def save(self, epoch, engine, lineage, full_every):
-        """Checkpoint the engine's state after committed epoch `epoch` into this rank's chain of `lineage`: a snapshot
-        when the chain has none or `full_every` deltas followed the newest one, else the epoch's delta.  Deletes this
-        rank's files of epochs >= `epoch` first (an abandoned lineage), and after the write every file of this rank
-        that the newest two snapshots of the chain no longer need (other lineages included)."""
-        from .engine import save_state_file
+        """Checkpoint the engine's state after epoch `epoch` into this rank's chain of `lineage` (prepare + write)."""
+        return self.write(self.prepare(epoch, engine, lineage, full_every))
+
+    def prepare(self, epoch, engine, lineage, full_every):
+        """The engine's part of a checkpoint of epoch `epoch` (call it from the engine's thread, before the next batch
+        changes the state): a snapshot when this rank's chain of `lineage` has none or `full_every` deltas followed
+        the newest one, else the epoch's delta (hm_state_export_touched), copied to host memory.  Returns the job
+        write() finishes -- the file I/O, which may run on another thread (foreach_batch_func overlaps it with the
+        sink's writes)."""
         epoch = int(epoch)
-        os.makedirs(self.root, exist_ok=True)
-        entries = self.scan()
-        mine = [e for e in entries if e.rank == self.rank and e.world == self.world]
-        for e in mine:
-            if e.epoch >= epoch:
-                _remove(e.path)
-        entries = [e for e in entries if not (e.rank == self.rank and e.world == self.world and e.epoch >= epoch)]
+        entries = [e for e in self.scan() if not (e.rank == self.rank and e.world == self.world and e.epoch >= epoch)]
         ch = None   # this rank's chain of `lineage` ending at its newest epoch before `epoch`
         for C in sorted({e.epoch for e in entries if e.rank == self.rank and e.world == self.world}, reverse=True):
             c = self.chain_to(self.rank, self.world, C, entries)
@@ -177,9 +175,21 @@ class StateCheckpoints:
             meta = {"lineage": lineage, "base": ch[0].epoch, "prev": ch[-1].epoch, "rank": self.rank,
                     "world": self.world}
             kind = "delta"
-        save_state_file(self.path(kind, epoch), info, recs, meta=json.dumps(meta))
-        self._prune(lineage, epoch)
-        return kind
+        return {"epoch": epoch, "kind": kind, "info": info, "recs": recs, "meta": meta}
+
+    def write(self, job):
+        """The file side of a prepared checkpoint: this rank's files of epochs >= its epoch deleted (an abandoned
+        lineage), the file written atomically (fsync + rename), then every file of this rank that the newest two
+        snapshots of the chain no longer need (other lineages included).  Returns the kind written."""
+        from .engine import save_state_file
+        epoch = job["epoch"]
+        os.makedirs(self.root, exist_ok=True)
+        for e in self.scan():
+            if e.rank == self.rank and e.world == self.world and e.epoch >= epoch:
+                _remove(e.path)
+        save_state_file(self.path(job["kind"], epoch), job["info"], job["recs"], meta=json.dumps(job["meta"]))
+        self._prune(job["meta"]["lineage"], epoch)
+        return job["kind"]
 
     def _prune(self, lineage, epoch):
         mine = [e for e in self.scan() if e.rank == self.rank and e.world == self.world]

@@ -195,10 +195,21 @@ class RankRunner:
         return stats, tiles, positions
 
     def commit(self, epoch):
-        if self.cfg["checkpoint"] and self.engine is not None:
-            _trace(self.rank, f"checkpoint {epoch}")
-            kind = self.store.save(epoch, self.engine, self.lineage, self.cfg["full_every"])
-            _trace(self.rank, f"checkpoint {epoch}: {kind} written")
+        job = self.commit_prepare(epoch)
+        if job is not None:
+            self.commit_write(job)
+
+    def commit_prepare(self, epoch):
+        """The GPU half of the rank's checkpoint of `epoch` (mobheat.checkpoint prepare), or None when off."""
+        if not (self.cfg["checkpoint"] and self.engine is not None):
+            return None
+        _trace(self.rank, f"checkpoint {epoch}")
+        return self.store.prepare(epoch, self.engine, self.lineage, self.cfg["full_every"])
+
+    def commit_write(self, job):
+        kind = self.store.write(job)
+        _trace(self.rank, f"checkpoint {job['epoch']}: {kind} written")
+        return kind
 
 
 
@@ -385,16 +396,34 @@ class ShardedStream:
         return v["b"], v["o"]
 
     def commit(self, epoch):
-        """Checkpoint every rank's state after the committed epoch (rank 0 last; then the files of an older world size
-        are dropped once every rank of this one holds a snapshot)."""
+        """Checkpoint every rank's state after the epoch (commit_begin + commit_end)."""
+        self.commit_begin(epoch)
+        self.commit_end()
+
+    def commit_begin(self, epoch):
+        """Every rank checkpoints its state after the epoch: the workers in their processes, rank 0's file on a
+        background thread -- concurrently with the driver's writes of the statements (stream._foreach_sharded)."""
         _trace(0, f"commit {epoch}")
         for c in self.conns:
             c.send(("commit", int(epoch)))
-        err = None
+        self._commit = (None, None)
         try:
-            self.runner.commit(epoch)
+            job = self.runner.commit_prepare(epoch)
+            if job is not None:
+                from concurrent.futures import ThreadPoolExecutor
+                if getattr(self, "_io", None) is None:
+                    self._io = ThreadPoolExecutor(1, thread_name_prefix="mobheat-checkpoint")
+                self._commit = (self._io.submit(self.runner.commit_write, job), None)
         except Exception as e:
-            err = e
+            self._commit = (None, e)
+
+    def commit_end(self):
+        """Wait for every rank's checkpoint; then the files of an older world size are dropped once every rank of this
+        one holds a snapshot."""
+        fut, err = self._commit
+        if fut is not None:
+            e = fut.exception()
+            err = err or e
         for r, c in enumerate(self.conns, start=1):
             m = self._recv(c, r)
             if m[0] != "ok" and err is None:

@@ -44,6 +44,14 @@ N_GPUS = int(os.getenv("MOBHEAT_GPUS", "1"))
 DIST_BACKEND = os.getenv("MOBHEAT_DIST_BACKEND", "nccl")
 STATE_CHECKPOINT = os.getenv("MOBHEAT_STATE_CHECKPOINT", "1") == "1"
 STATE_FULL_EVERY = int(os.getenv("MOBHEAT_STATE_FULL_EVERY", "10"))
+# The engine's window tables are carved from a zeroed reservation made at its creation (hm_config.state_arena_bytes)
+# before any allocation inside a batch: "auto" sizes it from the first batch the process sees (ARENA_BYTES_PER_ROW per
+# row, at most a quarter of the device), a number of bytes pins it, 0 turns it off.  (A window table's first
+# hipMalloc inside a batch took seconds on some boxes)
+STATE_ARENA = os.getenv("MOBHEAT_STATE_ARENA_BYTES", "auto")
+ARENA_BYTES_PER_ROW = 16 * 65   # ~8 live or pooled window tables of 2 x rows 65-B slots
+
+LAST_TIMINGS = {}   # host-side phases (ms) of the last foreach_batch_func call: columns, process, checkpoint, sink ...
 
 _ENGINE = None
 _LAST_EPOCH = None   # the last epoch committed (merged and written) from _ENGINE's state
@@ -83,9 +91,23 @@ def restore_state(eng, epoch_id):
     return pt.epoch
 
 
-def get_engine(epoch_id=None):
+def _arena_bytes(n_rows):
+    if STATE_ARENA != "auto":
+        return int(STATE_ARENA)
+    if not n_rows or n_rows < 100_000:
+        return 0
+    from . import _lib
+    import ctypes
+    free, total = ctypes.c_int64(), ctypes.c_int64()
+    if _lib.load().hm_device_memory(DEVICE, ctypes.byref(free), ctypes.byref(total)) != 0:
+        return 0
+    return int(min(ARENA_BYTES_PER_ROW * int(n_rows), total.value // 4, free.value // 2))
+
+
+def get_engine(epoch_id=None, n_rows=None):
     """The process's engine; a new one resumes from the newest state checkpoint older than `epoch_id` (Spark
-    re-runs the first uncommitted epoch on the state of the one before it)."""
+    re-runs the first uncommitted epoch on the state of the one before it) and, created for a batch of `n_rows`
+    rows, reserves its state arena and per-batch buffers for batches of that size."""
     global _ENGINE, _LAST_EPOCH, _LINEAGE
     if _ENGINE is not None and epoch_id is not None and _LAST_EPOCH is not None and int(epoch_id) <= _LAST_EPOCH:
         # Spark re-runs an epoch this engine already merged (the query restarted in this process): rebuild the state
@@ -94,7 +116,8 @@ def get_engine(epoch_id=None):
     if _ENGINE is None:
         from .checkpoint import new_lineage
         eng = HeatmapEngine(h3_res=H3_RES, tile_minutes=TILE_MIN, watermark_delay_ms=WATERMARK_DELAY_MS,
-                            device=DEVICE)
+                            device=DEVICE, state_arena_bytes=_arena_bytes(n_rows),
+                            batch_capacity_hint=int(n_rows) if n_rows and n_rows >= 100_000 else 0)
         if STATE_CHECKPOINT and epoch_id is not None:
             restore_state(eng, epoch_id)
         else:
@@ -104,12 +127,32 @@ def get_engine(epoch_id=None):
 
 
 def save_state_checkpoint(epoch_id):
-    """Checkpoint the engine's state after committed epoch `epoch_id` into its chain (mobheat.checkpoint): a full
-    snapshot when the chain has none or STATE_FULL_EVERY deltas followed the newest one, else the batch's delta; files
-    of epochs >= epoch_id (an abandoned lineage) are deleted first, and the chain keeps its newest two snapshots."""
-    st = _store()
-    st.save(epoch_id, get_engine(), _LINEAGE, STATE_FULL_EVERY)
-    st.prune_other_worlds(_LINEAGE)
+    """Checkpoint the engine's state after epoch `epoch_id` into its chain (mobheat.checkpoint): a full snapshot when
+    the chain has none or STATE_FULL_EVERY deltas followed the newest one, else the batch's delta; files of epochs >=
+    epoch_id (an abandoned lineage) are deleted first, and the chain keeps its newest two snapshots."""
+    return checkpoint_begin(epoch_id).result()
+
+
+_IO = None
+
+
+def checkpoint_begin(epoch_id):
+    """save_state_checkpoint in two halves: the export from the GPU now (before the next batch changes the state), the
+    file write on a background thread -- foreach_batch_func overlaps it with the sink's writes and waits for it before
+    returning.  (Written before the writes succeed is safe: a restart re-runs an uncommitted epoch E on the newest
+    chain ending BEFORE E, and a replay of E in this process rewrites E's file.)  Returns a Future of the kind."""
+    global _IO
+    if _IO is None:
+        from concurrent.futures import ThreadPoolExecutor
+        _IO = ThreadPoolExecutor(1, thread_name_prefix="mobheat-checkpoint")
+    st, lineage = _store(), _LINEAGE
+    job = st.prepare(epoch_id, get_engine(), lineage, STATE_FULL_EVERY)
+
+    def write():
+        kind = st.write(job)
+        st.prune_other_worlds(lineage)
+        return kind
+    return _IO.submit(write)
 
 
 def reset_engine():
@@ -511,6 +554,9 @@ def _foreach_sharded(df, epoch):
             dicts = (cols["provider_uniques"], cols["vehicle_uniques"])
         per_rank = sh.process(epoch, cols, dicts)
         _PENDING = (epoch, per_rank, None)
+    # every rank's state checkpoint, written while the statements go out (see checkpoint_begin)
+    if STATE_CHECKPOINT:
+        sh.commit_begin(epoch)
     sink = SINK_FACTORY()
     try:
         for _, tiles, _ in per_rank:
@@ -518,10 +564,10 @@ def _foreach_sharded(df, epoch):
         for _, _, pos in per_rank:
             if pos is not None:
                 _flush_statements(sink, "positions_latest", *pos)
-        if STATE_CHECKPOINT:
-            sh.commit(epoch)
     finally:
         sink.close()
+        if STATE_CHECKPOINT:
+            sh.commit_end()
     _PENDING = None
     _LAST_EPOCH = epoch
     st = [x[0] for x in per_rank]
@@ -539,17 +585,27 @@ def foreach_batch_func(df, epoch_id: int):
     losing state: a batch that fails before its merge leaves the state untouched (hm_state_version); one that fails
     during the merge drops the state, which the retry rebuilds from the checkpoints; one whose writes fail keeps the
     merged state and, when Spark re-runs that epoch, writes the same documents again without merging twice."""
-    global _LAST_EPOCH, _PENDING
+    global _LAST_EPOCH, _PENDING, LAST_TIMINGS
+    import time
     epoch = int(epoch_id)
     if N_GPUS > 1:
         return _foreach_sharded(df, epoch)
+    tm = {}
+    clock = [time.perf_counter()]
+
+    def lap(name):
+        t = time.perf_counter()
+        tm[name] = tm.get(name, 0.0) + 1e3 * (t - clock[0])
+        clock[0] = t
     if _PENDING is not None and _PENDING[0] == epoch and _ENGINE is not None:
         res, dicts = _PENDING[1], _PENDING[2]   # the replay of the epoch whose writes failed: its state is in place
     else:
         if _PENDING is not None:   # another epoch while one is uncommitted: that merge never committed
             reset_engine()
         cols = batch_columns(df)
-        eng = get_engine(epoch)
+        lap("columns")
+        eng = get_engine(epoch, cols.get("n"))
+        lap("engine")
         v0 = eng.state_version()
         try:
             res, dicts = _process(eng, epoch, cols)
@@ -557,21 +613,33 @@ def foreach_batch_func(df, epoch_id: int):
             if _ENGINE is not None and _ENGINE.state_version() != v0:
                 reset_engine()   # the merge began: the state may hold part of the batch
             raise
+        lap("process")
         _PENDING = (epoch, res, dicts)
     eng = get_engine()
+    # the batch's state checkpoint: exported now, its file written while the statements go out
+    ckpt = checkpoint_begin(epoch) if STATE_CHECKPOINT else None
+    lap("checkpoint_export")
     sink = SINK_FACTORY()
     try:
         # ---- 1) Upsert tiles (TTL via staleAt): the UpdateOne statements, BSON-encoded on the GPU ----
         buf, offs = eng.encode_tile_updates(CITY, TTL_MIN)
+        lap("encode")
         _flush_statements(sink, "tiles", buf, offs)
+        lap("sink")
         # ---- 2) latest per (provider, vehicleId) within this micro-batch: statements encoded on the GPU ----
         if res.n_latest:
             buf, offs = eng.encode_position_updates(*dicts)   # (local offsets of the rows' 900-s buckets)
+            lap("encode")
             _flush_statements(sink, "positions_latest", buf, offs)
-        if STATE_CHECKPOINT:   # after the writes succeeded: the batch is committed
-            save_state_checkpoint(epoch)
+            lap("sink")
     finally:
         sink.close()
+        if ckpt is not None:   # (also when a write failed: a replay must not race the file)
+            exc = ckpt.exception()
+            lap("checkpoint_wait")
+    if ckpt is not None and exc is not None:
+        raise exc
+    LAST_TIMINGS = tm
     _PENDING = None
     _LAST_EPOCH = epoch
     return res

@@ -49,8 +49,9 @@ class OracleRunner(RankRunner):
                      watermark_ms=int(o.wm_cur), batch_max_event_ms=0, late_watermark_ms=0, n_partials=0)
         return stats, tiles, pos
 
-    def commit(self, epoch):
+    def commit_prepare(self, epoch):
         OracleRunner.commits.append((self.rank, int(epoch)))
+        return None
 
 
 def statements_of_tiles(tiles, cfg):

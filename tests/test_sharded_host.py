@@ -1,7 +1,7 @@
 """CPU, world_size 2 over gloo: the sharded writer behind foreach_batch_func (mobheat.sharded, MOBHEAT_GPUS = 2;
 reference heatmap_stream.py:150,159-235,244-245) -- a spawned worker rank, the batch's columns and string dictionaries
 handed over in shared memory, every rank encoding the statements of what it owns, the driver writing them tiles first,
-commits after the writes, and Spark's replay of a batch whose writes failed.
+every rank's checkpoint written while the statements go out, and Spark's replay of a batch whose writes failed.
 
 The ranks' stages are the oracle restatement (tests/sharded_fake.OracleRunner over test_distributed_gloo.OracleStages)
 and their statements come from the library's host-executed encoders, so the written statements must equal those of
@@ -85,7 +85,7 @@ def test_sharded_writer_world2_gloo(tmp_path, monkeypatch, oracle_h3):
     try:
         stream.foreach_batch_func(frames[0], 0)
         stream.foreach_batch_func(frames[1], 1)
-        # the writes of batch 2 fail: nothing is committed; Spark re-runs epoch 2 and the same statements are written
+        # the writes of batch 2 fail: the epoch is not committed; Spark re-runs it and the same statements are written
         # without a second merge (the oracle's state would double-count the batch)
         Capture.fail = True
         with pytest.raises(IOError):
@@ -101,5 +101,6 @@ def test_sharded_writer_world2_gloo(tmp_path, monkeypatch, oracle_h3):
         for coll in ("tiles", "positions_latest"):
             assert sorted(written[e][coll]) == exp[e][coll], (e, coll)
     assert len(exp[2]["tiles"]) > 100 and res.n_tiles == len(exp[2]["tiles"])
-    # (rank 0's commits are recorded here; the worker's in its own process) epochs 0, 1 and 2 once, after the writes
-    assert OracleRunner.commits == [(0, 0), (0, 1), (0, 2)]
+    # (rank 0's checkpoints are recorded here; the worker's in its own process) one per epoch, written while the
+    # statements go out -- epoch 2 twice: its first writes failed, and the replay checkpoints it again (the same state)
+    assert OracleRunner.commits == [(0, 0), (0, 1), (0, 2), (0, 2)]
