@@ -397,7 +397,9 @@ void oracle_libm_batch(int fn, const double *a, const double *b, int64_t n, doub
             case 0: libm_sincos(a[i], &out[i], &out2[i]); break;
             case 1: out[i] = acos(a[i]); break;
             case 2: out[i] = atan2(a[i], b[i]); break;
-            default: out[i] = tan(a[i]); break;
+            case 3: out[i] = tan(a[i]); break;
+            case 4: out[i] = asin(a[i]); break;
+            default: out[i] = atan(a[i]); break;
         }
     }
 }

@@ -60,11 +60,11 @@ def latlng_to_cell(lat, lon, res):
     return out
 
 
-LIBM_FNS = {"sincos": 0, "acos": 1, "atan2": 2, "tan": 3}
+LIBM_FNS = {"sincos": 0, "acos": 1, "atan2": 2, "tan": 3, "asin": 4, "atan": 5}
 
 
 def libm(fn, a, b=None):
-    """glibc's sincos (-> (sin, cos)), acos, atan2(a, b) or tan of each element, through this process's libm."""
+    """glibc's sincos (-> (sin, cos)), acos, atan2(a, b), tan, asin or atan of each element, through this process's libm."""
     L = load()
     a = np.ascontiguousarray(a, dtype=np.float64)
     b = None if b is None else np.ascontiguousarray(b, dtype=np.float64)

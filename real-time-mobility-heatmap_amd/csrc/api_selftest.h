@@ -169,10 +169,10 @@ int hm_selftest_latlng_to_cell_fast_host(const double *lat, const double *lon, i
     return HM_OK;
 }
 
-// glibc's sincos / acos / atan2 / tan as restated in glibc_libm.h (fn 0 sincos: out = sin, out2 = cos; 1 acos(a);
-// 2 atan2(a, b); 3 tan(a)), executed on the host and on the GPU (test entry points; tests/test_glibc_libm.py)
+// glibc's sincos / acos / atan2 / tan / asin / atan as restated in glibc_libm.h (fn 0 sincos: out = sin, out2 = cos;
+// 1 acos(a); 2 atan2(a, b); 3 tan(a); 4 asin(a); 5 atan(a)), executed on the host and on the GPU (test entry points; tests/test_glibc_libm.py)
 static int glm_check(int32_t fn, const double *a, const double *b, int64_t n, double *out, double *out2) {
-    if (!a || !out || n < 0 || fn < 0 || fn > 3 || (fn == 0 && !out2) || (fn == 2 && !b)) return HM_E_INVALID;
+    if (!a || !out || n < 0 || fn < 0 || fn > 5 || (fn == 0 && !out2) || (fn == 2 && !b)) return HM_E_INVALID;
     return HM_OK;
 }
 HM_HD void glm_eval(int32_t fn, int64_t i, const double *a, const double *b, double *out, double *out2,
@@ -181,7 +181,9 @@ HM_HD void glm_eval(int32_t fn, int64_t i, const double *a, const double *b, dou
         case 0: glm::sincos(a[i], out[i], out2[i], G); break;
         case 1: out[i] = glm::acos(a[i], G); break;
         case 2: out[i] = glm::atan2(a[i], b[i], G); break;
-        default: out[i] = glm::tan(a[i], G); break;
+        case 3: out[i] = glm::tan(a[i], G); break;
+        case 4: out[i] = glm::asin(a[i], G); break;
+        default: out[i] = glm::atan(a[i], G); break;
     }
 }
 __global__ __launch_bounds__(256) void k_glibc_libm(int32_t fn, const double *a, const double *b, int64_t n,

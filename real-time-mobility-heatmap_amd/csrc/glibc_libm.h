@@ -1,21 +1,24 @@
-// The glibc double routines upstream H3's latLngToCell calls, restated for host and device (CDNA4 fp64 VALU).
+// The glibc double routines upstream H3's latLngToCell and cellToBoundary call, restated for host and device (CDNA4
+// fp64 VALU).
 //
 // Why: the reference's cell ids come from h3 linked against the host's glibc (reference heatmap_stream.py:65-75 ->
-// h3.latlng_to_cell -> H3 C latLngToCell: sincos (gcc fuses upstream's sin/cos pairs), acos, atan2, tan).  On a
-// knife-edge input the last bit of one of those results decides the cell, so the exact path (h3_device.h
-// latLngToCellDeg, run for the ~0.01% of events whose fast-path margins are too small) computes them exactly as
-// glibc 2.35 does on the reference's x86-64 hosts:
+// h3.latlng_to_cell -> H3 C latLngToCell: sincos (gcc fuses upstream's sin/cos pairs), acos, atan2, tan), and so do
+// its cell boundaries (reference app.py:19-41 -> h3.cell_to_boundary: sincos, asin, atan2, atan).  On a knife-edge
+// input the last bit of one of those results decides the cell, so the exact path (h3_device.h latLngToCellDeg, run
+// for the ~0.01% of events whose fast-path margins are too small) and the boundary kernel (h3_boundary.h) compute
+// them exactly as glibc 2.35 does on the reference's x86-64 hosts:
 //   * sincos -- generic dbl-64 s_sincos.c + s_sin.c (do_sin, do_cos, TAYLOR_SIN, reduce_sincos): 2.35 has no
 //     multiarch sincos, so this is plain IEEE double arithmetic in source order, no FMA;
-//   * acos, atan2, tan -- the variants glibc's IFUNC resolvers pick on an FMA+AVX2 CPU (__ieee754_acos_fma,
-//     __ieee754_atan2_fma, __tan_fma: e_asin.c, e_atan2.c, s_tan.c built with -mfma -mavx2), whose fused
-//     multiply-adds are part of the result; every fma() below is one vfmadd/vfnmadd/vfmsub of that machine code.
+//   * acos, asin, atan2, atan, tan -- the variants glibc's IFUNC resolvers pick on an FMA+AVX2 CPU
+//     (__ieee754_acos_fma, __ieee754_asin_fma, __ieee754_atan2_fma, __atan_fma, __tan_fma: e_asin.c, e_atan2.c,
+//     s_atan.c, s_tan.c built with -mfma -mavx2), whose fused multiply-adds are part of the result; every fma()
+//     below is one vfmadd/vfnmadd/vfmsub of that machine code.
 // Constants and tables: glibc_libm.inc (tools/gen_glibc_libm.py reads them from the image's libm.so.6).  The same
 // code runs on the host (hm_selftest_glibc_libm_host) and on the GPU (hm_selftest_glibc_libm_device); tests/
 // test_glibc_libm.py compares both with the running glibc on >= 1e7 arguments per function.
-// Domain: everything latLngToCell passes (|x| < 105414350 for sincos -- glibc's __branred range is not restated --,
-// |x| <= 0.787 for tan -- r = acos(1 - sqd/2) <= 0.66 --, all of acos and atan2); outside it the functions return
-// NaN, which no caller produces.
+// Domain: everything latLngToCell and cellToBoundary pass (|x| < 105414350 for sincos -- glibc's __branred range is
+// not restated --, |x| <= 0.787 for tan -- r = acos(1 - sqd/2) <= 0.66 --, all of acos, asin, atan and atan2);
+// outside it the functions return NaN, which no caller produces.
 // The whole file must be compiled with -ffp-contract=off (the Makefile does): the non-fma expressions are separate
 // roundings, as in glibc's code.
 //
@@ -39,6 +42,7 @@ struct Tables {
     double asncs[2566];
     double inroot[128];
     double powtwo[28];
+    double atan1_cij[241 * 7];
 };
 
 #define GLM_HD __host__ __device__ __forceinline__
@@ -179,13 +183,16 @@ GLM_HD double tan(double x, const Tables &G) {
 // ---------------------------------------------------------------- acos (e_asin.c, __ieee754_acos_fma)
 // one interval polynomial of the asncs table: T[0] the interval point, z = |x| - T[0],
 // res1 = z T[1] + (z^2 (z-Horner of T[top..2]) + T[top+1]), then acos = (hp1 - res1) + (hp0 - T[top+2]) for x > 0
-GLM_HD double acos_interval(double ax, int32_t hx, const double *T, int top) {
+GLM_HD double asncs_res1(double ax, const double *T, int top) {
     const double z = ax - T[0];
     double p = fma_(z, T[top], T[top - 1]);
     const double z2 = z * z;
     for (int j = top - 2; j >= 2; j--) p = fma_(z, p, T[j]);
     p = fma_(z2, p, T[top + 1]);
-    const double res1 = fma_(z, T[1], p);
+    return fma_(z, T[1], p);
+}
+GLM_HD double acos_interval(double ax, int32_t hx, const double *T, int top) {
+    const double res1 = asncs_res1(ax, T, top);
     const double c = T[top + 2];
     if (hx > 0) return (GLM_HP1 - res1) + (GLM_HP0 - c);
     return (res1 + GLM_HP1) + (c + GLM_HP0);
@@ -250,9 +257,9 @@ GLM_HD double acos(double x, const Tables &G) {
 
 // ---------------------------------------------------------------- atan2 (e_atan2.c, __ieee754_atan2_fma)
 // atan of the reduced argument u (+ du) from the cij table row nearest u: zz, t1 = cij[i][1] as the caller combines
-GLM_HD const double *atan_row(double u, const Tables &G) {
+GLM_HD const double *atan_row(double u, const double *cij) {
     const int i = (int)(fma_(u, GLM_TWO8, GLM_TWO52) - GLM_TWO52) - 16;
-    return &G.atan_cij[7 * i];
+    return &cij[7 * i];
 }
 GLM_HD double atan_poly5(double v, const double *c) {   // c2 + v (c3 + v (c4 + v (c5 + v c6)))
     double p = fma_(v, c[6], c[5]);
@@ -321,7 +328,7 @@ GLM_HD double atan2(double y, double x, const Tables &G) {
                 const double p = atan_small(v);
                 return copysign_(u + fma_(u * v, p, du), y);
             }
-            const double *c = atan_row(u, G);
+            const double *c = atan_row(u, G.atan_cij);
             const double t3 = u - c[0];
             const double v = du + t3;   // EADD(t3, du, v, dv)
             const double dv = fabs_(t3) > fabs_(du) ? (t3 - v) + du : (du - v) + t3;
@@ -341,7 +348,7 @@ GLM_HD double atan2(double y, double x, const Tables &G) {
             const double cor = GLM_HP0 > fabs_(u) ? (GLM_HP0 - t2) - u : GLM_HP0 - (u + t2);
             return copysign_((((cor + GLM_HP1) - du) - zz) + t2, y);
         }
-        const double *c = atan_row(u, G);
+        const double *c = atan_row(u, G.atan_cij);
         const double v = (u - c[0]) + du;
         const double zz = fma_(-v, atan_poly5(v, c), GLM_HP1);
         return copysign_((GLM_HP0 - c[1]) + zz, y);
@@ -355,7 +362,7 @@ GLM_HD double atan2(double y, double x, const Tables &G) {
             const double cor = GLM_HP0 > fabs_(u) ? (GLM_HP0 - t2) + u : (u - t2) + GLM_HP0;
             return copysign_((((cor + GLM_HP1) + du) + zz) + t2, y);
         }
-        const double *c = atan_row(u, G);
+        const double *c = atan_row(u, G.atan_cij);
         const double v = (u - c[0]) + du;
         const double zz = fma_(v, atan_poly5(v, c), GLM_HP1);
         return copysign_((GLM_HP0 + c[1]) + zz, y);
@@ -369,10 +376,111 @@ GLM_HD double atan2(double y, double x, const Tables &G) {
         const double cor = GLM_PI > fabs_(u) ? (GLM_PI - t2) - u : GLM_PI - (t2 + u);
         return copysign_((((cor + GLM_PI1) - du) - zz) + t2, y);
     }
-    const double *c = atan_row(u, G);
+    const double *c = atan_row(u, G.atan_cij);
     const double v = (u - c[0]) + du;
     const double zz = fma_(-v, atan_poly5(v, c), GLM_PI1);
     return copysign_((GLM_PI - c[1]) + zz, y);
+}
+
+// ---------------------------------------------------------------- asin (e_asin.c, __ieee754_asin_fma)
+// the interval polynomials are acos's (asncs_res1): asin(|x|) = res1 + T[top + 2]
+GLM_HD double asin(double x, const Tables &G) {
+    const int32_t hx = hi32(x);
+    const int32_t k = hx & 0x7fffffff;
+    if (k < 0x3e500000) return x;   // |x| < 2^-26
+    if (k < 0x3fc00000) {            // |x| < 0.125: Taylor
+        const double x2 = x * x;
+        double p = fma_(x2, GLM_AC_F6, GLM_AC_F5);
+        p = fma_(x2, p, GLM_AC_F4);
+        p = fma_(x2, p, GLM_AC_F3);
+        p = fma_(x2, p, GLM_AC_F2);
+        p = fma_(x2, p, GLM_AC_F1);
+        return fma_(p, x * x2, x);
+    }
+    const double ax = hx > 0 ? x : -x;
+    double r;
+    if (k < 0x3fd00000) r = asncs_res1(ax, &G.asncs[11 * ((k >> 15) & 0x1f)], 6) + G.asncs[11 * ((k >> 15) & 0x1f) + 8];
+    else if (k < 0x3fe00000) {
+        const double *T = &G.asncs[11 * ((k >> 14) & 0x3f) + 0x160];
+        r = asncs_res1(ax, T, 6) + T[8];
+    } else if (k < 0x3fe80000) {
+        const double *T = &G.asncs[3 * ((k >> 11) & 0x1fc) + 0x420];
+        r = asncs_res1(ax, T, 7) + T[9];
+    } else if (k < 0x3fed8000) {
+        const double *T = &G.asncs[13 * ((k >> 13) & 0x7f) + 0x3e0];
+        r = asncs_res1(ax, T, 8) + T[10];
+    } else if (k < 0x3fee8000) {
+        const double *T = &G.asncs[14 * ((k >> 13) & 0x7f) + 0x374];
+        r = asncs_res1(ax, T, 9) + T[11];
+    } else if (k < 0x3fef0000) {
+        const double *T = &G.asncs[15 * ((k >> 13) & 0x7f) + 0x300];
+        r = asncs_res1(ax, T, 10) + T[12];
+    } else if (k < 0x3ff00000) {   // 0.96875 <= |x| < 1: pi/2 - 2 asin(sqrt((1 - |x|) / 2)), root.tbl's 1/sqrt
+        double z = hx > 0 ? GLM_ONE - x : x + GLM_ONE;
+        z = z * GLM_HALF;
+        const uint64_t b = bits(z);
+        const double y0 = G.inroot[(int)(b >> 46) & 0x7f] * G.powtwo[0x1ff - (int)(b >> 53)];
+        const double rr = fma_(-(y0 * y0), z, GLM_ONE);
+        double q = fma_(rr, GLM_RT3, GLM_RT2);
+        q = fma_(rr, q, GLM_RT1);
+        q = fma_(rr, q, GLM_RT0);
+        const double t = q * y0;
+        const double c = z * t;
+        const double d = fma_(-c, t * GLM_HALF, GLM_THREE_HALVES);
+        const double y = (c + GLM_T24) - GLM_T24;
+        const double cc = fma_(-y, y, z) / fma_(d, c, y);
+        double p = fma_(z, GLM_AC_F6, GLM_AC_F5);
+        p = fma_(z, p, GLM_AC_F4);
+        p = fma_(z, p, GLM_AC_F3);
+        p = fma_(z, p, GLM_AC_F2);
+        p = fma_(z, p, GLM_AC_F1);
+        p = p * z;
+        const double yc = y + cc;
+        const double cor = fma_(-(yc + yc), p, fma_(-GLM_TWO, cc, GLM_HP1));
+        r = cor + fma_(-GLM_TWO, y, GLM_HP0);
+    } else {
+        if (k == 0x3ff00000 && lo32(x) == 0) return hx > 0 ? GLM_HP0 : GLM_MHP0;
+        if (k > 0x7ff00000 || (k == 0x7ff00000 && lo32(x) != 0)) return x + x;
+        return qnan();   // |x| > 1
+    }
+    return hx > 0 ? r : -r;
+}
+
+// ---------------------------------------------------------------- atan (s_atan.c, __atan_fma)
+// thresholds A (~1.29e-8), B = 1/16, C = 1, D = 16, E (~5.8e15); the cij rows are s_atan.c's own table
+GLM_HD double atan(double x, const Tables &G) {
+    const int32_t hx = hi32(x);
+    if ((hx & 0x7ff00000) == 0x7ff00000 && ((hx & 0xfffff) | lo32(x)) != 0) return x + x;
+    const double u = x < 0 ? -x : x;
+    if (u < GLM_ONE) {
+        if (u < GLM_INV16) {
+            if (u < GLM_AT_A) return x;
+            const double v = x * x;
+            return fma_(x * v, atan_small(v), x);
+        }
+        const double *c = atan_row(u, G.atan1_cij);
+        const double z = u - c[0];
+        return copysign_(fma_(atan_poly5(z, c), z, c[1]), x);
+    }
+    if (u < GLM_AT_D) {   // 1 <= u < 16: pi/2 - atan(1/u)
+        const double w = GLM_ONE / u;
+        const double t1 = u * w, t2 = fma_(u, w, -t1);   // EMULV
+        const double *c = atan_row(w, G.atan1_cij);
+        const double z = fma_((GLM_ONE - t1) - t2, w, w - c[0]);
+        const double yy = fma_(-z, atan_poly5(z, c), GLM_HP1);
+        return copysign_((GLM_HP0 - c[1]) + yy, x);
+    }
+    if (u < GLM_AT_E) {   // 16 <= u < E
+        const double w = GLM_ONE / u;
+        const double v = w * w;
+        const double t1 = u * w, t2 = fma_(u, w, -t1);
+        const double yy = (w * v) * atan_small(v);
+        const double ww = ((GLM_ONE - t1) - t2) * w;
+        const double t3 = GLM_HP0 - w;   // ESUB(hpi, w, t3, cor)
+        const double cor = GLM_HP0 > fabs_(w) ? (GLM_HP0 - t3) - w : GLM_HP0 - (w + t3);
+        return copysign_((((cor + GLM_HP1) - ww) - yy) + t3, x);
+    }
+    return 0 < x ? GLM_HP0 : GLM_MHP0;
 }
 
 }  // namespace glm

@@ -5,9 +5,9 @@
 // _faceIjkPentToCellBoundary (faceijk.c) with their substrate-grid helpers, in the operation order of the CPU
 // oracle (oracle/h3_oracle.c, the checker).  upstream's long double constants (M_SQRT3_2, M_RSQRT7, M_ONETHIRD,
 // M_180_PI, M_AP7_ROT_RADS, M_2PI, EPSILON) are applied with the exact x87 emulation of h3_device.h; the
-// face-centre sin/cos come from the host libm (H3Tables); atan2/atan/asin/sin/cos of per-vertex values use the
-// device math library, whose last bit can differ from glibc's: the parity bar is stated in the tests
-// (tests/test_gpu_boundary.py) -- vertex counts exact, coordinates within 1e-12 degrees.
+// face-centre sin/cos come from the host libm (H3Tables); sincos/asin/atan2/atan of per-vertex values are glibc's own
+// (glibc_libm.h: the FMA variants the reference host's libm runs), so the vertices are bit-identical to the
+// glibc-linked oracle's (tests/test_gpu_boundary.py).
 #pragma once
 #include "h3_device.h"
 
@@ -166,17 +166,18 @@ HM_HD void geoAzDistanceFromFace(const H3Tables &T, int f, double az, double dis
         // glibc's sincos and sin differ in the last bit for ~0.1% of arguments)
         const double s1 = T.faceSinLat[f], c1 = T.faceCosLat[f];
         double sd, cd, saz, caz;
-        sincos(distance, &sd, &cd);
-        sincos(az, &saz, &caz);
+        const glm::Tables &G = *T.glm;
+        glm::sincos(distance, sd, cd, G);
+        glm::sincos(az, saz, caz, G);
         double sinlat = s1 * cd + c1 * sd * caz;
         if (sinlat > 1.0) sinlat = 1.0;
         if (sinlat < -1.0) sinlat = -1.0;
-        lat = asin(sinlat);
+        lat = glm::asin(sinlat, G);
         if (ld_eps_lt(__builtin_fabs(lat - M_PI_2))) { lat = M_PI_2; lng = 0.0; }
         else if (ld_eps_lt(__builtin_fabs(lat + M_PI_2))) { lat = -M_PI_2; lng = 0.0; }
         else {
             double s2, c2;
-            sincos(lat, &s2, &c2);
+            glm::sincos(lat, s2, c2, G);
             const double invcosp2lat = 1.0 / c2;
             double sinlng = saz * sd * invcosp2lat;
             double coslng = (cd - s1 * s2) / c1 * invcosp2lat;
@@ -184,7 +185,7 @@ HM_HD void geoAzDistanceFromFace(const H3Tables &T, int f, double az, double dis
             if (sinlng < -1.0) sinlng = -1.0;
             if (coslng > 1.0) coslng = 1.0;
             if (coslng < -1.0) coslng = -1.0;
-            lng = p1lng + atan2(sinlng, coslng);
+            lng = p1lng + glm::atan2(sinlng, coslng, G);
         }
     }
     while (lng > M_PI) lng = lng - (2 * M_PI);   // constrainLng
@@ -199,12 +200,12 @@ HM_HD void hex2dToGeoDeg(const H3Tables &T, V2 v, int face, int res, double &lat
         lat = T.faceCenterGeo[face][0];
         lng = T.faceCenterGeo[face][1];
     } else {
-        double theta = atan2(v.y, v.x);
+        double theta = glm::atan2(v.y, v.x, *T.glm);
         for (int i = 0; i < res; i++) r = XMUL(r, RSQRT7);
         r = XMUL(r, ONETHIRD);
         if (res & 1) r = XMUL(r, RSQRT7);
         r *= HM_RES0_U_GNOMONIC;
-        r = atan(r);
+        r = glm::atan(r, *T.glm);
         theta = posAngleRads(T.faceAxesAz0[face] - theta);
         geoAzDistanceFromFace(T, face, theta, r, lat, lng);
     }

@@ -67,6 +67,7 @@ struct hm_ctx {
     DevBuf s_cell, s_ws, s_cnt, s_sp, s_spn, s_lon, s_lat;   // k_merge_owned's rows in per-bin segments (with gaps)
     DevBuf bin_cnt, bin_off;          // k_merge_owned: touched keys per bin, their output offsets
     DevBuf parts_regrow;              // growth: the old tables' keys as partial records
+    DevBuf parts_regrow_sorted;       // growth: the same, partitioned (not parts_sorted: a binned batch's slabs are there)
     DevBuf gapbuf;                    // k_gap_counts / k_fill_gaps: per-bin gap and donor counts + donor offsets
     unsigned long long seq = 0;
     // dedup table (persistent, cleared through its used list)
@@ -424,7 +425,7 @@ static int rp_scan(hm_ctx *ctx, int64_t m) {
 // radix partition of n partial records into RP_BINS bins (one per (window, region)); the sorted copy goes to
 // ctx->parts_sorted, bin b starts at rp_O[b * ntiles]
 // In -> Out: TilePartial -> SortedRec (table mode / stage merge, into parts_sorted), GrowRec -> GrowRec (growth, into
-// parts_sorted), TilePartial -> TilePartial (the owner partition, into the caller's send buffer)
+// parts_regrow_sorted), TilePartial -> TilePartial (the owner partition, into the caller's send buffer)
 template <typename In, typename Out>
 static int partition(hm_ctx *ctx, const In *parts, int64_t n, int64_t &ntiles, int nranks = 0, Out *dst = nullptr) {
     const int nbins = nranks > 0 ? nranks : RP_BINS;
@@ -504,9 +505,9 @@ static RowsOut staged_rows(hm_ctx *ctx) {
 // the batch sequence number kept in the slots' touched words (32 bits, never 0: fresh slots hold 0)
 static unsigned seq32(const hm_ctx *ctx) { return (unsigned)(ctx->seq % 0xffffffffull) + 1u; }
 
-// merge the partitioned records (ctx->parts_sorted) of n_rows staging rows
+// merge the partitioned records (ctx->parts_sorted, or src) of n_rows staging rows
 template <typename Rec>
-static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t slab = 0) {
+static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t slab = 0, const Rec *src = nullptr) {
     constexpr bool rehash = std::is_same<Rec, GrowRec>::value;
     int rc;
     if ((rc = ensure(ctx, ctx->bin_cnt, RP_BINS * 4)) || (rc = ensure(ctx, ctx->bin_off, RP_BINS * 8)))
@@ -538,7 +539,7 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t sla
         resident = need <= tag_bytes && nwin <= MO_RES_MAX && ctx->n_glist <= GC_MAX;
     }
     auto launch = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(MO_THREADS), tag_bytes, ctx->stream, (const Rec *)ctx->parts_sorted.p, slab,
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(MO_THREADS), tag_bytes, ctx->stream, src ? src : (const Rec *)ctx->parts_sorted.p, slab,
                            (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
                            ctx->n_glist, (const WInfo *)ctx->d_winfo, cell_hi_of(ctx->cfg.h3_res), seq32(ctx), staged_rows(ctx),
                            (unsigned *)ctx->bin_cnt.p, ctx->d_st, tag_bytes);
@@ -679,8 +680,11 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census, int mi
         }
         HIPCHK(ctx, hipGetLastError());
         int64_t ntiles;
-        if ((rc = partition<GrowRec, GrowRec>(ctx, (const GrowRec *)ctx->parts_regrow.p, moved, ntiles))) return rc;
-        if ((rc = merge_sorted<GrowRec>(ctx, moved, ntiles))) return rc;
+        if ((rc = ensure(ctx, ctx->parts_regrow_sorted, std::max<int64_t>(moved, 1) * sizeof(GrowRec))) ||
+            (rc = partition<GrowRec, GrowRec>(ctx, (const GrowRec *)ctx->parts_regrow.p, moved, ntiles, 0,
+                                              (GrowRec *)ctx->parts_regrow_sorted.p)) ||
+            (rc = merge_sorted<GrowRec>(ctx, moved, ntiles, 0, (const GrowRec *)ctx->parts_regrow_sorted.p)))
+            return rc;
         HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         for (const auto &g : old)
             if ((rc = table_release(ctx, g.tab, g.log2cap))) return rc;

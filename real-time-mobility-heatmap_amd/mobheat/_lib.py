@@ -209,11 +209,11 @@ def latlng_to_cell_host_selftest(lat, lon, res):
     return out
 
 
-GLIBC_FNS = {"sincos": 0, "acos": 1, "atan2": 2, "tan": 3}
+GLIBC_FNS = {"sincos": 0, "acos": 1, "atan2": 2, "tan": 3, "asin": 4, "atan": 5}
 
 
 def glibc_libm_selftest(fn, a, b=None, device=None):
-    """glibc's sincos (-> (sin, cos)) / acos / atan2(a, b) / tan as csrc/glibc_libm.h restates them, executed on the
+    """glibc's sincos (-> (sin, cos)) / acos / atan2(a, b) / tan / asin / atan as csrc/glibc_libm.h restates them, executed on the
     host (device=None) or on GPU `device`."""
     lib = load()
     a = np.ascontiguousarray(a, dtype=np.float64)

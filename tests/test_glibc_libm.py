@@ -1,5 +1,6 @@
-"""glibc's sincos / acos / atan2 / tan as the exact latLngToCell path restates them (csrc/glibc_libm.h) against the
-running glibc (oracle.h3_oracle.libm, the same libm the reference's h3 calls: heatmap_stream.py:65-75).
+"""glibc's sincos / acos / atan2 / tan (the exact latLngToCell path) and asin / atan (cellToBoundary, with sincos and
+atan2) as csrc/glibc_libm.h restates them, against the running glibc (oracle.h3_oracle.libm, the same libm the
+reference's h3 calls: heatmap_stream.py:65-75, app.py:19-41).
 
 Bar: bit-identical results.  Arguments: >= 1e7 per function over the domain latLngToCell uses (and beyond), plus the
 exact arguments latLngToCell hands glibc for the constructed near-tie inputs of every resolution (cell vertices, edge
@@ -32,6 +33,21 @@ def _args(seed, n):
     y = np.concatenate([y, np.repeat(sp, sp.size), rng.uniform(-1, 1, q)])
     x = np.concatenate([x, np.tile(sp, sp.size), rng.uniform(-1, 1, q)])
     return sc, ac, tn, y, x
+
+
+def _args_boundary(seed, n):
+    """asin over [-1, 1] (every interval of e_asin.c, the Taylor and tiny ranges, 1 - 2^-k), atan over every branch
+    of s_atan.c (|x| < 2^-27 .. 1/16 .. 1 .. 16 .. E and beyond, +-0, +-inf)"""
+    rng = np.random.default_rng(seed)
+    q = n // 4
+    asn = np.concatenate([rng.uniform(-1, 1, q), rng.uniform(0.9, 1, q), -rng.uniform(0.5, 1, q // 2),
+                          1 - np.ldexp(rng.uniform(0, 1, q // 2), rng.integers(-53, -5, q // 2)), rng.uniform(-0.13, 0.13, q // 2),
+                          np.ldexp(rng.uniform(0.5, 1, q // 4), rng.integers(-60, -2, q // 4)),
+                          np.array([1.0, -1.0, 0.0, -0.0, 0.125, 0.25, 0.5, 0.75, 0.921875, 0.953125, 0.96875])])
+    m = 2 * q
+    atn = np.concatenate([rng.standard_normal(m) * np.exp(rng.uniform(-45, 45, m)), rng.uniform(-20, 20, q),
+                          rng.uniform(-1, 1, q // 2), np.array([0.0, -0.0, np.inf, -np.inf, 1.0, -1.0, 16.0, 0.0625, 1e16])])
+    return asn, atn
 
 
 def _same(name, got, exp, args):
@@ -69,6 +85,8 @@ def _near_tie_args():
 def test_host_restatement_equals_glibc_1e7_per_function():
     sc, ac, tn, y, x = _args(7, 14_000_000)
     n = [_check("sincos", sc), _check("acos", ac), _check("tan", tn), _check("atan2", y, x)]
+    asn, atn = _args_boundary(9, 14_000_000)
+    n += [_check("asin", asn), _check("atan", atn)]
     assert min(n) >= 10_000_000, n
 
 
@@ -94,7 +112,9 @@ def test_host_exact_path_equals_oracle_on_near_ties():
 @pytest.mark.gpu
 def test_device_restatement_equals_glibc():
     sc, ac, tn, y, x = _args(8, 14_000_000)
-    for fn, a, b in [("sincos", sc, None), ("acos", ac, None), ("tan", tn, None), ("atan2", y, x)]:
+    asn, atn = _args_boundary(10, 14_000_000)
+    for fn, a, b in [("sincos", sc, None), ("acos", ac, None), ("tan", tn, None), ("atan2", y, x), ("asin", asn, None),
+                     ("atan", atn, None)]:
         _check(fn, a, b, device=0)
     sc, ac, tn, y, x = _near_tie_args()
     for fn, a, b in [("sincos", sc, None), ("acos", ac, None), ("tan", tn, None), ("atan2", y, x)]:

@@ -9,19 +9,8 @@ from oracle import h3_oracle
 
 pytestmark = pytest.mark.gpu
 PENTAGON_BASE_CELLS = [4, 14, 24, 38, 49, 58, 63, 72, 83, 97, 107, 117]
-# boundary coordinates: vertex counts exact; each vertex within 1e-11 degrees of arc (~1 um on the ground) of the
-# glibc-linked oracle's -- the device math library's atan2/atan/asin/sincos may differ from glibc's in the last bits,
-# and asin near +-1 amplifies them (measured on MI355X: up to 1.65e-12 degrees of latitude at res 12).
-# Longitude is compared as ground distance (x cos(lat), modulo 360): near a pole a last-bit difference of the
-# vertex moves its longitude by far more than 1e-12 degrees (a plain longitude test failed on MI355X at res 5 with
-# 1.3e-12 degrees).
-BOUNDARY_TOL_DEG = 1e-11
-
-
-def _arc_diff(la, lo, x, y):
-    """(|dlat|, |dlon| cos(lat)) in degrees of arc, the longitude difference taken modulo 360"""
-    dlo = np.abs((lo - y + 180.0) % 360.0 - 180.0) * np.cos(np.radians(x))
-    return np.abs(la - x), dlo
+# boundary coordinates: bit-identical to the glibc-linked oracle's -- the kernel computes sincos/asin/atan2/atan as
+# glibc's FMA variants do (csrc/glibc_libm.h), and upstream's long double constants with the x87 emulation
 
 
 def _random_cells(res, n, seed):
@@ -43,11 +32,11 @@ def test_cells_to_boundary_matches_oracle(res):
     z = np.maximum(z, 0)
     assert np.array_equal(nv, z)
     m = ~np.isnan(x)
-    dla, dlo = _arc_diff(la[m], lo[m], x[m], y[m])
-    exact = float(((la[m] == x[m]) & (lo[m] == y[m])).mean())
-    print(f"res {res}: {cells.size} cells, {exact:.6f} of the vertices bit-identical to the oracle, "
-          f"max |dlat| {dla.max():.3g} deg, max |dlon| cos(lat) {dlo.max():.3g} deg")
-    assert dla.max() <= BOUNDARY_TOL_DEG and dlo.max() <= BOUNDARY_TOL_DEG
+    assert np.array_equal(np.isnan(la), np.isnan(x)) and np.array_equal(np.isnan(lo), np.isnan(y))
+    bad = np.nonzero((la[m].view(np.uint64) != x[m].view(np.uint64)) | (lo[m].view(np.uint64) != y[m].view(np.uint64)))[0]
+    print(f"res {res}: {cells.size} cells, {int(m.sum())} vertex coordinates, {bad.size} differ from the oracle")
+    assert bad.size == 0, [(float(la[m][i]).hex(), float(x[m][i]).hex(), float(lo[m][i]).hex(), float(y[m][i]).hex())
+                           for i in bad[:4]]
 
 
 def test_boundary_geojson_ring_and_collection():

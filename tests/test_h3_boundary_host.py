@@ -1,7 +1,7 @@
 """CPU: row f4's cellToBoundary (csrc/h3_boundary.h, the read side of reference app.py:19-41) executed on the host
 against the oracle's restatement (oracle/h3_oracle.c oracle_cell_to_boundary), and the oracle against a published
-example.  Host execution uses the host libm, so it must equal the oracle bit for bit; on the GPU the device math
-library's last bits may differ (tests/test_gpu_boundary.py states that tolerance)."""
+example.  The kernel's sincos/asin/atan2/atan are glibc's routines restated (csrc/glibc_libm.h), so its host execution
+equals the glibc-linked oracle bit for bit -- and so does the GPU (tests/test_gpu_boundary.py)."""
 import numpy as np
 import pytest
 

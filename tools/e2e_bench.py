@@ -12,10 +12,13 @@ usage: python tools/e2e_bench.py [--events 100000000] [--steps 4]   (one JSON li
          foreach_batch_func on the raw Kafka `value` column (the producer's JSON records, mbta_to_kafka.py:66-74,
          decoded on the GPU by hm_decode_json) end to end through the same loopback wire sink
        python tools/e2e_bench.py --foreach [--events 10000000]
-         foreach_batch_func end to end: C1 (10k events, the reference's Boston batch) and a
-         uniform batch of --events events (~that many tiles at res 8), as pandas frames, written through the wire
-         sink to a loopback server that acknowledges every OP_MSG (no MongoDB on the box: the server only reads the
-         bytes and replies ok, so the time is the writer's own: frame decode, GPU path, statements, sends).
+         foreach_batch_func end to end in its DEFAULT configuration (state checkpoints on, the state arena sized from
+         the first batch): C1 (10k events, the reference's Boston batch) and a uniform batch of --events events (~that
+         many tiles at res 8), as pandas frames, written (a) through the wire sink to a loopback server that
+         acknowledges every OP_MSG (no MongoDB on the box: the server only reads the bytes and replies ok) and (b) into a
+         null sink that takes the statements and sends nothing, so that the product's own host cost is separated from
+         the loopback server's; per phase (stream.LAST_TIMINGS: columns, process, checkpoint export / wait, encode, sink)
+         and the engine's allocations + frees after the first batch that evicted a window.
 """
 import socket
 import struct
@@ -80,18 +83,35 @@ class LoopbackMongo:
             c.close()
 
 
+class NullSink:
+    """Takes every update command's statements and sends nothing (the product's host cost alone)."""
+
+    def update_statements(self, collection, buf, offs):
+        pass
+
+    def close(self):
+        pass
+
+
 def foreach_mode(a):
+    import tempfile
+
     import pandas as pd
     from mobheat import stream, synth
     srv = LoopbackMongo()
     stream.MONGO_URI = f"mongodb://127.0.0.1:{srv.port}"
-    stream.STATE_CHECKPOINT = False
-    out = {"what": "foreach_batch_func(df, epoch) end to end: pandas frame -> columns -> GPU path (rows stay on the "
-                   "device) -> tile and position statements encoded on the GPU -> OP_MSG frames over TCP to a "
-                   "loopback server that acknowledges each; median of the timed batches"}
-    cases = [("c1", synth.c1_boston(seed=0)), ("uniform", None)]
-    for name, b in cases:
-        n = 10_000 if b is not None else a.events
+    stream.CHECKPOINT_DIR = tempfile.mkdtemp(prefix="mobheat-e2e-")   # (checkpoints ON: the default)
+    out = {"what": "foreach_batch_func(df, epoch) end to end, default configuration (state checkpoints on, state arena "
+                   "auto): pandas frame -> columns -> GPU path (rows stay on the device) -> checkpoint exported, its "
+                   "file written while the tile and position statements (encoded on the GPU) go out as OP_MSG frames "
+                   "over TCP to a loopback server that acknowledges each / into a null sink; median of the timed "
+                   "batches (each batch advances 1 minute: windows re-touched, one evicted every 5 batches)",
+           "checkpoint": stream.STATE_CHECKPOINT, "state_arena": stream.STATE_ARENA}
+    cases = [("c1", synth.c1_boston(seed=0), "wire"), ("uniform", None, "wire"), ("uniform", None, "null")]
+    for name, b, sink_kind in cases:
+        name = f"{name}_{sink_kind}_sink"
+        stream.SINK_FACTORY = NullSink if sink_kind == "null" else stream.MongoSink
+        n = 10_000 if b is not None and name.startswith("c1") else a.events
         if b is None:
             rng = np.random.default_rng(3)
             b = dict(lat=np.degrees(np.arcsin(rng.uniform(-1, 1, n))), lon=rng.uniform(-180, 180, n),
@@ -100,22 +120,34 @@ def foreach_mode(a):
                      row_valid=np.ones(n, bool))
         sp = b["speed"].astype(float).copy()
         sp[~b["speed_valid"]] = np.nan
+        vids = pd.Series(b["vkey"]).map("v{:05d}".format)
         frames = []
         for s in range(a.steps + 1):
-            df = pd.DataFrame({"provider": "mbta", "vehicleId": pd.Series(b["vkey"]).map("v{:05d}".format),
+            df = pd.DataFrame({"provider": "mbta", "vehicleId": vids,
                                "lat": b["lat"], "lon": b["lon"], "speedKmh": pd.Series(sp).astype(object).where(b["speed_valid"], None),
                                "eventTs": pd.to_datetime(b["ts_us"] + s * 60_000_000, unit="us")})
             frames.append(df)
         stream.reset_engine()
-        times = []
+        import shutil
+        shutil.rmtree(stream.CHECKPOINT_DIR, ignore_errors=True)
+        times, phases, allocs = [], [], []
         m0, b0 = srv.messages, srv.bytes
         for s, df in enumerate(frames):
             t = time.perf_counter()
             stream.foreach_batch_func(df, s)
             if s >= 1:
                 times.append(time.perf_counter() - t)
+                phases.append(dict(stream.LAST_TIMINGS))
+            c = stream.get_engine().last_counts()
+            allocs.append(c["allocs"] + c["frees"])
         ms = 1e3 * float(np.median(times))
+        keys = sorted({k for p in phases for k in p})
         out[name] = {"events": n, "ms_per_batch": round(ms, 2), "events_per_s": n / (ms * 1e-3),
+                     "batch_ms": [round(1e3 * x, 1) for x in times],
+                     "phase_ms_median": {k: round(float(np.median([p.get(k, 0.0) for p in phases])), 2) for k in keys},
+                     "checkpoint_frac": round(float(np.median([(p.get("checkpoint_export", 0) + p.get("checkpoint_wait", 0))
+                                                               / (1e3 * t) for p, t in zip(phases, times)])), 3),
+                     "allocs_frees_cumulative": allocs,
                      "messages_per_batch": (srv.messages - m0) / len(frames),
                      "wire_bytes_per_batch": (srv.bytes - b0) / len(frames)}
     stream.reset_engine()
