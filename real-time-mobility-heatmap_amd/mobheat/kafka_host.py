@@ -64,10 +64,10 @@ def _jackson_text(v):
         return str(v)
     if isinstance(v, float):
         return java_double(v)
+    if isinstance(v, _Pairs):   # every pair, duplicates included, in input order (copyCurrentStructure copies tokens)
+        return "{" + ",".join(json.dumps(k, ensure_ascii=False) + ":" + _jackson_value(x) for k, x in v) + "}"
     if isinstance(v, list):
         return "[" + ",".join(_jackson_value(x) for x in v) + "]"
-    if isinstance(v, dict):
-        return "{" + ",".join(json.dumps(k, ensure_ascii=False) + ":" + _jackson_value(x) for k, x in v.items()) + "}"
     raise TypeError(type(v))
 
 
@@ -79,8 +79,12 @@ def _jackson_value(v):
     return _jackson_text(v)
 
 
-def _pairs_keep_last(pairs):
-    return dict(pairs)   # the last duplicate wins, as the device decoder and Jackson's tree for from_json
+class _Pairs(list):
+    """A JSON object as its (key, value) pairs in input order: nested objects are re-serialised token for token."""
+
+
+def _pairs(pairs):
+    return _Pairs(pairs)
 
 
 def decode_record(raw):
@@ -90,11 +94,12 @@ def decode_record(raw):
         i = 0
         while i < len(text) and text[i] in " \t\n\r":
             i += 1
-        obj, _ = json.JSONDecoder(object_pairs_hook=_pairs_keep_last).raw_decode(text, i)
+        obj, _ = json.JSONDecoder(object_pairs_hook=_pairs).raw_decode(text, i)
     except (UnicodeDecodeError, ValueError):
         return None
-    if not isinstance(obj, dict):
+    if not isinstance(obj, _Pairs):
         return None
+    obj = dict(obj)   # the record's own fields: the last duplicate wins, as the device decoder and from_json's parser
     out = {}
     for f, kind in SCHEMA.items():
         v = obj.get(f)

@@ -492,16 +492,29 @@ def _process(eng, epoch_id, cols):
         try:
             res, kb = eng.process_kafka(epoch_id, *cols["kafka"], rows_on_device=True)
             return res, (kb.providers, kb.vehicles)
-        except RuntimeError as e:
-            if getattr(e, "code", None) != _lib.HM_E_UNSUPPORTED:
+        except RuntimeError as err:
+            if getattr(err, "code", None) != _lib.HM_E_UNSUPPORTED:
                 raise
+            e = err
         # a record outside the device decoder's scope: decode the batch on the host (kafka_host) -- one such record
         # must not stop the stream (Spark would replay the same offsets into the same failure)
-        from . import kafka_host
-        cols = batch_columns(kafka_host.decode_table(*cols["kafka"]))
+        cols = _kafka_host_decode(*cols["kafka"], str(e))
     res = eng.process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"], cols["speed_valid"],
                             cols["vkey"], cols["row_valid"], rows_on_device=True)
     return res, (cols["provider_uniques"], cols["vehicle_uniques"])
+
+
+def _kafka_host_decode(values, offsets, why):
+    """The whole batch decoded on the host (kafka_host) -- pure Python per record, so it is logged with its size and
+    time: a stream that keeps producing records outside the device decoder pays this on every batch."""
+    import time
+    import warnings
+    from . import kafka_host
+    t0 = time.perf_counter()
+    cols = batch_columns(kafka_host.decode_table(values, offsets))
+    warnings.warn(f"mobheat: {why}; the batch's {len(offsets) - 1} Kafka values were decoded on the host in "
+                  f"{time.perf_counter() - t0:.2f} s", RuntimeWarning, stacklevel=3)
+    return cols
 
 
 def _kafka_host_columns(eng, values, offsets):
@@ -513,8 +526,7 @@ def _kafka_host_columns(eng, values, offsets):
     except RuntimeError as e:
         if getattr(e, "code", None) != _lib.HM_E_UNSUPPORTED:
             raise
-        from . import kafka_host
-        cols = batch_columns(kafka_host.decode_table(values, offsets))
+        cols = _kafka_host_decode(values, offsets, str(e))
         return cols, (cols["provider_uniques"], cols["vehicle_uniques"])
     b = kb.batch
     n = int(b.n)

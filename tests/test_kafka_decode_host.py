@@ -195,3 +195,14 @@ def test_host_fallback_writes_non_string_values_as_jackson_text():
         assert kafka_host.java_double(v) == want, v
     r = kafka_host.decode_record(b'{"provider":[1,2.5,"x",null,true],"vehicleId":{"k":{"z":-3}},"lat":1,"lon":2,"ts":"2025-10-04"}')
     assert r["provider"] == '[1,2.5,"x",null,true]' and r["vehicleId"] == '{"k":{"z":-3}}'
+
+
+def test_host_decode_keeps_nested_duplicate_keys():
+    """A StringType field holding an object is its JSON text as Jackson's copyCurrentStructure writes it: every token,
+    nested duplicate keys included, in input order; the record's own duplicate fields: the last one wins (from_json)."""
+    from mobheat import kafka_host
+    r = kafka_host.decode_record(b'{"provider":"x","vehicleId":{"a":1,"a":[2,{"d":2,"d":3.5}],"b":{"c":1,"c":true}},'
+                                 b'"lat":1,"lat":2.5,"provider":{"x":1,"x":null}}')
+    assert r["vehicleId"] == '{"a":1,"a":[2,{"d":2,"d":3.5}],"b":{"c":1,"c":true}}'
+    assert r["provider"] == '{"x":1,"x":null}' and r["lat"] == 2.5
+    assert kafka_host.decode_record(b'[{"provider":"x"}]') is None
