@@ -37,7 +37,7 @@ T0 = 1759572000 * 1_000_000
 SPAN_US = 15 * 60 * 1_000_000
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector peak: 1024 SIMDs x 16 FMA lanes x 2 x 2.4 GHz
-SIMDS, CLOCK_HZ = 1024, 2.4e9
+SIMDS = 1024
 
 # Algorithmic HBM bytes of each stage, from the batch's counts (hm_last_counts): n events, R partial
 # records merged (direct path: one per aggregated row), T tiles emitted, E of them keys that existed before the batch
@@ -79,8 +79,8 @@ def s8d(n, c, ms):
 STAGES = ["ingest", "aggregate", "send", "partition", "merge", "emit", "dedup"]
 CONCURRENT_STAGES = ("dedup",)   # side stream (hm_process_batch): its kernel_ms is the side-stream span
 # HBM traffic per dispatch of every kernel and k_ingest's VALU instruction mix per event of this workload, counted by
-# rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r3/kernel_pmc.json).
-PMC_FILE = os.path.join(ROOT, "profiles", "r3", "kernel_pmc.json")
+# rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r4/kernel_pmc.json).
+PMC_FILE = os.path.join(ROOT, "profiles", "r4", "kernel_pmc.json")
 STAGE_KERNELS = {"ingest": ["k_ingest"], "aggregate": ["k_agg", "k_bin_reduce"], "send": ["k_ev_hist", "k_ev_scatter"],
                  "partition": ["k_ev_hist", "k_ev_scatter_rec"], "merge": ["k_merge_owned"], "emit": ["k_fill_gaps"],
                  "dedup": ["k_dedup_flag"]}
@@ -266,11 +266,15 @@ def main():
         # k_ingest is bound by VALU issue and latency, not HBM: its VALU side from the same PMC file
         sec = avg_ms["ingest"] * 1e-3
         tf = pmc["fp64_flops_per_event"] * n / sec / 1e12
-        # VALU issue: SIMD-32 pipes, 2 cycles per wave64 32-bit op, 4 per fp64 op (MI355X_MICROARCH.md)
-        simd_cycles = (pmc["valu_f64_insts_per_event"] * 4 + pmc["valu_other_insts_per_event"] * 2) * n / 64
+        # VALU issue: a wave64 instruction holds its SIMD-32 for 2 cycles (32-bit ops) or 4 (fp64 and 64-bit integer
+        # ops), as tools/microbench/valu_rate measures at saturation (profiles/r4/valu_rate.txt); the cycles are the
+        # PMC dispatch's own (GRBM_GUI_ACTIVE / 8), so the fraction comes from counters of one dispatch only
+        f64, i64 = pmc["valu_f64_wave_insts_per_64_events"], pmc["valu_int64_wave_insts_per_64_events"]
+        simd_cycles = (4 * f64 + 4 * i64 + 2 * pmc["valu_other_wave_insts_per_64_events"]) * n / 64
         roof["ingest_valu"] = {"fp64_tflops": tf, "fp64_peak_tflops": FP64_PEAK_TFLOPS, "fp64_frac": tf / FP64_PEAK_TFLOPS,
-                               "issue_frac": simd_cycles / (SIMDS * CLOCK_HZ * sec),
-                               "valu_insts_per_event": pmc["valu_insts_per_event"],
+                               "issue_frac": simd_cycles / (SIMDS * pmc["dispatch_cycles"]),
+                               "active_inst_valu_per_busy_cu_cycle": pmc["active_inst_valu_per_busy_cu_cycle"],
+                               "valu_wave_insts_per_64_events": pmc["valu_wave_insts_per_64_events"],
                                "fp64_flops_per_event": pmc["fp64_flops_per_event"]}
     step_bytes = sum(kb.values())
     roof.update({"kernel_ms": {k: round(v, 3) for k, v in avg_ms.items()}, "concurrent_stages": list(CONCURRENT_STAGES),

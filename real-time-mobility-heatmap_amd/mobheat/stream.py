@@ -545,8 +545,9 @@ def _kafka_host_columns(eng, values, offsets):
 
 def _foreach_sharded(df, epoch):
     """foreach_batch_func over N_GPUS ranks (mobheat.sharded): every rank merges the keys it owns and encodes the
-    statements of its tiles and of its latest rows; they are written here, tiles first (:159-235), and every rank
-    checkpoints after the writes succeeded.  Replay and failure semantics as the single-GPU path."""
+    statements of its tiles and of its latest rows; they are written here, tiles first (:159-235), while every rank
+    writes its checkpoint (a chain ending at an epoch whose writes failed is never restored from: the replay re-runs
+    that epoch on the state before it).  Replay and failure semantics as the single-GPU path."""
     global _LAST_EPOCH, _PENDING
     from .engine import BatchResult
     sh = get_sharded()

@@ -42,12 +42,22 @@ def main():
         w = sum(cv["WRITE_SIZE"]) / len(cv["WRITE_SIZE"]) * 1024
         kernels[k] = {"dispatches": len(dur[k]), "mean_dispatch_ms": 1e3 * sum(dur[k].values()) / len(dur[k]),
                       "fetch_bytes_raw": f, "write_bytes": w, "hbm_bytes": 2 * f + w}
+    i64 = c.get("SQ_INSTS_VALU_INT64", 0)
+    cycles = c.get("GRBM_GUI_ACTIVE", 0) / 8   # the dispatch's shader cycles (rocprofv3 sums the 8 XCDs)
     d = {"h3_res": a.res, "events_per_dispatch": n,
          "fp64_flops_per_event": flops / n,
          "fp64_flops_per_event_from_inst_counts": lanes / n,
-         "valu_insts_per_event": c.get("SQ_INSTS_VALU", 0) * 64 / n,
-         "valu_f64_insts_per_event": f64_insts * 64 / n,
-         "valu_other_insts_per_event": (c.get("SQ_INSTS_VALU", 0) - f64_insts) * 64 / n,
+         # wave64 VALU instructions per 64 events (= lane-instructions per event)
+         "valu_wave_insts_per_64_events": c.get("SQ_INSTS_VALU", 0) * 64 / n,
+         "valu_f64_wave_insts_per_64_events": f64_insts * 64 / n,
+         "valu_int64_wave_insts_per_64_events": i64 * 64 / n,
+         "valu_other_wave_insts_per_64_events": (c.get("SQ_INSTS_VALU", 0) - f64_insts - i64) * 64 / n,
+         "dispatch_cycles": cycles,
+         # SQ_ACTIVE_INST_VALU counts one per VALU instruction (equal to SQ_INSTS_VALU in every valu_rate dispatch)
+         # and SQ_BUSY_CU_CYCLES CU-cycles: VALU instructions per CU-cycle (ceiling 4 SIMDs / 2 cycles for 32-bit
+         # ops, 4 / 4 for fp64 and 64-bit integer ops)
+         "active_inst_valu_per_busy_cu_cycle": (c.get("SQ_ACTIVE_INST_VALU", 0) / c["SQ_BUSY_CU_CYCLES"]
+                                                if c.get("SQ_BUSY_CU_CYCLES") else None),
          "hbm_bytes_per_event": (fetch + write) / n,
          "hbm_read_bytes_per_event": fetch / n, "hbm_write_bytes_per_event": write / n,
          "mean_dispatch_ms": 1e3 * sum(dur["k_ingest"].values()) / len(dur["k_ingest"]),

@@ -1,0 +1,191 @@
+// Binning 1e8 32-B records into 8192 (window, region) bins on MI355X: the write pattern of k_ingest's fused binning
+// (each lane reserves a slot with a per-bin atomic and writes its record there) against alternatives:
+//   seq      record i -> slot i (the HBM write roofline of the same bytes)
+//   direct   per-record atomic cursor of 8192 bins (k_ingest<true> today)
+//   xcd      per-record atomic cursor of (bin, XCC id): 8 sub-slabs per bin, each written from one XCD only
+//   lds S    per workgroup tile of 2048 records sorted in LDS by S super-bins, one atomic per (tile, super-bin),
+//            the runs written coalesced; then "split": one workgroup per super-bin splits it into its 8192 / S bins
+//            the same way (the second pass of a two-pass radix partition)
+// Records are read from a source array (sequential) and their bin is a hash of the index.
+// Build: hipcc --offload-arch=gfx950 -O3 -o bin_scatter bin_scatter.hip      Run: ./bin_scatter [n]
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+
+#define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+constexpr int BINS = 8192;
+constexpr int T = 2048;   // records per LDS tile
+
+__device__ __forceinline__ uint64_t mixh(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33; return x;
+}
+__device__ __forceinline__ unsigned bin_of(int64_t i) { return (unsigned)(mixh((uint64_t)i) >> 51); }   // 13 bits
+
+__global__ __launch_bounds__(512) void k_seq(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n) {
+    for (int64_t j = (int64_t)blockIdx.x * 512 + threadIdx.x; j < 2 * n; j += (int64_t)gridDim.x * 512) dst[j] = src[j];
+}
+
+template <bool XCD>
+__global__ __launch_bounds__(256) void k_direct(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n,
+                                                unsigned *cur, unsigned cap) {
+    unsigned x = 0;
+    if (XCD) x = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 7u;   // HW_REG_XCC_ID bits [2:0]
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const uint4 a = src[2 * i], b = src[2 * i + 1];
+        const unsigned s = XCD ? bin_of(i) * 8 + x : bin_of(i);
+        const unsigned p = atomicAdd(&cur[s], 1u);
+        if (p < cap) {
+            dst[2 * ((int64_t)s * cap + p)] = a;
+            dst[2 * ((int64_t)s * cap + p) + 1] = b;
+        }
+    }
+}
+
+// tile-sorted binning: the tile's records grouped by bin (shift: bin = hash >> (51 + shift) ... via sel), written as runs
+template <int S>
+__device__ __forceinline__ void tile_bin(const uint4 *__restrict__ src, int64_t r0, int nt, const unsigned *binv,
+                                         uint4 *__restrict__ dst, unsigned *cur, unsigned cap, uint4 *stage,
+                                         unsigned short *binof, unsigned *cnt, unsigned *off, unsigned *gbase) {
+    const int t = threadIdx.x;
+    for (int b = t; b < S; b += 512) cnt[b] = 0;
+    __syncthreads();
+    unsigned bk[T / 512], rk[T / 512];
+#pragma unroll
+    for (int k = 0; k < T / 512; k++) {
+        const int q = t + k * 512;
+        if (q < nt) {
+            bk[k] = binv[q];
+            rk[k] = atomicAdd(&cnt[bk[k]], 1u);
+        }
+    }
+    __syncthreads();
+    // exclusive scan of cnt (S <= 1024: two entries per thread at most), and the global reservations
+    {   // block exclusive scan: E = S / 512 (or 1) consecutive entries per thread, wave scans, 8 wave totals
+        constexpr int E = S >= 512 ? S / 512 : 1;
+        unsigned loc = 0;
+        if (t * E < S)
+            for (int e = 0; e < E; e++) loc += cnt[t * E + e];
+        unsigned inc = loc;
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned y = __shfl_up(inc, d, 64);
+            if ((t & 63) >= d) inc += y;
+        }
+        __shared__ unsigned wtot[8];
+        if ((t & 63) == 63) wtot[t >> 6] = inc;
+        __syncthreads();
+        unsigned wb = 0;
+        for (int w = 0; w < (t >> 6); w++) wb += wtot[w];
+        unsigned ex = wb + inc - loc;
+        if (t * E < S)
+            for (int e = 0; e < E; e++) { off[t * E + e] = ex; ex += cnt[t * E + e]; }
+    }
+    for (int b = t; b < S; b += 512) gbase[b] = cnt[b] ? atomicAdd(&cur[b], cnt[b]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < T / 512; k++) {
+        const int q = t + k * 512;
+        if (q < nt) {
+            const unsigned p = off[bk[k]] + rk[k];
+            stage[2 * p] = src[2 * (r0 + q)];
+            stage[2 * p + 1] = src[2 * (r0 + q) + 1];
+            binof[p] = (unsigned short)bk[k];
+        }
+    }
+    __syncthreads();
+    for (int j = t; j < 2 * nt; j += 512) {
+        const int p = j >> 1;
+        const unsigned b = binof[p];
+        const unsigned g = gbase[b] + (p - off[b]);
+        if (g < cap) dst[2 * ((int64_t)b * cap + g) + (j & 1)] = stage[j];
+    }
+    __syncthreads();
+}
+
+template <int S>
+__global__ __launch_bounds__(512) void k_lds(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n,
+                                             unsigned *cur, unsigned cap) {
+    __shared__ uint4 stage[2 * T];
+    __shared__ unsigned short binof[T];
+    __shared__ unsigned cnt[S], off[S], gbase[S], binv[T];
+    for (int64_t r0 = (int64_t)blockIdx.x * T; r0 < n; r0 += (int64_t)gridDim.x * T) {
+        const int nt = (int)((n - r0) < T ? (n - r0) : T);
+        for (int q = threadIdx.x; q < nt; q += 512) binv[q] = bin_of(r0 + q) >> (13 - __builtin_ctz(S));
+        __syncthreads();
+        tile_bin<S>(src, r0, nt, binv, dst, cur, cap, stage, binof, cnt, off, gbase);
+    }
+}
+
+// second pass: super-bin s (records [s * cap_in, + cnt_in[s])) -> its 8192 / S bins
+template <int S>
+__global__ __launch_bounds__(512) void k_split(const uint4 *__restrict__ src, const unsigned *cnt_in, unsigned cap_in,
+                                               uint4 *__restrict__ dst, unsigned *cur, unsigned cap) {
+    constexpr int SUB = BINS / S;
+    __shared__ uint4 stage[2 * T];
+    __shared__ unsigned short binof[T];
+    __shared__ unsigned cnt[SUB], off[SUB], gbase[SUB], binv[T];
+    const int s = blockIdx.x;
+    const int64_t m = cnt_in[s] < cap_in ? cnt_in[s] : cap_in;
+    const uint4 *in = src + 2 * (int64_t)s * cap_in;
+    for (int64_t r0 = 0; r0 < m; r0 += T) {
+        const int nt = (int)((m - r0) < T ? (m - r0) : T);
+        // (the record's bin would come from its key; here from its first word)
+        for (int q = threadIdx.x; q < nt; q += 512) binv[q] = in[2 * (r0 + q)].x & (SUB - 1);
+        __syncthreads();
+        tile_bin<SUB>(in, r0, nt, binv, dst + 2 * (int64_t)s * SUB * cap, cur + s * SUB, cap, stage, binof, cnt, off, gbase);
+    }
+}
+
+__global__ void k_fill(uint4 *p, int64_t n2) {
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n2; j += (int64_t)gridDim.x * 256)
+        p[j] = make_uint4((unsigned)(mixh(j) & 0xffffffff), 1u, 2u, 3u);
+}
+
+int main(int argc, char **argv) {
+    const int64_t n = argc > 1 ? atoll(argv[1]) : 100000000;
+    const unsigned cap = (unsigned)(n / BINS + n / BINS / 4 + 256);
+    uint4 *src, *dst, *mid;
+    unsigned *cur;
+    CHK(hipMalloc(&src, n * 32));
+    CHK(hipMalloc(&dst, (size_t)BINS * 8 * (cap / 8 + 256) * 32 + (size_t)BINS * cap * 32));
+    CHK(hipMalloc(&mid, (size_t)n * 32 * 2));
+    CHK(hipMalloc(&cur, BINS * 8 * 4));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, src, 2 * n);
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    auto timed = [&](auto launch) {
+        CHK(hipMemset(cur, 0, BINS * 8 * 4));
+        CHK(hipDeviceSynchronize());
+        CHK(hipEventRecord(a));
+        launch();
+        CHK(hipEventRecord(b));
+        CHK(hipEventSynchronize(b));
+        float ms = 0;
+        CHK(hipEventElapsedTime(&ms, a, b));
+        return ms;
+    };
+    const int grid = 256 * 16;
+    for (int rep = 0; rep < 2; rep++) {
+        printf("rep %d seq            %.3f ms\n", rep, timed([&] { hipLaunchKernelGGL(k_seq, dim3(8192), dim3(512), 0, 0, src, dst, n); }));
+        printf("rep %d direct 8192    %.3f ms\n", rep,
+               timed([&] { hipLaunchKernelGGL(k_direct<false>, dim3(grid), dim3(256), 0, 0, src, dst, n, cur, cap); }));
+        printf("rep %d xcd 8192x8     %.3f ms\n", rep,
+               timed([&] { hipLaunchKernelGGL(k_direct<true>, dim3(grid), dim3(256), 0, 0, src, dst, n, cur, cap / 8 + 256); }));
+        auto two = [&](auto kl, auto ks, int S) {
+            const unsigned cap_in = (unsigned)(n / S + n / S / 8 + 4096);
+            const float t1 = timed([&] { hipLaunchKernelGGL(kl, dim3(1024), dim3(512), 0, 0, src, mid, n, cur, cap_in); });
+            unsigned *cnt_in;
+            CHK(hipMalloc(&cnt_in, S * 4));
+            CHK(hipMemcpy(cnt_in, cur, S * 4, hipMemcpyDeviceToDevice));
+            const float t2 = timed([&] { hipLaunchKernelGGL(ks, dim3(S), dim3(512), 0, 0, mid, cnt_in, cap_in, dst, cur, cap); });
+            CHK(hipFree(cnt_in));
+            printf("rep %d lds %4d        %.3f ms + split %.3f ms = %.3f ms\n", rep, S, t1, t2, t1 + t2);
+        };
+        two(k_lds<256>, k_split<256>, 256);
+        two(k_lds<512>, k_split<512>, 512);
+        two(k_lds<1024>, k_split<1024>, 1024);
+    }
+    return 0;
+}
