@@ -50,10 +50,10 @@ SIMDS = 1024
 #                 8192 bin counts)
 #                 merge 32/record read + 113/tile (64-B state line + 49-B row written) + 64/pre-existing key read
 #                 emit 98/gap (a 49-B row moved into a gap; gaps = R - T), dedup 20/event
-#   multi-GPU     send (the sender's partition by owner) 16/event + 57/sent record (speed, speed_valid, lat, lon
-#                           read: 25; 8-B key + 24-B payload written)
-#                 partition (the owner's) 80/received record: census 8 + histogram 8 read, key 8 + payload 24 read,
-#                           the 32-B EventRec written
+#   multi-GPU     (stage API) the sender's records grouped by region field as above -- binned in k_ingest, or the
+#                 partition with one bin per region field -- then send 64/sent record (k_stage_pack: the 32-B record
+#                 read from its bin, written into its destination's chunk); the owner merges each bin from its
+#                 senders' segments: no partition (merge as above over the R records it received)
 #   table mode    aggregate 41/event + 48/record, partition 160/record (48 + 48 read, 64 written), merge 64/record
 #                 read + 113/tile + 64/pre-existing key
 def stage_bytes(n, c, world=1):
@@ -62,12 +62,15 @@ def stage_bytes(n, c, world=1):
     b = {"ingest": 42 * n, "dedup": 20 * n, "emit": 98 * max(R - T, 0), "send": 0}
     if c["table_mode"]:
         b.update(aggregate=41 * n + 48 * R, partition=160 * R, merge=64 * R + 113 * T + 64 * E)
-    elif c.get("binned"):
-        b.update(ingest=51 * n + 32 * R, aggregate=0, partition=0, merge=32 * R + 113 * T + 64 * E)
-    elif world > 1:
-        b.update(aggregate=0, send=16 * n + 57 * c["sent"], partition=80 * R, merge=32 * R + 113 * T + 64 * E)
+        return b
+    S = c["sent"] if world > 1 else R   # records this rank grouped (and sent)
+    b.update(aggregate=0, merge=32 * R + 113 * T + 64 * E)
+    if c.get("binned"):
+        b.update(ingest=51 * n + 32 * S, partition=0)
     else:
-        b.update(aggregate=0, partition=16 * n + 57 * R, merge=32 * R + 113 * T + 64 * E)
+        b.update(partition=16 * n + 57 * S)
+    if world > 1:
+        b["send"] = 64 * S
     return b
 
 
@@ -81,7 +84,7 @@ CONCURRENT_STAGES = ("dedup",)   # side stream (hm_process_batch): its kernel_ms
 # HBM traffic per dispatch of every kernel and k_ingest's VALU instruction mix per event of this workload, counted by
 # rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r4/kernel_pmc.json).
 PMC_FILE = os.path.join(ROOT, "profiles", "r4", "kernel_pmc.json")
-STAGE_KERNELS = {"ingest": ["k_ingest"], "aggregate": ["k_agg", "k_bin_reduce"], "send": ["k_ev_hist", "k_ev_scatter"],
+STAGE_KERNELS = {"ingest": ["k_ingest"], "aggregate": ["k_agg", "k_bin_reduce"], "send": ["k_stage_pack"],
                  "partition": ["k_ev_hist", "k_ev_scatter_rec"], "merge": ["k_merge_owned"], "emit": ["k_fill_gaps"],
                  "dedup": ["k_dedup_flag"]}
 
@@ -156,7 +159,8 @@ def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, ar
     from mobheat.distributed import LibStages, ShardedHeatmap
     total_steps = args.warmup + args.steps
     data = gen_batch(n, total_steps, seed=seed, dev=dev, span_us=span_us, advance_us=advance_us)
-    eng = mobheat.HeatmapEngine(h3_res=res, device=local, batch_capacity_hint=n, state_arena_bytes=arena_bytes)
+    eng = mobheat.HeatmapEngine(h3_res=res, device=local, batch_capacity_hint=n, state_arena_bytes=arena_bytes,
+                                shard=(rank, world) if world > 1 else None)
     sharded = ShardedHeatmap(LibStages(eng), dev) if world > 1 else None
 
     def step(s):

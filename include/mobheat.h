@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 9
+#define HM_ABI_VERSION 10
 
 /* error codes */
 #define HM_OK 0
@@ -63,6 +63,10 @@ typedef struct hm_config {
     int64_t batch_capacity_hint;    /* expected max events per batch (0 = grow on demand) */
     int64_t state_arena_bytes;      /* device memory reserved (and zeroed) at create for the window tables; tables
                                        are carved from it before any allocation in a batch (0 = none) */
+    int32_t shard_rank;             /* multi-GPU: this context is rank shard_rank of shard_count (the stage API); its
+                                       state holds only the keys that rank owns.  shard_count 0 = not fixed at create
+                                       (the first hm_stage_ingest fixes it), 1 = a single GPU */
+    int32_t shard_count;
 } hm_config;
 
 /* One micro-batch of raw events, structure of arrays. All arrays have n entries.
@@ -140,31 +144,34 @@ int64_t hm_latlng_to_cell_last_exact(int32_t device);
  *    summary (HM_STAGE_SUMMARY_WORDS int64 words, host memory) for the caller to all-gather.
  * 2. hm_stage_send(all ranks' summaries, [nranks][HM_STAGE_SUMMARY_WORDS], rank-major): every rank derives the
  *    same batch-wide decisions from them -- the global max event time (the watermark's input, :107), the
- *    aggregation path and the batch's global window registry -- and writes its records grouped by owner rank
- *    (a function of the key's hash) into the caller's send buffers, with per-destination counts (host arrays of
- *    nranks entries):
- *      direct path (sizes.table_mode == 0): one record per aggregated row, 32 B on the wire, as two streams:
- *        tile stream    8 B per row: the cell's low 52 bits | (1 + the window's global registry slot) << 52
- *        payload stream 24 B per row: speed bits (null = 0x7ff0000000000001, NaN canonical), f64 lat, f64 lon
- *      table mode (sizes.table_mode == 1, low-cardinality batches): the tile stream holds 48-B tile partials,
- *        one per key of the rank's shard: u64 cell, i64 window_start_us, u32 count, u32 n_speed, f64 sum_speed,
- *        f64 sum_lat, f64 sum_lon; the payload stream is unused;
- *      latest candidates, 32 B: u64 vkey, i64 ts_us, i64 row, i64 origin_rank.
- *    Capacities are in records; tile_send_buf >= 48 B and payload_send_buf >= 24 B per event of the rank's batch,
- *    cand_send_buf >= 32 B per event are always enough.
- * 3. caller: all_to_all of the three streams (record counts per destination as returned).
- * 4. hm_stage_merge: the owner merges the received tile records into the persistent state it owns, emits the
- *    tiles it owns, reduces the received candidates to winners, and writes the winners' row indices grouped by
- *    origin rank into winner_send_buf (capacity >= n_cand_recv) with per-origin counts.
+ *    aggregation path and the batch's global window registry -- and writes ONE chunk per destination rank into the
+ *    caller's device send buffer (send_cap bytes; hm_stage_send_capacity(n, nranks) bytes are always enough), its
+ *    size in bytes into send_bytes[r].  A tile key's destination owns a contiguous range of the key hash's 13-bit
+ *    region field (rank r: [ceil(r 8192 / nranks), ceil((r + 1) 8192 / nranks))); a candidate's is a hash of its
+ *    vkey.  Chunk (little-endian, every part 32-B aligned):
+ *      header, 8 int64: magic 0x314b4e5548434d48, records, candidates, record bytes, bins, records offset,
+ *        candidates offset, chunk bytes
+ *      direct path (sizes.table_mode == 0): u32 counts[bins] (the records of each region field the destination
+ *        owns, in order), u32 census[4096] (records per global window slot), then one 32-B record per aggregated
+ *        row, grouped by region field: u64 cell's low 52 bits | (1 + the window's global registry slot) << 52,
+ *        speed bits (null = 0x7ff0000000000001, NaN canonical), f64 lat, f64 lon;
+ *      table mode (sizes.table_mode == 1, low-cardinality batches): bins = 0, one 48-B tile partial per key of the
+ *        rank's shard: u64 cell, i64 window_start_us, u32 count, u32 n_speed, f64 sum_speed, f64 sum_lat, f64 sum_lon;
+ *      then the latest candidates, 32 B: u64 vkey, i64 ts_us, i64 row, i64 origin_rank.
+ * 3. caller: one all_to_all of the chunks (sizes first); recv_buf holds the chunks of ranks 0..nranks-1 in order.
+ * 4. hm_stage_merge: the owner merges the received tile records into the persistent state it owns (each of its
+ *    (window, region) bins from its senders' segments: no second partition), emits the tiles it owns, reduces the
+ *    received candidates to winners, and writes the winners' row indices grouped by origin rank into
+ *    winner_send_buf (capacity >= the candidates received) with per-origin counts.
  * 5. caller: exchange winners back; hm_stage_finish takes the received winners (rows of this rank).
  * After hm_stage_merge the owner's tiles can be encoded (hm_last_windows, hm_encode_tile_updates); after hm_stage_finish
  * the rank's latest rows can (hm_last_latest_buckets, hm_encode_position_updates, with the batch's dictionaries): every
  * rank writes the statements of what it owns, so no statement crosses the exchange.  A device caller keeps its input
- * buffers until then. */
+ * buffers until then.  A context serves one rank of one world size (hm_config.shard_rank / shard_count, or fixed by
+ * its first hm_stage_ingest): its tables hold that rank's keys only. */
 #define HM_STAGE_SUMMARY_WORDS 8200
 #define HM_TILE_REC_BYTES 48
-#define HM_TILE_KEY_BYTES 8
-#define HM_TILE_PAYLOAD_BYTES 24
+#define HM_EVENT_REC_BYTES 32
 #define HM_CAND_REC_BYTES 32
 typedef struct hm_stage_sizes {
     int64_t table_mode;                  /* the batch's aggregation path (the same on every rank) */
@@ -176,11 +183,10 @@ typedef struct hm_stage_sizes {
 
 int hm_stage_ingest(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t nranks, int32_t rank,
                     int64_t *summary);
-int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *tile_send_buf, void *payload_send_buf,
-                  int64_t tile_send_cap, int64_t *tile_send_counts, void *cand_send_buf, int64_t cand_send_cap,
-                  int64_t *cand_send_counts, hm_stage_sizes *sizes);
-int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, const void *payload_recv_dev, int64_t n_tile_recv,
-                   const void *cand_recv_dev, int64_t n_cand_recv, int32_t out_memory, hm_batch_out *out,
+int64_t hm_stage_send_capacity(int64_t n_rows, int32_t nranks);
+int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *send_buf, int64_t send_cap, int64_t *send_bytes,
+                  hm_stage_sizes *sizes);
+int hm_stage_merge(hm_ctx *ctx, const void *recv_buf, const int64_t *recv_bytes, int32_t out_memory, hm_batch_out *out,
                    void *winner_send_buf, int64_t winner_send_cap, int64_t *winner_send_counts);
 int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_recv, int32_t out_memory,
                     hm_batch_out *out);

@@ -12,6 +12,11 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     // (windows of at least a second: TILE_MINUTES is whole minutes in the reference, heatmap_stream.py:29; the
     // window registry's LDS cache relies on |ts / tile_us| < 2^51)
     if (cfg->tile_us < 1000000 || cfg->watermark_delay_ms < 0) { g_create_err = "bad tile/watermark"; return HM_E_INVALID; }
+    if (cfg->shard_count < 0 || cfg->shard_count > 64 || cfg->shard_rank < 0 ||
+        (cfg->shard_count > 0 && cfg->shard_rank >= cfg->shard_count) || (cfg->shard_count == 0 && cfg->shard_rank != 0)) {
+        g_create_err = "bad shard_rank/shard_count";
+        return HM_E_INVALID;
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         (void)hipGetLastError();
@@ -22,6 +27,8 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     hm_ctx *ctx = new hm_ctx();
     ctx->cfg = *cfg;
     ctx->device = cfg->device;
+    ctx->shard_rank = cfg->shard_rank;
+    ctx->shard_count = cfg->shard_count;
     auto fail = [&](const char *what) {
         g_create_err = std::string(what) + ": " + ctx->err;
         hm_destroy(ctx);
@@ -42,7 +49,10 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         hipFuncSetAttribute((const void *)k_merge_owned<EventRec, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
         hipFuncSetAttribute((const void *)k_merge_owned<SortedRec, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
         hipFuncSetAttribute((const void *)k_merge_owned<SortedRec, false>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
-        hipFuncSetAttribute((const void *)k_merge_owned<SortedRec, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess) {
+        hipFuncSetAttribute((const void *)k_merge_owned<SortedRec, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_merge_owned<EventRec, false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_merge_owned<EventRec, true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
+        hipFuncSetAttribute((const void *)k_merge_owned<EventRec, true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess) {
         ctx->err = "merge LDS attribute";
         return fail("create");
     }
@@ -134,10 +144,10 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     // state_capacity_hint: one window table for that many keys, reserved now into the pool (a 70-GB table costs
     // ~2 s in hipMalloc: C5's first batch)
     if (cfg->state_capacity_hint > 0) {
-        int L = ilog2(next_pow2((uint64_t)std::max<int64_t>(2 * cfg->state_capacity_hint, 1024)));
-        unsigned rb = 0;
+        Geo geo{};
+        geo.log2cap = ilog2(next_pow2((uint64_t)std::max<int64_t>(2 * cfg->state_capacity_hint, 1024)));
         TileSlot *t = nullptr;
-        if (table_acquire(ctx, L, rb, &t) || table_release(ctx, t, L)) return fail("create");
+        if (table_acquire(ctx, geo, &t) || table_release(ctx, t, geo.log2cap)) return fail("create");
     }
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) { ctx->err = "sync"; return fail("create"); }
     *out = ctx;
@@ -151,7 +161,8 @@ void hm_destroy(hm_ctx *ctx) {
     if (ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
     DevBuf *bufs[] = {&ctx->in_lat, &ctx->in_lon, &ctx->in_ts, &ctx->in_speed, &ctx->in_sv, &ctx->in_vkey, &ctx->in_rv,
                       &ctx->cell, &ctx->wstart, &ctx->flags, &ctx->win, &ctx->rows, &ctx->block_counts, &ctx->block_offs,
-                      &ctx->partials, &ctx->cands, &ctx->slow, &ctx->parts_sorted, &ctx->parts_regrow, &ctx->parts_regrow_sorted, &ctx->rp_H, &ctx->rp_O,
+                      &ctx->partials, &ctx->cands, &ctx->slow, &ctx->parts_sorted, &ctx->parts_regrow, &ctx->parts_regrow_sorted, &ctx->stage_meta, &ctx->stage_C, &ctx->stage_P,
+                      &ctx->stage_SO, &ctx->stage_SP, &ctx->stage_T, &ctx->cands_recv, &ctx->stage_tmp, &ctx->rp_H, &ctx->rp_O,
                       &ctx->rp_btot, &ctx->rp_boff,
                       &ctx->s_cell, &ctx->s_ws, &ctx->s_cnt, &ctx->s_sp, &ctx->s_spn, &ctx->s_lon, &ctx->s_lat, &ctx->bin_cnt, &ctx->bin_off, &ctx->dfused.used, &ctx->dfull.used, &ctx->o_cell, &ctx->o_ws, &ctx->o_cnt, &ctx->o_sp, &ctx->o_spn,
                       &ctx->o_lon, &ctx->o_lat, &ctx->td_sizes, &ctx->td_off, &ctx->td_btot, &ctx->td_boff, &ctx->td_bytes,
@@ -231,6 +242,9 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if (in->n > MAX_BATCH_ROWS) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds %lld", (long long)in->n, (long long)MAX_BATCH_ROWS);
     if (in->n > 0 && (!in->lat || !in->lon || !in->ts_us || !in->vkey))
         return set_err(ctx, HM_E_INVALID, "lat, lon, ts_us and vkey are required");
+    if (ctx->shard_count > 1)
+        return set_err(ctx, HM_E_STATE, "a context of shard %d of %d runs the stage API (its state is that shard's keys)",
+                       ctx->shard_rank, ctx->shard_count);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     host_batch_begin(ctx);
     const BatchClock clock_(ctx);

@@ -16,6 +16,14 @@ int hm_stage_ingest(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_
     if (in->n > MAX_BATCH_ROWS) return set_err(ctx, HM_E_INVALID, "batch of %lld events exceeds %lld", (long long)in->n, (long long)MAX_BATCH_ROWS);
     if (in->n > 0 && (!in->lat || !in->lon || !in->ts_us || !in->vkey))
         return set_err(ctx, HM_E_INVALID, "lat, lon, ts_us and vkey are required");
+    if (ctx->shard_count == 0 && ctx->gens.empty()) {   // (fixed by the first batch; a context holding state keeps its own)
+        ctx->shard_rank = rank;
+        ctx->shard_count = nranks;
+    }
+    if (ctx->shard_count != nranks && !(ctx->shard_count <= 1 && nranks == 1))
+        return set_err(ctx, HM_E_STATE, "the context is shard %d of %d, not %d of %d", ctx->shard_rank, ctx->shard_count, rank, nranks);
+    if (ctx->shard_count > 1 && ctx->shard_rank != rank)
+        return set_err(ctx, HM_E_STATE, "the context is shard %d of %d, not %d of %d", ctx->shard_rank, ctx->shard_count, rank, nranks);
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc;
     ctx->stage = 0;
@@ -27,7 +35,7 @@ int hm_stage_ingest(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_
     Inputs I;
     I.n = in->n;
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
-    if ((rc = phase_local(ctx, I, late_wm))) return rc;
+    if ((rc = phase_local(ctx, I, late_wm, true))) return rc;   // (large batches: bins of region fields, fused)
     const DevStats s1 = *ctx->h_st;
     ctx->stage_I = I;
     ctx->stage_s1 = s1;
@@ -96,15 +104,37 @@ static int stage_decide(hm_ctx *ctx, const int64_t *sums) {
     return HM_OK;
 }
 
-int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *tile_send_buf, void *payload_send_buf, int64_t tile_send_cap,
-                  int64_t *tile_send_counts, void *cand_send_buf, int64_t cand_send_cap, int64_t *cand_send_counts,
+int64_t hm_stage_send_capacity(int64_t n_rows, int32_t nranks) {
+    if (n_rows < 0 || nranks < 1) return 0;
+    // records (<= 48 B) and candidates (32 B) of every row, per chunk its header, counts, census and alignment
+    return n_rows * (HM_TILE_REC_BYTES + HM_CAND_REC_BYTES) + (int64_t)nranks * (sizeof(ChunkHdr) + 96 + CENSUS_WORDS * 4) +
+           (int64_t)RP_BINS * 4;
+}
+
+// chunk layouts of this rank's send: records and candidates per destination -> headers, starts, total bytes
+static int stage_layout(hm_ctx *ctx, const int64_t *recs, const int64_t *cands, bool table, int64_t cap,
+                        std::vector<ChunkHdr> &hdr, std::vector<int64_t> &start, int64_t *send_bytes) {
+    const int W = ctx->nranks;
+    hdr.resize(W);
+    start.resize(W + 1);
+    int64_t off = 0;
+    for (int o = 0; o < W; o++) {
+        const int64_t bins = table ? 0 : (int64_t)(shard_lo(o + 1, W) - shard_lo(o, W));
+        hdr[o] = chunk_layout(recs[o], cands[o], table ? (int64_t)sizeof(TilePartial) : (int64_t)sizeof(EventRec), bins);
+        start[o] = off;
+        send_bytes[o] = hdr[o].bytes;
+        off += hdr[o].bytes;
+    }
+    start[W] = off;
+    if (off > cap) return set_err(ctx, HM_E_INVALID, "send buffer of %lld bytes too small (%lld needed)", (long long)cap, (long long)off);
+    return HM_OK;
+}
+
+int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *send_buf, int64_t send_cap, int64_t *send_bytes,
                   hm_stage_sizes *sizes) {
-    if (!ctx || !summaries || !tile_send_counts || !cand_send_counts)
-        return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (!ctx || !summaries || !send_bytes || send_cap < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
     if (ctx->stage != 1) return set_err(ctx, HM_E_STATE, "hm_stage_send before hm_stage_ingest");
     const Inputs &I = ctx->stage_I;
-    if (I.n > 0 && (!tile_send_buf || !payload_send_buf || !cand_send_buf))
-        return set_err(ctx, HM_E_INVALID, "send buffers are required");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc;
     const int W = ctx->nranks;
@@ -120,17 +150,51 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *tile_send_buf, vo
     if (table && (rc = phase_table(ctx, I, n_agg, &n_records))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     ctx->census_ready = false;   // (the owner counts what it receives)
-    // local dedup over rows -> local winners -> candidates
+    // local dedup over rows -> local winners -> candidates, counted per owner
     if ((rc = phase_dedup(ctx, &I, nullptr, I.n, s1.dedup_retry != 0))) return rc;
     if ((rc = ensure(ctx, ctx->cands, std::max<int64_t>(I.n, 1) * sizeof(Cand)))) return rc;
     hipLaunchKernelGGL(k_make_cands, dim3(grid_for(std::max<int64_t>(I.n, 1), 256)), dim3(256), 0, ctx->stream,
                        (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, I.vk, I.ts, ctx->rank, (Cand *)ctx->cands.p);
     HIPCHK(ctx, hipGetLastError());
-    // partition both record kinds by owner rank: candidates by counts + cursors here, tile records below
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch, 0, 128 * 8, ctx->stream));
     const int gb = grid_for(std::max<int64_t>(I.n, 1), 256);
     hipLaunchKernelGGL(k_part_count<Cand>, dim3(gb), dim3(256), 0, ctx->stream, (const Cand *)ctx->cands.p, ctx->d_scratch + 255,
                        W, ctx->d_scratch + 64);
+    HIPCHK(ctx, hipGetLastError());
+    // the tile records grouped by destination: table mode, the partials partitioned by owner (stage_tmp); direct path,
+    // the records grouped by region field -- k_ingest's slabs, or the partition with one bin per region field -- whose
+    // destinations are contiguous ranges of bins
+    HIPCHK(ctx, hipEventRecord(ctx->ev[8], ctx->stream));
+    int64_t stride = 1, slab = 0;
+    if (table) {
+        if ((rc = ensure(ctx, ctx->stage_tmp, std::max<int64_t>(n_records, 1) * sizeof(TilePartial)))) return rc;
+        int64_t ntiles = 1;
+        if (n_records > 0) {
+            if ((rc = partition<TilePartial, TilePartial>(ctx, (const TilePartial *)ctx->partials.p, n_records, ntiles, W,
+                                                          (TilePartial *)ctx->stage_tmp.p)))
+                return rc;
+            hipLaunchKernelGGL(k_digit_starts, dim3(1), dim3(128), 0, ctx->stream, (const unsigned long long *)ctx->rp_O.p, ntiles,
+                               W + 1, ctx->d_scratch + 128);
+        } else {
+            HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + 128, 0, (W + 1) * 8, ctx->stream));
+        }
+    } else if (I.n > 0) {
+        if (ctx->binned) {   // k_ingest's slabs: bin b's records at b * slab_cap, its count in bin_cur[b]
+            slab = ctx->slab_cap;
+            if ((rc = ensure(ctx, ctx->rp_O, (RP_BINS + 1) * 8)) ||
+                (rc = scan_counts(ctx, (const unsigned *)ctx->bin_cur.p, RP_BINS + 1, (unsigned long long *)ctx->rp_O.p)))
+                return rc;
+        } else {             // the partition with one bin per region field (WInfo without table geometry: binp 0)
+            int64_t ntiles;
+            if ((rc = winfo_upload(ctx, false)) || (rc = ev_partition(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, ntiles)))
+                return rc;
+            stride = ntiles;
+        }
+        hipLaunchKernelGGL(k_shard_starts, dim3(1), dim3(128), 0, ctx->stream, (const unsigned long long *)ctx->rp_O.p, stride, W,
+                           ctx->d_scratch + 128);
+    } else {
+        HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + 128, 0, (W + 1) * 8, ctx->stream));
+    }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, 256 * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_st, ctx->d_st, sizeof(DevStats), hipMemcpyDeviceToHost, ctx->stream));
@@ -138,60 +202,69 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *tile_send_buf, vo
     if (ctx->h_st->overflow) return set_err(ctx, HM_E_OVERFLOW, "device hash table overflow");
     if (ctx->h_st->bad_vkey) return set_err(ctx, HM_E_INVALID, "vkey UINT64_MAX is reserved");
     ctx->dedup_seen = (int64_t)ctx->h_scratch[ctx->dlast->used_word];
-    if (n_records > tile_send_cap || (int64_t)ctx->h_scratch[255] > cand_send_cap)
-        return set_err(ctx, HM_E_INVALID, "send buffer too small (%lld tile records, %llu candidates)", (long long)n_records,
-                       ctx->h_scratch[255]);
-    // candidates: exclusive offsets -> cursors
-    unsigned long long cur[128];
-    unsigned long long acc = 0;
-    for (int r = 0; r < W; r++) { cur[64 + r] = acc; cand_send_counts[r] = (int64_t)ctx->h_scratch[64 + r]; acc += ctx->h_scratch[64 + r]; }
-    HIPCHK(ctx, hipMemcpyAsync(ctx->d_scratch + 64, cur + 64, 64 * 8, hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_part_scatter<Cand>, dim3(gb), dim3(256), 0, ctx->stream, (const Cand *)ctx->cands.p, ctx->d_scratch + 255,
-                       W, ctx->d_scratch + 64, (Cand *)cand_send_buf);
-    HIPCHK(ctx, hipGetLastError());
-    // tile records: the radix partition with the owner rank as the digit, straight into the send streams
-    HIPCHK(ctx, hipEventRecord(ctx->ev[8], ctx->stream));
-    if (n_records > 0) {
-        int64_t ntiles;
-        if (table) {
-            if ((rc = partition<TilePartial, TilePartial>(ctx, (const TilePartial *)ctx->partials.p, n_records, ntiles, W,
-                                                          (TilePartial *)tile_send_buf)))
-                return rc;
-        } else {
-            // this rank's registry slots -> the batch's global slots (WInfo.gslot), keys rewritten by the scatter
-            ctx->stage_gslot.assign(WREG_SLOTS, 0u);
-            for (int w = 0; w < WREG_SLOTS; w++) {
-                const unsigned long long we = ctx->h_wreg[w];
-                if (!we) continue;
-                const auto it = std::find(ctx->stage_gwreg.begin(), ctx->stage_gwreg.end(), we);
-                if (it == ctx->stage_gwreg.end() && ctx->h_wcount[w])
-                    return set_err(ctx, HM_E_STATE, "a window of this rank is missing from the global registry");
-                ctx->stage_gslot[w] = (unsigned)(it - ctx->stage_gwreg.begin());
-            }
-            rc = winfo_upload(ctx, false);
-            ctx->stage_gslot.clear();
-            if (rc || (rc = ev_partition<WireKey>(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, nullptr, ntiles, W,
-                                                  (WireKey *)tile_send_buf, (uint64_t *)payload_send_buf)))
-                return rc;
+    std::vector<int64_t> recs(W), cands(W);
+    int64_t n_sent = 0;
+    for (int o = 0; o < W; o++) {
+        recs[o] = (int64_t)(ctx->h_scratch[128 + o + 1] - ctx->h_scratch[128 + o]);
+        cands[o] = (int64_t)ctx->h_scratch[64 + o];
+        n_sent += recs[o];
+    }
+    std::vector<ChunkHdr> hdr;
+    std::vector<int64_t> start;
+    if ((rc = stage_layout(ctx, recs.data(), cands.data(), table, send_cap, hdr, start, send_bytes))) return rc;
+    if (start[W] > 0 && !send_buf) return set_err(ctx, HM_E_INVALID, "send buffer is required");
+    // headers, the local -> global window slot map, chunk starts -> device
+    const size_t meta = (size_t)W * sizeof(ChunkHdr) + (size_t)(W + 1) * 8 + WREG_SLOTS * sizeof(unsigned short);
+    if ((rc = ensure(ctx, ctx->stage_meta, meta))) return rc;
+    std::vector<uint8_t> hm(meta);
+    memcpy(hm.data(), hdr.data(), (size_t)W * sizeof(ChunkHdr));
+    memcpy(hm.data() + (size_t)W * sizeof(ChunkHdr), start.data(), (size_t)(W + 1) * 8);
+    unsigned short *gmap = (unsigned short *)(hm.data() + (size_t)W * sizeof(ChunkHdr) + (size_t)(W + 1) * 8);
+    for (int w = 0; w < WREG_SLOTS; w++) {
+        gmap[w] = 0;
+        const unsigned long long we = ctx->h_wreg[w];
+        if (!we) continue;
+        const auto it = std::find(ctx->stage_gwreg.begin(), ctx->stage_gwreg.end(), we);
+        if (it == ctx->stage_gwreg.end()) {
+            if (ctx->h_wcount[w]) return set_err(ctx, HM_E_STATE, "a window of this rank is missing from the global registry");
+            continue;
         }
-        hipLaunchKernelGGL(k_digit_starts, dim3(1), dim3(128), 0, ctx->stream, (const unsigned long long *)ctx->rp_O.p, ntiles,
-                           W + 1, ctx->d_scratch);
+        gmap[w] = (unsigned short)(it - ctx->stage_gwreg.begin());
+    }
+    HIPCHK(ctx, hipMemcpyAsync(ctx->stage_meta.p, hm.data(), meta, hipMemcpyHostToDevice, ctx->stream));
+    const ChunkHdr *d_hdr = (const ChunkHdr *)ctx->stage_meta.p;
+    const int64_t *d_start = (const int64_t *)((uint8_t *)ctx->stage_meta.p + (size_t)W * sizeof(ChunkHdr));
+    const unsigned short *d_gmap = (const unsigned short *)((uint8_t *)ctx->stage_meta.p + (size_t)W * sizeof(ChunkHdr) + (size_t)(W + 1) * 8);
+    uint8_t *out = (uint8_t *)send_buf;
+    if (start[W] > 0) {
+        hipLaunchKernelGGL(k_stage_chunk_init, dim3(W), dim3(256), 0, ctx->stream, d_hdr, d_start, out);
+        if (table) {
+            for (int o = 0, first = 0; o < W; o++) {
+                if (recs[o])
+                    HIPCHK(ctx, hipMemcpyAsync(out + start[o] + hdr[o].recs_off, (const TilePartial *)ctx->stage_tmp.p + first,
+                                               recs[o] * sizeof(TilePartial), hipMemcpyDeviceToDevice, ctx->stream));
+                first += (int)recs[o];
+            }
+        } else if (n_sent > 0) {
+            hipLaunchKernelGGL(k_stage_pack, dim3(RP_BINS), dim3(256), 0, ctx->stream, (const EventRec *)ctx->parts_sorted.p, slab,
+                               (const unsigned long long *)ctx->rp_O.p, stride, d_gmap, W, d_start, out);
+        }
+        // candidates: per-destination cursors (in Cand units) into the chunks
+        unsigned long long cur[64];
+        for (int o = 0; o < W; o++) cur[o] = (unsigned long long)((start[o] + hdr[o].cands_off) / (int64_t)sizeof(Cand));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_scratch + 64, cur, W * 8, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_part_scatter<Cand>, dim3(gb), dim3(256), 0, ctx->stream, (const Cand *)ctx->cands.p, ctx->d_scratch + 255,
+                           W, ctx->d_scratch + 64, (Cand *)out);
         HIPCHK(ctx, hipGetLastError());
-        HIPCHK(ctx, hipMemcpyAsync(ctx->h_scratch, ctx->d_scratch, (W + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[9], ctx->stream));
-    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
-    for (int r = 0; r < W; r++) {
-        const int64_t start = n_records > 0 ? (int64_t)ctx->h_scratch[r] : 0;
-        const int64_t end = n_records > 0 ? (int64_t)ctx->h_scratch[r + 1] : 0;   // [W]: the gaps' digit
-        tile_send_counts[r] = end - start;
-    }
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));   // (the caller's collective reads the buffer on its own stream)
     ctx->stage_agg_rows = n_agg;
-    ctx->stage_sent = n_records;
+    ctx->stage_sent = n_sent;
     hm_stage_sizes z{};
     z.table_mode = table ? 1 : 0;
-    z.n_tile_records = n_records;
-    for (int r = 0; r < W; r++) z.n_cands += cand_send_counts[r];
+    z.n_tile_records = n_sent;
+    for (int o = 0; o < W; o++) z.n_cands += cands[o];
     z.global_batch_max_event_ms = ctx->stage_gmax_ms;
     z.n_valid = (int64_t)s1.n_valid;
     z.n_late = (int64_t)s1.n_late;
@@ -201,57 +274,119 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *tile_send_buf, vo
     return HM_OK;
 }
 
-// the multi-GPU owner's direct path: the received key + payload streams (n rows of all ranks) -> census per global
-// window -> window tables -> (window, region) partition into EventRecs -> merge -> rows
-static int merge_received_events(hm_ctx *ctx, const uint64_t *keys, const uint64_t *payload, int64_t n) {
+// the multi-GPU owner's direct path: every sender's chunk holds the records of the owner's region fields in order
+// (counts per field) -> census per global window -> window tables (range geometry) -> each bin merged from its
+// senders' segments -> rows
+static int merge_received_chunks(hm_ctx *ctx, const uint8_t *recv, const int64_t *d_off, const std::vector<ChunkHdr> &hdr,
+                                 int64_t n) {
     int rc;
+    const int W = ctx->nranks;
     if (n > MAX_BATCH_ROWS) return set_err(ctx, HM_E_INVALID, "%lld received records exceed %lld", (long long)n, (long long)MAX_BATCH_ROWS);
     ctx->n_partials_merged = n;
     if ((rc = merge_begin(ctx, n))) return rc;
     if (n == 0) return merge_nothing(ctx);
     memcpy(ctx->h_wreg, ctx->stage_gwreg.data(), WREG_SLOTS * sizeof(unsigned long long));
-    HIPCHK(ctx, hipMemsetAsync(ctx->d_wcount, 0, (WREG_SLOTS + 1) * 8, ctx->stream));
-    hipLaunchKernelGGL(k_key_census, dim3(grid_for(n, 256, 256 * 8)), dim3(256), 0, ctx->stream, keys, n, ctx->d_wcount);
-    HIPCHK(ctx, hipGetLastError());
-    HIPCHK(ctx, hipMemcpyAsync(ctx->h_wcount, ctx->d_wcount, WREG_SLOTS * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     for (int w = 0; w < WREG_SLOTS; w++)
         if (ctx->h_wcount[w] && !ctx->h_wreg[w]) return set_err(ctx, HM_E_INVALID, "received a record of an unknown window slot");
     std::vector<WinCount> census;
     census_of_registry(ctx, census);
-    if ((rc = gens_prepare(ctx, census)) || (rc = winfo_upload(ctx, true))) return rc;
+    if ((rc = gens_prepare(ctx, census, true)) || (rc = winfo_upload(ctx, true))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
-    int64_t ntiles;
-    if ((rc = ev_partition<EventRec>(ctx, keys, n, nullptr, payload, ntiles))) return rc;
+    const unsigned lo = shard_lo(ctx->rank, W), bins = shard_lo(ctx->rank + 1, W) - lo;
+    const int64_t m = (int64_t)W * (bins + 1);
+    if ((rc = ensure(ctx, ctx->stage_C, m * 4)) || (rc = ensure(ctx, ctx->stage_P, m * 8)) ||
+        (rc = ensure(ctx, ctx->stage_SO, (size_t)RP_BINS * W * 8)) || (rc = ensure(ctx, ctx->stage_SP, (size_t)RP_BINS * W * 4)) ||
+        (rc = ensure(ctx, ctx->stage_T, (RP_BINS + 1) * 4)) || (rc = ensure(ctx, ctx->rp_O, (RP_BINS + 1) * 8)))
+        return rc;
+    hipLaunchKernelGGL(k_stage_counts, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, recv, d_off, W, bins, (unsigned *)ctx->stage_C.p);
+    if ((rc = scan_counts(ctx, (const unsigned *)ctx->stage_C.p, m, (unsigned long long *)ctx->stage_P.p))) return rc;
+    HIPCHK(ctx, hipMemsetAsync((unsigned *)ctx->stage_T.p + RP_BINS, 0, 4, ctx->stream));
+    hipLaunchKernelGGL(k_stage_segments, dim3(grid_for(RP_BINS, 256)), dim3(256), 0, ctx->stream, recv, d_off,
+                       (const unsigned long long *)ctx->stage_P.p, W, lo, bins, (unsigned long long *)ctx->stage_SO.p,
+                       (unsigned *)ctx->stage_SP.p, (unsigned *)ctx->stage_T.p);
+    if ((rc = scan_counts(ctx, (const unsigned *)ctx->stage_T.p, RP_BINS + 1, (unsigned long long *)ctx->rp_O.p))) return rc;
+    HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
-    if ((rc = merge_sorted<EventRec>(ctx, n, ntiles))) return rc;
+    Segs seg;
+    seg.SO = (const unsigned long long *)ctx->stage_SO.p;
+    seg.SP = (const unsigned *)ctx->stage_SP.p;
+    seg.nseg = W;
+    if ((rc = merge_sorted<EventRec>(ctx, n, 1, 0, (const EventRec *)recv, seg))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
-    if ((rc = rows_densify(ctx, ntiles))) return rc;
+    if ((rc = rows_densify(ctx, 1))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+    (void)hdr;
     return HM_OK;
 }
 
-int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, const void *payload_recv_dev, int64_t n_tile_recv,
-                   const void *cand_recv_dev, int64_t n_cand_recv, int32_t out_memory, hm_batch_out *out,
+int hm_stage_merge(hm_ctx *ctx, const void *recv_buf, const int64_t *recv_bytes, int32_t out_memory, hm_batch_out *out,
                    void *winner_send_buf, int64_t winner_send_cap, int64_t *winner_send_counts) {
-    if (!ctx || !out || !winner_send_counts || n_tile_recv < 0 || n_cand_recv < 0 || winner_send_cap < n_cand_recv ||
-        (n_cand_recv > 0 && (!winner_send_buf || !cand_recv_dev)) || (n_tile_recv > 0 && !tile_recv_dev))
+    if (!ctx || !out || !winner_send_counts || !recv_bytes || winner_send_cap < 0)
         return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
     if (ctx->stage != 2) return set_err(ctx, HM_E_STATE, "hm_stage_merge before hm_stage_send");
-    if (!ctx->stage_table && n_tile_recv > 0 && !payload_recv_dev)
-        return set_err(ctx, HM_E_INVALID, "the direct path needs the received payload stream");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc;
+    const int W = ctx->nranks;
     memset(out, 0, sizeof(*out));
     const int64_t late_wm = ctx->cfg.late_uses_prev_watermark ? ctx->wm_prev : ctx->wm_cur;
-    if (ctx->stage_table) rc = merge_partials(ctx, (const TilePartial *)tile_recv_dev, n_tile_recv);
-    else rc = merge_received_events(ctx, (const uint64_t *)tile_recv_dev, (const uint64_t *)payload_recv_dev, n_tile_recv);
+    // the chunks: offsets, headers (and the direct path's census) read back
+    std::vector<int64_t> off(W + 1, 0);
+    for (int s = 0; s < W; s++) {
+        if (recv_bytes[s] < 0 || (recv_bytes[s] & 7)) return set_err(ctx, HM_E_INVALID, "chunk %d: %lld bytes", s, (long long)recv_bytes[s]);
+        off[s + 1] = off[s] + recv_bytes[s];
+    }
+    if (off[W] > 0 && !recv_buf) return set_err(ctx, HM_E_INVALID, "receive buffer is required");
+    const uint8_t *recv = (const uint8_t *)recv_buf;
+    const bool table = ctx->stage_table;
+    const unsigned bins = shard_lo(ctx->rank + 1, W) - shard_lo(ctx->rank, W);
+    const size_t meta = (size_t)(2 * W + 1) * 8 + (size_t)W * sizeof(ChunkHdr);
+    if ((rc = ensure(ctx, ctx->stage_meta, meta))) return rc;
+    int64_t *d_off = (int64_t *)ctx->stage_meta.p;
+    int64_t *d_bytes = d_off + W + 1;
+    ChunkHdr *d_hdr = (ChunkHdr *)(d_bytes + W);
+    HIPCHK(ctx, hipMemcpyAsync(d_off, off.data(), (W + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(d_bytes, recv_bytes, W * 8, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_stage_headers, dim3(16), dim3(256), 0, ctx->stream, recv, d_off, d_bytes, W, d_hdr,
+                       table ? (int64_t)0 : chunk_census_off(bins), ctx->d_wcount);
+    HIPCHK(ctx, hipGetLastError());
+    std::vector<ChunkHdr> hdr(W);
+    HIPCHK(ctx, hipMemcpyAsync(hdr.data(), d_hdr, W * sizeof(ChunkHdr), hipMemcpyDeviceToHost, ctx->stream));
+    if (!table) HIPCHK(ctx, hipMemcpyAsync(ctx->h_wcount, ctx->d_wcount, WREG_SLOTS * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+    int64_t n_rec = 0, n_cand = 0;
+    for (int s = 0; s < W; s++) {
+        const ChunkHdr &h = hdr[s];
+        const ChunkHdr want = chunk_layout(h.records, h.cands, table ? (int64_t)sizeof(TilePartial) : (int64_t)sizeof(EventRec),
+                                           table ? 0 : (int64_t)bins);
+        if (h.magic != CHUNK_MAGIC || h.records < 0 || h.cands < 0 || memcmp(&h, &want, sizeof h) != 0 || h.bytes != recv_bytes[s])
+            return set_err(ctx, HM_E_INVALID, "chunk of rank %d is malformed", s);
+        n_rec += h.records;
+        n_cand += h.cands;
+    }
+    if (winner_send_cap < n_cand || (n_cand > 0 && !winner_send_buf))
+        return set_err(ctx, HM_E_INVALID, "winner buffer of %lld rows for %lld candidates", (long long)winner_send_cap, (long long)n_cand);
+    // the candidates (and table mode's partials) of all senders, contiguous
+    if ((rc = ensure(ctx, ctx->cands_recv, std::max<int64_t>(n_cand, 1) * sizeof(Cand)))) return rc;
+    if (table && (rc = ensure(ctx, ctx->stage_tmp, std::max<int64_t>(n_rec, 1) * sizeof(TilePartial)))) return rc;
+    for (int s = 0, c = 0, r = 0; s < W; s++) {
+        if (hdr[s].cands)
+            HIPCHK(ctx, hipMemcpyAsync((Cand *)ctx->cands_recv.p + c, recv + off[s] + hdr[s].cands_off, hdr[s].cands * sizeof(Cand),
+                                       hipMemcpyDeviceToDevice, ctx->stream));
+        if (table && hdr[s].records)
+            HIPCHK(ctx, hipMemcpyAsync((TilePartial *)ctx->stage_tmp.p + r, recv + off[s] + hdr[s].recs_off,
+                                       hdr[s].records * sizeof(TilePartial), hipMemcpyDeviceToDevice, ctx->stream));
+        c += (int)hdr[s].cands;
+        r += (int)hdr[s].records;
+    }
+    const Cand *cands = (const Cand *)ctx->cands_recv.p;
+    if (table) rc = merge_partials(ctx, (const TilePartial *)ctx->stage_tmp.p, n_rec);
+    else rc = merge_received_chunks(ctx, recv, d_off, hdr, n_rec);
     if (rc) return rc;
     // owner-side dedup over received candidates
-    if ((rc = phase_dedup(ctx, nullptr, (const Cand *)cand_recv_dev, n_cand_recv, true))) return rc;
+    if ((rc = phase_dedup(ctx, nullptr, cands, n_cand, true))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch, 0, 128 * 8, ctx->stream));
-    if (n_cand_recv > 0) {
-        hipLaunchKernelGGL(k_winner_route, dim3(grid_for(n_cand_recv, 256)), dim3(256), 0, ctx->stream, (const Cand *)cand_recv_dev,
+    if (n_cand > 0) {
+        hipLaunchKernelGGL(k_winner_route, dim3(grid_for(n_cand, 256)), dim3(256), 0, ctx->stream, cands,
                            (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, ctx->nranks, ctx->d_scratch, (int64_t *)nullptr, 0);
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
@@ -264,8 +399,8 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, const void *payload_r
     unsigned long long acc = 0;
     for (int r = 0; r < ctx->nranks; r++) { cur[r] = acc; winner_send_counts[r] = (int64_t)ctx->h_scratch[r]; acc += ctx->h_scratch[r]; }
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_scratch, cur, 64 * 8, hipMemcpyHostToDevice, ctx->stream));
-    if (n_cand_recv > 0) {
-        hipLaunchKernelGGL(k_winner_route, dim3(grid_for(n_cand_recv, 256)), dim3(256), 0, ctx->stream, (const Cand *)cand_recv_dev,
+    if (n_cand > 0) {
+        hipLaunchKernelGGL(k_winner_route, dim3(grid_for(n_cand, 256)), dim3(256), 0, ctx->stream, cands,
                            (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, ctx->nranks, ctx->d_scratch,
                            (int64_t *)winner_send_buf, 1);
         HIPCHK(ctx, hipGetLastError());
@@ -275,12 +410,12 @@ int hm_stage_merge(hm_ctx *ctx, const void *tile_recv_dev, const void *payload_r
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, 0, nullptr, out_memory, out))) return rc;
     // hm_last_counts: this rank's share of the batch (state keys created, records merged, tiles emitted, path)
     ctx->last_counts[0] = (int64_t)s2.n_state_new;
-    ctx->last_counts[1] = n_tile_recv;
+    ctx->last_counts[1] = n_rec;
     ctx->last_counts[2] = (int64_t)s2.n_touched;
     ctx->last_counts[3] = ctx->stage_table ? 1 : 0;
     ctx->last_counts[4] = ctx->stage_table ? ctx->table_evicted : 0;
     ctx->last_counts[5] = ctx->stage_sent;
-    ctx->last_binned = 0;
+    ctx->last_binned = ctx->binned ? 1 : 0;
     if (ctx->stage_agg_rows >= (int64_t(1) << 16)) {   // this rank's rows and owned keys (summed over ranks next batch)
         ctx->prev_agg_rows = ctx->stage_agg_rows;
         ctx->prev_keys = (int64_t)s2.n_touched;

@@ -22,12 +22,7 @@ static int state_dump(hm_ctx *ctx, hm_state_rec *recs, int64_t n, unsigned only_
     if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(n, 1) * sizeof(GrowRec)))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
     for (const auto &g : ctx->gens) {
-        GenDesc d{};
-        d.wenc = g.wenc;
-        d.tab = g.tab;
-        d.rbits = g.rbits;
-        d.rshift = (unsigned)g.log2cap - g.rbits;
-        d.rmask = (UINT64_C(1) << d.rshift) - 1;
+        const GenDesc d = gen_desc(g);
         hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
                            (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD, only_seq);
     }
@@ -71,12 +66,7 @@ int hm_state_export_touched(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs
         if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(live, 1) * sizeof(GrowRec)))) return rc;
         HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
         for (const auto &g : ctx->gens) {
-            GenDesc d{};
-            d.wenc = g.wenc;
-            d.tab = g.tab;
-            d.rbits = g.rbits;
-            d.rshift = (unsigned)g.log2cap - g.rbits;
-            d.rmask = (UINT64_C(1) << d.rshift) - 1;
+            const GenDesc d = gen_desc(g);
             hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
                                (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD, seq32(ctx));
         }
@@ -130,12 +120,10 @@ int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *
     }
     int rc;
     for (const auto &w : wins) {
-        int L;
-        unsigned rb;
-        gen_geometry(ctx, w.second, w.second, 0, L, rb);
+        Geo geo = gen_geometry(ctx, w.second, w.second, range_mode(ctx, false));
         TileSlot *t = nullptr;
-        if ((rc = table_acquire(ctx, L, rb, &t))) return rc;
-        ctx->gens.push_back({w.first, t, L, rb, w.second, 0});
+        if ((rc = table_acquire(ctx, geo, &t))) return rc;
+        ctx->gens.push_back(gen_of(w.first, t, geo, w.second, 0));
     }
     if ((rc = gens_upload(ctx))) return rc;
     if (n > 0) {

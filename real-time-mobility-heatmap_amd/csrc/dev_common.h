@@ -73,7 +73,7 @@ __device__ __forceinline__ int gmap_find(const GenDesc *gm, unsigned long long w
     return -1;
 }
 __device__ __forceinline__ unsigned long long home_slot(const GenDesc &g, uint64_t h) {
-    return ((unsigned long long)(region_field(h) >> (REGION_BITS - g.rbits)) << g.rshift) | (h & g.rmask);
+    return ((unsigned long long)((region_field(h) >> g.sb) - g.rbase) << g.rshift) | (h & g.rmask);
 }
 // linear probing wraps inside the key's region
 __device__ __forceinline__ unsigned long long next_slot(unsigned long long s, unsigned long long rmask) {
@@ -126,7 +126,7 @@ __device__ __forceinline__ int bin_of_c(const GenCache &C, const GenDesc *gm, ui
     const unsigned long long we = wenc_of(w);
     const GenDesc *g = gen_lookup(C, gm, we);
     if (!g) return -1;
-    const unsigned sb = REGION_BITS - g->rbits;
+    const unsigned sb = g->sb;
     const unsigned reg = region_field(h) >> sb;
     return (int)((reg << sb) | (window_salt(we) & ((1u << sb) - 1)));
 }

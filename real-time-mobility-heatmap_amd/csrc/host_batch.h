@@ -268,16 +268,16 @@ static int merge_events(hm_ctx *ctx, const Inputs &I, int64_t n_rec) {
     if (n_rec == 0) return merge_nothing(ctx);
     std::vector<WinCount> census;
     census_of_registry(ctx, census);
-    // binned in k_ingest: every window's table gets 2^REGION_BITS regions (a row's bin is its region), and the bins'
-    // row offsets are the exclusive scan of their cursors -- no partition pass over the keys and columns
+    // binned in k_ingest: every window's table in range geometry (a row's bin is its region), and the bins' row
+    // offsets are the exclusive scan of their cursors -- no partition pass over the keys and columns
     const bool binned = ctx->binned;
-    if ((rc = gens_prepare(ctx, census, binned ? REGION_BITS + REGION_MIN_BITS : 0)) || (rc = winfo_upload(ctx, true))) return rc;
+    if ((rc = gens_prepare(ctx, census, binned)) || (rc = winfo_upload(ctx, true))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
     int64_t ntiles = 1;
     if (binned) {
         if ((rc = ensure(ctx, ctx->rp_O, (RP_BINS + 1) * 8))) return rc;
         if ((rc = scan_counts(ctx, (const unsigned *)ctx->bin_cur.p, RP_BINS + 1, (unsigned long long *)ctx->rp_O.p))) return rc;
-    } else if ((rc = ev_partition<EventRec>(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, nullptr, ntiles))) {
+    } else if ((rc = ev_partition(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, ntiles))) {
         return rc;
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));

@@ -50,7 +50,8 @@ struct hm_ctx {
     DevBuf slow;   // k_ingest's fast-path exceptions (event indices) for k_ingest_exact
     // persistent tile state: one table per live window (kernels.h: GenDesc); released tables are pooled and
     // reused without clearing
-    struct Gen { unsigned long long wenc; TileSlot *tab; int log2cap; unsigned rbits; int64_t keys; int64_t batch_parts; };
+    // a window's table: 2^log2cap slots in 2^rbits regions, a key's region (region field >> sb) - rbase (GenDesc)
+    struct Gen { unsigned long long wenc; TileSlot *tab; int log2cap; unsigned rbits, sb, rbase; int64_t keys; int64_t batch_parts; };
     std::vector<Gen> gens;
     std::vector<std::pair<TileSlot *, int>> pool;   // (table, log2 slots)
     // state_arena_bytes: window tables carved from one zeroed reservation made at create (no driver allocation
@@ -68,6 +69,9 @@ struct hm_ctx {
     DevBuf bin_cnt, bin_off;          // k_merge_owned: touched keys per bin, their output offsets
     DevBuf parts_regrow;              // growth: the old tables' keys as partial records
     DevBuf parts_regrow_sorted;       // growth: the same, partitioned (not parts_sorted: a binned batch's slabs are there)
+    // multi-GPU exchange (api_stage.h): chunk starts and headers, the local -> global window slot map; the owner's
+    // per-sender bin counts and their scan, its bins' segments, the received candidates and table-mode partials
+    DevBuf stage_meta, stage_C, stage_P, stage_SO, stage_SP, stage_T, cands_recv, stage_tmp;
     DevBuf gapbuf;                    // k_gap_counts / k_fill_gaps: per-bin gap and donor counts + donor offsets
     unsigned long long seq = 0;
     // dedup table (persistent, cleared through its used list)
@@ -155,6 +159,9 @@ struct hm_ctx {
     int stage = 0;
     bool staged = false;                               // the last batch ran through the stage API
     int nranks = 1, rank = 0;
+    // the shard of a multi-GPU world this context's state is (hm_config.shard_count > 1, or adopted by the first
+    // hm_stage_ingest): its tables hold only the region fields it owns (tile_owner_of), in range geometry
+    int shard_rank = 0, shard_count = 0;
     int64_t stage_n_in = 0;
     int64_t stage_agg_rows = 0;
     hm_stage_sizes stage_sizes{};
@@ -300,13 +307,71 @@ static int64_t h3_cells_at(int res) {
     return c + 2;
 }
 
-static void gen_geometry(const hm_ctx *ctx, int64_t keys, int64_t parts, int min_log2, int &log2cap, unsigned &rbits) {
+// A window table's geometry.  Ordinary: 2^rbits regions of the region field's top rbits (sb = REGION_BITS - rbits),
+// as many as keep a merge workgroup's share of the batch's partials <= ~16k.  Range (a shard's tables, and every table
+// a batch binned in k_ingest merges into): one region per region field of the context's range [lo, hi) (sb = 0,
+// rbase = lo), so that a bin -- a region field -- is one region of every window.
+struct Geo { int log2cap; unsigned rbits, sb, rbase; bool range; };
+// the region fields a range-mode table holds: the shard's owned range, else all of them
+static void range_of(const hm_ctx *ctx, unsigned &lo, unsigned &hi) {
+    if (ctx->shard_count > 1) {
+        lo = shard_lo(ctx->shard_rank, ctx->shard_count);
+        hi = shard_lo(ctx->shard_rank + 1, ctx->shard_count);
+    } else {
+        lo = 0;
+        hi = 1u << REGION_BITS;
+    }
+}
+static bool range_mode(const hm_ctx *ctx, bool binned) { return binned || ctx->shard_count > 1; }
+// slots of a table that its keys can use (a range table's regions past the range stay empty)
+static int64_t usable_slots(const hm_ctx *ctx, const hm_ctx::Gen &g) {
+    if (g.sb != 0 || ctx->shard_count <= 1) return int64_t(1) << g.log2cap;
+    unsigned lo, hi;
+    range_of(ctx, lo, hi);
+    return (int64_t)(hi - lo) << (g.log2cap - (int)g.rbits);
+}
+// the geometry for `keys` keys receiving `parts` partials, at least 2^min_log2 slots
+static Geo gen_geometry(const hm_ctx *ctx, int64_t keys, int64_t parts, bool range, int min_log2 = 0) {
     keys = std::min(keys, h3_cells_at(ctx->cfg.h3_res));   // (the census bounds keys by rows; the grid bounds them too)
+    Geo g{};
+    g.range = range;
+    if (range) {
+        unsigned lo, hi;
+        range_of(ctx, lo, hi);
+        const int64_t nreg = hi - lo;
+        g.rbits = (unsigned)ilog2(next_pow2((uint64_t)nreg));
+        const int64_t per = (2 * std::max<int64_t>(keys, 1) + nreg - 1) / nreg;   // slots per region at load <= 1/2
+        const int rs = std::max(REGION_MIN_BITS, ilog2(next_pow2((uint64_t)per)));
+        g.log2cap = std::max((int)g.rbits + rs, min_log2);
+        g.sb = 0;
+        g.rbase = lo;
+        return g;
+    }
     int L = ilog2(next_pow2((uint64_t)std::max<int64_t>(2 * keys, 1024)));
     const int want_rb = std::min(RP_BITS, ilog2(next_pow2((uint64_t)std::max<int64_t>((parts + 16383) / 16384, 1))));
     L = std::max({L, want_rb + REGION_MIN_BITS, min_log2});
-    rbits = (unsigned)std::min(RP_BITS, L - REGION_MIN_BITS);
-    log2cap = L;
+    g.rbits = (unsigned)std::min(RP_BITS, L - REGION_MIN_BITS);
+    g.sb = REGION_BITS - g.rbits;
+    g.rbase = 0;
+    g.log2cap = L;
+    return g;
+}
+// a table's descriptor (gens_upload, growth, the state dump)
+static GenDesc gen_desc(const hm_ctx::Gen &g) {
+    GenDesc d{};
+    d.wenc = g.wenc;
+    d.tab = g.tab;
+    d.rbits = (unsigned char)g.rbits;
+    d.sb = (unsigned char)g.sb;
+    d.rbase = g.rbase;
+    d.rshift = (unsigned short)(g.log2cap - (int)g.rbits);
+    d.rmask = (UINT64_C(1) << d.rshift) - 1;
+    d.count = (unsigned long long)g.keys;
+    d.batch_parts = (unsigned long long)g.batch_parts;
+    return d;
+}
+static hm_ctx::Gen gen_of(unsigned long long wenc, TileSlot *t, const Geo &g, int64_t keys, int64_t parts) {
+    return hm_ctx::Gen{wenc, t, g.log2cap, g.rbits, g.sb, g.rbase, keys, parts};
 }
 
 static bool in_arena(const hm_ctx *ctx, const void *p) {
@@ -315,8 +380,9 @@ static bool in_arena(const hm_ctx *ctx, const void *p) {
 
 // A table of >= 2^log2cap slots: the smallest pooled table of 2^log2cap .. 2^(log2cap+2) slots (not cleared: see
 // kernels.h; a window whose key count sits near a power of two must not miss the pool and pay a multi-GB hipMalloc
-// every batch), else a new one zeroed once.  log2cap and rbits return the table's actual geometry.
-static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **out) {
+// every batch), else a new one zeroed once.  geo returns the table's actual geometry.
+static int table_acquire(hm_ctx *ctx, Geo &geo, TileSlot **out) {
+    int &log2cap = geo.log2cap;
     int best = -1;
     for (size_t i = 0; i < ctx->pool.size(); i++) {
         const int l = ctx->pool[i].second;
@@ -325,7 +391,10 @@ static int table_acquire(hm_ctx *ctx, int &log2cap, unsigned &rbits, TileSlot **
     if (best >= 0) {
         *out = ctx->pool[best].first;
         log2cap = ctx->pool[best].second;
-        rbits = (unsigned)std::min(RP_BITS, log2cap - REGION_MIN_BITS);
+        if (!geo.range) {   // (a range table keeps its regions: larger ones)
+            geo.rbits = (unsigned)std::min(RP_BITS, log2cap - REGION_MIN_BITS);
+            geo.sb = REGION_BITS - geo.rbits;
+        }
         ctx->pool.erase(ctx->pool.begin() + best);
         // the slots keep the previous window's keys (never matched: other wenc), the tags were cleared at release
         HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[3], 0));
@@ -387,14 +456,7 @@ static int gens_upload(hm_ctx *ctx) {
     for (const auto &g : ctx->gens) {
         unsigned h = (unsigned)(mix64(g.wenc) & (GMAP_SLOTS - 1));
         while (ctx->h_gmap[h].wenc) h = (h + 1) & (GMAP_SLOTS - 1);
-        GenDesc &d = ctx->h_gmap[h];
-        d.wenc = g.wenc;
-        d.tab = g.tab;
-        d.rbits = g.rbits;
-        d.rshift = (unsigned)g.log2cap - g.rbits;
-        d.rmask = (UINT64_C(1) << d.rshift) - 1;
-        d.count = (unsigned long long)g.keys;
-        d.batch_parts = (unsigned long long)g.batch_parts;
+        ctx->h_gmap[h] = gen_desc(g);
     }
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_gmap, ctx->h_gmap, GMAP_SLOTS * sizeof(GenDesc), hipMemcpyHostToDevice, ctx->stream));
     ctx->n_glist = 0;
@@ -446,9 +508,6 @@ static int partition(hm_ctx *ctx, const In *parts, int64_t n, int64_t &ntiles, i
     return HM_OK;
 }
 
-// the direct path's partition: n event keys with the batch's columns (I) or, on a multi-GPU owner, the received payload
-// stream -> EventRecs in (window, region) bins (parts_sorted); or with nranks > 0 the wire streams grouped by owner rank
-// (dst = key stream, payload_out); rows without a key fall into digit nbins (dropped)
 static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t n, bool rerun_max, hipStream_t st);
 // the batch's dedup on the side stream (hm_process_batch): side_ev[1] / [2] bracket it
 static int launch_side_dedup(hm_ctx *ctx, const Inputs *I) {
@@ -459,37 +518,25 @@ static int launch_side_dedup(hm_ctx *ctx, const Inputs *I) {
     return HM_OK;
 }
 
-template <typename Out>
-static int ev_partition(hm_ctx *ctx, const uint64_t *keys, int64_t n, const Inputs *I, const uint64_t *payload_in,
-                        int64_t &ntiles, int nranks = 0, Out *dst = nullptr, uint64_t *payload_out = nullptr) {
-    const int nbins = nranks > 0 ? nranks : RP_BINS;
+// the direct path's partition: n event keys with the batch's columns (I) -> EventRecs in (window, region) bins
+// (parts_sorted; the bins from the windows' WInfo.binp: with binp 0, one bin per region field -- the multi-GPU
+// sender's grouping); rows without a key fall into digit RP_BINS (dropped)
+static int ev_partition(hm_ctx *ctx, const uint64_t *keys, int64_t n, const Inputs *I, int64_t &ntiles) {
+    const int nbins = RP_BINS;
     const int64_t tile = rp_tile_for(n);
     ntiles = std::max<int64_t>((n + tile - 1) / tile, 1);
     const int64_t m = (int64_t)(nbins + 1) * ntiles;
     int rc;
     // (+ 64 slack records: k_ev_scatter_rec's lanes past a tile store there)
-    if (!dst && (rc = ensure(ctx, ctx->parts_sorted, (std::max<int64_t>(n, 1) + 64) * sizeof(Out)))) return rc;
+    if ((rc = ensure(ctx, ctx->parts_sorted, (std::max<int64_t>(n, 1) + 64) * sizeof(EventRec)))) return rc;
     if ((rc = ensure(ctx, ctx->rp_H, m * 4)) || (rc = ensure(ctx, ctx->rp_O, m * 8))) return rc;
     const uint64_t ch = cell_hi_of(ctx->cfg.h3_res);
     hipLaunchKernelGGL(k_ev_hist, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, (const WInfo *)ctx->d_winfo, ch,
-                       nranks, nbins, (unsigned *)ctx->rp_H.p, ntiles);
+                       0, nbins, (unsigned *)ctx->rp_H.p, ntiles);
     if ((rc = rp_scan(ctx, m))) return rc;
-    if constexpr (std::is_same<Out, EventRec>::value) {
-        if (nranks != 0 || dst) return set_err(ctx, HM_E_STATE, "ev_partition: EventRecs go to the context's bins");
-        if (payload_in)
-            hipLaunchKernelGGL(k_ev_scatter_rec<true>, dim3(ntiles), dim3(SR_THREADS), 0, ctx->stream, keys, n, tile, nullptr,
-                               nullptr, nullptr, nullptr, payload_in, (const WInfo *)ctx->d_winfo, ch, nbins,
-                               (const unsigned long long *)ctx->rp_O.p, ntiles, (EventRec *)ctx->parts_sorted.p);
-        else
-            hipLaunchKernelGGL(k_ev_scatter_rec<false>, dim3(ntiles), dim3(SR_THREADS), 0, ctx->stream, keys, n, tile, I->sp, I->sv,
-                               I->lat, I->lon, nullptr, (const WInfo *)ctx->d_winfo, ch, nbins,
-                               (const unsigned long long *)ctx->rp_O.p, ntiles, (EventRec *)ctx->parts_sorted.p);
-    } else {
-        hipLaunchKernelGGL(k_ev_scatter<Out>, dim3(ntiles), dim3(EV_THREADS), 0, ctx->stream, keys, n, tile, I ? I->sp : nullptr,
-                           I ? I->sv : nullptr, I ? I->lat : nullptr, I ? I->lon : nullptr, payload_in,
-                           (const WInfo *)ctx->d_winfo, ch, nranks, nbins, (const unsigned long long *)ctx->rp_O.p, ntiles,
-                           dst ? dst : (Out *)ctx->parts_sorted.p, payload_out);
-    }
+    hipLaunchKernelGGL(k_ev_scatter_rec, dim3(ntiles), dim3(SR_THREADS), 0, ctx->stream, keys, n, tile, I->sp, I->sv, I->lat, I->lon,
+                       (const WInfo *)ctx->d_winfo, ch, nbins, (const unsigned long long *)ctx->rp_O.p, ntiles,
+                       (EventRec *)ctx->parts_sorted.p);
     HIPCHK(ctx, hipGetLastError());
     return HM_OK;
 }
@@ -505,9 +552,16 @@ static RowsOut staged_rows(hm_ctx *ctx) {
 // the batch sequence number kept in the slots' touched words (32 bits, never 0: fresh slots hold 0)
 static unsigned seq32(const hm_ctx *ctx) { return (unsigned)(ctx->seq % 0xffffffffull) + 1u; }
 
+// the segments of a multi-GPU owner's bins (k_stage_segments; merge_sorted's kSeg variant)
+struct Segs {
+    const unsigned long long *SO = nullptr;
+    const unsigned *SP = nullptr;
+    int nseg = 0;
+};
 // merge the partitioned records (ctx->parts_sorted, or src) of n_rows staging rows
 template <typename Rec>
-static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t slab = 0, const Rec *src = nullptr) {
+static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t slab = 0, const Rec *src = nullptr,
+                        const Segs &seg = Segs()) {
     constexpr bool rehash = std::is_same<Rec, GrowRec>::value;
     int rc;
     if ((rc = ensure(ctx, ctx->bin_cnt, RP_BINS * 4)) || (rc = ensure(ctx, ctx->bin_off, RP_BINS * 8)))
@@ -538,12 +592,23 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t sla
             if (g.batch_parts) { need += size_t(1) << (g.log2cap - (int)g.rbits); nwin++; }
         resident = need <= tag_bytes && nwin <= MO_RES_MAX && ctx->n_glist <= GC_MAX;
     }
+    if (seg.nseg > MO_SEG_MAX) return set_err(ctx, HM_E_INVALID, "%d senders exceed %d", seg.nseg, MO_SEG_MAX);
     auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(grid), dim3(MO_THREADS), tag_bytes, ctx->stream, src ? src : (const Rec *)ctx->parts_sorted.p, slab,
+                           seg.SO, seg.SP, seg.nseg,
                            (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
                            ctx->n_glist, (const WInfo *)ctx->d_winfo, cell_hi_of(ctx->cfg.h3_res), seq32(ctx), staged_rows(ctx),
                            (unsigned *)ctx->bin_cnt.p, ctx->d_st, tag_bytes);
     };
+    if constexpr (std::is_same<Rec, EventRec>::value) {
+        if (seg.nseg > 0) {   // (the multi-GPU owner)
+            if (resident && ctx->merge_coop) launch(k_merge_owned<Rec, true, true, true>);
+            else if (resident) launch(k_merge_owned<Rec, true, false, true>);
+            else launch(k_merge_owned<Rec, false, false, true>);
+            HIPCHK(ctx, hipGetLastError());
+            return HM_OK;
+        }
+    }
     if constexpr (!rehash) {
         if (resident && ctx->merge_coop) launch(k_merge_owned<Rec, true, true>);
         else if (resident) launch(k_merge_owned<Rec, true>);
@@ -595,12 +660,11 @@ static int winfo_upload(hm_ctx *ctx, bool with_bins) {
         x.inner = window_inner(wdec(we));
         x.gslot = ctx->stage_gslot.empty() ? (unsigned)w : ctx->stage_gslot[w];
         if (with_bins) {
-            unsigned rbits = 0;
+            unsigned sb = 0;
             bool found = false;
             for (const auto &g : ctx->gens)
-                if (g.wenc == we) { rbits = g.rbits; found = true; break; }
+                if (g.wenc == we) { sb = g.sb; found = true; break; }
             if (!found) return set_err(ctx, HM_E_STATE, "window without a state table");
-            const unsigned sb = REGION_BITS - rbits;
             x.binp = (sb << 24) | (window_salt(we) & ((1u << sb) - 1));
         }
         lo = std::min(lo, w);
@@ -630,33 +694,35 @@ static int winfo_upload(hm_ctx *ctx, bool with_bins) {
 // Give every window of the census a table large enough for its keys after this batch (new windows: a new table;
 // windows that would pass load 1/2: a larger table, filled by dumping the old one and merging the dump in rehash
 // mode); upload the window map.
-// min_log2: every window's table at least 2^min_log2 slots (fused binning: 2^(REGION_BITS + REGION_MIN_BITS), so that
-// each has 2^REGION_BITS regions and a row's bin, chosen before the census, is its region)
-static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census, int min_log2 = 0) {
+// range: every window's table in range geometry (a shard's context, or a batch binned in k_ingest: a row's bin, chosen
+// before the census, is then its region in every window)
+static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census, bool range = false) {
     std::vector<hm_ctx::Gen> old;   // tables being replaced by larger ones
     int rc;
+    range = range_mode(ctx, range);
+    unsigned lo = 0, hi = 0;
+    range_of(ctx, lo, hi);
     for (auto &g : ctx->gens) g.batch_parts = 0;
     for (const WinCount &w : census) {
         ctx->batch_windows.push_back(wdec(w.wenc));
         const int64_t c = (int64_t)w.count;
         auto it = std::find_if(ctx->gens.begin(), ctx->gens.end(), [&](const hm_ctx::Gen &g) { return g.wenc == w.wenc; });
-        int L;
-        unsigned rb;
         if (it == ctx->gens.end()) {
-            gen_geometry(ctx, c, c, min_log2, L, rb);
+            Geo geo = gen_geometry(ctx, c, c, range);
             TileSlot *t = nullptr;
-            if ((rc = table_acquire(ctx, L, rb, &t))) return rc;
-            ctx->gens.push_back({w.wenc, t, L, rb, 0, c});
+            if ((rc = table_acquire(ctx, geo, &t))) return rc;
+            ctx->gens.push_back(gen_of(w.wenc, t, geo, c, c));
             continue;
         }
-        if (std::min(it->keys + c, h3_cells_at(ctx->cfg.h3_res)) * 2 > (int64_t(1) << it->log2cap) || it->log2cap < min_log2) {
-            gen_geometry(ctx, it->keys + c, c, std::max(it->log2cap + 1, min_log2), L, rb);
+        const bool full = std::min(it->keys + c, h3_cells_at(ctx->cfg.h3_res)) * 2 > usable_slots(ctx, *it);
+        const bool misfit = range && (it->sb != 0 || it->rbase != lo || (int64_t(1) << it->rbits) < (int64_t)(hi - lo));
+        if (full || misfit) {
+            Geo geo = gen_geometry(ctx, it->keys + c, c, range, full ? it->log2cap + 1 : 0);
             TileSlot *t = nullptr;
-            if ((rc = table_acquire(ctx, L, rb, &t))) return rc;
+            if ((rc = table_acquire(ctx, geo, &t))) return rc;
             old.push_back(*it);
-            it->tab = t;
-            it->log2cap = L;
-            it->rbits = rb;   // keys unchanged: the rehash merge moves them without counting
+            // keys unchanged: the rehash merge moves them without counting
+            *it = gen_of(it->wenc, t, geo, it->keys, 0);
         }
         it->batch_parts = c;
     }
@@ -669,12 +735,7 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census, int mi
         if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(moved, 1) * sizeof(GrowRec)))) return rc;
         HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
         for (const auto &g : old) {
-            GenDesc d{};
-            d.wenc = g.wenc;
-            d.tab = g.tab;
-            d.rbits = g.rbits;
-            d.rshift = (unsigned)g.log2cap - g.rbits;
-            d.rmask = (UINT64_C(1) << d.rshift) - 1;
+            const GenDesc d = gen_desc(g);
             hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
                                (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD);
         }

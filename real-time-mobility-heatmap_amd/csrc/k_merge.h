@@ -234,8 +234,12 @@ struct MLine {
 // existing keys (their lines then cost one cooperative round trip); a batch of mostly new keys runs the per-lane probe,
 // which carries less machinery per probed slot (bench leg: 3.72-3.81 vs 4.03-4.11 ms; state-read leg: 6.86-6.89 vs
 // 6.22-6.30 ms, profiles/r3/r3ab9/)
-template <typename Rec, bool kResident = false, bool kCoop = false>
+// kSeg (the multi-GPU owner): bin b's records are nseg segments, one per sender -- segment s at record SO[b * nseg + s]
+// of parts, after SP[b * nseg + s] records of the bin (k_stage_segments)
+constexpr int MO_SEG_MAX = 64;
+template <typename Rec, bool kResident = false, bool kCoop = false, bool kSeg = false>
 __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_merge_owned(const Rec *__restrict__ parts, int64_t slab,
+                                                            const unsigned long long *__restrict__ SO, const unsigned *__restrict__ SP, int nseg,
                                                             const unsigned long long *__restrict__ O, int64_t ntiles, int nbins,
                                                             GenDesc *gm, const GenDesc *glist, int n_glist,
                                                             const WInfo *__restrict__ winfo, uint64_t cell_hi,
@@ -246,6 +250,8 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     extern __shared__ unsigned mo_tags[];   // tag_bytes of resident region tags
     __shared__ WinLds WL;
     __shared__ GenCache C;
+    __shared__ unsigned long long seg_base[kSeg ? MO_SEG_MAX : 1];
+    __shared__ unsigned seg_pre[kSeg ? MO_SEG_MAX + 1 : 1];
     wl_init(WL);
     gc_load(C, glist, n_glist);
     const GenSink sink{gm};
@@ -266,11 +272,13 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                 for (int q = 0; q < C.n; q++) {
                     const GenDesc &g = C.e[q];
                     if (!g.batch_parts) continue;
-                    const unsigned sb = REGION_BITS - g.rbits, smask = (1u << sb) - 1;
+                    const unsigned sb = g.sb, smask = (1u << sb) - 1;
                     if (((unsigned)bin & smask) != (window_salt(g.wenc) & smask)) continue;
+                    const unsigned reg = ((unsigned)bin >> sb) - g.rbase;   // (a shard's table: its range only)
+                    if (reg >= (1u << g.rbits)) continue;
                     const unsigned slots = (unsigned)g.rmask + 1;
                     if (nr == MO_RES_MAX || off + slots > tag_bytes) continue;
-                    const unsigned long long first = (unsigned long long)((unsigned)bin >> sb) << g.rshift;
+                    const unsigned long long first = (unsigned long long)reg << g.rshift;
                     S.res_we[nr] = g.wenc;
                     S.res_slots[nr] = g.tab + first;
                     S.res_gtags[nr] = gen_tags(g) + first;
@@ -283,6 +291,13 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                 }
             }
             S.n_res = nr;
+        }
+        if constexpr (kSeg) {
+            for (int q = t; q < nseg; q += MO_THREADS) {
+                seg_base[q] = SO[(int64_t)bin * nseg + q];
+                seg_pre[q] = SP[(int64_t)bin * nseg + q];
+            }
+            if (t == 0) seg_pre[nseg] = (unsigned)(b1 - b0);
         }
         lds_barrier();
         const int nres = S.n_res;
@@ -595,7 +610,21 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         // the bin's records: [b0, b1) of the partitioned array, or (slab != 0: k_ingest's fused binning) the first
         // b1 - b0 records of the bin's slab; either way row k of the bin goes to b0 + k
         const Rec *__restrict__ bp = slab ? parts + ((int64_t)bin * slab - b0) : parts;
-        if (b0 + t < b1) nxt = ld_stream(bp + b0 + t);
+        // kSeg: the record at bin index v = i - b0 is in the last segment starting at or before v (binary search)
+        auto rec_at = [&](int64_t i) __attribute__((always_inline)) -> const Rec * {
+            if constexpr (kSeg) {
+                const unsigned v = (unsigned)(i - b0);
+                int lo = 0, hi = nseg;   // seg_pre[lo] <= v < seg_pre[hi]
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (seg_pre[mid] <= v) lo = mid; else hi = mid;
+                }
+                return parts + seg_base[lo] + (v - seg_pre[lo]);
+            } else {
+                return bp + i;
+            }
+        };
+        if (b0 + t < b1) nxt = ld_stream(rec_at(b0 + t));
         for (int64_t c0 = b0; c0 < b1; c0 += MO_THREADS) {
             // 1. stage this chunk's records in LDS
             const int64_t i = c0 + t;
@@ -603,7 +632,7 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             MRec p{};
             if (has) p = mrec_of(nxt, winfo, cell_hi);   // (the window parameters from an LDS image cost the state-read
                                                          // leg's merge ~1 ms, profiles/r3/r3ab11: a global load)
-            if (i + MO_THREADS < b1) nxt = ld_stream(bp + i + MO_THREADS);
+            if (i + MO_THREADS < b1) nxt = ld_stream(rec_at(i + MO_THREADS));
             if (has) {
                 S.sc[t] = p.cell;
                 S.sh[t] = p.hk;

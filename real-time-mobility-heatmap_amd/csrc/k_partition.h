@@ -24,7 +24,7 @@ constexpr int RP_THREADS = 256;
 __device__ __forceinline__ unsigned rp_digit(uint64_t cell, int64_t ws, const GenCache &C, const GenDesc *gm, int nranks,
                                              bool &bad) {
     const uint64_t h = tile_hash(cell, ws);
-    if (nranks > 0) return (unsigned)owner_of(h, nranks);
+    if (nranks > 0) return (unsigned)tile_owner_of(h, nranks);
     const int b = bin_of_c(C, gm, h, ws);
     bad |= b < 0;
     return b < 0 ? 0u : (unsigned)b;
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(RP_THREADS) void k_rp_scatter(const In *__restrict_
                 h = tile_hash(cell, ws);
                 unsigned d;
                 if (nranks > 0) {
-                    d = (unsigned)owner_of(h, nranks);
+                    d = (unsigned)tile_owner_of(h, nranks);
                 } else {
                     const int b = bin_of_c(C, gm, h, ws);
                     d = b < 0 ? 0u : (unsigned)b;   // (k_rp_hist flagged it)
@@ -214,7 +214,7 @@ __device__ __forceinline__ WInfo wi_get(const WiCacheL &C, const WInfo *winfo, u
 
 // the key's radix digit: with nranks > 0 its owner rank, else its (window, region) bin (binp: kernels.h WInfo)
 __device__ __forceinline__ unsigned ev_digit(uint64_t h, unsigned binp, int nranks) {
-    if (nranks > 0) return (unsigned)owner_of(h, nranks);
+    if (nranks > 0) return (unsigned)tile_owner_of(h, nranks);
     const unsigned sb = binp >> 24;
     return ((region_field(h) >> sb) << sb) | (binp & 0xffffffu);
 }
@@ -251,109 +251,12 @@ __global__ __launch_bounds__(EV_THREADS) void k_ev_hist(const uint64_t *__restri
     for (int d = threadIdx.x; d <= nbins; d += EV_THREADS) H[(int64_t)d * ntiles + blockIdx.x] = h[d];
 }
 
-// the direct path's multi-GPU wire format (hm_stage_send): a key stream (8 B per row: the cell's low 52 bits | 1 + the
-// batch's GLOBAL window slot << 52) and a payload stream (24 B: speed bits as in EventRec, lat, lon), both grouped by
-// owner rank; the owner partitions them into EventRecs (k_ev_scatter with payload_in)
-struct WireKey {
-    uint64_t key;
-};
-constexpr int WIRE_PAYLOAD_WORDS = 3;
-
-// Per wave and round, 64 rows: each lane takes its row's digit and position (LDS cursor) and builds its record in
-// LDS; then the wave writes the 64 records as rounds of 16-B parts, consecutive lanes covering consecutive parts of
-// one record (whole 32-B sectors at random places).
-//   Out = EventRec: the direct path's (window, region) bins; the row's speed/lat/lon come from the batch's columns,
-//         or (payload_in, the multi-GPU owner) from the received payload stream;
-//   Out = WireKey:  grouped by owner rank into the caller's key and payload streams (payload_out), the key's window
-//         slot rewritten from the rank's registry to the batch's global registry (WInfo.gslot).
-template <typename Out>
-__global__ __launch_bounds__(EV_THREADS) void k_ev_scatter(const uint64_t *__restrict__ keys, int64_t n, int64_t tile,
-                                                          const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
-                                                          const double *__restrict__ lat, const double *__restrict__ lon,
-                                                          const uint64_t *__restrict__ payload_in,
-                                                          const WInfo *__restrict__ winfo, uint64_t cell_hi, int nranks, int nbins,
-                                                          const unsigned long long *__restrict__ O, int64_t ntiles,
-                                                          Out *__restrict__ dst, uint64_t *__restrict__ payload_out) {
-    constexpr bool wire = std::is_same<Out, WireKey>::value;
-    static_assert(wire || std::is_same<Out, EventRec>::value, "k_ev_scatter output");
-    constexpr int QO = wire ? 1 : sizeof(Out) / 16;
-    __shared__ unsigned cur[RP_BINS];   // positions < 2^32 - 1 (hm_process_batch checks n)
-    __shared__ uint4 stage[wire ? 1 : (EV_THREADS / 64) * 64 * QO];
-    __shared__ WiCacheL WI;
-    for (int d = threadIdx.x; d < nbins; d += EV_THREADS) cur[d] = (unsigned)O[(int64_t)d * ntiles + blockIdx.x];
-    wi_load(WI, winfo);
-    __syncthreads();
-    const int64_t t0 = (int64_t)blockIdx.x * tile;
-    const int64_t t1 = t0 + tile < n ? t0 + tile : n;
-    uint4 *__restrict__ d4 = (uint4 *)dst;
-    uint4 *ws = stage + (wire ? 0 : (threadIdx.x >> 6) * 64 * QO);
-    const int ln = lane_id();
-    // a row's columns, loaded one round ahead (every load of a round is issued before the first is used); sv = 2:
-    // the speed word is already encoded (payload stream)
-    struct Row { uint64_t k, sp; double la, lo; uint8_t sv; };
-    auto load = [&](int64_t i) {
-        Row r{0, 0, 0.0, 0.0, 0};
-        if (i < t1) {
-            r.k = __builtin_nontemporal_load(&keys[i]);
-            if (payload_in) {
-                r.sp = __builtin_nontemporal_load(&payload_in[i * WIRE_PAYLOAD_WORDS]);
-                r.la = __builtin_bit_cast(double, __builtin_nontemporal_load(&payload_in[i * WIRE_PAYLOAD_WORDS + 1]));
-                r.lo = __builtin_bit_cast(double, __builtin_nontemporal_load(&payload_in[i * WIRE_PAYLOAD_WORDS + 2]));
-                r.sv = 2;
-            } else {
-                r.sp = speed ? __builtin_bit_cast(uint64_t, __builtin_nontemporal_load(&speed[i])) : 0;
-                r.sv = speed ? (speed_valid ? __builtin_nontemporal_load(&speed_valid[i]) : (uint8_t)1) : (uint8_t)0;
-                r.la = __builtin_nontemporal_load(&lat[i]);
-                r.lo = __builtin_nontemporal_load(&lon[i]);
-            }
-        }
-        return r;
-    };
-    int64_t i0 = t0 + (int64_t)(threadIdx.x >> 6) * 64;
-    Row nx = load(i0 + ln);
-    preheader_wait();
-    for (; i0 < t1; i0 += EV_THREADS) {
-        const Row r = nx;
-        nx = load(i0 + EV_THREADS + ln);
-        unsigned pos = ~0u;   // ~0u: no record
-        if (r.k) {
-            const uint64_t k = r.k;
-            const WInfo wi = wi_get(WI, winfo, ekey_widx(k));
-            const uint64_t cell = (k & CELL_LO) | cell_hi;
-            const uint64_t hh = mix64(cell ^ wi.inner);
-            pos = atomicAdd(&cur[ev_digit(hh, wi.binp, nranks)], 1u);
-            const double sp = __builtin_bit_cast(double, r.sp);
-            const uint64_t spb = r.sv == 2 ? r.sp : r.sv == 0 ? SPEED_NULL_BITS : sp != sp ? CANON_NAN_BITS : r.sp;
-            const uint64_t lab = __builtin_bit_cast(uint64_t, r.la), lob = __builtin_bit_cast(uint64_t, r.lo);
-            if constexpr (wire) {
-                // few digits (owner ranks): a wave's rows land in a few contiguous runs, written lane by lane
-                dst[pos].key = ekey_make(k, wi.gslot);
-                payload_out[(int64_t)pos * WIRE_PAYLOAD_WORDS + 0] = spb;
-                payload_out[(int64_t)pos * WIRE_PAYLOAD_WORDS + 1] = lab;
-                payload_out[(int64_t)pos * WIRE_PAYLOAD_WORDS + 2] = lob;
-            } else {
-                ws[ln * 2 + 0] = make_uint4((unsigned)k, (unsigned)(k >> 32), (unsigned)spb, (unsigned)(spb >> 32));
-                ws[ln * 2 + 1] = make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32));
-            }
-        }
-        if constexpr (!wire) {
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            for (int q = 0; q < QO; q++) {
-                const int idx = q * 64 + ln, rec = idx / QO, part = idx % QO;
-                const unsigned p = __shfl(pos, rec, 64);
-                if (p != ~0u) d4[(int64_t)p * QO + part] = ws[idx];
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-}
-
-// Out = EventRec (the direct path's (window, region) bins; the single-GPU partition and the multi-GPU owner's): the same
-// rows and records as k_ev_scatter above, with no wait for the stores or the next round's loads inside the loop.
-// Rounds alternate between two register sets (no loop-carried copy: a register copy of a pending load waits for it);
-// every load is unconditional (the row clamped into the tile, absent columns read from one-element device constants,
-// the payload stream chosen at compile time), and every lane stores a record each round -- a row without a key goes
+// The direct path's (window, region) bins: each aggregated row's 32-B EventRec (its key, speed, lat, lon) at its bin's
+// cursor; a wave builds its 64 records in LDS and writes them as rounds of 16-B parts, consecutive lanes covering
+// consecutive parts of one record (whole 32-B sectors at random places), with no wait for the stores or the next
+// round's loads inside the loop.  Rounds alternate between two register sets (no loop-carried copy: a register copy of
+// a pending load waits for it); every load is unconditional (the row clamped into the tile, absent columns read from
+// one-element device constants), and every lane stores a record each round -- a row without a key goes
 // to the gap digit after every bin (counted by k_ev_hist; never read by the merge), a lane past the tile to the slack
 // records after the n-th (ensured by ev_partition) -- so the stores are unconditional too: the wait before a round's
 // rows only waits for them, not for the previous round's stores (measured before: a vmcnt(0) at the loop latch and
@@ -366,11 +269,9 @@ typedef __attribute__((address_space(1))) hm_v4u g_v4u;
 __device__ __forceinline__ void st_g16(void *p, uint4 v) { *(g_v4u *)p = hm_v4u{v.x, v.y, v.z, v.w}; }   // global 16-B store
 // workgroup size of k_ev_scatter_rec (its LDS: the 8193 cursors + a 32-B record per lane)
 constexpr int SR_THREADS = 512;
-template <bool kPayload>
 __global__ __launch_bounds__(SR_THREADS) void k_ev_scatter_rec(const uint64_t *__restrict__ keys, int64_t n, int64_t tile,
                                                               const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid,
                                                               const double *__restrict__ lat, const double *__restrict__ lon,
-                                                              const uint64_t *__restrict__ payload_in,
                                                               const WInfo *__restrict__ winfo, uint64_t cell_hi, int nbins,
                                                               const unsigned long long *__restrict__ O, int64_t ntiles,
                                                               EventRec *__restrict__ dst) {
@@ -394,17 +295,10 @@ __global__ __launch_bounds__(SR_THREADS) void k_ev_scatter_rec(const uint64_t *_
         r.in = i < t1;
         const int64_t j = r.in ? i : t1 - 1;
         r.k = __builtin_nontemporal_load((gcu64 *)&keys[j]);
-        if constexpr (kPayload) {
-            r.sp = __builtin_nontemporal_load((gcu64 *)&payload_in[j * WIRE_PAYLOAD_WORDS]);
-            r.la = __builtin_bit_cast(double, __builtin_nontemporal_load((gcu64 *)&payload_in[j * WIRE_PAYLOAD_WORDS + 1]));
-            r.lo = __builtin_bit_cast(double, __builtin_nontemporal_load((gcu64 *)&payload_in[j * WIRE_PAYLOAD_WORDS + 2]));
-            r.sv = 2;
-        } else {
-            r.sp = __builtin_bit_cast(uint64_t, __builtin_nontemporal_load((gcd *)(speed ? &speed[j] : &g_zero_double)));
-            r.sv = __builtin_nontemporal_load((gcu8 *)(speed_valid ? &speed_valid[j] : speed ? &g_one_byte : &g_zero_byte));
-            r.la = __builtin_nontemporal_load((gcd *)&lat[j]);
-            r.lo = __builtin_nontemporal_load((gcd *)&lon[j]);
-        }
+        r.sp = __builtin_bit_cast(uint64_t, __builtin_nontemporal_load((gcd *)(speed ? &speed[j] : &g_zero_double)));
+        r.sv = __builtin_nontemporal_load((gcu8 *)(speed_valid ? &speed_valid[j] : speed ? &g_one_byte : &g_zero_byte));
+        r.la = __builtin_nontemporal_load((gcd *)&lat[j]);
+        r.lo = __builtin_nontemporal_load((gcd *)&lon[j]);
         return r;
     };
     auto put = [&](const Row &r) __attribute__((always_inline)) {
@@ -425,8 +319,8 @@ __global__ __launch_bounds__(SR_THREADS) void k_ev_scatter_rec(const uint64_t *_
             if (r.in && !k) pos = gb + (unsigned)__popcll(gm & ((UINT64_C(1) << ln) - 1));
         }
         if (!r.in) pos = (unsigned)n + (unsigned)ln;
-        const uint64_t spb = kPayload ? r.sp : r.sv == 0 ? SPEED_NULL_BITS
-                                                        : __builtin_bit_cast(double, r.sp) != __builtin_bit_cast(double, r.sp) ? CANON_NAN_BITS : r.sp;
+        const uint64_t spb = r.sv == 0 ? SPEED_NULL_BITS
+                                       : __builtin_bit_cast(double, r.sp) != __builtin_bit_cast(double, r.sp) ? CANON_NAN_BITS : r.sp;
         const uint64_t lab = __builtin_bit_cast(uint64_t, r.la), lob = __builtin_bit_cast(uint64_t, r.lo);
         ws[ln * 2 + 0] = make_uint4((unsigned)k, (unsigned)(k >> 32), (unsigned)spb, (unsigned)(spb >> 32));
         ws[ln * 2 + 1] = make_uint4((unsigned)lab, (unsigned)(lab >> 32), (unsigned)lob, (unsigned)(lob >> 32));
@@ -453,27 +347,4 @@ __global__ __launch_bounds__(SR_THREADS) void k_ev_scatter_rec(const uint64_t *_
         i0 += 2 * SR_THREADS;
         if (i0 >= t1) break;
     }
-}
-
-// the multi-GPU owner's census: received direct-path records per global window slot (sizes the window tables)
-struct SlotSink {
-    unsigned long long *cnt;   // WREG_SLOTS counters
-    __device__ bool add(unsigned long long id, unsigned long long c) const {
-        atomicAdd(&cnt[id - 1], c);
-        return true;
-    }
-};
-__global__ __launch_bounds__(256) void k_key_census(const uint64_t *__restrict__ keys, int64_t n, unsigned long long *cnt) {
-    __shared__ WinLds WL;
-    wl_init(WL);
-    __syncthreads();
-    const SlotSink sink{cnt};
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
-        const int64_t i = base + threadIdx.x;
-        const uint64_t k = i < n ? __builtin_nontemporal_load(&keys[i]) : 0;
-        wave_count_windows(k != 0, (unsigned long long)ekey_widx(k) + 1, 1ull, WL, sink);
-    }
-    __syncthreads();
-    wl_flush(WL, sink);
 }

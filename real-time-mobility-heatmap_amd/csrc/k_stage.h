@@ -9,7 +9,7 @@ template <typename Rec>
 __device__ __forceinline__ int rec_owner(const Rec &r, int nranks);
 template <>
 __device__ __forceinline__ int rec_owner<TilePartial>(const TilePartial &r, int nranks) {
-    return owner_of(tile_hash(r.cell, r.wstart), nranks);
+    return tile_owner_of(tile_hash(r.cell, r.wstart), nranks);
 }
 template <>
 __device__ __forceinline__ int rec_owner<Cand>(const Cand &r, int nranks) {
@@ -89,5 +89,152 @@ __global__ __launch_bounds__(256) void k_winner_route(const Cand *__restrict__ c
         if (o < 0 || o >= nranks) continue;
         unsigned long long p = atomicAdd(&counts_or_cursor[o], 1ull);
         if (pass == 1) out[p] = c.row;
+    }
+}
+
+// =====================================================================================================
+// The multi-GPU exchange: ONE chunk per (sender, destination) rank, moved by one all_to_all (hm_stage_send ->
+// hm_stage_merge).  Every part 32-B aligned:
+//   ChunkHdr (64 B)
+//   direct path:  u32 counts[bins] -- the records of each region field the destination owns (shard_lo range, in
+//                 order); u32 census[CENSUS_WORDS] -- records per global window slot (the destination's table sizes)
+//   records       direct: EventRec with the batch's GLOBAL window slot in the key, grouped by region field;
+//                 table mode: TilePartial
+//   candidates    Cand (latest positions, to the vkey's owner)
+// A record's destination is tile_owner_of(its key hash): contiguous ranges of region fields, so the sender's (window,
+// region) bins -- k_ingest's fused binning, or the partition with one bin per region field -- are already grouped by
+// destination, and the owner merges each bin from its senders' segments (no second partition).
+// =====================================================================================================
+constexpr int64_t CHUNK_MAGIC = 0x314b4e5548434d48ll;   // "HMCHUNK1"
+constexpr int CENSUS_WORDS = WREG_SLOTS + 1;
+struct ChunkHdr {
+    int64_t magic;
+    int64_t records;
+    int64_t cands;
+    int64_t rec_bytes;   // 32 (EventRec) or 48 (TilePartial)
+    int64_t bins;        // direct path: the destination's region fields; table mode: 0
+    int64_t recs_off;    // bytes from the chunk's start
+    int64_t cands_off;
+    int64_t bytes;       // the whole chunk
+};
+static_assert(sizeof(ChunkHdr) == 64, "ChunkHdr is 64 B");
+HM_HD int64_t pad32(int64_t b) { return (b + 31) & ~int64_t(31); }
+// the layout of a chunk of `records` records (rec_bytes each) and `cands` candidates; bins > 0: the direct path's
+// counts and census precede the records
+HM_HD ChunkHdr chunk_layout(int64_t records, int64_t cands, int64_t rec_bytes, int64_t bins) {
+    ChunkHdr h{};
+    h.magic = CHUNK_MAGIC;
+    h.records = records;
+    h.cands = cands;
+    h.rec_bytes = rec_bytes;
+    h.bins = bins;
+    h.recs_off = (int64_t)sizeof(ChunkHdr) + (bins > 0 ? pad32(bins * 4) + pad32((int64_t)CENSUS_WORDS * 4) : 0);
+    h.cands_off = h.recs_off + pad32(records * rec_bytes);
+    h.bytes = h.cands_off + cands * (int64_t)sizeof(Cand);
+    return h;
+}
+HM_HD int64_t chunk_census_off(int64_t bins) { return (int64_t)sizeof(ChunkHdr) + pad32(bins * 4); }
+
+// Sender, direct path: one workgroup per region field b -- its records (slab b of k_ingest's fused binning, or the
+// partition's bin b: [S[b * stride] - S[lo]) ...) copied into its owner's chunk with the key's window slot rewritten to
+// the batch's global slot; the bin's count and the records' census into the chunk.  slab > 0: bin b's records start at
+// src + b * slab, else at src + S[b * stride].  S: exclusive scan of the bins' record counts (stride words apart).
+__global__ __launch_bounds__(256) void k_stage_pack(const EventRec *__restrict__ src, int64_t slab,
+                                                    const unsigned long long *__restrict__ S, int64_t stride,
+                                                    const unsigned short *__restrict__ gslot_of, int nranks,
+                                                    const int64_t *__restrict__ chunk_start, uint8_t *__restrict__ out) {
+    __shared__ unsigned cc[CENSUS_WORDS];
+    for (int q = threadIdx.x; q < CENSUS_WORDS; q += blockDim.x) cc[q] = 0;
+    __syncthreads();
+    const int b = blockIdx.x;
+    const int o = (int)(((unsigned)b * (unsigned)nranks) >> REGION_BITS);
+    const unsigned lo = shard_lo(o, nranks), hi = shard_lo(o + 1, nranks);
+    const int64_t s0 = (int64_t)S[(int64_t)b * stride], cnt = (int64_t)S[(int64_t)(b + 1) * stride] - s0;
+    const int64_t dst0 = s0 - (int64_t)S[(int64_t)lo * stride];
+    uint8_t *chunk = out + chunk_start[o];
+    const int64_t census_off = chunk_census_off((int64_t)(hi - lo));
+    const ChunkHdr lay = chunk_layout(0, 0, (int64_t)sizeof(EventRec), (int64_t)(hi - lo));
+    if (threadIdx.x == 0) ((unsigned *)(chunk + sizeof(ChunkHdr)))[b - lo] = (unsigned)cnt;
+    const EventRec *in = src + (slab > 0 ? (int64_t)b * slab : s0);
+    EventRec *dst = (EventRec *)(chunk + lay.recs_off) + dst0;
+    for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+        EventRec r = in[i];
+        const unsigned g = gslot_of[ekey_widx(r.key)];
+        r.key = (r.key & CELL_LO) | ((uint64_t)(g + 1) << 52);
+        dst[i] = r;
+        atomicAdd(&cc[g], 1u);
+    }
+    __syncthreads();
+    unsigned *census = (unsigned *)(chunk + census_off);
+    for (int q = threadIdx.x; q < CENSUS_WORDS; q += blockDim.x)
+        if (cc[q]) atomicAdd(&census[q], cc[q]);
+}
+
+// Owner, direct path: the segments of every region field it owns.  For bin b (global numbering, in [lo, hi)) and
+// sender s: its records start at record index SO[b * nseg + s] of the receive buffer (in EventRecs) and hold
+// C[s][b - lo] of them (the chunk's counts); SP[b * nseg + s] = the records of b from senders < s; T[b] = all of them.
+// C is read from each chunk (chunk_off[s]: its byte offset); prefix: the exclusive scan of k_stage_counts' rows.
+__global__ __launch_bounds__(256) void k_stage_segments(const uint8_t *__restrict__ recv, const int64_t *__restrict__ chunk_off,
+                                                        const unsigned long long *__restrict__ prefix, int nseg, unsigned lo,
+                                                        unsigned bins, unsigned long long *__restrict__ SO, unsigned *__restrict__ SP,
+                                                        unsigned *__restrict__ T) {
+    for (unsigned k = blockIdx.x * blockDim.x + threadIdx.x; k < (unsigned)RP_BINS; k += gridDim.x * blockDim.x) {
+        if (k < lo || k >= lo + bins) {
+            T[k] = 0;
+            continue;
+        }
+        const unsigned j = k - lo;
+        unsigned acc = 0;
+        for (int s = 0; s < nseg; s++) {
+            const uint8_t *chunk = recv + chunk_off[s];
+            const ChunkHdr lay = chunk_layout(0, 0, (int64_t)sizeof(EventRec), (int64_t)bins);
+            const unsigned c = ((const unsigned *)(chunk + sizeof(ChunkHdr)))[j];
+            const unsigned long long *P = prefix + (int64_t)s * (bins + 1);   // (one scan over all senders' rows)
+            SO[(int64_t)k * nseg + s] = (unsigned long long)((chunk_off[s] + lay.recs_off) / (int64_t)sizeof(EventRec)) + (P[j] - P[0]);
+            SP[(int64_t)k * nseg + s] = acc;
+            acc += c;
+        }
+        T[k] = acc;
+    }
+}
+// the chunks' counts as one u32 array per sender (scan input: [s][0, bins])
+__global__ __launch_bounds__(256) void k_stage_counts(const uint8_t *__restrict__ recv, const int64_t *__restrict__ chunk_off,
+                                                      int nseg, unsigned bins, unsigned *__restrict__ C) {
+    const int64_t m = (int64_t)nseg * (bins + 1);
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (int64_t)gridDim.x * blockDim.x) {
+        const int s = (int)(q / (bins + 1));
+        const unsigned j = (unsigned)(q % (bins + 1));
+        C[q] = j < bins ? ((const unsigned *)(recv + chunk_off[s] + sizeof(ChunkHdr)))[j] : 0u;
+    }
+}
+// sender: every chunk's header, and its counts and census zeroed (one workgroup per destination)
+__global__ __launch_bounds__(256) void k_stage_chunk_init(const ChunkHdr *__restrict__ hdr, const int64_t *__restrict__ chunk_start,
+                                                          uint8_t *__restrict__ out) {
+    const int o = blockIdx.x;
+    uint8_t *chunk = out + chunk_start[o];
+    const ChunkHdr h = hdr[o];
+    if (threadIdx.x == 0) *(ChunkHdr *)chunk = h;
+    unsigned *z = (unsigned *)(chunk + sizeof(ChunkHdr));
+    const int64_t nz = (h.recs_off - (int64_t)sizeof(ChunkHdr)) / 4;
+    for (int64_t q = threadIdx.x; q < nz; q += blockDim.x) z[q] = 0u;
+}
+// the region-field bin starts at the destinations' range starts: out[o] = S[shard_lo(o) * stride], o = 0..nranks
+__global__ void k_shard_starts(const unsigned long long *__restrict__ S, int64_t stride, int nranks, unsigned long long *out) {
+    for (int o = threadIdx.x; o <= nranks; o += blockDim.x) out[o] = S[(int64_t)shard_lo(o, nranks) * stride];
+}
+// owner: the senders' headers gathered (one 64-B header per chunk) and their census summed (per global window slot)
+__global__ __launch_bounds__(256) void k_stage_headers(const uint8_t *__restrict__ recv, const int64_t *__restrict__ chunk_off,
+                                                       const int64_t *__restrict__ chunk_bytes, int nseg, ChunkHdr *__restrict__ hdr,
+                                                       int64_t census_off, unsigned long long *__restrict__ census) {
+    for (int s = threadIdx.x; s < nseg; s += blockDim.x) {
+        if (chunk_bytes[s] >= (int64_t)sizeof(ChunkHdr)) hdr[s] = *(const ChunkHdr *)(recv + chunk_off[s]);
+        else hdr[s] = ChunkHdr{};
+    }
+    if (census_off <= 0) return;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < CENSUS_WORDS; q += gridDim.x * blockDim.x) {
+        unsigned long long a = 0;
+        for (int s = 0; s < nseg; s++)
+            if (chunk_bytes[s] >= census_off + CENSUS_WORDS * 4) a += ((const unsigned *)(recv + chunk_off[s] + census_off))[q];
+        census[q] = a;
     }
 }

@@ -155,8 +155,11 @@ struct GenDesc {
     unsigned long long wenc;   // 0 = empty map slot
     TileSlot *tab;
     unsigned long long rmask;  // slots per region - 1
-    unsigned int rshift;       // log2(slots per region)
-    unsigned int rbits;        // log2(regions), <= REGION_BITS
+    unsigned short rshift;     // log2(slots per region)
+    unsigned char rbits;       // log2(regions), <= REGION_BITS
+    unsigned char sb;          // a key's table region is (region field >> sb) - rbase
+    unsigned int rbase;        // (sb = REGION_BITS - rbits, rbase = 0: every region field has a region; sb = 0:
+                               // the table holds the region fields [rbase, rbase + 2^rbits) -- a shard's owned range)
     unsigned long long count;  // keys of this window in its table (the merge adds created keys)
     unsigned long long batch_parts;   // partials of the current batch in this window (0: not merged into now)
 };
@@ -246,11 +249,15 @@ inline FloorDiv make_floor_div(int64_t d) {
 }
 
 HM_HD uint64_t vkey_hash(uint64_t v) { return mix64(v ^ UINT64_C(0x2545f4914f6cdd1d)); }
-// owner rank of a key: taken from high hash bits so it is independent of the table index bits
+// owner rank of a vkey (latest-position candidates): high hash bits
 HM_HD int owner_of(uint64_t h, int nranks) { return (int)(((h >> 32) * (uint64_t)nranks) >> 32); }
-// a key's REGION_BITS-bit region field, hash bits [32 - REGION_BITS, 32) (independent of the table size and of
-// the owner bits)
+// a key's REGION_BITS-bit region field, hash bits [32 - REGION_BITS, 32) (independent of the table size)
 HM_HD unsigned region_field(uint64_t h) { return (unsigned)(h >> (32 - REGION_BITS)) & ((1u << REGION_BITS) - 1); }
+// owner rank of a tile key (hash h): contiguous ranges of region fields, so that a rank's (window, region) bins --
+// k_ingest's fused binning -- are already grouped by owner, and an owner's tables hold only its range
+HM_HD int tile_owner_of(uint64_t h, int nranks) { return (int)((region_field(h) * (unsigned)nranks) >> REGION_BITS); }
+// the region fields rank r of nranks owns: [shard_lo(r), shard_lo(r + 1))
+HM_HD unsigned shard_lo(int r, int nranks) { return (unsigned)(((r << REGION_BITS) + nranks - 1) / nranks); }
 HM_HD unsigned window_salt(unsigned long long we) { return (unsigned)mix64(we ^ UINT64_C(0x51ed270b27e5b3c1)); }
 
 }  // namespace hm

@@ -14,14 +14,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MOBHEAT_LIB: load another build of the same ABI (kernel variants under csrc/variants/ for tuning runs)
 LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
 
-HM_ABI_VERSION = 9
+HM_ABI_VERSION = 10
 HM_MEM_HOST = 0
 HM_MEM_DEVICE = 1
 HM_E_INVALID, HM_E_HIP, HM_E_NOMEM, HM_E_OVERFLOW, HM_E_STATE, HM_E_UNSUPPORTED = -1, -2, -3, -4, -5, -6
 HM_STAGE_SUMMARY_WORDS = 8200
 HM_TILE_REC_BYTES = 48       # table mode's tile partial
-HM_TILE_KEY_BYTES = 8        # direct path: key stream
-HM_TILE_PAYLOAD_BYTES = 24   # direct path: payload stream
+HM_EVENT_REC_BYTES = 32      # direct path: one record per aggregated row
 HM_CAND_REC_BYTES = 32
 
 c_i32, c_i64, c_u64, c_dbl, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double, ctypes.c_void_p
@@ -31,7 +30,7 @@ class HmConfig(ctypes.Structure):
     _fields_ = [
         ("abi_version", c_i32), ("h3_res", c_i32), ("device", c_i32), ("late_uses_prev_watermark", c_i32),
         ("tile_us", c_i64), ("watermark_delay_ms", c_i64), ("state_capacity_hint", c_i64),
-        ("batch_capacity_hint", c_i64), ("state_arena_bytes", c_i64),
+        ("batch_capacity_hint", c_i64), ("state_arena_bytes", c_i64), ("shard_rank", c_i32), ("shard_count", c_i32),
     ]
 
 
@@ -98,8 +97,9 @@ SIGNATURES = {
     "hm_process_batch": (c_i32, [c_vp, c_i64, _P(HmBatchIn), c_i32, _P(HmBatchOut)]),
     "hm_latlng_to_cell": (c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp]),
     "hm_stage_ingest": (c_i32, [c_vp, c_i64, _P(HmBatchIn), c_i32, c_i32, c_vp]),
-    "hm_stage_send": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, _P(HmStageSizes)]),
-    "hm_stage_merge": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, _P(HmBatchOut), c_vp, c_i64, c_vp]),
+    "hm_stage_send_capacity": (c_i64, [c_i64, c_i32]),
+    "hm_stage_send": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, _P(HmStageSizes)]),
+    "hm_stage_merge": (c_i32, [c_vp, c_vp, c_vp, c_i32, _P(HmBatchOut), c_vp, c_i64, c_vp]),
     "hm_stage_finish": (c_i32, [c_vp, c_vp, c_i64, c_i32, _P(HmBatchOut)]),
     "hm_device_memory": (c_i32, [c_i32, _P(c_i64), _P(c_i64)]),
     "hm_device_alloc": (c_i32, [c_i32, c_i64, _P(c_vp)]),

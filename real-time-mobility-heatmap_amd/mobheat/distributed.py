@@ -1,18 +1,18 @@
 """Multi-GPU hot path: one process per GPU, torch.distributed (backend "nccl" = RCCL over xGMI).
 
 Replaces Spark's shuffle of the two aggregations (spark.sql.shuffle.partitions = 4, reference
-heatmap_stream.py:44).  Per micro-batch every rank snaps its own shard of the events (hm_stage_ingest), then
+heatmap_stream.py:44).  Per micro-batch every rank snaps its own shard of the events (hm_stage_ingest: large shards
+bin their records by region field inside k_ingest), then
 
   1. all_gather of the ranks' summaries (counts, max event time, window registry: ~64 KB per rank), from which
      every rank derives the same batch-wide decisions -- the watermark's input (:107), the aggregation path, the
      batch's global window registry;
-  2. hm_stage_send writes the records grouped by owner rank:
-       * direct path: one 32-B record per aggregated row, as a key stream (8 B) and a payload stream (24 B), owner
-         = hash(cell, windowStart) % world -- the owner merges them into the persistent state it owns and emits them;
-       * table mode (low cardinality): one 48-B tile partial per key of the shard;
-       * latest-position candidates (32 B: vkey, ts, row, origin rank) to owner hash(vkey) % world, which keeps the
-         rows tied at the global max and routes the winning row indices back to their origin;
-  3. ONE all_to_all of every stream's per-destination counts, then one all_to_all per stream;
+  2. hm_stage_send writes ONE chunk per destination rank (include/mobheat.h): its tile records -- direct path, one 32-B
+     record per aggregated row, grouped by region field with per-field counts and a per-window census; table mode,
+     one 48-B partial per key -- and its latest-position candidates (32 B: vkey, ts, row, origin rank).  A tile key's
+     owner holds a contiguous range of the key hash's region field (tile_owner), so the sender's bins are already
+     grouped by destination and the owner merges each of its bins from the senders' segments;
+  3. ONE all_to_all of the chunk sizes (with each rank's status), then ONE all_to_all of the chunks;
   4. hm_stage_merge on the owner, the winners' all_to_all back, hm_stage_finish.
 
 Ownership is a pure function of the key, so the persistent state never moves between batches.  The exchange buffers
@@ -26,8 +26,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from ._lib import (HM_CAND_REC_BYTES, HM_MEM_DEVICE, HM_STAGE_SUMMARY_WORDS, HM_TILE_KEY_BYTES, HM_TILE_PAYLOAD_BYTES,
-                   HM_TILE_REC_BYTES, HmBatchIn, HmBatchOut, HmStageSizes, check)
+from ._lib import HM_MEM_DEVICE, HM_STAGE_SUMMARY_WORDS, HmBatchIn, HmBatchOut, HmStageSizes, check
 
 # one record stream of an exchange: buf (uint8 tensor), counts[r] records for rank r, rec_bytes per record
 Stream = namedtuple("Stream", "name buf counts rec_bytes")
@@ -37,7 +36,7 @@ Stream = namedtuple("Stream", "name buf counts rec_bytes")
 SW_N_IN, SW_VALID, SW_LATE, SW_AGG, SW_MAX_MS, SW_SAMPLE_RUN, SW_PREV_AGG, SW_PREV_KEYS, SW_NWIN, SW_STATUS = range(10)
 SW_WIN0 = 10
 WREG_SLOTS = 4095
-MAX_STREAMS = 3   # record streams of one exchange (direct path: key, payload, candidates)
+MAX_STREAMS = 1   # record streams of one exchange (exchange(): the winners)
 
 
 class PeerFailed(RuntimeError):
@@ -94,6 +93,32 @@ def exchange(streams, device, status=0):
     return out
 
 
+def exchange_chunks(buf, send_bytes, device, status=0):
+    """The batch's record exchange: one all_to_all of the per-destination chunk sizes in bytes (with this rank's
+    status: a rank whose stage failed sends status != 0 and no chunks, and every rank raises PeerFailed before the
+    payloads move), then ONE all_to_all of the chunks, as 8-byte words (chunk sizes are multiples of 32; a rank's share
+    at 1e8 events per GPU is several GB, past 2^31 single-byte elements).  Returns (recv uint8 tensor, recv_bytes per
+    source rank)."""
+    world = dist.get_world_size()
+    sc = torch.tensor([[int(send_bytes[r]) if send_bytes else 0, status] for r in range(world)], dtype=torch.int64,
+                      device=device)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc)
+    rs = rc.cpu().tolist()
+    bad = [r for r in range(world) if rs[r][1]]
+    if bad and status == 0:
+        raise PeerFailed(f"rank(s) {bad} failed the batch's stage before the exchange")
+    if status:
+        return None, []
+    recv_bytes = [int(rs[r][0]) for r in range(world)]
+    assert all(b % 8 == 0 for b in recv_bytes) and all(int(b) % 8 == 0 for b in send_bytes)
+    nrecv, nsend = sum(recv_bytes), int(sum(send_bytes))
+    recv = torch.empty(max(nrecv // 8, 2), dtype=torch.int64, device=device)
+    dist.all_to_all_single(recv[: nrecv // 8], buf[:nsend].view(torch.int64), [b // 8 for b in recv_bytes],
+                           [int(b) // 8 for b in send_bytes])
+    return recv.view(torch.uint8), recv_bytes
+
+
 def global_window_registry(summaries, tile_us):
     """Python twin of the library's stage_decide registry: the union of the ranks' windows in ascending order,
     hashed like k_ingest's registry (slot = window quotient mod WREG_SLOTS, linear probing).  Returns wenc per slot."""
@@ -147,35 +172,30 @@ class LibStages:
         return self._summary
 
     def send(self, summaries):
+        """-> (send buffer, bytes of each destination's chunk)"""
         world, n = self.world, self._n
         summaries = np.ascontiguousarray(summaries, dtype=np.int64)
-        tile = self._buf("tile", n * HM_TILE_REC_BYTES)
-        pay = self._buf("payload", n * HM_TILE_PAYLOAD_BYTES)
-        cand = self._buf("cand", n * HM_CAND_REC_BYTES)
-        tc, cc = (ctypes.c_int64 * world)(), (ctypes.c_int64 * world)()
+        cap = int(self.lib.hm_stage_send_capacity(n, world))
+        buf = self._buf("send", cap)
+        sb = (ctypes.c_int64 * world)()
         sizes = HmStageSizes()
         ctx = self.engine._ctx
-        check(self.lib.hm_stage_send(ctx, summaries.ctypes.data, tile.data_ptr(), pay.data_ptr(), n, tc, cand.data_ptr(),
-                                     n, cc, ctypes.byref(sizes)), ctx, "hm_stage_send")
+        check(self.lib.hm_stage_send(ctx, summaries.ctypes.data, buf.data_ptr(), cap, sb, ctypes.byref(sizes)), ctx,
+              "hm_stage_send")
         self.table_mode = bool(sizes.table_mode)
-        if self.table_mode:
-            return [Stream("tile", tile, list(tc), HM_TILE_REC_BYTES), Stream("cand", cand, list(cc), HM_CAND_REC_BYTES)]
-        return [Stream("tile", tile, list(tc), HM_TILE_KEY_BYTES), Stream("payload", pay, list(tc), HM_TILE_PAYLOAD_BYTES),
-                Stream("cand", cand, list(cc), HM_CAND_REC_BYTES)]
+        self.sizes = sizes
+        return buf, list(sb)
 
-    def merge(self, recv, out_memory):
+    def merge(self, recv, recv_bytes, out_memory):
         world = self.world
-        (tile_recv, trc) = recv[0]
-        pay_recv = None if self.table_mode else recv[1][0]
-        cand_recv, crc = recv[-1]
-        n_tile, n_cand = int(sum(trc)), int(sum(crc))
-        winner_send = self._buf("winner", max(n_cand, 1) * 8)
+        cap = max(sum(recv_bytes) // 32, 1)   # (candidates are 32 B each: at most one winner per received 32 B)
+        winner_send = self._buf("winner", cap * 8)
+        rb = (ctypes.c_int64 * world)(*recv_bytes)
         wc = (ctypes.c_int64 * world)()
         out = HmBatchOut()
         ctx = self.engine._ctx
-        check(self.lib.hm_stage_merge(ctx, tile_recv.data_ptr(), None if pay_recv is None else pay_recv.data_ptr(), n_tile,
-                                      cand_recv.data_ptr(), n_cand, out_memory, ctypes.byref(out), winner_send.data_ptr(),
-                                      max(n_cand, 1), wc), ctx, "hm_stage_merge")
+        check(self.lib.hm_stage_merge(ctx, recv.data_ptr(), rb, out_memory, ctypes.byref(out), winner_send.data_ptr(),
+                                      cap, wc), ctx, "hm_stage_merge")
         return out, Stream("winner", winner_send, list(wc), 8)
 
     def finish(self, winner_recv, n_winner, out_memory, out):
@@ -213,14 +233,14 @@ class ShardedHeatmap:
         if err:
             raise err
         try:
-            streams = self.stages.send(summaries)
+            buf, send_bytes = self.stages.send(summaries)
         except Exception as e:
-            exchange([], self.device, status=1)
+            exchange_chunks(None, None, self.device, status=1)
             raise e
-        recv = exchange(streams, self.device)
+        recv, recv_bytes = exchange_chunks(buf, send_bytes, self.device)
         sync()
         try:
-            out, winners = self.stages.merge(recv, out_memory)
+            out, winners = self.stages.merge(recv, recv_bytes, out_memory)
         except Exception as e:
             exchange([], self.device, status=1)
             raise e
@@ -237,9 +257,22 @@ def tile_hash(cell, wstart):
                                                            np.uint64(0x9E3779B97F4A7C15)))
 
 
+REGION_BITS = 13
+
+
+def region_field(h):
+    """Python twin of kernels.h region_field: hash bits [32 - REGION_BITS, 32)."""
+    return ((np.asarray(h, np.uint64) >> np.uint64(32 - REGION_BITS)) & np.uint64((1 << REGION_BITS) - 1)).astype(np.int64)
+
+
+def shard_lo(r, world):
+    """The first region field rank r of `world` owns (kernels.h shard_lo)."""
+    return ((r << REGION_BITS) + world - 1) // world
+
+
 def tile_owner(cell, wstart, world):
-    """Python twin of the device routing (kernels.h owner_of(tile_hash(...)))."""
-    return _owner(tile_hash(cell, wstart), world)
+    """Python twin of the device routing (kernels.h tile_owner_of(tile_hash(...))): contiguous region-field ranges."""
+    return (region_field(tile_hash(cell, wstart)) * world) >> REGION_BITS
 
 
 def vkey_owner(vkey, world):

@@ -70,7 +70,10 @@ def _u8(a, n):
 
 class HeatmapEngine:
     def __init__(self, h3_res=8, tile_minutes=5, watermark_delay_ms=600_000, device=0,
-                 late_uses_prev_watermark=True, state_capacity_hint=0, batch_capacity_hint=0, state_arena_bytes=0):
+                 late_uses_prev_watermark=True, state_capacity_hint=0, batch_capacity_hint=0, state_arena_bytes=0,
+                 shard=None):
+        """shard: (rank, world) of a multi-GPU stage context (its state holds only the keys that rank owns); None =
+        fixed by the first hm_stage_ingest, or a single GPU."""
         self._lib = _lib.load()
         self.h3_res = int(h3_res)
         self.tile_us = int(tile_minutes) * 60 * 1_000_000
@@ -78,7 +81,8 @@ class HeatmapEngine:
         cfg = HmConfig(abi_version=_lib.HM_ABI_VERSION, h3_res=self.h3_res, device=self.device,
                        late_uses_prev_watermark=1 if late_uses_prev_watermark else 0, tile_us=self.tile_us,
                        watermark_delay_ms=int(watermark_delay_ms), state_capacity_hint=int(state_capacity_hint),
-                       batch_capacity_hint=int(batch_capacity_hint), state_arena_bytes=int(state_arena_bytes))
+                       batch_capacity_hint=int(batch_capacity_hint), state_arena_bytes=int(state_arena_bytes),
+                       shard_rank=int(shard[0]) if shard else 0, shard_count=int(shard[1]) if shard else 0)
         h = ctypes.c_void_p()
         check(self._lib.hm_create(ctypes.byref(cfg), ctypes.byref(h)), None, "hm_create")
         self._ctx = h

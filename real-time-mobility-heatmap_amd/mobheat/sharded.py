@@ -145,7 +145,7 @@ class RankRunner:
         from .engine import HeatmapEngine
         c = self.cfg
         eng = HeatmapEngine(h3_res=c["h3_res"], tile_minutes=c["tile_minutes"], watermark_delay_ms=c["delay_ms"],
-                            device=self.device_index)
+                            device=self.device_index, shard=(self.rank, self.world))
         kind, val = restore
         if kind == "point":
             info, recs = self.store.load(val, owner=lambda cl, ws: tile_owner(cl, ws, self.world) == self.rank)

@@ -39,5 +39,10 @@ def test_stage_bytes_multi_gpu_owner():
     n, R, S = 50_000_000, 49_000_000, 50_000_000
     c = {"partials": R, "tiles": R, "state_new": R, "table_mode": False, "sent": S}
     s = b.stage_bytes(n, c, world=2)
-    assert s["send"] == 16 * n + (25 + 32) * S        # keys read twice; columns read, key + payload written
-    assert s["partition"] == (8 + 8 + 8 + 24 + 32) * R
+    # the sender's partition by region field (keys read twice; columns read, the 32-B record written), then each
+    # record read from its bin and written into its destination's chunk; the owner merges without a partition
+    assert s["partition"] == 16 * n + (25 + 32) * S
+    assert s["send"] == (32 + 32) * S
+    assert s["merge"] == 32 * R + 113 * R
+    s = b.stage_bytes(n, dict(c, binned=1), world=2)
+    assert s["partition"] == 0 and s["ingest"] == 51 * n + 32 * S and s["send"] == 64 * S

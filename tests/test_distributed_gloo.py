@@ -1,8 +1,8 @@
 """CPU, world_size 2 over gloo: the sharded path (mobheat.distributed.ShardedHeatmap) -- ingest, all_gather of the
-ranks' summaries, the batch-wide decisions (global window registry, max event time), the owner-grouped record streams
-(direct path: 8-B keys + 24-B payloads; table mode: 48-B tile partials; 32-B latest candidates), one all_to_all of
-every stream's counts then one per stream, owner merge, winners routed back -- must produce exactly the single-shard
-result.
+ranks' summaries, the batch-wide decisions (global window registry, max event time), one chunk per destination
+(direct path: 32-B records grouped by region field with per-field counts and a window census; table mode: 48-B tile
+partials; 32-B latest candidates: tests/stage_chunks.py), one all_to_all of the chunk sizes then one of the chunks,
+owner merge, winners routed back -- must produce exactly the single-shard result.
 
 The stages here are a numpy restatement of hm_stage_ingest / send / merge / finish built on the oracle (test-only
 stand-in for the GPU) that writes the library's wire formats; the orchestration, exchange code, owner functions and
@@ -18,10 +18,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-TILE_DT = np.dtype([("cell", "<u8"), ("ws", "<i8"), ("count", "<u4"), ("nsp", "<u4"), ("ssp", "<f8"), ("slat", "<f8"),
-                    ("slon", "<f8")])   # HM_TILE_REC_BYTES = 48
-PAY_DT = np.dtype([("sp", "<u8"), ("lat", "<f8"), ("lon", "<f8")])   # HM_TILE_PAYLOAD_BYTES = 24
-CAND_DT = np.dtype([("vkey", "<u8"), ("ts", "<i8"), ("row", "<i8"), ("origin", "<i8")])
+from stage_chunks import CAND_DT, CENSUS_WORDS, EVENT_DT, TILE_DT, pack, unpack
 CELL_LO = (1 << 52) - 1
 SPEED_NULL = 0x7FF0000000000001
 I64_MIN = np.iinfo(np.int64).min
@@ -67,16 +64,12 @@ class OracleStages:
         return S
 
     def send(self, summaries):
-        from mobheat.distributed import SW_MAX_MS, Stream, global_window_registry, tile_hash, vkey_owner
-        from mobheat.distributed import _owner as owner_of
+        from mobheat.distributed import SW_MAX_MS, global_window_registry, region_field, shard_lo, tile_hash, tile_owner
         o, b, world, rank = self.o, self.b, self.world, self.rank
         self.gmax = int(max(S[SW_MAX_MS] for S in summaries))
         self.reg = global_window_registry(summaries, o.tile)
         gslot = {we: i for i, we in enumerate(self.reg) if we}
         agg, cells, ws = self.agg, self.cells, self.ws
-        own = owner_of(tile_hash(cells, ws), world)
-        order = np.argsort(own, kind="stable")
-        tcounts = np.bincount(own, minlength=world).tolist()
         if self.table:
             recs = np.zeros(0, TILE_DT)
             if agg.size:
@@ -91,17 +84,25 @@ class OracleStages:
                 recs["ssp"] = np.bincount(inv[sv], weights=b["speed"][agg][sv], minlength=uq.size)
                 recs["slat"] = np.bincount(inv, weights=b["lat"][agg], minlength=uq.size)
                 recs["slon"] = np.bincount(inv, weights=b["lon"][agg], minlength=uq.size)
-            own = owner_of(tile_hash(recs["cell"], recs["ws"]), world)
-            order = np.argsort(own, kind="stable")
-            streams = [Stream("tile", _t(recs[order]), np.bincount(own, minlength=world).tolist(), 48)]
+            own = tile_owner(recs["cell"], recs["ws"], world)
+            per_dest = [(recs[own == d], None, None, None) for d in range(world)]
         else:
-            key = (cells & np.uint64(CELL_LO)) | (np.array([gslot[int(w)] + 1 for w in _wenc(ws)], np.uint64) << np.uint64(52))
-            pay = np.zeros(agg.size, PAY_DT)
+            slot = np.array([gslot[int(w)] for w in _wenc(ws)], np.int64)
+            recs = np.zeros(agg.size, EVENT_DT)
+            recs["key"] = (cells & np.uint64(CELL_LO)) | ((slot + 1).astype(np.uint64) << np.uint64(52))
             sv, sp = b["speed_valid"][agg], b["speed"][agg]
             bits = np.where(np.isnan(sp), np.uint64(0x7FF8000000000000), sp.view(np.uint64))
-            pay["sp"] = np.where(sv, bits, np.uint64(SPEED_NULL))
-            pay["lat"], pay["lon"] = b["lat"][agg], b["lon"][agg]
-            streams = [Stream("tile", _t(key[order]), tcounts, 8), Stream("payload", _t(pay[order]), tcounts, 24)]
+            recs["sp"] = np.where(sv, bits, np.uint64(SPEED_NULL))
+            recs["lat"], recs["lon"] = b["lat"][agg], b["lon"][agg]
+            field = region_field(tile_hash(cells, ws))
+            order = np.argsort(field, kind="stable")
+            recs, field, slot = recs[order], field[order], slot[order]
+            per_dest = []
+            for d in range(world):
+                lo, hi = shard_lo(d, world), shard_lo(d + 1, world)
+                m = (field >= lo) & (field < hi)
+                per_dest.append((recs[m], hi - lo, np.bincount(field[m] - lo, minlength=hi - lo).astype(np.uint32),
+                                 np.bincount(slot[m], minlength=CENSUS_WORDS).astype(np.uint32)))
         # local latest candidates: rows tied at the local max of their vehicle
         v = np.nonzero(self.valid)[0]
         ts = b["ts_us"]
@@ -114,21 +115,21 @@ class OracleStages:
             win = srt[tv[srt] == tv[srt][last][grp]]
             cands = np.zeros(win.size, CAND_DT)
             cands["vkey"], cands["ts"], cands["row"], cands["origin"] = vk[win], tv[win], v[win], rank
+        from mobheat.distributed import vkey_owner
         cown = vkey_owner(cands["vkey"], world)
-        corder = np.argsort(cown, kind="stable")
-        return streams + [Stream("cand", _t(cands[corder]), np.bincount(cown, minlength=world).tolist(), 32)]
+        chunks = [pack(r, cands[cown == d], bins, cnt, cen) for d, (r, bins, cnt, cen) in enumerate(per_dest)]
+        return _t(np.concatenate(chunks)), [c.size for c in chunks]
 
-    def merge(self, recv, out_memory):
+    def merge(self, recv, recv_bytes, out_memory):
         from mobheat.distributed import Stream
         o = self.o
+        got, cands, _ = unpack(recv.numpy()[: sum(recv_bytes)], recv_bytes, direct=not self.table)
         if self.table:
-            (tb, trc) = recv[0]
-            recs = tb.numpy()[: sum(trc) * 48].view(TILE_DT)
+            recs = got
         else:
-            (kb, trc), (pb, _) = recv[0], recv[1]
-            n = sum(trc)
-            key = kb.numpy()[: n * 8].view(np.uint64)
-            pay = pb.numpy()[: n * 24].view(PAY_DT)
+            n = got.size
+            key = got["key"]
+            pay = got
             wenc = np.array(self.reg, np.uint64)[(key >> np.uint64(52)).astype(np.int64) - 1]
             recs = np.zeros(n, TILE_DT)
             recs["cell"] = (key & np.uint64(CELL_LO)) | np.uint64((1 << 59) | (self.res << 52))
@@ -154,8 +155,6 @@ class OracleStages:
             del o.state[k]
         nxt = o.wm_cur if self.gmax == I64_MIN else max(o.wm_cur, self.gmax - o.delay)
         o.wm_prev, o.wm_cur = o.wm_cur, nxt
-        cand_recv, crc = recv[-1]
-        cands = cand_recv.numpy()[: sum(crc) * 32].view(CAND_DT)
         world = self.world
         rows_by_origin = [[] for _ in range(world)]
         if cands.size:

@@ -38,8 +38,7 @@ class DevBuf:
 def _stage_batch(engines, lib, batches_per_rank, epoch):
     """One micro-batch through the stage API of W contexts, exchanges routed on the host.  Returns the owners' tiles,
     each rank's latest rows, per-rank tile/candidate send counts and whether table mode ran."""
-    from mobheat._lib import (HM_CAND_REC_BYTES, HM_MEM_HOST, HM_STAGE_SUMMARY_WORDS, HM_TILE_KEY_BYTES,
-                              HM_TILE_PAYLOAD_BYTES, HM_TILE_REC_BYTES, HmBatchIn, HmBatchOut, HmStageSizes, check)
+    from mobheat._lib import HM_MEM_HOST, HM_STAGE_SUMMARY_WORDS, HmBatchIn, HmBatchOut, HmStageSizes, check
     W = len(engines)
     bufs, keep = [], []
     summaries = np.zeros((W, HM_STAGE_SUMMARY_WORDS), np.int64)
@@ -52,54 +51,53 @@ def _stage_batch(engines, lib, batches_per_rank, epoch):
                        ts_us=k["ts_us"].ctypes.data, speed=k["speed"].ctypes.data, speed_valid=k["sv"].ctypes.data,
                        vkey=k["vkey"].ctypes.data, row_valid=k["rv"].ctypes.data)
         check(lib.hm_stage_ingest(eng._ctx, epoch, ctypes.byref(bi), W, r, summaries[r].ctypes.data), eng._ctx)
-    sends, tcounts, ccounts, table = [], [], [], None
+    from stage_chunks import unpack
+    sends, sbytes, tcounts, ccounts, table = [], [], [], [], None
     for r, (eng, b) in enumerate(zip(engines, batches_per_rank)):
         n = b["lat"].size
-        tb, pb, cb = DevBuf(lib, n * HM_TILE_REC_BYTES), DevBuf(lib, n * HM_TILE_PAYLOAD_BYTES), DevBuf(lib, n * HM_CAND_REC_BYTES)
-        bufs += [tb, pb, cb]
-        tc, cc = (ctypes.c_int64 * W)(), (ctypes.c_int64 * W)()
+        cap = lib.hm_stage_send_capacity(n, W)
+        sb_ = DevBuf(lib, cap)
+        bufs.append(sb_)
+        sb = (ctypes.c_int64 * W)()
         sz = HmStageSizes()
-        check(lib.hm_stage_send(eng._ctx, summaries.ctypes.data, tb.p, pb.p, n, tc, cb.p, n, cc, ctypes.byref(sz)), eng._ctx)
+        check(lib.hm_stage_send(eng._ctx, summaries.ctypes.data, sb_.p, cap, sb, ctypes.byref(sz)), eng._ctx)
         assert table is None or table == bool(sz.table_mode), "ranks disagree on the aggregation path"
         table = bool(sz.table_mode)
         assert sz.global_batch_max_event_ms == max(summaries[:, 4])
-        tcounts.append(list(tc)); ccounts.append(list(cc))
-        if not table:   # one 32-B wire record (8-B key + 24-B payload) per aggregated row of the rank
+        raw = sb_.get(sum(sb))
+        sends.append(raw)
+        sbytes.append(list(sb))
+        off, tc, cc = 0, [], []
+        for d in range(W):   # each destination's chunk: its header's record and candidate counts
+            h = raw[off: off + 64].view(np.int64)
+            tc.append(int(h[1]))
+            cc.append(int(h[2]))
+            off += sb[d]
+        tcounts.append(tc)
+        ccounts.append(cc)
+        if not table:   # one 32-B record per aggregated row of the rank
             assert sum(tc) == summaries[r][3] == sz.n_tile_records
-        trec = HM_TILE_REC_BYTES if table else HM_TILE_KEY_BYTES
-        sends.append((tb.get(sum(tc) * trec), None if table else pb.get(sum(tc) * HM_TILE_PAYLOAD_BYTES),
-                      cb.get(sum(cc) * HM_CAND_REC_BYTES)))
-
-    def route(r, kind, rec):
-        parts = []
-        for s in range(W):
-            cnt = (ccounts if kind == 2 else tcounts)[s]
-            off = sum(cnt[:r]) * rec
-            parts.append(sends[s][kind][off: off + cnt[r] * rec])
-        return np.concatenate(parts)
 
     outs, wsends, wcounts = [], [], []
     for r, eng in enumerate(engines):
-        trec = HM_TILE_REC_BYTES if table else HM_TILE_KEY_BYTES
-        trecv, crecv = route(r, 0, trec), route(r, 2, HM_CAND_REC_BYTES)
-        precv = None if table else route(r, 1, HM_TILE_PAYLOAD_BYTES)
-        tb, cb, wb = DevBuf(lib, trecv.nbytes), DevBuf(lib, crecv.nbytes), DevBuf(lib, max(crecv.nbytes // 4, 8))
-        pb = DevBuf(lib, 16 if table else precv.nbytes)
-        bufs += [tb, pb, cb, wb]
-        tb.put(trecv); cb.put(crecv)
-        if not table:
-            pb.put(precv)
-        nc = crecv.nbytes // HM_CAND_REC_BYTES
+        parts = [sends[s][sum(sbytes[s][:r]): sum(sbytes[s][:r + 1])] for s in range(W)]
+        recv = np.concatenate(parts)
+        rbytes = [p.size for p in parts]
+        recs, cands, _ = unpack(recv, rbytes, direct=not table)
+        nc = cands.size
+        rb_, wb = DevBuf(lib, recv.nbytes), DevBuf(lib, max(nc, 1) * 8)
+        bufs += [rb_, wb]
+        rb_.put(recv)
         out = HmBatchOut()
         wc = (ctypes.c_int64 * W)()
-        check(lib.hm_stage_merge(eng._ctx, tb.p, None if table else pb.p, trecv.nbytes // trec, cb.p, nc, HM_MEM_HOST,
-                                 ctypes.byref(out), wb.p, max(nc, 1), wc), eng._ctx)
+        check(lib.hm_stage_merge(eng._ctx, rb_.p, (ctypes.c_int64 * W)(*rbytes), HM_MEM_HOST, ctypes.byref(out), wb.p,
+                                 max(nc, 1), wc), eng._ctx)
         res = eng._result_from_host(out)
         outs.append(res.tiles)
         wcounts.append(list(wc))
         wsends.append(wb.get(sum(wc) * 8).view(np.int64))
         c = eng.last_counts()
-        assert c["partials"] == trecv.nbytes // trec and c["tiles"] == len(res.tiles) and c["sent"] == sum(tcounts[r])
+        assert c["partials"] == recs.size and c["tiles"] == len(res.tiles) and c["sent"] == sum(tcounts[r])
     latest = []
     for r, eng in enumerate(engines):
         rows = np.concatenate([wsends[s][sum(wcounts[s][:r]): sum(wcounts[s][:r + 1])] for s in range(W)])
@@ -116,11 +114,11 @@ def _stage_batch(engines, lib, batches_per_rank, epoch):
     return outs, latest, tcounts, ccounts, table
 
 
-@pytest.mark.parametrize("world,mode", [(2, "direct"), (3, "direct"), (2, "table")])
+@pytest.mark.parametrize("world,mode", [(2, "direct"), (3, "direct"), (2, "table"), (2, "binned"), (3, "binned")])
 def test_stage_api_matches_single_shard(world, mode, monkeypatch):
-    """Both aggregation paths pinned, four batches (one empty): on the direct path every aggregated row crosses as a
-    32-B record (8-B key with the batch's global window slot + 24-B payload) and the owner partitions them into the
-    same 32-B EventRecs the single-GPU merge uses."""
+    """Both aggregation paths pinned, four batches (one empty): on the direct path every aggregated row crosses as one
+    32-B record (the key with the batch's global window slot) grouped by region field, and the owner merges each of its
+    bins from the senders' segments with the single-GPU merge."""
     monkeypatch.setenv("MOBHEAT_INGEST_MODE", mode)
     import mobheat
     from mobheat import synth
