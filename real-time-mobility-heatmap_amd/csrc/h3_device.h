@@ -356,6 +356,7 @@ struct H3Tables {
     // [0] Class II, [1] Class III (rotated by -M_AP7_ROT_RADS); S_res = (1/RES0_U_GNOMONIC) sqrt(7)^res
     double fastU[2][20][2][3];
     double fastScale[16];
+    double fastTauS[16];   // the margin bound's S term: 8 x 32 eps S_res (a table constant: a uniform scalar load)
     int faceIjkBaseCells[20][3][3][3][2];
     int baseCellData[122][7];
     // cellToBoundary (h3_boundary.h): faceNeighbors[f][dir] = {face, translate i, j, k, ccwRot60} (dir 0 centre,
@@ -415,6 +416,7 @@ HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const TT &T) {
     // the classes alternate: pairs (odd r: Class II, then r - 1: Class III) with no class branch per digit
     int r = res - 1;
     if (!(r & 1)) up(r--, std::true_type{});
+#pragma unroll 1
     for (; r >= 1; r -= 2) {
         up(r, std::false_type{});
         up(r - 1, std::true_type{});
@@ -650,11 +652,9 @@ HM_HD bool latLngToCellFastP(double lat_deg, double lng_deg, int res, const H3Ta
 #else
     const double rq = (double)(1.0f / (float)sqd) * (1.0 + 0x1p-20);
 #endif
-    const double tau0 = M * (4.0 * rq + 145.0) * eps + S * 32.0 * eps;
-#ifndef HM_FAST_TAU_SCALE
-#define HM_FAST_TAU_SCALE 8.0
-#endif
-    const double tau = HM_FAST_TAU_SCALE * tau0;
+    // tau = 8 x that bound (the S term from the table: a loop-invariant fp64 value computed here was the register the
+    // resolution-specialised kernels spilled to scratch, reloaded with a full wait every round)
+    const double tau = (M * (4.0 * rq + 145.0)) * (8.0 * eps) + T.fastTauS[res];
     // _hex2dToCoordIJK with the margin of every comparison it makes
     const double x2 = a2 * 1.15470053837925152902;        // M_RSIN60
     const double x1 = a1 + x2 / 2.0;

@@ -39,7 +39,10 @@ static hm::H3Tables hm_make_tables() {
             T.fastU[1][f][1][k] = (double)(cosl(ap7) * uy[k] - sinl(ap7) * ux[k]);
         }
     }
-    for (int r = 0; r < 16; r++) T.fastScale[r] = (double)((long double)HM_INV_RES0_U_GNOMONIC * powl(sqrtl(7.0L), r));
+    for (int r = 0; r < 16; r++) {
+        T.fastScale[r] = (double)((long double)HM_INV_RES0_U_GNOMONIC * powl(sqrtl(7.0L), r));
+        T.fastTauS[r] = T.fastScale[r] * 32.0 * 0x1p-52 * 8.0;
+    }
     memcpy(T.faceIjkBaseCells, H3T_faceIjkBaseCells, sizeof(T.faceIjkBaseCells));
     memcpy(T.baseCellData, H3T_baseCellData, sizeof(T.baseCellData));
     memcpy(T.faceNeighbors, H3T_faceNeighbors, sizeof(T.faceNeighbors));

@@ -711,7 +711,7 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census, bool r
             Geo geo = gen_geometry(ctx, c, c, range);
             TileSlot *t = nullptr;
             if ((rc = table_acquire(ctx, geo, &t))) return rc;
-            ctx->gens.push_back(gen_of(w.wenc, t, geo, c, c));
+            ctx->gens.push_back(gen_of(w.wenc, t, geo, 0, c));   // (keys: the merge counts the ones it creates)
             continue;
         }
         const bool full = std::min(it->keys + c, h3_cells_at(ctx->cfg.h3_res)) * 2 > usable_slots(ctx, *it);
