@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 10
+#define HM_ABI_VERSION 11
 
 /* error codes */
 #define HM_OK 0
@@ -327,11 +327,15 @@ int hm_last_timings(const hm_ctx *ctx, double *ms, int32_t n);
  * vehicleId and eventTs non-null, and vkey = provider_code * n_vehicles + vehicle_code from the batch's exact
  * string dictionaries (code order unspecified; strings as Arrow offsets + UTF-8 bytes in pinned host memory, the
  * layout hm_encode_position_updates takes).  Records the device decoder does not handle (see json_decode.h) fail
- * the call with HM_E_UNSUPPORTED; malformed records decode to all-null rows (counted). */
+ * the call with HM_E_UNSUPPORTED, unless flags holds HM_JSON_SPLICE: then they decode to all-null rows listed in
+ * unsupported_rows, the dictionaries hold the other rows' strings only, and the caller decodes those records on the
+ * host and writes them in with hm_json_patch before hm_process_batch (mobheat/engine.py decode_json).  Malformed
+ * records decode to all-null rows (counted). */
+#define HM_JSON_SPLICE 1
 typedef struct hm_json_in {
     int64_t n;
     int32_t memory;            /* HM_MEM_HOST or HM_MEM_DEVICE: where bytes and offsets live */
-    int32_t reserved;
+    int32_t flags;             /* HM_JSON_SPLICE or 0 */
     const uint8_t *bytes;
     const int64_t *offsets;    /* n + 1 */
 } hm_json_in;
@@ -344,9 +348,19 @@ typedef struct hm_json_out {
     const int64_t *vehicle_offsets;    /* n_vehicles + 1 */
     const uint8_t *vehicle_bytes;
     int64_t n_malformed;       /* records that decoded to all-null rows (from_json's malformed records) */
-    int64_t n_unsupported;     /* > 0 only with HM_E_UNSUPPORTED */
+    int64_t n_unsupported;     /* records outside the device decoder (HM_E_UNSUPPORTED, or spliced) */
+    const int64_t *unsupported_rows;   /* HM_JSON_SPLICE: their row indices, ascending (host memory, valid until the
+                                          next hm_decode_json) */
 } hm_json_out;
 int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out);
+/* The splice step: rows[k] (from unsupported_rows) of the last hm_decode_json get lat / lon / ts_us / speed /
+ * speed_valid / row_valid and the dictionary codes pcode[k] / vcode[k] (host arrays, m entries; codes index the
+ * extended dictionaries of n_providers / n_vehicles strings: the decoder's strings with the caller's appended);
+ * every other valid row's vkey is re-encoded for the new n_vehicles.  The batch from hm_decode_json then holds the
+ * whole micro-batch. */
+int hm_json_patch(hm_ctx *ctx, int64_t m, const int64_t *rows, const double *lat, const double *lon,
+                  const int64_t *ts_us, const double *speed, const uint8_t *speed_valid, const uint8_t *row_valid,
+                  const int64_t *pcode, const int64_t *vcode, int64_t n_providers, int64_t n_vehicles);
 
 /* The distinct 900-s buckets floor(ts_s / 900) of the last hm_process_batch's latest rows, ascending (computed on
  * the device; *n = count, up to cap written): the buckets whose local offsets hm_encode_position_updates needs. */

@@ -169,6 +169,7 @@ void hm_destroy(hm_ctx *ctx) {
                       &ctx->td_params, &ctx->gapbuf, &ctx->keys, &ctx->bin_cur, &ctx->agg_bucket, &ctx->agg_cursor,
                       &ctx->jd_bytes, &ctx->jd_offs, &ctx->jd_scratch, &ctx->jd_lat, &ctx->jd_lon, &ctx->jd_ts, &ctx->jd_speed,
                       &ctx->jd_sv, &ctx->jd_rv, &ctx->jd_vkey, &ctx->jd_poff, &ctx->jd_plen, &ctx->jd_voff, &ctx->jd_vlen,
+                      &ctx->jd_un, &ctx->jd_unrows, &ctx->jd_patch,
                       &ctx->lb_set, &ctx->lb_list};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);

@@ -112,14 +112,18 @@ int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out) {
     if (n > (int64_t)UINT32_MAX - 2) return set_err(ctx, HM_E_INVALID, "%lld records exceed 2^32-2", (long long)n);
     if (n > 0 && (!in->bytes || !in->offsets)) return set_err(ctx, HM_E_INVALID, "bytes and offsets are required");
     if (in->memory != HM_MEM_HOST && in->memory != HM_MEM_DEVICE) return set_err(ctx, HM_E_INVALID, "bad memory kind");
+    if (in->flags & ~HM_JSON_SPLICE) return set_err(ctx, HM_E_INVALID, "unknown flags %d", in->flags);
     memset(out, 0, sizeof(*out));
+    ctx->jd_n = -1;
+    ctx->jd_unsup.clear();
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc;
     const size_t m = (size_t)std::max<int64_t>(n, 1);
     if ((rc = ensure(ctx, ctx->jd_lat, m * 8)) || (rc = ensure(ctx, ctx->jd_lon, m * 8)) || (rc = ensure(ctx, ctx->jd_ts, m * 8)) ||
         (rc = ensure(ctx, ctx->jd_speed, m * 8)) || (rc = ensure(ctx, ctx->jd_sv, m)) || (rc = ensure(ctx, ctx->jd_rv, m)) ||
         (rc = ensure(ctx, ctx->jd_vkey, m * 8)) || (rc = ensure(ctx, ctx->jd_poff, m * 8)) || (rc = ensure(ctx, ctx->jd_plen, m * 4)) ||
-        (rc = ensure(ctx, ctx->jd_voff, m * 8)) || (rc = ensure(ctx, ctx->jd_vlen, m * 4)))
+        (rc = ensure(ctx, ctx->jd_voff, m * 8)) || (rc = ensure(ctx, ctx->jd_vlen, m * 4)) ||
+        (rc = ensure(ctx, ctx->jd_un, m)))
         return rc;
     int64_t o0 = 0, on = 0;
     const uint8_t *dbytes = nullptr;
@@ -154,14 +158,22 @@ int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out) {
         hipLaunchKernelGGL(k_json_parse, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, dbytes, doffs, o0, n,
                            (uint8_t *)ctx->jd_scratch.p, (double *)ctx->jd_lat.p, (double *)ctx->jd_lon.p, (int64_t *)ctx->jd_ts.p,
                            (double *)ctx->jd_speed.p, (uint8_t *)ctx->jd_sv.p, (uint8_t *)ctx->jd_rv.p, (int64_t *)ctx->jd_poff.p,
-                           (int32_t *)ctx->jd_plen.p, (int64_t *)ctx->jd_voff.p, (int32_t *)ctx->jd_vlen.p, w);
+                           (int32_t *)ctx->jd_plen.p, (int64_t *)ctx->jd_voff.p, (int32_t *)ctx->jd_vlen.p,
+                           (uint8_t *)ctx->jd_un.p, w);
         HIPCHK(ctx, hipGetLastError());
         unsigned long long counts[2];
         HIPCHK(ctx, hipMemcpyAsync(counts, w, 16, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         out->n_malformed = (int64_t)counts[0];
         out->n_unsupported = (int64_t)counts[1];
-        if (counts[1])
+        if (counts[1] && (in->flags & HM_JSON_SPLICE)) {   // the rows for the host to decode (hm_json_patch)
+            if ((rc = ensure(ctx, ctx->jd_unrows, (size_t)n * 8))) return rc;
+            if ((rc = compact_flags(ctx, (const uint8_t *)ctx->jd_un.p, n, (int64_t *)ctx->jd_unrows.p, ctx->stream))) return rc;
+            ctx->jd_unsup.resize(counts[1]);
+            HIPCHK(ctx, hipMemcpyAsync(ctx->jd_unsup.data(), ctx->jd_unrows.p, counts[1] * 8, hipMemcpyDeviceToHost, ctx->stream));
+            HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+            out->unsupported_rows = ctx->jd_unsup.data();
+        } else if (counts[1])
             return set_err(ctx, HM_E_UNSUPPORTED, "%llu records outside the device decoder (a number of more than 19 significant "
                            "digits on a rounding boundary, or a float/object/array as a string field)", counts[1]);
     }
@@ -193,6 +205,59 @@ int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out) {
     out->n_vehicles = ctx->jd_veh.n_codes;
     out->vehicle_offsets = (const int64_t *)ctx->jd_veh.h_off;
     out->vehicle_bytes = (const uint8_t *)ctx->jd_veh.h_bytes;
+    ctx->jd_n = n;
+    ctx->jd_nv = ctx->jd_veh.n_codes;
+    ctx->jd_np = ctx->jd_prov.n_codes;
+    return HM_OK;
+}
+
+int hm_json_patch(hm_ctx *ctx, int64_t m, const int64_t *rows, const double *lat, const double *lon, const int64_t *ts_us,
+                  const double *speed, const uint8_t *speed_valid, const uint8_t *row_valid, const int64_t *pcode,
+                  const int64_t *vcode, int64_t n_providers, int64_t n_vehicles) {
+    if (!ctx || m < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->jd_n < 0) return set_err(ctx, HM_E_STATE, "no hm_decode_json batch to patch");
+    if (m > 0 && (!rows || !lat || !lon || !ts_us || !speed || !speed_valid || !row_valid || !pcode || !vcode))
+        return set_err(ctx, HM_E_INVALID, "null column");
+    if (n_providers < ctx->jd_np || n_vehicles < ctx->jd_nv)
+        return set_err(ctx, HM_E_INVALID, "dictionaries may only grow (%lld < %lld providers or %lld < %lld vehicles)",
+                       (long long)n_providers, (long long)ctx->jd_np, (long long)n_vehicles, (long long)ctx->jd_nv);
+    const uint64_t nv_old = (uint64_t)std::max<int64_t>(ctx->jd_nv, 1), nv_new = (uint64_t)std::max<int64_t>(n_vehicles, 1);
+    if (n_providers > 0 && (uint64_t)n_providers > (UINT64_MAX - 1) / nv_new)
+        return set_err(ctx, HM_E_INVALID, "vkey space overflows");
+    std::vector<JsonPatchRow> P((size_t)m);
+    for (int64_t k = 0; k < m; k++) {
+        if (rows[k] < 0 || rows[k] >= ctx->jd_n) return set_err(ctx, HM_E_INVALID, "row %lld outside the batch", (long long)rows[k]);
+        if (row_valid[k] && (pcode[k] < 0 || pcode[k] >= n_providers || vcode[k] < 0 || vcode[k] >= n_vehicles))
+            return set_err(ctx, HM_E_INVALID, "row %lld: code outside the dictionaries", (long long)rows[k]);
+        JsonPatchRow &p = P[k];
+        memset(&p, 0, sizeof(p));
+        p.row = rows[k];
+        p.ts_us = ts_us[k];
+        p.pcode = pcode[k];
+        p.vcode = vcode[k];
+        p.lat = lat[k];
+        p.lon = lon[k];
+        p.speed = speed[k];
+        p.sv = speed_valid[k] ? 1 : 0;
+        p.rv = row_valid[k] ? 1 : 0;
+    }
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int64_t n = ctx->jd_n;
+    int rc;
+    if (n > 0 && nv_new != nv_old)
+        hipLaunchKernelGGL(k_json_rekey, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, (const uint8_t *)ctx->jd_rv.p, n,
+                           nv_old, nv_new, (uint64_t *)ctx->jd_vkey.p);
+    if (m > 0) {
+        if ((rc = ensure(ctx, ctx->jd_patch, (size_t)m * sizeof(JsonPatchRow)))) return rc;
+        HIPCHK(ctx, hipMemcpyAsync(ctx->jd_patch.p, P.data(), (size_t)m * sizeof(JsonPatchRow), hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_json_patch, dim3(grid_for(m, 256)), dim3(256), 0, ctx->stream, (const JsonPatchRow *)ctx->jd_patch.p,
+                           m, nv_new, (double *)ctx->jd_lat.p, (double *)ctx->jd_lon.p, (int64_t *)ctx->jd_ts.p,
+                           (double *)ctx->jd_speed.p, (uint8_t *)ctx->jd_sv.p, (uint8_t *)ctx->jd_rv.p, (uint64_t *)ctx->jd_vkey.p);
+    }
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));   // (P is pageable host memory)
+    ctx->jd_nv = n_vehicles;
+    ctx->jd_np = n_providers;
     return HM_OK;
 }
 

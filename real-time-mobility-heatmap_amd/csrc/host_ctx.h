@@ -113,7 +113,9 @@ struct hm_ctx {
         size_t h_off_cap = 0, h_bytes_cap = 0;
     };
     DevBuf jd_bytes, jd_offs, jd_scratch, jd_lat, jd_lon, jd_ts, jd_speed, jd_sv, jd_rv, jd_vkey, jd_poff, jd_plen, jd_voff,
-        jd_vlen;
+        jd_vlen, jd_un, jd_unrows, jd_patch;
+    std::vector<int64_t> jd_unsup;      // the last hm_decode_json's unsupported rows (HM_JSON_SPLICE)
+    int64_t jd_n = -1, jd_np = 0, jd_nv = 0;   // its row count (-1: none to patch) and dictionary sizes
     Dict jd_prov, jd_veh;
     DevBuf lb_set, lb_list;   // hm_last_latest_buckets
     DevBuf keys;                     // k_ingest's event key per row (kernels.h ekey)

@@ -16,15 +16,17 @@ __global__ __launch_bounds__(256) void k_json_parse(const uint8_t *__restrict__ 
                                                     uint8_t *__restrict__ sv, uint8_t *__restrict__ rv,
                                                     int64_t *__restrict__ p_off, int32_t *__restrict__ p_len,
                                                     int64_t *__restrict__ v_off, int32_t *__restrict__ v_len,
-                                                    unsigned long long *counts) {
+                                                    uint8_t *__restrict__ unsup_row, unsigned long long *counts) {
     unsigned long long bad = 0, unsup = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         JsonRow r;
         parse_record(bytes, offs[i] - base, offs[i + 1] - base, scratch, r);
-        const uint32_t f = r.flags;
+        const bool u = (r.flags & JF_UNSUPPORTED) != 0;
+        const uint32_t f = u ? 0u : r.flags;   // an unsupported record stays an all-null row until the host splices it
         bad += (f & JF_MALFORMED) != 0;
-        unsup += (f & JF_UNSUPPORTED) != 0;
+        unsup += u;
+        unsup_row[i] = u;
         lat[i] = (f & JF_LAT) ? r.lat : __builtin_nan("");
         lon[i] = (f & JF_LON) ? r.lon : __builtin_nan("");
         ts[i] = (f & JF_TS) ? r.ts_us : 0;
@@ -143,6 +145,38 @@ __global__ __launch_bounds__(256) void k_json_vkey(const uint8_t *__restrict__ r
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
         vkey[i] = rv[i] ? (uint64_t)pcode[pslot[i]] * n_vehicles + vcode[vslot[i]] : 0;
+}
+// hm_json_patch: every valid row's vkey re-encoded for the extended vehicle dictionary (nv_old -> nv_new), then the
+// host-decoded rows written over the unsupported ones (P = m rows of JsonPatchRow)
+struct JsonPatchRow {
+    int64_t row, ts_us, pcode, vcode;
+    double lat, lon, speed;
+    uint8_t sv, rv, pad[6];
+};
+static_assert(sizeof(JsonPatchRow) == 64, "JsonPatchRow is 64 B");
+__global__ __launch_bounds__(256) void k_json_rekey(const uint8_t *__restrict__ rv, int64_t n, uint64_t nv_old,
+                                                    uint64_t nv_new, uint64_t *__restrict__ vkey) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        if (rv[i]) vkey[i] = vkey[i] / nv_old * nv_new + vkey[i] % nv_old;
+}
+__global__ __launch_bounds__(256) void k_json_patch(const JsonPatchRow *__restrict__ P, int64_t m, uint64_t nv,
+                                                    double *__restrict__ lat, double *__restrict__ lon,
+                                                    int64_t *__restrict__ ts, double *__restrict__ speed,
+                                                    uint8_t *__restrict__ sv, uint8_t *__restrict__ rv,
+                                                    uint64_t *__restrict__ vkey) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += stride) {
+        const JsonPatchRow p = P[k];
+        const int64_t i = p.row;
+        lat[i] = p.lat;
+        lon[i] = p.lon;
+        ts[i] = p.ts_us;
+        speed[i] = p.speed;
+        sv[i] = p.sv;
+        rv[i] = p.rv;
+        vkey[i] = p.rv ? (uint64_t)p.pcode * nv + (uint64_t)p.vcode : 0;
+    }
 }
 // the distinct 900-s buckets of the latest rows' eventTs (a set of int64, EMPTY = INT64_MIN), compacted into list
 __global__ __launch_bounds__(256) void k_latest_buckets(const int64_t *__restrict__ rows, int64_t m,

@@ -147,10 +147,9 @@ HM_HD int64_t wdec(unsigned long long e) { return (int64_t)(e ^ (UINT64_C(1) << 
 // merge workgroup of a bin is the only writer of the regions it receives.
 constexpr int GMAP_SLOTS = 4096;        // live windows per context (open addressing by wenc)
 constexpr int REGION_MIN_BITS = 8;      // >= 256 slots per region (overflow-free at load <= 1/2)
-#ifndef HM_REGION_BITS
-#define HM_REGION_BITS 13
-#endif
-constexpr int REGION_BITS = HM_REGION_BITS;   // at most 2^REGION_BITS regions per table = radix bins of the partition
+// at most 2^REGION_BITS regions per table = radix bins of the partition (mobheat/distributed.py REGION_BITS: the
+// multi-GPU owner ranges are ranges of this field)
+constexpr int REGION_BITS = 13;
 struct GenDesc {
     unsigned long long wenc;   // 0 = empty map slot
     TileSlot *tab;

@@ -14,9 +14,10 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MOBHEAT_LIB: load another build of the same ABI (kernel variants under csrc/variants/ for tuning runs)
 LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE, "..", "csrc", "libmobheat.so"))
 
-HM_ABI_VERSION = 10
+HM_ABI_VERSION = 11
 HM_MEM_HOST = 0
 HM_MEM_DEVICE = 1
+HM_JSON_SPLICE = 1
 HM_E_INVALID, HM_E_HIP, HM_E_NOMEM, HM_E_OVERFLOW, HM_E_STATE, HM_E_UNSUPPORTED = -1, -2, -3, -4, -5, -6
 HM_STAGE_SUMMARY_WORDS = 8200
 HM_TILE_REC_BYTES = 48       # table mode's tile partial
@@ -53,13 +54,13 @@ class HmBatchOut(ctypes.Structure):
 
 
 class HmJsonIn(ctypes.Structure):
-    _fields_ = [("n", c_i64), ("memory", c_i32), ("reserved", c_i32), ("bytes", c_vp), ("offsets", c_vp)]
+    _fields_ = [("n", c_i64), ("memory", c_i32), ("flags", c_i32), ("bytes", c_vp), ("offsets", c_vp)]
 
 
 class HmJsonOut(ctypes.Structure):
     _fields_ = [("batch", HmBatchIn), ("n_providers", c_i64), ("provider_offsets", c_vp), ("provider_bytes", c_vp),
                 ("n_vehicles", c_i64), ("vehicle_offsets", c_vp), ("vehicle_bytes", c_vp), ("n_malformed", c_i64),
-                ("n_unsupported", c_i64)]
+                ("n_unsupported", c_i64), ("unsupported_rows", c_vp)]
 
 
 class HmStageSizes(ctypes.Structure):
@@ -125,6 +126,7 @@ SIGNATURES = {
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_last_counts": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_decode_json": (c_i32, [c_vp, _P(HmJsonIn), _P(HmJsonOut)]),
+    "hm_json_patch": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64]),
     "hm_latlng_to_cell_last_exact": (c_i64, [c_i32]),
     "hm_cells_to_boundary": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "hm_selftest_cells_to_boundary_host": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp]),

@@ -10,7 +10,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import (HM_MEM_DEVICE, HM_MEM_HOST, STATE_REC_DTYPE, HmBatchIn, HmBatchOut, HmConfig, HmJsonIn, HmJsonOut,
+from ._lib import (HM_JSON_SPLICE, HM_MEM_DEVICE, HM_MEM_HOST, STATE_REC_DTYPE, HmBatchIn, HmBatchOut, HmConfig, HmJsonIn, HmJsonOut,
                    HmStateInfo, check, ptr)
 
 _INFO_FIELDS = [f for f, _ in HmStateInfo._fields_ if f != "reserved"]
@@ -40,6 +40,7 @@ class KafkaBatch:
     providers: tuple            # (n, offsets int64[n+1], bytes uint8): Arrow layout, as _lib._dictionary builds
     vehicles: tuple
     n_malformed: int
+    n_spliced: int = 0          # records decoded on the host (kafka_host) and written in with hm_json_patch
 
 
 @dataclass
@@ -56,6 +57,29 @@ class BatchResult:
     n_partials: int = 0         # partial records merged (direct path: aggregated rows; table mode: ~ distinct keys)
     n_tiles: int = 0
     n_latest: int = 0
+
+
+def _extend_dictionary(d, strings):
+    """Arrow-layout dictionary (n, offsets, bytes) + strings (str or None) -> (the dictionary with the new strings
+    appended, int64 codes: -1 for None)."""
+    n, offs, raw = d
+    have = {raw[offs[i]:offs[i + 1]].tobytes(): i for i in range(n)} if any(s is not None for s in strings) else {}
+    new, codes = [], np.full(len(strings), -1, np.int64)
+    for k, s in enumerate(strings):
+        if s is None:
+            continue
+        b = s.encode("utf-8")
+        code = have.get(b)
+        if code is None:
+            code = have[b] = n + len(new)
+            new.append(b)
+        codes[k] = code
+    if not new:
+        return d, codes
+    tail = np.cumsum([len(b) for b in new], dtype=np.int64) + offs[n]
+    blob = np.frombuffer(b"".join(new), np.uint8) if any(new) else np.zeros(0, np.uint8)
+    raw2 = np.concatenate([raw[:offs[n]], blob]) if int(tail[-1]) else np.zeros(1, np.uint8)
+    return (n + len(new), np.concatenate([offs[:n + 1], tail]), raw2), codes
 
 
 def _u8(a, n):
@@ -124,10 +148,12 @@ class HeatmapEngine:
     # ---- Kafka values (row f1): JSON decoded on the GPU, then the batch ----
     def decode_json(self, values, offsets):
         """The micro-batch's Kafka values (bytes uint8 back to back + offsets int64[n+1], Arrow's binary layout) ->
-        KafkaBatch: from_json(value, schema) + to_timestamp(ts) on the device (reference heatmap_stream.py:88-93)."""
+        KafkaBatch: from_json(value, schema) + to_timestamp(ts) on the device (reference heatmap_stream.py:88-93).
+        The records outside the device decoder (HM_JSON_SPLICE lists them) are decoded on the host and spliced in."""
         buf = np.ascontiguousarray(values, dtype=np.uint8)
         offs = np.ascontiguousarray(offsets, dtype=np.int64)
-        jin = HmJsonIn(n=offs.size - 1, memory=HM_MEM_HOST, bytes=ptr(buf) if buf.size else None, offsets=ptr(offs))
+        jin = HmJsonIn(n=offs.size - 1, memory=HM_MEM_HOST, flags=HM_JSON_SPLICE, bytes=ptr(buf) if buf.size else None,
+                       offsets=ptr(offs))
         jout = HmJsonOut()
         check(self._lib.hm_decode_json(self._ctx, ctypes.byref(jin), ctypes.byref(jout)), self._ctx, "hm_decode_json")
 
@@ -137,10 +163,38 @@ class HeatmapEngine:
             raw = (np.ctypeslib.as_array(ctypes.cast(pb, ctypes.POINTER(ctypes.c_uint8)), shape=(total,)).copy()
                    if total else np.zeros(1, np.uint8))
             return n, offs_, raw
-        return KafkaBatch(batch=jout.batch, providers=dictionary(int(jout.n_providers), jout.provider_offsets,
-                                                                  jout.provider_bytes),
-                          vehicles=dictionary(int(jout.n_vehicles), jout.vehicle_offsets, jout.vehicle_bytes),
-                          n_malformed=int(jout.n_malformed))
+        kb = KafkaBatch(batch=jout.batch, providers=dictionary(int(jout.n_providers), jout.provider_offsets,
+                                                                jout.provider_bytes),
+                        vehicles=dictionary(int(jout.n_vehicles), jout.vehicle_offsets, jout.vehicle_bytes),
+                        n_malformed=int(jout.n_malformed))
+        m = int(jout.n_unsupported)
+        if m:
+            rows = np.ctypeslib.as_array(ctypes.cast(jout.unsupported_rows, ctypes.POINTER(ctypes.c_int64)),
+                                         shape=(m,)).copy()
+            self._splice(kb, buf, offs, rows)
+        return kb
+
+    def _splice(self, kb, buf, offs, rows):
+        """Decode records `rows` on the host (kafka_host: the device decoder's rules plus the cases it leaves out),
+        extend the string dictionaries with their new strings and write them into the device batch (hm_json_patch)."""
+        from . import kafka_host
+        c = kafka_host.decode_columns(buf, offs, rows)
+        kb.providers, pcode = _extend_dictionary(kb.providers, c["provider"])
+        kb.vehicles, vcode = _extend_dictionary(kb.vehicles, c["vehicleId"])
+        m = rows.size
+        f64 = lambda v: np.array([np.nan if x is None else x for x in v], np.float64)   # noqa: E731
+        lat, lon = f64(c["lat"]), f64(c["lon"])
+        sv = np.array([x is not None for x in c["speedKmh"]], np.uint8)
+        speed = np.where(sv.astype(bool), f64(c["speedKmh"]), 0.0)
+        ts_ok = np.asarray(c["ts_ok"], bool)
+        rv = ((pcode >= 0) & (vcode >= 0) & ts_ok).astype(np.uint8)
+        ts = np.where(ts_ok, np.asarray(c["ts_us"], np.int64), 0)
+        pcode, vcode = np.maximum(pcode, 0), np.maximum(vcode, 0)
+        check(self._lib.hm_json_patch(self._ctx, m, ptr(rows), ptr(lat), ptr(lon), ptr(ts), ptr(speed), ptr(sv),
+                                      ptr(rv), ptr(pcode), ptr(vcode), kb.providers[0], kb.vehicles[0]),
+              self._ctx, "hm_json_patch")
+        kb.n_malformed += int(sum(c["malformed"]))
+        kb.n_spliced = int(m)
 
     def process_kafka(self, epoch_id, values, offsets, copy=True, rows_on_device=False):
         """decode_json + hm_process_batch on the decoded device columns; (BatchResult, KafkaBatch)."""

@@ -1,12 +1,12 @@
-"""Host decode of a micro-batch's Kafka values for the records the GPU decoder does not handle.
+"""Host decode of the Kafka records the GPU decoder does not handle (spliced into the device batch).
 
 hm_decode_json (row f1, csrc/json_decode.h) decodes the producer's records on the device and, for the rare record
-outside its scope (a non-string JSON value in a StringType field, a >19-digit number on a rounding boundary), fails the
-call with HM_E_UNSUPPORTED instead of silently differing.  The reference never rejects such a record: Spark's from_json
-(heatmap_stream.py:88-93, PERMISSIVE, Spark 3.5) keeps it, turning e.g. a numeric vehicleId into that value's JSON
-text.  So that one such record cannot stop the stream (Spark would replay the same offsets forever), the batch is then
-decoded here, on the host, with the same rules as the device decoder plus the cases it leaves out, and runs through the
-ordinary column path (stream.batch_columns).
+outside its scope (a non-string JSON value in a StringType field, a >19-digit number on a rounding boundary), does not
+silently differ: with HM_JSON_SPLICE it leaves that row all-null and lists it.  The reference never rejects such a
+record: Spark's from_json (heatmap_stream.py:88-93, PERMISSIVE, Spark 3.5) keeps it, turning e.g. a numeric vehicleId
+into that value's JSON text.  So the engine (engine.py decode_json) decodes just the listed records here, on the host,
+with the same rules as the device decoder plus the cases it leaves out, and writes them into the device batch with
+hm_json_patch -- a batch with one odd record costs one record's host decode, not the whole batch's.
 
 Rules (Spark 3.5 JacksonParser, schema heatmap_stream.py:51-60):
   * a value that is not a JSON object (or not UTF-8 / not JSON) -> an all-null record;
@@ -145,19 +145,30 @@ def _to_timestamp_us(strings):
     return out, ok
 
 
-def decode_table(values, offsets):
-    """The batch's values (bytes uint8 + offsets int64[n+1], Arrow binary layout) -> a pyarrow Table with the columns
-    stream.batch_columns takes (provider, vehicleId, lat, lon, speedKmh, eventTs: null where from_json /
-    to_timestamp give null; NaN speeds stay NaN)."""
-    import pyarrow as pa
-    buf = np.asarray(values, np.uint8).tobytes()
+def decode_columns(values, offsets, rows=None):
+    """Records `rows` (int indices; all by default) of the batch's values (bytes uint8 + offsets int64[n+1], Arrow
+    binary layout) -> columns as Python lists: provider / vehicleId (str or None, as the UTF-8 Spark stores), lat /
+    lon / speedKmh (float or None), ts (the raw string), plus ts_us int64 / ts_ok bool (to_timestamp) and malformed
+    (from_json's all-null record)."""
     offs = np.asarray(offsets, np.int64)
-    n = offs.size - 1
-    recs = [decode_record(buf[offs[k]:offs[k + 1]]) for k in range(n)]
+    buf = np.asarray(values, np.uint8)
+    if rows is None:
+        rows = range(offs.size - 1)
+    recs = [decode_record(buf[offs[k]:offs[k + 1]].tobytes()) for k in rows]
     col = {f: [None if r is None else r[f] for r in recs] for f in ("provider", "vehicleId", "lat", "lon", "speedKmh", "ts")}
     for f in ("provider", "vehicleId"):   # the UTF-8 Spark stores: Java's encoder writes '?' for a lone surrogate
         col[f] = [None if v is None else v.encode("utf-8", "replace").decode("utf-8") for v in col[f]]
-    ts_us, ts_ok = _to_timestamp_us(col["ts"])
+    col["ts_us"], col["ts_ok"] = _to_timestamp_us(col["ts"])
+    col["malformed"] = [r is None for r in recs]
+    return col
+
+
+def decode_table(values, offsets):
+    """The whole batch decoded on the host -> a pyarrow Table with the columns stream.batch_columns takes (provider,
+    vehicleId, lat, lon, speedKmh, eventTs: null where from_json / to_timestamp give null; NaN speeds stay NaN)."""
+    import pyarrow as pa
+    col = decode_columns(values, offsets)
+    ts_us, ts_ok = col["ts_us"], col["ts_ok"]
     return pa.table({
         "provider": pa.array(col["provider"], pa.string()),
         "vehicleId": pa.array(col["vehicleId"], pa.string()),

@@ -486,48 +486,22 @@ def _flush_statements(sink, collection, buf, offs):
 # ------------------ the drop-in boundary ------------------
 def _process(eng, epoch_id, cols):
     """Merge the batch into the engine's state; (result, the string dictionaries of its vkeys)."""
-    from . import _lib
     # (the tile and latest rows stay on the device: the statements are encoded there from them)
-    if "kafka" in cols:   # raw Kafka values: from_json + to_timestamp on the GPU (row f1)
-        try:
-            res, kb = eng.process_kafka(epoch_id, *cols["kafka"], rows_on_device=True)
-            return res, (kb.providers, kb.vehicles)
-        except RuntimeError as err:
-            if getattr(err, "code", None) != _lib.HM_E_UNSUPPORTED:
-                raise
-            e = err
-        # a record outside the device decoder's scope: decode the batch on the host (kafka_host) -- one such record
-        # must not stop the stream (Spark would replay the same offsets into the same failure)
-        cols = _kafka_host_decode(*cols["kafka"], str(e))
+    if "kafka" in cols:   # raw Kafka values: from_json + to_timestamp on the GPU (row f1; the records outside the
+        # device decoder are decoded on the host and spliced in, engine.decode_json: one such record cannot stop the
+        # stream, where Spark would replay the same offsets into the same failure)
+        res, kb = eng.process_kafka(epoch_id, *cols["kafka"], rows_on_device=True)
+        return res, (kb.providers, kb.vehicles)
     res = eng.process_batch(epoch_id, cols["lat"], cols["lon"], cols["ts_us"], cols["speed"], cols["speed_valid"],
                             cols["vkey"], cols["row_valid"], rows_on_device=True)
     return res, (cols["provider_uniques"], cols["vehicle_uniques"])
-
-
-def _kafka_host_decode(values, offsets, why):
-    """The whole batch decoded on the host (kafka_host) -- pure Python per record, so it is logged with its size and
-    time: a stream that keeps producing records outside the device decoder pays this on every batch."""
-    import time
-    import warnings
-    from . import kafka_host
-    t0 = time.perf_counter()
-    cols = batch_columns(kafka_host.decode_table(values, offsets))
-    warnings.warn(f"mobheat: {why}; the batch's {len(offsets) - 1} Kafka values were decoded on the host in "
-                  f"{time.perf_counter() - t0:.2f} s", RuntimeWarning, stacklevel=3)
-    return cols
 
 
 def _kafka_host_columns(eng, values, offsets):
     """Raw Kafka values decoded on `eng`'s GPU (hm_decode_json) and copied to host columns: the sharded writer hands
     every rank its share from host memory (the batch-wide string dictionaries keep the vkeys consistent across ranks)."""
     from . import _lib
-    try:
-        kb = eng.decode_json(values, offsets)
-    except RuntimeError as e:
-        if getattr(e, "code", None) != _lib.HM_E_UNSUPPORTED:
-            raise
-        cols = _kafka_host_decode(values, offsets, str(e))
-        return cols, (cols["provider_uniques"], cols["vehicle_uniques"])
+    kb = eng.decode_json(values, offsets)
     b = kb.batch
     n = int(b.n)
     lib = _lib.load()

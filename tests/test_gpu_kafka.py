@@ -36,6 +36,19 @@ def _dict_strings(d):
     return [raw[offs[k]:offs[k + 1]].tobytes() for k in range(n)]
 
 
+def _host_expected(values, offsets, rows=None):
+    """mobheat.kafka_host's decode of the batch in _check_decoded's layout."""
+    from mobheat import kafka_host
+    c = kafka_host.decode_columns(values, offsets, rows)
+    f64 = lambda v: np.array([np.nan if x is None else x for x in v], np.float64)   # noqa: E731
+    sv = np.array([x is not None for x in c["speedKmh"]], bool)
+    enc = lambda v: [None if x is None else x.encode("utf-8") for x in v]   # noqa: E731
+    prov, veh = enc(c["provider"]), enc(c["vehicleId"])
+    rv = np.array([p is not None and v is not None for p, v in zip(prov, veh)], bool) & np.asarray(c["ts_ok"], bool)
+    return dict(lat=f64(c["lat"]), lon=f64(c["lon"]), speed=np.where(sv, f64(c["speedKmh"]), 0.0), speed_valid=sv,
+                ts_us=np.asarray(c["ts_us"], np.int64), row_valid=rv, provider=prov, vehicleId=veh)
+
+
 def _check_decoded(kb, exp, n):
     b = kb.batch
     assert b.n == n and b.memory == _lib.HM_MEM_DEVICE
@@ -70,8 +83,11 @@ def test_decode_golden_fixture():
                vehicleId=_strings(z["vehicle_present"], z["vehicle_bytes"], z["vehicle_len"]))
     _check_decoded(kb, exp, z["offsets"].size - 1)
     assert kb.n_malformed == int(z["n_malformed"])
-    with pytest.raises(RuntimeError, match="outside the device decoder"):
-        eng.decode_json(z["unsupported_bytes"], z["unsupported_offsets"])
+    # the fixture's unsupported records: spliced in from the host decode (engine.decode_json, hm_json_patch)
+    ub, uo = z["unsupported_bytes"], z["unsupported_offsets"]
+    kb = eng.decode_json(ub, uo)
+    assert kb.n_spliced == uo.size - 1
+    _check_decoded(kb, _host_expected(ub, uo), uo.size - 1)
     kb = eng.decode_json(np.zeros(0, np.uint8), np.zeros(1, np.int64))   # an empty batch
     assert kb.batch.n == 0 and kb.providers[0] == 0
     eng.close()
@@ -168,10 +184,44 @@ def test_foreach_batch_func_kafka_values_equal_decoded_frame():
         assert gs == ws and g["q"] == w["q"]
 
 
+def test_splice_unsupported_records_into_device_batch():
+    """Records outside the device decoder (a number / object / array as a string field, strings new to the batch and
+    strings it already holds) in a large batch: hm_decode_json lists them, the engine decodes just those on the host
+    and hm_json_patch writes them in, re-encoding every vkey for the grown vehicle dictionary -- the whole batch then
+    equals the host decode row for row, strings through the dictionaries.  Without HM_JSON_SPLICE the call fails."""
+    from mobheat import HeatmapEngine
+    rng = random.Random(23)
+    vals = _producer_values(rng, 40_000, 900)
+    odd = [b'{"provider":"mbta","vehicleId":1.5,"lat":42.3,"lon":-71.1,"speedKmh":10,"ts":"2025-10-04T10:22:05Z"}',
+           b'{"provider":{"a":[1,2]},"vehicleId":"v-0","lat":42.31,"lon":-71.11,"ts":"2025-10-04T10:22:05Z"}',
+           b'{"provider":"mbta","vehicleId":[true,null],"lat":42.32,"lon":-71.12,"ts":"2025-10-04 10:22:06"}',
+           b'{"provider":"mbta","vehicleId":12345678901234567890123,"lat":1,"lon":2}',
+           b'{"provider":"mbta","vehicleId":{"x":"y"},"speedKmh":null,"ts":"2025-10-04T10:22:05+01:00"}']
+    pos = sorted(rng.sample(range(len(vals) + len(odd)), len(odd)))
+    for p, v in zip(pos, odd):
+        vals.insert(p, v)
+    buf = np.frombuffer(b"".join(vals), np.uint8)
+    offs = np.cumsum([0] + [len(v) for v in vals]).astype(np.int64)
+    eng = HeatmapEngine(h3_res=8)
+    kb = eng.decode_json(buf, offs)
+    assert kb.n_spliced == len(odd)
+    _check_decoded(kb, _host_expected(buf, offs), len(vals))
+    assert b"mbta" in _dict_strings(kb.providers) and b"1.5" in _dict_strings(kb.vehicles)
+    # the batch through hm_process_batch: the spliced rows are ordinary rows
+    res, _ = eng.process_kafka(0, buf, offs)
+    assert res.n_valid == int(_host_expected(buf, offs)["row_valid"].sum())
+    lib = _lib.load()
+    jin = _lib.HmJsonIn(n=offs.size - 1, memory=_lib.HM_MEM_HOST, flags=0, bytes=buf.ctypes.data,
+                        offsets=offs.ctypes.data)
+    jout = _lib.HmJsonOut()
+    assert lib.hm_decode_json(eng._ctx, jin, jout) == _lib.HM_E_UNSUPPORTED and jout.n_unsupported == len(odd)
+    eng.close()
+
+
 def test_foreach_batch_func_kafka_values_with_unsupported_records():
-    """A batch holding records outside the device decoder's scope (a number as vehicleId, an object as provider) no
-    longer fails (hm_decode_json's HM_E_UNSUPPORTED -> the host decode of mobheat.kafka_host): it writes the documents
-    of the same batch decoded on the host, the odd records' strings being their JSON text as Spark stores them."""
+    """A batch holding records outside the device decoder's scope (a number as vehicleId, an object as provider) does
+    not fail (those records are decoded on the host and spliced into the device batch): it writes the documents of
+    the same batch decoded on the host, the odd records' strings being their JSON text as Spark stores them."""
     import numpy as np
     import pandas as pd
     from mobheat import kafka_host, stream
@@ -201,8 +251,7 @@ def test_foreach_batch_func_kafka_values_with_unsupported_records():
             stream.reset_engine()
         return ops
 
-    with pytest.warns(RuntimeWarning, match="2 records outside the device decoder.*5002 Kafka values were decoded on the host"):
-        got = run(pd.DataFrame({"value": vals}))
+    got = run(pd.DataFrame({"value": vals}))
     offs = np.cumsum([0] + [len(v) for v in vals])
     want = run(kafka_host.decode_table(np.frombuffer(b"".join(vals), np.uint8), offs))
     assert got["positions_latest"] == want["positions_latest"]

@@ -206,3 +206,31 @@ def test_host_decode_keeps_nested_duplicate_keys():
     assert r["vehicleId"] == '{"a":1,"a":[2,{"d":2,"d":3.5}],"b":{"c":1,"c":true}}'
     assert r["provider"] == '{"x":1,"x":null}' and r["lat"] == 2.5
     assert kafka_host.decode_record(b'[{"provider":"x"}]') is None
+
+
+def test_splice_dictionary_extension():
+    """engine._extend_dictionary (the splice step's host half): strings the batch's dictionary holds keep their code,
+    new ones are appended once each in Arrow layout, None -> -1."""
+    from mobheat.engine import _extend_dictionary
+    offs = np.array([0, 4, 7], np.int64)
+    d = (2, offs, np.frombuffer(b"mbtay\xce\x8e", np.uint8).copy())
+    (n, o, raw), codes = _extend_dictionary(d, ["yΎ", None, "1.5", "mbta", "1.5", '{"a":1}'])
+    assert n == 4 and codes.tolist() == [1, -1, 2, 0, 2, 3]
+    assert [raw[o[k]:o[k + 1]].tobytes() for k in range(n)] == [b"mbta", b"y\xce\x8e", b"1.5", b'{"a":1}']
+    (n, o, raw), codes = _extend_dictionary((0, np.zeros(1, np.int64), np.zeros(1, np.uint8)), ["", None])
+    assert n == 1 and codes.tolist() == [0, -1] and o.tolist() == [0, 0]
+    assert _extend_dictionary(d, [None, "mbta"])[0] is d
+
+
+def test_decode_columns_rows_subset():
+    """kafka_host.decode_columns on a subset of rows decodes exactly those records (the splice decodes only the
+    records hm_decode_json lists)."""
+    vals = [b'{"provider":"a","vehicleId":1,"ts":"2025-10-04T10:00:00Z"}', b"garbage",
+            b'{"provider":"b","vehicleId":"v","lat":1.5,"ts":"2025-10-04 10:00:01"}']
+    offs = np.cumsum([0] + [len(v) for v in vals])
+    buf = np.frombuffer(b"".join(vals), np.uint8)
+    from mobheat import kafka_host
+    c = kafka_host.decode_columns(buf, offs, [2, 0])
+    assert c["provider"] == ["b", "a"] and c["vehicleId"] == ["v", "1"] and c["lat"] == [1.5, None]
+    assert c["ts_ok"].tolist() == [True, True] and c["malformed"] == [False, False]
+    assert kafka_host.decode_columns(buf, offs, [1])["malformed"] == [True]
