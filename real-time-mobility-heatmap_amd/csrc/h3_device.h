@@ -20,6 +20,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <type_traits>
 
 #include "glibc_libm.h"
@@ -242,6 +243,51 @@ HM_HD void ijkNormalize(IJK &c) {
 // coordinates of a res-15 point on its face stay below 2^24).
 HM_HD int round_div7(int n) { return (int)((unsigned)(n + 3 + 7 * (1 << 27)) / 7u) - (1 << 27); }
 
+// One aperture-7 step up in axial coordinates (x, y) = (i - k, j - k) (_upAp7r / _upAp7 of the normalised IJK: they
+// read only these; _downAp7r / _downAp7 are linear and keep the (1,1,1) direction, so the parent and its centre child
+// need no normalisation): (x, y) becomes the parent, the result is the child's digit -- the normalised unit IJK of
+// (child - centre child), a lookup on (dx, dy) in {-1,0,1}^2, 7 when that is not a unit vector (cf. _unitIjkToDigit).
+// Class II: _upAp7r, centre child by _downAp7r (i -> (3,1,0), j -> (0,3,1)); Class III: _upAp7, by _downAp7
+// (i -> (3,0,1), j -> (1,3,0)).
+template <bool kClass3>
+HM_HD unsigned ap7Up(int &x, int &y) {
+    int px, py, cx, cy;
+    if (kClass3) {
+        px = round_div7(3 * x - y);
+        py = round_div7(x + 2 * y);
+        cx = 2 * px + py;
+        cy = 3 * py - px;
+    } else {
+        px = round_div7(2 * x + y);
+        py = round_div7(3 * y - x);
+        cx = 3 * px - py;
+        cy = px + 2 * py;
+    }
+    const int dx = x - cx, dy = y - cy;
+    unsigned digit = 7;
+    if ((unsigned)(dx + 1) <= 2u && (unsigned)(dy + 1) <= 2u) digit = (0x69d0bd9u >> (3 * ((dx + 1) * 3 + (dy + 1)))) & 7u;
+    x = px;
+    y = py;
+    return digit;
+}
+// Steps in pairs and quads.  A Class II step's centre-child map times the next Class III step's is 7 I in axial
+// coordinates ([[3,-1],[1,2]] [[2,1],[-1,3]]), so (x, y) -> (x, y) + 7 e moves that step pair's grandparent by e and
+// leaves both digits alone: two steps' digits and the grandparent's offset from floor((x, y) / 7) depend only on
+// (x mod 7, y mod 7), and four steps' on (x mod 49, y mod 49).  ap7Pair[7 a + b] / ap7Quad[49 a + b] hold them for
+// (x, y) = (a, b): the digits of the steps in order from bit 0 (3 bits each: 6 / 12 bits), then the ancestor's x + 2
+// and y + 2 in 3 bits each -- computed by running the single steps (hm_make_tables), so equal to them for every
+// input, digit 7 included.
+constexpr int AP7_PAIR = 49, AP7_QUAD = 2401;
+HM_HD int floor_div7(int n) { return (int)((unsigned)(n + 7 * (1 << 27)) / 7u) - (1 << 27); }
+HM_HD int floor_div49(int n) { return (int)((unsigned)(n + 49 * (1 << 24)) / 49u) - (1 << 24); }
+inline unsigned ap7TableEntry(int a, int b, int nsteps) {
+    int x = a, y = b;
+    unsigned e = 0;
+    for (int q = 0; q < nsteps; q++) e |= ((q & 1) ? ap7Up<true>(x, y) : ap7Up<false>(x, y)) << (3 * q);
+    if (x < -2 || x > 5 || y < -2 || y > 5) abort();   // (cannot happen: |ancestor| <= (a, b) / 7^(steps/2) + 1)
+    return e | (unsigned)(x + 2) << (3 * nsteps) | (unsigned)(y + 2) << (3 * nsteps + 3);
+}
+
 // _hex2dToCoordIJK (coordijk.c)
 HM_HD IJK hex2dToCoordIJK(double vx, double vy) {
     IJK h;
@@ -365,14 +411,18 @@ struct H3Tables {
     int faceNeighbors[20][4][5];
     signed char adjacentFaceDir[20][20];
     double edgeY[17];
+    unsigned ap7Quad[AP7_QUAD];    // _faceIjkToH3's digits four steps at a time (ap7TableEntry)
+    unsigned short ap7Pair[AP7_PAIR];
     // glibc's sincos/acos/atan2/tan tables (glibc_libm.h): the device copy for c_tab, the host copy for self-tests
     const glm::Tables *glm;
 };
 
-// the two tables _faceIjkToH3 reads (k_ingest keeps a copy in LDS)
+// the tables _faceIjkToH3 reads (k_ingest keeps a copy in LDS)
 struct H3BaseTables {
     int faceIjkBaseCells[20][3][3][3][2];
     int baseCellData[122][7];
+    unsigned ap7Quad[AP7_QUAD];
+    unsigned short ap7Pair[AP7_PAIR];
 };
 
 // _faceIjkToH3 (faceijk.c), res >= 1.  TT: any table holding faceIjkBaseCells and baseCellData (H3Tables, or the
@@ -384,42 +434,32 @@ HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const TT &T) {
         if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
         return h | ((uint64_t)T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][0] << 45);
     }
-    // Digits from the finest resolution up, in axial coordinates (x, y) = (i - k, j - k): _upAp7/_upAp7r read
-    // only these, _downAp7/_downAp7r are linear and keep the (1,1,1) direction, so the parent and the centre
-    // child need no normalisation; the digit is the normalised unit IJK of (last - centre), a lookup on
-    // (dx, dy) in {-1,0,1}^2 (7 when it is not a unit vector; cf. _unitIjkToDigit).
+    // Digits from the finest resolution up, in axial coordinates (ap7Up): step r (r = res - 1 .. 0) writes the
+    // digit of resolution r + 1 and is Class III when r is even.  After a first single step when res - 1 is even,
+    // the steps run in Class II / Class III pairs: one pair from ap7Pair when their count is odd, then quads from
+    // ap7Quad (res 8: two quad lookups instead of eight steps).
     int x = ijk.i - ijk.k, y = ijk.j - ijk.k;
     uint64_t digits = 0;
-    // one aperture-7 step up: resolution r + 1's digit; Class III (r even): _upAp7, centre child by _downAp7
-    // (i -> (3,0,1), j -> (1,3,0)); Class II: _upAp7r, centre child by _downAp7r (i -> (3,1,0), j -> (0,3,1))
-    auto up = [&](int r, auto cls3) __attribute__((always_inline)) {
-        int px, py, cx, cy;
-        if constexpr (decltype(cls3)::value) {
-            px = round_div7(3 * x - y);
-            py = round_div7(x + 2 * y);
-            cx = 2 * px + py;
-            cy = 3 * py - px;
-        } else {
-            px = round_div7(2 * x + y);
-            py = round_div7(3 * y - x);
-            cx = 3 * px - py;
-            cy = px + 2 * py;
-        }
-        const int dx = x - cx, dy = y - cy;
-        uint32_t digit = 7;
-        if ((unsigned)(dx + 1) <= 2u && (unsigned)(dy + 1) <= 2u)
-            digit = (0x69d0bd9u >> (3 * ((dx + 1) * 3 + (dy + 1)))) & 7u;
-        digits |= (uint64_t)digit << ((14 - r) * 3);
-        x = px;
-        y = py;
-    };
-    // the classes alternate: pairs (odd r: Class II, then r - 1: Class III) with no class branch per digit
     int r = res - 1;
-    if (!(r & 1)) up(r--, std::true_type{});
+    if (!(r & 1)) {
+        digits = (uint64_t)ap7Up<true>(x, y) << ((14 - r) * 3);
+        r--;
+    }
+    if ((r + 1) & 2) {
+        const int qx = floor_div7(x), qy = floor_div7(y);
+        const unsigned e = T.ap7Pair[(x - 7 * qx) * 7 + (y - 7 * qy)];
+        digits |= (uint64_t)(e & 63u) << ((14 - r) * 3);
+        x = qx + (int)((e >> 6) & 7u) - 2;
+        y = qy + (int)((e >> 9) & 7u) - 2;
+        r -= 2;
+    }
 #pragma unroll 1
-    for (; r >= 1; r -= 2) {
-        up(r, std::false_type{});
-        up(r - 1, std::true_type{});
+    for (; r >= 3; r -= 4) {
+        const int qx = floor_div49(x), qy = floor_div49(y);
+        const unsigned e = T.ap7Quad[(x - 49 * qx) * 49 + (y - 49 * qy)];
+        digits |= (uint64_t)(e & 4095u) << ((14 - r) * 3);
+        x = qx + (int)((e >> 12) & 7u) - 2;
+        y = qy + (int)((e >> 15) & 7u) - 2;
     }
     h = (h & ~(HM_DIG_MASK & ~((UINT64_C(1) << (3 * (15 - res))) - 1))) | digits;
     ijk.i = x;

@@ -46,6 +46,11 @@ static hm::H3Tables hm_make_tables() {
     memcpy(T.faceIjkBaseCells, H3T_faceIjkBaseCells, sizeof(T.faceIjkBaseCells));
     memcpy(T.baseCellData, H3T_baseCellData, sizeof(T.baseCellData));
     memcpy(T.faceNeighbors, H3T_faceNeighbors, sizeof(T.faceNeighbors));
+    for (int a = 0; a < 49; a++)
+        for (int b = 0; b < 49; b++) {
+            T.ap7Quad[a * 49 + b] = hm::ap7TableEntry(a, b, 4);
+            if (a < 7 && b < 7) T.ap7Pair[a * 7 + b] = (unsigned short)hm::ap7TableEntry(a, b, 2);
+        }
     for (int a = 0; a < 20; a++)
         for (int b = 0; b < 20; b++) {
             signed char d = a == b ? 0 : -1;
