@@ -84,6 +84,9 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     if (const char *m = getenv("MOBHEAT_INGEST_MODE"))
         ctx->ingest_mode = !strcmp(m, "direct") ? 1 : !strcmp(m, "table") ? 2 : !strcmp(m, "binned") ? 3 : 0;
     if (const char *m = getenv("MOBHEAT_MERGE_GRID")) ctx->merge_grid = std::max(0, atoi(m));
+    // MOBHEAT_DEDUP_STREAM=main runs the dedup on the main stream after the merge path (its cost to the overlapped
+    // kernels, measured by the bench with and without it); default: the side stream
+    if (const char *m = getenv("MOBHEAT_DEDUP_STREAM")) ctx->dedup_main = !strcmp(m, "main");
     // the registry, its census and the batch statistics side by side (one reset, one readback after k_ingest)
     if (hipMalloc(&ctx->d_wreg, REG_BLOCK_BYTES) != hipSuccess || !(ctx->d_wcount = ctx->d_wreg + WREG_SLOTS + 1) ||
         !(ctx->d_st = (DevStats *)(ctx->d_wreg + 2 * (WREG_SLOTS + 1))) ||
@@ -270,7 +273,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     ctx->last_table = table;
     // 4. dedup over the batch's valid rows -- on the side stream, concurrently with step 3 (the rerun of the max on a
     // full table, after the fused one gave up, prepares that table on the main stream: it stays there)
-    ctx->dedup_side = s1.dedup_retry == 0;
+    ctx->dedup_side = s1.dedup_retry == 0 && !ctx->dedup_main;
     // (launched here, ahead of the partition: 1-3% faster on the bench than launched after the merge path's kernels,
     // ~5% faster than overlapping the merge only, 2-4% faster than behind k_ev_hist -- profiles/r3/r3ab12/, r3ab13/)
     if (ctx->dedup_side) {

@@ -232,10 +232,11 @@ __device__ __forceinline__ int wreg_find(unsigned long long *reg, int64_t wq, un
 constexpr int WC_SLOTS = 32;
 struct WinCacheL {
     unsigned long long e[WC_SLOTS];
+    unsigned long long inner[WC_SLOTS];   // window_inner of the cached window, 0 until a row has computed it
     unsigned cnt[WC_SLOTS];   // aggregated rows per cached window (the direct path's census)
 };
 __device__ __forceinline__ void wc_init(WinCacheL &C) {
-    for (int q = threadIdx.x; q < WC_SLOTS; q += blockDim.x) { C.e[q] = 0; C.cnt[q] = 0; }
+    for (int q = threadIdx.x; q < WC_SLOTS; q += blockDim.x) { C.e[q] = 0; C.inner[q] = 0; C.cnt[q] = 0; }
 }
 // widx of window wq (-1: registry full); slot = its cache entry (-1: the cache is full)
 __device__ __forceinline__ int wc_lookup(WinCacheL &C, unsigned long long *reg, int64_t wq, unsigned long long enc, int &slot) {

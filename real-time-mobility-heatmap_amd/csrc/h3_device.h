@@ -453,7 +453,6 @@ HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const TT &T) {
         y = qy + (int)((e >> 9) & 7u) - 2;
         r -= 2;
     }
-#pragma unroll 1
     for (; r >= 3; r -= 4) {
         const int qx = floor_div49(x), qy = floor_div49(y);
         const unsigned e = T.ap7Quad[(x - 49 * qx) * 49 + (y - 49 * qy)];

@@ -34,6 +34,7 @@ struct hm_ctx {
     hipStream_t side_stream = nullptr;
     hipEvent_t side_ev[4] = {};   // [3]: the pooled tables' tags cleared (table_release)
     bool dedup_side = false;
+    bool dedup_main = false;   // MOBHEAT_DEDUP_STREAM=main: never the side stream
     hipEvent_t h2d_ev[H2D_CHUNKS] = {};
     struct H2D { const void *src; void *dst; size_t el; };
     H2D h2d[7] = {};

@@ -213,7 +213,14 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         if constexpr (kBin) {
             // the row's EventRec into its bin (exceptions: k_ingest_exact, once their cell is known)
             if (agg && !exc) {
-                const uint64_t h = mix64(cell ^ window_inner(ws));
+                // the window's hash constant from the window cache (computed by the first rows that find it unset:
+                // every writer stores the same value)
+                uint64_t inner = wslot >= 0 ? __hip_atomic_load(&WC.inner[wslot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
+                if (inner == 0) {
+                    inner = window_inner(ws);
+                    if (wslot >= 0) __hip_atomic_store(&WC.inner[wslot], inner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                const uint64_t h = mix64(cell ^ inner);
                 const unsigned b = region_field(h);
                 const unsigned p = atomicAdd(&bin_cur[b], 1u);
                 if (p < slab_cap) {

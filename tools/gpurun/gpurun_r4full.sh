@@ -1,7 +1,7 @@
 # Round 4 full pass: GPU tests, smoke, the bench, kernel-trace stats of the bench, PMC passes of its first leg
 # -> profiles/r4/kernel_pmc.json (bench.py's roofline traffic and VALU issue), the bench again with the PMC file in
 # place, the gloo N=2 rehearsal beside its N=1 twin, and foreach_batch_func end to end in its default configuration
-# (checkpoints on, null sink beside the loopback wire sink).  $TAG names the output directory; NOTESTS=1 skips the tests.
+# (checkpoints on, null sink beside the loopback wire sink); the dedup on the side stream vs the main stream.  $TAG names the output directory; NOTESTS=1 skips the tests.
 set -o pipefail
 O=gpurun_out/${TAG:-r4full}
 mkdir -p $O
@@ -17,6 +17,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc_write -o r
 python3 tools/ingest_pmc.py --res 8 --events 100000000 --out $O/kernel_pmc.json $O/pmc_f64 $O/pmc_sq $O/pmc_fetch $O/pmc_write > $O/ingest_pmc.log 2>&1 && \
 mkdir -p profiles/r4 && cp $O/kernel_pmc.json profiles/r4/kernel_pmc.json && \
 timeout -k 10 600 python3 bench.py > $O/bench.log 2>&1 && \
+timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-state-leg > $O/bench_dedup_side.log 2>&1 && \
+MOBHEAT_DEDUP_STREAM=main timeout -k 10 300 python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-state-leg > $O/bench_dedup_main.log 2>&1 && \
 MOBHEAT_DIST_BACKEND=gloo timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
   bench.py --gpus 2 --steps 4 --warmup 2 --events 20000000 --no-state-leg > $O/bench_n2.log 2>&1 && \
 timeout -k 10 120 python3 bench.py --gpus 1 --steps 4 --warmup 2 --events 20000000 --no-cpu-baseline --no-state-leg > $O/bench_n1_small.log 2>&1 && \
