@@ -599,11 +599,9 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             tbase = __shfl(tbase, 0, 64);
             return tbase + (unsigned)__popcll(fb & ((1ull << lane_id()) - 1));
         };
+        // (one LDS add per created key: a ballot per resident region measured 0.17 ms slower on the bench, r4j/)
         auto count_created = [&](bool created, int r) __attribute__((always_inline)) {
-            for (int q = 0; q < nres; q++) {
-                const unsigned long long m = __ballot(created && r == q);
-                if (m && lane_id() == 0) atomicAdd(&S.res_new[q], (unsigned)__popcll(m));
-            }
+            if (created && r >= 0) atomicAdd(&S.res_new[r], 1u);
         };
         // software pipeline: the next chunk's record is loaded while this chunk is merged
         Rec nxt;

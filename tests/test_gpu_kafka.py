@@ -204,7 +204,7 @@ def test_splice_unsupported_records_into_device_batch():
     offs = np.cumsum([0] + [len(v) for v in vals]).astype(np.int64)
     eng = HeatmapEngine(h3_res=8)
     kb = eng.decode_json(buf, offs)
-    assert kb.n_spliced == len(odd)
+    assert kb.n_spliced == len(odd) - 1   # (an integer as a string field is the device decoder's own: its text)
     _check_decoded(kb, _host_expected(buf, offs), len(vals))
     assert b"mbta" in _dict_strings(kb.providers) and b"1.5" in _dict_strings(kb.vehicles)
     # the batch through hm_process_batch: the spliced rows are ordinary rows
@@ -214,7 +214,7 @@ def test_splice_unsupported_records_into_device_batch():
     jin = _lib.HmJsonIn(n=offs.size - 1, memory=_lib.HM_MEM_HOST, flags=0, bytes=buf.ctypes.data,
                         offsets=offs.ctypes.data)
     jout = _lib.HmJsonOut()
-    assert lib.hm_decode_json(eng._ctx, jin, jout) == _lib.HM_E_UNSUPPORTED and jout.n_unsupported == len(odd)
+    assert lib.hm_decode_json(eng._ctx, jin, jout) == _lib.HM_E_UNSUPPORTED and jout.n_unsupported == len(odd) - 1
     eng.close()
 
 

@@ -28,7 +28,7 @@ def main():
     for r in csv.DictReader(open(os.path.join(a.dir, "run_counter_collection.csv"))):
         name = r["Kernel_Name"]
         k = "k_phase<%s>" % name.split("k_phase<")[1][0] if "k_phase<" in name else \
-            ("k_ingest<%s>" % ("true" if "<true>" in name else "false") if "k_ingest<" in name else short(name))
+            ("k_ingest<%s>" % ("true" if "<true" in name else "false") if "k_ingest<" in name else short(name))
         per[k][r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
         dur[k][r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
     n = a.events
