@@ -209,7 +209,8 @@ def test_splice_unsupported_records_into_device_batch():
     assert b"mbta" in _dict_strings(kb.providers) and b"1.5" in _dict_strings(kb.vehicles)
     # the batch through hm_process_batch: the spliced rows are ordinary rows
     res, _ = eng.process_kafka(0, buf, offs)
-    assert res.n_valid == int(_host_expected(buf, offs)["row_valid"].sum())
+    e = _host_expected(buf, offs)   # valid: row_valid and lat / lon in range (the sanity filter, :96-106)
+    assert res.n_valid == int((e["row_valid"] & (np.abs(e["lat"]) <= 90) & (np.abs(e["lon"]) <= 180)).sum())
     lib = _lib.load()
     jin = _lib.HmJsonIn(n=offs.size - 1, memory=_lib.HM_MEM_HOST, flags=0, bytes=buf.ctypes.data,
                         offsets=offs.ctypes.data)
