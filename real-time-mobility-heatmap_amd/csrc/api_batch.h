@@ -60,7 +60,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     if (upload_tables() != hipSuccess) { ctx->err = "tables"; return fail("create"); }
     for (int variant = 0; variant < 2; variant++) {
-        const void *kern = variant ? (const void *)ingest_kernel<true>(cfg->h3_res) : (const void *)ingest_kernel<false>(cfg->h3_res);
+        const void *kern = variant ? (const void *)k_ingest<true> : (const void *)k_ingest<false>;
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, IG_THREADS, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) {

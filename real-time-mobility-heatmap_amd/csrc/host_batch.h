@@ -68,7 +68,7 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
                 HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->h2d_ev[c], 0));
             }
             const int blocks = (int)std::min<int64_t>((b - a + IG_THREADS - 1) / IG_THREADS, bin ? ctx->ingest_grid_bin : ctx->ingest_grid);
-            auto kern = bin ? ingest_kernel<true>(ctx->cfg.h3_res) : ingest_kernel<false>(ctx->cfg.h3_res);
+            auto kern = bin ? k_ingest<true> : k_ingest<false>;
             hipLaunchKernelGGL(kern, dim3(blocks), dim3(IG_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.vk, a, b,
                                ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
                                (uint64_t *)ctx->keys.p, ctx->dfused.tab, ctx->dfused.cap - 1, (unsigned int *)ctx->dfused.used.p,

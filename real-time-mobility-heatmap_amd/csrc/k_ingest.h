@@ -68,9 +68,10 @@ __device__ __forceinline__ void wave_count_slots(bool pred, int slot, unsigned *
 // has 2^REGION_BITS regions, so region = bin, kernels.h) at slab b * slab_cap + a returned atomic on the bin's
 // cursor -- instead of a later histogram + scatter pass over the keys and columns.  A bin past slab_cap counts in
 // DevStats.bin_overflow and the host partitions the batch from its keys instead.
-// kRes: the resolution as a compile-time constant (one variant per resolution: the digit loop of _faceIjkToH3 unrolled,
-// its shifts constant; ingest_kernel picks the context's), -1 = res_arg at run time
-template <bool kBin, int kRes = -1>
+// (one kernel for every resolution: per-resolution specialisations of this kernel, measured no faster once the digits
+// came from the step tables, were miscompiled at res 3 by this compiler -- wrong cells, caught by
+// test_ingest_cells_every_resolution, profiles/r4/r4w/)
+template <bool kBin>
 __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     const double *__restrict__ lat, const double *__restrict__ lon, const int64_t *__restrict__ ts,
     const uint8_t *__restrict__ row_valid, const uint64_t *__restrict__ vkey, int64_t i_begin, int64_t n, int res_arg, FloorDiv wdiv,
@@ -79,7 +80,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     unsigned long long *n_slow, unsigned long long *dgiveup, unsigned long long *wreg, unsigned long long *wcount,
     DevStats *st, const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid, unsigned *__restrict__ bin_cur,
     EventRec *__restrict__ slabs, unsigned slab_cap) {
-    const int res = kRes >= 0 ? kRes : res_arg;
+    const int res = res_arg;
     __shared__ WinCacheL WC;
     __shared__ double Fc[20][3], Fu[20][2][3];   // the fast path's per-face tables (res parity): LDS reads
     __shared__ unsigned dskip;                    // the fused dedup has given up (*dgiveup) -- skip it
@@ -264,18 +265,6 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     }
 }
 
-using IngestFn = decltype(&k_ingest<false>);
-#define HM_INGEST_CASE(r) case r: return k_ingest<kBin, r>;
-template <bool kBin>
-static IngestFn ingest_kernel(int res) {
-    switch (res) {
-        HM_INGEST_CASE(0) HM_INGEST_CASE(1) HM_INGEST_CASE(2) HM_INGEST_CASE(3) HM_INGEST_CASE(4) HM_INGEST_CASE(5)
-        HM_INGEST_CASE(6) HM_INGEST_CASE(7) HM_INGEST_CASE(8) HM_INGEST_CASE(9) HM_INGEST_CASE(10) HM_INGEST_CASE(11)
-        HM_INGEST_CASE(12) HM_INGEST_CASE(13) HM_INGEST_CASE(14) HM_INGEST_CASE(15)
-        default: return k_ingest<kBin>;
-    }
-}
-#undef HM_INGEST_CASE
 
 // exceptions of k_ingest's fast path: upstream's exact sequence; the cell bits go into the row's key (k_ingest
 // wrote its window slot); with slabs (k_ingest<true>) the row's EventRec into its bin as k_ingest does

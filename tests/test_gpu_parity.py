@@ -37,7 +37,8 @@ def assert_batch_equal(res, exp):
     g = _tiles_dict_gpu(res.tiles)
     o = _tiles_dict_oracle(exp["tiles"])
     assert len(g) == len(res.tiles), "duplicate keys emitted"
-    assert set(g) == set(o), f"key sets differ: gpu-only {len(set(g) - set(o))}, oracle-only {len(set(o) - set(g))}"
+    go, oo = set(g) - set(o), set(o) - set(g)   # (a plain set assert's diff repr takes minutes on 1e5 keys)
+    assert not go and not oo, f"key sets differ: gpu-only {len(go)} {sorted(go)[:3]}, oracle-only {len(oo)} {sorted(oo)[:3]}"
     bad = [k for k in g if g[k][0] != o[k][0] or not all(_close(g[k][i], o[k][i]) for i in (1, 2, 3))]
     assert not bad, f"{len(bad)} tiles differ, e.g. {bad[0]}: gpu {g[bad[0]]} oracle {o[bad[0]]}"
     np.testing.assert_array_equal(np.sort(res.latest_rows), exp["latest_rows"])
@@ -65,6 +66,30 @@ def test_latlng_to_cell_random_and_edges(oracle_h3, res):
         exp = np.where((lat >= -90) & (lat <= 90) & (lon >= -180) & (lon <= 180), exp, 0)
     bad = got != exp
     assert not bad.any(), f"res {res}: {bad.sum()} / {lat.size} mismatches, e.g. {lat[bad][:3]}, {lon[bad][:3]}"
+
+
+@pytest.mark.parametrize("res", range(16))
+def test_ingest_cells_every_resolution(res):
+    """k_ingest computes its cells with a kernel specialised per resolution: the tiles of one batch (one window)
+    hold exactly the cells latlng_to_cell gives for its points, with the right counts, at every resolution
+    (a miscompiled specialisation showed up only at some resolutions)."""
+    import mobheat
+    from mobheat import HeatmapEngine
+    rng = np.random.default_rng(900 + res)
+    n = 200_000
+    lat = np.degrees(np.arcsin(rng.uniform(-1.0, 1.0, n)))
+    lon = rng.uniform(-180.0, 180.0, n)
+    ts = 1_759_572_000_000_000 + rng.integers(0, 60_000_000, n)
+    eng = HeatmapEngine(h3_res=res)
+    r = eng.process_batch(0, lat, lon, ts, rng.uniform(0, 90, n), np.ones(n, bool),
+                          rng.integers(0, 5000, n).astype(np.uint64), np.ones(n, bool))
+    cells, counts = np.unique(mobheat.latlng_to_cell(lat, lon, res), return_counts=True)
+    got = dict(zip(r.tiles.cell.tolist(), r.tiles.count.tolist()))
+    want = dict(zip(cells.tolist(), counts.tolist()))
+    bad = set(got) ^ set(want)
+    assert not bad, f"res {res}: {len(bad)} cells differ, e.g. {[hex(c) for c in sorted(bad)[:3]]}"
+    assert got == want
+    eng.close()
 
 
 def test_latlng_to_cell_golden():
@@ -159,6 +184,7 @@ def test_state_read_regime_matches_oracle():
     ora = SparkHeatmapOracle(h3_res=3)
     for epoch in range(7):
         b = dict(lat=lat, lon=lon, ts_us=base + epoch * 60_000_000, speed=speed, speed_valid=sv, vkey=vkey, row_valid=rv)
+        print(f"state-read regime: batch {epoch}", flush=True)
         res, exp = _run(eng, ora, b, epoch)
         assert_batch_equal(res, exp)
         if 0 < epoch < 5:
