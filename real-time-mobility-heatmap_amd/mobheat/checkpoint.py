@@ -4,7 +4,8 @@ Spark keeps the aggregation state under the query's checkpointLocation and, afte
 uncommitted epoch on the state of the epoch before it.  Here every rank (one GPU, one engine) keeps a chain of files
 under ``<CHECKPOINT>/mobheat-state``, like Spark's HDFS state store: a full snapshot (``state-<E>``), then one delta per
 committed epoch (``delta-<E>``: the keys that epoch touched, hm_state_export_touched), a new snapshot every
-``full_every`` deltas.  File names carry the rank and the world size: ``state-<E>.r<rank>of<world>.npz``.
+``full_every`` deltas.  File names carry the rank and the world size: ``state-<E>.r<rank>of<world>.mhs`` (a JSON
+header and the raw records, engine.save_state_file; ``.npz`` files of earlier versions are read too).
 
 Every file records, besides the engine's state (hm_state_info + 64-B records), its chain: the lineage id (one per
 uninterrupted stream of epochs: a fresh stream starts a new one), the epoch of the chain's snapshot and of the file
@@ -27,7 +28,7 @@ from collections import namedtuple
 import numpy as np
 
 Entry = namedtuple("Entry", "epoch kind rank world path")
-_NAME = re.compile(r"^(state|delta)-(-?\d+)(?:\.r(\d+)of(\d+))?\.npz$")
+_NAME = re.compile(r"^(state|delta)-(-?\d+)(?:\.r(\d+)of(\d+))?\.(?:mhs|npz)$")
 RestorePoint = namedtuple("RestorePoint", "epoch world lineage")
 
 
@@ -63,17 +64,18 @@ class StateCheckpoints:
     def path(self, kind, epoch, rank=None, world=None):
         rank = self.rank if rank is None else rank
         world = self.world if world is None else world
-        return os.path.join(self.root, f"{'state' if kind == 'full' else 'delta'}-{int(epoch)}.r{rank}of{world}.npz")
+        return os.path.join(self.root, f"{'state' if kind == 'full' else 'delta'}-{int(epoch)}.r{rank}of{world}.mhs")
 
     def meta(self, e):
         """The chain record of a file: lineage, base (its snapshot's epoch), prev (the file before it, -1 for a
         snapshot).  Files without one (written before chains were recorded) read as their own one-file chain."""
         key = (e.path, os.path.getmtime(e.path) if os.path.exists(e.path) else 0)
         if key not in self._meta_cache:
+            from .engine import read_state_meta
             try:
-                with np.load(e.path, allow_pickle=False) as z:
-                    m = json.loads(str(z["meta"])) if "meta" in z.files else None
-            except (OSError, ValueError, KeyError):
+                raw = read_state_meta(e.path)
+                m = json.loads(raw) if raw is not None else None
+            except (OSError, ValueError, KeyError, RuntimeError):
                 m = None
             if m is None:
                 m = {"lineage": None, "base": e.epoch if e.kind == "full" else None, "prev": -1 if e.kind == "full" else None}

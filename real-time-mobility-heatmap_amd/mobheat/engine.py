@@ -5,6 +5,7 @@ tile state (Spark's state store for the window aggregation, reference heatmap_st
 update mode, :243) and the watermark bookkeeping (withWatermark 10 minutes, :107).
 """
 import ctypes
+import json
 from dataclasses import dataclass
 
 import numpy as np
@@ -264,7 +265,7 @@ class HeatmapEngine:
               "hm_state_import")
 
     def save_state(self, path):
-        """export_state() written atomically to `path` (.npz: plain arrays, no pickles)."""
+        """export_state() written atomically to `path` (save_state_file: a JSON header and the raw records)."""
         info, recs = self.export_state()
         save_state_file(path, info, recs)
         return info
@@ -397,26 +398,66 @@ def merge_state(base, deltas):
     return info, np.ascontiguousarray(allr)
 
 
+STATE_FILE_MAGIC = b"MHSTATE1"   # raw state file: magic, u64 header bytes, JSON header, padding to 64 B, the records
+
+
 def save_state_file(path, info, recs, meta=None):
-    """info + records written atomically to `path` (.npz of plain arrays, no pickles); `meta` (a str: the checkpoint
-    chain record, mobheat.checkpoint) is stored beside them."""
+    """info + records written atomically to `path` (tmp file, fsync, rename): a JSON header (the hm_state_info fields,
+    the record count and layout, `meta` -- a str: the checkpoint chain record, mobheat.checkpoint) and the 64-B records
+    as raw bytes in one write.  (np.savez's zip container CRC-checked and copied every byte under the GIL: the
+    checkpoint thread then slowed the next batch's host work and waited ~0.4 s per 10M-key delta, profiles/r4.)"""
     import os
+    recs = np.ascontiguousarray(recs, dtype=STATE_REC_DTYPE)
+    head = json.dumps({"info": {k: int(info[k]) for k in _INFO_FIELDS}, "n": int(recs.size),
+                       "fields": list(STATE_REC_DTYPE.names), "itemsize": STATE_REC_DTYPE.itemsize,
+                       "meta": meta}).encode()
+    head += b" " * (-(len(head) + 16) % 64)
     tmp = f"{path}.tmp{os.getpid()}"
-    extra = {} if meta is None else {"meta": np.array(meta)}
     with open(tmp, "wb") as f:
-        np.savez(f, info=np.array([info[k] for k in _INFO_FIELDS], np.int64), recs=recs, **extra)
+        f.write(STATE_FILE_MAGIC + len(head).to_bytes(8, "little") + head)
+        if recs.size:
+            f.write(memoryview(recs).cast("B"))
         f.flush()
         os.fsync(f.fileno())
     os.replace(tmp, path)
 
 
+def _state_header(f, path):
+    """The JSON header of a raw state file (f positioned at its start), or None for a legacy .npz file."""
+    if f.read(8) != STATE_FILE_MAGIC:
+        return None
+    n = int.from_bytes(f.read(8), "little")
+    h = json.loads(f.read(n))
+    if h.get("itemsize") != STATE_REC_DTYPE.itemsize or h.get("fields") != list(STATE_REC_DTYPE.names):
+        raise RuntimeError(f"{path}: state records of another layout")
+    return h
+
+
 def load_state_file(path):
+    """(info, records) of a state file: the raw format, or the .npz files written before round 4."""
+    with open(path, "rb") as f:
+        h = _state_header(f, path)
+        if h is not None:
+            recs = np.fromfile(f, dtype=STATE_REC_DTYPE, count=h["n"])
+            if recs.size != h["n"]:
+                raise RuntimeError(f"{path}: truncated ({recs.size} of {h['n']} records)")
+            return {k: int(h["info"][k]) for k in _INFO_FIELDS}, recs
     with np.load(path, allow_pickle=False) as z:
         vals = z["info"]
         recs = z["recs"]
     if vals.size != len(_INFO_FIELDS) or recs.dtype != STATE_REC_DTYPE:
         raise RuntimeError(f"{path}: not a mobheat state checkpoint")
     return {k: int(v) for k, v in zip(_INFO_FIELDS, vals)}, recs
+
+
+def read_state_meta(path):
+    """The `meta` string stored with a state file (None when it has none)."""
+    with open(path, "rb") as f:
+        h = _state_header(f, path)
+        if h is not None:
+            return h.get("meta")
+    with np.load(path, allow_pickle=False) as z:
+        return str(z["meta"]) if "meta" in z.files else None
 
 
 def latlng_to_cell(lat, lon, res, device=0):

@@ -158,11 +158,19 @@ def test_state_checkpoint_files_and_resume_choice(tmp_path, monkeypatch):
     recs["sum_speed"] = [0.5, np.nan, -1.25]
     info = dict(epoch_id=7, n_keys=3, watermark_ms=11, prev_watermark_ms=10, tile_us=300_000_000,
                 watermark_delay_ms=600_000, h3_res=8)
-    p = str(tmp_path / "s.npz")
-    eng_mod.save_state_file(p, info, recs)
+    p = str(tmp_path / "s.mhs")
+    eng_mod.save_state_file(p, info, recs, meta='{"lineage": "L"}')
     info2, recs2 = eng_mod.load_state_file(p)
-    assert info2 == info
+    assert info2 == info and eng_mod.read_state_meta(p) == '{"lineage": "L"}'
     np.testing.assert_array_equal(recs2.view(np.uint8), recs.view(np.uint8))
+    # the .npz files of earlier versions still load (and an empty state round-trips)
+    legacy = str(tmp_path / "old.npz")
+    np.savez(legacy, info=np.array([info[k] for k in eng_mod._INFO_FIELDS], np.int64), recs=recs, meta=np.array("m"))
+    info3, recs3 = eng_mod.load_state_file(legacy)
+    assert info3 == info and eng_mod.read_state_meta(legacy) == "m"
+    np.testing.assert_array_equal(recs3.view(np.uint8), recs.view(np.uint8))
+    eng_mod.save_state_file(p, info, recs[:0])
+    assert eng_mod.load_state_file(p)[1].size == 0 and eng_mod.read_state_meta(p) is None
 
     imported = []
 
