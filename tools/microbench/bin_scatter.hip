@@ -1,6 +1,8 @@
 // Binning 1e8 32-B records into 8192 (window, region) bins on MI355X: the write pattern of k_ingest's fused binning
 // (each lane reserves a slot with a per-bin atomic and writes its record there) against alternatives:
 //   seq      record i -> slot i (the HBM write roofline of the same bytes)
+//   atomic   direct's per-record returned atomic, the records written in order (its atomics alone)
+//   scatter  direct's scattered writes to slots reserved beforehand (its write pattern alone)
 //   direct   per-record atomic cursor of 8192 bins (k_ingest<true> today)
 //   xcd      per-record atomic cursor of (bin, XCC id): 8 sub-slabs per bin, each written from one XCD only
 //   lds S    per workgroup tile of 2048 records sorted in LDS by S super-bins, one atomic per (tile, super-bin),
@@ -36,6 +38,33 @@ __global__ __launch_bounds__(256) void k_direct(const uint4 *__restrict__ src, u
         const uint4 a = src[2 * i], b = src[2 * i + 1];
         const unsigned s = XCD ? bin_of(i) * 8 + x : bin_of(i);
         const unsigned p = atomicAdd(&cur[s], 1u);
+        if (p < cap) {
+            dst[2 * ((int64_t)s * cap + p)] = a;
+            dst[2 * ((int64_t)s * cap + p) + 1] = b;
+        }
+    }
+}
+
+// the two halves of `direct` apart: the per-record returned atomic with the records written in order (slot i), and the
+// scattered writes to slots reserved beforehand (slot[i] from an untimed pass; +4 B read per record)
+__global__ __launch_bounds__(256) void k_atomic_seq(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n,
+                                                    unsigned *cur) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const uint4 a = src[2 * i], b = src[2 * i + 1];
+        const unsigned p = atomicAdd(&cur[bin_of(i)], 1u);
+        dst[2 * i] = make_uint4(a.x, a.y, a.z, p);   // (the returned slot is used: the atomic's latency counts)
+        dst[2 * i + 1] = b;
+    }
+}
+__global__ __launch_bounds__(256) void k_slots(int64_t n, unsigned *cur, unsigned *slot) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        slot[i] = atomicAdd(&cur[bin_of(i)], 1u);
+}
+__global__ __launch_bounds__(256) void k_scatter_pre(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n,
+                                                     const unsigned *__restrict__ slot, unsigned cap) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const uint4 a = src[2 * i], b = src[2 * i + 1];
+        const unsigned s = bin_of(i), p = slot[i];
         if (p < cap) {
             dst[2 * ((int64_t)s * cap + p)] = a;
             dst[2 * ((int64_t)s * cap + p) + 1] = b;
@@ -171,6 +200,18 @@ int main(int argc, char **argv) {
         printf("rep %d seq            %.3f ms\n", rep, timed([&] { hipLaunchKernelGGL(k_seq, dim3(8192), dim3(512), 0, 0, src, dst, n); }));
         printf("rep %d direct 8192    %.3f ms\n", rep,
                timed([&] { hipLaunchKernelGGL(k_direct<false>, dim3(grid), dim3(256), 0, 0, src, dst, n, cur, cap); }));
+        printf("rep %d atomic, seq    %.3f ms\n", rep,
+               timed([&] { hipLaunchKernelGGL(k_atomic_seq, dim3(grid), dim3(256), 0, 0, src, dst, n, cur); }));
+        {
+            unsigned *slot;
+            CHK(hipMalloc(&slot, n * 4));
+            CHK(hipMemset(cur, 0, BINS * 8 * 4));
+            hipLaunchKernelGGL(k_slots, dim3(grid), dim3(256), 0, 0, n, cur, slot);
+            CHK(hipDeviceSynchronize());
+            const float t = timed([&] { hipLaunchKernelGGL(k_scatter_pre, dim3(grid), dim3(256), 0, 0, src, dst, n, slot, cap); });
+            printf("rep %d scatter, pre   %.3f ms\n", rep, t);
+            CHK(hipFree(slot));
+        }
         printf("rep %d xcd 8192x8     %.3f ms\n", rep,
                timed([&] { hipLaunchKernelGGL(k_direct<true>, dim3(grid), dim3(256), 0, 0, src, dst, n, cur, cap / 8 + 256); }));
         auto two = [&](auto kl, auto ks, int S) {
