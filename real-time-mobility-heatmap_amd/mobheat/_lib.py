@@ -284,9 +284,11 @@ def tile_statements_selftest(tiles, city, h3_res, ttl_minutes, tile_us):
 
 
 def _dictionary(strings):
-    """(n, offsets int64[n+1], bytes) of a list of str, UTF-8 (Arrow's string layout)."""
+    """(n, offsets int64[n+1], bytes) of a list of str or an Arrow string array, UTF-8 (Arrow's string layout)."""
     import pyarrow as pa
-    arr = pa.array(list(strings), type=pa.large_string())
+    if isinstance(strings, pa.ChunkedArray):
+        strings = strings.combine_chunks()
+    arr = strings.cast(pa.large_string()) if isinstance(strings, pa.Array) else pa.array(list(strings), type=pa.large_string())
     n = len(arr)
     offs = np.frombuffer(arr.buffers()[1], dtype=np.int64, count=n + 1, offset=arr.offset * 8).copy() if n else np.zeros(1, np.int64)
     offs -= offs[0]
