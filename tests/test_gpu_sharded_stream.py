@@ -180,3 +180,40 @@ def test_sharded_foreach_batch_func_general_inputs_and_replay(tmp_path, monkeypa
         # for one _id, in no defined order, as in the reference's unordered bulk)
         _assert_same_statements(got[k]["positions_latest"], ref[e]["positions_latest"], f"epoch {e} positions_latest")
     stream.close_sharded()
+
+
+def test_sharded_foreach_batch_func_on_kafka_values(tmp_path, monkeypatch):
+    """The raw Kafka `value` column over 2 ranks (decoded on rank 0's GPU, records outside the device decoder spliced
+    in from the host decode, the batch-wide dictionaries shared): the same statements as one GPU, byte for byte
+    (dyadic coordinates: exact in JSON and in every sum)."""
+    import datetime
+    import json
+    from mobheat import stream
+    rng = np.random.default_rng(17)
+    frames = []
+    for b in range(3):
+        n = 20_000
+        vals = []
+        for k in range(n):
+            ts = datetime.datetime.fromtimestamp(T0 + b * 240 + int(rng.integers(0, 360)), datetime.timezone.utc)
+            vals.append(json.dumps({"provider": "mbta" if k % 7 == 0 else "opensky",
+                                    "vehicleId": f"v{int(rng.integers(0, 1500)):04d}",
+                                    "lat": 42.0 + int(rng.integers(0, 1 << 14)) / 65536.0,
+                                    "lon": -71.25 + int(rng.integers(0, 1 << 14)) / 65536.0,
+                                    "speedKmh": None if k % 10 == 0 else int(rng.integers(0, 160)) * 0.5,
+                                    "bearing": 90, "accuracyM": None,
+                                    "ts": ts.strftime("%Y-%m-%dT%H:%M:%SZ")}).encode())
+        vals[5] = b'{"provider":"mbta","vehicleId":1.5,"lat":42.25,"lon":-71.0,"ts":"2025-10-04T10:00:30Z"}'
+        vals[9] = b'{"provider":{"a":1},"vehicleId":"v0001","lat":42.125,"lon":-71.125,"ts":"2025-10-04T10:01:00Z"}'
+        frames.append(pd.DataFrame({"value": vals}))
+    _set(monkeypatch, stream, tmp_path, 1, "k1")
+    ref = _run(stream, frames, range(3))
+    stream.reset_engine()
+    _set(monkeypatch, stream, tmp_path, 2, "k2")
+    got = _run(stream, frames, range(3))
+    for e in range(3):
+        for coll in ("tiles", "positions_latest"):
+            _assert_same_statements(got[e][coll], ref[e][coll], f"epoch {e} {coll}")
+        assert len(ref[e]["positions_latest"]) > 1000
+    assert any(b"mbta|1.5" in s for s in ref[0]["positions_latest"])
+    stream.close_sharded()
