@@ -173,6 +173,11 @@ __device__ __forceinline__ MRec mrec_of(const SortedRec &p, const WInfo *, uint6
 __device__ __forceinline__ MRec mrec_of(const GrowRec &p, const WInfo *, uint64_t) {
     return MRec{p.cell, wenc_of(p.wstart), tile_hash(p.cell, p.wstart), p.count, p.nspeed, p.sspeed, p.slat, p.slon, p.touched};
 }
+__device__ __forceinline__ MRec mrec_of_wi(const EventRec &p, const WInfo &wi, uint64_t cell_hi) {
+    const uint64_t cell = (p.key & CELL_LO) | cell_hi;
+    const bool sv = __builtin_bit_cast(uint64_t, p.speed) != SPEED_NULL_BITS;
+    return MRec{cell, wi.wenc, mix64(cell ^ wi.inner), 1ull, sv ? 1ull : 0ull, sv ? p.speed : 0.0, p.lat, p.lon, 0ull};
+}
 __device__ __forceinline__ MRec mrec_of(const EventRec &p, const WInfo *winfo, uint64_t cell_hi) {
     const WInfo &wi = winfo[ekey_widx(p.key)];   // (an LDS copy measured no faster here: the chunk loop hides it)
     const uint64_t cell = (p.key & CELL_LO) | cell_hi;
@@ -622,14 +627,22 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                 return bp + i;
             }
         };
+        constexpr bool kEv = std::is_same<Rec, EventRec>::value;
+        // EventRec: the next chunk's window parameters are loaded with the chunk's store drain, so that the record's
+        // hash needs no dependent load at the chunk's start (state-read leg's merge -0.27 ms, bench leg unchanged:
+        // profiles/r4/r4v7/)
+        WInfo nwi{};
         if (b0 + t < b1) nxt = ld_stream(rec_at(b0 + t));
+        if constexpr (kEv) { if (b0 + t < b1) nwi = winfo[ekey_widx(nxt.key)]; }
         for (int64_t c0 = b0; c0 < b1; c0 += MO_THREADS) {
             // 1. stage this chunk's records in LDS
             const int64_t i = c0 + t;
             const bool has = i < b1;
             MRec p{};
-            if (has) p = mrec_of(nxt, winfo, cell_hi);   // (the window parameters from an LDS image cost the state-read
-                                                         // leg's merge ~1 ms, profiles/r3/r3ab11: a global load)
+            if (has) {
+                if constexpr (kEv) p = mrec_of_wi(nxt, nwi, cell_hi);
+                else p = mrec_of(nxt, winfo, cell_hi);
+            }
             if (i + MO_THREADS < b1) nxt = ld_stream(rec_at(i + MO_THREADS));
             if (has) {
                 S.sc[t] = p.cell;
@@ -704,6 +717,7 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                 const bool count_here = created && !rehash && r < 0;
                 if (__ballot(count_here) && !wave_count_windows(count_here, p.we, 1ull, WL, sink)) overflow = true;
             }
+            if constexpr (kEv) { if (i + MO_THREADS < b1) nwi = winfo[ekey_widx(nxt.key)]; }
             // 5. drain this chunk's stores (visible to the next chunk's probes: a full barrier waits for every store of
             // the wave -- measured: draining them a chunk later instead, deferring the keys the previous chunk wrote,
             // cost 1.5 ms on the bench and 4.5 ms on the state-read leg); release the claims
