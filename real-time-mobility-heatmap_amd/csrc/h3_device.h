@@ -413,26 +413,31 @@ struct H3Tables {
     double edgeY[17];
     unsigned ap7Quad[AP7_QUAD];    // _faceIjkToH3's digits four steps at a time (ap7TableEntry)
     unsigned short ap7Pair[AP7_PAIR];
+    // _faceIjkToH3's reads of faceIjkBaseCells and baseCellData, packed (one LDS read each in k_ingest):
+    // fijkPacked[((face * 3 + i) * 3 + j) * 3 + k] = base cell | numRots << 8;
+    // bcdPacked[base cell] = pentagon | (cw offset face 0 + 1) << 8 | (cw offset face 1 + 1) << 16
+    unsigned short fijkPacked[20 * 27];
+    unsigned bcdPacked[122];
     // glibc's sincos/acos/atan2/tan tables (glibc_libm.h): the device copy for c_tab, the host copy for self-tests
     const glm::Tables *glm;
 };
 
 // the tables _faceIjkToH3 reads (k_ingest keeps a copy in LDS)
 struct H3BaseTables {
-    int faceIjkBaseCells[20][3][3][3][2];
-    int baseCellData[122][7];
     unsigned ap7Quad[AP7_QUAD];
+    unsigned bcdPacked[122];
+    unsigned short fijkPacked[20 * 27];
     unsigned short ap7Pair[AP7_PAIR];
 };
 
-// _faceIjkToH3 (faceijk.c), res >= 1.  TT: any table holding faceIjkBaseCells and baseCellData (H3Tables, or the
+// _faceIjkToH3 (faceijk.c), res >= 1.  TT: any table holding the packed base-cell tables (H3Tables, or the
 // LDS copy k_ingest keeps: lane-indexed reads there do not wait behind the vector loads in flight)
 template <typename TT>
 HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const TT &T) {
     uint64_t h = UINT64_C(0x00001fffffffffff) | (UINT64_C(1) << 59) | ((uint64_t)res << 52);
     if (res == 0) {
         if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
-        return h | ((uint64_t)T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][0] << 45);
+        return h | ((uint64_t)(T.fijkPacked[((face * 3 + ijk.i) * 3 + ijk.j) * 3 + ijk.k] & 0x7fu) << 45);
     }
     // Digits from the finest resolution up, in axial coordinates (ap7Up): step r (r = res - 1 .. 0) writes the
     // digit of resolution r + 1 and is Class III when r is even.  After a first single step when res - 1 is even,
@@ -466,8 +471,9 @@ HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const TT &T) {
     ijk.k = 0;
     ijkNormalize(ijk);
     if (ijk.i > 2 || ijk.j > 2 || ijk.k > 2) return 0;
-    int baseCell = T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][0];
-    int numRots = T.faceIjkBaseCells[face][ijk.i][ijk.j][ijk.k][1];
+    const unsigned fe = T.fijkPacked[((face * 3 + ijk.i) * 3 + ijk.j) * 3 + ijk.k];
+    const int baseCell = (int)(fe & 0x7fu);
+    const int numRots = (int)(fe >> 8);
     h |= (uint64_t)baseCell << 45;
     // the rotations as one count m of 60-degree ccw steps, applied once (rotate60k).  Hexagon: numRots.  Pentagon
     // (upstream: a leading K digit is first rotated out, cw on the base cell's cw-offset faces, then numRots
@@ -475,11 +481,12 @@ HM_HD uint64_t faceIjkToH3(int face, IJK ijk, int res, const TT &T) {
     // position q in the cycle 5 -> 4 -> 6 -> 2 -> 3, numRots steps pass the deleted K (q + numRots) / 5 times
     // (numRots <= 5, q <= 4).  Equal to rotatePent60ccw applied numRots times (test_device_numerics_host).
     int m = numRots;
-    if (T.baseCellData[baseCell][4]) {
+    const unsigned bd = T.bcdPacked[baseCell];
+    if (bd & 1u) {
         int lead = leadingNonZeroDigit(h, res);
         int m0 = 0;
         if (lead == 1) {
-            const bool cw = T.baseCellData[baseCell][5] == face || T.baseCellData[baseCell][6] == face;
+            const bool cw = ((bd >> 8) & 0xffu) == (unsigned)face + 1u || ((bd >> 16) & 0xffu) == (unsigned)face + 1u;
             m0 = cw ? 5 : 1;
             lead = cw ? 3 : 5;
         }

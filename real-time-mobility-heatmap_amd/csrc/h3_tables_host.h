@@ -45,6 +45,17 @@ static hm::H3Tables hm_make_tables() {
     }
     memcpy(T.faceIjkBaseCells, H3T_faceIjkBaseCells, sizeof(T.faceIjkBaseCells));
     memcpy(T.baseCellData, H3T_baseCellData, sizeof(T.baseCellData));
+    for (int f = 0; f < 20; f++)
+        for (int q = 0; q < 27; q++) {
+            const int bc = H3T_faceIjkBaseCells[f][q / 9][(q / 3) % 3][q % 3][0], rots = H3T_faceIjkBaseCells[f][q / 9][(q / 3) % 3][q % 3][1];
+            if (bc < 0 || bc >= 122 || rots < 0 || rots > 5) abort();
+            T.fijkPacked[f * 27 + q] = (unsigned short)(bc | rots << 8);
+        }
+    for (int b = 0; b < 122; b++) {
+        const int *d = H3T_baseCellData[b];
+        if (d[5] < -1 || d[5] > 19 || d[6] < -1 || d[6] > 19) abort();
+        T.bcdPacked[b] = (d[4] ? 1u : 0u) | (unsigned)(d[5] + 1) << 8 | (unsigned)(d[6] + 1) << 16;
+    }
     memcpy(T.faceNeighbors, H3T_faceNeighbors, sizeof(T.faceNeighbors));
     for (int a = 0; a < 49; a++)
         for (int b = 0; b < 49; b++) {

@@ -87,11 +87,11 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     __shared__ long long tmax_l[IG_THREADS];      // per-thread max ts (an LDS max per row instead of 2 live registers)
     for (int k = threadIdx.x; k < 60; k += IG_THREADS) (&Fc[0][0])[k] = (&c_tab.faceCenterPoint[0][0])[k];
     for (int k = threadIdx.x; k < 120; k += IG_THREADS) (&Fu[0][0][0])[k] = (&c_tab.fastU[res & 1][0][0][0])[k];
-    // _faceIjkToH3's base-cell and digit tables in LDS (17.4 KB): from __constant__ memory they were lane-indexed vector loads
+    // _faceIjkToH3's packed base-cell and digit tables in LDS (11.2 KB): from __constant__ memory they were lane-indexed vector loads
     // at the end of every cell, each with a full wait that also waited for the next round's prefetched columns
     __shared__ H3BaseTables BT;
-    for (int k = threadIdx.x; k < 20 * 27 * 2; k += IG_THREADS) (&BT.faceIjkBaseCells[0][0][0][0][0])[k] = (&c_tab.faceIjkBaseCells[0][0][0][0][0])[k];
-    for (int k = threadIdx.x; k < 122 * 7; k += IG_THREADS) (&BT.baseCellData[0][0])[k] = (&c_tab.baseCellData[0][0])[k];
+    for (int k = threadIdx.x; k < 20 * 27; k += IG_THREADS) BT.fijkPacked[k] = c_tab.fijkPacked[k];
+    for (int k = threadIdx.x; k < 122; k += IG_THREADS) BT.bcdPacked[k] = c_tab.bcdPacked[k];
     for (int k = threadIdx.x; k < AP7_QUAD; k += IG_THREADS) BT.ap7Quad[k] = c_tab.ap7Quad[k];
     for (int k = threadIdx.x; k < AP7_PAIR; k += IG_THREADS) BT.ap7Pair[k] = c_tab.ap7Pair[k];
     wc_init(WC);

@@ -40,8 +40,8 @@ struct Lds {
 __device__ void lds_load(Lds &L) {
     for (int k = threadIdx.x; k < 60; k += IG_THREADS) (&L.Fc[0][0])[k] = (&c_tab.faceCenterPoint[0][0])[k];
     for (int k = threadIdx.x; k < 120; k += IG_THREADS) (&L.Fu[0][0][0])[k] = (&c_tab.fastU[RES & 1][0][0][0])[k];
-    for (int k = threadIdx.x; k < 20 * 27 * 2; k += IG_THREADS) (&L.BT.faceIjkBaseCells[0][0][0][0][0])[k] = (&c_tab.faceIjkBaseCells[0][0][0][0][0])[k];
-    for (int k = threadIdx.x; k < 122 * 7; k += IG_THREADS) (&L.BT.baseCellData[0][0])[k] = (&c_tab.baseCellData[0][0])[k];
+    for (int k = threadIdx.x; k < 20 * 27; k += IG_THREADS) L.BT.fijkPacked[k] = c_tab.fijkPacked[k];
+    for (int k = threadIdx.x; k < 122; k += IG_THREADS) L.BT.bcdPacked[k] = c_tab.bcdPacked[k];
     for (int k = threadIdx.x; k < AP7_QUAD; k += IG_THREADS) L.BT.ap7Quad[k] = c_tab.ap7Quad[k];
     for (int k = threadIdx.x; k < AP7_PAIR; k += IG_THREADS) L.BT.ap7Pair[k] = c_tab.ap7Pair[k];
     __syncthreads();
