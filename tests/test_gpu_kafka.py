@@ -218,13 +218,10 @@ def test_splice_unsupported_records_into_device_batch():
     assert lib.hm_decode_json(eng._ctx, jin, jout) == _lib.HM_E_UNSUPPORTED and jout.n_unsupported == len(odd) - 1
     # hm_json_patch's argument checks: rows outside the batch, codes outside the dictionaries, dictionaries that shrink
     kb = eng.decode_json(buf, offs)
-    one = lambda v, t: np.array([v], t)   # noqa: E731
     def patch(row, pcode, np_, nv):
-        return lib.hm_json_patch(eng._ctx, 1, one(row, np.int64).ctypes.data, one(1.0, np.float64).ctypes.data,
-                                 one(2.0, np.float64).ctypes.data, one(0, np.int64).ctypes.data,
-                                 one(0.0, np.float64).ctypes.data, one(0, np.uint8).ctypes.data,
-                                 one(1, np.uint8).ctypes.data, one(pcode, np.int64).ctypes.data,
-                                 one(0, np.int64).ctypes.data, np_, nv)
+        a = [np.array([row], np.int64), np.array([1.0]), np.array([2.0]), np.array([0], np.int64), np.array([0.0]),
+             np.array([0], np.uint8), np.array([1], np.uint8), np.array([pcode], np.int64), np.array([0], np.int64)]
+        return lib.hm_json_patch(eng._ctx, 1, *[x.ctypes.data for x in a], np_, nv)   # (a keeps the arrays alive)
     n_p, n_v = kb.providers[0], kb.vehicles[0]
     assert patch(len(vals), 0, n_p, n_v) == _lib.HM_E_INVALID
     assert patch(0, n_p, n_p, n_v) == _lib.HM_E_INVALID
