@@ -8,7 +8,8 @@
 // list; a second kernel runs upstream's exact sequence (latLngToCellDeg, ~170 VGPRs) on that list only, so
 // the register footprint of the exact path never limits the occupancy of the streaming kernel.
 // =====================================================================================================
-// waves per SIMD for k_ingest: 6 (<= 80 VGPRs, no spills; 7 or 8 only lengthened the waits, profiles/r3/r3ab15/)
+// waves per SIMD for k_ingest: 6 (<= 80 VGPRs, no spills; 7 or 8 spill and only lengthen the waits, profiles/r3/r3ab15/,
+// profiles/r4/r4wv/)
 #define HM_SNAP_ATTR __attribute__((amdgpu_waves_per_eu(6)))
 // standalone UDF: cells only (hm_latlng_to_cell); exceptions -> slow[]
 __global__ __launch_bounds__(256) void k_cells(const double *__restrict__ lat, const double *__restrict__ lon, int64_t n,
