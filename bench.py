@@ -152,7 +152,77 @@ def cpu_baseline(sample, res):
                               "sample": f"the same on 1 thread, {n1:,}-event batches: {dt1:.2f} s"}}
 
 
-def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, arena_bytes=0):
+def cpu_baseline_c1(reps=5):
+    """BASELINE.md section 2's mandatory C1 CPU baseline: configs[0]'s Boston batch (10,000 events, one per vehicle, res
+    8, crossing a 5-minute edge, 15% null speeds, 1% invalid rows; synth.c1_boston) through the oracle's C restatement of
+    the micro-batch (oracle/heatmap_cpu.c) on every host thread this job may use and on one, then the reference-form
+    UpdateOne ops of foreach_batch_func (stream.tile_ops / position_ops, heatmap_stream.py:159-235) built from its
+    output and BSON-encoded as pymongo sends them (the sink itself replaced, as the plan says).  1 warm-up + the median
+    of `reps`; each run a fresh stream (a new state), as the reference's first batch."""
+    from mobheat import stream, synth
+    from oracle.heatmap_cpu import CpuHeatmap
+    b = synth.c1_boston(seed=0)
+    n = b["lat"].size
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    cols = dict(provider=["mbta"] * n, vehicleId=[f"v{i:05d}" for i in range(n)], ts_us=b["ts_us"], lat=b["lat"],
+                lon=b["lon"])
+
+    def batch(th):
+        c = CpuHeatmap(h3_res=8, threads=th)
+        t = time.perf_counter()
+        r = c.process_batch(**b)
+        dt = time.perf_counter() - t
+        c.close()
+        return dt, r
+
+    def ops(r):
+        import bson
+        import pandas as pd
+        T = r["tiles"]
+        tiles = _Tiles(dict(T, window_end_us=T["window_start_us"] + 300_000_000))
+        t = time.perf_counter()
+        o = stream.tile_ops(tiles, city="ath", h3_res=8, ttl_min=45) + \
+            stream.position_ops({k: (pd.Series(v) if k in ("provider", "vehicleId") else v) for k, v in cols.items()},
+                                r["latest_rows"])
+        for op in o:   # the statement pymongo's bulk encodes for each UpdateOne
+            bson.encode({"q": op._filter, "u": op._doc, "multi": False, "upsert": True})
+        return time.perf_counter() - t, len(o)
+
+    out = {"config": "C1: 10,000 Boston events (synth.c1_boston seed 0), one micro-batch, H3 res 8", "events": n,
+           "protocol": f"1 warm-up + median of {reps}"}
+    for th in (threads, 1):
+        batch(th)
+        runs = [batch(th) for _ in range(reps)]
+        ts = sorted(x[0] for x in runs)
+        med = ts[len(ts) // 2]
+        out[f"restatement_{th}t"] = {"value": n / med, "unit": "events/s", "cores": th, "median_s": med,
+                                     "kind": "port", "tiles": int(runs[0][1]["tiles"]["cell"].size)}
+    r = runs[0][1]
+    ops(r)
+    ot = sorted(ops(r) for _ in range(reps))
+    med_ops = ot[len(ot) // 2][0]
+    out["foreach_ops_1t"] = {"median_s": med_ops, "ops": ot[0][1],
+                             "note": "the reference's per-row UpdateOne build + BSON encode (heatmap_stream.py:159-235)"}
+    one = out["restatement_1t"]["median_s"] + med_ops
+    out["value"] = n / one
+    out["unit"] = "events/s"
+    out["cores"] = 1
+    out["kind"] = "port"
+    out["sample"] = "C1 batch through the restatement on 1 thread + the reference-form ops, median of 5"
+    return out
+
+
+class _Tiles:
+    """tile_ops' view of a tiles dict (attribute access and len())."""
+
+    def __init__(self, d):
+        self.__dict__.update(d)
+
+    def __len__(self):
+        return len(self.cell)
+
+
+def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, arena_bytes=0, sharded=False):
     """Warmup + exactly K timed steps (barrier + synchronize on both sides, max over ranks); per-stage HIP-event
     times (the library's events on its own stream) and algorithmic bytes of the timed steps."""
     import mobheat
@@ -161,7 +231,7 @@ def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, ar
     data = gen_batch(n, total_steps, seed=seed, dev=dev, span_us=span_us, advance_us=advance_us)
     eng = mobheat.HeatmapEngine(h3_res=res, device=local, batch_capacity_hint=n, state_arena_bytes=arena_bytes,
                                 shard=(rank, world) if world > 1 else None)
-    sharded = ShardedHeatmap(LibStages(eng), dev) if world > 1 else None
+    sharded = ShardedHeatmap(LibStages(eng), dev) if (world > 1 or sharded) else None
 
     def step(s):
         ptrs = dict(n=n, lat=data["lat"].data_ptr(), lon=data["lon"].data_ptr(), ts_us=data["ts"][s].data_ptr(),
@@ -174,7 +244,7 @@ def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, ar
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     kt = {k: 0.0 for k in STAGES}
@@ -196,11 +266,11 @@ def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, ar
         for k, v in stage_bytes(n, counts, world).items():
             kb[k] += v
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist.is_initialized():
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -233,7 +303,14 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=12_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-state-leg", action="store_true", help="skip the 1-minute-advance state-read leg")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the multi-GPU stage path (mobheat.distributed over torch.distributed) even at --gpus 1: "
+                         "at N=1 the exchange is RCCL's all-to-all of a rank with itself (the N>1 code path on one GPU)")
+    ap.add_argument("--c1-baseline", action="store_true", help="only the C1 CPU baseline (BASELINE.md section 2)")
     args = ap.parse_args()
+    if args.c1_baseline:
+        print(json.dumps(cpu_baseline_c1()), flush=True)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -244,15 +321,22 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    sharded = world > 1 or args.sharded
+    if sharded:
         # RCCL ("nccl") over xGMI; MOBHEAT_DIST_BACKEND=gloo only to rehearse several ranks on one GPU (RCCL
-        # refuses two ranks on one device)
+        # refuses two ranks on one device).  A --sharded N=1 run started without torchrun rendezvouses by itself.
+        if "MASTER_ADDR" not in os.environ:
+            import socket
+            s = socket.socket()
+            s.bind(("127.0.0.1", 0))
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]), RANK="0", WORLD_SIZE="1")
+            s.close()
         backend = os.environ.get("MOBHEAT_DIST_BACKEND", "nccl")
         dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
 
     n = args.events
     K = args.steps
-    A = run_leg(args, n, args.res, SPAN_US, SPAN_US, 1 + 7919 * rank, dev, local, world, rank)
+    A = run_leg(args, n, args.res, SPAN_US, SPAN_US, 1 + 7919 * rank, dev, local, world, rank, sharded=sharded)
     elapsed, avg_ms, kb, c = A["elapsed"], A["kt"], A["kb"], A["counts"]
     ms_step = elapsed / K * 1e3
     # Roofline of the dominant stage by time, priced on HBM (the metric's "% HBM peak"), with the PMC-counted
@@ -300,8 +384,9 @@ def main():
                                f"15 min of event time (3 windows) per step, advancing 15 min per step; H3 res {args.res}",
                    "events_per_step_per_gpu": n, "h3_res": args.res, "parallelism": f"dp{world}",
                    # the process group the exchange ran on, as torch.distributed reports it (None: one GPU, no exchange)
-                   "dist_backend": dist.get_backend() if world > 1 else None,
-                   "dist_world_size": dist.get_world_size() if world > 1 else 1,
+                   "dist_backend": dist.get_backend() if dist.is_initialized() else None,
+                   "dist_world_size": dist.get_world_size() if dist.is_initialized() else 1,
+                   "stage_path": sharded,
                    "binned_in_ingest": bool(c.get("binned")),
                    "tiles_emitted_last_step": c["tiles"], "partials_last_step": c["partials"],
                    "records_sent_last_step": c["sent"],
@@ -310,7 +395,7 @@ def main():
         "slowest_step": slowest_step(A),
     }
     B = None
-    if world == 1 and not args.no_state_leg:
+    if world == 1 and not sharded and not args.no_state_leg:
         # second leg: the state-read regime of the reference's ~2-s trigger (README.md:134-135) -- each micro-batch
         # holds 1 minute of event time and the stream advances 1 minute per step, so consecutive batches update the
         # same open windows and the merge reads existing state lines.  res 7 (configs[1]'s resolution): 1e8 events
@@ -330,14 +415,15 @@ def main():
             "tiles_last_step": B["counts"]["tiles"], "state_keys_created_last_step": B["counts"]["state_new"],
             "step_frac": bb / (bms * 1e-3) / 1e9 / HBM_PEAK_GBS, "step_s8d": s8d(n, B["counts"], bms),
             "slowest_step": slowest_step(B)}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not sharded and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_sample, args.res)
+        out["cpu_baseline"]["c1"] = cpu_baseline_c1()
     if rank == 0:
         print("per-step ms (host wall, rank 0): " + " ".join(f"{x:.1f}" for x in A["step_ms"]), file=sys.stderr, flush=True)
         if B is not None:
             print("state-read leg per-step ms: " + " ".join(f"{x:.1f}" for x in B["step_ms"]), file=sys.stderr, flush=True)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

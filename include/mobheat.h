@@ -190,6 +190,11 @@ int hm_stage_merge(hm_ctx *ctx, const void *recv_buf, const int64_t *recv_bytes,
                    void *winner_send_buf, int64_t winner_send_cap, int64_t *winner_send_counts);
 int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_recv, int32_t out_memory,
                     hm_batch_out *out);
+/* Orders the context's stream after the work queued so far on `stream` (a hipStream_t of the caller: the stream its
+ * collective ran on, e.g. torch's current stream after RCCL's all_to_all): an event recorded there and waited for on
+ * the library's stream, so that the next stage reads the received buffer without a host synchronization.  NULL = the
+ * legacy default stream. */
+int hm_stream_wait(hm_ctx *ctx, void *stream);
 
 /* device helpers for the caller's exchange buffers */
 int hm_device_memory(int32_t device, int64_t *free_bytes, int64_t *total_bytes);   /* (sizes a state arena) */

@@ -215,6 +215,7 @@ void hm_destroy(hm_ctx *ctx) {
     for (auto &e : ctx->side_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->winfo_ev) (void)hipEventDestroy(ctx->winfo_ev);
+    if (ctx->ext_ev) (void)hipEventDestroy(ctx->ext_ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

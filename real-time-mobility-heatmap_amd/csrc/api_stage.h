@@ -466,3 +466,14 @@ int hm_stage_finish(hm_ctx *ctx, const void *winner_recv_dev, int64_t n_winner_r
     ctx->stage = 0;
     return HM_OK;
 }
+
+// the caller's collective stream -> the library's stream, without a host synchronization (distributed.py: RCCL's
+// all_to_all of the chunks on torch's current stream, then hm_stage_merge / hm_stage_finish reading what it received)
+int hm_stream_wait(hm_ctx *ctx, void *stream) {
+    if (!ctx) return HM_E_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (!ctx->ext_ev) HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ext_ev, hipEventDisableTiming));
+    HIPCHK(ctx, hipEventRecord(ctx->ext_ev, (hipStream_t)stream));
+    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ext_ev, 0));
+    return 0;
+}

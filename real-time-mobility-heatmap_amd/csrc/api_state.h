@@ -106,6 +106,13 @@ int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *
         if (r.cell == 0 || r.reserved != 0 || r.count < 1 || r.n_speed < 0 || r.n_speed > r.count ||
             ((r.window_start_us % T) + T) % T != 0)
             return set_err(ctx, HM_E_INVALID, "state record %lld is malformed", (long long)i);
+        // a shard context's tables cover only its own region fields (range geometry): a foreign key would index
+        // below its table's first region
+        if (ctx->shard_count > 1 && tile_owner_of(tile_hash(r.cell, r.window_start_us), ctx->shard_count) != ctx->shard_rank)
+            return set_err(ctx, HM_E_INVALID, "state record %lld (cell %llx) belongs to rank %d, not to this shard %d of %d",
+                           (long long)i, (unsigned long long)r.cell,
+                           tile_owner_of(tile_hash(r.cell, r.window_start_us), ctx->shard_count), ctx->shard_rank,
+                           ctx->shard_count);
         const unsigned long long we = wenc_of(r.window_start_us);
         if (last >= wins.size() || wins[last].first != we) {
             last = 0;

@@ -131,6 +131,7 @@ struct hm_ctx {
     unsigned long long *d_wcount = nullptr, *h_wcount = nullptr; // aggregated rows per registry slot (census)
     WInfo *d_winfo = nullptr, *h_winfo = nullptr;   // per registry slot: window parameters of the direct path
     hipEvent_t winfo_ev = nullptr;                    // recorded after the last upload from h_winfo
+    hipEvent_t ext_ev = nullptr;                      // hm_stream_wait: recorded on the caller's stream
     DevBuf agg_bucket, agg_cursor;   // table mode: k_agg's buckets (AG_BINS x AG_SUB x cap AggRecs) + fill cursors
     unsigned agg_cap = 0;            // AggRecs per sub-bucket
     std::vector<unsigned long long> h_agg_cursor;

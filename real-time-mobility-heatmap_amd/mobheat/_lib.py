@@ -102,6 +102,7 @@ SIGNATURES = {
     "hm_stage_send": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_vp, _P(HmStageSizes)]),
     "hm_stage_merge": (c_i32, [c_vp, c_vp, c_vp, c_i32, _P(HmBatchOut), c_vp, c_i64, c_vp]),
     "hm_stage_finish": (c_i32, [c_vp, c_vp, c_i64, c_i32, _P(HmBatchOut)]),
+    "hm_stream_wait": (c_i32, [c_vp, c_vp]),
     "hm_device_memory": (c_i32, [c_i32, _P(c_i64), _P(c_i64)]),
     "hm_device_alloc": (c_i32, [c_i32, c_i64, _P(c_vp)]),
     "hm_device_free": (c_i32, [c_i32, c_vp]),

@@ -30,6 +30,7 @@ import numpy as np
 Entry = namedtuple("Entry", "epoch kind rank world path")
 _NAME = re.compile(r"^(state|delta)-(-?\d+)(?:\.r(\d+)of(\d+))?\.(?:mhs|npz)$")
 RestorePoint = namedtuple("RestorePoint", "epoch world lineage")
+LEGACY = "legacy"   # the lineage of files written before chains were recorded (no meta)
 
 
 def new_lineage():
@@ -66,9 +67,7 @@ class StateCheckpoints:
         world = self.world if world is None else world
         return os.path.join(self.root, f"{'state' if kind == 'full' else 'delta'}-{int(epoch)}.r{rank}of{world}.mhs")
 
-    def meta(self, e):
-        """The chain record of a file: lineage, base (its snapshot's epoch), prev (the file before it, -1 for a
-        snapshot).  Files without one (written before chains were recorded) read as their own one-file chain."""
+    def _raw_meta(self, e):
         key = (e.path, os.path.getmtime(e.path) if os.path.exists(e.path) else 0)
         if key not in self._meta_cache:
             from .engine import read_state_meta
@@ -77,10 +76,27 @@ class StateCheckpoints:
                 m = json.loads(raw) if raw is not None else None
             except (OSError, ValueError, KeyError, RuntimeError):
                 m = None
-            if m is None:
-                m = {"lineage": None, "base": e.epoch if e.kind == "full" else None, "prev": -1 if e.kind == "full" else None}
             self._meta_cache[key] = m
         return self._meta_cache[key]
+
+    def meta(self, e):
+        """The chain record of a file: lineage, base (its snapshot's epoch), prev (the file before it, -1 for a
+        snapshot).  Files without one -- the ``state-<E>.npz`` / ``delta-<E>.npz`` files of the version before chains
+        were recorded -- follow that version's rule: a legacy delta continues the legacy file of its rank just
+        before it, on the newest legacy snapshot before it, all in one lineage "legacy"; a stream restored from them
+        continues that lineage."""
+        m = self._raw_meta(e)
+        if m is not None:
+            return m
+        if e.kind == "full":
+            return {"lineage": LEGACY, "base": e.epoch, "prev": -1}
+        older = [x for x in self.scan() if x.rank == e.rank and x.world == e.world and x.epoch < e.epoch
+                 and self._raw_meta(x) is None]
+        if not older:
+            return {"lineage": LEGACY, "base": None, "prev": None}
+        prev = older[-1].epoch
+        fulls = [x.epoch for x in older if x.kind == "full"]
+        return {"lineage": LEGACY, "base": fulls[-1] if fulls else None, "prev": prev}
 
     # ---- chains ----
     def chain_to(self, rank, world, epoch, entries=None):

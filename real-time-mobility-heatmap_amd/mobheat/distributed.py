@@ -198,6 +198,12 @@ class LibStages:
                                       cap, wc), ctx, "hm_stage_merge")
         return out, Stream("winner", winner_send, list(wc), 8)
 
+    def wait_stream(self, stream):
+        """The library's stream waits for the work queued on `stream` (torch's current stream, where the collective
+        ran): hm_stream_wait, no host synchronization."""
+        ctx = self.engine._ctx
+        check(self.lib.hm_stream_wait(ctx, stream.cuda_stream), ctx, "hm_stream_wait")
+
     def finish(self, winner_recv, n_winner, out_memory, out):
         ctx = self.engine._ctx
         check(self.lib.hm_stage_finish(ctx, winner_recv.data_ptr(), n_winner, out_memory, ctypes.byref(out)), ctx,
@@ -221,9 +227,16 @@ class ShardedHeatmap:
         """One micro-batch on this rank.  A stage that raises on one rank makes every rank leave at the next
         collective (the failed rank re-raises its error, the others PeerFailed), so no rank waits on a collective its
         peers never reach."""
-        # the library reads the received buffers on its own stream: RCCL's (torch's current stream) must be done
-        sync = sync or (lambda: torch.cuda.current_stream(self.device).synchronize()
-                        if self.device.type == "cuda" else None)
+        # the library reads the received buffers on its own stream, after RCCL's (torch's current stream): an event
+        # wait between the two streams (the stages' wait_stream), not a host synchronization
+        if sync is None:
+            wait = getattr(self.stages, "wait_stream", None)
+            if self.device.type == "cuda" and wait is not None:
+                sync = lambda: wait(torch.cuda.current_stream(self.device))   # noqa: E731
+            elif self.device.type == "cuda":
+                sync = lambda: torch.cuda.current_stream(self.device).synchronize()   # noqa: E731
+            else:
+                sync = lambda: None   # noqa: E731
         err = None
         try:
             summary = self.stages.ingest(epoch, batch, self.world, self.rank)

@@ -16,8 +16,10 @@ Workers are started with a fresh spawn (never an exec of a process that touched 
      statement crosses the exchange; workers hand theirs back through shared memory;
   4. the driver writes them through the sink, tiles first, as the reference does (one connection per batch, unordered
      bulks of 1000);
-  5. after the writes succeeded (the batch is committed) every rank checkpoints its own state (mobheat.checkpoint:
-     per-rank chains; a restore into another GPU count re-partitions the keys by owner).
+  5. every rank checkpoints its own state (mobheat.checkpoint: per-rank chains; a restore into another GPU count
+     re-partitions the keys by owner) while the driver writes the statements -- before the writes are known to have
+     succeeded, which is safe: a restart re-runs the first uncommitted epoch E on the newest chain ending BEFORE E, and a
+     replay of E in this process rewrites E's files.
 
 A failure on any rank fails the batch (every rank leaves at the same collective, distributed.PeerFailed); a failure
 after a merge began resets every rank's state, which the replayed epoch restores from the checkpoints.
@@ -53,10 +55,13 @@ _DT = {"lat": np.float64, "lon": np.float64, "ts_us": np.int64, "speed": np.floa
 # ------------------ shared memory ------------------
 class ShmArena:
     """A growable POSIX shared-memory region holding named arrays (64-B aligned); put() returns the manifest a reader
-    maps them with (shm_views)."""
+    maps them with (shm_views).  A region replaced by a larger one is unlinked at once but stays mapped until
+    close_retired(): numpy views of it (the last batch's statements, ShardedStream.last) do not pin the mapping, so
+    closing it under them would leave them pointing at unmapped memory."""
 
     def __init__(self):
         self.shm = None
+        self._retired = []   # replaced regions, unlinked, still mapped
 
     def put(self, arrays):
         layout, off = [], 0
@@ -78,20 +83,39 @@ class ShmArena:
         old = self.shm
         self.shm = shared_memory.SharedMemory(create=True, size=int(nbytes + nbytes // 4 + (1 << 20)))
         if old is not None:
-            old.close()
-            old.unlink()
+            _unlink(old)
+            self._retired.append(old)
+
+    def close_retired(self):
+        """Unmap the replaced regions (the caller holds no view of them any more: a new batch began)."""
+        for r in self._retired:
+            _close(r)
+        self._retired = []
 
     def close(self):
+        self.close_retired()
         if self.shm is not None:
-            self.shm.close()
-            try:
-                self.shm.unlink()
-            except FileNotFoundError:
-                pass
+            _unlink(self.shm)
+            _close(self.shm)
             self.shm = None
 
 
+def _unlink(shm):
+    try:
+        shm.unlink()
+    except FileNotFoundError:
+        pass
+
+
+def _close(shm):
+    try:
+        shm.close()
+    except BufferError:   # (a buffer export still alive: the mapping goes with the object)
+        pass
+
+
 _ATTACHED = {}
+_DETACHED = []   # attachments to regions their writer replaced: still mapped until close_detached()
 
 
 def shm_views(name, layout, slot="in"):
@@ -101,11 +125,19 @@ def shm_views(name, layout, slot="in"):
     from multiprocessing import shared_memory
     cur = _ATTACHED.get(slot)   # (slot: the writer -- its previous region is gone once it grew into a new one)
     if cur is None or cur.name != name:
-        if cur is not None:
-            cur.close()
+        if cur is not None:   # (views of it may still be alive: unmapped by close_detached at the next batch)
+            _DETACHED.append(cur)
         cur = _ATTACHED[slot] = shared_memory.SharedMemory(name=name)
     shm = cur
     return {n: np.ndarray(shp, np.dtype(dt), buffer=shm.buf, offset=o) for n, dt, shp, o in layout}
+
+
+def close_detached():
+    """Unmap the attachments to replaced regions (no view of them is left: a new batch began)."""
+    global _DETACHED
+    for r in _DETACHED:
+        _close(r)
+    _DETACHED = []
 
 
 def dictionary_arrays(uniques):
@@ -162,6 +194,9 @@ class RankRunner:
         statements as the manifests of the rank's shared-memory regions (positions None when it holds no latest row)."""
         if self.engine is None:
             self._start(restore)
+        if self.rank:   # (a worker holds no view of its own replaced regions; rank 0's are dropped by the driver)
+            self.out_t.close_retired()
+            self.out_p.close_retired()
         eng = self.engine
         self.began = False
         v0 = eng.state_version()
@@ -345,6 +380,12 @@ class ShardedStream:
         """Run one micro-batch on every rank; returns the per-rank stats.  Raises (every rank's state reset when a merge
         may have begun) if any rank failed."""
         from .distributed import PeerFailed
+        # the last batch's statement views are dropped: the regions replaced since can be unmapped now
+        self.last = None
+        self.inputs.close_retired()
+        self.runner.out_t.close_retired()
+        self.runner.out_p.close_retired()
+        close_detached()
         n = int(cols["n"])
         arrays = {k: np.ascontiguousarray(cols[k] if cols.get(k) is not None else np.zeros(n), dtype=_DT[k]) for k in COLS}
         if cols.get("speed") is None:   # (no speed column: all null)
@@ -379,9 +420,15 @@ class ShardedStream:
                 self.reset()
             first = next((e for _, e in errs if not isinstance(e, PeerFailed) and "PeerFailed" not in str(e)), errs[0][1])
             raise first
-        per_rank = []
-        for r, (stats, tiles, pos) in enumerate([res0] + [m[1:4] for m in replies]):
-            per_rank.append((stats, self._views(r, tiles, "t"), self._views(r, pos, "p")))
+        try:
+            per_rank = []
+            for r, (stats, tiles, pos) in enumerate([res0] + [m[1:4] for m in replies]):
+                per_rank.append((stats, self._views(r, tiles, "t"), self._views(r, pos, "p")))
+        except BaseException:
+            # every rank merged the batch but its statements cannot be handed over: drop every rank's state, so that
+            # Spark's re-run of the epoch restores the state before it from the checkpoints instead of merging twice
+            self.reset()
+            raise
         self.last = per_rank
         return per_rank
 

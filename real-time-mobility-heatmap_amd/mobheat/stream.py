@@ -42,6 +42,9 @@ CHECKPOINT_DIR = os.getenv("CHECKPOINT", "/tmp/heatmap-checkpoint")
 # spawned workers the others; torch.distributed over RCCL, or MOBHEAT_DIST_BACKEND=gloo to rehearse on one GPU)
 N_GPUS = int(os.getenv("MOBHEAT_GPUS", "1"))
 DIST_BACKEND = os.getenv("MOBHEAT_DIST_BACKEND", "nccl")
+# MOBHEAT_SHARDED=1: the sharded writer even at one GPU (a process group of one rank over RCCL: the N>1 code path on a
+# one-GPU machine)
+FORCE_SHARDED = os.getenv("MOBHEAT_SHARDED", "0") == "1"
 STATE_CHECKPOINT = os.getenv("MOBHEAT_STATE_CHECKPOINT", "1") == "1"
 STATE_FULL_EVERY = int(os.getenv("MOBHEAT_STATE_FULL_EVERY", "10"))
 # The engine's window tables are carved from a zeroed reservation made at its creation (hm_config.state_arena_bytes)
@@ -167,7 +170,7 @@ def reset_engine():
         _SHARDED.reset()
 
 
-_SHARDED = None   # mobheat.sharded.ShardedStream when N_GPUS > 1
+_SHARDED = None   # mobheat.sharded.ShardedStream when N_GPUS > 1 (or FORCE_SHARDED)
 SHARDED_EXTRA = {}   # more ShardedStream config (the CPU tests: {"cpu": True, "runner": "module:Class"})
 
 
@@ -580,10 +583,18 @@ def _foreach_sharded(df, epoch):
         for _, _, pos in per_rank:
             if pos is not None:
                 _flush_statements(sink, "positions_latest", *pos)
-    finally:
+    except BaseException as write_err:
         sink.close()
         if STATE_CHECKPOINT:
-            sh.commit_end()
+            try:   # (the checkpoints must be finished before a replay; their own failure must not hide the sink's)
+                sh.commit_end()
+            except Exception as ck_err:
+                import warnings
+                warnings.warn(f"mobheat: checkpoint of epoch {epoch} failed after its writes failed: {ck_err!r}")
+        raise write_err
+    sink.close()
+    if STATE_CHECKPOINT:
+        sh.commit_end()
     _PENDING = None
     _LAST_EPOCH = epoch
     st = [x[0] for x in per_rank]
@@ -604,7 +615,7 @@ def foreach_batch_func(df, epoch_id: int):
     global _LAST_EPOCH, _PENDING, LAST_TIMINGS
     import time
     epoch = int(epoch_id)
-    if N_GPUS > 1:
+    if N_GPUS > 1 or FORCE_SHARDED:
         return _foreach_sharded(df, epoch)
     tm = {}
     clock = [time.perf_counter()]

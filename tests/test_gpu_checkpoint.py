@@ -272,3 +272,37 @@ def test_foreach_batch_func_failed_writes_without_checkpoints(monkeypatch):
     got = run([(0, False), (1, True), (1, True), (1, False), (2, False), (3, False)])
     stream.reset_engine()
     assert got == ref
+
+
+def test_shard_import_rejects_foreign_keys():
+    """a shard context (rank r of W: tables over its own region fields only) refuses to import a record that
+    another rank owns (distributed.tile_owner) -- its slot index would fall below the table -- and imports its own."""
+    import mobheat
+    from mobheat._lib import STATE_REC_DTYPE
+    from mobheat.distributed import tile_owner
+    W = 4
+    ws = (T0 // 300_000_000) * 300_000_000
+    cells = np.array([0x8828308281fffff + (k << 12) for k in range(64)], np.uint64)
+    own = tile_owner(cells, np.full(cells.size, ws, np.int64), W)
+    assert (own == 1).any() and (own != 1).any()
+    info = dict(epoch_id=3, n_keys=0, watermark_ms=0, prev_watermark_ms=0, tile_us=300_000_000,
+                watermark_delay_ms=600_000, h3_res=8)
+
+    def recs(sel):
+        r = np.zeros(int(sel.sum()), STATE_REC_DTYPE)
+        r["cell"], r["window_start_us"], r["count"], r["n_speed"] = cells[sel], ws, 2, 1
+        return r
+    eng = mobheat.HeatmapEngine(h3_res=8, device=0, shard=(1, W))
+    try:
+        with pytest.raises(RuntimeError, match="belongs to rank"):
+            eng.import_state(dict(info, n_keys=int(cells.size)), recs(np.ones(cells.size, bool)))
+    finally:
+        eng.close()
+    eng = mobheat.HeatmapEngine(h3_res=8, device=0, shard=(1, W))
+    try:
+        mine = recs(own == 1)
+        eng.import_state(dict(info, n_keys=mine.size), mine)
+        _, back = eng.export_state()
+        assert sorted(back["cell"].tolist()) == sorted(mine["cell"].tolist())
+    finally:
+        eng.close()

@@ -32,12 +32,13 @@ class Capture:
         pass
 
 
-def _frames(n_batches=3, n=3000, seed=2):
+def _frames(n_batches=3, n=3000, seed=2, grid=1 << 8):
+    """dyadic micro-batches: lat/lon on a `grid` x `grid` lattice of 1/1024-degree steps"""
     rng = np.random.default_rng(seed)
     out = []
     for b in range(n_batches):
-        lat = 42.0 + rng.integers(0, 1 << 8, n) / 1024.0
-        lon = -71.25 + rng.integers(0, 1 << 8, n) / 1024.0
+        lat = 42.0 + rng.integers(0, grid, n) / 1024.0
+        lon = -71.25 + rng.integers(0, grid, n) / 1024.0
         speed = pd.array(rng.integers(0, 160, n) * 0.5, dtype="Float64")
         speed[rng.random(n) < 0.1] = pd.NA
         ts = 1759572000 + b * 240 + rng.integers(0, 360, n)
@@ -104,3 +105,57 @@ def test_sharded_writer_world2_gloo(tmp_path, monkeypatch, oracle_h3):
     # (rank 0's checkpoints are recorded here; the worker's in its own process) one per epoch, written while the
     # statements go out -- epoch 2 twice: its first writes failed, and the replay checkpoints it again (the same state)
     assert OracleRunner.commits == [(0, 0), (0, 1), (0, 2), (0, 2)]
+
+
+def test_sharded_writer_growing_batches(tmp_path, monkeypatch, oracle_h3):
+    """Batches that outgrow the shared-memory regions (3k, then 40k rows, then 3k): the regions holding the ranks'
+    statements grow while the previous batch's views of them are still referenced (a region closed under
+    live views raised BufferError after every rank had merged), and every batch still writes the oracle's statements."""
+    frames = [_frames(n_batches=1, n=n, seed=sd, grid=1 << 12)[0] for n, sd in ((3000, 3), (40000, 4), (3000, 5))]
+    for b, f in enumerate(frames):   # (consecutive batches of one stream: 4 minutes apart)
+        f["eventTs"] = f["eventTs"] + pd.Timedelta(minutes=4 * b)
+    exp = _expected(frames)
+    monkeypatch.setattr(stream, "SINK_FACTORY", Capture)
+    monkeypatch.setattr(stream, "N_GPUS", 2)
+    monkeypatch.setattr(stream, "DIST_BACKEND", "gloo")
+    monkeypatch.setattr(stream, "STATE_CHECKPOINT", True)
+    monkeypatch.setattr(stream, "SHARDED_EXTRA", {"cpu": True, "runner": "sharded_fake:OracleRunner"})
+    stream.close_sharded()
+    Capture.log.clear()
+    try:
+        for e, f in enumerate(frames):
+            stream.foreach_batch_func(f, e)
+            # the views the driver kept for a replay read back exactly the statements it wrote
+            last = stream._SHARDED.last
+            assert sorted(bytes(b[o[k]:o[k + 1]]) for _, (b, o), _ in last for k in range(o.size - 1)) == \
+                sorted(Capture.log[-1]["tiles"])
+    finally:
+        stream.close_sharded()
+    written = [c for c in Capture.log if c["tiles"] or c["positions_latest"]]
+    assert len(written) == 3
+    for e in range(3):
+        for coll in ("tiles", "positions_latest"):
+            assert sorted(written[e][coll]) == exp[e][coll], (e, coll)
+    # (40k rows over a 4-degree box: ~10 MB of tile statements, past the 3k-row batch's regions and their 1 MiB slack)
+    assert len(exp[1]["tiles"]) > 30000 and len(exp[1]["tiles"]) > 10 * len(exp[0]["tiles"])
+
+
+def test_shm_arena_keeps_replaced_regions_mapped_until_released():
+    """ShmArena: a region replaced by a larger one stays mapped (the last batch's views read it) until close_retired;
+    its name is unlinked at once."""
+    from multiprocessing import shared_memory
+    from mobheat.sharded import ShmArena
+    a = ShmArena()
+    try:
+        name, lay = a.put({"x": np.arange(1000, dtype=np.int64)})
+        v = np.ndarray(lay[0][2], np.dtype(lay[0][1]), buffer=a.shm.buf, offset=lay[0][3])
+        a.put({"x": np.zeros(1 << 20, np.int64)})   # grows: a new region
+        assert a.shm.name != name and len(a._retired) == 1
+        assert int(v.sum()) == 499500                # the old view still reads the old region
+        with pytest.raises(FileNotFoundError):
+            shared_memory.SharedMemory(name=name)
+        del v
+        a.close_retired()
+        assert not a._retired
+    finally:
+        a.close()

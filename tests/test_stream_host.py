@@ -222,6 +222,61 @@ def test_state_checkpoint_files_and_resume_choice(tmp_path, monkeypatch):
     stream.reset_engine()
 
 
+def test_state_checkpoint_legacy_files_restore_and_continue(tmp_path, monkeypatch):
+    """CPU: checkpoint files in the naming and format of the version before chains were recorded
+    (``state-<E>.npz`` / ``delta-<E>.npz``, np.savez of info + recs, no chain record) are restored by that version's rule
+    -- the newest snapshot plus every delta after it, in epoch order -- not only from the last snapshot; the stream then
+    continues the same chain with the current format, and a restart resumes from the mixed chain."""
+    from mobheat import checkpoint as ck
+    from mobheat import engine as eng_mod
+    from mobheat._lib import STATE_REC_DTYPE
+    T = 300_000_000
+    w0 = 100 * T
+    info = dict(epoch_id=0, n_keys=0, watermark_ms=0, prev_watermark_ms=0, tile_us=T, watermark_delay_ms=600_000,
+                h3_res=8)
+    root = tmp_path / "mobheat-state"
+    root.mkdir()
+
+    def legacy(kind, epoch, keys):
+        r = np.zeros(len(keys), STATE_REC_DTYPE)
+        for k, (c, n) in enumerate(keys):
+            r[k]["cell"], r[k]["window_start_us"], r[k]["count"] = c, w0, n
+        inf = dict(info, epoch_id=epoch, n_keys=len(keys))
+        np.savez(str(root / f"{kind}-{epoch}.npz"), info=np.array([inf[f] for f in eng_mod._INFO_FIELDS], np.int64),
+                 recs=r)
+
+    legacy("state", 0, [(1, 1), (2, 1)])
+    legacy("delta", 1, [(2, 4)])
+    legacy("delta", 2, [(3, 1)])
+    legacy("state", 3, [(1, 1), (2, 4), (3, 1), (4, 2)])
+    legacy("delta", 4, [(4, 9)])
+    st = ck.StateCheckpoints(str(root))
+    got = {}
+    for before in (1, 2, 3, 4, 5, 9):
+        pt = st.restore_point(before)
+        _, recs = st.load(pt)
+        got[before] = (pt.epoch, pt.lineage, {int(r["cell"]): int(r["count"]) for r in recs})
+    assert got[1] == (0, ck.LEGACY, {1: 1, 2: 1})
+    assert got[2] == (1, ck.LEGACY, {1: 1, 2: 4})
+    assert got[3] == (2, ck.LEGACY, {1: 1, 2: 4, 3: 1})             # was: the snapshot of epoch 0 only
+    assert got[5][2] == got[9][2] == {1: 1, 2: 4, 3: 1, 4: 9}
+
+    class Eng:   # a state of {cell: count}; the batch of epoch 5 touched cell 5
+        def export_state(self):
+            raise AssertionError("the restored chain continues with a delta")
+
+        def export_state_delta(self):
+            r = np.zeros(1, STATE_REC_DTYPE)
+            r[0]["cell"], r[0]["window_start_us"], r[0]["count"] = 5, w0, 3
+            return dict(info, epoch_id=5, n_keys=1), r
+
+    pt = st.restore_point(5)
+    assert st.save(5, Eng(), pt.lineage, full_every=10) == "delta"
+    pt = st.restore_point(6)
+    _, recs = st.load(pt)
+    assert pt.epoch == 5 and {int(r["cell"]): int(r["count"]) for r in recs} == {1: 1, 2: 4, 3: 1, 4: 9, 5: 3}
+
+
 def test_state_checkpoint_chains_lineage_and_pruning(tmp_path, monkeypatch):
     """CPU: the checkpoint chains (mobheat.checkpoint).  (1) Saves with a snapshot every 2 deltas keep only
     the files from the second-newest snapshot on, and a restart before every epoch restores exactly the state after the
