@@ -367,6 +367,31 @@ int hm_json_patch(hm_ctx *ctx, int64_t m, const int64_t *rows, const double *lat
                   const int64_t *ts_us, const double *speed, const uint8_t *speed_valid, const uint8_t *row_valid,
                   const int64_t *pcode, const int64_t *vcode, int64_t n_providers, int64_t n_vehicles);
 
+/* ---- Arrow columns -> batch columns on the device (the boundary's Spark / Arrow / pandas frames; reference
+ * heatmap_stream.py:51-61,150) ----
+ * The micro-batch's columns in Arrow's memory layout, in host memory (zero-copy views of a pyarrow Table, of pyspark's
+ * collected Arrow batches or of a pandas frame converted to Arrow): the library copies them to the device and builds
+ * hm_batch_in there -- lat / lon null -> NaN (fails between(), :101-102), speedKmh null -> speed_valid 0, row_valid =
+ * provider, vehicleId and eventTs non-null (:99-103) -- and factorises provider and vehicleId with the exact device
+ * string dictionaries of hm_decode_json (vkey = provider_code * n_vehicles + vehicle_code; the dictionaries come back
+ * as Arrow offsets + UTF-8 bytes for hm_encode_position_updates).  Outputs as hm_decode_json (n_malformed and
+ * n_unsupported 0), valid until the next hm_decode_json / hm_arrow_columns on this context. */
+typedef struct hm_arrow_col {
+    const void *values;        /* float64 (lat, lon, speed) / int64 (ts_us, microseconds UTC) values, or a string column's
+                                  n + 1 offsets into data; NULL = the column is absent (every row null) */
+    const uint8_t *data;       /* string columns: the UTF-8 bytes the offsets point into */
+    const uint8_t *validity;   /* Arrow validity bitmap (bit validity_offset + i, least significant bit first); NULL =
+                                  no nulls */
+    int64_t validity_offset;
+    int32_t offset_bytes;      /* string columns: 4 (Arrow string) or 8 (large_string) */
+    int32_t reserved;
+} hm_arrow_col;
+typedef struct hm_arrow_in {
+    int64_t n;
+    hm_arrow_col lat, lon, speed, ts_us, provider, vehicle;
+} hm_arrow_in;
+int hm_arrow_columns(hm_ctx *ctx, const hm_arrow_in *in, hm_json_out *out);
+
 /* The distinct 900-s buckets floor(ts_s / 900) of the last hm_process_batch's latest rows, ascending (computed on
  * the device; *n = count, up to cap written): the buckets whose local offsets hm_encode_position_updates needs. */
 int hm_last_latest_buckets(hm_ctx *ctx, int64_t *bucket_ids, int64_t cap, int64_t *n);

@@ -211,6 +211,114 @@ int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out) {
     return HM_OK;
 }
 
+// ---- Arrow columns -> batch columns (the boundary's Arrow / Spark / pandas frames) ----
+// one column's host buffers -> device (values into dst, or the string offsets / bytes into the column's own buffers)
+static int arrow_upload(hm_ctx *ctx, const hm_arrow_col &c, int64_t n, size_t elem, void *dst, DevBuf &bits, DevBuf &offs,
+                        DevBuf &data, ArrowDevCol &d, bool is_string) {
+    memset(&d, 0, sizeof(d));
+    if (!c.values || n == 0) return HM_OK;
+    d.present = 1;
+    if (c.validity) {
+        if (c.validity_offset < 0) return set_err(ctx, HM_E_INVALID, "negative validity offset");
+        const int64_t b0 = c.validity_offset >> 3, nb = ((c.validity_offset & 7) + n + 7) >> 3;
+        int rc;
+        if ((rc = ensure(ctx, bits, (size_t)nb))) return rc;
+        HIPCHK(ctx, hipMemcpyAsync(bits.p, c.validity + b0, (size_t)nb, hipMemcpyHostToDevice, ctx->stream));
+        d.valid = (const uint8_t *)bits.p;
+        d.bit0 = (int16_t)(c.validity_offset & 7);
+    }
+    if (!is_string) {
+        HIPCHK(ctx, hipMemcpyAsync(dst, c.values, (size_t)n * elem, hipMemcpyHostToDevice, ctx->stream));
+        return HM_OK;
+    }
+    if (c.offset_bytes != 4 && c.offset_bytes != 8) return set_err(ctx, HM_E_INVALID, "string offsets of %d bytes", c.offset_bytes);
+    const int64_t o0 = c.offset_bytes == 4 ? ((const int32_t *)c.values)[0] : ((const int64_t *)c.values)[0];
+    const int64_t on = c.offset_bytes == 4 ? ((const int32_t *)c.values)[n] : ((const int64_t *)c.values)[n];
+    if (o0 < 0 || on < o0) return set_err(ctx, HM_E_INVALID, "bad string offsets");
+    if (on > o0 && !c.data) return set_err(ctx, HM_E_INVALID, "string column without bytes");
+    int rc;
+    if ((rc = ensure(ctx, offs, (size_t)(n + 1) * c.offset_bytes)) || (rc = ensure(ctx, data, (size_t)(on - o0) + 16))) return rc;
+    HIPCHK(ctx, hipMemcpyAsync(offs.p, c.values, (size_t)(n + 1) * c.offset_bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (on > o0) HIPCHK(ctx, hipMemcpyAsync(data.p, c.data + o0, (size_t)(on - o0), hipMemcpyHostToDevice, ctx->stream));
+    d.offs = offs.p;
+    d.base = o0;
+    d.offset_bytes = c.offset_bytes;
+    return HM_OK;
+}
+
+int hm_arrow_columns(hm_ctx *ctx, const hm_arrow_in *in, hm_json_out *out) {
+    if (!ctx || !in || !out || in->n < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    const int64_t n = in->n;
+    if (n > (int64_t)UINT32_MAX - 2) return set_err(ctx, HM_E_INVALID, "%lld rows exceed 2^32-2", (long long)n);
+    memset(out, 0, sizeof(*out));
+    ctx->jd_n = -1;   // (nothing to patch: hm_json_patch is the JSON decoder's)
+    ctx->jd_unsup.clear();
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc;
+    const size_t m = (size_t)std::max<int64_t>(n, 1);
+    if ((rc = ensure(ctx, ctx->jd_lat, m * 8)) || (rc = ensure(ctx, ctx->jd_lon, m * 8)) || (rc = ensure(ctx, ctx->jd_ts, m * 8)) ||
+        (rc = ensure(ctx, ctx->jd_speed, m * 8)) || (rc = ensure(ctx, ctx->jd_sv, m)) || (rc = ensure(ctx, ctx->jd_rv, m)) ||
+        (rc = ensure(ctx, ctx->jd_vkey, m * 8)) || (rc = ensure(ctx, ctx->jd_poff, m * 8)) || (rc = ensure(ctx, ctx->jd_plen, m * 4)) ||
+        (rc = ensure(ctx, ctx->jd_voff, m * 8)) || (rc = ensure(ctx, ctx->jd_vlen, m * 4)))
+        return rc;
+    ArrowDevCol dl, dn, ds, dt, dp, dv;
+    if ((rc = arrow_upload(ctx, in->lat, n, 8, ctx->jd_lat.p, ctx->ar_bits[0], ctx->ar_offs[0], ctx->ar_data[0], dl, false)) ||
+        (rc = arrow_upload(ctx, in->lon, n, 8, ctx->jd_lon.p, ctx->ar_bits[1], ctx->ar_offs[0], ctx->ar_data[0], dn, false)) ||
+        (rc = arrow_upload(ctx, in->speed, n, 8, ctx->jd_speed.p, ctx->ar_bits[2], ctx->ar_offs[0], ctx->ar_data[0], ds, false)) ||
+        (rc = arrow_upload(ctx, in->ts_us, n, 8, ctx->jd_ts.p, ctx->ar_bits[3], ctx->ar_offs[0], ctx->ar_data[0], dt, false)) ||
+        (rc = arrow_upload(ctx, in->provider, n, 0, nullptr, ctx->ar_bits[4], ctx->ar_offs[0], ctx->ar_data[0], dp, true)) ||
+        (rc = arrow_upload(ctx, in->vehicle, n, 0, nullptr, ctx->ar_bits[5], ctx->ar_offs[1], ctx->ar_data[1], dv, true)))
+        return rc;
+    if (n > 0) {
+        // (absent columns: every row null -- the prep kernel writes their values; nothing was copied)
+        unsigned long long *w = ctx->d_scratch + JSON_WORD;
+        HIPCHK(ctx, hipMemsetAsync(w, 0, 8, ctx->stream));
+        if (dp.present) hipLaunchKernelGGL(k_arrow_check_offsets, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, dp, n, w);
+        if (dv.present) hipLaunchKernelGGL(k_arrow_check_offsets, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, dv, n, w);
+        unsigned long long hb = 0;
+        HIPCHK(ctx, hipMemcpyAsync(&hb, w, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+        if (hb) return set_err(ctx, HM_E_INVALID, "%llu string offsets out of order", hb);
+        hipLaunchKernelGGL(k_arrow_prep, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, n, dl, dn, ds, dt, dp, dv,
+                           (double *)ctx->jd_lat.p, (double *)ctx->jd_lon.p, (double *)ctx->jd_speed.p, (uint8_t *)ctx->jd_sv.p,
+                           (int64_t *)ctx->jd_ts.p, (uint8_t *)ctx->jd_rv.p, (int64_t *)ctx->jd_poff.p, (int32_t *)ctx->jd_plen.p,
+                           (int64_t *)ctx->jd_voff.p, (int32_t *)ctx->jd_vlen.p);
+        HIPCHK(ctx, hipGetLastError());
+    }
+    if ((rc = dict_build(ctx, ctx->jd_prov, (const uint8_t *)ctx->ar_data[0].p, nullptr, (const int64_t *)ctx->jd_poff.p,
+                         (const int32_t *)ctx->jd_plen.p, n)) ||
+        (rc = dict_build(ctx, ctx->jd_veh, (const uint8_t *)ctx->ar_data[1].p, nullptr, (const int64_t *)ctx->jd_voff.p,
+                         (const int32_t *)ctx->jd_vlen.p, n)))
+        return rc;
+    const int64_t nv = std::max<int64_t>(ctx->jd_veh.n_codes, 1);
+    if (ctx->jd_prov.n_codes > 0 && (uint64_t)ctx->jd_prov.n_codes > (UINT64_MAX - 1) / (uint64_t)nv)
+        return set_err(ctx, HM_E_INVALID, "vkey space overflows");
+    if (n > 0)
+        hipLaunchKernelGGL(k_json_vkey, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, (const uint8_t *)ctx->jd_rv.p,
+                           (const unsigned *)ctx->jd_prov.slot_of.p, (const unsigned *)ctx->jd_veh.slot_of.p,
+                           (const unsigned *)ctx->jd_prov.code_of_slot.p, (const unsigned *)ctx->jd_veh.code_of_slot.p, n,
+                           (uint64_t)nv, (uint64_t *)ctx->jd_vkey.p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+    hm_batch_in &b = out->batch;
+    b.n = n;
+    b.memory = HM_MEM_DEVICE;
+    b.lat = (const double *)ctx->jd_lat.p;
+    b.lon = (const double *)ctx->jd_lon.p;
+    b.ts_us = (const int64_t *)ctx->jd_ts.p;
+    b.speed = (const double *)ctx->jd_speed.p;
+    b.speed_valid = (const uint8_t *)ctx->jd_sv.p;
+    b.vkey = (const uint64_t *)ctx->jd_vkey.p;
+    b.row_valid = (const uint8_t *)ctx->jd_rv.p;
+    out->n_providers = ctx->jd_prov.n_codes;
+    out->provider_offsets = (const int64_t *)ctx->jd_prov.h_off;
+    out->provider_bytes = (const uint8_t *)ctx->jd_prov.h_bytes;
+    out->n_vehicles = ctx->jd_veh.n_codes;
+    out->vehicle_offsets = (const int64_t *)ctx->jd_veh.h_off;
+    out->vehicle_bytes = (const uint8_t *)ctx->jd_veh.h_bytes;
+    return HM_OK;
+}
+
 int hm_json_patch(hm_ctx *ctx, int64_t m, const int64_t *rows, const double *lat, const double *lon, const int64_t *ts_us,
                   const double *speed, const uint8_t *speed_valid, const uint8_t *row_valid, const int64_t *pcode,
                   const int64_t *vcode, int64_t n_providers, int64_t n_vehicles) {

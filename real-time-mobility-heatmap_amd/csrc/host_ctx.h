@@ -118,6 +118,7 @@ struct hm_ctx {
     std::vector<int64_t> jd_unsup;      // the last hm_decode_json's unsupported rows (HM_JSON_SPLICE)
     int64_t jd_n = -1, jd_np = 0, jd_nv = 0;   // its row count (-1: none to patch) and dictionary sizes
     Dict jd_prov, jd_veh;
+    DevBuf ar_bits[6], ar_offs[2], ar_data[2];   // hm_arrow_columns: validity bitmaps, the string columns' offsets / bytes
     DevBuf lb_set, lb_list;   // hm_last_latest_buckets
     DevBuf keys;                     // k_ingest's event key per row (kernels.h ekey)
     // k_ingest's fused binning (large direct-path batches): the bins' cursors (RP_BINS + 1 u32: the last stays 0, so

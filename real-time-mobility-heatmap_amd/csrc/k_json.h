@@ -201,3 +201,69 @@ __global__ __launch_bounds__(256) void k_fill_i64(long long *p, int64_t n, long 
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
 }
+
+// hm_arrow_columns: Arrow nulls -> the batch columns' conventions (lat / lon NaN, speed_valid, row_valid), in place on the
+// values copied to the device; the string columns' spans (off into the column's bytes, len -1 = null) for dict_build
+struct ArrowDevCol {
+    const void *offs;         // string columns: n + 1 offsets (4 or 8 B), relative to data
+    const uint8_t *valid;     // validity bitmap bytes from bit 0 = row 0 (shifted copy), nullptr = no nulls
+    int64_t base;             // string columns: offs[0] (the bytes were copied from it)
+    int32_t offset_bytes;
+    int16_t present;          // 0: the column is absent (every row null)
+    int16_t bit0;             // row 0's bit in valid[0]
+};
+__device__ __forceinline__ bool arrow_valid(const ArrowDevCol &c, int64_t i) {
+    const int64_t j = i + c.bit0;
+    return c.present && (!c.valid || ((c.valid[j >> 3] >> (j & 7)) & 1));
+}
+__device__ __forceinline__ int64_t arrow_off(const ArrowDevCol &c, int64_t i) {
+    return (c.offset_bytes == 4 ? (int64_t)((const int32_t *)c.offs)[i] : ((const int64_t *)c.offs)[i]) - c.base;
+}
+// a string column's offsets: non-decreasing, every string shorter than 2^31 bytes
+__global__ __launch_bounds__(256) void k_arrow_check_offsets(ArrowDevCol c, int64_t n, unsigned long long *bad) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    unsigned long long b = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const int64_t d = arrow_off(c, i + 1) - arrow_off(c, i);
+        b += d < 0 || d > INT32_MAX;
+    }
+    b = wave_sum(b);
+    if (b && lane_id() == 0) atomicAdd(bad, b);
+}
+__global__ __launch_bounds__(256) void k_arrow_prep(int64_t n, ArrowDevCol lat_c, ArrowDevCol lon_c, ArrowDevCol sp_c,
+                                                    ArrowDevCol ts_c, ArrowDevCol pv_c, ArrowDevCol vh_c,
+                                                    double *__restrict__ lat, double *__restrict__ lon,
+                                                    double *__restrict__ speed, uint8_t *__restrict__ sv,
+                                                    int64_t *__restrict__ ts, uint8_t *__restrict__ rv,
+                                                    int64_t *__restrict__ poff, int32_t *__restrict__ plen,
+                                                    int64_t *__restrict__ voff, int32_t *__restrict__ vlen) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const double qnan = __builtin_nan("");
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (!arrow_valid(lat_c, i)) lat[i] = qnan;
+        if (!arrow_valid(lon_c, i)) lon[i] = qnan;
+        const bool s = arrow_valid(sp_c, i);
+        sv[i] = s;
+        if (!s) speed[i] = 0.0;
+        const bool t = arrow_valid(ts_c, i);
+        if (!t) ts[i] = 0;
+        const bool p = arrow_valid(pv_c, i), v = arrow_valid(vh_c, i);
+        if (p) {
+            const int64_t a = arrow_off(pv_c, i), b = arrow_off(pv_c, i + 1);
+            poff[i] = a;
+            plen[i] = (int32_t)(b - a);
+        } else {
+            poff[i] = 0;
+            plen[i] = -1;
+        }
+        if (v) {
+            const int64_t a = arrow_off(vh_c, i), b = arrow_off(vh_c, i + 1);
+            voff[i] = a;
+            vlen[i] = (int32_t)(b - a);
+        } else {
+            voff[i] = 0;
+            vlen[i] = -1;
+        }
+        rv[i] = p && v && t;
+    }
+}

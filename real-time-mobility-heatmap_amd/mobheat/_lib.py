@@ -63,6 +63,16 @@ class HmJsonOut(ctypes.Structure):
                 ("n_unsupported", c_i64), ("unsupported_rows", c_vp)]
 
 
+class HmArrowCol(ctypes.Structure):
+    _fields_ = [("values", c_vp), ("data", c_vp), ("validity", c_vp), ("validity_offset", c_i64), ("offset_bytes", c_i32),
+                ("reserved", c_i32)]
+
+
+class HmArrowIn(ctypes.Structure):
+    _fields_ = [("n", c_i64), ("lat", HmArrowCol), ("lon", HmArrowCol), ("speed", HmArrowCol), ("ts_us", HmArrowCol),
+                ("provider", HmArrowCol), ("vehicle", HmArrowCol)]
+
+
 class HmStageSizes(ctypes.Structure):
     _fields_ = [("table_mode", c_i64), ("n_tile_records", c_i64), ("n_cands", c_i64), ("global_batch_max_event_ms", c_i64),
                 ("n_valid", c_i64), ("n_late", c_i64)]
@@ -127,6 +137,7 @@ SIGNATURES = {
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_last_counts": (c_i32, [c_vp, c_vp, c_i32]),
     "hm_decode_json": (c_i32, [c_vp, _P(HmJsonIn), _P(HmJsonOut)]),
+    "hm_arrow_columns": (c_i32, [c_vp, _P(HmArrowIn), _P(HmJsonOut)]),
     "hm_json_patch": (c_i32, [c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64]),
     "hm_latlng_to_cell_last_exact": (c_i64, [c_i32]),
     "hm_cells_to_boundary": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),

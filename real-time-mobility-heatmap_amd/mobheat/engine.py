@@ -11,8 +11,8 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import (HM_JSON_SPLICE, HM_MEM_DEVICE, HM_MEM_HOST, STATE_REC_DTYPE, HmBatchIn, HmBatchOut, HmConfig, HmJsonIn, HmJsonOut,
-                   HmStateInfo, check, ptr)
+from ._lib import (HM_JSON_SPLICE, HM_MEM_DEVICE, HM_MEM_HOST, STATE_REC_DTYPE, HmArrowIn, HmBatchIn, HmBatchOut, HmConfig,
+                   HmJsonIn, HmJsonOut, HmStateInfo, check, ptr)
 
 _INFO_FIELDS = [f for f, _ in HmStateInfo._fields_ if f != "reserved"]
 
@@ -157,17 +157,7 @@ class HeatmapEngine:
                        offsets=ptr(offs))
         jout = HmJsonOut()
         check(self._lib.hm_decode_json(self._ctx, ctypes.byref(jin), ctypes.byref(jout)), self._ctx, "hm_decode_json")
-
-        def dictionary(n, po, pb):
-            offs_ = np.ctypeslib.as_array(ctypes.cast(po, ctypes.POINTER(ctypes.c_int64)), shape=(n + 1,)).copy()
-            total = int(offs_[-1])
-            raw = (np.ctypeslib.as_array(ctypes.cast(pb, ctypes.POINTER(ctypes.c_uint8)), shape=(total,)).copy()
-                   if total else np.zeros(1, np.uint8))
-            return n, offs_, raw
-        kb = KafkaBatch(batch=jout.batch, providers=dictionary(int(jout.n_providers), jout.provider_offsets,
-                                                                jout.provider_bytes),
-                        vehicles=dictionary(int(jout.n_vehicles), jout.vehicle_offsets, jout.vehicle_bytes),
-                        n_malformed=int(jout.n_malformed))
+        kb = _device_batch(jout)
         m = int(jout.n_unsupported)
         if m:
             rows = np.ctypeslib.as_array(ctypes.cast(jout.unsupported_rows, ctypes.POINTER(ctypes.c_int64)),
@@ -196,6 +186,23 @@ class HeatmapEngine:
               self._ctx, "hm_json_patch")
         kb.n_malformed += int(sum(c["malformed"]))
         kb.n_spliced = int(m)
+
+    def arrow_columns(self, arrow_in):
+        """hm_arrow_columns: the micro-batch's Arrow columns (an HmArrowIn over host buffers the caller keeps alive,
+        stream.ArrowColumns) -> KafkaBatch: the batch columns on the device and the string dictionaries."""
+        jout = HmJsonOut()
+        check(self._lib.hm_arrow_columns(self._ctx, ctypes.byref(arrow_in), ctypes.byref(jout)), self._ctx,
+              "hm_arrow_columns")
+        return _device_batch(jout)
+
+    def process_arrow(self, epoch_id, arrow_in, copy=True, rows_on_device=False):
+        """arrow_columns + hm_process_batch on the device columns; (BatchResult, KafkaBatch)."""
+        kb = self.arrow_columns(arrow_in)
+        out = HmBatchOut()
+        mem = HM_MEM_DEVICE if rows_on_device else HM_MEM_HOST
+        check(self._lib.hm_process_batch(self._ctx, int(epoch_id), ctypes.byref(kb.batch), mem, ctypes.byref(out)),
+              self._ctx, "hm_process_batch")
+        return (self._result_counts(out) if rows_on_device else self._result_from_host(out, copy)), kb
 
     def process_kafka(self, epoch_id, values, offsets, copy=True, rows_on_device=False):
         """decode_json + hm_process_batch on the decoded device columns; (BatchResult, KafkaBatch)."""
@@ -364,6 +371,20 @@ class HeatmapEngine:
                            batch_max_event_ms=int(out.batch_max_event_ms), watermark_ms=int(out.watermark_ms),
                            late_watermark_ms=int(out.late_watermark_ms), n_partials=int(out.n_partials),
                            n_tiles=int(out.n_tiles), n_latest=int(out.n_latest))
+
+
+def _device_batch(jout):
+    """KafkaBatch of an HmJsonOut (hm_decode_json / hm_arrow_columns): the device columns and copies of the dictionaries
+    (the library's pinned buffers are reused by the next call)."""
+    def dictionary(n, po, pb):
+        offs_ = np.ctypeslib.as_array(ctypes.cast(po, ctypes.POINTER(ctypes.c_int64)), shape=(n + 1,)).copy()
+        total = int(offs_[-1])
+        raw = (np.ctypeslib.as_array(ctypes.cast(pb, ctypes.POINTER(ctypes.c_uint8)), shape=(total,)).copy()
+               if total else np.zeros(1, np.uint8))
+        return n, offs_, raw
+    return KafkaBatch(batch=jout.batch, providers=dictionary(int(jout.n_providers), jout.provider_offsets, jout.provider_bytes),
+                      vehicles=dictionary(int(jout.n_vehicles), jout.vehicle_offsets, jout.vehicle_bytes),
+                      n_malformed=int(jout.n_malformed))
 
 
 def _host_statements(pb, po, nd, copy):

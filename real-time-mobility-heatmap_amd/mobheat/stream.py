@@ -432,6 +432,103 @@ def batch_columns(df):
                 row_valid=row_valid, provider=prov, vehicleId=vid, provider_uniques=p_uni, vehicle_uniques=v_uni)
 
 
+class ArrowColumns:
+    """The micro-batch's columns as Arrow arrays (one chunk each) and the hm_arrow_in over their buffers (zero-copy):
+    hm_arrow_columns copies them to the device, turns Arrow's nulls into the batch columns' conventions and factorises
+    the provider / vehicleId strings there (engine.process_arrow).  The arrays are kept here: the struct points into
+    them."""
+
+    def __init__(self, t, n):
+        import pyarrow as pa
+        from ._lib import HmArrowIn
+        self.n = n
+        self.keep = []
+        a = HmArrowIn(n=n)
+        for field, name in (("lat", "lat"), ("lon", "lon"), ("speed", "speedKmh")):
+            self._numeric(getattr(a, field), t, name, pa.float64())
+        self._ts(a.ts_us, t)
+        self._string(a.provider, t, "provider")
+        self._string(a.vehicle, t, "vehicleId")
+        self.struct = a
+
+    @staticmethod
+    def _chunk(t, name):
+        import pyarrow as pa
+        if name not in t.column_names:
+            return None
+        c = t.column(name)
+        c = c.combine_chunks() if isinstance(c, pa.ChunkedArray) else c
+        if pa.types.is_dictionary(c.type):
+            c = c.dictionary_decode()
+        return None if pa.types.is_null(c.type) or c.null_count == len(c) else c
+
+    def _validity(self, col, arr):
+        b = arr.buffers()[0]
+        if b is not None and arr.null_count:
+            col.validity, col.validity_offset = b.address, arr.offset
+        self.keep.append(arr)
+
+    def _numeric(self, col, t, name, typ):
+        import pyarrow.compute as pc
+        arr = self._chunk(t, name)
+        if arr is None:
+            return
+        if arr.type != typ:
+            arr = pc.cast(arr, typ)
+        col.values = arr.buffers()[1].address + arr.offset * 8
+        self._validity(col, arr)
+
+    def _ts(self, col, t):
+        import pyarrow as pa
+        import pyarrow.compute as pc
+        arr = self._chunk(t, "eventTs") if "eventTs" in t.column_names else None
+        if arr is not None and pa.types.is_timestamp(arr.type):
+            if arr.type.unit != "us":
+                arr = pc.cast(arr, pa.timestamp("us", tz=arr.type.tz), safe=False)
+        elif arr is not None or "eventTs" not in t.column_names:
+            # raw ISO strings (to_timestamp, :92), or eventTs of another type: parsed / cast on the host
+            vals, valid = _event_ts_us(t)
+            arr = pa.array(vals, mask=~valid) if not valid.all() else pa.array(vals)
+        else:
+            return
+        col.values = arr.buffers()[1].address + arr.offset * 8
+        self._validity(col, arr)
+
+    def _string(self, col, t, name):
+        import pyarrow as pa
+        import pyarrow.compute as pc
+        arr = self._chunk(t, name)
+        if arr is None:
+            return
+        if not (pa.types.is_string(arr.type) or pa.types.is_large_string(arr.type)):
+            arr = pc.cast(arr, pa.string())
+        w = 8 if pa.types.is_large_string(arr.type) else 4
+        bufs = arr.buffers()
+        col.values = bufs[1].address + arr.offset * w
+        col.data = bufs[2].address if bufs[2] is not None else None
+        col.offset_bytes = w
+        self._validity(col, arr)
+
+
+def device_columns(df):
+    """The frame's columns for the device path (hm_arrow_columns): {"arrow": ArrowColumns, "n": n}, or batch_columns'
+    host columns when the frame is not columnar Arrow-convertible (MOBHEAT_COLUMNS=host pins the host path), or the raw
+    Kafka values ({"kafka": ...})."""
+    if os.getenv("MOBHEAT_COLUMNS", "device") == "host":
+        return batch_columns(df)
+    try:
+        t = _to_arrow(df)
+    except Exception:
+        return batch_columns(df)
+    if "value" in t.column_names:
+        return {"kafka": kafka_values(t), "n": t.num_rows}
+    import pyarrow as pa
+    try:
+        return {"arrow": ArrowColumns(t, t.num_rows), "n": t.num_rows}
+    except (pa.ArrowException, TypeError, ValueError):   # (a column Arrow cannot cast: the host path decides)
+        return batch_columns(t)
+
+
 # ------------------ document builders (reference :164-188 and :211-228) ------------------
 def _spark_datetime(us):
     # pyspark TimestampType.fromInternal: naive local time; the reference's '...Z' ids assume a UTC driver
@@ -519,6 +616,9 @@ def _flush_statements(sink, collection, buf, offs):
 def _process(eng, epoch_id, cols):
     """Merge the batch into the engine's state; (result, the string dictionaries of its vkeys)."""
     # (the tile and latest rows stay on the device: the statements are encoded there from them)
+    if "arrow" in cols:   # the frame's Arrow columns: nulls and the string dictionaries resolved on the GPU
+        res, kb = eng.process_arrow(epoch_id, cols["arrow"].struct, rows_on_device=True)
+        return res, (kb.providers, kb.vehicles)
     if "kafka" in cols:   # raw Kafka values: from_json + to_timestamp on the GPU (row f1; the records outside the
         # device decoder are decoded on the host and spliced in, engine.decode_json: one such record cannot stop the
         # stream, where Spark would replay the same offsets into the same failure)
@@ -629,7 +729,7 @@ def foreach_batch_func(df, epoch_id: int):
     else:
         if _PENDING is not None:   # another epoch while one is uncommitted: that merge never committed
             reset_engine()
-        cols = batch_columns(df)
+        cols = device_columns(df)
         lap("columns")
         eng = get_engine(epoch, cols.get("n"))
         lap("engine")

@@ -1,0 +1,113 @@
+"""GPU: hm_arrow_columns -- the boundary's frames (Spark's Arrow batches, Arrow tables, pandas frames) handed to the
+device as their Arrow buffers, nulls resolved and provider / vehicleId factorised there (reference
+heatmap_stream.py:51-61,96-106,150).  The device columns must give exactly what the host columns (stream.batch_columns)
+give: the same tiles and latest rows through the engine, and the same statements through foreach_batch_func (dyadic
+inputs: every fp64 sum exact, so no summation order shows)."""
+import ctypes
+
+import numpy as np
+import pandas as pd
+import pyarrow as pa
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _tiles(r):
+    t = r.tiles
+    return {(int(t.cell[k]), int(t.window_start_us[k])): (int(t.count[k]), float(t.avg_speed[k]), bool(t.speed_null[k]),
+                                                           float(t.avg_lat[k]), float(t.avg_lon[k]))
+            for k in range(len(t))}
+
+
+def _forms():
+    from spark_standin import spark_table
+    from test_spark_frame_host import spark_like_frames
+    out = []
+    for b, pdf in enumerate(spark_like_frames(n_batches=3, n=60_000, seed=31)):
+        t = spark_table(pdf)
+        out.append(("spark", t))
+        out.append(("sliced", pa.concat_tables([t.slice(7, 20_000), t.slice(20_007, 39_000)])))
+        out.append(("pandas", pdf))
+    return out
+
+
+def test_arrow_columns_equal_host_columns_through_the_engine():
+    import mobheat
+    from mobheat import stream
+    eng_a = mobheat.HeatmapEngine(h3_res=8, device=0)
+    eng_h = mobheat.HeatmapEngine(h3_res=8, device=0)
+    try:
+        for e, (form, df) in enumerate(_forms()):
+            cols = stream.device_columns(df)
+            assert "arrow" in cols, form
+            ra, kb = eng_a.process_arrow(e, cols["arrow"].struct)
+            h = stream.batch_columns(df)
+            rh = eng_h.process_batch(e, h["lat"], h["lon"], h["ts_us"], h["speed"], h["speed_valid"], h["vkey"],
+                                     h["row_valid"])
+            assert _tiles(ra) == _tiles(rh), (e, form)
+            np.testing.assert_array_equal(ra.latest_rows, rh.latest_rows)
+            assert (ra.n_valid, ra.n_late, ra.watermark_ms, ra.n_state) == (rh.n_valid, rh.n_late, rh.watermark_ms,
+                                                                            rh.n_state)
+            # the dictionaries hold exactly the strings of the rows
+            pn, po, pb = kb.providers
+            names = {bytes(pb[po[k]:po[k + 1]]).decode() for k in range(pn)}
+            assert names == set(x for x in h["provider_uniques"].to_pylist() if x is not None)
+            assert kb.vehicles[0] == len(h["vehicle_uniques"])
+            assert len(ra.tiles) > 1000
+    finally:
+        eng_a.close()
+        eng_h.close()
+
+
+def test_foreach_batch_func_device_columns_equal_host_columns(monkeypatch):
+    from mobheat import stream
+    from spark_standin import Spark35Frame
+    from test_spark_frame_host import spark_like_frames
+
+    class Capture:
+        log = []
+
+        def __init__(self):
+            self.cur = {"tiles": [], "positions_latest": []}
+            Capture.log.append(self.cur)
+
+        def update_raw(self, collection, statements):
+            self.cur[collection].extend(bytes(s.raw) for s in statements)
+
+        def close(self):
+            pass
+    frames = spark_like_frames(n_batches=3, n=80_000, seed=41)
+    monkeypatch.setattr(stream, "SINK_FACTORY", Capture)
+    out = {}
+    for mode in ("host", "device"):
+        monkeypatch.setenv("MOBHEAT_COLUMNS", mode)
+        stream.reset_engine()
+        Capture.log.clear()
+        for e, f in enumerate(frames):
+            stream.foreach_batch_func(Spark35Frame(f) if e % 2 else f, e)
+        out[mode] = [{k: sorted(v) for k, v in c.items()} for c in Capture.log]
+    stream.reset_engine()
+    assert out["host"] == out["device"]
+    assert all(len(c["tiles"]) > 1000 and len(c["positions_latest"]) > 100 for c in out["device"])
+
+
+def test_arrow_columns_rejects_bad_offsets():
+    import mobheat
+    from mobheat._lib import HmArrowIn
+    n = 4
+    offs = np.array([0, 3, 2, 5, 6], np.int32)   # not monotonic
+    data = np.frombuffer(b"abcdefgh", np.uint8).copy()
+    lat = np.zeros(n)
+    a = HmArrowIn(n=n)
+    a.lat.values = a.lon.values = lat.ctypes.data
+    a.vehicle.values, a.vehicle.data, a.vehicle.offset_bytes = offs.ctypes.data, data.ctypes.data, 4
+    eng = mobheat.HeatmapEngine(h3_res=8, device=0)
+    try:
+        with pytest.raises(RuntimeError, match="offsets out of order"):
+            eng.arrow_columns(a)
+        a.vehicle.offset_bytes = 3
+        with pytest.raises(RuntimeError, match="string offsets of 3 bytes"):
+            eng.arrow_columns(a)
+    finally:
+        eng.close()

@@ -46,7 +46,10 @@ def test_foreach_batch_func_on_spark_frames_matches_oracle(monkeypatch, oracle_h
 
 
 def test_foreach_batch_func_spark_frame_equals_pandas_frame(monkeypatch):
-    """a 400k-row batch (general, non-dyadic values): the Spark form writes the pandas form's statements"""
+    """a 400k-row batch (general, non-dyadic values): the Spark form writes the pandas form's statements -- positions
+    byte for byte, tiles as documents with averages within 1e-9 relative (the GPU sums a tile's rows in an order set by
+    the device's scheduling, so two runs of the same batch may differ in the last bits of a sum)"""
+    from test_gpu_sharded_stream import _same_docs
     import pandas as pd
     from mobheat import stream
     from spark_standin import Spark35Frame
@@ -67,5 +70,6 @@ def test_foreach_batch_func_spark_frame_equals_pandas_frame(monkeypatch):
         stream.foreach_batch_func(df, 0)
         out.append({k: sorted(v) for k, v in Capture.log[0].items()})
     stream.reset_engine()
-    assert out[0] == out[1]
+    assert out[0]["positions_latest"] == out[1]["positions_latest"]
+    _same_docs(out[1]["tiles"], out[0]["tiles"])
     assert len(out[0]["tiles"]) > 1000 and len(out[0]["positions_latest"]) > 10000

@@ -1,0 +1,203 @@
+// Round 5: where the cost of k_ingest<true>'s binned record writes comes from, and whether per-workgroup slot chunks
+// remove it.  1e8 32-B records (read sequentially from a source array, bin = a hash of the index) into 8192 bins:
+//   seq        record i -> slot i (the HBM write roofline of the same bytes)
+//   direct     a returned atomic on the bin's cursor per record, the record stored there (k_ingest<true> today)
+//   atomics    the same atomics, the records stored in order (the atomics' cost alone)
+//   pre        the direct pattern's scattered stores into slots reserved by an untimed pass (the stores' cost alone)
+//   xcdpre     slots reserved beforehand per (bin, XCD): each sub-slab written from one XCD, so a line's four records
+//              meet in that XCD's L2 (whether scattered stores that combine in L2 are cheap)
+//   chunk C    persistent 768-lane workgroups (2 per CU) keep, per bin, a chunk of C slots reserved with ONE atomic; a
+//              record takes the next slot of its workgroup's chunk with an LDS atomic (chunk full: the lane that finds it
+//              full reserves the next chunk, the others retry); unused slots of the last chunks written as holes
+//   chunkx C   chunk, with the chunks of a bin reserved per (bin, XCD) (sub-slabs per XCD: a chunk's lines meet in L2)
+// Build: hipcc --offload-arch=gfx950 -O3 -o bin_chunk bin_chunk.hip      Run: ./bin_chunk [n]
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+constexpr int BINS = 8192;
+
+__device__ __forceinline__ uint64_t mixh(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33; return x;
+}
+__device__ __forceinline__ unsigned bin_of(int64_t i) { return (unsigned)(mixh((uint64_t)i) >> 51); }   // 13 bits
+__device__ __forceinline__ unsigned xcc_id() { return __builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 7u; }
+
+__global__ __launch_bounds__(512) void k_seq(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n) {
+    for (int64_t j = (int64_t)blockIdx.x * 512 + threadIdx.x; j < 2 * n; j += (int64_t)gridDim.x * 512) dst[j] = src[j];
+}
+
+__global__ __launch_bounds__(256) void k_direct(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n,
+                                                unsigned *cur, unsigned cap) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const uint4 a = src[2 * i], b = src[2 * i + 1];
+        const unsigned s = bin_of(i);
+        const unsigned p = atomicAdd(&cur[s], 1u);
+        if (p < cap) {
+            dst[2 * ((int64_t)s * cap + p)] = a;
+            dst[2 * ((int64_t)s * cap + p) + 1] = b;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_atomics(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n,
+                                                 unsigned *cur) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const uint4 a = src[2 * i], b = src[2 * i + 1];
+        const unsigned p = atomicAdd(&cur[bin_of(i)], 1u);
+        dst[2 * i] = make_uint4(a.x, a.y, a.z, p);
+        dst[2 * i + 1] = b;
+    }
+}
+
+// slots for the pre-reserved patterns (untimed): sub = 1 -> per bin; 8 -> per (bin, XCD of the executing workgroup)
+__global__ __launch_bounds__(256) void k_slots(int64_t n, unsigned *cur, unsigned *slot, int sub) {
+    const unsigned x = sub > 1 ? xcc_id() : 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const unsigned s = bin_of(i) * sub + x;
+        slot[i] = atomicAdd(&cur[s], 1u);
+        slot[n + i] = s;
+    }
+}
+__global__ __launch_bounds__(256) void k_pre(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n,
+                                             const unsigned *__restrict__ slot, unsigned cap) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const uint4 a = src[2 * i], b = src[2 * i + 1];
+        const unsigned s = slot[n + i], p = slot[i];
+        if (p < cap) {
+            dst[2 * ((int64_t)s * cap + p)] = a;
+            dst[2 * ((int64_t)s * cap + p) + 1] = b;
+        }
+    }
+}
+
+// per-workgroup chunks: LDS word per (sub-)bin = chunk index << 16 | fill; fill == C: full (first finder reserves)
+constexpr int CW = 768;
+template <int C, bool XCD>
+__global__ __launch_bounds__(CW) void k_chunk(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n,
+                                              unsigned *chunks, unsigned cap_chunks, unsigned long long *holes) {
+    __shared__ unsigned st[BINS];
+    for (int b = threadIdx.x; b < BINS; b += CW) st[b] = (0xffffu << 16) | C;   // no chunk yet: "full"
+    __syncthreads();
+    const unsigned x = XCD ? xcc_id() : 0;
+    const int64_t stride = (int64_t)gridDim.x * CW;
+    for (int64_t base = (int64_t)blockIdx.x * CW; base < n; base += stride) {
+        const int64_t i = base + threadIdx.x;
+        if (i >= n) continue;
+        const uint4 a = src[2 * i], b = src[2 * i + 1];
+        const unsigned bin = bin_of(i);
+        const unsigned sb = XCD ? bin * 8 + x : bin;
+        unsigned slot = 0xffffffffu;
+        for (;;) {
+            const unsigned old = atomicAdd(&st[bin], 1u);
+            const unsigned f = old & 0xffffu;
+            if (f < C) { slot = (old >> 16) * C + f; break; }
+            if (f == C) {   // this lane reserves the next chunk
+                const unsigned c = atomicAdd(&chunks[sb], 1u);
+                __hip_atomic_store(&st[bin], (c << 16) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                slot = c * C;
+                break;
+            }
+            // another lane is reserving: wait for the chunk index to change, then retry
+            while ((__hip_atomic_load(&st[bin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 16) == (old >> 16))
+                __builtin_amdgcn_s_sleep(1);
+        }
+        if (slot / C < cap_chunks) {
+            const int64_t d = (int64_t)sb * cap_chunks * C + slot;
+            dst[2 * d] = a;
+            dst[2 * d + 1] = b;
+        }
+    }
+    __syncthreads();
+    // the unused slots of the last chunks: holes (key word 0)
+    unsigned long long h = 0;
+    for (int bin = threadIdx.x; bin < BINS; bin += CW) {
+        const unsigned s = st[bin], f = s & 0xffffu, c = s >> 16;
+        if (f < C && c < cap_chunks) {
+            const unsigned sb = XCD ? bin * 8 + x : bin;
+            for (unsigned k = f; k < C; k++) {
+                dst[2 * ((int64_t)sb * cap_chunks * C + c * C + k)] = make_uint4(0, 0, 0, 0);
+                h++;
+            }
+        }
+    }
+    atomicAdd(holes, h);
+}
+
+__global__ void k_fill(uint4 *p, int64_t n2) {
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < n2; j += (int64_t)gridDim.x * 256)
+        p[j] = make_uint4((unsigned)(mixh(j) & 0xffffffff) | 1u, 1u, 2u, 3u);
+}
+
+int main(int argc, char **argv) {
+    setvbuf(stdout, nullptr, _IOLBF, 0);
+    const int64_t n = argc > 1 ? atoll(argv[1]) : 100000000;
+    const char *only = argc > 2 ? argv[2] : "";   // run only the patterns whose name starts with this
+    const unsigned cap = (unsigned)(n / BINS + n / BINS / 4 + 256);
+    uint4 *src, *dst;
+    unsigned *cur, *slot;
+    unsigned long long *holes;
+    const size_t dst_bytes = (size_t)BINS * 48000 * 32;   // >= every pattern's slabs (chunk 16: cap + 1024 * 16 slots per bin)
+    CHK(hipMalloc(&src, n * 32));
+    CHK(hipMalloc(&dst, dst_bytes));
+    CHK(hipMalloc(&cur, BINS * 8 * 4));
+    CHK(hipMalloc(&slot, n * 8));
+    CHK(hipMalloc(&holes, 8));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, src, 2 * n);
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    auto timed = [&](auto launch) {
+        CHK(hipMemset(cur, 0, BINS * 8 * 4));
+        CHK(hipMemset(holes, 0, 8));
+        CHK(hipDeviceSynchronize());
+        CHK(hipEventRecord(a));
+        launch();
+        CHK(hipEventRecord(b));
+        CHK(hipEventSynchronize(b));
+        float ms = 0;
+        CHK(hipEventElapsedTime(&ms, a, b));
+        return ms;
+    };
+    const int grid = 256 * 16;
+    auto want = [&](const char *name) { return strncmp(name, only, strlen(only)) == 0; };
+    for (int rep = 0; rep < 2; rep++) {
+        if (want("seq")) printf("rep %d seq          %.3f ms\n", rep, timed([&] { hipLaunchKernelGGL(k_seq, dim3(8192), dim3(512), 0, 0, src, dst, n); }));
+        if (want("direct")) printf("rep %d direct       %.3f ms\n", rep,
+               timed([&] { hipLaunchKernelGGL(k_direct, dim3(grid), dim3(256), 0, 0, src, dst, n, cur, cap); }));
+        if (want("atomics")) printf("rep %d atomics      %.3f ms\n", rep,
+               timed([&] { hipLaunchKernelGGL(k_atomics, dim3(grid), dim3(256), 0, 0, src, dst, n, cur); }));
+        for (int sub : {1, 8}) {
+            if (!want(sub == 1 ? "pre" : "xcdpre")) continue;
+            CHK(hipMemset(cur, 0, BINS * 8 * 4));
+            hipLaunchKernelGGL(k_slots, dim3(grid), dim3(256), 0, 0, n, cur, slot, sub);
+            CHK(hipDeviceSynchronize());
+            const unsigned c = sub == 1 ? cap : cap / 8 * 2 + 512;
+            const float t = timed([&] { hipLaunchKernelGGL(k_pre, dim3(grid), dim3(256), 0, 0, src, dst, n, slot, c); });
+            printf("rep %d %s       %.3f ms\n", rep, sub == 1 ? "pre   " : "xcdpre", t);
+        }
+        auto chunk = [&](auto kern, const char *name, int C, bool xcd) {
+            if (!want(name)) return;
+            const unsigned capc = xcd ? (cap / 8 * 2 + 512) / C : (cap + 2 * 512 * C) / C;
+            const float t = timed([&] { hipLaunchKernelGGL(kern, dim3(512), dim3(CW), 0, 0, src, dst, n, cur, capc, holes); });
+            unsigned long long h = 0;
+            CHK(hipMemcpy(&h, holes, 8, hipMemcpyDeviceToHost));
+            unsigned hc[BINS * 8];
+            CHK(hipMemcpy(hc, cur, sizeof(hc), hipMemcpyDeviceToHost));
+            unsigned long long chunks = 0, mx = 0;
+            for (int k = 0; k < BINS * (xcd ? 8 : 1); k++) { chunks += hc[k]; mx = hc[k] > mx ? hc[k] : mx; }
+            printf("rep %d %s %2d     %.3f ms  (%llu chunk atomics, %llu holes = %.1f%%, max chunks/bin %llu of %u)\n", rep,
+                   name, C, t, chunks, h, 100.0 * h / n, mx, capc);
+        };
+        chunk(k_chunk<4, false>, "chunk ", 4, false);
+        chunk(k_chunk<8, false>, "chunk ", 8, false);
+        chunk(k_chunk<16, false>, "chunk ", 16, false);
+        chunk(k_chunk<4, true>, "chunkx", 4, true);
+        chunk(k_chunk<8, true>, "chunkx", 8, true);
+    }
+    return 0;
+}
