@@ -570,6 +570,7 @@ def test_failed_writes_and_replays_do_not_merge_twice(tmp_path, monkeypatch, che
       * an epoch the live engine already committed is re-run on the state of the epoch before it."""
     from mobheat import engine as eng_mod
     from mobheat._lib import STATE_REC_DTYPE
+    monkeypatch.setenv("MOBHEAT_COLUMNS", "host")   # (the fake engine takes host columns)
     created, merged = [], []
     mode = {"fail_write": False, "fail_before": False, "fail_during": False}
 
