@@ -201,6 +201,9 @@ int hm_device_memory(int32_t device, int64_t *free_bytes, int64_t *total_bytes);
 int hm_device_alloc(int32_t device, int64_t bytes, void **ptr);
 int hm_device_free(int32_t device, void *ptr);
 int hm_memcpy(void *dst, const void *src, int64_t bytes, int32_t kind); /* 0 H2D 1 D2H 2 D2D */
+/* page-locked host memory (the checkpoint's export buffer: a device-to-host copy into it runs at the link's rate) */
+int hm_host_alloc(int64_t bytes, void **ptr);
+int hm_host_free(void *ptr);
 
 /* Self-test entry (host-side execution of the device numerics; no GPU needed): evaluates the
  * extended-precision emulation used by the kernels, op codes as oracle_ld_ops(). */

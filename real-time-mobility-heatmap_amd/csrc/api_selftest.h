@@ -52,6 +52,11 @@ int hm_device_free(int32_t device, void *ptr) {
     if (hipSetDevice(device) != hipSuccess) return HM_E_HIP;
     return hipFree(ptr) == hipSuccess ? HM_OK : HM_E_HIP;
 }
+int hm_host_alloc(int64_t bytes, void **ptr) {
+    if (!ptr || bytes < 0) return HM_E_INVALID;
+    return hipHostMalloc(ptr, std::max<int64_t>(bytes, 16), hipHostMallocDefault) == hipSuccess ? HM_OK : HM_E_NOMEM;
+}
+int hm_host_free(void *ptr) { return hipHostFree(ptr) == hipSuccess ? HM_OK : HM_E_HIP; }
 int hm_memcpy(void *dst, const void *src, int64_t bytes, int32_t kind) {
     hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
     return hipMemcpy(dst, src, bytes, k) == hipSuccess ? HM_OK : HM_E_HIP;

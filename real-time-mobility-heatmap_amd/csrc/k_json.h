@@ -80,7 +80,10 @@ __global__ __launch_bounds__(256) void k_dict_insert(const uint8_t *__restrict__
             unsigned long long k = __hip_atomic_load(&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (k == DICT_EMPTY) k = atomicCAS(&tab[s].key, DICT_EMPTY, (unsigned long long)h);
             if (k == DICT_EMPTY || k == h) {
-                atomicMin(&tab[s].rep, (unsigned)i);
+                // (the representative only moves down: a row above it adds nothing -- a batch's one provider string
+                // would otherwise put every row's atomic on one address)
+                if ((unsigned)i < __hip_atomic_load(&tab[s].rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                    atomicMin(&tab[s].rep, (unsigned)i);
                 got = (unsigned)s;
                 break;
             }

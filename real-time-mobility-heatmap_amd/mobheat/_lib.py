@@ -116,6 +116,8 @@ SIGNATURES = {
     "hm_device_memory": (c_i32, [c_i32, _P(c_i64), _P(c_i64)]),
     "hm_device_alloc": (c_i32, [c_i32, c_i64, _P(c_vp)]),
     "hm_device_free": (c_i32, [c_i32, c_vp]),
+    "hm_host_alloc": (c_i32, [c_i64, _P(c_vp)]),
+    "hm_host_free": (c_i32, [c_vp]),
     "hm_memcpy": (c_i32, [c_vp, c_vp, c_i64, c_i32]),
     "hm_selftest_ld_ops": (c_i32, [c_vp, c_i64, c_i32, c_vp]),
     "hm_selftest_floor_div": (c_i32, [c_vp, c_i64, c_i64, c_vp]),

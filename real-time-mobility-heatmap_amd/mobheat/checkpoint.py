@@ -184,12 +184,14 @@ class StateCheckpoints:
             if c is not None and self.meta(c[-1])["lineage"] == lineage:
                 ch = c
             break
+        # (the records: a view of the engine's page-locked export buffer, valid until its next export -- the caller
+        # writes the file before the next batch: foreach_batch_func and the sharded writer wait for it)
         if ch is None or len(ch) - 1 >= int(full_every):
-            info, recs = engine.export_state()
+            info, recs = engine.export_state(reuse=True)
             meta = {"lineage": lineage, "base": epoch, "prev": -1, "rank": self.rank, "world": self.world}
             kind = "full"
         else:
-            info, recs = engine.export_state_delta()
+            info, recs = engine.export_state_delta(reuse=True)
             meta = {"lineage": lineage, "base": ch[0].epoch, "prev": ch[-1].epoch, "rank": self.rank,
                     "world": self.world}
             kind = "delta"

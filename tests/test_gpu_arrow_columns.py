@@ -14,9 +14,12 @@ pytestmark = pytest.mark.gpu
 
 
 def _tiles(r):
+    """{(cell, window): (count, avg speed bits, null, avg lat bits, avg lon bits)} (bit patterns: NaN averages compare)"""
     t = r.tiles
-    return {(int(t.cell[k]), int(t.window_start_us[k])): (int(t.count[k]), float(t.avg_speed[k]), bool(t.speed_null[k]),
-                                                           float(t.avg_lat[k]), float(t.avg_lon[k]))
+    b = lambda a: np.asarray(a, np.float64).view(np.uint64)   # noqa: E731
+    sp, la, lo = b(t.avg_speed), b(t.avg_lat), b(t.avg_lon)
+    return {(int(t.cell[k]), int(t.window_start_us[k])): (int(t.count[k]), int(sp[k]), bool(t.speed_null[k]), int(la[k]),
+                                                           int(lo[k]))
             for k in range(len(t))}
 
 

@@ -262,10 +262,10 @@ def test_state_checkpoint_legacy_files_restore_and_continue(tmp_path, monkeypatc
     assert got[5][2] == got[9][2] == {1: 1, 2: 4, 3: 1, 4: 9}
 
     class Eng:   # a state of {cell: count}; the batch of epoch 5 touched cell 5
-        def export_state(self):
+        def export_state(self, reuse=False):
             raise AssertionError("the restored chain continues with a delta")
 
-        def export_state_delta(self):
+        def export_state_delta(self, reuse=False):
             r = np.zeros(1, STATE_REC_DTYPE)
             r[0]["cell"], r[0]["window_start_us"], r[0]["count"] = 5, w0, 3
             return dict(info, epoch_id=5, n_keys=1), r
@@ -307,10 +307,10 @@ def test_state_checkpoint_chains_lineage_and_pruning(tmp_path, monkeypatch):
                 r[i]["cell"], r[i]["window_start_us"], r[i]["count"] = k, 0, self.state[k]
             return dict(self.info, n_keys=len(keys)), r
 
-        def export_state(self):
+        def export_state(self, reuse=False):
             return self._recs(self.state)
 
-        def export_state_delta(self):
+        def export_state_delta(self, reuse=False):
             return self._recs(self.touched)
 
     root = str(tmp_path / "st")
@@ -608,10 +608,10 @@ def test_failed_writes_and_replays_do_not_merge_twice(tmp_path, monkeypatch, che
             return dict(epoch_id=self.epochs[-1] if self.epochs and isinstance(self.epochs[-1], int) else -1, n_keys=0,
                         watermark_ms=0, prev_watermark_ms=0, tile_us=300_000_000, watermark_delay_ms=600_000, h3_res=8)
 
-        def export_state(self):
+        def export_state(self, reuse=False):
             return self._info(), np.zeros(0, STATE_REC_DTYPE)
 
-        def export_state_delta(self):
+        def export_state_delta(self, reuse=False):
             return self._info(), np.zeros(0, STATE_REC_DTYPE)
 
         def close(self):

@@ -107,9 +107,19 @@ def foreach_mode(a):
                    "over TCP to a loopback server that acknowledges each / into a null sink; median of the timed "
                    "batches (each batch advances 1 minute: windows re-touched, one evicted every 5 batches)",
            "checkpoint": stream.STATE_CHECKPOINT, "state_arena": stream.STATE_ARENA}
-    cases = [("c1", synth.c1_boston(seed=0), "wire"), ("uniform", None, "wire"), ("uniform", None, "null")]
-    for name, b, sink_kind in cases:
-        name = f"{name}_{sink_kind}_sink"
+    import os
+    import pyarrow as pa
+    # (form: the frame handed over -- pandas, or the Arrow table pyspark's collection gives (Spark's types); columns:
+    # MOBHEAT_COLUMNS, the device column path (hm_arrow_columns) or the host one (batch_columns))
+    cases = [("c1", synth.c1_boston(seed=0), "wire", "pandas", "device"), ("uniform", None, "wire", "pandas", "device"),
+             ("uniform", None, "null", "pandas", "device"), ("uniform", None, "null", "arrow", "device"),
+             ("uniform", None, "wire", "arrow", "device"), ("uniform", None, "null", "pandas", "host"),
+             ("uniform", None, "null", "arrow", "host")]
+    if a.cases:
+        cases = [c for c in cases if f"{c[0]}_{c[2]}_{c[3]}_{c[4]}" in a.cases.split(",")]
+    for name, b, sink_kind, form, columns in cases:
+        name = f"{name}_{sink_kind}_sink_{form}_{columns}"
+        os.environ["MOBHEAT_COLUMNS"] = columns
         stream.SINK_FACTORY = NullSink if sink_kind == "null" else stream.MongoSink
         n = 10_000 if b is not None and name.startswith("c1") else a.events
         if b is None:
@@ -123,9 +133,16 @@ def foreach_mode(a):
         vids = pd.Series(b["vkey"]).map("v{:05d}".format)
         frames = []
         for s in range(a.steps + 1):
-            df = pd.DataFrame({"provider": "mbta", "vehicleId": vids,
-                               "lat": b["lat"], "lon": b["lon"], "speedKmh": pd.Series(sp).astype(object).where(b["speed_valid"], None),
-                               "eventTs": pd.to_datetime(b["ts_us"] + s * 60_000_000, unit="us")})
+            if form == "arrow":   # Spark's Arrow types: strings, nullable doubles, timestamp[us, tz=UTC]
+                df = pa.table({"provider": pa.array(np.full(n, "mbta", object), pa.string()),
+                               "vehicleId": pa.array(vids.to_numpy(), pa.string()),
+                               "lat": pa.array(b["lat"]), "lon": pa.array(b["lon"]),
+                               "speedKmh": pa.array(b["speed"].astype(float), mask=~np.asarray(b["speed_valid"], bool)),
+                               "eventTs": pa.array(b["ts_us"] + s * 60_000_000, pa.timestamp("us", tz="UTC"))})
+            else:
+                df = pd.DataFrame({"provider": "mbta", "vehicleId": vids,
+                                   "lat": b["lat"], "lon": b["lon"], "speedKmh": pd.Series(sp).astype(object).where(b["speed_valid"], None),
+                                   "eventTs": pd.to_datetime(b["ts_us"] + s * 60_000_000, unit="us")})
             frames.append(df)
         stream.reset_engine()
         import shutil
@@ -221,6 +238,7 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--foreach", action="store_true")
     ap.add_argument("--kafka", action="store_true")
+    ap.add_argument("--cases", default="", help="--foreach: comma-separated case names (default: all)")
     a = ap.parse_args()
     if a.foreach:
         return foreach_mode(a)

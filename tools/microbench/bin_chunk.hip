@@ -91,20 +91,33 @@ __global__ __launch_bounds__(CW) void k_chunk(const uint4 *__restrict__ src, uin
         const uint4 a = src[2 * i], b = src[2 * i + 1];
         const unsigned bin = bin_of(i);
         const unsigned sb = XCD ? bin * 8 + x : bin;
+        // a wave-uniform loop: each round a lane still without a slot either takes the next slot of its bin's chunk
+        // (LDS atomic), or -- the one lane that finds the chunk exactly full -- reserves the next chunk and publishes it,
+        // or waits (one LDS read per round) until the chunk index changes; nobody spins inside a divergent branch
         unsigned slot = 0xffffffffu;
-        for (;;) {
-            const unsigned old = atomicAdd(&st[bin], 1u);
-            const unsigned f = old & 0xffffu;
-            if (f < C) { slot = (old >> 16) * C + f; break; }
-            if (f == C) {   // this lane reserves the next chunk
-                const unsigned c = atomicAdd(&chunks[sb], 1u);
-                __hip_atomic_store(&st[bin], (c << 16) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                slot = c * C;
-                break;
+        bool done = false, waiting = false;
+        unsigned seen = 0;
+        while (__ballot(!done)) {
+            if (!done) {
+                if (waiting) {
+                    waiting = (__hip_atomic_load(&st[bin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 16) == seen;
+                } else {
+                    const unsigned old = atomicAdd(&st[bin], 1u);
+                    const unsigned f = old & 0xffffu;
+                    if (f < C) {
+                        slot = (old >> 16) * C + f;
+                        done = true;
+                    } else if (f == C) {
+                        const unsigned c = atomicAdd(&chunks[sb], 1u);
+                        __hip_atomic_store(&st[bin], (c << 16) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        slot = c * C;
+                        done = true;
+                    } else {
+                        waiting = true;
+                        seen = old >> 16;
+                    }
+                }
             }
-            // another lane is reserving: wait for the chunk index to change, then retry
-            while ((__hip_atomic_load(&st[bin], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 16) == (old >> 16))
-                __builtin_amdgcn_s_sleep(1);
         }
         if (slot / C < cap_chunks) {
             const int64_t d = (int64_t)sb * cap_chunks * C + slot;
