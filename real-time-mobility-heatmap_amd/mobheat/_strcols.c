@@ -1,0 +1,101 @@
+/* pandas object columns of Python str -> Arrow string layout (n + 1 int64 offsets + UTF-8 bytes), for the boundary's
+ * device column path (mobheat.stream.ArrowColumns -> hm_arrow_columns; reference heatmap_stream.py:51-61,150: provider
+ * and vehicleId are StringType).  pyarrow's conversion of an object column visits every row under the GIL (~0.3 s per
+ * 1e7-row column, most of a pandas micro-batch's host time); here the compact-ASCII strings -- CPython keeps their
+ * bytes right after the object header -- are measured and copied by several threads with the GIL released, and the
+ * rest (None, non-ASCII str, other objects) are left to the caller.
+ *
+ * lengths(ptrs, n, lens, threads): ptrs = the address of the object array's n PyObject pointers, lens = int64[n] out:
+ *   the byte length of a compact-ASCII str, -1 for None, -2 for anything else (the caller encodes or rejects it).
+ * copy(ptrs, n, offsets, data, threads): the bytes of every row with lens >= 0 to data[offsets[i], offsets[i+1]).
+ * The object array must stay alive (it holds the references) and unchanged during both calls. */
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <string.h>
+
+typedef struct {
+    PyObject *const *obj;
+    int64_t lo, hi;
+    int64_t *lens;
+    const int64_t *offs;
+    uint8_t *data;
+} Job;
+
+static int is_ascii_str(PyObject *o) {
+    return PyUnicode_Check(o) && PyUnicode_IS_READY(o) && PyUnicode_IS_COMPACT_ASCII(o);
+}
+
+static void *len_job(void *p) {
+    Job *j = (Job *)p;
+    for (int64_t i = j->lo; i < j->hi; i++) {
+        PyObject *o = j->obj[i];
+        j->lens[i] = o == Py_None ? -1 : is_ascii_str(o) ? (int64_t)PyUnicode_GET_LENGTH(o) : -2;
+    }
+    return NULL;
+}
+
+static void *copy_job(void *p) {
+    Job *j = (Job *)p;
+    for (int64_t i = j->lo; i < j->hi; i++) {
+        PyObject *o = j->obj[i];
+        const int64_t a = j->offs[i], b = j->offs[i + 1];
+        if (b > a && is_ascii_str(o) && PyUnicode_GET_LENGTH(o) == b - a) memcpy(j->data + a, PyUnicode_DATA(o), (size_t)(b - a));
+    }
+    return NULL;
+}
+
+static void run(void *(*fn)(void *), Job base, int64_t n, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 64) threads = 64;
+    if (n < 65536) threads = 1;
+    pthread_t th[64];
+    Job jobs[64];
+    int started[64] = {0};
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = base;
+        jobs[t].lo = n * t / threads;
+        jobs[t].hi = n * (t + 1) / threads;
+    }
+    for (int t = 1; t < threads; t++) {
+        started[t] = pthread_create(&th[t], NULL, fn, &jobs[t]) == 0;
+        if (!started[t]) fn(&jobs[t]);   /* (no thread: done here) */
+    }
+    fn(&jobs[0]);
+    for (int t = 1; t < threads; t++)
+        if (started[t]) pthread_join(th[t], NULL);
+}
+
+static PyObject *py_lengths(PyObject *self, PyObject *args) {
+    unsigned long long ptrs, lens;
+    long long n;
+    int threads;
+    if (!PyArg_ParseTuple(args, "KLKi", &ptrs, &n, &lens, &threads)) return NULL;
+    Job j = {(PyObject *const *)(uintptr_t)ptrs, 0, 0, (int64_t *)(uintptr_t)lens, NULL, NULL};
+    Py_BEGIN_ALLOW_THREADS
+    run(len_job, j, n, threads);
+    Py_END_ALLOW_THREADS
+    Py_RETURN_NONE;
+}
+
+static PyObject *py_copy(PyObject *self, PyObject *args) {
+    unsigned long long ptrs, offs, data;
+    long long n;
+    int threads;
+    if (!PyArg_ParseTuple(args, "KLKKi", &ptrs, &n, &offs, &data, &threads)) return NULL;
+    Job j = {(PyObject *const *)(uintptr_t)ptrs, 0, 0, NULL, (const int64_t *)(uintptr_t)offs, (uint8_t *)(uintptr_t)data};
+    Py_BEGIN_ALLOW_THREADS
+    run(copy_job, j, n, threads);
+    Py_END_ALLOW_THREADS
+    Py_RETURN_NONE;
+}
+
+static PyMethodDef methods[] = {
+    {"lengths", py_lengths, METH_VARARGS, "byte lengths of compact-ASCII str objects (-1 None, -2 other)"},
+    {"copy", py_copy, METH_VARARGS, "copy the compact-ASCII strings' bytes to their offsets"},
+    {NULL, NULL, 0, NULL}};
+
+static struct PyModuleDef mod = {PyModuleDef_HEAD_INIT, "_strcols", NULL, -1, methods};
+
+PyMODINIT_FUNC PyInit__strcols(void) { return PyModule_Create(&mod); }

@@ -510,16 +510,66 @@ class ArrowColumns:
         self._validity(col, arr)
 
 
+def _object_strings(values):
+    """A pandas object column of Python str -> pa.large_string array (None / NaN / pd.NA -> null): the compact-ASCII
+    strings measured and copied by _strcols' threads without the GIL, any other str encoded here.  None when the column
+    holds a non-string value (the caller converts it another way)."""
+    import pyarrow as pa
+    from . import _strcols
+    a = np.ascontiguousarray(values, dtype=object)
+    n = a.size
+    threads = min(16, os.cpu_count() or 1)
+    lens = np.empty(n, np.int64)
+    if n:
+        _strcols.lengths(a.ctypes.data, n, lens.ctypes.data, threads)
+    enc = {}
+    for i in np.nonzero(lens == -2)[0].tolist():
+        v = a[i]
+        if isinstance(v, str):
+            enc[i] = v.encode("utf-8", "surrogatepass")
+            lens[i] = len(enc[i])
+        elif isinstance(v, float) and v != v or v is getattr(__import__("pandas"), "NA", None):
+            lens[i] = -1
+        else:
+            return None
+    valid = lens >= 0
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(np.maximum(lens, 0), out=offs[1:])
+    data = np.empty(max(int(offs[-1]), 1), np.uint8)
+    if n:
+        _strcols.copy(a.ctypes.data, n, offs.ctypes.data, data.ctypes.data, threads)
+    for i, b in enc.items():
+        data[offs[i]:offs[i + 1]] = np.frombuffer(b, np.uint8)
+    nulls = int(n - valid.sum())
+    bitmap = pa.py_buffer(np.packbits(valid, bitorder="little")) if nulls else None
+    return pa.Array.from_buffers(pa.large_string(), n, [bitmap, pa.py_buffer(offs), pa.py_buffer(data)], null_count=nulls)
+
+
 def device_columns(df):
     """The frame's columns for the device path (hm_arrow_columns): {"arrow": ArrowColumns, "n": n}, or batch_columns'
     host columns when the frame is not columnar Arrow-convertible (MOBHEAT_COLUMNS=host pins the host path), or the raw
     Kafka values ({"kafka": ...})."""
     if os.getenv("MOBHEAT_COLUMNS", "device") == "host":
         return batch_columns(df)
+    strs = {}
+    if _is_pandas(df) and "value" not in df.columns:
+        # the pandas frame's string columns straight to Arrow's layout (_strcols: threads, no GIL), the rest by pyarrow
+        for c in ("provider", "vehicleId"):
+            if c in df.columns and df[c].dtype == object:
+                try:
+                    arr = _object_strings(df[c].to_numpy())
+                except ImportError:   # (the helper is not built: pyarrow converts the column)
+                    arr = None
+                if arr is not None:
+                    strs[c] = arr
+        if strs:
+            df = df.drop(columns=list(strs))
     try:
         t = _to_arrow(df)
     except Exception:
         return batch_columns(df)
+    for c, arr in strs.items():
+        t = t.append_column(c, arr) if t.num_columns else __import__("pyarrow").table({c: arr})
     if "value" in t.column_names:
         return {"kafka": kafka_values(t), "n": t.num_rows}
     import pyarrow as pa

@@ -121,3 +121,15 @@ def test_device_columns_host_switch_and_kafka(monkeypatch):
     monkeypatch.setenv("MOBHEAT_COLUMNS", "host")
     c = stream.device_columns(spark_like_frames(1, n=10)[0])
     assert "vkey" in c and "arrow" not in c
+
+
+def test_object_strings_to_arrow():
+    """_strcols (threads copying compact-ASCII str bytes) + the host's handling of the rest: equal to pyarrow's own
+    conversion, None / NaN / pd.NA null, non-ASCII encoded, a non-string value -> None (the caller's fallback)"""
+    vals = np.array(["mbta", None, "v0001", float("nan"), "vé", "", pd.NA, "x" * 300, "日本"] * 20000, dtype=object)
+    got = stream._object_strings(vals)
+    exp = pa.array([None if (v is None or v is pd.NA or (isinstance(v, float) and v != v)) else v for v in vals],
+                   pa.large_string())
+    assert got.equals(exp)
+    assert stream._object_strings(np.array(["a", 3, "b"], dtype=object)) is None
+    assert len(stream._object_strings(np.array([], dtype=object))) == 0
