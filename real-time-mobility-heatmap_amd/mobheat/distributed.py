@@ -19,6 +19,7 @@ Ownership is a pure function of the key, so the persistent state never moves bet
 are torch tensors handed to RCCL directly; the library writes/reads them through plain device pointers.
 """
 import ctypes
+import os
 from collections import namedtuple
 
 import numpy as np
@@ -93,30 +94,64 @@ def exchange(streams, device, status=0):
     return out
 
 
+# bytes of one (sender, receiver) pair moved per all_to_all round: a rank's share of a 1e8-event batch is ~3.2 GB of
+# records, and one all_to_all of it faulted the GPU (profiles/r5: hm_stage_merge saw the illegal access right after the
+# 3.2-GB all_to_all of a world-1 RCCL group, while 4.5M-row batches passed) -- the payload moves in rounds of at most this
+# per pair, each round's pieces received in place.  0 = one round.
+EXCHANGE_ROUND_BYTES = int(os.environ.get("MOBHEAT_EXCHANGE_ROUND_BYTES", str(1 << 30)))
+
+
 def exchange_chunks(buf, send_bytes, device, status=0):
-    """The batch's record exchange: one all_to_all of the per-destination chunk sizes in bytes (with this rank's
+    """The batch's record exchange: one all_gather of every rank's per-destination chunk sizes in bytes (with its
     status: a rank whose stage failed sends status != 0 and no chunks, and every rank raises PeerFailed before the
-    payloads move), then ONE all_to_all of the chunks, as 8-byte words (chunk sizes are multiples of 32; a rank's share
-    at 1e8 events per GPU is several GB, past 2^31 single-byte elements).  Returns (recv uint8 tensor, recv_bytes per
-    source rank)."""
-    world = dist.get_world_size()
-    sc = torch.tensor([[int(send_bytes[r]) if send_bytes else 0, status] for r in range(world)], dtype=torch.int64,
-                      device=device)
-    rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc)
-    rs = rc.cpu().tolist()
-    bad = [r for r in range(world) if rs[r][1]]
+    payloads move), then the chunks -- one all_to_all, or (a pair moving more than EXCHANGE_ROUND_BYTES) rounds of
+    all_to_all of at most that per pair, every piece received at its place -- as 8-byte words (chunk sizes are multiples
+    of 32).  Returns (recv uint8 tensor, recv_bytes per source rank)."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    row = torch.tensor([int(send_bytes[r]) if send_bytes else 0 for r in range(world)] + [status], dtype=torch.int64,
+                       device=device)
+    rows = [torch.empty_like(row) for _ in range(world)]
+    dist.all_gather(rows, row)
+    M = torch.stack(rows).cpu().tolist()   # M[s][r]: bytes s sends r; M[s][world]: s's status
+    bad = [r for r in range(world) if M[r][world]]
     if bad and status == 0:
         raise PeerFailed(f"rank(s) {bad} failed the batch's stage before the exchange")
     if status:
         return None, []
-    recv_bytes = [int(rs[r][0]) for r in range(world)]
+    recv_bytes = [int(M[s][rank]) for s in range(world)]
     assert all(b % 8 == 0 for b in recv_bytes) and all(int(b) % 8 == 0 for b in send_bytes)
     nrecv, nsend = sum(recv_bytes), int(sum(send_bytes))
     recv = torch.empty(max(nrecv // 8, 2), dtype=torch.int64, device=device)
-    dist.all_to_all_single(recv[: nrecv // 8], buf[:nsend].view(torch.int64), [b // 8 for b in recv_bytes],
-                           [int(b) // 8 for b in send_bytes])
+    words = buf[:nsend].view(torch.int64)
+    step = EXCHANGE_ROUND_BYTES // 8
+    biggest = max(max(r[:world]) for r in M) // 8
+    rounds = 1 if step <= 0 or biggest <= step else -(-biggest // step)
+    if rounds == 1:
+        dist.all_to_all_single(recv[: nrecv // 8], words, [b // 8 for b in recv_bytes], [int(b) // 8 for b in send_bytes])
+        return recv.view(torch.uint8), recv_bytes
+    s_off = [sum(int(b) for b in send_bytes[:r]) // 8 for r in range(world)]
+    r_off = [sum(recv_bytes[:s]) // 8 for s in range(world)]
+    for k in range(rounds):
+        a = k * step
+        ins = [words[s_off[r] + a: s_off[r] + a + max(0, min(step, int(send_bytes[r]) // 8 - a))] for r in range(world)]
+        outs = [recv[r_off[s] + a: r_off[s] + a + max(0, min(step, recv_bytes[s] // 8 - a))] for s in range(world)]
+        _all_to_all_views(outs, ins)
     return recv.view(torch.uint8), recv_bytes
+
+
+def _all_to_all_views(outs, ins):
+    """all_to_all of tensor views: RCCL takes the lists as they are (grouped send/recv); gloo has only the single-tensor
+    form, so the pieces go through one contiguous send and receive buffer there."""
+    if dist.get_backend() == "nccl":
+        dist.all_to_all(outs, ins)
+        return
+    send = torch.cat(ins) if ins else None
+    recv = torch.empty(sum(o.numel() for o in outs), dtype=outs[0].dtype, device=outs[0].device)
+    dist.all_to_all_single(recv, send, [o.numel() for o in outs], [i.numel() for i in ins])
+    k = 0
+    for o in outs:
+        o.copy_(recv[k: k + o.numel()])
+        k += o.numel()
 
 
 def global_window_registry(summaries, tile_us):

@@ -173,10 +173,13 @@ class OracleStages:
         return out
 
 
-def _worker(rank, world, port, batches, res, table, q):
+def _worker(rank, world, port, batches, res, table, q, round_bytes=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mobheat import distributed
     from mobheat.distributed import ShardedHeatmap
+    if round_bytes:   # (the payload exchanged in rounds of at most this many bytes per rank pair)
+        distributed.EXCHANGE_ROUND_BYTES = round_bytes
     sh = ShardedHeatmap(OracleStages(res, table=table), torch.device("cpu"))
     results = []
     for e, b in enumerate(batches):
@@ -199,8 +202,8 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("table", [False, True])
-def test_sharded_equals_single_shard(oracle_h3, table):
+@pytest.mark.parametrize("table,round_bytes", [(False, None), (True, None), (False, 4096)])
+def test_sharded_equals_single_shard(oracle_h3, table, round_bytes):
     from mobheat import synth
     from oracle.spark_oracle import SparkHeatmapOracle
     rng = np.random.default_rng(5)
@@ -219,7 +222,7 @@ def test_sharded_equals_single_shard(oracle_h3, table):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, batches, 8, table, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, batches, 8, table, q, round_bytes)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=300) for _ in range(world))

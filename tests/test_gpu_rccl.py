@@ -54,13 +54,16 @@ def _tiles(r):
             for k in range(len(t))}
 
 
-def _stage_worker(port, q):
+def _stage_worker(port, round_bytes, q):
     """ShardedHeatmap over RCCL at world 1 against HeatmapEngine.process_batch on the same batches."""
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         import torch
         import torch.distributed as dist
         import mobheat
+        from mobheat import distributed
+        if round_bytes:   # (the record exchange in rounds of at most this many bytes per rank pair: RCCL's list form)
+            distributed.EXCHANGE_ROUND_BYTES = round_bytes
         from mobheat._lib import HM_MEM_HOST
         from mobheat.distributed import LibStages, ShardedHeatmap
         dev = torch.device("cuda", 0)
@@ -176,10 +179,12 @@ def _spawn(target, *args, timeout=300):
     return m
 
 
-def test_sharded_heatmap_over_rccl_world1_equals_single_engine():
+@pytest.mark.parametrize("round_bytes", [0, 16 << 20])
+def test_sharded_heatmap_over_rccl_world1_equals_single_engine(round_bytes):
     """ShardedHeatmap (summaries all_gather, chunk all_to_all, owner merge, winners back) over RCCL: every batch's tiles
-    and latest rows equal the single-engine path's, including a 4.5M-row batch whose records k_ingest binned."""
-    m = _spawn(_stage_worker, _free_port())
+    and latest rows equal the single-engine path's, including a 4.5M-row batch whose records k_ingest binned; with a
+    16-MiB round size the 144-MB record exchange of that batch moves in rounds (distributed.EXCHANGE_ROUND_BYTES)."""
+    m = _spawn(_stage_worker, _free_port(), round_bytes)
     _, backend, res = m
     assert backend == "nccl"
     for r in res:
