@@ -54,6 +54,37 @@ __global__ __launch_bounds__(256) void k_atomics(const uint4 *__restrict__ src, 
     }
 }
 
+// the same patterns with each record stored by two lanes together (lane 2k + h writes half h of record k of the
+// round): one 16-B store instruction writes 32 whole 32-B records instead of one 16-B half of 64 records
+__device__ __forceinline__ void store_coop(uint4 *__restrict__ dst, int64_t d, uint4 a, uint4 b, bool ok) {
+    const int ln = __lane_id();
+    const unsigned long long dd = ok ? (unsigned long long)d : ~0ull;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const int src = r * 32 + (ln >> 1), h = ln & 1;
+        const unsigned long long t = __shfl(dd, src, 64);
+        uint4 va, vb;   // (both halves shuffled: the lane keeps the one it stores)
+        va.x = __shfl(a.x, src, 64); va.y = __shfl(a.y, src, 64); va.z = __shfl(a.z, src, 64); va.w = __shfl(a.w, src, 64);
+        vb.x = __shfl(b.x, src, 64); vb.y = __shfl(b.y, src, 64); vb.z = __shfl(b.z, src, 64); vb.w = __shfl(b.w, src, 64);
+        const uint4 v = h ? vb : va;
+        if (t != ~0ull) dst[2 * t + h] = v;
+    }
+}
+template <bool PRE>
+__global__ __launch_bounds__(256) void k_coop(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n,
+                                              unsigned *cur, const unsigned *__restrict__ slot, unsigned cap) {
+    for (int64_t base = (int64_t)blockIdx.x * 256; base < n; base += (int64_t)gridDim.x * 256) {
+        const int64_t i = base + threadIdx.x;
+        const bool in = i < n;
+        const int64_t j = in ? i : n - 1;
+        const uint4 a = src[2 * j], b = src[2 * j + 1];
+        unsigned s, p;
+        if (PRE) { s = slot[n + j]; p = slot[j]; }
+        else { s = bin_of(j); p = in ? atomicAdd(&cur[s], 1u) : cap; }
+        store_coop(dst, (int64_t)s * cap + p, a, b, in && p < cap);
+    }
+}
+
 // slots for the pre-reserved patterns (untimed): sub = 1 -> per bin; 8 -> per (bin, XCD of the executing workgroup)
 __global__ __launch_bounds__(256) void k_slots(int64_t n, unsigned *cur, unsigned *slot, int sub) {
     const unsigned x = sub > 1 ? xcc_id() : 0;
@@ -192,6 +223,15 @@ int main(int argc, char **argv) {
             const unsigned c = sub == 1 ? cap : cap / 8 * 2 + 512;
             const float t = timed([&] { hipLaunchKernelGGL(k_pre, dim3(grid), dim3(256), 0, 0, src, dst, n, slot, c); });
             printf("rep %d %s       %.3f ms\n", rep, sub == 1 ? "pre   " : "xcdpre", t);
+        }
+        if (want("coop")) {
+            printf("rep %d coopdirect   %.3f ms\n", rep,
+                   timed([&] { hipLaunchKernelGGL(k_coop<false>, dim3(grid), dim3(256), 0, 0, src, dst, n, cur, slot, cap); }));
+            CHK(hipMemset(cur, 0, BINS * 8 * 4));
+            hipLaunchKernelGGL(k_slots, dim3(grid), dim3(256), 0, 0, n, cur, slot, 1);
+            CHK(hipDeviceSynchronize());
+            printf("rep %d cooppre      %.3f ms\n", rep,
+                   timed([&] { hipLaunchKernelGGL(k_coop<true>, dim3(grid), dim3(256), 0, 0, src, dst, n, cur, slot, cap); }));
         }
         auto chunk = [&](auto kern, const char *name, int C, bool xcd) {
             if (!want(name)) return;
