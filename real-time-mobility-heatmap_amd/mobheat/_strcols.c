@@ -8,6 +8,8 @@
  * lengths(ptrs, n, lens, threads): ptrs = the address of the object array's n PyObject pointers, lens = int64[n] out:
  *   the byte length of a compact-ASCII str, -1 for None, -2 for anything else (the caller encodes or rejects it).
  * copy(ptrs, n, offsets, data, threads): the bytes of every row with lens >= 0 to data[offsets[i], offsets[i+1]).
+ * floats(ptrs, n, values, kinds, threads): an object column of Python float / None (a nullable double column as pandas
+ *   holds it): values[i] = the float, kinds[i] = 1 float, 0 None, 2 anything else (the caller converts those).
  * The object array must stay alive (it holds the references) and unchanged during both calls. */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
@@ -21,6 +23,7 @@ typedef struct {
     int64_t *lens;
     const int64_t *offs;
     uint8_t *data;
+    double *vals;
 } Job;
 
 static int is_ascii_str(PyObject *o) {
@@ -42,6 +45,22 @@ static void *copy_job(void *p) {
         PyObject *o = j->obj[i];
         const int64_t a = j->offs[i], b = j->offs[i + 1];
         if (b > a && is_ascii_str(o) && PyUnicode_GET_LENGTH(o) == b - a) memcpy(j->data + a, PyUnicode_DATA(o), (size_t)(b - a));
+    }
+    return NULL;
+}
+
+/* object column of Python float / None: the value (exact float objects only), data[i] = 1 valid, 0 None, 2 other */
+static void *float_job(void *p) {
+    Job *j = (Job *)p;
+    for (int64_t i = j->lo; i < j->hi; i++) {
+        PyObject *o = j->obj[i];
+        if (PyFloat_CheckExact(o)) {
+            j->vals[i] = PyFloat_AS_DOUBLE(o);
+            j->data[i] = 1;
+        } else {
+            j->vals[i] = 0.0;
+            j->data[i] = o == Py_None ? 0 : 2;
+        }
     }
     return NULL;
 }
@@ -72,7 +91,7 @@ static PyObject *py_lengths(PyObject *self, PyObject *args) {
     long long n;
     int threads;
     if (!PyArg_ParseTuple(args, "KLKi", &ptrs, &n, &lens, &threads)) return NULL;
-    Job j = {(PyObject *const *)(uintptr_t)ptrs, 0, 0, (int64_t *)(uintptr_t)lens, NULL, NULL};
+    Job j = {(PyObject *const *)(uintptr_t)ptrs, 0, 0, (int64_t *)(uintptr_t)lens, NULL, NULL, NULL};
     Py_BEGIN_ALLOW_THREADS
     run(len_job, j, n, threads);
     Py_END_ALLOW_THREADS
@@ -84,14 +103,27 @@ static PyObject *py_copy(PyObject *self, PyObject *args) {
     long long n;
     int threads;
     if (!PyArg_ParseTuple(args, "KLKKi", &ptrs, &n, &offs, &data, &threads)) return NULL;
-    Job j = {(PyObject *const *)(uintptr_t)ptrs, 0, 0, NULL, (const int64_t *)(uintptr_t)offs, (uint8_t *)(uintptr_t)data};
+    Job j = {(PyObject *const *)(uintptr_t)ptrs, 0, 0, NULL, (const int64_t *)(uintptr_t)offs, (uint8_t *)(uintptr_t)data, NULL};
     Py_BEGIN_ALLOW_THREADS
     run(copy_job, j, n, threads);
     Py_END_ALLOW_THREADS
     Py_RETURN_NONE;
 }
 
+static PyObject *py_floats(PyObject *self, PyObject *args) {
+    unsigned long long ptrs, vals, kinds;
+    long long n;
+    int threads;
+    if (!PyArg_ParseTuple(args, "KLKKi", &ptrs, &n, &vals, &kinds, &threads)) return NULL;
+    Job j = {(PyObject *const *)(uintptr_t)ptrs, 0, 0, NULL, NULL, (uint8_t *)(uintptr_t)kinds, (double *)(uintptr_t)vals};
+    Py_BEGIN_ALLOW_THREADS
+    run(float_job, j, n, threads);
+    Py_END_ALLOW_THREADS
+    Py_RETURN_NONE;
+}
+
 static PyMethodDef methods[] = {
+    {"floats", py_floats, METH_VARARGS, "values of float objects (kinds: 1 float, 0 None, 2 other)"},
     {"lengths", py_lengths, METH_VARARGS, "byte lengths of compact-ASCII str objects (-1 None, -2 other)"},
     {"copy", py_copy, METH_VARARGS, "copy the compact-ASCII strings' bytes to their offsets"},
     {NULL, NULL, 0, NULL}};

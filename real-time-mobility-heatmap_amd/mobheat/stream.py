@@ -545,6 +545,31 @@ def _object_strings(values):
     return pa.Array.from_buffers(pa.large_string(), n, [bitmap, pa.py_buffer(offs), pa.py_buffer(data)], null_count=nulls)
 
 
+def _object_floats(values):
+    """A pandas object column of Python float / None (how a nullable double column often arrives) -> pa.float64 array
+    (None / pd.NA -> null, NaN stays a value): _strcols' threads read the float objects without the GIL; ints and other
+    numbers are converted here.  None when a value is not a number."""
+    import pyarrow as pa
+    from . import _strcols
+    a = np.ascontiguousarray(values, dtype=object)
+    n = a.size
+    vals = np.empty(n, np.float64)
+    kinds = np.empty(n, np.uint8)
+    if n:
+        _strcols.floats(a.ctypes.data, n, vals.ctypes.data, kinds.ctypes.data, min(16, os.cpu_count() or 1))
+    na = getattr(__import__("pandas"), "NA", None)
+    for i in np.nonzero(kinds == 2)[0].tolist():
+        v = a[i]
+        if v is na:
+            kinds[i] = 0
+        elif isinstance(v, (int, float, np.integer, np.floating)) and not isinstance(v, bool):
+            vals[i], kinds[i] = float(v), 1
+        else:
+            return None
+    valid = kinds == 1
+    return pa.array(vals, mask=~valid) if not valid.all() else pa.array(vals)
+
+
 def device_columns(df):
     """The frame's columns for the device path (hm_arrow_columns): {"arrow": ArrowColumns, "n": n}, or batch_columns'
     host columns when the frame is not columnar Arrow-convertible (MOBHEAT_COLUMNS=host pins the host path), or the raw
@@ -554,10 +579,11 @@ def device_columns(df):
     strs = {}
     if _is_pandas(df) and "value" not in df.columns:
         # the pandas frame's string columns straight to Arrow's layout (_strcols: threads, no GIL), the rest by pyarrow
-        for c in ("provider", "vehicleId"):
+        for c, conv in (("provider", _object_strings), ("vehicleId", _object_strings), ("lat", _object_floats),
+                        ("lon", _object_floats), ("speedKmh", _object_floats)):
             if c in df.columns and df[c].dtype == object:
                 try:
-                    arr = _object_strings(df[c].to_numpy())
+                    arr = conv(df[c].to_numpy())
                 except ImportError:   # (the helper is not built: pyarrow converts the column)
                     arr = None
                 if arr is not None:

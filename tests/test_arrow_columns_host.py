@@ -133,3 +133,24 @@ def test_object_strings_to_arrow():
     assert got.equals(exp)
     assert stream._object_strings(np.array(["a", 3, "b"], dtype=object)) is None
     assert len(stream._object_strings(np.array([], dtype=object))) == 0
+
+
+def test_object_floats_to_arrow():
+    """_strcols.floats + the host's handling of the rest: float objects as values (NaN stays a value), None / pd.NA
+    null, ints converted, a non-number -> None"""
+    vals = np.array([1.5, None, float("nan"), pd.NA, 3, -0.0, np.float64(2.25)] * 20000, dtype=object)
+    got = stream._object_floats(vals)
+    want_valid = np.array([True, False, True, False, True, True, True] * 20000)
+    assert got.type == pa.float64() and got.null_count == int((~want_valid).sum())
+    v = got.to_numpy(zero_copy_only=False)
+    assert np.isnan(v[2]) and v[0] == 1.5 and v[4] == 3.0 and np.signbit(v[5]) and v[6] == 2.25
+    assert not got.is_valid().to_numpy(zero_copy_only=False)[1]
+    assert stream._object_floats(np.array([1.0, "x"], dtype=object)) is None
+
+
+def test_pandas_object_speed_column_reads_back_host_columns():
+    pdf = spark_like_frames(1, n=3000, seed=22)[0]
+    pdf["speedKmh"] = pdf["speedKmh"].astype(object).where(pdf["speedKmh"].notna(), None)
+    pdf["lat"] = pdf["lat"].astype(object)
+    cols = stream.device_columns(pdf)
+    _same(_readback(cols["arrow"]), _host(pdf))
