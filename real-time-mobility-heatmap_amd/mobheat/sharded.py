@@ -213,7 +213,38 @@ class RankRunner:
             batch[k] = a.ctypes.data + lo * a.itemsize if a.size else None
         _trace(self.rank, f"batch {epoch}: {n} rows")
         out = self.sharded.process_batch(epoch, batch, out_memory=HM_MEM_DEVICE)
-        _trace(self.rank, f"batch {epoch}: merged, {int(out.n_tiles)} tiles, {int(out.n_latest)} latest rows")
+        return self._statements(eng, out, views)
+
+    def run_device(self, epoch, views, bounds, restore, send=None):
+        """The device-column form of run: the batch's columns were built on rank 0's GPU (hm_arrow_columns /
+        hm_decode_json) and packed per rank (pack_columns); every rank takes its slice in the exchange's all_to_all
+        (rank 0 sends, every rank receives -- device to device, no host copy of the columns) and runs the stages on it.
+        views: the batch-wide string dictionaries (shared memory); send: rank 0's (buffer, bytes per rank)."""
+        if self.engine is None:
+            self._start(restore)
+        if self.rank:
+            self.out_t.close_retired()
+            self.out_p.close_retired()
+        eng = self.engine
+        self.began = False
+        v0 = eng.state_version()
+        try:
+            from .distributed import exchange_chunks
+            buf, sb = send if send is not None else (None, [0] * self.world)
+            recv, rb = exchange_chunks(buf, sb, self.device)
+            n = int(bounds[self.rank + 1] - bounds[self.rank])
+            assert sum(rb) == packed_bytes(n), (sum(rb), n)
+            self._cols = recv   # (alive until the next batch: the library reads it)
+            batch = packed_batch(recv.data_ptr(), n)
+            _trace(self.rank, f"batch {epoch}: {n} rows (device columns)")
+            out = self.sharded.process_batch(epoch, batch, out_memory=HM_MEM_DEVICE)
+            return self._statements(eng, out, views)
+        finally:
+            self.began = eng.state_version() != v0
+
+    def _statements(self, eng, out, views):
+        epoch_trace = f"{int(out.n_tiles)} tiles, {int(out.n_latest)} latest rows"
+        _trace(self.rank, f"merged, {epoch_trace}")
         c = self.cfg
         tb, to = eng.encode_tile_updates(c["city"], c["ttl_min"])   # (views: copied before the next encode)
         tiles = self.out_t.put({"b": tb, "o": to})
@@ -246,6 +277,48 @@ class RankRunner:
         _trace(self.rank, f"checkpoint {job['epoch']}: {kind} written")
         return kind
 
+
+
+# the device-column exchange: a rank's slice of n rows as one buffer -- lat, lon, ts_us, speed, vkey (8 B each), then
+# speed_valid and row_valid (1 B each, each padded to 8 B)
+_PACK = (("lat", 8), ("lon", 8), ("ts_us", 8), ("speed", 8), ("vkey", 8), ("speed_valid", 1), ("row_valid", 1))
+
+
+def _pad8(b):
+    return (b + 7) & ~7
+
+
+def packed_bytes(n):
+    return sum(_pad8(n * el) for _, el in _PACK)
+
+
+def packed_batch(addr, n):
+    """the stage API's batch over a packed slice at device address `addr`"""
+    b, off = {"n": n, "memory": HM_MEM_DEVICE}, 0
+    for k, el in _PACK:
+        b[k] = addr + off if n else None
+        off += _pad8(n * el)
+    return b
+
+
+def pack_columns(batch, bounds, device):
+    """rank 0: the device columns of the whole batch (an HmBatchIn, device memory) packed per rank (rank r: rows
+    [bounds[r], bounds[r+1])) into one device buffer by device-to-device copies -> (buffer, bytes per rank)"""
+    import torch
+    lib = _lib.load()
+    world = len(bounds) - 1
+    sizes = [packed_bytes(int(bounds[r + 1] - bounds[r])) for r in range(world)]
+    buf = torch.empty(max(sum(sizes), 8), dtype=torch.uint8, device=device)
+    base = buf.data_ptr()
+    for r in range(world):
+        lo, n = int(bounds[r]), int(bounds[r + 1] - bounds[r])
+        for k, el in _PACK:
+            src = getattr(batch, k)
+            if n and src:
+                _lib.check(lib.hm_memcpy(base, src + lo * el, n * el, 2), None, "hm_memcpy")
+            base += _pad8(n * el)
+    torch.cuda.synchronize(device)
+    return buf, sizes
 
 
 def _runner_class(cfg):
@@ -293,6 +366,10 @@ def _worker_main(rank, world, port, conn, cfg):
             if op == "batch":
                 _, epoch, name, layout, lo, hi, restore = msg
                 stats, tiles, positions = runner.run(epoch, shm_views(name, layout), lo, hi, restore)
+                conn.send(("ok", stats, tiles, positions))
+            elif op == "batch_dev":
+                _, epoch, name, layout, bounds, restore = msg
+                stats, tiles, positions = runner.run_device(epoch, shm_views(name, layout), bounds, restore)
                 conn.send(("ok", stats, tiles, positions))
             elif op == "commit":
                 runner.commit(msg[1])
@@ -406,6 +483,39 @@ class ShardedStream:
             res0 = self.runner.run(int(epoch), views, bounds[0], bounds[1], self.restore)
         except Exception as e:
             err0 = e
+        return self._collect(err0, res0, PeerFailed)
+
+    def process_device(self, epoch, batch, dicts):
+        """process() on device columns: `batch` (an HmBatchIn in rank 0's device memory: its engine's
+        hm_arrow_columns / hm_decode_json) is packed per rank on rank 0's GPU and each rank takes its slice in one
+        all_to_all -- no host copy of the columns; the string dictionaries (small) go through shared memory."""
+        from .distributed import PeerFailed
+        self.last = None
+        self.inputs.close_retired()
+        self.runner.out_t.close_retired()
+        self.runner.out_p.close_retired()
+        close_detached()
+        n = int(batch.n)
+        pn, po, pb = dictionary_arrays(dicts[0])
+        vn, vo, vb = dictionary_arrays(dicts[1])
+        name, layout = self.inputs.put(dict(prov_n=np.array([pn], np.int64), prov_offs=po, prov_bytes=pb,
+                                            veh_n=np.array([vn], np.int64), veh_offs=vo, veh_bytes=vb))
+        views = {k: np.ndarray(shp, np.dtype(d), buffer=self.inputs.shm.buf, offset=o) for k, d, shp, o in layout}
+        bounds = [r * n // self.world for r in range(self.world + 1)]
+        if self.restore is None:
+            self.restore = self._restore_point(epoch)
+        send = pack_columns(batch, bounds, self.runner.device)
+        for c in self.conns:
+            c.send(("batch_dev", int(epoch), name, layout, bounds, self.restore))
+        err0 = res0 = None
+        try:
+            res0 = self.runner.run_device(int(epoch), views, bounds, self.restore, send=send)
+        except Exception as e:
+            err0 = e
+        del send
+        return self._collect(err0, res0, PeerFailed)
+
+    def _collect(self, err0, res0, PeerFailed):
         replies = [self._recv(c, r) for r, c in enumerate(self.conns, start=1)]
         errs = [(0, err0)] if err0 is not None else []
         began = err0 is not None and getattr(self.runner, "began", False)
@@ -414,8 +524,6 @@ class ShardedStream:
                 errs.append((r, RuntimeError(f"rank {r}: {m[1]}\n{m[2]}")))
                 began = began or bool(m[4])
         if errs:
-            # a merge began on some rank: every rank's state is dropped (the replayed epoch restores it from the
-            # checkpoints); a batch that failed before any merge leaves every state as it was
             if began:
                 self.reset()
             first = next((e for _, e in errs if not isinstance(e, PeerFailed) and "PeerFailed" not in str(e)), errs[0][1])

@@ -742,12 +742,27 @@ def _foreach_sharded(df, epoch):
             sh.reset()
             _LAST_EPOCH = None
         _PENDING = None
-        cols = batch_columns(df)
-        if "kafka" in cols:
-            cols, dicts = _kafka_host_columns(sh.rank0_engine(epoch), *cols["kafka"])
+        if sh.cfg.get("cpu"):   # (ranks without a GPU: the host columns)
+            cols = batch_columns(df)
+            if "kafka" in cols:
+                cols, dicts = _kafka_host_columns(sh.rank0_engine(epoch), *cols["kafka"])
+            else:
+                dicts = (cols["provider_uniques"], cols["vehicle_uniques"])
+            per_rank = sh.process(epoch, cols, dicts)
         else:
-            dicts = (cols["provider_uniques"], cols["vehicle_uniques"])
-        per_rank = sh.process(epoch, cols, dicts)
+            # the columns built on rank 0's GPU -- the frame's Arrow buffers (hm_arrow_columns) or the raw Kafka values
+            # (hm_decode_json) -- and every rank's slice moved device to device (ShardedStream.process_device)
+            cols = device_columns(df)
+            if "arrow" in cols:
+                kb = sh.rank0_engine(epoch).arrow_columns(cols["arrow"].struct)
+            elif "kafka" in cols:
+                kb = sh.rank0_engine(epoch).decode_json(*cols["kafka"])
+            else:
+                kb = None
+            if kb is not None:
+                per_rank = sh.process_device(epoch, kb.batch, (kb.providers, kb.vehicles))
+            else:
+                per_rank = sh.process(epoch, cols, (cols["provider_uniques"], cols["vehicle_uniques"]))
         _PENDING = (epoch, per_rank, None)
     # every rank's state checkpoint, written while the statements go out (see checkpoint_begin)
     if STATE_CHECKPOINT:

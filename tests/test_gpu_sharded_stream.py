@@ -184,8 +184,9 @@ def test_sharded_foreach_batch_func_general_inputs_and_replay(tmp_path, monkeypa
 
 def test_sharded_foreach_batch_func_on_kafka_values(tmp_path, monkeypatch):
     """The raw Kafka `value` column over 2 ranks (decoded on rank 0's GPU, records outside the device decoder spliced
-    in from the host decode, the batch-wide dictionaries shared): the same statements as one GPU, byte for byte
-    (dyadic coordinates: exact in JSON and in every sum)."""
+    in from the host decode, the batch-wide dictionaries shared; every rank's slice of the decoded columns moved device
+    to device, never through the host): the same statements as one GPU, byte for byte (dyadic coordinates: exact in
+    JSON and in every sum)."""
     import datetime
     import json
     from mobheat import stream
@@ -210,6 +211,10 @@ def test_sharded_foreach_batch_func_on_kafka_values(tmp_path, monkeypatch):
     ref = _run(stream, frames, range(3))
     stream.reset_engine()
     _set(monkeypatch, stream, tmp_path, 2, "k2")
+
+    def no_host_columns(*a, **k):
+        raise AssertionError("the sharded writer copied decoded columns to the host")
+    monkeypatch.setattr(stream, "_kafka_host_columns", no_host_columns)   # (rank 0 decodes, ranks take slices on-device)
     got = _run(stream, frames, range(3))
     for e in range(3):
         for coll in ("tiles", "positions_latest"):
