@@ -122,7 +122,7 @@ def exchange_chunks(buf, send_bytes, device, status=0):
     assert all(b % 8 == 0 for b in recv_bytes) and all(int(b) % 8 == 0 for b in send_bytes)
     nrecv, nsend = sum(recv_bytes), int(sum(send_bytes))
     recv = torch.empty(max(nrecv // 8, 2), dtype=torch.int64, device=device)
-    words = buf[:nsend].view(torch.int64)
+    words = buf[:nsend].view(torch.int64) if nsend else torch.empty(0, dtype=torch.int64, device=device)
     step = EXCHANGE_ROUND_BYTES // 8
     biggest = max(max(r[:world]) for r in M) // 8
     rounds = 1 if step <= 0 or biggest <= step else -(-biggest // step)

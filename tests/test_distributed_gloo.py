@@ -246,3 +246,40 @@ def test_sharded_equals_single_shard(oracle_h3, table, round_bytes):
             assert abs(lat - o[k]["avg_lat"]) <= 1e-9 * abs(lat)
         latest = sorted(got[0][e][1] + got[1][e][1])
         assert latest == exp["latest_rows"].tolist()
+
+
+def _scatter_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mobheat import distributed
+    distributed.EXCHANGE_ROUND_BYTES = 64   # (rounds of 8 words per rank pair)
+    if rank == 0:   # rank 0 alone sends: rank r gets words [sum(sizes[:r]), ...)
+        sizes = [8 * (20 + 7 * r) for r in range(world)]
+        buf = torch.arange(sum(sizes) // 8, dtype=torch.int64).view(torch.uint8)
+        recv, rb = distributed.exchange_chunks(buf, sizes, torch.device("cpu"))
+    else:
+        recv, rb = distributed.exchange_chunks(None, [0] * world, torch.device("cpu"))
+    q.put((rank, rb, recv.view(torch.int64)[: sum(rb) // 8].tolist()))
+    dist.destroy_process_group()
+
+
+def test_exchange_from_one_sender_in_rounds():
+    """The sharded writer's device-column scatter pattern (sharded.ShardedStream.process_device): rank 0 alone sends,
+    every rank (rank 0 too) receives its slice, moved in rounds (distributed.EXCHANGE_ROUND_BYTES)"""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (rb, w)) for r, rb, w in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    start = 0
+    for r in range(world):
+        n = 20 + 7 * r
+        assert got[r][0] == [8 * n] + [0] * (world - 1)
+        assert got[r][1] == list(range(start, start + n))
+        start += n
