@@ -251,6 +251,7 @@ def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, ar
     kb = {k: 0.0 for k in STAGES}
     step_ms = []
     host = []   # per step: the library call's host side (wall, syncs, allocations; single GPU)
+    phases = []   # per step (sharded path): host wall ms of each stage phase (distributed.ShardedHeatmap)
     counts = None
     t0 = time.perf_counter()
     for s in range(args.warmup, total_steps):
@@ -259,6 +260,8 @@ def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, ar
         step_ms.append((time.perf_counter() - ts0) * 1e3)
         if sharded is None:
             host.append(eng.last_host_timings())
+        else:
+            phases.append(dict(sharded.last_phase_ms))
         tm = eng.last_timings()
         counts = eng.last_counts()
         for k in STAGES:
@@ -279,7 +282,8 @@ def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, ar
     torch.cuda.empty_cache()
     K = args.steps
     return dict(elapsed=elapsed, step_ms=step_ms, kt={k: v / K for k, v in kt.items()},
-                kb={k: v / K for k, v in kb.items()}, counts=counts, host=host)
+                kb={k: v / K for k, v in kb.items()}, counts=counts, host=host,
+                phases={k: round(float(np.median([p[k] for p in phases])), 3) for k in phases[0]} if phases else None)
 
 
 def slowest_step(leg):
@@ -394,6 +398,8 @@ def main():
         "roofline": roof,
         "slowest_step": slowest_step(A),
     }
+    if A["phases"]:   # the sharded path: median host wall ms per stage phase (rank 0)
+        out["stage_phase_ms"] = A["phases"]
     B = None
     if world == 1 and not sharded and not args.no_state_leg:
         # second leg: the state-read regime of the reference's ~2-s trigger (README.md:134-135) -- each micro-batch

@@ -246,6 +246,22 @@ class LibStages:
         return out
 
 
+class _PhaseClock:
+    """host wall time of each phase of a sharded batch (ms; a phase ends where the host next waits for the device or a
+    collective: the stages' own synchronizations, .cpu() of the collectives' sizes)"""
+
+    def __init__(self):
+        import time
+        self._t = time.perf_counter
+        self._last = self._t()
+        self.ms = {}
+
+    def __call__(self, name):
+        t = self._t()
+        self.ms[name] = round(1e3 * (t - self._last), 3)
+        self._last = t
+
+
 class ShardedHeatmap:
     """One rank of the sharded hot path. ``stages`` provides ingest / send / merge / finish (LibStages on GPUs)."""
 
@@ -273,11 +289,14 @@ class ShardedHeatmap:
             else:
                 sync = lambda: None   # noqa: E731
         err = None
+        clock = _PhaseClock()
         try:
             summary = self.stages.ingest(epoch, batch, self.world, self.rank)
         except Exception as e:
             err, summary = e, np.zeros(HM_STAGE_SUMMARY_WORDS, np.int64)
+        clock("ingest")
         summaries = all_gather_summaries(summary, self.device, status=1 if err else 0)
+        clock("summaries")
         if err:
             raise err
         try:
@@ -285,17 +304,24 @@ class ShardedHeatmap:
         except Exception as e:
             exchange_chunks(None, None, self.device, status=1)
             raise e
+        clock("send")
         recv, recv_bytes = exchange_chunks(buf, send_bytes, self.device)
         sync()
+        clock("exchange")
         try:
             out, winners = self.stages.merge(recv, recv_bytes, out_memory)
         except Exception as e:
             exchange([], self.device, status=1)
             raise e
+        clock("merge")
         [(winner_recv, wrc)] = exchange([winners], self.device)
         sync()
+        clock("winners")
         self._recv = (recv, winner_recv)
-        return self.stages.finish(winner_recv, int(sum(wrc)), out_memory, out)
+        res = self.stages.finish(winner_recv, int(sum(wrc)), out_memory, out)
+        clock("finish")
+        self.last_phase_ms = clock.ms
+        return res
 
 
 def tile_hash(cell, wstart):

@@ -3,5 +3,5 @@ set -o pipefail
 O=gpurun_out/${TAG:-r5g}
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 1100 python -u -m pytest tests/test_gpu_sharded_stream.py tests/test_gpu_rccl.py tests/test_gpu_arrow_columns.py tests/test_gpu_kafka.py -m gpu -x -v -p no:cacheprovider --timeout 600 --timeout-method thread -rf > $O/gpu_tests.log 2>&1
+timeout -k 10 1100 python -u -m pytest tests/test_gpu_sharded_stream.py tests/test_gpu_rccl.py tests/test_gpu_arrow_columns.py tests/test_gpu_kafka.py -m gpu -x -v -p no:cacheprovider --timeout 170 --timeout-method thread -rf > $O/gpu_tests.log 2>&1
 rc=$?; echo "done rc=$rc"; exit $rc
