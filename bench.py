@@ -52,25 +52,30 @@ SIMDS = 1024
 #                 emit 98/gap (a 49-B row moved into a gap; gaps = R - T), dedup 20/event
 #   multi-GPU     (stage API) the sender's records grouped by region field as above -- binned in k_ingest, or the
 #                 partition with one bin per region field -- then send 64/sent record (k_stage_pack: the 32-B record
-#                 read from its bin, written into its destination's chunk); the owner merges each bin from its
-#                 senders' segments: no partition (merge as above over the R records it received)
+#                 read from its bin, written into its destination's chunk) -- except the H records of the bins the
+#                 rank owns itself, kept in its slabs (binned; hm_last_counts "self_held"): 8/record, their keys read
+#                 for the census; the owner merges each bin from its senders' segments and its own slabs: no partition
+#                 (merge as above over the R records it received or kept)
 #   table mode    aggregate 41/event + 48/record, partition 160/record (48 + 48 read, 64 written), merge 64/record
 #                 read + 113/tile + 64/pre-existing key
-def stage_bytes(n, c, world=1):
+def stage_bytes(n, c, world=1, staged=None):
+    """staged: the batch ran through the stage API (default: world > 1; bench --sharded runs it at world 1 too)."""
+    staged = world > 1 if staged is None else staged
     R, T = c["partials"], c["tiles"]
     E = max(T - c["state_new"], 0)
     b = {"ingest": 42 * n, "dedup": 20 * n, "emit": 98 * max(R - T, 0), "send": 0}
     if c["table_mode"]:
         b.update(aggregate=41 * n + 48 * R, partition=160 * R, merge=64 * R + 113 * T + 64 * E)
         return b
-    S = c["sent"] if world > 1 else R   # records this rank grouped (and sent)
+    S = c["sent"] if staged else R   # records this rank grouped (and sent)
     b.update(aggregate=0, merge=32 * R + 113 * T + 64 * E)
     if c.get("binned"):
         b.update(ingest=51 * n + 32 * S, partition=0)
     else:
         b.update(partition=16 * n + 57 * S)
-    if world > 1:
-        b["send"] = 64 * S
+    if staged:
+        H = c.get("self_held", 0)
+        b["send"] = 64 * (S - H) + 8 * H
     return b
 
 
@@ -266,7 +271,7 @@ def run_leg(args, n, res, span_us, advance_us, seed, dev, local, world, rank, ar
         counts = eng.last_counts()
         for k in STAGES:
             kt[k] += max(tm[k], 0.0)
-        for k, v in stage_bytes(n, counts, world).items():
+        for k, v in stage_bytes(n, counts, world, staged=sharded is not None).items():
             kb[k] += v
     torch.cuda.synchronize()
     if dist.is_initialized():

@@ -179,6 +179,9 @@ typedef struct hm_stage_sizes {
     int64_t n_cands;                     /* latest candidates this rank sent */
     int64_t global_batch_max_event_ms;   /* max over all ranks */
     int64_t n_valid, n_late;             /* this rank's rows */
+    int64_t n_self_records;              /* of n_tile_records: the ones of bins this rank owns, kept in its own slabs
+                                            (the chunk it addresses to itself carries their counts and census, and
+                                            records = 0 in its header; hm_stage_merge merges them from the slabs) */
 } hm_stage_sizes;
 
 int hm_stage_ingest(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_t nranks, int32_t rank,
@@ -422,7 +425,8 @@ int hm_selftest_cells_to_boundary_host(const uint64_t *cells, int64_t n, double 
  * received as owner), [2] tiles emitted, [3] 1 if table mode ran, [4] table mode: aggregates evicted from k_agg's
  * LDS tables into its buckets, [5] stage API: tile records this rank sent, [6] device + pinned-host allocations and
  * [7] frees the context made since hm_create (steady-state batches make none: tests/test_gpu_parity.py), [8] 1 if the
- * direct path's rows were binned by the ingest itself (no separate partition pass). */
+ * direct path's rows were binned by the ingest itself (no separate partition pass), [9] stage API: of [5], the records
+ * of bins this rank owns, kept in its slabs (hm_stage_sizes.n_self_records). */
 int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n);
 /* Version of the persistent tile state: incremented when a batch starts merging into it (hm_process_batch,
  * hm_stage_merge, growth).  A call that failed without changing it left the state as it was (-1: ctx NULL). */

@@ -87,6 +87,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     // MOBHEAT_DEDUP_STREAM=main runs the dedup on the main stream after the merge path (its cost to the overlapped
     // kernels, measured by the bench with and without it); default: the side stream
     if (const char *m = getenv("MOBHEAT_DEDUP_STREAM")) ctx->dedup_main = !strcmp(m, "main");
+    if (const char *m = getenv("MOBHEAT_STAGE_SELF")) ctx->self_hold_ok = strcmp(m, "copy") != 0;
     // the registry, its census and the batch statistics side by side (one reset, one readback after k_ingest)
     if (hipMalloc(&ctx->d_wreg, REG_BLOCK_BYTES) != hipSuccess || !(ctx->d_wcount = ctx->d_wreg + WREG_SLOTS + 1) ||
         !(ctx->d_st = (DevStats *)(ctx->d_wreg + 2 * (WREG_SLOTS + 1))) ||
@@ -238,6 +239,7 @@ int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n) {
     if (n > 6) c[6] = ctx->n_allocs;
     if (n > 7) c[7] = ctx->n_frees;
     if (n > 8) c[8] = ctx->last_binned;
+    if (n > 9) c[9] = ctx->staged ? ctx->stage_self_recs : 0;
     return HM_OK;
 }
 

@@ -209,19 +209,10 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *send_buf, int64_t
         cands[o] = (int64_t)ctx->h_scratch[64 + o];
         n_sent += recs[o];
     }
-    std::vector<ChunkHdr> hdr;
-    std::vector<int64_t> start;
-    if ((rc = stage_layout(ctx, recs.data(), cands.data(), table, send_cap, hdr, start, send_bytes))) return rc;
-    if (start[W] > 0 && !send_buf) return set_err(ctx, HM_E_INVALID, "send buffer is required");
-    // headers, the local -> global window slot map, chunk starts -> device
-    const size_t meta = (size_t)W * sizeof(ChunkHdr) + (size_t)(W + 1) * 8 + WREG_SLOTS * sizeof(unsigned short);
-    if ((rc = ensure(ctx, ctx->stage_meta, meta))) return rc;
-    std::vector<uint8_t> hm(meta);
-    memcpy(hm.data(), hdr.data(), (size_t)W * sizeof(ChunkHdr));
-    memcpy(hm.data() + (size_t)W * sizeof(ChunkHdr), start.data(), (size_t)(W + 1) * 8);
-    unsigned short *gmap = (unsigned short *)(hm.data() + (size_t)W * sizeof(ChunkHdr) + (size_t)(W + 1) * 8);
+    // the local -> global window slot map
+    std::vector<unsigned short> gmap(WREG_SLOTS, 0);
+    bool same_slots = true;
     for (int w = 0; w < WREG_SLOTS; w++) {
-        gmap[w] = 0;
         const unsigned long long we = ctx->h_wreg[w];
         if (!we) continue;
         const auto it = std::find(ctx->stage_gwreg.begin(), ctx->stage_gwreg.end(), we);
@@ -230,7 +221,27 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *send_buf, int64_t
             continue;
         }
         gmap[w] = (unsigned short)(it - ctx->stage_gwreg.begin());
+        same_slots = same_slots && (gmap[w] == w || !ctx->h_wcount[w]);
     }
+    // the records of the bins this rank owns stay in its slabs when their keys need no rewrite (binned; every local
+    // window slot is its global one -- the registry hashes a window to the same slot on every rank unless two of the
+    // batch's windows collide): the chunk it addresses to itself then carries their counts and census only
+    const bool self_held = ctx->self_hold_ok && !table && ctx->binned && I.n > 0 && same_slots;
+    ctx->stage_self_held = self_held;
+    ctx->stage_self_recs = self_held ? recs[ctx->rank] : 0;
+    std::vector<int64_t> chunk_recs(recs);
+    if (self_held) chunk_recs[ctx->rank] = 0;
+    std::vector<ChunkHdr> hdr;
+    std::vector<int64_t> start;
+    if ((rc = stage_layout(ctx, chunk_recs.data(), cands.data(), table, send_cap, hdr, start, send_bytes))) return rc;
+    if (start[W] > 0 && !send_buf) return set_err(ctx, HM_E_INVALID, "send buffer is required");
+    // headers, chunk starts, the window slot map -> device
+    const size_t meta = (size_t)W * sizeof(ChunkHdr) + (size_t)(W + 1) * 8 + WREG_SLOTS * sizeof(unsigned short);
+    if ((rc = ensure(ctx, ctx->stage_meta, meta))) return rc;
+    std::vector<uint8_t> hm(meta);
+    memcpy(hm.data(), hdr.data(), (size_t)W * sizeof(ChunkHdr));
+    memcpy(hm.data() + (size_t)W * sizeof(ChunkHdr), start.data(), (size_t)(W + 1) * 8);
+    memcpy(hm.data() + (size_t)W * sizeof(ChunkHdr) + (size_t)(W + 1) * 8, gmap.data(), WREG_SLOTS * sizeof(unsigned short));
     HIPCHK(ctx, hipMemcpyAsync(ctx->stage_meta.p, hm.data(), meta, hipMemcpyHostToDevice, ctx->stream));
     const ChunkHdr *d_hdr = (const ChunkHdr *)ctx->stage_meta.p;
     const int64_t *d_start = (const int64_t *)((uint8_t *)ctx->stage_meta.p + (size_t)W * sizeof(ChunkHdr));
@@ -247,7 +258,7 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *send_buf, int64_t
             }
         } else if (n_sent > 0) {
             hipLaunchKernelGGL(k_stage_pack, dim3(RP_BINS), dim3(256), 0, ctx->stream, (const EventRec *)ctx->parts_sorted.p, slab,
-                               (const unsigned long long *)ctx->rp_O.p, stride, d_gmap, W, d_start, out);
+                               (const unsigned long long *)ctx->rp_O.p, stride, d_gmap, W, self_held ? ctx->rank : -1, d_start, out);
         }
         // candidates: per-destination cursors (in Cand units) into the chunks
         unsigned long long cur[64];
@@ -264,6 +275,7 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *send_buf, int64_t
     hm_stage_sizes z{};
     z.table_mode = table ? 1 : 0;
     z.n_tile_records = n_sent;
+    z.n_self_records = ctx->stage_self_recs;
     for (int o = 0; o < W; o++) z.n_cands += cands[o];
     z.global_batch_max_event_ms = ctx->stage_gmax_ms;
     z.n_valid = (int64_t)s1.n_valid;
@@ -302,7 +314,8 @@ static int merge_received_chunks(hm_ctx *ctx, const uint8_t *recv, const int64_t
     if ((rc = scan_counts(ctx, (const unsigned *)ctx->stage_C.p, m, (unsigned long long *)ctx->stage_P.p))) return rc;
     HIPCHK(ctx, hipMemsetAsync((unsigned *)ctx->stage_T.p + RP_BINS, 0, 4, ctx->stream));
     hipLaunchKernelGGL(k_stage_segments, dim3(grid_for(RP_BINS, 256)), dim3(256), 0, ctx->stream, recv, d_off,
-                       (const unsigned long long *)ctx->stage_P.p, W, lo, bins, (unsigned long long *)ctx->stage_SO.p,
+                       (const unsigned long long *)ctx->stage_P.p, W, lo, bins, ctx->stage_self_held ? ctx->rank : -1,
+                       (const EventRec *)ctx->parts_sorted.p, (int64_t)ctx->slab_cap, (unsigned long long *)ctx->stage_SO.p,
                        (unsigned *)ctx->stage_SP.p, (unsigned *)ctx->stage_T.p);
     if ((rc = scan_counts(ctx, (const unsigned *)ctx->stage_T.p, RP_BINS + 1, (unsigned long long *)ctx->rp_O.p))) return rc;
     HIPCHK(ctx, hipGetLastError());
@@ -380,7 +393,7 @@ int hm_stage_merge(hm_ctx *ctx, const void *recv_buf, const int64_t *recv_bytes,
     }
     const Cand *cands = (const Cand *)ctx->cands_recv.p;
     if (table) rc = merge_partials(ctx, (const TilePartial *)ctx->stage_tmp.p, n_rec);
-    else rc = merge_received_chunks(ctx, recv, d_off, hdr, n_rec);
+    else rc = merge_received_chunks(ctx, recv, d_off, hdr, n_rec + ctx->stage_self_recs);   // (+ the self-held ones)
     if (rc) return rc;
     // owner-side dedup over received candidates
     if ((rc = phase_dedup(ctx, nullptr, cands, n_cand, true))) return rc;
@@ -410,7 +423,7 @@ int hm_stage_merge(hm_ctx *ctx, const void *recv_buf, const int64_t *recv_bytes,
     if ((rc = finish_outputs(ctx, (int64_t)s2.n_touched, 0, nullptr, out_memory, out))) return rc;
     // hm_last_counts: this rank's share of the batch (state keys created, records merged, tiles emitted, path)
     ctx->last_counts[0] = (int64_t)s2.n_state_new;
-    ctx->last_counts[1] = n_rec;
+    ctx->last_counts[1] = n_rec + (table ? 0 : ctx->stage_self_recs);
     ctx->last_counts[2] = (int64_t)s2.n_touched;
     ctx->last_counts[3] = ctx->stage_table ? 1 : 0;
     ctx->last_counts[4] = ctx->stage_table ? ctx->table_evicted : 0;

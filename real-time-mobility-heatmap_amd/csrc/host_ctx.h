@@ -176,6 +176,12 @@ struct hm_ctx {
     bool stage_table = false;                          // the batch's aggregation path (the same on every rank)
     int64_t stage_gmax_ms = INT64_MIN;                 // the batch's max event time over all ranks
     int64_t stage_sent = 0;                            // tile records this rank sent
+    // the direct path's records this rank owns itself, kept in its slabs instead of packed into the chunk it
+    // addresses to itself (hm_stage_send: binned batch, local window slots = global ones); MOBHEAT_STAGE_SELF=copy
+    // packs them like any other destination's (A/B)
+    int64_t stage_self_recs = 0;
+    bool stage_self_held = false;
+    bool self_hold_ok = true;
     std::vector<unsigned long long> stage_gwreg;       // the batch's global window registry (WREG_SLOTS wenc)
     std::vector<unsigned> stage_gslot;                 // this rank's registry slot -> global slot
 };

@@ -239,8 +239,8 @@ struct MLine {
 // existing keys (their lines then cost one cooperative round trip); a batch of mostly new keys runs the per-lane probe,
 // which carries less machinery per probed slot (bench leg: 3.72-3.81 vs 4.03-4.11 ms; state-read leg: 6.86-6.89 vs
 // 6.22-6.30 ms, profiles/r3/r3ab9/)
-// kSeg (the multi-GPU owner): bin b's records are nseg segments, one per sender -- segment s at record SO[b * nseg + s]
-// of parts, after SP[b * nseg + s] records of the bin (k_stage_segments)
+// kSeg (the multi-GPU owner): bin b's records are nseg segments, one per sender -- segment s at address SO[b * nseg + s]
+// (the receive buffer, or the owner's own slab), after SP[b * nseg + s] records of the bin (k_stage_segments)
 constexpr int MO_SEG_MAX = 64;
 template <typename Rec, bool kResident = false, bool kCoop = false, bool kSeg = false>
 __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_merge_owned(const Rec *__restrict__ parts, int64_t slab,
@@ -622,7 +622,7 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                     const int mid = (lo + hi) >> 1;
                     if (seg_pre[mid] <= v) lo = mid; else hi = mid;
                 }
-                return parts + seg_base[lo] + (v - seg_pre[lo]);
+                return (const Rec *)(uintptr_t)seg_base[lo] + (v - seg_pre[lo]);
             } else {
                 return bp + i;
             }

@@ -139,9 +139,12 @@ HM_HD int64_t chunk_census_off(int64_t bins) { return (int64_t)sizeof(ChunkHdr) 
 // partition's bin b: [S[b * stride] - S[lo]) ...) copied into its owner's chunk with the key's window slot rewritten to
 // the batch's global slot; the bin's count and the records' census into the chunk.  slab > 0: bin b's records start at
 // src + b * slab, else at src + S[b * stride].  S: exclusive scan of the bins' record counts (stride words apart).
+// self_rank >= 0: the bins this rank owns itself stay in its slabs (self-held: the local and global window slots are
+// the same, hm_stage_send) -- only their counts and census go into the chunk it addresses to itself, whose header
+// then counts no records; the owner merges those bins' own segment from the slabs (k_stage_segments).
 __global__ __launch_bounds__(256) void k_stage_pack(const EventRec *__restrict__ src, int64_t slab,
                                                     const unsigned long long *__restrict__ S, int64_t stride,
-                                                    const unsigned short *__restrict__ gslot_of, int nranks,
+                                                    const unsigned short *__restrict__ gslot_of, int nranks, int self_rank,
                                                     const int64_t *__restrict__ chunk_start, uint8_t *__restrict__ out) {
     __shared__ unsigned cc[CENSUS_WORDS];
     for (int q = threadIdx.x; q < CENSUS_WORDS; q += blockDim.x) cc[q] = 0;
@@ -156,13 +159,17 @@ __global__ __launch_bounds__(256) void k_stage_pack(const EventRec *__restrict__
     const ChunkHdr lay = chunk_layout(0, 0, (int64_t)sizeof(EventRec), (int64_t)(hi - lo));
     if (threadIdx.x == 0) ((unsigned *)(chunk + sizeof(ChunkHdr)))[b - lo] = (unsigned)cnt;
     const EventRec *in = src + (slab > 0 ? (int64_t)b * slab : s0);
-    EventRec *dst = (EventRec *)(chunk + lay.recs_off) + dst0;
-    for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-        EventRec r = in[i];
-        const unsigned g = gslot_of[ekey_widx(r.key)];
-        r.key = (r.key & CELL_LO) | ((uint64_t)(g + 1) << 52);
-        dst[i] = r;
-        atomicAdd(&cc[g], 1u);
+    if (o == self_rank) {   // self-held: the census only (keys read, nothing copied)
+        for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) atomicAdd(&cc[gslot_of[ekey_widx(in[i].key)]], 1u);
+    } else {
+        EventRec *dst = (EventRec *)(chunk + lay.recs_off) + dst0;
+        for (int64_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+            EventRec r = in[i];
+            const unsigned g = gslot_of[ekey_widx(r.key)];
+            r.key = (r.key & CELL_LO) | ((uint64_t)(g + 1) << 52);
+            dst[i] = r;
+            atomicAdd(&cc[g], 1u);
+        }
     }
     __syncthreads();
     unsigned *census = (unsigned *)(chunk + census_off);
@@ -171,12 +178,14 @@ __global__ __launch_bounds__(256) void k_stage_pack(const EventRec *__restrict__
 }
 
 // Owner, direct path: the segments of every region field it owns.  For bin b (global numbering, in [lo, hi)) and
-// sender s: its records start at record index SO[b * nseg + s] of the receive buffer (in EventRecs) and hold
-// C[s][b - lo] of them (the chunk's counts); SP[b * nseg + s] = the records of b from senders < s; T[b] = all of them.
-// C is read from each chunk (chunk_off[s]: its byte offset); prefix: the exclusive scan of k_stage_counts' rows.
+// sender s: its records start at address SO[b * nseg + s] (in the receive buffer; the owner's own segment, self-held,
+// in its slab: self_slab + b * slab_cap) and hold C[s][b - lo] of them (the chunk's counts); SP[b * nseg + s] = the
+// records of b from senders < s; T[b] = all of them.  C is read from each chunk (chunk_off[s]: its byte offset);
+// prefix: the exclusive scan of k_stage_counts' rows.
 __global__ __launch_bounds__(256) void k_stage_segments(const uint8_t *__restrict__ recv, const int64_t *__restrict__ chunk_off,
                                                         const unsigned long long *__restrict__ prefix, int nseg, unsigned lo,
-                                                        unsigned bins, unsigned long long *__restrict__ SO, unsigned *__restrict__ SP,
+                                                        unsigned bins, int self_rank, const EventRec *self_slab, int64_t slab_cap,
+                                                        unsigned long long *__restrict__ SO, unsigned *__restrict__ SP,
                                                         unsigned *__restrict__ T) {
     for (unsigned k = blockIdx.x * blockDim.x + threadIdx.x; k < (unsigned)RP_BINS; k += gridDim.x * blockDim.x) {
         if (k < lo || k >= lo + bins) {
@@ -190,7 +199,9 @@ __global__ __launch_bounds__(256) void k_stage_segments(const uint8_t *__restric
             const ChunkHdr lay = chunk_layout(0, 0, (int64_t)sizeof(EventRec), (int64_t)bins);
             const unsigned c = ((const unsigned *)(chunk + sizeof(ChunkHdr)))[j];
             const unsigned long long *P = prefix + (int64_t)s * (bins + 1);   // (one scan over all senders' rows)
-            SO[(int64_t)k * nseg + s] = (unsigned long long)((chunk_off[s] + lay.recs_off) / (int64_t)sizeof(EventRec)) + (P[j] - P[0]);
+            const EventRec *base = s == self_rank ? self_slab + (int64_t)k * slab_cap
+                                                  : (const EventRec *)(chunk + lay.recs_off) + (P[j] - P[0]);
+            SO[(int64_t)k * nseg + s] = (unsigned long long)(uintptr_t)base;
             SP[(int64_t)k * nseg + s] = acc;
             acc += c;
         }

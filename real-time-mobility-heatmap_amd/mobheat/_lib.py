@@ -75,7 +75,7 @@ class HmArrowIn(ctypes.Structure):
 
 class HmStageSizes(ctypes.Structure):
     _fields_ = [("table_mode", c_i64), ("n_tile_records", c_i64), ("n_cands", c_i64), ("global_batch_max_event_ms", c_i64),
-                ("n_valid", c_i64), ("n_late", c_i64)]
+                ("n_valid", c_i64), ("n_late", c_i64), ("n_self_records", c_i64)]
 
 
 class HmStateInfo(ctypes.Structure):

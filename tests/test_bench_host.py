@@ -46,3 +46,15 @@ def test_stage_bytes_multi_gpu_owner():
     assert s["merge"] == 32 * R + 113 * R
     s = b.stage_bytes(n, dict(c, binned=1), world=2)
     assert s["partition"] == 0 and s["ingest"] == 51 * n + 32 * S and s["send"] == 64 * S
+
+
+def test_stage_bytes_self_held_records():
+    """The records of the bins a rank owns stay in its slabs (binned): only their keys are read (census), 8 B each;
+    the bench's --sharded run prices the stage API at world 1 too."""
+    b = _bench()
+    n, S, H = 50_000_000, 50_000_000, 25_000_000
+    c = {"partials": S, "tiles": S, "state_new": S, "table_mode": False, "sent": S, "binned": 1, "self_held": H}
+    assert b.stage_bytes(n, c, world=2)["send"] == 64 * (S - H) + 8 * H
+    c1 = dict(c, self_held=S)
+    assert b.stage_bytes(n, c1, world=1, staged=True)["send"] == 8 * S
+    assert b.stage_bytes(n, c1, world=1)["send"] == 0   # (hm_process_batch: no stage API)

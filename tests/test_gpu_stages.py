@@ -52,7 +52,7 @@ def _stage_batch(engines, lib, batches_per_rank, epoch):
                        vkey=k["vkey"].ctypes.data, row_valid=k["rv"].ctypes.data)
         check(lib.hm_stage_ingest(eng._ctx, epoch, ctypes.byref(bi), W, r, summaries[r].ctypes.data), eng._ctx)
     from stage_chunks import unpack
-    sends, sbytes, tcounts, ccounts, table = [], [], [], [], None
+    sends, sbytes, tcounts, ccounts, table, self_recs = [], [], [], [], None, []
     for r, (eng, b) in enumerate(zip(engines, batches_per_rank)):
         n = b["lat"].size
         cap = lib.hm_stage_send_capacity(n, W)
@@ -75,8 +75,10 @@ def _stage_batch(engines, lib, batches_per_rank, epoch):
             off += sb[d]
         tcounts.append(tc)
         ccounts.append(cc)
-        if not table:   # one 32-B record per aggregated row of the rank
-            assert sum(tc) == summaries[r][3] == sz.n_tile_records
+        if not table:   # one 32-B record per aggregated row of the rank (its own bins' ones may stay in its slabs)
+            assert sum(tc) + sz.n_self_records == summaries[r][3] == sz.n_tile_records
+            assert sz.n_self_records == 0 or tc[r] == 0
+        self_recs.append(sz.n_self_records)
 
     outs, wsends, wcounts = [], [], []
     for r, eng in enumerate(engines):
@@ -97,7 +99,8 @@ def _stage_batch(engines, lib, batches_per_rank, epoch):
         wcounts.append(list(wc))
         wsends.append(wb.get(sum(wc) * 8).view(np.int64))
         c = eng.last_counts()
-        assert c["partials"] == recs.size and c["tiles"] == len(res.tiles) and c["sent"] == sum(tcounts[r])
+        assert c["partials"] == recs.size + self_recs[r] and c["tiles"] == len(res.tiles)
+        assert c["sent"] == sum(tcounts[r]) + self_recs[r]
     latest = []
     for r, eng in enumerate(engines):
         rows = np.concatenate([wsends[s][sum(wcounts[s][:r]): sum(wcounts[s][:r + 1])] for s in range(W)])

@@ -10,6 +10,10 @@
 //              record takes the next slot of its workgroup's chunk with an LDS atomic (chunk full: the lane that finds it
 //              full reserves the next chunk, the others retry); unused slots of the last chunks written as holes
 //   chunkx C   chunk, with the chunks of a bin reserved per (bin, XCD) (sub-slabs per XCD: a chunk's lines meet in L2)
+//   xcddir     direct with a cursor and a sub-slab per (bin, XCD of the executing workgroup): agent-scope atomics
+//   xcdl2      xcddir with the cursor atomics at workgroup scope (executed in the XCD's L2, no sc1; each XCD's cursors on
+//              lines of their own, cur[x * BINS + bin], touched only by that XCD's workgroups); checked: every slot below
+//              each cursor written once, the record ids' sum
 // Build: hipcc --offload-arch=gfx950 -O3 -o bin_chunk bin_chunk.hip      Run: ./bin_chunk [n]
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -42,6 +46,40 @@ __global__ __launch_bounds__(256) void k_direct(const uint4 *__restrict__ src, u
             dst[2 * ((int64_t)s * cap + p) + 1] = b;
         }
     }
+}
+
+template <bool L2>
+__global__ __launch_bounds__(256) void k_xcddir(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n,
+                                                unsigned *cur, unsigned cap) {
+    const unsigned x = xcc_id();
+    unsigned *cx = cur + x * BINS;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const uint4 a = src[2 * i], b = src[2 * i + 1];
+        const unsigned s = bin_of(i);
+        const unsigned p = L2 ? __hip_atomic_fetch_add(&cx[s], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                              : atomicAdd(&cx[s], 1u);
+        if (p < cap) {
+            const int64_t d = ((int64_t)s * 8 + x) * cap + p;
+            dst[2 * d] = make_uint4((unsigned)i + 1u, a.y, a.z, a.w);
+            dst[2 * d + 1] = b;
+        }
+    }
+}
+// check of xcddir/xcdl2: per sub-slab (bin, x), slots [0, min(cur, cap)) hold ids (nonzero), the rest 0; sums of ids
+__global__ __launch_bounds__(256) void k_xcdcheck(const uint4 *__restrict__ dst, const unsigned *cur, unsigned cap,
+                                                  unsigned long long *out) {
+    unsigned long long sum = 0, bad = 0, cnt = 0;
+    for (int sb = blockIdx.x; sb < BINS * 8; sb += gridDim.x) {
+        const int bin = sb >> 3, x = sb & 7;
+        const unsigned c = cur[x * BINS + bin] < cap ? cur[x * BINS + bin] : cap;
+        for (unsigned k = threadIdx.x; k < cap; k += 256) {
+            const unsigned id = dst[2 * ((int64_t)sb * cap + k)].x;
+            if (k < c) { sum += id; cnt++; bad += id == 0; } else bad += id != 0;
+        }
+    }
+    atomicAdd(&out[0], sum);
+    atomicAdd(&out[1], bad);
+    atomicAdd(&out[2], cnt);
 }
 
 __global__ __launch_bounds__(256) void k_atomics(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n,
@@ -215,6 +253,25 @@ int main(int argc, char **argv) {
                timed([&] { hipLaunchKernelGGL(k_direct, dim3(grid), dim3(256), 0, 0, src, dst, n, cur, cap); }));
         if (want("atomics")) printf("rep %d atomics      %.3f ms\n", rep,
                timed([&] { hipLaunchKernelGGL(k_atomics, dim3(grid), dim3(256), 0, 0, src, dst, n, cur); }));
+        for (int l2 = 0; l2 < 2; l2++) {
+            if (!want(l2 ? "xcdl2" : "xcddir")) continue;
+            const unsigned c = cap / 8 * 2 + 512;
+            CHK(hipMemset(dst, 0, (size_t)BINS * 8 * c * 32));
+            const float t = timed([&] {
+                if (l2) hipLaunchKernelGGL(k_xcddir<true>, dim3(grid), dim3(256), 0, 0, src, dst, n, cur, c);
+                else hipLaunchKernelGGL(k_xcddir<false>, dim3(grid), dim3(256), 0, 0, src, dst, n, cur, c);
+            });
+            unsigned long long *chk;
+            CHK(hipMalloc(&chk, 24));
+            CHK(hipMemset(chk, 0, 24));
+            hipLaunchKernelGGL(k_xcdcheck, dim3(4096), dim3(256), 0, 0, dst, cur, c, chk);
+            unsigned long long h[3];
+            CHK(hipMemcpy(h, chk, 24, hipMemcpyDeviceToHost));
+            CHK(hipFree(chk));
+            const unsigned long long want_sum = (unsigned long long)n * (n + 1) / 2;
+            printf("rep %d %s       %.3f ms  (records %llu of %lld, bad slots %llu, id sum %s)\n", rep, l2 ? "xcdl2 " : "xcddir", t,
+                   h[2], (long long)n, h[1], h[0] == want_sum ? "ok" : "WRONG");
+        }
         for (int sub : {1, 8}) {
             if (!want(sub == 1 ? "pre" : "xcdpre")) continue;
             CHK(hipMemset(cur, 0, BINS * 8 * 4));
