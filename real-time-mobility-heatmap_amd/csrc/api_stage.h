@@ -257,8 +257,19 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *send_buf, int64_t
                 first += (int)recs[o];
             }
         } else if (n_sent > 0) {
+            // (a world of one holds every bin itself: its census is the ingest's, written from the host)
+            const bool census_host = self_held && W == 1;
             hipLaunchKernelGGL(k_stage_pack, dim3(RP_BINS), dim3(256), 0, ctx->stream, (const EventRec *)ctx->parts_sorted.p, slab,
-                               (const unsigned long long *)ctx->rp_O.p, stride, d_gmap, W, self_held ? ctx->rank : -1, d_start, out);
+                               (const unsigned long long *)ctx->rp_O.p, stride, d_gmap, W, self_held ? ctx->rank : -1,
+                               census_host ? 0 : 1, d_start, out);
+            if (census_host) {
+                std::vector<unsigned> &cen = ctx->stage_cen;   // (kept until the send's synchronization below)
+                cen.assign(CENSUS_WORDS, 0u);
+                for (int w = 0; w < WREG_SLOTS; w++)
+                    if (ctx->h_wcount[w]) cen[gmap[w]] += (unsigned)ctx->h_wcount[w];
+                HIPCHK(ctx, hipMemcpyAsync(out + start[ctx->rank] + chunk_census_off((int64_t)RP_BINS), cen.data(),
+                                           CENSUS_WORDS * 4, hipMemcpyHostToDevice, ctx->stream));
+            }
         }
         // candidates: per-destination cursors (in Cand units) into the chunks
         unsigned long long cur[64];

@@ -182,6 +182,7 @@ struct hm_ctx {
     int64_t stage_self_recs = 0;
     bool stage_self_held = false;
     bool self_hold_ok = true;
+    std::vector<unsigned> stage_cen;   // a world of one: the census of its self-held records (host -> its own chunk)
     std::vector<unsigned long long> stage_gwreg;       // the batch's global window registry (WREG_SLOTS wenc)
     std::vector<unsigned> stage_gslot;                 // this rank's registry slot -> global slot
 };
