@@ -88,6 +88,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     // kernels, measured by the bench with and without it); default: the side stream
     if (const char *m = getenv("MOBHEAT_DEDUP_STREAM")) ctx->dedup_main = !strcmp(m, "main");
     if (const char *m = getenv("MOBHEAT_STAGE_SELF")) ctx->self_hold_ok = strcmp(m, "copy") != 0;
+    if (const char *m = getenv("MOBHEAT_DEDUP_DENSE")) ctx->dense_ok = strcmp(m, "0") != 0;
     // the registry, its census and the batch statistics side by side (one reset, one readback after k_ingest)
     if (hipMalloc(&ctx->d_wreg, REG_BLOCK_BYTES) != hipSuccess || !(ctx->d_wcount = ctx->d_wreg + WREG_SLOTS + 1) ||
         !(ctx->d_st = (DevStats *)(ctx->d_wreg + 2 * (WREG_SLOTS + 1))) ||
@@ -174,7 +175,7 @@ void hm_destroy(hm_ctx *ctx) {
                       &ctx->jd_bytes, &ctx->jd_offs, &ctx->jd_scratch, &ctx->jd_lat, &ctx->jd_lon, &ctx->jd_ts, &ctx->jd_speed,
                       &ctx->jd_sv, &ctx->jd_rv, &ctx->jd_vkey, &ctx->jd_poff, &ctx->jd_plen, &ctx->jd_voff, &ctx->jd_vlen,
                       &ctx->jd_un, &ctx->jd_unrows, &ctx->jd_patch,
-                      &ctx->lb_set, &ctx->lb_list};
+                      &ctx->lb_set, &ctx->lb_list, &ctx->dense};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (hm_ctx::Dict *d : {&ctx->jd_prov, &ctx->jd_veh}) {

@@ -34,6 +34,21 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
         (rc = ensure(ctx, ctx->keys, n * 8)) || (rc = ensure(ctx, ctx->slow, n * sizeof(unsigned int))))
         return rc;
     if ((rc = dedup_prepare(ctx, ctx->dfused, dedup_fused_keys(ctx, n), true))) return rc;
+    // the dense dedup table: room for the last batch's vkeys (first batch: 2^20), 2^16 .. 2^22 words; none when the
+    // last batch's vkeys were not dense codes (above 2^24)
+    {
+        const int64_t b = ctx->vkey_bound;
+        unsigned long long cap = 0;
+        if (ctx->dense_ok && n > 0 && b <= (int64_t(1) << 24)) {
+            cap = b < 0 ? (1ull << 20) : 1ull << 16;
+            while (cap < (unsigned long long)b && cap < (1ull << 22)) cap <<= 1;
+        }
+        ctx->dense_cap = cap;
+        if (cap) {
+            if ((rc = ensure(ctx, ctx->dense, cap * 8))) return rc;
+            HIPCHK(ctx, hipMemsetAsync(ctx->dense.p, 0, cap * 8, ctx->stream));
+        }
+    }
     const bool bin = allow_bin && n > 0 && choose_binned(ctx, n);
     ctx->slab_cap = bin ? slab_cap_for(n, ctx->bin_skew) : 0;
     ctx->binned = false;
@@ -74,7 +89,8 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
                                (uint64_t *)ctx->keys.p, ctx->dfused.tab, ctx->dfused.cap - 1, (unsigned int *)ctx->dfused.used.p,
                                ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
                                ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st, I.sp, I.sv,
-                               (unsigned *)ctx->bin_cur.p, bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap);
+                               (unsigned *)ctx->bin_cur.p, bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap,
+                               (unsigned long long *)ctx->dense.p, ctx->dense_cap);
         }
         ctx->n_h2d = 0;
         hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, ctx->cfg.h3_res,
@@ -99,6 +115,7 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
         return set_err(ctx, HM_E_OVERFLOW, "more than %d distinct windows in one micro-batch (%llu rows)", WREG_SLOTS,
                        ctx->h_st->win_overflow);
     ctx->binned = bin && ctx->h_st->bin_overflow == 0;
+    if (ctx->h_st->vkey_max1) ctx->vkey_bound = (int64_t)ctx->h_st->vkey_max1;
     return HM_OK;
 }
 
@@ -177,7 +194,8 @@ static int phase_dedup(hm_ctx *ctx, const Inputs *I, const Cand *cands, int64_t 
         }
         hipLaunchKernelGGL(k_dedup_flag, dim3(grid_for(n, 256)), dim3(256), 0, st, I ? I->vk : nullptr,
                            I ? I->ts : nullptr, (const uint8_t *)ctx->flags.p, cands, n, d.tab, d.cap - 1,
-                           (uint8_t *)ctx->win.p, !need_max);
+                           (uint8_t *)ctx->win.p, !need_max, (const unsigned long long *)ctx->dense.p,
+                           need_max ? 0ull : ctx->dense_cap);
         HIPCHK(ctx, hipGetLastError());
         if ((rc = compact_flags(ctx, (const uint8_t *)ctx->win.p, n, (int64_t *)ctx->rows.p, st))) return rc;
     } else {

@@ -179,6 +179,12 @@ struct hm_ctx {
     // the direct path's records this rank owns itself, kept in its slabs instead of packed into the chunk it
     // addresses to itself (hm_stage_send: binned batch, local window slots = global ones); MOBHEAT_STAGE_SELF=copy
     // packs them like any other destination's (A/B)
+    // k_ingest's dense dedup table (k_ingest.h): dense_cap words of this batch (0: none), sized from the last batch's
+    // max vkey (vkey_bound; -1: no batch yet); MOBHEAT_DEDUP_DENSE=0 turns it off (the hash table for every vkey)
+    DevBuf dense;
+    unsigned long long dense_cap = 0;
+    int64_t vkey_bound = -1;
+    bool dense_ok = true;
     int64_t stage_self_recs = 0;
     bool stage_self_held = false;
     bool self_hold_ok = true;

@@ -107,12 +107,14 @@ __global__ __launch_bounds__(256) void k_dedup_max(const uint64_t *__restrict__ 
 }
 
 // winner flag per row (or candidate): ts == max ts of its vkey.  DF_U rows per thread, their first probes
-// issued together, each probe one 16-B slot load (key and max ts): the lookups' latencies overlap.
+// issued together, each probe one 16-B slot load (key and max ts): the lookups' latencies overlap.  dense_cap > 0
+// (only_cand: k_ingest's fused max): a vkey below it has its max in dense[vkey] (k_ingest.h DENSE_SIGN)
 constexpr int DF_U = 4;
 __global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__ vkey, const int64_t *__restrict__ ts,
                                                     const uint8_t *__restrict__ flags, const Cand *__restrict__ cands, int64_t n,
                                                     const DedupSlot *__restrict__ tab, unsigned long long mask,
-                                                    uint8_t *__restrict__ win, bool only_cand) {
+                                                    uint8_t *__restrict__ win, bool only_cand,
+                                                    const unsigned long long *__restrict__ dense, unsigned long long dense_cap) {
     const int64_t step = (int64_t)blockDim.x * DF_U;
     for (int64_t base = (int64_t)blockIdx.x * step; base < n; base += (int64_t)gridDim.x * step) {
         unsigned long long v[DF_U], h[DF_U];
@@ -134,12 +136,20 @@ __global__ __launch_bounds__(256) void k_dedup_flag(const uint64_t *__restrict__
             h[u] = vkey_hash(v[u]) & mask;
         }
         DedupSlot sl[DF_U];
-        for (int u = 0; u < DF_U; u++)
-            if (take[u]) sl[u] = tab[h[u]];
+        unsigned long long dn[DF_U];
+        for (int u = 0; u < DF_U; u++) {
+            dn[u] = 0;
+            if (take[u]) {
+                if (v[u] < dense_cap) dn[u] = dense[v[u]];
+                else sl[u] = tab[h[u]];
+            }
+        }
         for (int u = 0; u < DF_U; u++) {
             const int64_t i = base + u * blockDim.x + threadIdx.x;
             uint8_t w = 0;
-            if (take[u]) {
+            if (take[u] && v[u] < dense_cap) {
+                w = (long long)(dn[u] ^ DENSE_SIGN) == t[u];
+            } else if (take[u]) {
                 for (unsigned long long probe = 0; probe <= mask; probe++) {
                     if (sl[u].vkey == v[u]) { w = sl[u].maxts == t[u]; break; }
                     if (sl[u].vkey == EMPTY_VKEY) break;

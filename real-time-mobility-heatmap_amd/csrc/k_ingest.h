@@ -45,6 +45,12 @@ __global__ __launch_bounds__(256) void k_cells_exact(const double *__restrict__ 
 // input of both aggregation paths (direct: partition + merge; table: k_agg + k_bin_reduce).  The fp64 cell
 // computation dominates; the dedup's table atomics overlap with it.
 // =====================================================================================================
+// Dense vkeys (the boundary's are dictionary codes, pcode * n_vehicles + vcode: stream.batch_columns, k_json_vkey):
+// a vkey below dense_cap keeps its max ts in dense[vkey] -- the ts with its sign bit flipped, so that unsigned order is
+// signed order and 0 (memset) is "no row yet" -- one 8-B load and, when the ts is a new max, one atomicMax; no probing,
+// no claims.  Larger vkeys take the hash table below.  (The hash table's probe path -- a key not in its home slot, a
+// quarter of them at load 1/2, and one such lane makes its whole wave probe with a full wait per step -- cost the bench
+// ~0.9 ms of k_ingest's 6.7: tools/variants/ingest_ddload.patch, profiles/r5/r5ab6/.)
 // The fused per-vkey max gives up on a key after DEDUP_FUSED_PROBES probes (its table was sized from the previous
 // batch and is too small); the first give-up is published in *dgiveup, a word on a cache line of its own, polled
 // every 16 rounds (polling a DevStats word every round, a line other atomics hit, made the ingest 4x slower), and
@@ -80,12 +86,13 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     unsigned long long dmask, unsigned int *dused, unsigned long long *n_dused, unsigned int *__restrict__ slow,
     unsigned long long *n_slow, unsigned long long *dgiveup, unsigned long long *wreg, unsigned long long *wcount,
     DevStats *st, const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid, unsigned *__restrict__ bin_cur,
-    EventRec *__restrict__ slabs, unsigned slab_cap) {
+    EventRec *__restrict__ slabs, unsigned slab_cap, unsigned long long *__restrict__ dense, unsigned long long dense_cap) {
     const int res = res_arg;
     __shared__ WinCacheL WC;
     __shared__ double Fc[20][3], Fu[20][2][3];   // the fast path's per-face tables (res parity): LDS reads
     __shared__ unsigned dskip;                    // the fused dedup has given up (*dgiveup) -- skip it
     __shared__ long long tmax_l[IG_THREADS];      // per-thread max ts (an LDS max per row instead of 2 live registers)
+    __shared__ long long vmax_l[IG_THREADS];      // per-thread max vkey + 1 of the deduplicated rows (the same way)
     for (int k = threadIdx.x; k < 60; k += IG_THREADS) (&Fc[0][0])[k] = (&c_tab.faceCenterPoint[0][0])[k];
     for (int k = threadIdx.x; k < 120; k += IG_THREADS) (&Fu[0][0][0])[k] = (&c_tab.fastU[res & 1][0][0][0])[k];
     // _faceIjkToH3's packed base-cell and digit tables in LDS (11.2 KB): from __constant__ memory they were lane-indexed vector loads
@@ -103,6 +110,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     // the cell computation, whose peak spilled the prefetched columns
     unsigned nvalid = 0, nlate = 0, bad = 0, wover = 0, binover = 0;
     tmax_l[threadIdx.x] = INT64_MIN;
+    vmax_l[threadIdx.x] = 0;
     bool dretry = false;
     int round = 0;
     const int64_t gstride = (int64_t)gridDim.x * IG_THREADS;
@@ -163,9 +171,14 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         // dedup: the vkey's home slot is loaded now, its latency hidden behind the cell computation (a plain load:
         // a stale copy can only show the slot empty or its max lower, both of which the atomics below correct)
         const bool dd = ok && v != EMPTY_VKEY && !__hip_atomic_load(&dskip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const bool dv = v < dense_cap;   // (dense_cap < 2^64 - 1: EMPTY_VKEY is never dense)
         const unsigned long long dh0 = vkey_hash(v) & dmask;
         DedupSlot d0{EMPTY_VKEY, 0};
-        if (dd) d0 = dtab[dh0];
+        unsigned long long dn = 0;
+        if (dd) {
+            if (dv) dn = dense[v];
+            else d0 = dtab[dh0];
+        }
         uint8_t fl = 0;
         int widx = -1, wslot = -1;
         int64_t ws = 0;
@@ -193,7 +206,12 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         long long dh = -1;
         bad += ok && v == EMPTY_VKEY;
         bool cand = false;
-        if (dd) {
+        if (dd) atomicMax(&vmax_l[threadIdx.x], (long long)(v < (1ull << 62) ? v + 1 : (1ull << 62)));
+        if (dd && dv) {
+            const long long cur = (long long)(dn ^ DENSE_SIGN);   // (0: INT64_MIN, no row yet)
+            cand = t >= cur;
+            if (t > cur) atomicMax(&dense[v], (unsigned long long)t ^ DENSE_SIGN);
+        } else if (dd) {
             long long cur = d0.maxts;
             if (d0.vkey == v) dh = (long long)dh0;   // the usual case: the key sits in its home slot
             else dh = find_or_claim_vkey_ts(dtab, dmask, v, claimed, DEDUP_FUSED_PROBES, cur);
@@ -254,11 +272,13 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     const unsigned long long wbad = wave_sum((unsigned long long)bad), wwover = wave_sum((unsigned long long)wover);
     const unsigned long long wbinover = kBin ? wave_sum((unsigned long long)binover) : 0ull;
     const long long tmax = wave_max(tmax_l[threadIdx.x]);
+    const long long vmax = wave_max(vmax_l[threadIdx.x]);
     const unsigned long long rt = __ballot(dretry);
     if (lane_id() == 0) {
         if (wvalid) atomicAdd(&st->n_valid, wvalid);
         if (wlate) atomicAdd(&st->n_late, wlate);
         if (tmax != INT64_MIN) atomicMax(&st->max_ts_ms, (long long)(tmax / 1000));   // trunc(max) = max(trunc)
+        if (vmax > 0) atomicMax(&st->vkey_max1, (unsigned long long)vmax);
         if (wbad) atomicAdd(&st->bad_vkey, wbad);
         if (wwover) atomicAdd(&st->win_overflow, wwover);
         if (rt) atomicAdd(&st->dedup_retry, 1ull);

@@ -200,7 +200,12 @@ struct DevStats {
     unsigned long long n_evicted;   // table mode: aggregates k_agg evicted into the buckets
     unsigned long long sample_max_run;   // k_sample_heavy: occurrences of the most frequent key in a key sample
     unsigned long long bin_overflow;     // k_ingest<true>: rows whose bin slab was full (the batch re-partitions)
+    unsigned long long vkey_max1;        // k_ingest: max vkey + 1 of its deduplicated rows (capped at 2^62; sizes the
+                                         // next batch's dense dedup table)
 };
+
+// the dense dedup table's word: a max ts with its sign bit flipped (k_ingest.h: unsigned order = signed order, 0 = none)
+constexpr unsigned long long DENSE_SIGN = 0x8000000000000000ull;
 
 HM_HD uint64_t mix64(uint64_t x) {
     x ^= x >> 33;

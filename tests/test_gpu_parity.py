@@ -260,10 +260,14 @@ def test_dedup_ties_c5_sample():
     eng.close()
 
 
-def test_dedup_more_vehicles_than_fused_table():
-    """k_ingest's fused dedup table is sized from the previous batch's distinct vehicles (>= 2^18 keys); a
-    first batch with 1.2M vehicles overflows its bounded probes, so the max pass reruns on a full-size table.
-    The second batch (sized from the first) takes the fused path. Both must equal the oracle."""
+@pytest.mark.parametrize("dense", ["1", "0"])
+def test_dedup_more_vehicles_than_fused_table(dense, monkeypatch):
+    """k_ingest's fused dedup: dense vkeys below the dense table's size (2^20 on a first batch, then sized from the
+    last batch's largest vkey) keep their max in it, the others in the hash table, which is sized from the previous
+    batch's distinct vehicles (>= 2^18 keys) -- the first batch's 1.2M vehicles (vkeys 0 .. 1.2M: 2^20 of them dense)
+    overflow its bounded probes without the dense table (dense "0": MOBHEAT_DEDUP_DENSE=0), so the max pass reruns on
+    a full-size table.  The second batch takes the fused path either way. Both must equal the oracle."""
+    monkeypatch.setenv("MOBHEAT_DEDUP_DENSE", dense)
     from mobheat import HeatmapEngine, synth
     from oracle.spark_oracle import SparkHeatmapOracle
     eng = HeatmapEngine(h3_res=8)
@@ -274,6 +278,28 @@ def test_dedup_more_vehicles_than_fused_table():
         res, exp = _run(eng, ora, b, epoch)
         assert_batch_equal(res, exp)
         assert len(res.latest_rows) >= 1_200_000
+    eng.close()
+
+
+def test_dedup_sparse_and_dense_vkeys():
+    """vkeys that are not dense codes (64-bit values: the hash table only, and the next batch without a dense table),
+    then dense ones (the dense table sized from scratch), then a mix of both in one batch."""
+    from mobheat import HeatmapEngine, synth
+    from oracle.spark_oracle import SparkHeatmapOracle
+    eng = HeatmapEngine(h3_res=7)
+    ora = SparkHeatmapOracle(h3_res=7)
+    rng = np.random.default_rng(5)
+    for epoch, kind in enumerate(("sparse", "sparse", "dense", "mixed", "dense")):
+        b = synth.c5_dedup(seed=60 + epoch, n_vehicles=30_000, updates=4)
+        b["ts_us"] = b["ts_us"] + epoch * 600_000_000
+        v = b["vkey"].astype(np.uint64)
+        big = (v * np.uint64(0x9E3779B97F4A7C15)) | np.uint64(1 << 40)
+        if kind == "sparse":
+            b["vkey"] = big
+        elif kind == "mixed":
+            b["vkey"] = np.where(rng.random(v.size) < 0.5, v, big).astype(np.uint64)
+        res, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res, exp)
     eng.close()
 
 
