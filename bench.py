@@ -88,7 +88,7 @@ STAGES = ["ingest", "aggregate", "send", "partition", "merge", "emit", "dedup"]
 CONCURRENT_STAGES = ("dedup",)   # side stream (hm_process_batch): its kernel_ms is the side-stream span
 # HBM traffic per dispatch of every kernel and k_ingest's VALU instruction mix per event of this workload, counted by
 # rocprofv3 PMC passes of this same command (tools/ingest_pmc.py -> profiles/r4/kernel_pmc.json).
-PMC_FILE = os.path.join(ROOT, "profiles", "r4", "kernel_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r5", "kernel_pmc.json")
 STAGE_KERNELS = {"ingest": ["k_ingest"], "aggregate": ["k_agg", "k_bin_reduce"], "send": ["k_stage_pack"],
                  "partition": ["k_ev_hist", "k_ev_scatter_rec"], "merge": ["k_merge_owned"], "emit": ["k_fill_gaps"],
                  "dedup": ["k_dedup_flag"]}
@@ -356,8 +356,12 @@ def main():
             "frac": gbs / HBM_PEAK_GBS, "traffic": None}
     pmc = ingest_pmc(args.res, n, world)
     if pmc is not None and all(k in pmc.get("kernels", {}) for k in STAGE_KERNELS[dom]):
-        # FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, per dispatch, summed over the stage's kernels
-        roof["traffic"] = sum(pmc["kernels"][k]["hbm_bytes"] for k in STAGE_KERNELS[dom])
+        # FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE, per dispatch, summed over the stage's kernels; a kernel
+        # whose patterns were calibrated (tools/pmc_calib.py: k_ingest's 8-B loads, returned atomics, scattered
+        # records on known byte counts) counts its calibrated bytes, the counted ones beside them
+        ks = [pmc["kernels"][k] for k in STAGE_KERNELS[dom]]
+        roof["traffic"] = sum(k.get("calibrated", {}).get("hbm_bytes", k["hbm_bytes"]) for k in ks)
+        roof["traffic_counted"] = sum(k["hbm_bytes"] for k in ks)
         roof["traffic_source"] = os.path.relpath(PMC_FILE, ROOT)
     if pmc is not None:
         # k_ingest is bound by VALU issue and latency, not HBM: its VALU side from the same PMC file
