@@ -281,6 +281,32 @@ def test_dedup_more_vehicles_than_fused_table(dense, monkeypatch):
     eng.close()
 
 
+def test_merge_many_duplicate_keys_per_chunk():
+    """Every key of a 6M-row binned batch occurs 4 times (1.5M keys, ~183 per bin, one window): a merge chunk of 512
+    records holds more keys with in-chunk duplicates than k_merge_owned's joiner accumulator pool (MO_ACC = 128), so
+    the joiners left over wait for a second pass of the chunk.  Counts and averages against the oracle, then the same
+    keys again in a second batch (every key existing)."""
+    from mobheat import HeatmapEngine
+    from oracle.spark_oracle import SparkHeatmapOracle
+    rng = np.random.default_rng(77)
+    m, rep = 1_500_000, 4
+    lat0 = np.degrees(np.arcsin(rng.uniform(-1, 1, m)))
+    lon0 = rng.uniform(-180, 180, m)
+    eng = HeatmapEngine(h3_res=8)
+    ora = SparkHeatmapOracle(h3_res=8)
+    t0 = 1759572000 * 1_000_000
+    for epoch in range(2):
+        perm = rng.permutation(m * rep)
+        idx = np.repeat(np.arange(m), rep)[perm]
+        n = m * rep
+        b = dict(lat=lat0[idx], lon=lon0[idx], ts_us=t0 + rng.integers(0, 240_000_000, n) + epoch * 1_000_000,
+                 speed=rng.uniform(0, 80, n).round(0), speed_valid=rng.random(n) >= 0.1,
+                 vkey=rng.integers(0, 40_000, n).astype(np.uint64), row_valid=np.ones(n, bool))
+        res, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res, exp)
+    eng.close()
+
+
 def test_dedup_sparse_and_dense_vkeys():
     """vkeys that are not dense codes (64-bit values: the hash table only, and the next batch without a dense table),
     then dense ones (the dense table sized from scratch), then a mix of both in one batch."""
