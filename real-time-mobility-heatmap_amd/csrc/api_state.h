@@ -4,7 +4,8 @@
 
 // ---- tile-state checkpoint (Spark's state store behind checkpointLocation, heatmap_stream.py:37,244) ----
 // Export: every live window's keys dumped by k_dump_gen (the growth path's kernel) into one GrowRec array, copied
-// to the caller; the touched word (this context's batch sequence) is cleared -- it means nothing elsewhere.
+// to the caller; the touched word (this context's batch sequence) is cleared on the device -- it means nothing
+// elsewhere (a host loop over the records cost ~10 ms per 1e7 keys).
 static void state_info_of(const hm_ctx *ctx, hm_state_info *info, int64_t n_keys) {
     memset(info, 0, sizeof(*info));
     info->epoch_id = ctx->epoch;
@@ -19,12 +20,13 @@ static void state_info_of(const hm_ctx *ctx, hm_state_info *info, int64_t n_keys
 // every live window's keys (only_seq != 0: those the batch with that sequence touched) into recs[0, n)
 static int state_dump(hm_ctx *ctx, hm_state_rec *recs, int64_t n, unsigned only_seq) {
     int rc;
+    ctx->touched_dump_seq = -1;   // (parts_regrow is overwritten)
     if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(n, 1) * sizeof(GrowRec)))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
     for (const auto &g : ctx->gens) {
         const GenDesc d = gen_desc(g);
         hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
-                           (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD, only_seq);
+                           (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD, only_seq, true);
     }
     HIPCHK(ctx, hipGetLastError());
     unsigned long long dumped = 0;
@@ -32,7 +34,6 @@ static int state_dump(hm_ctx *ctx, hm_state_rec *recs, int64_t n, unsigned only_
     HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     if ((int64_t)dumped != n) return set_err(ctx, HM_E_STATE, "state dump found %llu keys, expected %lld", dumped, (long long)n);
     if (n > 0) HIPCHK(ctx, hipMemcpy(recs, ctx->parts_regrow.p, n * sizeof(GrowRec), hipMemcpyDeviceToHost));
-    for (int64_t i = 0; i < n; i++) recs[i].reserved = 0;
     return HM_OK;
 }
 
@@ -59,28 +60,33 @@ int hm_state_export_touched(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs
     int64_t live = 0;
     for (const auto &g : ctx->gens) live += g.keys;
     state_info_of(ctx, info, live);
-    // the last batch's touched keys that are still live (a touched key of an evicted window went with its table)
+    // the last batch's touched keys that are still live (a touched key of an evicted window went with its table);
+    // the dump is kept for the call that fetches it (the caller's first call sizes its buffer: one scan of the
+    // tables per export, not two)
     int64_t n = 0;
-    if (ctx->seq > 0 && !ctx->gens.empty()) {
+    if (ctx->touched_dump_seq == (int64_t)ctx->seq) {
+        n = ctx->touched_dump_n;
+    } else if (ctx->seq > 0 && !ctx->gens.empty()) {
         int rc;
         if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(live, 1) * sizeof(GrowRec)))) return rc;
         HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
         for (const auto &g : ctx->gens) {
             const GenDesc d = gen_desc(g);
             hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
-                               (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD, seq32(ctx));
+                               (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD, seq32(ctx), true);
         }
         HIPCHK(ctx, hipGetLastError());
         unsigned long long dumped = 0;
         HIPCHK(ctx, hipMemcpyAsync(&dumped, ctx->d_scratch + REGROW_WORD, 8, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         n = (int64_t)dumped;
+        ctx->touched_dump_seq = (int64_t)ctx->seq;
+        ctx->touched_dump_n = n;
     }
     *n_out = n;
     if (!recs) return HM_OK;
     if (cap < n) return set_err(ctx, HM_E_INVALID, "%lld touched keys do not fit %lld records", (long long)n, (long long)cap);
     if (n > 0) HIPCHK(ctx, hipMemcpy(recs, ctx->parts_regrow.p, n * sizeof(GrowRec), hipMemcpyDeviceToHost));
-    for (int64_t i = 0; i < n; i++) recs[i].reserved = 0;
     return HM_OK;
 }
 
@@ -134,6 +140,7 @@ int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *
     }
     if ((rc = gens_upload(ctx))) return rc;
     if (n > 0) {
+        ctx->touched_dump_seq = -1;
         if ((rc = ensure(ctx, ctx->parts_regrow, n * sizeof(GrowRec)))) return rc;
         HIPCHK(ctx, hipMemcpy(ctx->parts_regrow.p, recs, n * sizeof(GrowRec), hipMemcpyHostToDevice));
         HIPCHK(ctx, hipMemsetAsync(&ctx->d_st->overflow, 0, 8, ctx->stream));

@@ -69,6 +69,8 @@ struct hm_ctx {
     DevBuf s_cell, s_ws, s_cnt, s_sp, s_spn, s_lon, s_lat;   // k_merge_owned's rows in per-bin segments (with gaps)
     DevBuf bin_cnt, bin_off;          // k_merge_owned: touched keys per bin, their output offsets
     DevBuf parts_regrow;              // growth: the old tables' keys as partial records
+    int64_t touched_dump_seq = -1;    // parts_regrow holds hm_state_export_touched's dump of batch seq (-1: none)
+    int64_t touched_dump_n = 0;
     DevBuf parts_regrow_sorted;       // growth: the same, partitioned (not parts_sorted: a binned batch's slabs are there)
     // multi-GPU exchange (api_stage.h): chunk starts and headers, the local -> global window slot map; the owner's
     // per-sender bin counts and their scan, its bins' segments, the received candidates and table-mode partials
@@ -750,6 +752,7 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census, bool r
     if (!old.empty()) {
         int64_t moved = 0;
         for (const auto &g : old) moved += g.keys;
+        ctx->touched_dump_seq = -1;
         if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(moved, 1) * sizeof(GrowRec)))) return rc;
         HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
         for (const auto &g : old) {

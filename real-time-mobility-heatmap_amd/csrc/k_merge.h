@@ -24,8 +24,9 @@ __global__ __launch_bounds__(256) void k_census(const TilePartial *__restrict__ 
 // growth: the live keys of one window's old table as partial records (aux = the key's touched word), to be
 // merged into its new table by k_merge_owned in rehash mode
 // (only_seq != 0: only the keys whose touched word carries that batch sequence -- an incremental checkpoint)
+// (clear_touched: a checkpoint export -- the touched word means nothing outside this context)
 __global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, GrowRec *__restrict__ out, unsigned long long *n_out,
-                                                  unsigned only_seq = 0) {
+                                                  unsigned only_seq = 0, bool clear_touched = false) {
     const unsigned long long cap = (g.rmask + 1) << g.rbits;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < (int64_t)cap; base += stride) {
@@ -42,7 +43,7 @@ __global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, GrowRec *__restrict
             p.sspeed = sl.sspeed;
             p.slat = sl.slat;
             p.slon = sl.slon;
-            p.touched = sl.touched;
+            p.touched = clear_touched ? 0ull : sl.touched;
         }
         const unsigned long long pos = wave_append(live, n_out);
         if (live) out[pos] = p;
