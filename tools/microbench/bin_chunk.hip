@@ -20,15 +20,19 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
-constexpr int BINS = 8192;
+#ifndef BINS_N
+#define BINS_N 8192
+#endif
+constexpr int BINS = BINS_N;
 
 __device__ __forceinline__ uint64_t mixh(uint64_t x) {
     x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33; return x;
 }
-__device__ __forceinline__ unsigned bin_of(int64_t i) { return (unsigned)(mixh((uint64_t)i) >> 51); }   // 13 bits
+__device__ __forceinline__ unsigned bin_of(int64_t i) { return (unsigned)(mixh((uint64_t)i) >> (64 - __builtin_ctz(BINS))); }   // log2(BINS) bits
 __device__ __forceinline__ unsigned xcc_id() { return __builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 7u; }
 
 __global__ __launch_bounds__(512) void k_seq(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n) {
@@ -223,7 +227,8 @@ int main(int argc, char **argv) {
     uint4 *src, *dst;
     unsigned *cur, *slot;
     unsigned long long *holes;
-    const size_t dst_bytes = (size_t)BINS * 48000 * 32;   // >= every pattern's slabs (chunk 16: cap + 1024 * 16 slots per bin)
+    // >= every pattern's slabs (chunk 16: cap + 1024 * 16 slots per bin; per-XCD sub-slabs: 8 x (cap / 8 x 2 + 512))
+    const size_t dst_bytes = (size_t)BINS * std::max<size_t>(48000, 2 * (size_t)cap + 8 * 512 + 1024 * 16) * 32;
     CHK(hipMalloc(&src, n * 32));
     CHK(hipMalloc(&dst, dst_bytes));
     CHK(hipMalloc(&cur, BINS * 8 * 4));
