@@ -89,6 +89,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     if (const char *m = getenv("MOBHEAT_DEDUP_STREAM")) ctx->dedup_main = !strcmp(m, "main");
     if (const char *m = getenv("MOBHEAT_STAGE_SELF")) ctx->self_hold_ok = strcmp(m, "copy") != 0;
     if (const char *m = getenv("MOBHEAT_DEDUP_DENSE")) ctx->dense_ok = strcmp(m, "0") != 0;
+    if (const char *m = getenv("MOBHEAT_SUBBINS")) ctx->subbins_mode = !strcmp(m, "0") ? 0 : !strcmp(m, "1") ? 1 : 2;
     // the registry, its census and the batch statistics side by side (one reset, one readback after k_ingest)
     if (hipMalloc(&ctx->d_wreg, REG_BLOCK_BYTES) != hipSuccess || !(ctx->d_wcount = ctx->d_wreg + WREG_SLOTS + 1) ||
         !(ctx->d_st = (DevStats *)(ctx->d_wreg + 2 * (WREG_SLOTS + 1))) ||
@@ -102,7 +103,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         return fail("create");
     }
     if (hipMalloc(&ctx->d_scratch, 256 * 8) != hipSuccess || hipHostMalloc(&ctx->h_scratch, 256 * 8) != hipSuccess ||
-        hipHostMalloc(&ctx->h_bincur, (RP_BINS + 1) * 4, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(&ctx->h_bincur, ((RP_BINS << SUB_BITS) + 1) * 4, hipHostMallocDefault) != hipSuccess) {
         ctx->err = "stats alloc";
         return fail("create");
     }
@@ -269,7 +270,8 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     I.n = in->n;
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
     // 2. snap + window registry + event keys
-    if ((rc = phase_local(ctx, I, late_wm, true))) return rc;
+    const bool sub = ctx->subbins_mode == 1 || (ctx->subbins_mode == 2 && ctx->merge_coop);
+    if ((rc = phase_local(ctx, I, late_wm, true, sub))) return rc;
     DevStats s1 = *ctx->h_st;
     const int64_t n_agg = (int64_t)s1.n_valid - (int64_t)s1.n_late;
     // the aggregation path of this batch (table mode: two LDS passes first; direct: every row a record)

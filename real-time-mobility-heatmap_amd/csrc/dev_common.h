@@ -73,7 +73,7 @@ __device__ __forceinline__ int gmap_find(const GenDesc *gm, unsigned long long w
     return -1;
 }
 __device__ __forceinline__ unsigned long long home_slot(const GenDesc &g, uint64_t h) {
-    return ((unsigned long long)((region_field(h) >> g.sb) - g.rbase) << g.rshift) | (h & g.rmask);
+    return ((unsigned long long)((region_field(h) >> g.sb) - g.rbase) << g.rshift) | inreg_slot(h, g.rmask);
 }
 // linear probing wraps inside the key's region
 __device__ __forceinline__ unsigned long long next_slot(unsigned long long s, unsigned long long rmask) {

@@ -19,15 +19,16 @@ static bool choose_binned(const hm_ctx *ctx, int64_t n) {
 // wide), so the mean + 25% + 256 overflows only on skewed keys (then the batch re-partitions from its keys)
 // (clustered keys -- a key's rows share its bin -- widen that; the last binned batch's fullest bin / mean, `skew`, with
 // 10% room, covers a stream whose clustering is steady)
-static unsigned slab_cap_for(int64_t n, double skew) {
-    const int64_t m = (n + RP_BINS - 1) / RP_BINS;
+static unsigned slab_cap_for(int64_t n, double skew, int64_t nbins) {
+    const int64_t m = (n + nbins - 1) / nbins;
     const int64_t c = std::max<int64_t>(m + m / 4 + 256, (int64_t)(skew * 1.1 * (double)m) + 256);
     return (unsigned)std::min<int64_t>((c + 1) & ~int64_t(1), (int64_t)UINT32_MAX / 2);   // (even: 64-B aligned slabs)
 }
 
 // k_ingest + k_ingest_exact: flags, event keys, the window registry and its census, dedup max, batch statistics;
-// allow_bin: the batch may bin its rows in k_ingest (hm_process_batch; not the stage API)
-static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool allow_bin = false) {
+// allow_bin: the batch may bin its rows in k_ingest; sub: in sub-bins (hm_process_batch; the stage API's senders keep
+// whole bins, the unit its chunks and self-held segments are made of)
+static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool allow_bin = false, bool sub = false) {
     int64_t n = I.n;
     int rc;
     if ((rc = ensure(ctx, ctx->flags, n)) || (rc = ensure(ctx, ctx->win, n)) || (rc = ensure(ctx, ctx->rows, n * 8)) ||
@@ -50,16 +51,18 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
         }
     }
     const bool bin = allow_bin && n > 0 && choose_binned(ctx, n);
-    ctx->slab_cap = bin ? slab_cap_for(n, ctx->bin_skew) : 0;
+    ctx->sub_bits = bin && sub ? SUB_BITS : 0;
+    const int nbins = RP_BINS << ctx->sub_bits;
+    ctx->slab_cap = bin ? slab_cap_for(n, ctx->bin_skew, nbins) : 0;
     ctx->binned = false;
-    if ((rc = ensure(ctx, ctx->bin_cur, (RP_BINS + 1) * 4))) return rc;
+    if ((rc = ensure(ctx, ctx->bin_cur, ((RP_BINS << SUB_BITS) + 1) * 4))) return rc;
     // (+ 64 slack records: k_ev_scatter_rec's, when a slab overflows and the batch is re-partitioned)
-    if (bin && (rc = ensure(ctx, ctx->parts_sorted, ((size_t)RP_BINS * ctx->slab_cap + 64) * sizeof(EventRec)))) return rc;
+    if (bin && (rc = ensure(ctx, ctx->parts_sorted, ((size_t)nbins * ctx->slab_cap + 64) * sizeof(EventRec)))) return rc;
     {
         const int nw = 2 * (WREG_SLOTS + 1);   // d_wreg and d_wcount: one allocation (hm_create)
-        hipLaunchKernelGGL(k_batch_reset, dim3((nw + 255) / 256), dim3(256), 0, ctx->stream, (unsigned long long *)ctx->d_st,
-                           ctx->d_scratch + SLOW_WORD, ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, nw, (unsigned *)ctx->bin_cur.p,
-                           RP_BINS + 1);
+        hipLaunchKernelGGL(k_batch_reset, dim3((std::max(nw, nbins + 1) + 255) / 256), dim3(256), 0, ctx->stream,
+                           (unsigned long long *)ctx->d_st, ctx->d_scratch + SLOW_WORD, ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg,
+                           nw, (unsigned *)ctx->bin_cur.p, nbins + 1);
         HIPCHK(ctx, hipGetLastError());
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
@@ -90,13 +93,13 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
                                ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
                                ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st, I.sp, I.sv,
                                (unsigned *)ctx->bin_cur.p, bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap,
-                               (unsigned long long *)ctx->dense.p, ctx->dense_cap);
+                               (unsigned long long *)ctx->dense.p, ctx->dense_cap, ctx->sub_bits);
         }
         ctx->n_h2d = 0;
         hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, ctx->cfg.h3_res,
                            (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, (uint64_t *)ctx->keys.p, I.sp, I.sv,
                            (const unsigned long long *)ctx->d_wreg, (unsigned *)ctx->bin_cur.p,
-                           bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap, ctx->d_st);
+                           bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap, ctx->d_st, ctx->sub_bits);
         hipLaunchKernelGGL(k_sample_heavy, dim3(1), dim3(HS_THREADS), 0, ctx->stream, (const uint64_t *)ctx->keys.p, n, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
         ctx->dfused.dirty = true;
@@ -104,12 +107,12 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
     // the batch statistics and the registry with its census, read back together
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_wreg, ctx->d_wreg, REG_BLOCK_BYTES, hipMemcpyDeviceToHost, ctx->stream));   // (+ h_wcount, h_st)
-    if (bin) HIPCHK(ctx, hipMemcpyAsync(ctx->h_bincur, ctx->bin_cur.p, RP_BINS * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (bin) HIPCHK(ctx, hipMemcpyAsync(ctx->h_bincur, ctx->bin_cur.p, (size_t)nbins * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     if (bin) {   // the fullest bin against the mean: the next batch's slab room
         unsigned long long tot = 0, mx = 0;
-        for (int b = 0; b < RP_BINS; b++) { tot += ctx->h_bincur[b]; mx = std::max<unsigned long long>(mx, ctx->h_bincur[b]); }
-        if (tot) ctx->bin_skew = std::max(1.0, (double)mx * RP_BINS / (double)tot);
+        for (int b = 0; b < nbins; b++) { tot += ctx->h_bincur[b]; mx = std::max<unsigned long long>(mx, ctx->h_bincur[b]); }
+        if (tot) ctx->bin_skew = std::max(1.0, (double)mx * nbins / (double)tot);
     }
     if (ctx->h_st->win_overflow)
         return set_err(ctx, HM_E_OVERFLOW, "more than %d distinct windows in one micro-batch (%llu rows)", WREG_SLOTS,
@@ -292,14 +295,32 @@ static int merge_events(hm_ctx *ctx, const Inputs &I, int64_t n_rec) {
     if ((rc = gens_prepare(ctx, census, binned)) || (rc = winfo_upload(ctx, true))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
     int64_t ntiles = 1;
-    if (binned) {
+    const bool subs = binned && ctx->sub_bits;
+    Segs seg;
+    if (subs) {   // each bin's sub-slabs as its segments, in sub-region order (k_sub_segments)
+        constexpr int NS = 1 << SUB_BITS;
+        static_assert(SUB_BITS == 3, "k_sub_segments and the merge's segment table assume 8 sub-bins");
+        if ((rc = ensure(ctx, ctx->rp_O, (RP_BINS + 1) * 8)) || (rc = ensure(ctx, ctx->stage_SO, (size_t)RP_BINS * NS * 8)) ||
+            (rc = ensure(ctx, ctx->stage_SP, (size_t)RP_BINS * NS * 4)) || (rc = ensure(ctx, ctx->stage_T, (RP_BINS + 1) * 4)))
+            return rc;
+        hipLaunchKernelGGL(k_sub_segments, dim3(grid_for(RP_BINS + 1, 256)), dim3(256), 0, ctx->stream, (const unsigned *)ctx->bin_cur.p,
+                           (const EventRec *)ctx->parts_sorted.p, (int64_t)ctx->slab_cap, (unsigned long long *)ctx->stage_SO.p,
+                           (unsigned *)ctx->stage_SP.p, (unsigned *)ctx->stage_T.p);
+        HIPCHK(ctx, hipGetLastError());
+        if ((rc = scan_counts(ctx, (const unsigned *)ctx->stage_T.p, RP_BINS + 1, (unsigned long long *)ctx->rp_O.p))) return rc;
+        seg.SO = (const unsigned long long *)ctx->stage_SO.p;
+        seg.SP = (const unsigned *)ctx->stage_SP.p;
+        seg.nseg = NS;
+    } else if (binned) {
         if ((rc = ensure(ctx, ctx->rp_O, (RP_BINS + 1) * 8))) return rc;
         if ((rc = scan_counts(ctx, (const unsigned *)ctx->bin_cur.p, RP_BINS + 1, (unsigned long long *)ctx->rp_O.p))) return rc;
     } else if ((rc = ev_partition(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, ntiles))) {
         return rc;
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));
-    if ((rc = merge_sorted<EventRec>(ctx, I.n, ntiles, binned ? ctx->slab_cap : 0))) return rc;
+    if (subs) rc = merge_sorted<EventRec>(ctx, I.n, 1, 0, (const EventRec *)ctx->parts_sorted.p, seg);
+    else rc = merge_sorted<EventRec>(ctx, I.n, ntiles, binned ? ctx->slab_cap : 0);
+    if (rc) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
     if ((rc = rows_densify(ctx, ntiles))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[5], ctx->stream));

@@ -130,6 +130,13 @@ struct hm_ctx {
     unsigned *h_bincur = nullptr;    // the cursors read back (pinned): the fullest bin sizes the next batch's slabs
     double bin_skew = 1.0;           // the last binned batch's fullest bin / mean bin
     bool binned = false;             // this batch's rows are in their bins (k_ingest<true>, no slab overflowed)
+    // the bins split into sub-bins by sub-region (k_ingest sub_bits: SUB_BITS, or 0 = whole bins): on hm_process_batch's
+    // binned batches when the last batch re-touched mostly existing keys (merge_coop) -- its merge then reads old state
+    // lines inside 1/8 of each region at a time (state-read leg 6.6-6.75 -> 5.25-5.36 ms), while a batch of new keys
+    // keeps whole bins (65536 cursors and slabs cost k_ingest +0.5-0.7 ms and gain its merge nothing: profiles/r5/r5sub/);
+    // the stage API's senders keep whole bins.  MOBHEAT_SUBBINS=0 never, =1 always (tests, A/B)
+    unsigned sub_bits = 0;
+    int subbins_mode = 2;
     unsigned long long *d_wreg = nullptr, *h_wreg = nullptr;     // the batch's window registry (WREG_SLOTS wenc)
     unsigned long long *d_wcount = nullptr, *h_wcount = nullptr; // aggregated rows per registry slot (census)
     WInfo *d_winfo = nullptr, *h_winfo = nullptr;   // per registry slot: window parameters of the direct path

@@ -74,7 +74,8 @@ __device__ __forceinline__ void wave_count_slots(bool pred, int slot, unsigned *
 // 32-B EventRec goes straight to its bin's slab -- bin = the key hash's region field (every window of such a batch
 // has 2^REGION_BITS regions, so region = bin, kernels.h) at slab b * slab_cap + a returned atomic on the bin's
 // cursor -- instead of a later histogram + scatter pass over the keys and columns.  A bin past slab_cap counts in
-// DevStats.bin_overflow and the host partitions the batch from its keys instead.
+// DevStats.bin_overflow and the host partitions the batch from its keys instead.  sub_bits (hm_process_batch: SUB_BITS;
+// the stage API: 0): each bin split into the key's sub-regions (kernels.h inreg_slot), slab (bin << sub_bits) | sub.
 // (one kernel for every resolution: per-resolution specialisations of this kernel, measured no faster once the digits
 // came from the step tables, were miscompiled at res 3 by this compiler -- wrong cells, caught by
 // test_ingest_cells_every_resolution, profiles/r4/r4w/)
@@ -86,7 +87,8 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     unsigned long long dmask, unsigned int *dused, unsigned long long *n_dused, unsigned int *__restrict__ slow,
     unsigned long long *n_slow, unsigned long long *dgiveup, unsigned long long *wreg, unsigned long long *wcount,
     DevStats *st, const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid, unsigned *__restrict__ bin_cur,
-    EventRec *__restrict__ slabs, unsigned slab_cap, unsigned long long *__restrict__ dense, unsigned long long dense_cap) {
+    EventRec *__restrict__ slabs, unsigned slab_cap, unsigned long long *__restrict__ dense, unsigned long long dense_cap,
+    unsigned sub_bits) {
     const int res = res_arg;
     __shared__ WinCacheL WC;
     __shared__ double Fc[20][3], Fu[20][2][3];   // the fast path's per-face tables (res parity): LDS reads
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
                     if (wslot >= 0) __hip_atomic_store(&WC.inner[wslot], inner, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 const uint64_t h = mix64(cell ^ inner);
-                const unsigned b = region_field(h);
+                const unsigned b = (region_field(h) << sub_bits) | (sub_field(h) & ((1u << sub_bits) - 1));
                 const unsigned p = atomicAdd(&bin_cur[b], 1u);
                 if (p < slab_cap) {
                     const uint64_t sp = svb == 0 ? SPEED_NULL_BITS
@@ -294,7 +296,7 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
                                                       uint64_t *__restrict__ keys, const double *__restrict__ speed,
                                                       const uint8_t *__restrict__ speed_valid, const unsigned long long *wreg,
                                                       unsigned *__restrict__ bin_cur, EventRec *__restrict__ slabs, unsigned slab_cap,
-                                                      DevStats *st) {
+                                                      DevStats *st, unsigned sub_bits) {
     const int64_t m = (int64_t)*n_slow;
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (int64_t)gridDim.x * blockDim.x) {
         const unsigned i = slow[q];
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
         keys[i] = key;
         if (slabs) {
             const uint64_t h = mix64(cell ^ window_inner(wdec(wreg[ekey_widx(key)])));
-            const unsigned b = region_field(h);
+            const unsigned b = (region_field(h) << sub_bits) | (sub_field(h) & ((1u << sub_bits) - 1));
             const unsigned p = atomicAdd(&bin_cur[b], 1u);
             if (p >= slab_cap) { atomicAdd(&st->bin_overflow, 1ull); continue; }
             const bool sv = speed && (!speed_valid || speed_valid[i]);

@@ -348,7 +348,7 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             if (r >= 0) {
                 const unsigned rmask = S.res_mask[r], off = S.res_off[r];
                 TileSlot *const base = S.res_slots[r];
-                unsigned s = (unsigned)hk & rmask;
+                unsigned s = (unsigned)inreg_slot(hk, rmask);
                 // Tags scanned 8 at a time (one 8-B LDS read): only slots whose tag is empty or this key's are visited
                 // one by one, so a wave's loop runs its lanes' longest count of such slots, not of probed slots.
                 // (regions are >= 256 slots and start at multiples of their size: a word never crosses a region)
@@ -448,7 +448,7 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                 rmask = S.res_mask[r];
                 off = S.res_off[r];
                 base = S.res_slots[r];
-                s = (unsigned)hk & rmask;
+                s = (unsigned)inreg_slot(hk, rmask);
             }
             const unsigned long long tgv = (unsigned long long)tg * UINT64_C(0x0101010101010101);
             const unsigned long long *tags64 = (const unsigned long long *)mo_tags;

@@ -227,6 +227,25 @@ __global__ __launch_bounds__(256) void k_stage_segments(const uint8_t *__restric
         T[k] = acc;
     }
 }
+// One GPU's binned batch in sub-bins (k_ingest sub_bits = SUB_BITS): bin k's 2^SUB_BITS sub-slabs as the segments of
+// k_merge_owned's kSeg variant, in sub-region order -- SO the sub-slab's address, SP the bin's records in earlier
+// sub-slabs, T[k] the bin's records (scan input; T[RP_BINS] = 0)
+__global__ __launch_bounds__(256) void k_sub_segments(const unsigned *__restrict__ cur, const EventRec *slabs, int64_t slab_cap,
+                                                      unsigned long long *__restrict__ SO, unsigned *__restrict__ SP,
+                                                      unsigned *__restrict__ T) {
+    constexpr int NS = 1 << SUB_BITS;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k <= RP_BINS; k += gridDim.x * blockDim.x) {
+        if (k == RP_BINS) { T[k] = 0; continue; }
+        unsigned acc = 0;
+        for (int s = 0; s < NS; s++) {
+            const int64_t q = (int64_t)k * NS + s;
+            SO[q] = (unsigned long long)(uintptr_t)(slabs + q * slab_cap);
+            SP[q] = acc;
+            acc += cur[q];
+        }
+        T[k] = acc;
+    }
+}
 // the chunks' counts as one u32 array per sender (scan input: [s][0, bins])
 __global__ __launch_bounds__(256) void k_stage_counts(const uint8_t *__restrict__ recv, const int64_t *__restrict__ chunk_off,
                                                       int nseg, unsigned bins, unsigned *__restrict__ C) {

@@ -525,15 +525,18 @@ def test_window_tables_growth_many_windows_and_reuse():
     eng.close()
 
 
-@pytest.mark.parametrize("mode", ["direct", "table", "binned"])
+@pytest.mark.parametrize("mode", ["direct", "table", "binned", "binned_whole"])
 def test_ingest_modes_parity(mode, monkeypatch):
     """The aggregation paths pinned (MOBHEAT_INGEST_MODE): direct (every aggregated row a 32-B record through the
-    partition and merge), binned (the same records written into their bins by k_ingest itself; a batch whose hot keys
-    overflow a bin's slab falls back to the partition) and table (k_agg's LDS table with hot-key retention +
-    k_bin_reduce, picked adaptively for low-cardinality batches) give the oracle's results on a multi-batch stream with
-    late rows, ties, nulls, an empty batch, many windows and few hot keys."""
+    partition and merge), binned (the same records written into their sub-bins by k_ingest itself, merged a bin's
+    sub-slabs in order -- MOBHEAT_SUBBINS=1; a batch whose hot keys overflow a slab falls back to the partition;
+    binned_whole: whole bins, MOBHEAT_SUBBINS=0) and table (k_agg's LDS table with hot-key retention + k_bin_reduce, picked adaptively for
+    low-cardinality batches) give the oracle's results on a multi-batch stream with late rows, ties, nulls, an empty
+    batch, many windows and few hot keys."""
     from mobheat import HeatmapEngine, synth
     from oracle.spark_oracle import SparkHeatmapOracle
+    monkeypatch.setenv("MOBHEAT_SUBBINS", "0" if mode == "binned_whole" else "1")
+    mode = "binned" if mode == "binned_whole" else mode
     monkeypatch.setenv("MOBHEAT_INGEST_MODE", mode)
     rng = np.random.default_rng(31)
     binned = []
@@ -557,7 +560,7 @@ def test_ingest_modes_parity(mode, monkeypatch):
     eng.close()
 
 
-@pytest.mark.parametrize("mode", ["direct", "binned"])
+@pytest.mark.parametrize("mode", ["direct", "binned", "binned_whole"])
 def test_direct_merge_keys_repeated_across_chunks(mode, monkeypatch):
     """k_merge_owned with every key in several consecutive 512-record chunks of its bin (direct path forced: 1.2e7 rows
     over ~5e5 res-11 keys, ~1.5k rows per bin): a chunk's stores are only drained by the next chunk's full barrier, so
@@ -565,6 +568,8 @@ def test_direct_merge_keys_repeated_across_chunks(mode, monkeypatch):
     still add up exactly; a second batch in the same window re-reads every key's state."""
     from mobheat import HeatmapEngine, synth
     from oracle.spark_oracle import SparkHeatmapOracle
+    monkeypatch.setenv("MOBHEAT_SUBBINS", "0" if mode == "binned_whole" else "1")
+    mode = "binned" if mode == "binned_whole" else mode
     monkeypatch.setenv("MOBHEAT_INGEST_MODE", mode)
     rng = np.random.default_rng(77)
     eng = HeatmapEngine(h3_res=11)
