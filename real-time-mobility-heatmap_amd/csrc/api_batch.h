@@ -87,6 +87,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     // MOBHEAT_DEDUP_STREAM=main runs the dedup on the main stream after the merge path (its cost to the overlapped
     // kernels, measured by the bench with and without it); default: the side stream
     if (const char *m = getenv("MOBHEAT_DEDUP_STREAM")) ctx->dedup_main = !strcmp(m, "main");
+    if (const char *m = getenv("MOBHEAT_DEDUP_EARLY")) ctx->early_ok = strcmp(m, "0") != 0;
     if (const char *m = getenv("MOBHEAT_STAGE_SELF")) ctx->self_hold_ok = strcmp(m, "copy") != 0;
     if (const char *m = getenv("MOBHEAT_DEDUP_DENSE")) ctx->dense_ok = strcmp(m, "0") != 0;
     if (const char *m = getenv("MOBHEAT_SUBBINS")) ctx->subbins_mode = !strcmp(m, "0") ? 0 : !strcmp(m, "1") ? 1 : 2;
@@ -271,7 +272,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
     // 2. snap + window registry + event keys
     const bool sub = ctx->subbins_mode == 1 || (ctx->subbins_mode == 2 && ctx->merge_coop);
-    if ((rc = phase_local(ctx, I, late_wm, true, sub))) return rc;
+    if ((rc = phase_local(ctx, I, late_wm, true, sub, ctx->early_ok && !ctx->dedup_main))) return rc;
     DevStats s1 = *ctx->h_st;
     const int64_t n_agg = (int64_t)s1.n_valid - (int64_t)s1.n_late;
     // the aggregation path of this batch (table mode: two LDS passes first; direct: every row a record)
@@ -280,9 +281,12 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     // 4. dedup over the batch's valid rows -- on the side stream, concurrently with step 3 (the rerun of the max on a
     // full table, after the fused one gave up, prepares that table on the main stream: it stays there)
     ctx->dedup_side = s1.dedup_retry == 0 && !ctx->dedup_main;
-    // (launched here, ahead of the partition: 1-3% faster on the bench than launched after the merge path's kernels,
-    // ~5% faster than overlapping the merge only, 2-4% faster than behind k_ev_hist -- profiles/r3/r3ab12/, r3ab13/)
-    if (ctx->dedup_side) {
+    // (launched behind k_ingest -- phase_local, early_dedup -- or else here, ahead of the partition: 1-3% faster on the
+    // bench than launched after the merge path's kernels, ~5% faster than overlapping the merge only, 2-4% faster than
+    // behind k_ev_hist -- profiles/r3/r3ab12/, r3ab13/)
+    if (ctx->dedup_early && !ctx->dedup_side)   // (the fused max gave up: the rerun below overwrites its outputs)
+        HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[2], 0));
+    if (ctx->dedup_side && !ctx->dedup_early) {
         HIPCHK(ctx, hipEventRecord(ctx->side_ev[0], ctx->stream));
         HIPCHK(ctx, hipStreamWaitEvent(ctx->side_stream, ctx->side_ev[0], 0));
         if ((rc = launch_side_dedup(ctx, &I))) return rc;

@@ -28,7 +28,12 @@ static unsigned slab_cap_for(int64_t n, double skew, int64_t nbins) {
 // k_ingest + k_ingest_exact: flags, event keys, the window registry and its census, dedup max, batch statistics;
 // allow_bin: the batch may bin its rows in k_ingest; sub: in sub-bins (hm_process_batch; the stage API's senders keep
 // whole bins, the unit its chunks and self-held segments are made of)
-static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool allow_bin = false, bool sub = false) {
+// early_dedup (hm_process_batch): the latest-position dedup launched on the side stream right behind the ingest, so
+// that it runs while the host reads the batch statistics back and prepares the merge (it assumes the fused max did not
+// give up; hm_process_batch reruns it on the main stream when it did)
+static int launch_side_dedup(hm_ctx *ctx, const Inputs *I);
+static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool allow_bin = false, bool sub = false,
+                       bool early_dedup = false) {
     int64_t n = I.n;
     int rc;
     if ((rc = ensure(ctx, ctx->flags, n)) || (rc = ensure(ctx, ctx->win, n)) || (rc = ensure(ctx, ctx->rows, n * 8)) ||
@@ -105,6 +110,11 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
         ctx->dfused.dirty = true;
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+    ctx->dedup_early = early_dedup && n > 0;
+    if (ctx->dedup_early) {
+        HIPCHK(ctx, hipStreamWaitEvent(ctx->side_stream, ctx->ev[1], 0));
+        if ((rc = launch_side_dedup(ctx, &I))) return rc;
+    }
     // the batch statistics and the registry with its census, read back together
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_wreg, ctx->d_wreg, REG_BLOCK_BYTES, hipMemcpyDeviceToHost, ctx->stream));   // (+ h_wcount, h_st)
     if (bin) HIPCHK(ctx, hipMemcpyAsync(ctx->h_bincur, ctx->bin_cur.p, (size_t)nbins * 4, hipMemcpyDeviceToHost, ctx->stream));

@@ -35,6 +35,8 @@ struct hm_ctx {
     hipEvent_t side_ev[4] = {};   // [3]: the pooled tables' tags cleared (table_release)
     bool dedup_side = false;
     bool dedup_main = false;   // MOBHEAT_DEDUP_STREAM=main: never the side stream
+    bool dedup_early = false;  // this batch's side-stream dedup was launched behind k_ingest (phase_local)
+    bool early_ok = true;      // MOBHEAT_DEDUP_EARLY=0: launched after the readback instead (A/B)
     hipEvent_t h2d_ev[H2D_CHUNKS] = {};
     struct H2D { const void *src; void *dst; size_t el; };
     H2D h2d[7] = {};
