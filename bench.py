@@ -36,6 +36,7 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 T0 = 1759572000 * 1_000_000
 SPAN_US = 15 * 60 * 1_000_000
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+BIN_STORE_FLOOR_MS_PER_1E8 = 4.04   # 1e8 32-B records binned into 8192 bins, no other work (profiles/r5/r5mb3/)
 FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 vector peak: 1024 SIMDs x 16 FMA lanes x 2 x 2.4 GHz
 SIMDS = 1024
 
@@ -377,6 +378,13 @@ def main():
                                "active_inst_valu_per_busy_cu_cycle": pmc["active_inst_valu_per_busy_cu_cycle"],
                                "valu_wave_insts_per_64_events": pmc["valu_wave_insts_per_64_events"],
                                "fp64_flops_per_event": pmc["fp64_flops_per_event"]}
+    if dom == "ingest" and c.get("binned"):
+        # what bounds the binned ingest instead of HBM bandwidth: its records' scattered 32-B
+        # stores and bin-cursor atomics alone, 1e8 records into 8192 bins, measured by tools/microbench/bin_chunk.hip
+        # ("direct" pattern, profiles/r5/r5mb3/direct_8192.txt) -- scaled to this launch's records
+        floor_ms = BIN_STORE_FLOOR_MS_PER_1E8 * c["partials"] / 1e8
+        roof["binning_floor"] = {"ms": floor_ms, "frac": floor_ms / avg_ms["ingest"] if avg_ms["ingest"] > 0 else None,
+                                 "source": "profiles/r5/r5mb3/direct_8192.txt"}
     step_bytes = sum(kb.values())
     roof.update({"kernel_ms": {k: round(v, 3) for k, v in avg_ms.items()}, "concurrent_stages": list(CONCURRENT_STAGES),
                  "algorithmic_bytes_per_launch": kb[dom],
