@@ -73,6 +73,18 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         hipFuncAttributes fa{};
         if (hipFuncGetAttributes(&fa, kern) == hipSuccess && fa.sharedSizeBytes > 0)
             per_cu = std::min<int>(per_cu, (int)(163840 / fa.sharedSizeBytes));
+        // k_ingest<true> (the binned ingest) runs 2 workgroups per CU, not the 6 that fit: its time is its records'
+        // scattered stores and bin-cursor atomics, which fewer waves in flight contend less for -- 5.41-5.50 ms at 2
+        // against 5.62-5.67 at 3 and 5.88-5.97 at 6 (profiles/r5/r5wg2/, r5wg3/; 1 per CU: ~7 ms); the unbinned
+        // kernel keeps every resident block (VALU and latency bound).  MOBHEAT_INGEST_WG_PER_CU overrides (tuning)
+        if (variant) per_cu = std::min(per_cu, 2);
+        if (const char *m = getenv("MOBHEAT_INGEST_WG_PER_CU")) {
+            int w = 0, cap = 0;
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&cap, kern, IG_THREADS, 0);
+            if (fa.sharedSizeBytes > 0) cap = std::min<int>(cap, (int)(163840 / fa.sharedSizeBytes));
+            w = atoi(m);
+            if (w > 0) per_cu = std::max(1, std::min(cap, w));
+        }
         if (getenv("MOBHEAT_DEBUG"))
             fprintf(stderr, "mobheat: k_ingest<%d> %d blocks/CU x %d CUs (LDS %zu B, %d VGPRs)\n", variant, per_cu, cus,
                     fa.sharedSizeBytes, fa.numRegs);
