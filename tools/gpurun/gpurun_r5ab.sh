@@ -5,6 +5,8 @@ set -o pipefail
 O=gpurun_out/${TAG:-r5ab}
 mkdir -p $O
 export TMPDIR=/tmp
+# (a throwaway warm-up run: the first bench process on a fresh box runs up to ~20% slow)
+timeout -k 10 300 python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-state-leg > $O/warmup.log 2>&1 || exit 1
 for r in $(seq 1 ${ROUNDS:-2}); do
 for v in ${MVARIANTS:-V0}; do
   L=real-time-mobility-heatmap_amd/csrc/variants/libmobheat_$v.so
