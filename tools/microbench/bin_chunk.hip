@@ -256,6 +256,10 @@ int main(int argc, char **argv) {
         if (want("seq")) printf("rep %d seq          %.3f ms\n", rep, timed([&] { hipLaunchKernelGGL(k_seq, dim3(8192), dim3(512), 0, 0, src, dst, n); }));
         if (want("direct")) printf("rep %d direct       %.3f ms\n", rep,
                timed([&] { hipLaunchKernelGGL(k_direct, dim3(grid), dim3(256), 0, 0, src, dst, n, cur, cap); }));
+        if (want("gridscan"))   // the direct pattern with fewer resident workgroups (k_ingest<true> runs 2 per CU)
+            for (int g : {256, 512, 1024, 2048, 4096})
+                printf("rep %d gridscan %-5d %.3f ms\n", rep, g,
+                       timed([&] { hipLaunchKernelGGL(k_direct, dim3(g), dim3(256), 0, 0, src, dst, n, cur, cap); }));
         if (want("capscan"))   // the direct pattern at slab capacities around the default: alignment of the bins' append points
             for (unsigned d : {0u, 2u, 4u, 6u, 8u, 16u, 32u, 64u, 128u, 256u, 512u, 1000u, 1024u})
                 printf("rep %d capscan +%-4u %.3f ms (cap %u)\n", rep, d,
