@@ -35,7 +35,9 @@ int hm_stage_ingest(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32_
     Inputs I;
     I.n = in->n;
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
-    if ((rc = phase_local(ctx, I, late_wm, true))) return rc;   // (large batches: bins of region fields, fused)
+    // (large batches: bins of region fields, fused; the local dedup launched on the side stream behind k_ingest, so that
+    // it runs while the ranks all-gather their summaries -- hm_stage_send waits for it)
+    if ((rc = phase_local(ctx, I, late_wm, true, false, ctx->early_ok && !ctx->dedup_main))) return rc;
     const DevStats s1 = *ctx->h_st;
     ctx->stage_I = I;
     ctx->stage_s1 = s1;
@@ -150,8 +152,10 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *send_buf, int64_t
     if (table && (rc = phase_table(ctx, I, n_agg, &n_records))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
     ctx->census_ready = false;   // (the owner counts what it receives)
-    // local dedup over rows -> local winners -> candidates, counted per owner
-    if ((rc = phase_dedup(ctx, &I, nullptr, I.n, s1.dedup_retry != 0))) return rc;
+    // local dedup over rows -> local winners -> candidates, counted per owner (launched in hm_stage_ingest unless the
+    // fused max gave up: then rerun here after it)
+    if (ctx->dedup_early) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[2], 0));
+    if ((!ctx->dedup_early || s1.dedup_retry != 0) && (rc = phase_dedup(ctx, &I, nullptr, I.n, s1.dedup_retry != 0))) return rc;
     if ((rc = ensure(ctx, ctx->cands, std::max<int64_t>(I.n, 1) * sizeof(Cand)))) return rc;
     hipLaunchKernelGGL(k_make_cands, dim3(grid_for(std::max<int64_t>(I.n, 1), 256)), dim3(256), 0, ctx->stream,
                        (const int64_t *)ctx->rows.p, ctx->d_scratch + 255, I.vk, I.ts, ctx->rank, (Cand *)ctx->cands.p);
