@@ -100,6 +100,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     // kernels, measured by the bench with and without it); default: the side stream
     if (const char *m = getenv("MOBHEAT_DEDUP_STREAM")) ctx->dedup_main = !strcmp(m, "main");
     if (const char *m = getenv("MOBHEAT_DEDUP_EARLY")) ctx->early_ok = strcmp(m, "0") != 0;
+    if (const char *m = getenv("MOBHEAT_OFFSETS_EARLY")) ctx->offsets_early = strcmp(m, "0") != 0;
     if (const char *m = getenv("MOBHEAT_STAGE_SELF")) ctx->self_hold_ok = strcmp(m, "copy") != 0;
     if (const char *m = getenv("MOBHEAT_DEDUP_DENSE")) ctx->dense_ok = strcmp(m, "0") != 0;
     if (const char *m = getenv("MOBHEAT_SUBBINS")) ctx->subbins_mode = !strcmp(m, "0") ? 0 : !strcmp(m, "1") ? 1 : 2;
@@ -284,7 +285,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
     // 2. snap + window registry + event keys
     const bool sub = ctx->subbins_mode == 1 || (ctx->subbins_mode == 2 && ctx->merge_coop);
-    if ((rc = phase_local(ctx, I, late_wm, true, sub, ctx->early_ok && !ctx->dedup_main))) return rc;
+    if ((rc = phase_local(ctx, I, late_wm, true, sub, ctx->early_ok && !ctx->dedup_main, ctx->offsets_early))) return rc;
     DevStats s1 = *ctx->h_st;
     const int64_t n_agg = (int64_t)s1.n_valid - (int64_t)s1.n_late;
     // the aggregation path of this batch (table mode: two LDS passes first; direct: every row a record)

@@ -31,9 +31,13 @@ static unsigned slab_cap_for(int64_t n, double skew, int64_t nbins) {
 // early_dedup (hm_process_batch): the latest-position dedup launched on the side stream right behind the ingest, so
 // that it runs while the host reads the batch statistics back and prepares the merge (it assumes the fused max did not
 // give up; hm_process_batch reruns it on the main stream when it did)
+// offsets: the binned batch's row offsets (bin_offsets) launched right behind k_ingest too, ahead of the side stream's
+// dedup (hm_process_batch): launched after the readback they queued behind the dedup's grid, 75 us on the merge's
+// critical path (profiles/r5/r5tl/)
 static int launch_side_dedup(hm_ctx *ctx, const Inputs *I);
+static int bin_offsets(hm_ctx *ctx);
 static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool allow_bin = false, bool sub = false,
-                       bool early_dedup = false) {
+                       bool early_dedup = false, bool offsets = false) {
     int64_t n = I.n;
     int rc;
     if ((rc = ensure(ctx, ctx->flags, n)) || (rc = ensure(ctx, ctx->win, n)) || (rc = ensure(ctx, ctx->rows, n * 8)) ||
@@ -60,6 +64,7 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
     const int nbins = RP_BINS << ctx->sub_bits;
     ctx->slab_cap = bin ? slab_cap_for(n, ctx->bin_skew, nbins) : 0;
     ctx->binned = false;
+    ctx->bin_offsets_ready = false;
     if ((rc = ensure(ctx, ctx->bin_cur, ((RP_BINS << SUB_BITS) + 1) * 4))) return rc;
     // (+ 64 slack records: k_ev_scatter_rec's, when a slab overflows and the batch is re-partitioned)
     if (bin && (rc = ensure(ctx, ctx->parts_sorted, ((size_t)nbins * ctx->slab_cap + 64) * sizeof(EventRec)))) return rc;
@@ -108,6 +113,11 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
         hipLaunchKernelGGL(k_sample_heavy, dim3(1), dim3(HS_THREADS), 0, ctx->stream, (const uint64_t *)ctx->keys.p, n, ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
         ctx->dfused.dirty = true;
+        // (a slab that overflowed makes the batch re-partition: these offsets then go unused)
+        if (bin && offsets) {
+            if ((rc = bin_offsets(ctx))) return rc;
+            ctx->bin_offsets_ready = true;
+        }
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
     ctx->dedup_early = early_dedup && n > 0;
@@ -289,6 +299,25 @@ static int merge_partials(hm_ctx *ctx, const TilePartial *parts, int64_t n_parts
     return HM_OK;
 }
 
+// the binned batch's row offsets rp_O (the exclusive scan of the bins' counts); in sub-bins, each bin's sub-slabs as
+// its segments first, in sub-region order (k_sub_segments: stage_SO / stage_SP, bin totals stage_T)
+static int bin_offsets(hm_ctx *ctx) {
+    int rc;
+    if ((rc = ensure(ctx, ctx->rp_O, (RP_BINS + 1) * 8))) return rc;
+    if (!ctx->sub_bits)
+        return scan_counts(ctx, (const unsigned *)ctx->bin_cur.p, RP_BINS + 1, (unsigned long long *)ctx->rp_O.p);
+    constexpr int NS = 1 << SUB_BITS;
+    static_assert(SUB_BITS == 3, "k_sub_segments and the merge's segment table assume 8 sub-bins");
+    if ((rc = ensure(ctx, ctx->stage_SO, (size_t)RP_BINS * NS * 8)) || (rc = ensure(ctx, ctx->stage_SP, (size_t)RP_BINS * NS * 4)) ||
+        (rc = ensure(ctx, ctx->stage_T, (RP_BINS + 1) * 4)))
+        return rc;
+    hipLaunchKernelGGL(k_sub_segments, dim3(grid_for(RP_BINS + 1, 256)), dim3(256), 0, ctx->stream, (const unsigned *)ctx->bin_cur.p,
+                       (const EventRec *)ctx->parts_sorted.p, (int64_t)ctx->slab_cap, (unsigned long long *)ctx->stage_SO.p,
+                       (unsigned *)ctx->stage_SP.p, (unsigned *)ctx->stage_T.p);
+    HIPCHK(ctx, hipGetLastError());
+    return scan_counts(ctx, (const unsigned *)ctx->stage_T.p, RP_BINS + 1, (unsigned long long *)ctx->rp_O.p);
+}
+
 // the direct path: the batch's event keys (k_ingest) -> census from the registry -> window tables -> event partition
 // -> merge -> rows.  n_rec = aggregated rows (keys != 0)
 static int merge_events(hm_ctx *ctx, const Inputs &I, int64_t n_rec) {
@@ -307,24 +336,12 @@ static int merge_events(hm_ctx *ctx, const Inputs &I, int64_t n_rec) {
     int64_t ntiles = 1;
     const bool subs = binned && ctx->sub_bits;
     Segs seg;
+    if (binned && !ctx->bin_offsets_ready && (rc = bin_offsets(ctx))) return rc;
     if (subs) {   // each bin's sub-slabs as its segments, in sub-region order (k_sub_segments)
-        constexpr int NS = 1 << SUB_BITS;
-        static_assert(SUB_BITS == 3, "k_sub_segments and the merge's segment table assume 8 sub-bins");
-        if ((rc = ensure(ctx, ctx->rp_O, (RP_BINS + 1) * 8)) || (rc = ensure(ctx, ctx->stage_SO, (size_t)RP_BINS * NS * 8)) ||
-            (rc = ensure(ctx, ctx->stage_SP, (size_t)RP_BINS * NS * 4)) || (rc = ensure(ctx, ctx->stage_T, (RP_BINS + 1) * 4)))
-            return rc;
-        hipLaunchKernelGGL(k_sub_segments, dim3(grid_for(RP_BINS + 1, 256)), dim3(256), 0, ctx->stream, (const unsigned *)ctx->bin_cur.p,
-                           (const EventRec *)ctx->parts_sorted.p, (int64_t)ctx->slab_cap, (unsigned long long *)ctx->stage_SO.p,
-                           (unsigned *)ctx->stage_SP.p, (unsigned *)ctx->stage_T.p);
-        HIPCHK(ctx, hipGetLastError());
-        if ((rc = scan_counts(ctx, (const unsigned *)ctx->stage_T.p, RP_BINS + 1, (unsigned long long *)ctx->rp_O.p))) return rc;
         seg.SO = (const unsigned long long *)ctx->stage_SO.p;
         seg.SP = (const unsigned *)ctx->stage_SP.p;
-        seg.nseg = NS;
-    } else if (binned) {
-        if ((rc = ensure(ctx, ctx->rp_O, (RP_BINS + 1) * 8))) return rc;
-        if ((rc = scan_counts(ctx, (const unsigned *)ctx->bin_cur.p, RP_BINS + 1, (unsigned long long *)ctx->rp_O.p))) return rc;
-    } else if ((rc = ev_partition(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, ntiles))) {
+        seg.nseg = 1 << SUB_BITS;
+    } else if (!binned && (rc = ev_partition(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, ntiles))) {
         return rc;
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));

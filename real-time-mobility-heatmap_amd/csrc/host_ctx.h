@@ -37,6 +37,7 @@ struct hm_ctx {
     bool dedup_main = false;   // MOBHEAT_DEDUP_STREAM=main: never the side stream
     bool dedup_early = false;  // this batch's side-stream dedup was launched behind k_ingest (phase_local)
     bool early_ok = true;      // MOBHEAT_DEDUP_EARLY=0: launched after the readback instead (A/B)
+    bool offsets_early = true; // MOBHEAT_OFFSETS_EARLY=0: the bins' row offsets launched after the readback (A/B)
     hipEvent_t h2d_ev[H2D_CHUNKS] = {};
     struct H2D { const void *src; void *dst; size_t el; };
     H2D h2d[7] = {};
@@ -132,6 +133,7 @@ struct hm_ctx {
     unsigned *h_bincur = nullptr;    // the cursors read back (pinned): the fullest bin sizes the next batch's slabs
     double bin_skew = 1.0;           // the last binned batch's fullest bin / mean bin
     bool binned = false;             // this batch's rows are in their bins (k_ingest<true>, no slab overflowed)
+    bool bin_offsets_ready = false;  // the bins' row offsets (bin_offsets) already launched behind k_ingest
     // the bins split into sub-bins by sub-region (k_ingest sub_bits: SUB_BITS, or 0 = whole bins): on hm_process_batch's
     // binned batches when the last batch re-touched mostly existing keys (merge_coop) -- its merge then reads old state
     // lines inside 1/8 of each region at a time (state-read leg 6.6-6.75 -> 5.25-5.36 ms), while a batch of new keys
@@ -762,6 +764,7 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census, bool r
         int64_t moved = 0;
         for (const auto &g : old) moved += g.keys;
         ctx->touched_dump_seq = -1;
+        ctx->bin_offsets_ready = false;   // (the regrow's partition below writes rp_O)
         if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(moved, 1) * sizeof(GrowRec)))) return rc;
         HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
         for (const auto &g : old) {
