@@ -459,15 +459,26 @@ static int table_acquire(hm_ctx *ctx, Geo &geo, TileSlot **out) {
 // (the stream must have drained every kernel that reads the table).  The table's tags are cleared at once on the
 // side stream -- behind the main stream's work so far, concurrent with the next batch's first kernels (k_ingest does
 // not use the HBM bandwidth) -- and table_acquire waits for that (side_ev[3]).
-static int table_release(hm_ctx *ctx, TileSlot *t, int log2cap) {
-    const int64_t n16 = (int64_t(1) << log2cap) / 16;   // (2^log2cap >= 1024 tag bytes, 64-B aligned)
+// Several tables at once (a batch's evicted windows): one event pair and one launch per ZR_MAX tables (one
+// release at a time cost ~30 us of host API calls each between batches, profiles/r5/r5tl/).
+static int table_release_all(hm_ctx *ctx, const std::vector<std::pair<TileSlot *, int>> &ts) {
+    if (ts.empty()) return HM_OK;
     HIPCHK(ctx, hipEventRecord(ctx->side_ev[0], ctx->stream));
     HIPCHK(ctx, hipStreamWaitEvent(ctx->side_stream, ctx->side_ev[0], 0));
-    hipLaunchKernelGGL(k_zero16, dim3(grid_for(n16, 256, 256 * 32)), dim3(256), 0, ctx->side_stream,
-                       (uint4 *)(t + (size_t(1) << log2cap)), n16);
-    HIPCHK(ctx, hipGetLastError());
+    for (size_t a = 0; a < ts.size(); a += ZR_MAX) {
+        ZeroRanges r = {};
+        const int k = (int)std::min<size_t>(ZR_MAX, ts.size() - a);
+        int64_t mx = 0;
+        for (int j = 0; j < k; j++) {   // (2^log2cap >= 1024 tag bytes, 64-B aligned)
+            r.p[j] = (uint4 *)(ts[a + j].first + (size_t(1) << ts[a + j].second));
+            r.n16[j] = (int64_t(1) << ts[a + j].second) / 16;
+            mx = std::max(mx, r.n16[j]);
+        }
+        hipLaunchKernelGGL(k_zero16_ranges, dim3(grid_for(mx, 256, 256 * 32), k), dim3(256), 0, ctx->side_stream, r);
+        HIPCHK(ctx, hipGetLastError());
+    }
     HIPCHK(ctx, hipEventRecord(ctx->side_ev[3], ctx->side_stream));
-    ctx->pool.emplace_back(t, log2cap);
+    for (const auto &t : ts) ctx->pool.push_back(t);
     size_t own = 0;   // pooled tables of our own allocations (arena tables stay pooled)
     for (auto &pt : ctx->pool) own += !in_arena(ctx, pt.first);
     for (size_t i = 0; own > 8 && i < ctx->pool.size();) {
@@ -480,6 +491,7 @@ static int table_release(hm_ctx *ctx, TileSlot *t, int log2cap) {
     }
     return HM_OK;
 }
+static int table_release(hm_ctx *ctx, TileSlot *t, int log2cap) { return table_release_all(ctx, {{t, log2cap}}); }
 
 static int gens_upload(hm_ctx *ctx) {
     memset(ctx->h_gmap, 0, GMAP_SLOTS * sizeof(GenDesc));
@@ -780,8 +792,9 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census, bool r
             (rc = merge_sorted<GrowRec>(ctx, moved, ntiles, 0, (const GrowRec *)ctx->parts_regrow_sorted.p)))
             return rc;
         HIPCHK(ctx, ctx_sync(ctx, __LINE__));
-        for (const auto &g : old)
-            if ((rc = table_release(ctx, g.tab, g.log2cap))) return rc;
+        std::vector<std::pair<TileSlot *, int>> rel;
+        for (const auto &g : old) rel.emplace_back(g.tab, g.log2cap);
+        if ((rc = table_release_all(ctx, rel))) return rc;
     }
     return HM_OK;
 }
@@ -797,17 +810,19 @@ static int state_account(hm_ctx *ctx, int64_t evict_wm_ms) {
     const int64_t dead_end_us = evict_wm_ms * 1000;
     int64_t live = 0;
     std::vector<hm_ctx::Gen> keep;
+    std::vector<std::pair<TileSlot *, int>> dead;
     for (auto &g : ctx->gens) {
         unsigned h = (unsigned)(mix64(g.wenc) & (GMAP_SLOTS - 1));
         for (int p = 0; p < GMAP_SLOTS && ctx->h_gmap[h].wenc; p++, h = (h + 1) & (GMAP_SLOTS - 1))
             if (ctx->h_gmap[h].wenc == g.wenc) { g.keys = (int64_t)ctx->h_gmap[h].count; break; }
         if (wdec(g.wenc) + ctx->cfg.tile_us <= dead_end_us) {
-            if (int rc = table_release(ctx, g.tab, g.log2cap)) return rc;
+            dead.emplace_back(g.tab, g.log2cap);
         } else {
             live += g.keys;
             keep.push_back(g);
         }
     }
+    if (int rc = table_release_all(ctx, dead)) return rc;
     ctx->gens.swap(keep);
     ctx->state_size = live;
     return HM_OK;

@@ -758,6 +758,17 @@ __global__ __launch_bounds__(256) void k_zero16(uint4 *__restrict__ p, int64_t n
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) p[i] = make_uint4(0u, 0u, 0u, 0u);
 }
+// up to ZR_MAX ranges in one launch (blockIdx.y = range): a batch's released tables
+constexpr int ZR_MAX = 8;
+struct ZeroRanges {
+    uint4 *p[ZR_MAX];
+    int64_t n16[ZR_MAX];
+};
+__global__ __launch_bounds__(256) void k_zero16_ranges(ZeroRanges r) {
+    uint4 *__restrict__ p = r.p[blockIdx.y];
+    const int64_t n16 = r.n16[blockIdx.y], stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
 
 // the start of a batch in one launch (was six memsets and a copy): the batch statistics (max ts / min window start
 // at their identities), the fast-path exception and dedup give-up words, the window registry and its census
