@@ -190,7 +190,8 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *send_buf, int64_t
                 return rc;
         } else {             // the partition with one bin per region field (WInfo without table geometry: binp 0)
             int64_t ntiles;
-            if ((rc = winfo_upload(ctx, false)) || (rc = ev_partition(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, ntiles)))
+            if ((rc = winfo_upload(ctx, false)) || (rc = keys_complete(ctx, I)) ||
+                (rc = ev_partition(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, ntiles)))
                 return rc;
             stride = ntiles;
         }

@@ -60,6 +60,8 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
         }
     }
     const bool bin = allow_bin && n > 0 && choose_binned(ctx, n);
+    ctx->keys_partial = bin;   // (k_ingest<true> writes the keys of the exception and sampled rows only)
+    ctx->keys_late_us = late_wm_ms * 1000;
     ctx->sub_bits = bin && sub ? SUB_BITS : 0;
     const int nbins = RP_BINS << ctx->sub_bits;
     ctx->slab_cap = bin ? slab_cap_for(n, ctx->bin_skew, nbins) : 0;
@@ -103,7 +105,7 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
                                ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
                                ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st, I.sp, I.sv,
                                (unsigned *)ctx->bin_cur.p, bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap,
-                               (unsigned long long *)ctx->dense.p, ctx->dense_cap, ctx->sub_bits);
+                               (unsigned long long *)ctx->dense.p, ctx->dense_cap, ctx->sub_bits, hs_stride(n) - 1);
         }
         ctx->n_h2d = 0;
         hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, ctx->cfg.h3_res,
@@ -142,6 +144,24 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
     return HM_OK;
 }
 
+// every row's event key after a binned ingest (k_ingest<false, true>): for the table mode and the re-partition of a
+// batch whose slab overflowed, the only readers of all the keys
+static int keys_complete(hm_ctx *ctx, const Inputs &I) {
+    if (!ctx->keys_partial) return HM_OK;
+    ctx->keys_partial = false;
+    if (I.n == 0) return HM_OK;
+    const int blocks = (int)std::min<int64_t>((I.n + IG_THREADS - 1) / IG_THREADS, ctx->ingest_grid);
+    hipLaunchKernelGGL((k_ingest<false, true>), dim3(blocks), dim3(IG_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.vk,
+                       (int64_t)0, I.n, ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), ctx->keys_late_us,
+                       (uint8_t *)ctx->flags.p, (uint64_t *)ctx->keys.p, ctx->dfused.tab, ctx->dfused.cap - 1,
+                       (unsigned int *)ctx->dfused.used.p, ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p,
+                       ctx->d_scratch + SLOW_WORD, ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st, I.sp,
+                       I.sv, (unsigned *)ctx->bin_cur.p, (EventRec *)nullptr, 0u, (unsigned long long *)ctx->dense.p, 0ull, 0u,
+                       (int64_t)0);
+    HIPCHK(ctx, hipGetLastError());
+    return HM_OK;
+}
+
 // Aggregation path of the batch: table mode when the last batches had few distinct keys that repeat a lot (their
 // aggregates fit k_bin_reduce's LDS tables), or when this batch's key sample shows heavy hitters (a key in >= 1/256
 // of the sampled rows: k_sample_heavy), else the direct path.
@@ -157,6 +177,7 @@ static bool choose_table(const hm_ctx *ctx, int64_t n_agg, unsigned long long sa
 static int phase_table(hm_ctx *ctx, const Inputs &I, int64_t n_agg, int64_t *n_parts) {
     int rc;
     const int64_t n = I.n;
+    if ((rc = keys_complete(ctx, I))) return rc;
     if ((rc = ensure(ctx, ctx->partials, std::max<int64_t>(n_agg, 1) * sizeof(TilePartial)))) return rc;
     const int nsub = AG_BINS * AG_SUB;
     if (ctx->agg_cap == 0)   // first table batch: room for about a quarter of the rows evicted twice over
@@ -341,7 +362,7 @@ static int merge_events(hm_ctx *ctx, const Inputs &I, int64_t n_rec) {
         seg.SO = (const unsigned long long *)ctx->stage_SO.p;
         seg.SP = (const unsigned *)ctx->stage_SP.p;
         seg.nseg = 1 << SUB_BITS;
-    } else if (!binned && (rc = ev_partition(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, ntiles))) {
+    } else if (!binned && ((rc = keys_complete(ctx, I)) || (rc = ev_partition(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, ntiles)))) {
         return rc;
     }
     HIPCHK(ctx, hipEventRecord(ctx->ev[7], ctx->stream));

@@ -133,6 +133,8 @@ struct hm_ctx {
     unsigned *h_bincur = nullptr;    // the cursors read back (pinned): the fullest bin sizes the next batch's slabs
     double bin_skew = 1.0;           // the last binned batch's fullest bin / mean bin
     bool binned = false;             // this batch's rows are in their bins (k_ingest<true>, no slab overflowed)
+    bool keys_partial = false;       // k_ingest<true> wrote only the exception and sampled rows' keys (keys_complete)
+    int64_t keys_late_us = 0;        // (the batch's late watermark, which keys_complete's pass needs again)
     bool bin_offsets_ready = false;  // the bins' row offsets (bin_offsets) already launched behind k_ingest
     // the bins split into sub-bins by sub-region (k_ingest sub_bits: SUB_BITS, or 0 = whole bins): on hm_process_batch's
     // binned batches when the last batch re-touched mostly existing keys (merge_coop) -- its merge then reads old state

@@ -79,7 +79,20 @@ __device__ __forceinline__ void wave_count_slots(bool pred, int slot, unsigned *
 // (one kernel for every resolution: per-resolution specialisations of this kernel, measured no faster once the digits
 // came from the step tables, were miscompiled at res 3 by this compiler -- wrong cells, caught by
 // test_ingest_cells_every_resolution, profiles/r4/r4w/)
-template <bool kBin>
+// k_sample_heavy's row stride for a batch of n rows: the largest power of two <= n / HS_SAMPLE (so that k_ingest<true>
+// can write the sampled rows' keys with a mask test)
+constexpr int HS_SAMPLE = 4096, HS_THREADS = 1024, HS_SLOTS = 2 * HS_SAMPLE;
+__host__ __device__ inline int64_t hs_stride(int64_t n) {
+    int64_t s = 1;
+    while (s * 2 <= n / HS_SAMPLE) s *= 2;
+    return s;
+}
+// kBin writes an event key only where something reads it before the merge: exception rows (k_ingest_exact completes
+// them) and k_sample_heavy's rows (i & smask == 0) -- the binned records carry their own keys.  A batch that then
+// needs every row's key (the key sample asks for table mode, or a slab overflowed and the batch re-partitions) runs
+// kKeys: the same rows again, writing only the keys of the non-exception rows (no flags, dedup, census, statistics,
+// bins), so that the keys read as one k_ingest<false> would have written them (keys_complete).
+template <bool kBin, bool kKeys = false>
 __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     const double *__restrict__ lat, const double *__restrict__ lon, const int64_t *__restrict__ ts,
     const uint8_t *__restrict__ row_valid, const uint64_t *__restrict__ vkey, int64_t i_begin, int64_t n, int res_arg, FloorDiv wdiv,
@@ -88,7 +101,8 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
     unsigned long long *n_slow, unsigned long long *dgiveup, unsigned long long *wreg, unsigned long long *wcount,
     DevStats *st, const double *__restrict__ speed, const uint8_t *__restrict__ speed_valid, unsigned *__restrict__ bin_cur,
     EventRec *__restrict__ slabs, unsigned slab_cap, unsigned long long *__restrict__ dense, unsigned long long dense_cap,
-    unsigned sub_bits) {
+    unsigned sub_bits, int64_t smask) {
+    static_assert(!(kBin && kKeys), "k_ingest: kKeys runs unbinned");
     const int res = res_arg;
     __shared__ WinCacheL WC;
     __shared__ double Fc[20][3], Fu[20][2][3];   // the fast path's per-face tables (res parity): LDS reads
@@ -172,7 +186,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         const bool ok = geo && t > INT64_MIN + 2 * tile_us && t < INT64_MAX - 2 * tile_us;
         // dedup: the vkey's home slot is loaded now, its latency hidden behind the cell computation (a plain load:
         // a stale copy can only show the slot empty or its max lower, both of which the atomics below correct)
-        const bool dd = ok && v != EMPTY_VKEY && !__hip_atomic_load(&dskip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const bool dd = !kKeys && ok && v != EMPTY_VKEY && !__hip_atomic_load(&dskip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const bool dv = v < dense_cap;   // (dense_cap < 2^64 - 1: EMPTY_VKEY is never dense)
         const unsigned long long dh0 = vkey_hash(v) & dmask;
         DedupSlot d0{EMPTY_VKEY, 0};
@@ -199,7 +213,7 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         }
         // cell of the aggregated rows; margin exceptions go to k_ingest_exact (exact path), which fills their key
         exc = exc && (fl & F_AGG) != 0;
-        {
+        if constexpr (!kKeys) {
             const unsigned long long pos = wave_append(exc, n_slow);
             if (exc) slow[pos] = (unsigned int)i;
         }
@@ -229,8 +243,8 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
         const bool agg = (fl & F_AGG) != 0;
         const uint64_t key = agg ? ekey_make(exc ? 0 : cell, (unsigned)widx) : 0;
         if (in) {
-            flags_out[i] = fl | (cand ? F_CAND : 0);
-            keys_out[i] = key;
+            if constexpr (!kKeys) flags_out[i] = fl | (cand ? F_CAND : 0);
+            if (kKeys ? !exc : !kBin || exc || (i & smask) == 0) keys_out[i] = key;
         }
         if constexpr (kBin) {
             // the row's EventRec into its bin (exceptions: k_ingest_exact, once their cell is known)
@@ -257,16 +271,19 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
                 }
             }
         }
-        const unsigned long long pos = wave_append(claimed, n_dused);
-        if (claimed) dused[pos] = (unsigned int)dh;
-        // census: aggregated rows per window (sizes the window tables of the direct path)
-        wave_count_slots(agg && wslot >= 0, wslot, WC.cnt);
-        if (agg && wslot < 0) atomicAdd(&wcount[widx], 1ull);
+        if constexpr (!kKeys) {
+            const unsigned long long pos = wave_append(claimed, n_dused);
+            if (claimed) dused[pos] = (unsigned int)dh;
+            // census: aggregated rows per window (sizes the window tables of the direct path)
+            wave_count_slots(agg && wslot >= 0, wslot, WC.cnt);
+            if (agg && wslot < 0) atomicAdd(&wcount[widx], 1ull);
+        }
         // poll the give-up flag now and then (its own cache line)
         if (threadIdx.x == 0 && (round & 15) == 15 && !dskip)
             __hip_atomic_store(&dskip, __hip_atomic_load(dgiveup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ? 1u : 0u,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    if constexpr (kKeys) return;   // (no census, no statistics: the batch's first pass counted them)
     __syncthreads();
     for (int q = threadIdx.x; q < WC_SLOTS; q += IG_THREADS)
         if (WC.cnt[q]) atomicAdd(&wcount[(WC.e[q] & 0xfff) - 1], (unsigned long long)WC.cnt[q]);
@@ -324,14 +341,13 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
 // (the first batch, or a sudden change of the data): HS_SAMPLE keys at an even stride, the largest
 // multiplicity among them -> DevStats.sample_max_run.  A key holding a few % of the rows would put that share of the
 // batch through one merge workgroup (one bin) on the direct path; table mode aggregates it in LDS first.
-constexpr int HS_SAMPLE = 4096, HS_THREADS = 1024, HS_SLOTS = 2 * HS_SAMPLE;
 // (the multiplicities counted in an LDS hash table at load <= 1/2: was a bitonic sort of the sample, 78 barriers)
 __global__ __launch_bounds__(HS_THREADS) void k_sample_heavy(const uint64_t *__restrict__ keys, int64_t n, DevStats *st) {
     __shared__ unsigned long long k[HS_SLOTS];
     __shared__ unsigned c[HS_SLOTS];
     __shared__ unsigned best;
     const int t = threadIdx.x;
-    const int64_t stride = n / HS_SAMPLE > 0 ? n / HS_SAMPLE : 1;
+    const int64_t stride = hs_stride(n);
     constexpr int PER = HS_SAMPLE / HS_THREADS;
     uint64_t v[PER];
 #pragma unroll

@@ -363,6 +363,24 @@ def test_clustered_city_res9():
     eng.close()
 
 
+def test_binned_ingest_then_table_mode():
+    """A batch large enough to be binned in k_ingest (>= 2^22 rows) whose key sample then shows heavy hitters: the
+    binned ingest wrote the event keys of its exception and sampled rows only, so the switch to table mode first
+    completes every row's key (keys_complete: k_ingest's keys-only pass) -- results equal the oracle's, over two
+    batches (the second chooses table mode from the first's cardinality, its keys written in full)."""
+    from mobheat import HeatmapEngine, synth
+    from oracle.spark_oracle import SparkHeatmapOracle
+    eng = HeatmapEngine(h3_res=9)
+    ora = SparkHeatmapOracle(h3_res=9)
+    for epoch in range(2):
+        b = synth.c3_city(seed=7 + epoch, n=4_400_000, n_vehicles=5000)
+        b["ts_us"] = b["ts_us"] + epoch * 600_000_000
+        res, exp = _run(eng, ora, b, epoch)
+        assert_batch_equal(res, exp)
+        assert eng.last_counts()["table_mode"]
+    eng.close()
+
+
 def test_full_size_properties_c2():
     """C2 size (1e8 events, res 8) through the device path: size-independent properties only."""
     import mobheat
