@@ -46,9 +46,10 @@ SIMDS = 1024
 #   direct path   ingest 42/event (lat, lon, ts, vkey 8 each + row_valid 1 read; flags 1 + event key 8 written)
 #                 partition 16/event (k_ev_hist and k_ev_scatter read the key) + 57/record (speed, speed_valid,
 #                           lat, lon read: 25; the 32-B EventRec written)
-#   binned        (the direct path's records written by k_ingest itself, hm_last_counts "binned") ingest 51/event (+ speed
-#                 and speed_valid read) + 32/record (the EventRec written into its bin); partition 0 (a scan of the
-#                 8192 bin counts)
+#   binned        (the direct path's records written by k_ingest itself, hm_last_counts "binned") ingest 43/event (+ speed
+#                 and speed_valid read; the event key not written -- the record carries it -- but for exception and
+#                 sampled rows) + 32/record (the EventRec written into its bin); partition 0 (a scan of the 8192 bin
+#                 counts)
 #                 merge 32/record read + 113/tile (64-B state line + 49-B row written) + 64/pre-existing key read
 #                 emit 98/gap (a 49-B row moved into a gap; gaps = R - T), dedup 20/event
 #   multi-GPU     (stage API) the sender's records grouped by region field as above -- binned in k_ingest, or the
@@ -71,7 +72,7 @@ def stage_bytes(n, c, world=1, staged=None):
     S = c["sent"] if staged else R   # records this rank grouped (and sent)
     b.update(aggregate=0, merge=32 * R + 113 * T + 64 * E)
     if c.get("binned"):
-        b.update(ingest=51 * n + 32 * S, partition=0)
+        b.update(ingest=43 * n + 32 * S, partition=0)
     else:
         b.update(partition=16 * n + 57 * S)
     if staged:

@@ -45,7 +45,7 @@ def test_stage_bytes_multi_gpu_owner():
     assert s["send"] == (32 + 32) * S
     assert s["merge"] == 32 * R + 113 * R
     s = b.stage_bytes(n, dict(c, binned=1), world=2)
-    assert s["partition"] == 0 and s["ingest"] == 51 * n + 32 * S and s["send"] == 64 * S
+    assert s["partition"] == 0 and s["ingest"] == 43 * n + 32 * S and s["send"] == 64 * S
 
 
 def test_stage_bytes_self_held_records():

@@ -56,14 +56,15 @@ def main():
         f_raw, w_raw = k["fetch_bytes_raw"], k["write_bytes"]
         reads = f_raw / cal["nt8_fetch_per_known_read"]
         w_atom = R * cal["atom_write_bytes_per_atomic"]
-        # the writes left once the atomics' counted bytes are taken out: flags + keys (9 B per event) and records (32 B
-        # per record), each at its pattern's counted / known ratio
+        # the writes left once the atomics' counted bytes are taken out: flags (1 B per event; the 8-B event key only
+        # for exception and sampled rows since round 5) and records (32 B per record), each at its pattern's counted /
+        # known ratio (the coalesced row-order pattern: st9's)
         w_data = w_raw - w_atom
-        w_model = cal["st9_write_per_known_write"] * 9 * ev + cal["scat32_write_per_known_write"] * 32 * R
-        writes = 9 * ev + 32 * R + (w_data - w_model)   # (the residual: counted writes the patterns do not explain)
+        w_model = cal["st9_write_per_known_write"] * 1 * ev + cal["scat32_write_per_known_write"] * 32 * R
+        writes = 1 * ev + 32 * R + (w_data - w_model)   # (the residual: counted writes the patterns do not explain)
         k["calibrated"] = {"read_bytes": reads, "write_bytes": writes, "hbm_bytes": reads + writes,
                            "atomics_counted_write_bytes": w_atom, "unexplained_write_bytes": w_data - w_model,
-                           "algorithmic_bytes": 51 * ev + 32 * R, "records": R}
+                           "algorithmic_bytes": 43 * ev + 32 * R, "records": R}
         d["calibration"] = cal
         json.dump(d, open(a.out or a.pmc, "w"), indent=1)
         out["k_ingest_calibrated"] = k["calibrated"]
