@@ -17,7 +17,7 @@ def short(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
-    ap.add_argument("--anchor", default="k_ingest<true>")
+    ap.add_argument("--anchor", default="k_ingest<true")
     ap.add_argument("--step", type=int, default=-2)
     ap.add_argument("--min-gap-us", type=float, default=5.0)
     a = ap.parse_args()
