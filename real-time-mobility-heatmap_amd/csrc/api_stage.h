@@ -305,8 +305,8 @@ int hm_stage_send(hm_ctx *ctx, const int64_t *summaries, void *send_buf, int64_t
 // the multi-GPU owner's direct path: every sender's chunk holds the records of the owner's region fields in order
 // (counts per field) -> census per global window -> window tables (range geometry) -> each bin merged from its
 // senders' segments -> rows
-static int merge_received_chunks(hm_ctx *ctx, const uint8_t *recv, const int64_t *d_off, const std::vector<ChunkHdr> &hdr,
-                                 int64_t n) {
+static int merge_received_chunks(hm_ctx *ctx, const uint8_t *recv, int64_t recv_total, const int64_t *d_off,
+                                 const std::vector<ChunkHdr> &hdr, int64_t n) {
     int rc;
     const int W = ctx->nranks;
     if (n > MAX_BATCH_ROWS) return set_err(ctx, HM_E_INVALID, "%lld received records exceed %lld", (long long)n, (long long)MAX_BATCH_ROWS);
@@ -340,6 +340,10 @@ static int merge_received_chunks(hm_ctx *ctx, const uint8_t *recv, const int64_t
     seg.SO = (const unsigned long long *)ctx->stage_SO.p;
     seg.SP = (const unsigned *)ctx->stage_SP.p;
     seg.nseg = W;
+    {   // (the senders' segments in the receive buffer, the self-held ones in this rank's slabs)
+        const unsigned long long r0 = (unsigned long long)(uintptr_t)recv, s0 = (unsigned long long)(uintptr_t)ctx->parts_sorted.p;
+        seg.bounds = SegBounds{{r0, s0}, {r0 + (unsigned long long)recv_total, s0 + ctx->parts_sorted.bytes}};
+    }
     if ((rc = merge_sorted<EventRec>(ctx, n, 1, 0, (const EventRec *)recv, seg))) return rc;
     HIPCHK(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
     if ((rc = rows_densify(ctx, 1))) return rc;
@@ -409,7 +413,7 @@ int hm_stage_merge(hm_ctx *ctx, const void *recv_buf, const int64_t *recv_bytes,
     }
     const Cand *cands = (const Cand *)ctx->cands_recv.p;
     if (table) rc = merge_partials(ctx, (const TilePartial *)ctx->stage_tmp.p, n_rec);
-    else rc = merge_received_chunks(ctx, recv, d_off, hdr, n_rec + ctx->stage_self_recs);   // (+ the self-held ones)
+    else rc = merge_received_chunks(ctx, recv, off[W], d_off, hdr, n_rec + ctx->stage_self_recs);   // (+ the self-held ones)
     if (rc) return rc;
     // owner-side dedup over received candidates
     if ((rc = phase_dedup(ctx, nullptr, cands, n_cand, true))) return rc;

@@ -40,6 +40,10 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
                        bool early_dedup = false, bool offsets = false) {
     int64_t n = I.n;
     int rc;
+    // the previous call's side-stream dedup may still run (a stage batch that a peer's failure ended before
+    // hm_stage_send waited for it -- ADVICE r5): nothing below touches its tables, flags or rows before it is done
+    if (ctx->dedup_early) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev[2], 0));
+    ctx->dedup_early = false;
     if ((rc = ensure(ctx, ctx->flags, n)) || (rc = ensure(ctx, ctx->win, n)) || (rc = ensure(ctx, ctx->rows, n * 8)) ||
         (rc = ensure(ctx, ctx->keys, n * 8)) || (rc = ensure(ctx, ctx->slow, n * sizeof(unsigned int))))
         return rc;
@@ -362,6 +366,8 @@ static int merge_events(hm_ctx *ctx, const Inputs &I, int64_t n_rec) {
         seg.SO = (const unsigned long long *)ctx->stage_SO.p;
         seg.SP = (const unsigned *)ctx->stage_SP.p;
         seg.nseg = 1 << SUB_BITS;
+        const unsigned long long a = (unsigned long long)(uintptr_t)ctx->parts_sorted.p;
+        seg.bounds = SegBounds{{a, a}, {a + ctx->parts_sorted.bytes, a + ctx->parts_sorted.bytes}};
     } else if (!binned && ((rc = keys_complete(ctx, I)) || (rc = ev_partition(ctx, (const uint64_t *)ctx->keys.p, I.n, &I, ntiles)))) {
         return rc;
     }

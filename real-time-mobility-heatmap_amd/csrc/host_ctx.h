@@ -602,6 +602,7 @@ struct Segs {
     const unsigned long long *SO = nullptr;
     const unsigned *SP = nullptr;
     int nseg = 0;
+    SegBounds bounds{};   // where the segments may lie (checked by the MOBHEAT_BOUNDS_CHECK build only)
 };
 // merge the partitioned records (ctx->parts_sorted, or src) of n_rows staging rows
 template <typename Rec>
@@ -638,6 +639,10 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t sla
         resident = need <= tag_bytes && nwin <= MO_RES_MAX && ctx->n_glist <= GC_MAX;
     }
     if (seg.nseg > MO_SEG_MAX) return set_err(ctx, HM_E_INVALID, "%d senders exceed %d", seg.nseg, MO_SEG_MAX);
+#if MOBHEAT_BOUNDS_CHECK
+    if (seg.nseg > 0) HIPCHK(ctx, hipMemcpyToSymbolAsync(HIP_SYMBOL(g_seg_bounds), &seg.bounds, sizeof(SegBounds), 0,
+                                                         hipMemcpyHostToDevice, ctx->stream));
+#endif
     auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(grid), dim3(MO_THREADS), tag_bytes, ctx->stream, src ? src : (const Rec *)ctx->parts_sorted.p, slab,
                            seg.SO, seg.SP, seg.nseg,

@@ -338,7 +338,7 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
 }
 
 // Heavy hitters in the batch's event keys, for the choice of the aggregation path when the last batch says nothing
-// (the first batch, or a sudden change of the data): HS_SAMPLE keys at an even stride, the largest
+// (the first batch, or a sudden change of the data): HS_SAMPLE keys spread evenly over the batch, the largest
 // multiplicity among them -> DevStats.sample_max_run.  A key holding a few % of the rows would put that share of the
 // batch through one merge workgroup (one bin) on the direct path; table mode aggregates it in LDS first.
 // (the multiplicities counted in an LDS hash table at load <= 1/2: was a bitonic sort of the sample, 78 barriers)
@@ -352,7 +352,10 @@ __global__ __launch_bounds__(HS_THREADS) void k_sample_heavy(const uint64_t *__r
     uint64_t v[PER];
 #pragma unroll
     for (int u = 0; u < PER; u++) {   // every load in flight before the table is cleared
-        const int64_t i = (int64_t)(t + u * HS_THREADS) * stride;
+        // (spread over the whole batch -- sample q at q n / HS_SAMPLE, rounded down to the stride k_ingest<true> writes
+        // keys at: the stride alone covered only the first HS_SAMPLE x stride rows, as little as half the batch, and a
+        // hot key late in a time-ordered batch went unseen -- ADVICE r5)
+        const int64_t i = ((int64_t)(t + u * HS_THREADS) * n / HS_SAMPLE) & ~(stride - 1);
         v[u] = i < n ? keys[i] : 0;
     }
     for (int q = t; q < HS_SLOTS; q += HS_THREADS) { k[q] = 0; c[q] = 0; }

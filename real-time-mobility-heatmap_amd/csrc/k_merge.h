@@ -243,6 +243,18 @@ struct MLine {
 // kSeg (the multi-GPU owner): bin b's records are nseg segments, one per sender -- segment s at address SO[b * nseg + s]
 // (the receive buffer, or the owner's own slab), after SP[b * nseg + s] records of the bin (k_stage_segments)
 constexpr int MO_SEG_MAX = 64;
+// Debug build (make libmobheat_dbg.so: MOBHEAT_BOUNDS_CHECK=1): every segment read of the kSeg variant must lie in one
+// of the two ranges the host declared for the launch (merge_sorted: the receive buffer, the owner's slabs) -- else the
+// kernel prints the bin, segment and address and traps, so that a fault names its access
+#ifndef MOBHEAT_BOUNDS_CHECK
+#define MOBHEAT_BOUNDS_CHECK 0
+#endif
+struct SegBounds {
+    unsigned long long lo[2], hi[2];
+};
+#if MOBHEAT_BOUNDS_CHECK
+__device__ SegBounds g_seg_bounds;
+#endif
 template <typename Rec, bool kResident = false, bool kCoop = false, bool kSeg = false>
 __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_merge_owned(const Rec *__restrict__ parts, int64_t slab,
                                                             const unsigned long long *__restrict__ SO, const unsigned *__restrict__ SP, int nseg,
@@ -623,7 +635,17 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                     const int mid = (lo + hi) >> 1;
                     if (seg_pre[mid] <= v) lo = mid; else hi = mid;
                 }
-                return (const Rec *)(uintptr_t)seg_base[lo] + (v - seg_pre[lo]);
+                const Rec *rp = (const Rec *)(uintptr_t)seg_base[lo] + (v - seg_pre[lo]);
+#if MOBHEAT_BOUNDS_CHECK
+                const unsigned long long a = (unsigned long long)(uintptr_t)rp, e = a + sizeof(Rec);
+                const SegBounds &B = g_seg_bounds;
+                if (!((a >= B.lo[0] && e <= B.hi[0]) || (a >= B.lo[1] && e <= B.hi[1]))) {
+                    printf("k_merge_owned: bin %d segment %d record %u at 0x%llx outside [0x%llx, 0x%llx) and [0x%llx, 0x%llx)\n",
+                           bin, lo, v, a, B.lo[0], B.hi[0], B.lo[1], B.hi[1]);
+                    __builtin_trap();
+                }
+#endif
+                return rp;
             } else {
                 return bp + i;
             }

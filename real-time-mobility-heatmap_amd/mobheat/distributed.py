@@ -63,14 +63,16 @@ def all_gather_summaries(summary, device, status=0):
 def exchange(streams, device, status=0):
     """all_to_all of several variable-size record streams: one all_to_all of all the per-destination counts (the
     batch's single host synchronization of the exchange; it also carries each rank's status: a rank whose stage failed
-    sends status != 0 and no streams, and every rank raises PeerFailed before the payloads move), then one all_to_all
-    per stream.  Payloads move as 8-byte words (record sizes are multiples of 8): a rank's share at 1e8 events per GPU
-    is several GB, past 2^31 single-byte elements.  Returns [(recv uint8 tensor, recv_counts per source)] in stream
-    order."""
+    sends status != 0 and no streams, and every rank raises PeerFailed before the payloads move -- and each rank's
+    largest piece, so that every rank runs the same rounds), then each stream's payload (_exchange_words: rounds of at
+    most round_bytes() per rank pair).  Payloads move as 8-byte words (record sizes are multiples of 8): a rank's share
+    at 1e8 events per GPU is several GB, past 2^31 single-byte elements.  Returns [(recv uint8 tensor, recv_counts per
+    source)] in stream order."""
     world = dist.get_world_size()
     k = len(streams)
     assert k <= MAX_STREAMS
-    cnt = [[(streams[j].counts[r] if j < k else 0) for j in range(MAX_STREAMS)] + [status] for r in range(world)]
+    big = [max([int(c) * (s.rec_bytes // 8) for c in s.counts] + [0]) for s in streams] + [0] * (MAX_STREAMS - k)
+    cnt = [[(streams[j].counts[r] if j < k else 0) for j in range(MAX_STREAMS)] + [status] + big for r in range(world)]
     sc = torch.tensor(cnt, dtype=torch.int64, device=device)
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc)
@@ -87,26 +89,63 @@ def exchange(streams, device, status=0):
         recv_counts = [int(rcounts[r][j]) for r in range(world)]
         nrecv, nsend = sum(recv_counts), int(sum(s.counts))
         recv = torch.empty(max(nrecv * w, 2), dtype=torch.int64, device=device)
-        dist.all_to_all_single(recv[: nrecv * w], s.buf[: nsend * s.rec_bytes].view(torch.int64),
-                               [c * w for c in recv_counts], [int(c) * w for c in s.counts])
+        biggest = max(int(rcounts[r][MAX_STREAMS + 1 + j]) for r in range(world))   # (every sender's largest piece)
+        _exchange_words(recv, s.buf[: nsend * s.rec_bytes].view(torch.int64), [c * w for c in recv_counts],
+                        [int(c) * w for c in s.counts], biggest)
         out.append((recv.view(torch.uint8), recv_counts))
     assert len(out) == k
     return out
 
 
-# bytes of one (sender, receiver) pair moved per all_to_all round: a rank's share of a 1e8-event batch is ~3.2 GB of
-# records, and one all_to_all of it faulted the GPU (profiles/r5: hm_stage_merge saw the illegal access right after the
-# 3.2-GB all_to_all of a world-1 RCCL group, while 4.5M-row batches passed) -- the payload moves in rounds of at most this
-# per pair, each round's pieces received in place.  0 = one round.
-EXCHANGE_ROUND_BYTES = int(os.environ.get("MOBHEAT_EXCHANGE_ROUND_BYTES", str(1 << 30)))
+# The largest piece of one (sender, receiver) pair that one all_to_all call moves -- a hard cap.  What was seen
+# (round 5): the sharded bench's single all_to_all of a rank's ~3.2 GB of records (a world-1 RCCL group: the rank's
+# whole share sent to itself in one call) was followed by hipErrorIllegalAddress, reported at hm_stage_merge's first
+# error check after the collective (profiles/r5/r5e/fault_before_rounds.log; gpurun_out r5c2/r5d the same); the same
+# exchange moved in rounds of <= 1 GiB per pair into the same receive buffer merged clean
+# (profiles/r5/r5e/bench_sharded.log), and 4.5M-row batches (144 MB in one call) always passed.  So the fault follows
+# one call that moves more than 2 GiB per peer (a 32-bit byte count or offset on the collective's path is the likely
+# limit; which kernel took the illegal access was not isolated -- the library's debug build, MOBHEAT_BOUNDS_CHECK, now
+# checks every segment read of the owner's merge).  The exchange never issues such a call: whatever
+# MOBHEAT_EXCHANGE_ROUND_BYTES says, a round moves at most this much per pair
+# (tests/test_distributed_gloo.py::test_exchange_round_cap records every call's per-pair sizes).
+EXCHANGE_ROUND_CAP = 1 << 30
+# the round size asked for (bytes per rank pair); values <= 0 or above the cap mean the cap
+EXCHANGE_ROUND_BYTES = int(os.environ.get("MOBHEAT_EXCHANGE_ROUND_BYTES", str(EXCHANGE_ROUND_CAP)))
+
+
+def round_bytes():
+    """bytes per rank pair and all_to_all call: EXCHANGE_ROUND_BYTES clamped to (0, EXCHANGE_ROUND_CAP], whole words"""
+    b = EXCHANGE_ROUND_BYTES
+    if b <= 0 or b > EXCHANGE_ROUND_CAP:
+        b = EXCHANGE_ROUND_CAP
+    return max(8, b & ~7)
+
+
+def _exchange_words(recv, words, recv_words, send_words, biggest):
+    """all_to_all of int64 words: send_words[r] of `words` (concatenated by destination) to rank r, recv_words[s] from
+    rank s into `recv` (concatenated by source).  `biggest`: the largest piece any pair moves, in words, the same on
+    every rank (it sets the round count); rounds of at most round_bytes() per pair, every piece received in place."""
+    world = len(send_words)
+    step = round_bytes() // 8
+    rounds = max(1, -(-int(biggest) // step))
+    if rounds == 1:
+        dist.all_to_all_single(recv[: sum(recv_words)], words, list(recv_words), list(send_words))
+        return
+    s_off = [sum(send_words[:r]) for r in range(world)]
+    r_off = [sum(recv_words[:s]) for s in range(world)]
+    for k in range(rounds):
+        a = k * step
+        ins = [words[s_off[r] + a: s_off[r] + a + max(0, min(step, send_words[r] - a))] for r in range(world)]
+        outs = [recv[r_off[s] + a: r_off[s] + a + max(0, min(step, recv_words[s] - a))] for s in range(world)]
+        _all_to_all_views(outs, ins)
 
 
 def exchange_chunks(buf, send_bytes, device, status=0):
     """The batch's record exchange: one all_gather of every rank's per-destination chunk sizes in bytes (with its
     status: a rank whose stage failed sends status != 0 and no chunks, and every rank raises PeerFailed before the
-    payloads move), then the chunks -- one all_to_all, or (a pair moving more than EXCHANGE_ROUND_BYTES) rounds of
-    all_to_all of at most that per pair, every piece received at its place -- as 8-byte words (chunk sizes are multiples
-    of 32).  Returns (recv uint8 tensor, recv_bytes per source rank)."""
+    payloads move), then the chunks in rounds of at most round_bytes() per rank pair (one all_to_all when every pair
+    fits), every piece received at its place -- as 8-byte words (chunk sizes are multiples of 32).  Returns (recv
+    uint8 tensor, recv_bytes per source rank)."""
     world, rank = dist.get_world_size(), dist.get_rank()
     row = torch.tensor([int(send_bytes[r]) if send_bytes else 0 for r in range(world)] + [status], dtype=torch.int64,
                        device=device)
@@ -123,19 +162,8 @@ def exchange_chunks(buf, send_bytes, device, status=0):
     nrecv, nsend = sum(recv_bytes), int(sum(send_bytes))
     recv = torch.empty(max(nrecv // 8, 2), dtype=torch.int64, device=device)
     words = buf[:nsend].view(torch.int64) if nsend else torch.empty(0, dtype=torch.int64, device=device)
-    step = EXCHANGE_ROUND_BYTES // 8
     biggest = max(max(r[:world]) for r in M) // 8
-    rounds = 1 if step <= 0 or biggest <= step else -(-biggest // step)
-    if rounds == 1:
-        dist.all_to_all_single(recv[: nrecv // 8], words, [b // 8 for b in recv_bytes], [int(b) // 8 for b in send_bytes])
-        return recv.view(torch.uint8), recv_bytes
-    s_off = [sum(int(b) for b in send_bytes[:r]) // 8 for r in range(world)]
-    r_off = [sum(recv_bytes[:s]) // 8 for s in range(world)]
-    for k in range(rounds):
-        a = k * step
-        ins = [words[s_off[r] + a: s_off[r] + a + max(0, min(step, int(send_bytes[r]) // 8 - a))] for r in range(world)]
-        outs = [recv[r_off[s] + a: r_off[s] + a + max(0, min(step, recv_bytes[s] // 8 - a))] for s in range(world)]
-        _all_to_all_views(outs, ins)
+    _exchange_words(recv, words, [b // 8 for b in recv_bytes], [int(b) // 8 for b in send_bytes], biggest)
     return recv.view(torch.uint8), recv_bytes
 
 
@@ -274,20 +302,25 @@ class ShardedHeatmap:
         # receive buffer (hm_stage_finish), so they stay alive until the next process_batch call
         self._recv = None
 
+    def after_collective(self):
+        """Order the library's next reads after the collectives queued so far: the library reads received buffers on
+        its own stream, after RCCL's (torch's current stream) -- an event wait between the two streams (the stages'
+        wait_stream, hm_stream_wait), not a host synchronization; without wait_stream, the current stream is
+        synchronized; on the CPU (gloo) nothing is asynchronous."""
+        if self.device.type != "cuda":
+            return
+        wait = getattr(self.stages, "wait_stream", None)
+        if wait is not None:
+            wait(torch.cuda.current_stream(self.device))
+        else:
+            torch.cuda.current_stream(self.device).synchronize()
+
     def process_batch(self, epoch, batch, out_memory=HM_MEM_DEVICE, sync=None):
         """One micro-batch on this rank.  A stage that raises on one rank makes every rank leave at the next
         collective (the failed rank re-raises its error, the others PeerFailed), so no rank waits on a collective its
         peers never reach."""
-        # the library reads the received buffers on its own stream, after RCCL's (torch's current stream): an event
-        # wait between the two streams (the stages' wait_stream), not a host synchronization
         if sync is None:
-            wait = getattr(self.stages, "wait_stream", None)
-            if self.device.type == "cuda" and wait is not None:
-                sync = lambda: wait(torch.cuda.current_stream(self.device))   # noqa: E731
-            elif self.device.type == "cuda":
-                sync = lambda: torch.cuda.current_stream(self.device).synchronize()   # noqa: E731
-            else:
-                sync = lambda: None   # noqa: E731
+            sync = self.after_collective
         err = None
         clock = _PhaseClock()
         try:

@@ -232,6 +232,10 @@ class RankRunner:
             from .distributed import exchange_chunks
             buf, sb = send if send is not None else (None, [0] * self.world)
             recv, rb = exchange_chunks(buf, sb, self.device)
+            # hm_stage_ingest reads the columns on the library's stream: it waits for the all_to_all that wrote them
+            # (queued on torch's current stream) -- ADVICE r5: without this wait, ranks could ingest columns that had
+            # only partly arrived
+            self.sharded.after_collective()
             n = int(bounds[self.rank + 1] - bounds[self.rank])
             assert sum(rb) == packed_bytes(n), (sum(rb), n)
             self._cols = recv   # (alive until the next batch: the library reads it)

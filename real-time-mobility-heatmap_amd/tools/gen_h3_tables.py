@@ -28,7 +28,9 @@ the 12 vertices each seen by exactly five faces, 122 base cells, and equality wi
 could be recalled from upstream (cells 0..58 of ``baseCellData``, face 0/1 rows of ``faceIjkBaseCells``,
 faces 0/1 of ``faceNeighbors``).
 
-Output: ``csrc/h3_tables.inc`` (C99/HIP initialisers, included by the device code and by the oracle).
+Output: ``csrc/h3_tables.inc`` (C99/HIP initialisers, included by the product's device and host code only: the oracle
+derives its own tables, oracle/h3_tables_derive.c, and never includes this file -- DESIGN.md §3,
+tests/test_h3_oracle.py::test_oracle_does_not_include_product_tables).
 """
 import itertools
 import math

@@ -283,3 +283,68 @@ def test_exchange_from_one_sender_in_rounds():
         assert got[r][0] == [8 * n] + [0] * (world - 1)
         assert got[r][1] == list(range(start, start + n))
         start += n
+
+
+def _cap_worker(rank, world, port, q):
+    """exchange_chunks and exchange under round sizes the cap must clamp, every all_to_all call's per-pair element
+    counts recorded"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mobheat import distributed
+    calls = []
+    real_single = distributed.dist.all_to_all_single
+
+    def rec_single(out, inp, out_split=None, in_split=None, **kw):
+        calls.append(max(list(out_split or [out.numel() // world]) + list(in_split or [inp.numel() // world])))
+        return real_single(out, inp, out_split, in_split, **kw)
+
+    distributed.dist.all_to_all_single = rec_single
+    distributed.EXCHANGE_ROUND_CAP = 256   # (bytes per pair and call: 32 words)
+    got = []
+    try:
+        for asked in (0, -8, 1 << 40, 100, 256):
+            distributed.EXCHANGE_ROUND_BYTES = asked
+            # chunk for rank r: 8 * (37 * (rank + 1) + 11 * r) bytes, words numbered by (sender, receiver, index)
+            sizes = [8 * (37 * (rank + 1) + 11 * r) for r in range(world)]
+            words = np.concatenate([(rank * 1000 + r * 100000) * 1000 + np.arange(s // 8) for r, s in enumerate(sizes)])
+            first = len(calls)
+            recv, rb = distributed.exchange_chunks(torch.from_numpy(words).view(torch.uint8), sizes, torch.device("cpu"))
+            payload_calls = calls[first + 0:]   # (exchange_chunks' size matrix moves by all_gather: not recorded)
+            # the winners' form: 8-B records
+            st = distributed.Stream("w", torch.from_numpy(words).view(torch.uint8), [s // 8 for s in sizes], 8)
+            first_w = len(calls)
+            [(wrecv, wrc)] = distributed.exchange([st], torch.device("cpu"))
+            got.append((asked, rb, recv.view(torch.int64)[: sum(rb) // 8].tolist(), payload_calls, wrc,
+                        wrecv.view(torch.int64)[: sum(wrc)].tolist(), calls[first_w + 1:]))
+    finally:
+        distributed.dist.all_to_all_single = real_single
+    q.put((rank, got))
+    dist.destroy_process_group()
+
+
+def test_exchange_round_cap():
+    """no all_to_all call moves more than distributed.EXCHANGE_ROUND_CAP bytes per rank pair,
+    whatever MOBHEAT_EXCHANGE_ROUND_BYTES asks (0, negative, above the cap: the cap; below it: that size), and the
+    pieces land where one call would put them"""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cap_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in range(world):
+        for asked, rb, words, calls, wrc, wwords, wcalls in got[rank]:
+            cap_words = (256 if asked <= 0 or asked > 256 else asked) // 8
+            assert calls and max(calls) <= cap_words, (asked, calls)
+            assert wcalls and max(wcalls) <= cap_words, (asked, wcalls)
+            # the biggest piece is 8 * (37 * 2 + 11) = 680 B: several rounds under the cap
+            assert len(calls) >= 3 and len(wcalls) >= 3
+            exp_rb = [8 * (37 * (s + 1) + 11 * rank) for s in range(world)]
+            exp = [w for s in range(world) for w in ((s * 1000 + rank * 100000) * 1000 + np.arange(exp_rb[s] // 8))]
+            assert rb == exp_rb and words == exp
+            assert wrc == [b // 8 for b in exp_rb] and wwords == exp

@@ -159,3 +159,39 @@ def test_shm_arena_keeps_replaced_regions_mapped_until_released():
         assert not a._retired
     finally:
         a.close()
+
+
+def test_run_device_orders_ingest_after_column_exchange(monkeypatch):
+    """the device-column path (RankRunner.run_device) must make the library's stream wait for the
+    all_to_all that delivered the rank's columns before hm_stage_ingest reads them -- exchange, then the stream wait
+    (ShardedHeatmap.after_collective), then the stages; and the columns handed to the stages are the received slice."""
+    from mobheat import distributed, sharded
+    import torch
+    order = []
+    recv = torch.zeros(sharded.packed_bytes(5), dtype=torch.uint8)
+
+    def fake_exchange(buf, sb, device, status=0):
+        order.append("exchange")
+        return recv, [sharded.packed_bytes(5)]
+
+    class Stop(Exception):
+        pass
+
+    class FakeSharded:
+        def after_collective(self):
+            order.append("wait")
+
+        def process_batch(self, epoch, batch, out_memory=None):
+            order.append(("stages", batch["n"], batch["lat"] >= recv.data_ptr()))
+            raise Stop
+
+    class FakeEng:
+        def state_version(self):
+            return 0
+
+    monkeypatch.setattr(distributed, "exchange_chunks", fake_exchange)
+    r = sharded.RankRunner.__new__(sharded.RankRunner)
+    r.rank, r.world, r.engine, r.sharded, r.device = 0, 1, FakeEng(), FakeSharded(), torch.device("cpu")
+    with pytest.raises(Stop):
+        r.run_device(3, {}, np.array([0, 5]), None)
+    assert order == ["exchange", "wait", ("stages", 5, True)]
