@@ -426,7 +426,8 @@ int hm_selftest_cells_to_boundary_host(const uint64_t *cells, int64_t n, double 
  * LDS tables into its buckets, [5] stage API: tile records this rank sent, [6] device + pinned-host allocations and
  * [7] frees the context made since hm_create (steady-state batches make none: tests/test_gpu_parity.py), [8] 1 if the
  * direct path's rows were binned by the ingest itself (no separate partition pass), [9] stage API: of [5], the records
- * of bins this rank owns, kept in its slabs (hm_stage_sizes.n_self_records). */
+ * of bins this rank owns, kept in its slabs (hm_stage_sizes.n_self_records), [10] hm_process_batch: the chunks the
+ * batch was pipelined in (each chunk's ingest overlapping the previous chunk's merge; 0: not pipelined). */
 int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n);
 /* Version of the persistent tile state: incremented when a batch starts merging into it (hm_process_batch,
  * hm_stage_merge, growth).  A call that failed without changing it left the state as it was (-1: ctx NULL). */

@@ -37,7 +37,12 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     if (hipSetDevice(ctx->device) != hipSuccess) { ctx->err = "hipSetDevice"; return fail("create"); }
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking) != hipSuccess) { ctx->err = "stream"; return fail("create"); }
+        hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->merge_stream, hipStreamNonBlocking) != hipSuccess) { ctx->err = "stream"; return fail("create"); }
+    for (auto &e : ctx->pipe_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
+    if (hipEventCreateWithFlags(&ctx->pipe_rb, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->pipe_done, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     for (auto &e : ctx->side_ev)
         if (hipEventCreate(&e) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     if (hipEventCreateWithFlags(&ctx->winfo_ev, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
@@ -104,6 +109,10 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     if (const char *m = getenv("MOBHEAT_STAGE_SELF")) ctx->self_hold_ok = strcmp(m, "copy") != 0;
     if (const char *m = getenv("MOBHEAT_DEDUP_DENSE")) ctx->dense_ok = strcmp(m, "0") != 0;
     if (const char *m = getenv("MOBHEAT_SUBBINS")) ctx->subbins_mode = !strcmp(m, "0") ? 0 : !strcmp(m, "1") ? 1 : 2;
+    // MOBHEAT_PIPELINE: unset / 0 never pipelines a batch (the default: slower on the bench, host_pipe.h), K >= 2
+    // pipelines every binned batch in K chunks (tests, A/B), "auto": batches of >= PIPE_MIN_ROWS rows in PIPE_CHUNKS chunks
+    if (const char *m = getenv("MOBHEAT_PIPELINE")) ctx->pipe_mode = !strcmp(m, "auto") ? -1 : std::max(0, std::min(atoi(m), hm_ctx::PIPE_MAX));
+    if (const char *m = getenv("MOBHEAT_TEST_SLAB_CAP")) ctx->test_slab_cap = (unsigned)std::max(0, atoi(m));
     // the registry, its census and the batch statistics side by side (one reset, one readback after k_ingest)
     if (hipMalloc(&ctx->d_wreg, REG_BLOCK_BYTES) != hipSuccess || !(ctx->d_wcount = ctx->d_wreg + WREG_SLOTS + 1) ||
         !(ctx->d_st = (DevStats *)(ctx->d_wreg + 2 * (WREG_SLOTS + 1))) ||
@@ -179,7 +188,8 @@ void hm_destroy(hm_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
-    DevBuf *bufs[] = {&ctx->in_lat, &ctx->in_lon, &ctx->in_ts, &ctx->in_speed, &ctx->in_sv, &ctx->in_vkey, &ctx->in_rv,
+    if (ctx->merge_stream) (void)hipStreamSynchronize(ctx->merge_stream);
+    DevBuf *bufs[] = {&ctx->pl_cur, &ctx->pl_slow, &ctx->pl_O, &ctx->pl_cnt, &ctx->pl_T, &ctx->in_lat, &ctx->in_lon, &ctx->in_ts, &ctx->in_speed, &ctx->in_sv, &ctx->in_vkey, &ctx->in_rv,
                       &ctx->cell, &ctx->wstart, &ctx->flags, &ctx->win, &ctx->rows, &ctx->block_counts, &ctx->block_offs,
                       &ctx->partials, &ctx->cands, &ctx->slow, &ctx->parts_sorted, &ctx->parts_regrow, &ctx->parts_regrow_sorted, &ctx->stage_meta, &ctx->stage_C, &ctx->stage_P,
                       &ctx->stage_SO, &ctx->stage_SP, &ctx->stage_T, &ctx->cands_recv, &ctx->stage_tmp, &ctx->rp_H, &ctx->rp_O,
@@ -229,6 +239,11 @@ void hm_destroy(hm_ctx *ctx) {
         if (e) (void)hipEventDestroy(e);
     if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);
+    if (ctx->merge_stream) (void)hipStreamDestroy(ctx->merge_stream);
+    for (auto &e : ctx->pipe_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->pipe_rb) (void)hipEventDestroy(ctx->pipe_rb);
+    if (ctx->pipe_done) (void)hipEventDestroy(ctx->pipe_done);
     for (auto &e : ctx->side_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->winfo_ev) (void)hipEventDestroy(ctx->winfo_ev);
@@ -256,6 +271,7 @@ int hm_last_counts(const hm_ctx *ctx, int64_t *c, int32_t n) {
     if (n > 7) c[7] = ctx->n_frees;
     if (n > 8) c[8] = ctx->last_binned;
     if (n > 9) c[9] = ctx->staged ? ctx->stage_self_recs : 0;
+    if (n > 10) c[10] = ctx->staged ? 0 : ctx->last_pipe_chunks;
     return HM_OK;
 }
 
@@ -285,11 +301,23 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
     if ((rc = stage_inputs(ctx, in, &I.lat, &I.lon, &I.ts, &I.sp, &I.sv, &I.vk, &I.rv))) return rc;
     // 2. snap + window registry + event keys
     const bool sub = ctx->subbins_mode == 1 || (ctx->subbins_mode == 2 && ctx->merge_coop);
-    if ((rc = phase_local(ctx, I, late_wm, true, sub, ctx->early_ok && !ctx->dedup_main, ctx->offsets_early))) return rc;
+    const bool early = ctx->early_ok && !ctx->dedup_main;
+    // a large binned batch is pipelined (host_pipe.h): its chunks' ingest overlaps the previous chunk's merge, and the
+    // rows come back densified (piped); else the ingest, then the merge path below
+    const int K = pipe_chunks_for(ctx, I);
+    bool piped = false;
+    ctx->last_pipe_chunks = 0;
+    if (K > 1) {
+        bool to_table = false;
+        if ((rc = process_pipelined(ctx, I, late_wm, sub, K, early, to_table))) return rc;
+        piped = !to_table;
+    } else if ((rc = phase_local(ctx, I, late_wm, true, sub, early, ctx->offsets_early))) {
+        return rc;
+    }
     DevStats s1 = *ctx->h_st;
     const int64_t n_agg = (int64_t)s1.n_valid - (int64_t)s1.n_late;
     // the aggregation path of this batch (table mode: two LDS passes first; direct: every row a record)
-    const bool table = choose_table(ctx, n_agg, s1.sample_max_run);
+    const bool table = !piped && choose_table(ctx, n_agg, s1.sample_max_run);
     ctx->last_table = table;
     // 4. dedup over the batch's valid rows -- on the side stream, concurrently with step 3 (the rerun of the max on a
     // full table, after the fused one gave up, prepares that table on the main stream: it stays there)
@@ -310,7 +338,7 @@ int hm_process_batch(hm_ctx *ctx, int64_t epoch_id, const hm_batch_in *in, int32
         if ((rc = phase_table(ctx, I, n_agg, &n_parts))) return rc;
         HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
         if ((rc = merge_partials(ctx, (const TilePartial *)ctx->partials.p, n_parts))) return rc;
-    } else {
+    } else if (!piped) {
         HIPCHK(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
         if ((rc = merge_events(ctx, I, n_agg))) return rc;
     }

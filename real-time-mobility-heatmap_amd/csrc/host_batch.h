@@ -36,9 +36,9 @@ static unsigned slab_cap_for(int64_t n, double skew, int64_t nbins) {
 // critical path (profiles/r5/r5tl/)
 static int launch_side_dedup(hm_ctx *ctx, const Inputs *I);
 static int bin_offsets(hm_ctx *ctx);
-static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool allow_bin = false, bool sub = false,
-                       bool early_dedup = false, bool offsets = false) {
-    int64_t n = I.n;
+// the batch's per-row buffers, dedup tables, bins and counters ready, k_batch_reset launched (phase_local, the
+// pipelined batch)
+static int prepare_local(hm_ctx *ctx, int64_t n, int64_t late_wm_ms, bool bin, bool sub) {
     int rc;
     // the previous call's side-stream dedup may still run (a stage batch that a peer's failure ended before
     // hm_stage_send waited for it -- ADVICE r5): nothing below touches its tables, flags or rows before it is done
@@ -63,12 +63,12 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
             HIPCHK(ctx, hipMemsetAsync(ctx->dense.p, 0, cap * 8, ctx->stream));
         }
     }
-    const bool bin = allow_bin && n > 0 && choose_binned(ctx, n);
     ctx->keys_partial = bin;   // (k_ingest<true> writes the keys of the exception and sampled rows only)
     ctx->keys_late_us = late_wm_ms * 1000;
     ctx->sub_bits = bin && sub ? SUB_BITS : 0;
     const int nbins = RP_BINS << ctx->sub_bits;
     ctx->slab_cap = bin ? slab_cap_for(n, ctx->bin_skew, nbins) : 0;
+    if (bin && ctx->test_slab_cap) ctx->slab_cap = std::min(ctx->slab_cap, ctx->test_slab_cap);
     ctx->binned = false;
     ctx->bin_offsets_ready = false;
     if ((rc = ensure(ctx, ctx->bin_cur, ((RP_BINS << SUB_BITS) + 1) * 4))) return rc;
@@ -81,6 +81,29 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
                            nw, (unsigned *)ctx->bin_cur.p, nbins + 1);
         HIPCHK(ctx, hipGetLastError());
     }
+    return HM_OK;
+}
+
+// k_ingest over rows [a, b) of the batch I (bin: k_ingest<true>, the rows' records into their bin slabs)
+static void launch_ingest(hm_ctx *ctx, const Inputs &I, int64_t a, int64_t b, bool bin, int64_t late_wm_ms) {
+    const int blocks = (int)std::min<int64_t>((b - a + IG_THREADS - 1) / IG_THREADS, bin ? ctx->ingest_grid_bin : ctx->ingest_grid);
+    auto kern = bin ? k_ingest<true> : k_ingest<false>;
+    hipLaunchKernelGGL(kern, dim3(std::max(blocks, 1)), dim3(IG_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.vk, a, b,
+                       ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
+                       (uint64_t *)ctx->keys.p, ctx->dfused.tab, ctx->dfused.cap - 1, (unsigned int *)ctx->dfused.used.p,
+                       ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
+                       ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st, I.sp, I.sv,
+                       (unsigned *)ctx->bin_cur.p, bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap,
+                       (unsigned long long *)ctx->dense.p, ctx->dense_cap, ctx->sub_bits, hs_stride(I.n) - 1);
+}
+
+static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool allow_bin = false, bool sub = false,
+                       bool early_dedup = false, bool offsets = false) {
+    int64_t n = I.n;
+    int rc;
+    const bool bin = allow_bin && n > 0 && choose_binned(ctx, n);
+    if ((rc = prepare_local(ctx, n, late_wm_ms, bin, sub))) return rc;
+    const int nbins = RP_BINS << ctx->sub_bits;
     HIPCHK(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
     if (n > 0) {
         // host inputs: row chunks copied on copy_stream, each chunk's k_ingest launched behind its copy (the copies
@@ -101,22 +124,16 @@ static int phase_local(hm_ctx *ctx, const Inputs &I, int64_t late_wm_ms, bool al
                 HIPCHK(ctx, hipEventRecord(ctx->h2d_ev[c], ctx->copy_stream));
                 HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->h2d_ev[c], 0));
             }
-            const int blocks = (int)std::min<int64_t>((b - a + IG_THREADS - 1) / IG_THREADS, bin ? ctx->ingest_grid_bin : ctx->ingest_grid);
-            auto kern = bin ? k_ingest<true> : k_ingest<false>;
-            hipLaunchKernelGGL(kern, dim3(blocks), dim3(IG_THREADS), 0, ctx->stream, I.lat, I.lon, I.ts, I.rv, I.vk, a, b,
-                               ctx->cfg.h3_res, make_floor_div(ctx->cfg.tile_us), late_wm_ms * 1000, (uint8_t *)ctx->flags.p,
-                               (uint64_t *)ctx->keys.p, ctx->dfused.tab, ctx->dfused.cap - 1, (unsigned int *)ctx->dfused.used.p,
-                               ctx->d_scratch + ctx->dfused.used_word, (unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD,
-                               ctx->d_scratch + GIVEUP_WORD, ctx->d_wreg, ctx->d_wcount, ctx->d_st, I.sp, I.sv,
-                               (unsigned *)ctx->bin_cur.p, bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap,
-                               (unsigned long long *)ctx->dense.p, ctx->dense_cap, ctx->sub_bits, hs_stride(n) - 1);
+            launch_ingest(ctx, I, a, b, bin, late_wm_ms);
         }
         ctx->n_h2d = 0;
         hipLaunchKernelGGL(k_ingest_exact, dim3(256), dim3(256), 0, ctx->stream, I.lat, I.lon, ctx->cfg.h3_res,
                            (const unsigned int *)ctx->slow.p, ctx->d_scratch + SLOW_WORD, (uint64_t *)ctx->keys.p, I.sp, I.sv,
                            (const unsigned long long *)ctx->d_wreg, (unsigned *)ctx->bin_cur.p,
-                           bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap, ctx->d_st, ctx->sub_bits);
-        hipLaunchKernelGGL(k_sample_heavy, dim3(1), dim3(HS_THREADS), 0, ctx->stream, (const uint64_t *)ctx->keys.p, n, ctx->d_st);
+                           bin ? (EventRec *)ctx->parts_sorted.p : nullptr, ctx->slab_cap, ctx->d_st, ctx->sub_bits,
+                           (const unsigned long long *)nullptr);
+        hipLaunchKernelGGL(k_sample_heavy, dim3(1), dim3(HS_THREADS), 0, ctx->stream, (const uint64_t *)ctx->keys.p, n, hs_stride(n),
+                           ctx->d_st);
         HIPCHK(ctx, hipGetLastError());
         ctx->dfused.dirty = true;
         // (a slab that overflowed makes the batch re-partition: these offsets then go unused)
@@ -263,21 +280,24 @@ static int ensure_outputs(hm_ctx *ctx, int64_t n_rows) {
 }
 
 // densify the merge's per-bin row segments into the output rows (k_gap_counts / k_fill_gaps, then a buffer swap)
-static int rows_densify(hm_ctx *ctx, int64_t ntiles) {
+// (O / cnt / nseg: the segments' row offsets and touched-key counts; default rp_O and bin_cnt over the RP_BINS bins --
+// a pipelined batch passes its chunks' segments, nseg = chunks x RP_BINS, ntiles 1)
+static int rows_densify(hm_ctx *ctx, int64_t ntiles, const unsigned long long *O = nullptr, const unsigned *cnt = nullptr,
+                        int nseg = RP_BINS) {
     int rc;
-    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, (const unsigned *)ctx->bin_cnt.p, (int64_t)RP_BINS,
-                       (unsigned long long *)ctx->bin_off.p, &ctx->d_st->n_touched);
-    if ((rc = ensure(ctx, ctx->gapbuf, (size_t)RP_BINS * 24))) return rc;
-    unsigned *gg = (unsigned *)ctx->gapbuf.p, *gv = gg + RP_BINS;
-    unsigned long long *gvo = (unsigned long long *)(gv + RP_BINS), *ggo = (unsigned long long *)ctx->bin_off.p;
-    const unsigned long long *O = (const unsigned long long *)ctx->rp_O.p;
-    hipLaunchKernelGGL(k_gap_counts, dim3(grid_for(RP_BINS, 256)), dim3(256), 0, ctx->stream, O, ntiles, RP_BINS,
-                       (const unsigned *)ctx->bin_cnt.p, &ctx->d_st->n_touched, gg, gv);
-    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, gg, (int64_t)RP_BINS, ggo, ctx->d_scratch + GAPS_WORD);
-    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, gv, (int64_t)RP_BINS, gvo, ctx->d_scratch + GAPS_WORD + 1);
-    hipLaunchKernelGGL(k_fill_gaps, dim3(RP_BINS), dim3(256), 0, ctx->stream, staged_rows(ctx), O, ntiles, RP_BINS,
-                       (const unsigned *)ctx->bin_cnt.p, &ctx->d_st->n_touched, (const unsigned *)gg,
-                       (const unsigned long long *)ggo, (const unsigned long long *)gvo);
+    if (!O) O = (const unsigned long long *)ctx->rp_O.p;
+    if (!cnt) cnt = (const unsigned *)ctx->bin_cnt.p;
+    if ((rc = ensure(ctx, ctx->bin_off, (size_t)nseg * 8)) || (rc = ensure(ctx, ctx->gapbuf, (size_t)nseg * 24))) return rc;
+    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, (int64_t)nseg, (unsigned long long *)ctx->bin_off.p,
+                       &ctx->d_st->n_touched);
+    unsigned *gg = (unsigned *)ctx->gapbuf.p, *gv = gg + nseg;
+    unsigned long long *gvo = (unsigned long long *)(gv + nseg), *ggo = (unsigned long long *)ctx->bin_off.p;
+    hipLaunchKernelGGL(k_gap_counts, dim3(grid_for(nseg, 256)), dim3(256), 0, ctx->stream, O, ntiles, nseg, cnt,
+                       &ctx->d_st->n_touched, gg, gv);
+    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, gg, (int64_t)nseg, ggo, ctx->d_scratch + GAPS_WORD);
+    hipLaunchKernelGGL(k_cp_scan, dim3(1), dim3(1024), 0, ctx->stream, gv, (int64_t)nseg, gvo, ctx->d_scratch + GAPS_WORD + 1);
+    hipLaunchKernelGGL(k_fill_gaps, dim3(nseg), dim3(256), 0, ctx->stream, staged_rows(ctx), O, ntiles, nseg, cnt,
+                       &ctx->d_st->n_touched, (const unsigned *)gg, (const unsigned long long *)ggo, (const unsigned long long *)gvo);
     HIPCHK(ctx, hipGetLastError());
     std::swap(ctx->s_cell, ctx->o_cell);
     std::swap(ctx->s_ws, ctx->o_ws);

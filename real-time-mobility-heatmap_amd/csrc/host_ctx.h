@@ -206,6 +206,21 @@ struct hm_ctx {
     std::vector<unsigned> stage_cen;   // a world of one: the census of its self-held records (host -> its own chunk)
     std::vector<unsigned long long> stage_gwreg;       // the batch's global window registry (WREG_SLOTS wenc)
     std::vector<unsigned> stage_gslot;                 // this rank's registry slot -> global slot
+    // a pipelined batch (host_pipe.h): its chunks' k_ingest<true> on the main stream, each chunk's merge on merge_stream
+    // as soon as the chunk's records are binned; pipe_mode: MOBHEAT_PIPELINE (0 off -- the default: measured slower,
+    // host_pipe.h --, K chunks, -1 "auto": PIPE_CHUNKS chunks from PIPE_MIN_ROWS rows)
+    static constexpr int PIPE_MAX = 16;
+    hipStream_t merge_stream = nullptr;
+    hipEvent_t pipe_ev[PIPE_MAX] = {};   // chunk k's records binned (main stream)
+    hipEvent_t pipe_rb = nullptr;        // the registry / census / statistics readback of the latest chunk
+    hipEvent_t pipe_done = nullptr;      // the last merge (merge stream)
+    int pipe_mode = 0;
+    int last_pipe_chunks = 0;            // hm_last_counts [10]: chunks of the last batch (0: not pipelined)
+    DevBuf pl_cur;                       // per chunk: the bin cursors after it (nbins + 1 words)
+    DevBuf pl_slow;                      // per chunk: the exception count after it (K + 1 words, [0] = 0)
+    DevBuf pl_O, pl_cnt;                 // the chunks' bins as row segments: offsets (K x RP_BINS + 1), touched keys
+    DevBuf pl_T;                         // one chunk's records per bin (k_chunk_segments -> k_seg_scan)
+    unsigned test_slab_cap = 0;          // MOBHEAT_TEST_SLAB_CAP: slabs of at most this many records (tests: overflow)
 };
 
 static std::string g_create_err;
@@ -605,9 +620,11 @@ struct Segs {
     SegBounds bounds{};   // where the segments may lie (checked by the MOBHEAT_BOUNDS_CHECK build only)
 };
 // merge the partitioned records (ctx->parts_sorted, or src) of n_rows staging rows
+// (O / cnt: the bins' row offsets and their touched-key counts; default rp_O and bin_cnt -- a pipelined batch's chunk k
+// passes its own slices of pl_O / pl_cnt)
 template <typename Rec>
 static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t slab = 0, const Rec *src = nullptr,
-                        const Segs &seg = Segs()) {
+                        const Segs &seg = Segs(), const unsigned long long *O = nullptr, unsigned *cnt = nullptr) {
     constexpr bool rehash = std::is_same<Rec, GrowRec>::value;
     int rc;
     if ((rc = ensure(ctx, ctx->bin_cnt, RP_BINS * 4)) || (rc = ensure(ctx, ctx->bin_off, RP_BINS * 8)))
@@ -646,9 +663,9 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t sla
     auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(grid), dim3(MO_THREADS), tag_bytes, ctx->stream, src ? src : (const Rec *)ctx->parts_sorted.p, slab,
                            seg.SO, seg.SP, seg.nseg,
-                           (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
+                           O ? O : (const unsigned long long *)ctx->rp_O.p, ntiles, RP_BINS, ctx->d_gmap, (const GenDesc *)ctx->d_glist,
                            ctx->n_glist, (const WInfo *)ctx->d_winfo, cell_hi_of(ctx->cfg.h3_res), seq32(ctx), staged_rows(ctx),
-                           (unsigned *)ctx->bin_cnt.p, ctx->d_st, tag_bytes);
+                           cnt ? cnt : (unsigned *)ctx->bin_cnt.p, ctx->d_st, tag_bytes);
     };
     if constexpr (std::is_same<Rec, EventRec>::value) {
         if (seg.nseg > 0) {   // (the multi-GPU owner)

@@ -308,14 +308,16 @@ __global__ __launch_bounds__(IG_THREADS) HM_SNAP_ATTR void k_ingest(
 
 // exceptions of k_ingest's fast path: upstream's exact sequence; the cell bits go into the row's key (k_ingest
 // wrote its window slot); with slabs (k_ingest<true>) the row's EventRec into its bin as k_ingest does
+// (n_slow_begin: the first exception to complete -- a pipelined batch completes each chunk's own, k_pipe_snap; null: 0)
 __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__ lat, const double *__restrict__ lon, int res,
                                                       const unsigned int *__restrict__ slow, const unsigned long long *n_slow,
                                                       uint64_t *__restrict__ keys, const double *__restrict__ speed,
                                                       const uint8_t *__restrict__ speed_valid, const unsigned long long *wreg,
                                                       unsigned *__restrict__ bin_cur, EventRec *__restrict__ slabs, unsigned slab_cap,
-                                                      DevStats *st, unsigned sub_bits) {
-    const int64_t m = (int64_t)*n_slow;
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (int64_t)gridDim.x * blockDim.x) {
+                                                      DevStats *st, unsigned sub_bits,
+                                                      const unsigned long long *n_slow_begin = nullptr) {
+    const int64_t m = (int64_t)*n_slow, q0 = n_slow_begin ? (int64_t)*n_slow_begin : 0;
+    for (int64_t q = q0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (int64_t)gridDim.x * blockDim.x) {
         const unsigned i = slow[q];
         const uint64_t cell = latLngToCellDeg(lat[i], lon[i], res, c_tab);
         const uint64_t key = keys[i] | (cell & CELL_LO);
@@ -342,20 +344,25 @@ __global__ __launch_bounds__(256) void k_ingest_exact(const double *__restrict__
 // multiplicity among them -> DevStats.sample_max_run.  A key holding a few % of the rows would put that share of the
 // batch through one merge workgroup (one bin) on the direct path; table mode aggregates it in LDS first.
 // (the multiplicities counted in an LDS hash table at load <= 1/2: was a bitonic sort of the sample, 78 barriers)
-__global__ __launch_bounds__(HS_THREADS) void k_sample_heavy(const uint64_t *__restrict__ keys, int64_t n, DevStats *st) {
+// stride: the rows k_ingest<true> wrote keys for (multiples of it; hs_stride of the whole batch), n: the rows sampled
+// ([0, n): the batch, or a pipelined batch's first chunk -- fewer than HS_SAMPLE multiples of the stride then, and the
+// largest multiplicity is scaled to HS_SAMPLE samples)
+__global__ __launch_bounds__(HS_THREADS) void k_sample_heavy(const uint64_t *__restrict__ keys, int64_t n, int64_t stride,
+                                                             DevStats *st) {
     __shared__ unsigned long long k[HS_SLOTS];
     __shared__ unsigned c[HS_SLOTS];
     __shared__ unsigned best;
     const int t = threadIdx.x;
-    const int64_t stride = hs_stride(n);
+    const int64_t ns = n / stride < HS_SAMPLE ? (n / stride > 0 ? n / stride : 1) : HS_SAMPLE;
     constexpr int PER = HS_SAMPLE / HS_THREADS;
     uint64_t v[PER];
 #pragma unroll
     for (int u = 0; u < PER; u++) {   // every load in flight before the table is cleared
-        // (spread over the whole batch -- sample q at q n / HS_SAMPLE, rounded down to the stride k_ingest<true> writes
-        // keys at: the stride alone covered only the first HS_SAMPLE x stride rows, as little as half the batch, and a
-        // hot key late in a time-ordered batch went unseen -- ADVICE r5)
-        const int64_t i = ((int64_t)(t + u * HS_THREADS) * n / HS_SAMPLE) & ~(stride - 1);
+        // (spread over the rows -- sample q at q n / ns, rounded down to the stride k_ingest<true> writes keys at (ns <=
+        // n / stride: distinct rows): the stride alone covered only the first HS_SAMPLE x stride rows, as little as half
+        // the batch, and a hot key late in a time-ordered batch went unseen -- ADVICE r5)
+        const int64_t q = t + u * HS_THREADS;
+        const int64_t i = q < ns ? (q * n / ns) & ~(stride - 1) : n;
         v[u] = i < n ? keys[i] : 0;
     }
     for (int q = t; q < HS_SLOTS; q += HS_THREADS) { k[q] = 0; c[q] = 0; }
@@ -376,7 +383,7 @@ __global__ __launch_bounds__(HS_THREADS) void k_sample_heavy(const uint64_t *__r
     for (int q = t; q < HS_SLOTS; q += HS_THREADS) m = c[q] > m ? c[q] : m;
     atomicMax(&best, m);
     __syncthreads();
-    if (t == 0) st->sample_max_run = best;
+    if (t == 0) st->sample_max_run = ns < HS_SAMPLE ? ((unsigned long long)best * HS_SAMPLE + ns - 1) / ns : best;
 }
 
 // the read side's cellToBoundary (row f4; h3_boundary.h): up to 10 vertices per cell, lat/lng degrees

@@ -63,8 +63,9 @@ __global__ __launch_bounds__(256) void k_dump_gen(GenDesc g, GrowRec *__restrict
 //    the tag byte of a created slot is stored to HBM.
 // The update-mode output row of a key (cumulative count/avg, heatmap_stream.py:124-132,243) is written at its
 // first touch in the batch to row b0 + k of the bin's segment (b0 = the bin's first partial, k = touch order
-// in the bin; the slot's `touched` word keeps (batch seq, k)), and rewritten in place when a later chunk
-// updates the key again; k_fill_gaps closes the gaps left by keys that had several partials.
+// in the bin; the slot's `touched` word keeps (batch seq, b0 + k)), and rewritten in place when a later chunk -- of
+// this launch, or a later merge of the same batch -- updates the key again; k_fill_gaps closes the gaps left by keys
+// that had several partials.
 // rehash != 0: growth (k_dump_gen records, unique keys, into the window's new table): created slots keep the
 // record's touched word, no rows are written.
 // =====================================================================================================
@@ -693,7 +694,9 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             MLine v{};
             const bool retouch = !rehash && gslot && !created && (unsigned)(o.touched >> 32) == seq;
             const bool first = !rehash && gslot && !retouch;
-            unsigned krow = touch_rows(first);
+            // (the row index is absolute -- the bin's first row b0 + its touch order -- so that a later merge of the same
+            // batch, whose segment of the bin starts elsewhere, rewrites the row in place: a pipelined batch's chunks)
+            unsigned krow = (unsigned)b0 + touch_rows(first);
             if (!first) krow = (unsigned)o.touched;
             if (gslot) v = line_of(p, o, first, krow);
             // 4. this chunk's stores: the state line (whole) and the key's row
@@ -732,7 +735,7 @@ __global__ __launch_bounds__(MO_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             }
             if (gslot) {
                 if (created) created_cnt++;
-                if (!rehash) put_row(rows, b0 + krow, p.cell, p.we, v.count, v.nspeed, v.sspeed, v.slat, v.slon);
+                if (!rehash) put_row(rows, (int64_t)krow, p.cell, p.we, v.count, v.nspeed, v.sspeed, v.slat, v.slon);
             }
             // created keys of non-resident windows count for their window here (resident ones: res_new); rehash:
             // the host already carries the moved keys

@@ -246,6 +246,67 @@ __global__ __launch_bounds__(256) void k_sub_segments(const unsigned *__restrict
         T[k] = acc;
     }
 }
+// ---- a pipelined batch (host_pipe.h): chunk k's records are the part of every bin slab written since chunk k - 1 ----
+// after chunk k's k_ingest<true> (+ its exceptions): the bin cursors (nbins + 1 words) into this chunk's snapshot, and
+// the exception count, so that the next chunk's k_ingest_exact starts after this chunk's exceptions
+__global__ __launch_bounds__(256) void k_pipe_snap(const unsigned *__restrict__ cur, int n, unsigned *__restrict__ snap,
+                                                   const unsigned long long *__restrict__ slow_word, unsigned long long *slow_snap) {
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) snap[q] = cur[q];
+    if (slow_snap && blockIdx.x == 0 && threadIdx.x == 0) *slow_snap = *slow_word;
+}
+// chunk k's segments of bin b (k_merge_owned's kSeg variant): for each of the bin's 2^sub_bits (sub-)slabs, the records
+// between the previous chunk's cursor and this chunk's -- SO the first one's address, SP the bin's records in earlier
+// segments, T[b] the bin's records of this chunk (scan input; T[RP_BINS] = 0).  A cursor past the slab (overflow: the
+// host re-partitions) is clamped, so no segment reads past its slab.
+__global__ __launch_bounds__(256) void k_chunk_segments(const unsigned *__restrict__ prev, const unsigned *__restrict__ cur,
+                                                        const EventRec *slabs, int64_t slab_cap, unsigned sub_bits,
+                                                        unsigned long long *__restrict__ SO, unsigned *__restrict__ SP,
+                                                        unsigned *__restrict__ T) {
+    const int ns = 1 << sub_bits;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k <= RP_BINS; k += gridDim.x * blockDim.x) {
+        if (k == RP_BINS) { T[k] = 0; continue; }
+        unsigned acc = 0;
+        for (int s = 0; s < ns; s++) {
+            const int64_t q = (int64_t)k * ns + s;
+            const unsigned lo = prev ? min(prev[q], (unsigned)slab_cap) : 0u, hi = min(cur[q], (unsigned)slab_cap);
+            SO[q] = (unsigned long long)(uintptr_t)(slabs + q * slab_cap + lo);
+            SP[q] = acc;
+            acc += hi > lo ? hi - lo : 0u;
+        }
+        T[k] = acc;
+    }
+}
+// exclusive scan of m u32 counts after a base: out[i] = out[0] (as found) + sum(c[0, i)) -- chunk k's row offsets
+// continue where chunk k - 1's ended (its scan's last word is this one's out[0]); one workgroup
+__global__ __launch_bounds__(1024) void k_seg_scan(const unsigned *__restrict__ c, int64_t m, unsigned long long *out) {
+    __shared__ unsigned long long base;
+    if (threadIdx.x == 0) base = out[0];
+    __syncthreads();
+    unsigned long long carry = base;
+    for (int64_t t0 = 0; t0 < m; t0 += 4096) {
+        const int64_t b = t0 + (int64_t)threadIdx.x * 4;
+        unsigned v[4];
+        unsigned long long sum = 0;
+        for (int q = 0; q < 4; q++) { v[q] = b + q < m ? c[b + q] : 0u; sum += v[q]; }
+        unsigned long long total;
+        unsigned long long run = carry + block1024_exclusive(sum, &total);
+        for (int q = 0; q < 4; q++)
+            if (b + q < m) { out[b + q] = run; run += v[q]; }
+        carry += total;
+        __syncthreads();
+    }
+}
+// the fallback of a pipelined batch whose slab overflowed in chunk k (host_pipe.h): the rest of the batch partitioned
+// by ev_partition (rp_O, digit-major over ntiles) -- its rows moved to start at base = out[0] (ev_partition's offsets
+// start at 0), and the bins' starts gathered into the chunk's flat segment offsets out[0, RP_BINS] (ntiles 1)
+__global__ __launch_bounds__(256) void k_seg_rebase(unsigned long long *__restrict__ rpO, int64_t m, int64_t ntiles,
+                                                    unsigned long long *out) {
+    const unsigned long long base = out[0];   // (read before any write: every thread writes out[b] = base + ..., out[0] = base)
+    __syncthreads();
+    for (int64_t q = threadIdx.x; q < m; q += blockDim.x) rpO[q] += base;
+    __syncthreads();
+    for (int b = threadIdx.x; b <= RP_BINS; b += blockDim.x) out[b] = rpO[(int64_t)b * ntiles];
+}
 // the chunks' counts as one u32 array per sender (scan input: [s][0, bins])
 __global__ __launch_bounds__(256) void k_stage_counts(const uint8_t *__restrict__ recv, const int64_t *__restrict__ chunk_off,
                                                       int nseg, unsigned bins, unsigned *__restrict__ C) {

@@ -79,6 +79,7 @@ static hipError_t upload_tables() {
 #include "k_stage.h"
 #include "host_ctx.h"
 #include "host_batch.h"
+#include "host_pipe.h"
 
 extern "C" {
 

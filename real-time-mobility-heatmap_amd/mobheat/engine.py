@@ -365,10 +365,11 @@ class HeatmapEngine:
                 "allocs_frees": int(ms[13])}
 
     def last_counts(self):
-        c = (ctypes.c_int64 * 10)()
-        check(self._lib.hm_last_counts(self._ctx, c, 10), self._ctx)
+        c = (ctypes.c_int64 * 11)()
+        check(self._lib.hm_last_counts(self._ctx, c, 11), self._ctx)
         return {"state_new": c[0], "partials": c[1], "tiles": c[2], "table_mode": bool(c[3]), "evicted": c[4],
-                "sent": c[5], "allocs": c[6], "frees": c[7], "binned": bool(c[8]), "self_held": c[9]}
+                "sent": c[5], "allocs": c[6], "frees": c[7], "binned": bool(c[8]), "self_held": c[9],
+                "pipe_chunks": c[10]}
 
     def _result_from_host(self, out, copy=True):
         def arr(p, n, dt):
