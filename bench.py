@@ -99,7 +99,8 @@ STAGES = ["ingest", "aggregate", "send", "partition", "merge", "emit", "dedup"]
 CONCURRENT_STAGES = ("dedup",)   # side stream (hm_process_batch): its kernel_ms is the side-stream span
 # HBM traffic per dispatch of every kernel and k_ingest's VALU instruction mix per event of this workload, counted by
 # rocprofv3 PMC passes of this same command (tools/ingest_pmc.py + tools/pmc_calib.py -> profiles/r5/kernel_pmc.json).
-PMC_FILE = os.path.join(ROOT, "profiles", "r5", "kernel_pmc.json")
+PMC_FILE = next((f for f in (os.path.join(ROOT, "profiles", r, "kernel_pmc.json") for r in ("r6", "r5")) if os.path.exists(f)),
+                os.path.join(ROOT, "profiles", "r6", "kernel_pmc.json"))
 STAGE_KERNELS = {"ingest": ["k_ingest"], "aggregate": ["k_agg", "k_bin_reduce"], "send": ["k_stage_pack"],
                  "partition": ["k_ev_hist", "k_ev_scatter_rec"], "merge": ["k_merge_owned"], "emit": ["k_fill_gaps"],
                  "dedup": ["k_dedup_flag"]}
