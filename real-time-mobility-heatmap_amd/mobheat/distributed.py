@@ -45,16 +45,43 @@ class PeerFailed(RuntimeError):
     batch leaves it; the caller resets or replays)."""
 
 
+# The batch's host metadata -- the summaries, the chunk sizes, the winner counts: host integers on every side -- moves
+# over a gloo group of the same ranks when the payloads go over RCCL (VERDICT r5 item 6): a collective of host tensors
+# needs no device round trip, where an RCCL one queued on torch's stream was followed by a .cpu() that waited for that
+# stream (and for everything queued on it before) three times per batch.  MOBHEAT_META_BACKEND=same keeps them on the
+# payloads' group; "gloo" forces a separate gloo group even under a gloo default (tests).
+META_BACKEND = os.environ.get("MOBHEAT_META_BACKEND", "auto")
+_META = {}
+
+
+def meta_group():
+    """(group, device) for the host metadata: a gloo group and the CPU when the default group is RCCL (or
+    META_BACKEND is "gloo"), else (None, None) -- the default group on the caller's device.  Created at the first
+    batch: every rank reaches it in the same order (ShardedHeatmap.process_batch, or the device-column scatter)."""
+    want = META_BACKEND == "gloo" or (META_BACKEND == "auto" and dist.get_backend() != "gloo")
+    if not want:
+        return None, None
+    if _META.get("world") is not dist.group.WORLD:   # (a new default group: a new metadata group with it)
+        _META.update(world=dist.group.WORLD, group=dist.new_group(backend="gloo"))
+    return _META["group"], torch.device("cpu")
+
+
+def _meta_all_gather(t):
+    """all_gather of a small int64 host-metadata tensor -> [world, ...] numpy (over meta_group when there is one)"""
+    g, d = meta_group()
+    x = t if g is None else t.to(d)
+    out = [torch.empty_like(x) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, x, group=g)
+    return torch.stack(out).cpu().numpy()
+
+
 def all_gather_summaries(summary, device, status=0):
     """all_gather of every rank's int64[HM_STAGE_SUMMARY_WORDS] summary -> host array [world, words]; `status` != 0
     (this rank's ingest failed) makes every rank raise PeerFailed after the collective."""
-    world = dist.get_world_size()
     summary = np.array(summary, dtype=np.int64)
     summary[SW_STATUS] = status
-    t = torch.from_numpy(summary).to(device)
-    out = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(out, t)
-    S = torch.stack(out).cpu().numpy()
+    g, _ = meta_group()
+    S = _meta_all_gather(torch.from_numpy(summary) if g is not None else torch.from_numpy(summary).to(device))
     if status == 0 and (S[:, SW_STATUS] != 0).any():
         raise PeerFailed(f"rank(s) {np.nonzero(S[:, SW_STATUS])[0].tolist()} failed the batch's ingest")
     return S
@@ -73,9 +100,10 @@ def exchange(streams, device, status=0):
     assert k <= MAX_STREAMS
     big = [max([int(c) * (s.rec_bytes // 8) for c in s.counts] + [0]) for s in streams] + [0] * (MAX_STREAMS - k)
     cnt = [[(streams[j].counts[r] if j < k else 0) for j in range(MAX_STREAMS)] + [status] + big for r in range(world)]
-    sc = torch.tensor(cnt, dtype=torch.int64, device=device)
+    g, md = meta_group()
+    sc = torch.tensor(cnt, dtype=torch.int64, device=md if g is not None else device)
     rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc)
+    dist.all_to_all_single(rc, sc, group=g)
     rcounts = rc.cpu().tolist()
     bad = [r for r in range(world) if rcounts[r][MAX_STREAMS]]
     if bad and status == 0:
@@ -147,11 +175,10 @@ def exchange_chunks(buf, send_bytes, device, status=0):
     fits), every piece received at its place -- as 8-byte words (chunk sizes are multiples of 32).  Returns (recv
     uint8 tensor, recv_bytes per source rank)."""
     world, rank = dist.get_world_size(), dist.get_rank()
+    g, _ = meta_group()
     row = torch.tensor([int(send_bytes[r]) if send_bytes else 0 for r in range(world)] + [status], dtype=torch.int64,
-                       device=device)
-    rows = [torch.empty_like(row) for _ in range(world)]
-    dist.all_gather(rows, row)
-    M = torch.stack(rows).cpu().tolist()   # M[s][r]: bytes s sends r; M[s][world]: s's status
+                       device="cpu" if g is not None else device)
+    M = _meta_all_gather(row).tolist()   # M[s][r]: bytes s sends r; M[s][world]: s's status
     bad = [r for r in range(world) if M[r][world]]
     if bad and status == 0:
         raise PeerFailed(f"rank(s) {bad} failed the batch's stage before the exchange")

@@ -173,13 +173,15 @@ class OracleStages:
         return out
 
 
-def _worker(rank, world, port, batches, res, table, q, round_bytes=None):
+def _worker(rank, world, port, batches, res, table, q, round_bytes=None, meta=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from mobheat import distributed
     from mobheat.distributed import ShardedHeatmap
     if round_bytes:   # (the payload exchanged in rounds of at most this many bytes per rank pair)
         distributed.EXCHANGE_ROUND_BYTES = round_bytes
+    if meta:   # (the host metadata over a group of its own, as under RCCL)
+        distributed.META_BACKEND = "gloo"
     sh = ShardedHeatmap(OracleStages(res, table=table), torch.device("cpu"))
     results = []
     for e, b in enumerate(batches):
@@ -202,8 +204,9 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("table,round_bytes", [(False, None), (True, None), (False, 4096)])
-def test_sharded_equals_single_shard(oracle_h3, table, round_bytes):
+@pytest.mark.parametrize("table,round_bytes,meta", [(False, None, False), (True, None, False), (False, 4096, False),
+                                                     (False, None, True)])
+def test_sharded_equals_single_shard(oracle_h3, table, round_bytes, meta):
     from mobheat import synth
     from oracle.spark_oracle import SparkHeatmapOracle
     rng = np.random.default_rng(5)
@@ -222,7 +225,8 @@ def test_sharded_equals_single_shard(oracle_h3, table, round_bytes):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, batches, 8, table, q, round_bytes)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, batches, 8, table, q, round_bytes, meta))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=300) for _ in range(world))
