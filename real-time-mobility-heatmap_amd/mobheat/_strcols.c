@@ -10,6 +10,13 @@
  * copy(ptrs, n, offsets, data, threads): the bytes of every row with lens >= 0 to data[offsets[i], offsets[i+1]).
  * floats(ptrs, n, values, kinds, threads): an object column of Python float / None (a nullable double column as pandas
  *   holds it): values[i] = the float, kinds[i] = 1 float, 0 None, 2 anything else (the caller converts those).
+ * measure(ptrs, n, offs, threads) -> (bytes, nulls, others, [per-block bytes]): the fused form's first pass -- offs
+ *   = int64[n + 1], offs[i + 1] = the byte length of row i (-1 None, -2 anything else); the rows split into blocks of
+ *   whole bytes of the validity bitmap (multiples of 64 rows), one per thread.
+ * fill(ptrs, n, offs, data, bitmap, block_bytes, threads): its second pass over the same blocks -- offs becomes the
+ *   exclusive offsets (offs[0] = 0, a null row adds 0), every compact-ASCII row's bytes are copied to data, and the
+ *   validity bitmap (Arrow: LSB first; bitmap may be 0) written: two threaded passes instead of lengths, a numpy
+ *   cumsum, copy and packbits (only when others == 0: the caller converts such a column another way).
  * The object array must stay alive (it holds the references) and unchanged during both calls. */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
@@ -122,7 +129,129 @@ static PyObject *py_floats(PyObject *self, PyObject *args) {
     Py_RETURN_NONE;
 }
 
+/* blocks of whole 64-row groups (so that no two threads share a byte of the bitmap): block t = [lo(t), lo(t + 1)) */
+static int64_t block_lo(int64_t n, int t, int threads) {
+    const int64_t g = (n + 63) / 64;
+    const int64_t lo = g * t / threads * 64;
+    return lo < n ? lo : n;
+}
+typedef struct {
+    PyObject *const *obj;
+    int64_t lo, hi;
+    int64_t *offs;
+    uint8_t *data, *bitmap;
+    int64_t base, bytes, nulls, others;
+} Blk;
+static void *measure_job(void *p) {
+    Blk *b = (Blk *)p;
+    int64_t bytes = 0, nulls = 0, others = 0;
+    for (int64_t i = b->lo; i < b->hi; i++) {
+        PyObject *o = b->obj[i];
+        int64_t l;
+        if (o == Py_None) { l = -1; nulls++; }
+        else if (is_ascii_str(o)) { l = (int64_t)PyUnicode_GET_LENGTH(o); bytes += l; }
+        else { l = -2; others++; }
+        b->offs[i + 1] = l;
+    }
+    b->bytes = bytes;
+    b->nulls = nulls;
+    b->others = others;
+    return NULL;
+}
+static void *fill_job(void *p) {
+    Blk *b = (Blk *)p;
+    int64_t run = b->base;
+    for (int64_t i = b->lo; i < b->hi; i++) {
+        const int64_t l = b->offs[i + 1];
+        if (l > 0) memcpy(b->data + run, PyUnicode_DATA(b->obj[i]), (size_t)l);
+        if (l > 0) run += l;
+        b->offs[i + 1] = run;
+        if (b->bitmap) {
+            if ((i & 7) == 0) b->bitmap[i >> 3] = 0;
+            if (l >= 0) b->bitmap[i >> 3] |= (uint8_t)(1u << (i & 7));
+        }
+    }
+    return NULL;
+}
+static void run_blocks(void *(*fn)(void *), Blk *blk, int threads) {
+    pthread_t th[64];
+    int started[64] = {0};
+    for (int t = 1; t < threads; t++) {
+        started[t] = pthread_create(&th[t], NULL, fn, &blk[t]) == 0;
+        if (!started[t]) fn(&blk[t]);
+    }
+    fn(&blk[0]);
+    for (int t = 1; t < threads; t++)
+        if (started[t]) pthread_join(th[t], NULL);
+}
+static int clamp_threads(int threads, int64_t n) {
+    if (threads < 1) threads = 1;
+    if (threads > 64) threads = 64;
+    if (n < 65536) threads = 1;
+    return threads;
+}
+static PyObject *py_measure(PyObject *self, PyObject *args) {
+    unsigned long long ptrs, offs;
+    long long n;
+    int threads;
+    if (!PyArg_ParseTuple(args, "KLKi", &ptrs, &n, &offs, &threads)) return NULL;
+    threads = clamp_threads(threads, n);
+    Blk blk[64];
+    for (int t = 0; t < threads; t++) {
+        memset(&blk[t], 0, sizeof blk[t]);
+        blk[t].obj = (PyObject *const *)(uintptr_t)ptrs;
+        blk[t].offs = (int64_t *)(uintptr_t)offs;
+        blk[t].lo = block_lo(n, t, threads);
+        blk[t].hi = block_lo(n, t + 1, threads);
+    }
+    Py_BEGIN_ALLOW_THREADS
+    run_blocks(measure_job, blk, threads);
+    Py_END_ALLOW_THREADS
+    long long bytes = 0, nulls = 0, others = 0;
+    PyObject *per = PyList_New(threads);
+    if (!per) return NULL;
+    for (int t = 0; t < threads; t++) {
+        bytes += blk[t].bytes;
+        nulls += blk[t].nulls;
+        others += blk[t].others;
+        PyList_SET_ITEM(per, t, PyLong_FromLongLong(blk[t].bytes));
+    }
+    return Py_BuildValue("LLLN", bytes, nulls, others, per);
+}
+static PyObject *py_fill(PyObject *self, PyObject *args) {
+    unsigned long long ptrs, offs, data, bitmap;
+    long long n;
+    PyObject *per;
+    int threads;
+    if (!PyArg_ParseTuple(args, "KLKKKOi", &ptrs, &n, &offs, &data, &bitmap, &per, &threads)) return NULL;
+    threads = clamp_threads(threads, n);
+    if (!PyList_Check(per) || PyList_GET_SIZE(per) != threads) {
+        PyErr_SetString(PyExc_ValueError, "fill: block_bytes must be measure's list (same n and threads)");
+        return NULL;
+    }
+    Blk blk[64];
+    int64_t base = 0;
+    for (int t = 0; t < threads; t++) {
+        memset(&blk[t], 0, sizeof blk[t]);
+        blk[t].obj = (PyObject *const *)(uintptr_t)ptrs;
+        blk[t].offs = (int64_t *)(uintptr_t)offs;
+        blk[t].data = (uint8_t *)(uintptr_t)data;
+        blk[t].bitmap = (uint8_t *)(uintptr_t)bitmap;
+        blk[t].lo = block_lo(n, t, threads);
+        blk[t].hi = block_lo(n, t + 1, threads);
+        blk[t].base = base;
+        base += PyLong_AsLongLong(PyList_GET_ITEM(per, t));
+    }
+    ((int64_t *)(uintptr_t)offs)[0] = 0;
+    Py_BEGIN_ALLOW_THREADS
+    run_blocks(fill_job, blk, threads);
+    Py_END_ALLOW_THREADS
+    Py_RETURN_NONE;
+}
+
 static PyMethodDef methods[] = {
+    {"measure", py_measure, METH_VARARGS, "fused pass 1: lengths into offs[1..n], totals and per-block bytes"},
+    {"fill", py_fill, METH_VARARGS, "fused pass 2: exclusive offsets, the bytes and the validity bitmap"},
     {"floats", py_floats, METH_VARARGS, "values of float objects (kinds: 1 float, 0 None, 2 other)"},
     {"lengths", py_lengths, METH_VARARGS, "byte lengths of compact-ASCII str objects (-1 None, -2 other)"},
     {"copy", py_copy, METH_VARARGS, "copy the compact-ASCII strings' bytes to their offsets"},

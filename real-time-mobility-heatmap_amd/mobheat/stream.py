@@ -265,14 +265,18 @@ SINK_FACTORY = MongoSink   # tests replace this with an in-memory capture sink
 
 
 # ------------------ batch columns ------------------
-def _pandas_to_arrow(pdf):
+def _pandas_to_arrow(pdf, pre=None):
     import pandas as pd
     """A pandas frame as Arrow WITHOUT pandas' NaN -> null mapping on float columns: a NaN speedKmh (Spark's JSON reader
     accepts NaN tokens, SURVEY App. A.2) must stay NaN so that avg(speedKmh) is NaN (App. A.4), while a missing value
-    (None in an object column, pd.NA in a nullable column) is null."""
+    (None in an object column, pd.NA in a nullable column) is null.  pre: columns already converted (device_columns'
+    _strcols arrays), taken as they are, in the frame's column order -- no copy of the frame without them."""
     import pyarrow as pa
     cols = {}
     for name in pdf.columns:
+        if pre and name in pre:
+            cols[str(name)] = pre[name]
+            continue
         c = pdf[name]
         if isinstance(c.dtype, pd.api.extensions.ExtensionDtype) and hasattr(c.array, "__arrow_array__"):
             # nullable extension arrays (Float64, Int64, string, ...): their mask is the null set -- pd.NA -> null, a
@@ -457,7 +461,8 @@ class ArrowColumns:
         if name not in t.column_names:
             return None
         c = t.column(name)
-        c = c.combine_chunks() if isinstance(c, pa.ChunkedArray) else c
+        if isinstance(c, pa.ChunkedArray):   # (one chunk -- a converted pandas frame's: taken as it is, no copy)
+            c = c.chunk(0) if c.num_chunks == 1 else c.combine_chunks()
         if pa.types.is_dictionary(c.type):
             c = c.dictionary_decode()
         return None if pa.types.is_null(c.type) or c.null_count == len(c) else c
@@ -519,9 +524,22 @@ def _object_strings(values):
     a = np.ascontiguousarray(values, dtype=object)
     n = a.size
     threads = min(16, os.cpu_count() or 1)
-    lens = np.empty(n, np.int64)
-    if n:
-        _strcols.lengths(a.ctypes.data, n, lens.ctypes.data, threads)
+    if n and hasattr(_strcols, "measure"):
+        # the fused form: lengths + per-block totals, then offsets, bytes and validity bitmap in one threaded pass
+        offs = np.empty(n + 1, np.int64)
+        total, nulls, others, per = _strcols.measure(a.ctypes.data, n, offs.ctypes.data, threads)
+        if not others:
+            data = np.empty(max(total, 1), np.uint8)
+            bitmap = np.empty((n + 7) // 8, np.uint8) if nulls else None
+            _strcols.fill(a.ctypes.data, n, offs.ctypes.data, data.ctypes.data,
+                          0 if bitmap is None else bitmap.ctypes.data, per, threads)
+            return pa.Array.from_buffers(pa.large_string(), n, [None if bitmap is None else pa.py_buffer(bitmap),
+                                         pa.py_buffer(offs), pa.py_buffer(data)], null_count=nulls)
+        lens = offs[1:].copy()
+    else:
+        lens = np.empty(n, np.int64)
+        if n:
+            _strcols.lengths(a.ctypes.data, n, lens.ctypes.data, threads)
     enc = {}
     for i in np.nonzero(lens == -2)[0].tolist():
         v = a[i]
@@ -566,8 +584,10 @@ def _object_floats(values):
             vals[i], kinds[i] = float(v), 1
         else:
             return None
-    valid = kinds == 1
-    return pa.array(vals, mask=~valid) if not valid.all() else pa.array(vals)
+    # kinds is 0 / 1 now: packed straight into Arrow's validity bitmap, the values buffer taken as it is
+    nulls = n - int(np.count_nonzero(kinds))
+    bitmap = pa.py_buffer(np.packbits(kinds, bitorder="little")) if nulls else None
+    return pa.Array.from_buffers(pa.float64(), n, [bitmap, pa.py_buffer(vals)], null_count=nulls)
 
 
 def device_columns(df):
@@ -588,14 +608,10 @@ def device_columns(df):
                     arr = None
                 if arr is not None:
                     strs[c] = arr
-        if strs:
-            df = df.drop(columns=list(strs))
     try:
-        t = _to_arrow(df)
+        t = _pandas_to_arrow(df, strs) if strs else _to_arrow(df)
     except Exception:
         return batch_columns(df)
-    for c, arr in strs.items():
-        t = t.append_column(c, arr) if t.num_columns else __import__("pyarrow").table({c: arr})
     if "value" in t.column_names:
         return {"kafka": kafka_values(t), "n": t.num_rows}
     import pyarrow as pa

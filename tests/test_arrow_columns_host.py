@@ -135,6 +135,24 @@ def test_object_strings_to_arrow():
     assert len(stream._object_strings(np.array([], dtype=object))) == 0
 
 
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 65536 + 37, 300_001])
+def test_object_strings_fused_pass(n):
+    """The fused _strcols.measure/fill form (compact-ASCII str and None only): offsets, bytes and the validity bitmap
+    written per block of whole 64-row groups by up to 16 threads -- equal to pyarrow's conversion at block edges, with
+    and without nulls."""
+    rng = np.random.default_rng(n)
+    words = np.array(["", "a", "v00017", "mbta", "x" * 70], dtype=object)
+    vals = words[rng.integers(0, words.size, n)]
+    for nulls in (False, True):
+        v = vals.copy()
+        if nulls:
+            v[rng.random(n) < 0.3] = None
+            v[-1] = None
+        got = stream._object_strings(v)
+        assert got.equals(pa.array(list(v), pa.large_string())), (n, nulls)
+        assert got.null_count == sum(x is None for x in v)
+
+
 def test_object_floats_to_arrow():
     """_strcols.floats + the host's handling of the rest: float objects as values (NaN stays a value), None / pd.NA
     null, ints converted, a non-number -> None"""
