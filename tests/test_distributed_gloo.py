@@ -204,9 +204,12 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("table,round_bytes,meta", [(False, None, False), (True, None, False), (False, 4096, False),
-                                                     (False, None, True)])
-def test_sharded_equals_single_shard(oracle_h3, table, round_bytes, meta):
+@pytest.mark.parametrize("table,round_bytes,meta,world", [(False, None, False, 2), (True, None, False, 2),
+                                                           (False, 4096, False, 2), (False, None, True, 2),
+                                                           (False, 4096, False, 3), (True, None, True, 3)])
+def test_sharded_equals_single_shard(oracle_h3, table, round_bytes, meta, world):
+    """world 2 and 3 over gloo, the payload exchanged in one call or in rounds of 4 KiB per rank pair (the chunked
+    exchange), the host metadata over the same group or a separate one: the union of the shards equals one engine."""
     from mobheat import synth
     from oracle.spark_oracle import SparkHeatmapOracle
     rng = np.random.default_rng(5)
@@ -221,7 +224,6 @@ def test_sharded_equals_single_shard(oracle_h3, table, round_bytes, meta):
         b["speed_valid"] = b["speed_valid"].astype(bool)
         b["row_valid"] = b["row_valid"].astype(bool)
         batches.append(b)
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -248,7 +250,7 @@ def test_sharded_equals_single_shard(oracle_h3, table, round_bytes, meta):
             assert (sp is None) == (o[k]["avg_speed"] is None)
             assert sp is None or abs(sp - o[k]["avg_speed"]) <= 1e-9 * abs(sp)
             assert abs(lat - o[k]["avg_lat"]) <= 1e-9 * abs(lat)
-        latest = sorted(got[0][e][1] + got[1][e][1])
+        latest = sorted(x for r in range(world) for x in got[r][e][1])
         assert latest == exp["latest_rows"].tolist()
 
 
