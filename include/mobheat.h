@@ -262,6 +262,15 @@ int hm_state_export(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs, int64_
  * state after that batch = the last-written record of every key of an older full export followed by the deltas of the
  * batches since, keeping keys whose window end > info->prev_watermark_ms * 1000. */
 int hm_state_export_touched(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs, int64_t cap, int64_t *n_out);
+/* The same exports in two halves, for a checkpoint file writer that overlaps the device-to-host copy with the
+ * statements' encode and the file write (the reference's state store write, heatmap_stream.py:37,244): _begin dumps the
+ * state -- every live key, or (touched_only) the last batch's touched keys -- into device memory and returns
+ * *n_out; _copy writes records [first, first + count) of that dump to host memory `recs` (page-locked memory: the
+ * copy runs at the link's rate).  _copy may run on another thread while hm_encode_tile_updates /
+ * hm_encode_position_updates run on this context (it uses a stream of its own), never beside hm_process_batch, a
+ * stage call or another export; a batch or another export in between makes it fail (HM_E_STATE). */
+int hm_state_export_begin(hm_ctx *ctx, hm_state_info *info, int32_t touched_only, int64_t *n_out);
+int hm_state_export_copy(hm_ctx *ctx, hm_state_rec *recs, int64_t first, int64_t count);
 /* Restores an exported state into a context that has processed no batch (HM_E_STATE otherwise); the
  * config fields of info must equal the context's (HM_E_INVALID). recs: info->n_keys distinct keys, host memory. */
 int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *recs);
@@ -390,7 +399,9 @@ typedef struct hm_arrow_col {
                                   no nulls */
     int64_t validity_offset;
     int32_t offset_bytes;      /* string columns: 4 (Arrow string) or 8 (large_string) */
-    int32_t reserved;
+    int32_t unit;              /* ts_us only: 0 = microseconds, 1 = nanoseconds (pandas' datetime64[ns], handed over as it
+                                  is: the device truncates toward zero to microseconds, as Arrow's unsafe cast does);
+                                  0 for every other column */
 } hm_arrow_col;
 typedef struct hm_arrow_in {
     int64_t n;

@@ -216,8 +216,11 @@ int hm_decode_json(hm_ctx *ctx, const hm_json_in *in, hm_json_out *out) {
 static int arrow_upload(hm_ctx *ctx, const hm_arrow_col &c, int64_t n, size_t elem, void *dst, DevBuf &bits, DevBuf &offs,
                         DevBuf &data, ArrowDevCol &d, bool is_string) {
     memset(&d, 0, sizeof(d));
+    if (c.unit != 0 && (is_string || elem != 8 || dst != ctx->jd_ts.p || c.unit != 1))
+        return set_err(ctx, HM_E_INVALID, "unit %d: only eventTs may be in nanoseconds (1)", c.unit);
     if (!c.values || n == 0) return HM_OK;
     d.present = 1;
+    d.ns = c.unit;
     if (c.validity) {
         if (c.validity_offset < 0) return set_err(ctx, HM_E_INVALID, "negative validity offset");
         const int64_t b0 = c.validity_offset >> 3, nb = ((c.validity_offset & 7) + n + 7) >> 3;

@@ -20,12 +20,12 @@ static void state_info_of(const hm_ctx *ctx, hm_state_info *info, int64_t n_keys
 // every live window's keys (only_seq != 0: those the batch with that sequence touched) into recs[0, n)
 static int state_dump(hm_ctx *ctx, hm_state_rec *recs, int64_t n, unsigned only_seq) {
     int rc;
-    ctx->touched_dump_seq = -1;   // (parts_regrow is overwritten)
+    ctx->touched_dump_seq = ctx->export_dump_n = -1;   // (parts_regrow is overwritten)
     if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(n, 1) * sizeof(GrowRec)))) return rc;
     HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
     for (const auto &g : ctx->gens) {
         const GenDesc d = gen_desc(g);
-        hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
+        hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256 * DUMP_PER)), dim3(256), 0, ctx->stream, d,
                            (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD, only_seq, true);
     }
     HIPCHK(ctx, hipGetLastError());
@@ -33,7 +33,7 @@ static int state_dump(hm_ctx *ctx, hm_state_rec *recs, int64_t n, unsigned only_
     HIPCHK(ctx, hipMemcpyAsync(&dumped, ctx->d_scratch + REGROW_WORD, 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     if ((int64_t)dumped != n) return set_err(ctx, HM_E_STATE, "state dump found %llu keys, expected %lld", dumped, (long long)n);
-    if (n > 0) HIPCHK(ctx, hipMemcpy(recs, ctx->parts_regrow.p, n * sizeof(GrowRec), hipMemcpyDeviceToHost));
+    if (n > 0 && recs) HIPCHK(ctx, hipMemcpy(recs, ctx->parts_regrow.p, n * sizeof(GrowRec), hipMemcpyDeviceToHost));
     return HM_OK;
 }
 
@@ -69,10 +69,11 @@ int hm_state_export_touched(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs
     } else if (ctx->seq > 0 && !ctx->gens.empty()) {
         int rc;
         if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(live, 1) * sizeof(GrowRec)))) return rc;
+        ctx->export_dump_n = -1;   // (parts_regrow is overwritten)
         HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
         for (const auto &g : ctx->gens) {
             const GenDesc d = gen_desc(g);
-            hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
+            hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256 * DUMP_PER)), dim3(256), 0, ctx->stream, d,
                                (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD, seq32(ctx), true);
         }
         HIPCHK(ctx, hipGetLastError());
@@ -87,6 +88,46 @@ int hm_state_export_touched(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs
     if (!recs) return HM_OK;
     if (cap < n) return set_err(ctx, HM_E_INVALID, "%lld touched keys do not fit %lld records", (long long)n, (long long)cap);
     if (n > 0) HIPCHK(ctx, hipMemcpy(recs, ctx->parts_regrow.p, n * sizeof(GrowRec), hipMemcpyDeviceToHost));
+    return HM_OK;
+}
+
+// The export in two halves, for a file writer that overlaps the copy with the statements' encode: begin dumps the
+// state (every live key, or the last batch's touched keys) into the device dump buffer and returns its size; copy
+// moves records [first, first + count) of that dump to host memory on copy_stream (idle between batches), so that it
+// can run on another thread while hm_encode_* run on this context's stream.
+int hm_state_export_begin(hm_ctx *ctx, hm_state_info *info, int32_t touched_only, int64_t *n_out) {
+    if (!ctx || !info || !n_out) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->stage != 0) return set_err(ctx, HM_E_STATE, "hm_state_export_begin between stage calls");
+    int rc;
+    int64_t n = 0;
+    if (touched_only) {
+        if ((rc = hm_state_export_touched(ctx, info, nullptr, 0, &n))) return rc;
+        if (n > 0 && ctx->touched_dump_seq != (int64_t)ctx->seq) return set_err(ctx, HM_E_STATE, "touched dump lost");
+    } else {
+        if ((rc = hm_state_export(ctx, info, nullptr, 0))) return rc;
+        n = info->n_keys;
+        if (n > 0) {
+            if ((rc = state_dump(ctx, nullptr, n, 0))) return rc;
+        }
+    }
+    ctx->export_dump_n = n;
+    ctx->export_dump_seq = ctx->seq;
+    *n_out = n;
+    return HM_OK;
+}
+
+int hm_state_export_copy(hm_ctx *ctx, hm_state_rec *recs, int64_t first, int64_t count) {
+    if (!ctx || first < 0 || count < 0 || (count > 0 && !recs)) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->export_dump_n < 0 || ctx->export_dump_seq != ctx->seq)
+        return set_err(ctx, HM_E_STATE, "hm_state_export_copy without an hm_state_export_begin after the last batch");
+    if (first + count > ctx->export_dump_n)
+        return set_err(ctx, HM_E_INVALID, "records [%lld, %lld) outside the dump of %lld", (long long)first,
+                       (long long)(first + count), (long long)ctx->export_dump_n);
+    if (count == 0) return HM_OK;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipMemcpyAsync(recs, (const GrowRec *)ctx->parts_regrow.p + first, (size_t)count * sizeof(GrowRec),
+                               hipMemcpyDeviceToHost, ctx->copy_stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->copy_stream));
     return HM_OK;
 }
 

@@ -74,6 +74,8 @@ struct hm_ctx {
     DevBuf parts_regrow;              // growth: the old tables' keys as partial records
     int64_t touched_dump_seq = -1;    // parts_regrow holds hm_state_export_touched's dump of batch seq (-1: none)
     int64_t touched_dump_n = 0;
+    int64_t export_dump_n = -1;       // hm_state_export_begin: records of the dump in parts_regrow (-1: none) ...
+    unsigned long long export_dump_seq = 0;   // ... made after batch seq (hm_state_export_copy checks both)
     DevBuf parts_regrow_sorted;       // growth: the same, partitioned (not parts_sorted: a binned batch's slabs are there)
     // multi-GPU exchange (api_stage.h): chunk starts and headers, the local -> global window slot map; the owner's
     // per-sender bin counts and their scan, its bins' segments, the received candidates and table-mode partials
@@ -803,9 +805,10 @@ static int gens_prepare(hm_ctx *ctx, const std::vector<WinCount> &census, bool r
         ctx->bin_offsets_ready = false;   // (the regrow's partition below writes rp_O)
         if ((rc = ensure(ctx, ctx->parts_regrow, std::max<int64_t>(moved, 1) * sizeof(GrowRec)))) return rc;
         HIPCHK(ctx, hipMemsetAsync(ctx->d_scratch + REGROW_WORD, 0, 8, ctx->stream));
+        ctx->touched_dump_seq = ctx->export_dump_n = -1;   // (parts_regrow is overwritten)
         for (const auto &g : old) {
             const GenDesc d = gen_desc(g);
-            hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256)), dim3(256), 0, ctx->stream, d,
+            hipLaunchKernelGGL(k_dump_gen, dim3(grid_for(int64_t(1) << g.log2cap, 256 * DUMP_PER)), dim3(256), 0, ctx->stream, d,
                                (GrowRec *)ctx->parts_regrow.p, ctx->d_scratch + REGROW_WORD);
         }
         HIPCHK(ctx, hipGetLastError());

@@ -214,6 +214,7 @@ struct ArrowDevCol {
     int32_t offset_bytes;
     int16_t present;          // 0: the column is absent (every row null)
     int16_t bit0;             // row 0's bit in valid[0]
+    int32_t ns;               // eventTs in nanoseconds: truncated toward zero to microseconds here (hm_arrow_col.unit)
 };
 __device__ __forceinline__ bool arrow_valid(const ArrowDevCol &c, int64_t i) {
     const int64_t j = i + c.bit0;
@@ -250,6 +251,7 @@ __global__ __launch_bounds__(256) void k_arrow_prep(int64_t n, ArrowDevCol lat_c
         if (!s) speed[i] = 0.0;
         const bool t = arrow_valid(ts_c, i);
         if (!t) ts[i] = 0;
+        else if (ts_c.ns) ts[i] = ts[i] / 1000;   // (C division: toward zero, as Arrow's unsafe ns -> us cast)
         const bool p = arrow_valid(pv_c, i), v = arrow_valid(vh_c, i);
         if (p) {
             const int64_t a = arrow_off(pv_c, i), b = arrow_off(pv_c, i + 1);

@@ -65,7 +65,7 @@ class HmJsonOut(ctypes.Structure):
 
 class HmArrowCol(ctypes.Structure):
     _fields_ = [("values", c_vp), ("data", c_vp), ("validity", c_vp), ("validity_offset", c_i64), ("offset_bytes", c_i32),
-                ("reserved", c_i32)]
+                ("unit", c_i32)]
 
 
 class HmArrowIn(ctypes.Structure):
@@ -127,6 +127,8 @@ SIGNATURES = {
     "hm_selftest_glibc_libm_device": (c_i32, [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32]),
     "hm_state_export": (c_i32, [c_vp, _P(HmStateInfo), c_vp, c_i64]),
     "hm_state_export_touched": (c_i32, [c_vp, _P(HmStateInfo), c_vp, c_i64, c_vp]),
+    "hm_state_export_begin": (c_i32, [c_vp, _P(HmStateInfo), c_i32, c_vp]),
+    "hm_state_export_copy": (c_i32, [c_vp, c_vp, c_i64, c_i64]),
     "hm_state_version": (c_i64, [c_vp]),
     "hm_state_import": (c_i32, [c_vp, _P(HmStateInfo), c_vp]),
     "hm_last_windows": (c_i32, [c_vp, c_vp, c_i64, _P(c_i64)]),

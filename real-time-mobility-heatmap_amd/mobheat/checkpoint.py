@@ -186,16 +186,20 @@ class StateCheckpoints:
             break
         # (the records: a view of the engine's page-locked export buffer, valid until its next export -- the caller
         # writes the file before the next batch: foreach_batch_func and the sharded writer wait for it)
-        if ch is None or len(ch) - 1 >= int(full_every):
-            info, recs = engine.export_state(reuse=True)
+        full = ch is None or len(ch) - 1 >= int(full_every)
+        if full:
             meta = {"lineage": lineage, "base": epoch, "prev": -1, "rank": self.rank, "world": self.world}
-            kind = "full"
         else:
-            info, recs = engine.export_state_delta(reuse=True)
             meta = {"lineage": lineage, "base": ch[0].epoch, "prev": ch[-1].epoch, "rank": self.rank,
                     "world": self.world}
-            kind = "delta"
-        return {"epoch": epoch, "kind": kind, "info": info, "recs": recs, "meta": meta}
+        job = {"epoch": epoch, "kind": "full" if full else "delta", "meta": meta, "fill": None, "raw": None}
+        if hasattr(engine, "export_begin"):
+            # only the dump here (~1 ms per 1e7 keys); the device-to-host copy runs in write(), slice by slice beside
+            # the file's writes -- and beside the statements' encode, which the caller starts meanwhile
+            job["info"], _, job["recs"], job["raw"], job["fill"] = engine.export_begin(touched_only=not full)
+        else:
+            job["info"], job["recs"] = engine.export_state(reuse=True) if full else engine.export_state_delta(reuse=True)
+        return job
 
     def write(self, job):
         """The file side of a prepared checkpoint: this rank's files of epochs >= its epoch deleted (an abandoned
@@ -207,7 +211,8 @@ class StateCheckpoints:
         for e in self.scan():
             if e.rank == self.rank and e.world == self.world and e.epoch >= epoch:
                 _remove(e.path)
-        save_state_file(self.path(job["kind"], epoch), job["info"], job["recs"], meta=json.dumps(job["meta"]))
+        save_state_file(self.path(job["kind"], epoch), job["info"], job["recs"], meta=json.dumps(job["meta"]),
+                        fill=job.get("fill"), raw=job.get("raw"))
         self._prune(job["meta"]["lineage"], epoch)
         return job["kind"]
 

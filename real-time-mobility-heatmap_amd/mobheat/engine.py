@@ -251,22 +251,45 @@ class HeatmapEngine:
         not touch the state)."""
         return int(self._lib.hm_state_version(self._ctx))
 
-    def _export_buffer(self, n, reuse):
+    def _export_buffer(self, n, reuse, raw_out=None):
         """n state records of host memory: a fresh array, or (reuse) a view of the engine's page-locked export buffer --
         valid until the next reuse export (a device-to-host copy into pageable memory ran at ~10 GB/s: 66 ms of a
-        1e7-key delta, profiles/r5)"""
+        1e7-key delta, profiles/r5).  The buffer is page-aligned and holds the records rounded up to 4 KiB (the
+        checkpoint writer's O_DIRECT writes); raw_out (a list) receives the whole buffer as uint8."""
         if not reuse:
             return np.zeros(n, STATE_REC_DTYPE)
         nbytes = max(n, 1) * STATE_REC_DTYPE.itemsize
+        need = -(-nbytes // 4096) * 4096
         buf = getattr(self, "_pinned", None)
-        if buf is None or buf[1] < nbytes:
+        if buf is None or buf[1] < need:
             self._free_pinned()
             p = ctypes.c_void_p()
-            cap = nbytes + nbytes // 4
+            cap = max(need, -(-(nbytes + nbytes // 4) // 4096) * 4096)
             check(self._lib.hm_host_alloc(cap, ctypes.byref(p)), None, "hm_host_alloc")
             buf = self._pinned = (p.value, cap)
         raw = np.ctypeslib.as_array(ctypes.cast(buf[0], ctypes.POINTER(ctypes.c_uint8)), shape=(buf[1],))
+        if raw_out is not None:
+            raw_out.append(raw)
         return raw[: n * STATE_REC_DTYPE.itemsize].view(STATE_REC_DTYPE)
+
+    def export_begin(self, touched_only):
+        """hm_state_export_begin: the state (or the last batch's touched keys) dumped on the device -> (info dict, n,
+        recs, raw, fill): recs a view of the page-locked export buffer (raw: all of it, uint8), filled by
+        fill(first, count) = hm_state_export_copy -- which may run on another thread while this engine encodes the
+        batch's statements (the checkpoint writer: mobheat.checkpoint)."""
+        info = HmStateInfo()
+        n = ctypes.c_int64()
+        check(self._lib.hm_state_export_begin(self._ctx, ctypes.byref(info), int(bool(touched_only)), ctypes.byref(n)),
+              self._ctx, "hm_state_export_begin")
+        raw = []
+        recs = self._export_buffer(int(n.value), True, raw)
+        base = raw[0].ctypes.data
+        size = STATE_REC_DTYPE.itemsize
+
+        def fill(first, count):
+            check(self._lib.hm_state_export_copy(self._ctx, base + first * size, int(first), int(count)), self._ctx,
+                  "hm_state_export_copy")
+        return {f: int(getattr(info, f)) for f in _INFO_FIELDS}, int(n.value), recs, raw[0], fill
 
     def _free_pinned(self):
         buf = getattr(self, "_pinned", None)
@@ -448,25 +471,141 @@ def merge_state(base, deltas):
 STATE_FILE_MAGIC = b"MHSTATE1"   # raw state file: magic, u64 header bytes, JSON header, padding to 64 B, the records
 
 
-def save_state_file(path, info, recs, meta=None):
+def save_state_file(path, info, recs, meta=None, fill=None, raw=None):
     """info + records written atomically to `path` (tmp file, fsync, rename): a JSON header (the hm_state_info fields,
     the record count and layout, `meta` -- a str: the checkpoint chain record, mobheat.checkpoint) and the 64-B records
-    as raw bytes in one write.  (np.savez's zip container CRC-checked and copied every byte under the GIL: the
-    checkpoint thread then slowed the next batch's host work and waited ~0.4 s per 10M-key delta, profiles/r4.)"""
+    as raw bytes.  (np.savez's zip container CRC-checked and copied every byte under the GIL: the checkpoint thread then
+    slowed the next batch's host work and waited ~0.4 s per 10M-key delta, profiles/r4.)
+
+    fill / raw (Engine.export_begin): the records are still on the device -- fill(first, count) copies them into recs,
+    slice by slice on a copier thread while this thread writes the slices that have landed; raw is recs' page-aligned
+    buffer, and the file then goes to the disk with O_DIRECT writes straight from it (the header padded to 4 KiB), so
+    that neither a page-cache copy nor an fsync of the data follows the write (on the GPU box: 635 MB in ~85 ms vs
+    ~62 ms write + ~63 ms fsync buffered, profiles/r6/r6d/file_probe.log).  MOBHEAT_CKPT_DIRECT=0, or a file system
+    that refuses O_DIRECT, writes buffered + fsync."""
     import os
-    recs = np.ascontiguousarray(recs, dtype=STATE_REC_DTYPE)
-    head = json.dumps({"info": {k: int(info[k]) for k in _INFO_FIELDS}, "n": int(recs.size),
+    recs = recs if fill is not None else np.ascontiguousarray(recs, dtype=STATE_REC_DTYPE)
+    n = int(recs.size)
+    size = STATE_REC_DTYPE.itemsize
+    direct = raw is not None and hasattr(os, "O_DIRECT") and os.getenv("MOBHEAT_CKPT_DIRECT", "1") != "0"
+    head = json.dumps({"info": {k: int(info[k]) for k in _INFO_FIELDS}, "n": n,
                        "fields": list(STATE_REC_DTYPE.names), "itemsize": STATE_REC_DTYPE.itemsize,
                        "meta": meta}).encode()
-    head += b" " * (-(len(head) + 16) % 64)
+    head += b" " * (-(len(head) + 16) % (4096 if direct else 64))
+    header = STATE_FILE_MAGIC + len(head).to_bytes(8, "little") + head
     tmp = f"{path}.tmp{os.getpid()}"
-    with open(tmp, "wb") as f:
-        f.write(STATE_FILE_MAGIC + len(head).to_bytes(8, "little") + head)
-        if recs.size:
-            f.write(memoryview(recs).cast("B"))
-        f.flush()
-        os.fsync(f.fileno())
+    slices = _Slices(n, fill)
+    try:
+        if direct:
+            try:
+                _write_direct(tmp, header, raw, n * size, slices)
+            except OSError as e:
+                import errno
+                if e.errno != errno.EINVAL:
+                    raise
+                direct = False   # (a file system without O_DIRECT: buffered below, the same bytes)
+                head = head.rstrip(b" ")
+                head += b" " * (-(len(head) + 16) % 64)
+                header = STATE_FILE_MAGIC + len(head).to_bytes(8, "little") + head
+        if not direct:
+            with open(tmp, "wb") as f:
+                f.write(header)
+                body = memoryview(recs.view(np.uint8)) if n else None
+                for lo, hi in slices:
+                    f.write(body[lo * size:hi * size])
+                f.flush()
+                os.fsync(f.fileno())
+    except BaseException:
+        slices.close()
+        try:
+            os.remove(tmp)
+        except OSError:
+            pass
+        raise
+    slices.close()
     os.replace(tmp, path)
+
+
+class _Slices:
+    """The records in slices of SLICE records, in order: each yielded (lo, hi) once fill(lo, hi - lo) has landed it --
+    a copier thread runs the fills ahead of the consumer (fill None: the records are in memory already)."""
+    SLICE = 1 << 19   # (32 MiB of records: a multiple of 4 KiB)
+
+    def __init__(self, n, fill):
+        import threading
+        self.bounds = [(lo, min(lo + self.SLICE, n)) for lo in range(0, n, self.SLICE)]
+        self.fill = fill
+        self.done = [threading.Event() for _ in self.bounds]
+        self.err = None
+        self.stop = False
+        self.thread = None
+        if fill is not None and self.bounds:
+            self.thread = threading.Thread(target=self._run, name="mobheat-export-copy", daemon=True)
+            self.thread.start()
+
+    def _run(self):
+        try:
+            for (lo, hi), ev in zip(self.bounds, self.done):
+                if self.stop:
+                    return
+                self.fill(lo, hi - lo)
+                ev.set()
+        except BaseException as e:   # (handed to the consumer)
+            self.err = e
+        finally:
+            for ev in self.done:
+                ev.set()
+
+    def __iter__(self):
+        for (lo, hi), ev in zip(self.bounds, self.done):
+            if self.thread is not None:
+                ev.wait()
+                if self.err is not None:
+                    raise self.err
+            yield lo, hi
+
+    def close(self):
+        self.stop = True
+        if self.thread is not None:
+            self.thread.join()
+            self.thread = None
+
+
+def _write_direct(tmp, header, raw, nbytes, slices):
+    """header + raw[:nbytes] to tmp with O_DIRECT writes (4-KiB aligned offsets, lengths and buffers: the last block
+    zero-padded in raw, then the file truncated to its size) and one fsync (metadata only: the data went to the disk)."""
+    import mmap
+    import os
+    fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC | os.O_DIRECT, 0o644)
+    try:
+        hb = mmap.mmap(-1, len(header))   # (page-aligned)
+        hb.write(header)
+        _pwrite_all(fd, memoryview(hb), 0)
+        hb.close()
+        off = len(header)
+        mv = memoryview(raw)
+        rec = STATE_REC_DTYPE.itemsize
+        for lo, hi in slices:
+            b0, b1 = lo * rec, hi * rec
+            if b1 == nbytes and b1 % 4096:
+                pad = -b1 % 4096
+                raw[b1:b1 + pad] = 0
+                b1 += pad
+            _pwrite_all(fd, mv[b0:b1], off + b0)
+        os.ftruncate(fd, off + nbytes)
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
+def _pwrite_all(fd, mv, off):
+    import os
+    done = 0
+    while done < len(mv):
+        k = os.pwrite(fd, mv[done:], off + done)
+        if k <= 0:
+            raise OSError("short O_DIRECT write")
+        done += k
 
 
 def _state_header(f, path):

@@ -284,6 +284,12 @@ def _pandas_to_arrow(pdf, pre=None):
             cols[str(name)] = pa.array(c.array)
         elif c.dtype.kind == "f":          # numpy float: NaN is a value, there is no null
             cols[str(name)] = pa.array(c.to_numpy(), from_pandas=False)
+        elif c.dtype == np.dtype("datetime64[ns]"):   # the values buffer as it is (no copy), NaT -> null
+            v = np.ascontiguousarray(c.to_numpy())
+            nat = v.view(np.int64) == np.iinfo(np.int64).min
+            k = int(np.count_nonzero(nat))
+            bits = pa.py_buffer(np.packbits(~nat, bitorder="little")) if k else None
+            cols[str(name)] = pa.Array.from_buffers(pa.timestamp("ns"), v.size, [bits, pa.py_buffer(v)], null_count=k)
         elif c.dtype == object:            # None -> null, float('nan') -> NaN
             try:
                 cols[str(name)] = pa.array(c.to_numpy(), from_pandas=False)
@@ -488,7 +494,9 @@ class ArrowColumns:
         import pyarrow.compute as pc
         arr = self._chunk(t, "eventTs") if "eventTs" in t.column_names else None
         if arr is not None and pa.types.is_timestamp(arr.type):
-            if arr.type.unit != "us":
+            if arr.type.unit == "ns":   # (pandas' datetime64[ns]: the device truncates to microseconds, no host cast)
+                col.unit = 1
+            elif arr.type.unit != "us":
                 arr = pc.cast(arr, pa.timestamp("us", tz=arr.type.tz), safe=False)
         elif arr is not None or "eventTs" not in t.column_names:
             # raw ISO strings (to_timestamp, :92), or eventTs of another type: parsed / cast on the host

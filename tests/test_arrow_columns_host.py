@@ -54,6 +54,8 @@ def _readback(ac):
     sv = _bits(a.speed.validity, a.speed.validity_offset, n) if v is not None else np.zeros(n, bool)
     out["speed_valid"], out["speed"] = sv, np.where(sv, v, 0.0) if v is not None else np.zeros(n)
     t = _vals(a.ts_us, n, ctypes.c_int64)
+    if t is not None and a.ts_us.unit == 1:   # (nanoseconds: truncated toward zero to microseconds on the device)
+        t = np.where(t < 0, -((-t) // 1000), t // 1000)
     tv = _bits(a.ts_us.validity, a.ts_us.validity_offset, n) if t is not None else np.zeros(n, bool)
     out["ts_us"] = np.where(tv, t, 0)
     p, v = _strings(a.provider, n), _strings(a.vehicle, n)

@@ -114,3 +114,43 @@ def test_arrow_columns_rejects_bad_offsets():
             eng.arrow_columns(a)
     finally:
         eng.close()
+
+
+def test_arrow_columns_nanosecond_timestamps():
+    """A pandas frame's datetime64[ns] eventTs goes to the device as it is (hm_arrow_col.unit = 1) and is truncated
+    toward zero to microseconds there -- equal to Arrow's unsafe ns -> us cast (the host path's), pre-1970 instants
+    with a sub-microsecond part and NaT (-> a null eventTs: the row is invalid) included; a unit on any other column
+    is refused."""
+    import pyarrow.compute as pc
+    import mobheat
+    from mobheat import _lib, stream
+    rng = np.random.default_rng(8)
+    n = 5000
+    ns = rng.integers(-2 * 10**18, 2 * 10**18, n)
+    ns[::7] -= ns[::7] % 1000    # (whole microseconds too)
+    ns[:4] = [-1, -999, -1000, -1001]
+    ts = pd.Series(pd.to_datetime(ns, unit="ns"))
+    ts[5::97] = pd.NaT
+    pdf = pd.DataFrame({"provider": "p", "vehicleId": [f"v{k % 50}" for k in range(n)], "lat": rng.uniform(-60, 60, n),
+                        "lon": rng.uniform(-180, 180, n), "speedKmh": rng.uniform(0, 50, n), "eventTs": ts})
+    cols = stream.device_columns(pdf)
+    a = cols["arrow"].struct
+    assert a.ts_us.unit == 1
+    exp = pc.cast(pa.array(ts), pa.timestamp("us"), safe=False)
+    exp_v = exp.is_valid().to_numpy(zero_copy_only=False)
+    exp_t = exp.cast(pa.int64()).fill_null(0).to_numpy()
+    eng = mobheat.HeatmapEngine(h3_res=8, device=0)
+    try:
+        kb = eng.arrow_columns(a)
+        lib = _lib.load()
+        got_t, got_v = np.empty(n, np.int64), np.empty(n, np.uint8)
+        _lib.check(lib.hm_memcpy(got_t.ctypes.data, kb.batch.ts_us, got_t.nbytes, 1), None, "hm_memcpy")
+        _lib.check(lib.hm_memcpy(got_v.ctypes.data, kb.batch.row_valid, got_v.nbytes, 1), None, "hm_memcpy")
+        np.testing.assert_array_equal(got_v.astype(bool), exp_v)
+        np.testing.assert_array_equal(got_t[exp_v], exp_t[exp_v])
+        assert list(got_t[:4]) == [0, 0, -1, -1]
+        a.lat.unit = 1
+        with pytest.raises(RuntimeError, match="only eventTs"):
+            eng.arrow_columns(a)
+    finally:
+        eng.close()

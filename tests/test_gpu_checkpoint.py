@@ -306,3 +306,51 @@ def test_shard_import_rejects_foreign_keys():
         assert sorted(back["cell"].tolist()) == sorted(mine["cell"].tolist())
     finally:
         eng.close()
+
+
+def test_export_begin_copy_equals_exports_and_runs_beside_encode(tmp_path):
+    """hm_state_export_begin / _copy (the checkpoint writer's two halves): the dump copied slice by slice equals
+    hm_state_export / hm_state_export_touched record for record (as sets), the copies running on a thread while the
+    batch's tile statements are encoded on this engine's stream give the same statements as an encode alone; a copy
+    outside the dump, or after another batch, is refused; the streamed file (save_state_file with fill / raw, O_DIRECT
+    where the file system takes it) reads back the same records."""
+    import threading
+    from mobheat import HeatmapEngine
+    from mobheat.engine import load_state_file, save_state_file
+    bs = _batches(seed=33)
+    eng = HeatmapEngine(h3_res=9)
+    try:
+        for e in range(4):
+            eng.process_batch(e, **bs[e])
+        ref_full = eng.export_state()
+        ref_delta = eng.export_state_delta()
+        ref_stm, ref_offs = eng.encode_tile_updates("ath", 45, copy=True)
+        for touched, (rinfo, rrecs) in ((False, ref_full), (True, ref_delta)):
+            info, n, recs, raw, fill = eng.export_begin(touched_only=touched)
+            assert info == rinfo and n == rrecs.size > 0
+            got = {}
+
+            def copier():
+                for lo in range(0, n, 997):
+                    fill(lo, min(997, n - lo))
+                got["done"] = True
+            th = threading.Thread(target=copier)
+            th.start()
+            stm, offs = eng.encode_tile_updates("ath", 45, copy=True)
+            th.join()
+            assert got.get("done")
+            np.testing.assert_array_equal(np.sort(recs), np.sort(rrecs))
+            assert stm.tobytes() == ref_stm.tobytes() and np.array_equal(offs, ref_offs)
+            with pytest.raises(RuntimeError, match="outside the dump"):
+                fill(n - 1, 2)
+            path = str(tmp_path / f"s{int(touched)}.mhs")
+            info, n, recs, raw, fill = eng.export_begin(touched_only=touched)
+            save_state_file(path, info, recs, meta="{}", fill=fill, raw=raw)
+            i2, r2 = load_state_file(path)
+            assert i2 == rinfo
+            np.testing.assert_array_equal(np.sort(r2), np.sort(rrecs))
+        eng.process_batch(4, **bs[4])
+        with pytest.raises(RuntimeError, match="without an hm_state_export_begin"):
+            fill(0, 1)
+    finally:
+        eng.close()
