@@ -271,6 +271,11 @@ int hm_state_export_touched(hm_ctx *ctx, hm_state_info *info, hm_state_rec *recs
  * stage call or another export; a batch or another export in between makes it fail (HM_E_STATE). */
 int hm_state_export_begin(hm_ctx *ctx, hm_state_info *info, int32_t touched_only, int64_t *n_out);
 int hm_state_export_copy(hm_ctx *ctx, hm_state_rec *recs, int64_t first, int64_t count);
+/* _copy split in two: _async enqueues the copy and marks its completion in slot (0..63) -- call it on the engine's
+ * thread BEFORE the statements' encode, so that the encode's copies queue behind it, not the other way round -- and
+ * _wait (any thread) blocks until the copy marked in slot has landed. */
+int hm_state_export_copy_async(hm_ctx *ctx, hm_state_rec *recs, int64_t first, int64_t count, int32_t slot);
+int hm_state_export_copy_wait(hm_ctx *ctx, int32_t slot);
 /* Restores an exported state into a context that has processed no batch (HM_E_STATE otherwise); the
  * config fields of info must equal the context's (HM_E_INVALID). recs: info->n_keys distinct keys, host memory. */
 int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *recs);

@@ -41,7 +41,12 @@ static int statements_out(hm_ctx *ctx, int64_t n, int64_t total, int32_t out_mem
         if ((rc = ensure_host(ctx, &ctx->h_td_off, dummy, want, 8))) return rc;
         ctx->h_td_off_cap = want;
     }
-    if (total) HIPCHK(ctx, hipMemcpyAsync(ctx->h_td_bytes, ctx->td_bytes.p, total, hipMemcpyDeviceToHost, ctx->stream));
+    // (in 128-MiB pieces: a checkpoint writer's export copies on copy_stream interleave with them instead of queueing
+    // behind one 3.7-GB copy -- the state file's disk writes then start while the statements are still landing)
+    constexpr int64_t PIECE = int64_t(128) << 20;
+    for (int64_t o = 0; o < total; o += PIECE)
+        HIPCHK(ctx, hipMemcpyAsync((uint8_t *)ctx->h_td_bytes + o, (const uint8_t *)ctx->td_bytes.p + o, (size_t)std::min(PIECE, total - o),
+                                   hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->h_td_off, off, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     *bytes = (const uint8_t *)ctx->h_td_bytes;

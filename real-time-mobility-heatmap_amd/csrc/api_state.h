@@ -131,6 +131,31 @@ int hm_state_export_copy(hm_ctx *ctx, hm_state_rec *recs, int64_t first, int64_t
     return HM_OK;
 }
 
+// The copies enqueued up front (before the statements' encode is: one hardware queue serves both streams, so a copy
+// enqueued after the encode's would land after all of its pieces), one event per slice; the writer waits slice by slice.
+int hm_state_export_copy_async(hm_ctx *ctx, hm_state_rec *recs, int64_t first, int64_t count, int32_t slot) {
+    if (!ctx || first < 0 || count < 0 || (count > 0 && !recs) || slot < 0 || slot >= hm_ctx::EXPORT_SLICES)
+        return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    if (ctx->export_dump_n < 0 || ctx->export_dump_seq != ctx->seq)
+        return set_err(ctx, HM_E_STATE, "hm_state_export_copy without an hm_state_export_begin after the last batch");
+    if (first + count > ctx->export_dump_n)
+        return set_err(ctx, HM_E_INVALID, "records [%lld, %lld) outside the dump of %lld", (long long)first,
+                       (long long)(first + count), (long long)ctx->export_dump_n);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (count > 0)
+        HIPCHK(ctx, hipMemcpyAsync(recs, (const GrowRec *)ctx->parts_regrow.p + first, (size_t)count * sizeof(GrowRec),
+                                   hipMemcpyDeviceToHost, ctx->copy_stream));
+    HIPCHK(ctx, hipEventRecord(ctx->export_ev[slot], ctx->copy_stream));
+    return HM_OK;
+}
+
+int hm_state_export_copy_wait(hm_ctx *ctx, int32_t slot) {
+    if (!ctx || slot < 0 || slot >= hm_ctx::EXPORT_SLICES) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, hipEventSynchronize(ctx->export_ev[slot]));
+    return HM_OK;
+}
+
 // Import: the records' windows get tables sized as a batch's new windows would be, then the records are merged
 // through the growth path (partition + k_merge_owned in rehash mode: no counting, no rows, no touched update).
 int hm_state_import(hm_ctx *ctx, const hm_state_info *info, const hm_state_rec *recs) {

@@ -76,6 +76,8 @@ struct hm_ctx {
     int64_t touched_dump_n = 0;
     int64_t export_dump_n = -1;       // hm_state_export_begin: records of the dump in parts_regrow (-1: none) ...
     unsigned long long export_dump_seq = 0;   // ... made after batch seq (hm_state_export_copy checks both)
+    static constexpr int EXPORT_SLICES = 64;
+    hipEvent_t export_ev[EXPORT_SLICES] = {};   // hm_state_export_copy_async: slice k landed
     DevBuf parts_regrow_sorted;       // growth: the same, partitioned (not parts_sorted: a binned batch's slabs are there)
     // multi-GPU exchange (api_stage.h): chunk starts and headers, the local -> global window slot map; the owner's
     // per-sender bin counts and their scan, its bins' segments, the received candidates and table-mode partials

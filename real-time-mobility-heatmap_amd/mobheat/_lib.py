@@ -129,6 +129,8 @@ SIGNATURES = {
     "hm_state_export_touched": (c_i32, [c_vp, _P(HmStateInfo), c_vp, c_i64, c_vp]),
     "hm_state_export_begin": (c_i32, [c_vp, _P(HmStateInfo), c_i32, c_vp]),
     "hm_state_export_copy": (c_i32, [c_vp, c_vp, c_i64, c_i64]),
+    "hm_state_export_copy_async": (c_i32, [c_vp, c_vp, c_i64, c_i64, c_i32]),
+    "hm_state_export_copy_wait": (c_i32, [c_vp, c_i32]),
     "hm_state_version": (c_i64, [c_vp]),
     "hm_state_import": (c_i32, [c_vp, _P(HmStateInfo), c_vp]),
     "hm_last_windows": (c_i32, [c_vp, c_vp, c_i64, _P(c_i64)]),

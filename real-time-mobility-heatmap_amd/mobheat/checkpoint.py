@@ -205,15 +205,22 @@ class StateCheckpoints:
         """The file side of a prepared checkpoint: this rank's files of epochs >= its epoch deleted (an abandoned
         lineage), the file written atomically (fsync + rename), then every file of this rank that the newest two
         snapshots of the chain no longer need (other lineages included).  Returns the kind written."""
+        import time
         from .engine import save_state_file
+        t0 = time.perf_counter()
         epoch = job["epoch"]
         os.makedirs(self.root, exist_ok=True)
         for e in self.scan():
             if e.rank == self.rank and e.world == self.world and e.epoch >= epoch:
                 _remove(e.path)
-        save_state_file(self.path(job["kind"], epoch), job["info"], job["recs"], meta=json.dumps(job["meta"]),
-                        fill=job.get("fill"), raw=job.get("raw"))
+        t1 = time.perf_counter()
+        stats = save_state_file(self.path(job["kind"], epoch), job["info"], job["recs"], meta=json.dumps(job["meta"]),
+                                fill=job.get("fill"), raw=job.get("raw"))
+        t2 = time.perf_counter()
         self._prune(job["meta"]["lineage"], epoch)
+        # (the file side's phases, ms: foreach_batch_func reports them beside its own)
+        job["timings"] = {"ckpt_clear": 1e3 * (t1 - t0), "ckpt_file": 1e3 * (t2 - t1),
+                          "ckpt_prune": 1e3 * (time.perf_counter() - t2), **stats}
         return job["kind"]
 
     def _prune(self, lineage, epoch):

@@ -272,24 +272,34 @@ class HeatmapEngine:
             raw_out.append(raw)
         return raw[: n * STATE_REC_DTYPE.itemsize].view(STATE_REC_DTYPE)
 
-    def export_begin(self, touched_only):
-        """hm_state_export_begin: the state (or the last batch's touched keys) dumped on the device -> (info dict, n,
-        recs, raw, fill): recs a view of the page-locked export buffer (raw: all of it, uint8), filled by
-        fill(first, count) = hm_state_export_copy -- which may run on another thread while this engine encodes the
-        batch's statements (the checkpoint writer: mobheat.checkpoint)."""
+    def export_begin(self, touched_only, slice_records=1 << 19):
+        """hm_state_export_begin: the state (or the last batch's touched keys) dumped on the device, and its copy into
+        the page-locked export buffer enqueued in slices (hm_state_export_copy_async, at most 64; call this before the
+        statements' encode, whose copies then queue behind these) -> (info dict, n, recs, raw, fill): recs a view of
+        the buffer (raw: all of it, uint8); fill(first, count) returns once records [first, first + count) have landed
+        (hm_state_export_copy_wait) -- from any thread, while this engine encodes the batch's statements (the
+        checkpoint writer: mobheat.checkpoint)."""
         info = HmStateInfo()
         n = ctypes.c_int64()
         check(self._lib.hm_state_export_begin(self._ctx, ctypes.byref(info), int(bool(touched_only)), ctypes.byref(n)),
               self._ctx, "hm_state_export_begin")
+        n = int(n.value)
         raw = []
-        recs = self._export_buffer(int(n.value), True, raw)
+        recs = self._export_buffer(n, True, raw)
         base = raw[0].ctypes.data
         size = STATE_REC_DTYPE.itemsize
+        s = max(int(slice_records), -(-n // 64), 1)
+        for k in range(-(-n // s)):
+            lo = k * s
+            check(self._lib.hm_state_export_copy_async(self._ctx, base + lo * size, lo, min(s, n - lo), k), self._ctx,
+                  "hm_state_export_copy_async")
 
         def fill(first, count):
-            check(self._lib.hm_state_export_copy(self._ctx, base + first * size, int(first), int(count)), self._ctx,
-                  "hm_state_export_copy")
-        return {f: int(getattr(info, f)) for f in _INFO_FIELDS}, int(n.value), recs, raw[0], fill
+            if first < 0 or count < 0 or first + count > n:
+                raise RuntimeError(f"hm_state_export_copy: records [{first}, {first + count}) outside the dump of {n}")
+            for k in range(first // s, -(-(first + count) // s)):
+                check(self._lib.hm_state_export_copy_wait(self._ctx, k), self._ctx, "hm_state_export_copy_wait")
+        return {f: int(getattr(info, f)) for f in _INFO_FIELDS}, n, recs, raw[0], fill
 
     def _free_pinned(self):
         buf = getattr(self, "_pinned", None)
@@ -524,6 +534,7 @@ def save_state_file(path, info, recs, meta=None, fill=None, raw=None):
         raise
     slices.close()
     os.replace(tmp, path)
+    return {"ckpt_copy_wait": slices.waited_ms, "ckpt_direct": float(direct)}
 
 
 class _Slices:
@@ -537,6 +548,7 @@ class _Slices:
         self.fill = fill
         self.done = [threading.Event() for _ in self.bounds]
         self.err = None
+        self.waited_ms = 0.0   # (the consumer's time blocked on slices not yet copied)
         self.stop = False
         self.thread = None
         if fill is not None and self.bounds:
@@ -559,7 +571,11 @@ class _Slices:
     def __iter__(self):
         for (lo, hi), ev in zip(self.bounds, self.done):
             if self.thread is not None:
-                ev.wait()
+                if not ev.is_set():
+                    import time
+                    t = time.perf_counter()
+                    ev.wait()
+                    self.waited_ms += 1e3 * (time.perf_counter() - t)
                 if self.err is not None:
                     raise self.err
             yield lo, hi

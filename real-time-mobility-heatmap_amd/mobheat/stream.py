@@ -155,7 +155,9 @@ def checkpoint_begin(epoch_id):
         kind = st.write(job)
         st.prune_other_worlds(lineage)
         return kind
-    return _IO.submit(write)
+    fut = _IO.submit(write)
+    fut.job = job
+    return fut
 
 
 def reset_engine():
@@ -879,6 +881,7 @@ def foreach_batch_func(df, epoch_id: int):
         if ckpt is not None:   # (also when a write failed: a replay must not race the file)
             exc = ckpt.exception()
             lap("checkpoint_wait")
+            tm.update(getattr(ckpt, "job", {}).get("timings", {}))
     if ckpt is not None and exc is not None:
         raise exc
     LAST_TIMINGS = tm

@@ -310,13 +310,15 @@ def test_shard_import_rejects_foreign_keys():
 
 def test_export_begin_copy_equals_exports_and_runs_beside_encode(tmp_path):
     """hm_state_export_begin / _copy (the checkpoint writer's two halves): the dump copied slice by slice equals
-    hm_state_export / hm_state_export_touched record for record (as sets), the copies running on a thread while the
-    batch's tile statements are encoded on this engine's stream give the same statements as an encode alone; a copy
-    outside the dump, or after another batch, is refused; the streamed file (save_state_file with fill / raw, O_DIRECT
-    where the file system takes it) reads back the same records."""
+    hm_state_export / hm_state_export_touched record for record (as sets), the copies (enqueued up front, waited for
+    slice by slice -- and the synchronous hm_state_export_copy) landing on a thread while the batch's tile statements
+    are encoded on this engine's stream give the same statements as an encode alone; a copy outside the dump, or
+    after another batch, is refused; the streamed file (save_state_file with fill / raw, O_DIRECT where the file system
+    takes it) reads back the same records."""
     import threading
-    from mobheat import HeatmapEngine
-    from mobheat.engine import load_state_file, save_state_file
+    from mobheat import HeatmapEngine, _lib
+    from mobheat.engine import STATE_REC_DTYPE, load_state_file, save_state_file
+    lib = _lib.load()
     bs = _batches(seed=33)
     eng = HeatmapEngine(h3_res=9)
     try:
@@ -326,13 +328,16 @@ def test_export_begin_copy_equals_exports_and_runs_beside_encode(tmp_path):
         ref_delta = eng.export_state_delta()
         ref_stm, ref_offs = eng.encode_tile_updates("ath", 45, copy=True)
         for touched, (rinfo, rrecs) in ((False, ref_full), (True, ref_delta)):
-            info, n, recs, raw, fill = eng.export_begin(touched_only=touched)
+            info, n, recs, raw, fill = eng.export_begin(touched_only=touched, slice_records=997)
             assert info == rinfo and n == rrecs.size > 0
+            sync = np.zeros(n, STATE_REC_DTYPE)
             got = {}
 
             def copier():
-                for lo in range(0, n, 997):
-                    fill(lo, min(997, n - lo))
+                for lo in range(0, n, 1500):
+                    fill(lo, min(1500, n - lo))
+                    _lib.check(lib.hm_state_export_copy(eng._ctx, sync[lo:].ctypes.data, lo, min(1500, n - lo)),
+                               eng._ctx, "hm_state_export_copy")
                 got["done"] = True
             th = threading.Thread(target=copier)
             th.start()
@@ -340,9 +345,12 @@ def test_export_begin_copy_equals_exports_and_runs_beside_encode(tmp_path):
             th.join()
             assert got.get("done")
             np.testing.assert_array_equal(np.sort(recs), np.sort(rrecs))
+            np.testing.assert_array_equal(sync, recs)
             assert stm.tobytes() == ref_stm.tobytes() and np.array_equal(offs, ref_offs)
             with pytest.raises(RuntimeError, match="outside the dump"):
                 fill(n - 1, 2)
+            with pytest.raises(RuntimeError, match="outside the dump"):
+                _lib.check(lib.hm_state_export_copy(eng._ctx, sync.ctypes.data, n - 1, 2), eng._ctx, "x")
             path = str(tmp_path / f"s{int(touched)}.mhs")
             info, n, recs, raw, fill = eng.export_begin(touched_only=touched)
             save_state_file(path, info, recs, meta="{}", fill=fill, raw=raw)
@@ -350,7 +358,10 @@ def test_export_begin_copy_equals_exports_and_runs_beside_encode(tmp_path):
             assert i2 == rinfo
             np.testing.assert_array_equal(np.sort(r2), np.sort(rrecs))
         eng.process_batch(4, **bs[4])
-        with pytest.raises(RuntimeError, match="without an hm_state_export_begin"):
-            fill(0, 1)
+        buf = np.zeros(1, STATE_REC_DTYPE)
+        for call in (lambda: lib.hm_state_export_copy(eng._ctx, buf.ctypes.data, 0, 1),
+                     lambda: lib.hm_state_export_copy_async(eng._ctx, buf.ctypes.data, 0, 1, 0)):
+            with pytest.raises(RuntimeError, match="without an hm_state_export_begin"):
+                _lib.check(call(), eng._ctx, "x")
     finally:
         eng.close()

@@ -106,6 +106,28 @@ def main():
         c0 = time.perf_counter()
         save_state_file(path + ".2", {f: int(getattr(info, f)) for f in stream_fields()}, recs, meta="{}")
         t["file_again"] = time.perf_counter() - c0
+        # the streamed checkpoint writer (export_begin + save_state_file with fill / raw: sliced copies + O_DIRECT)
+        c0 = time.perf_counter()
+        info3, n3, recs3, raw3, fill3 = eng.export_begin(True)
+        t["begin"] = time.perf_counter() - c0
+        c0 = time.perf_counter()
+        save_state_file(path + ".3", info3, recs3, meta="{}", fill=fill3, raw=raw3)
+        t["streamed_write"] = time.perf_counter() - c0
+        info3, n3, recs3, raw3, fill3 = eng.export_begin(True)
+        done = {}
+
+        def wr():
+            c1 = time.perf_counter()
+            save_state_file(path + ".4", info3, recs3, meta="{}", fill=fill3, raw=raw3)
+            done["t"] = time.perf_counter() - c1
+        c0 = time.perf_counter()
+        th = threading.Thread(target=wr)
+        th.start()
+        buf, offs = eng.encode_tile_updates("ath", 45)
+        t["encode_beside_streamed_write"] = time.perf_counter() - c0
+        th.join()
+        t["streamed_write_beside_encode"] = done["t"]
+        t["both_done"] = time.perf_counter() - c0
         out = {k2: (round(v * 1e3, 2) if isinstance(v, float) and not k2.endswith("GBps") else
                     (round(v, 2) if isinstance(v, float) else v)) for k2, v in t.items()}
         out.update(step=s, delta_keys=int(recs.size), delta_bytes=int(recs.nbytes), statements=int(offs.size - 1),

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--mb", type=int, default=635)
     ap.add_argument("--dir", default=tempfile.gettempdir())
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--pinned", action="store_true")
     a = ap.parse_args()
     nbytes = a.mb << 20
     mounts = [ln.split() for ln in open("/proc/mounts")]
@@ -53,8 +54,16 @@ def main():
     buf = memoryview(raw)
     np.frombuffer(raw, np.uint8)[:] = np.random.default_rng(0).integers(0, 256, nbytes, dtype=np.uint8)
     path = os.path.join(a.dir, "mobheat_file_probe.bin")
+    bufs = {"mmap": buf}
+    if a.pinned:   # page-locked host memory (hipHostMalloc, as the engine's export buffer): O_DIRECT from it
+        import torch
+        pt = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        pn = pt.numpy()
+        pn[:] = np.frombuffer(raw, np.uint8)
+        bufs["pinned"] = memoryview(pn)
     for rep in range(a.reps):
-        for mode, threads in (("write", 1), ("pwrite", 4), ("pwrite", 8), ("pwrite", 16), ("direct", 1), ("direct", 8)):
+      for src, buf in bufs.items():
+        for mode, threads in (("write", 1), ("pwrite", 4), ("direct", 1), ("direct", 4)):
             flags = os.O_WRONLY | os.O_CREAT | os.O_TRUNC
             if mode == "direct":
                 flags |= getattr(os, "O_DIRECT", 0)
@@ -74,7 +83,7 @@ def main():
                 t1 = time.perf_counter()
                 os.fsync(fd)
                 t2 = time.perf_counter()
-                print(json.dumps({"rep": rep, "mode": mode, "threads": threads, "write_ms": round(1e3 * (t1 - t0), 1),
+                print(json.dumps({"rep": rep, "src": src, "mode": mode, "threads": threads, "write_ms": round(1e3 * (t1 - t0), 1),
                                   "fsync_ms": round(1e3 * (t2 - t1), 1), "GBps": round(nbytes / (t2 - t0) / 1e9, 2)}),
                       flush=True)
             except OSError as e:
