@@ -49,6 +49,8 @@ extern "C" {
 /* memory kinds for batch pointers */
 #define HM_MEM_HOST 0
 #define HM_MEM_DEVICE 1
+#define HM_MEM_HOST_STREAM 2   /* hm_encode_* outputs only: pinned host memory; the offsets have landed when the call
+                                  returns, the bytes land in pieces after it (hm_statements_wait) */
 
 typedef struct hm_config {
     int32_t abi_version;            /* must be HM_ABI_VERSION */
@@ -323,6 +325,10 @@ typedef struct hm_position_doc_cfg {
 } hm_position_doc_cfg;
 int hm_encode_position_updates(hm_ctx *ctx, const hm_position_doc_cfg *cfg, int32_t out_memory, const uint8_t **bytes,
                                const int64_t **offsets, int64_t *n_docs);
+/* After an hm_encode_* call with HM_MEM_HOST_STREAM: blocks until bytes [0, upto) of its statements have landed in
+ * the host buffer (any thread), so that a sink sends each command as soon as its statements are there -- the
+ * statements' device-to-host copy overlaps the sink's writes instead of preceding them (reference :191-196,230-235). */
+int hm_statements_wait(hm_ctx *ctx, int64_t upto);
 
 /* Host execution of hm_encode_tile_updates' statement encoder on caller arrays (no GPU needed): statement i
  * is bytes[offsets[i], offsets[i+1]) (offsets: n+1 entries; HM_E_INVALID if cap bytes do not suffice). */

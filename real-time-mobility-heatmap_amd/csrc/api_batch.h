@@ -50,6 +50,8 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     for (auto &e : ctx->export_ev)
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
+    for (auto &e : ctx->stm_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) { ctx->err = "event"; return fail("create"); }
     // k_merge_owned's resident tags live in dynamic LDS of up to MO_TAG_MAX bytes (merge_sorted)
     if (hipFuncSetAttribute((const void *)k_merge_owned<EventRec, false>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
         hipFuncSetAttribute((const void *)k_merge_owned<EventRec, true>, hipFuncAttributeMaxDynamicSharedMemorySize, MO_TAG_MAX) != hipSuccess ||
@@ -241,6 +243,8 @@ void hm_destroy(hm_ctx *ctx) {
         if (e) (void)hipEventDestroy(e);
     if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
     for (auto &e : ctx->export_ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto &e : ctx->stm_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
     if (ctx->side_stream) (void)hipStreamDestroy(ctx->side_stream);

@@ -24,6 +24,12 @@ static int statements_out(hm_ctx *ctx, int64_t n, int64_t total, int32_t out_mem
     int rc;
     unsigned long long *off = (unsigned long long *)ctx->td_off.p;
     *n_docs = n;
+    if (out_memory != HM_MEM_HOST && out_memory != HM_MEM_DEVICE && out_memory != HM_MEM_HOST_STREAM)
+        return set_err(ctx, HM_E_INVALID, "bad memory kind %d", out_memory);
+    if (ctx->stm_pieces) {   // (a streamed encode's pieces still landing: they finish before the buffers are reused)
+        ctx->stm_pieces = 0;
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+    }
     if (out_memory == HM_MEM_DEVICE) {
         HIPCHK(ctx, ctx_sync(ctx, __LINE__));
         *bytes = (const uint8_t *)ctx->td_bytes.p;
@@ -41,6 +47,25 @@ static int statements_out(hm_ctx *ctx, int64_t n, int64_t total, int32_t out_mem
         if ((rc = ensure_host(ctx, &ctx->h_td_off, dummy, want, 8))) return rc;
         ctx->h_td_off_cap = want;
     }
+    *bytes = (const uint8_t *)ctx->h_td_bytes;
+    *offsets = (const int64_t *)ctx->h_td_off;
+    if (out_memory == HM_MEM_HOST_STREAM) {
+        // the offsets first (the sink cuts its commands from them), then the bytes in at most 64 pieces of >= 32 MiB,
+        // each marked by an event hm_statements_wait blocks on
+        HIPCHK(ctx, hipMemcpyAsync(ctx->h_td_off, off, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, ctx_sync(ctx, __LINE__));
+        const int64_t piece = std::max<int64_t>(int64_t(32) << 20, (total + hm_ctx::STM_PIECES - 1) / hm_ctx::STM_PIECES);
+        int k = 0;
+        for (int64_t o = 0; o < total; o += piece, k++) {
+            HIPCHK(ctx, hipMemcpyAsync((uint8_t *)ctx->h_td_bytes + o, (const uint8_t *)ctx->td_bytes.p + o,
+                                       (size_t)std::min(piece, total - o), hipMemcpyDeviceToHost, ctx->stream));
+            HIPCHK(ctx, hipEventRecord(ctx->stm_ev[k], ctx->stream));
+        }
+        ctx->stm_pieces = k;
+        ctx->stm_piece = piece;
+        ctx->stm_total = total;
+        return HM_OK;
+    }
     // (in 128-MiB pieces: a checkpoint writer's export copies on copy_stream interleave with them instead of queueing
     // behind one 3.7-GB copy -- the state file's disk writes then start while the statements are still landing)
     constexpr int64_t PIECE = int64_t(128) << 20;
@@ -51,6 +76,17 @@ static int statements_out(hm_ctx *ctx, int64_t n, int64_t total, int32_t out_mem
     HIPCHK(ctx, ctx_sync(ctx, __LINE__));
     *bytes = (const uint8_t *)ctx->h_td_bytes;
     *offsets = (const int64_t *)ctx->h_td_off;
+    return HM_OK;
+}
+
+int hm_statements_wait(hm_ctx *ctx, int64_t upto) {
+    if (!ctx || upto < 0) return ctx ? set_err(ctx, HM_E_INVALID, "bad argument") : HM_E_INVALID;
+    const int pieces = ctx->stm_pieces;
+    if (!pieces) return upto == 0 ? HM_OK : set_err(ctx, HM_E_STATE, "hm_statements_wait without a streamed encode");
+    if (upto > ctx->stm_total) return set_err(ctx, HM_E_INVALID, "%lld bytes of %lld", (long long)upto, (long long)ctx->stm_total);
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int last = (int)std::min<int64_t>((upto + ctx->stm_piece - 1) / ctx->stm_piece, pieces);
+    for (int k = 0; k < last; k++) HIPCHK(ctx, hipEventSynchronize(ctx->stm_ev[k]));
     return HM_OK;
 }
 

@@ -76,6 +76,10 @@ struct hm_ctx {
     int64_t touched_dump_n = 0;
     int64_t export_dump_n = -1;       // hm_state_export_begin: records of the dump in parts_regrow (-1: none) ...
     unsigned long long export_dump_seq = 0;   // ... made after batch seq (hm_state_export_copy checks both)
+    static constexpr int STM_PIECES = 64;
+    hipEvent_t stm_ev[STM_PIECES] = {};   // HM_MEM_HOST_STREAM statements: piece k of the bytes landed
+    int stm_pieces = 0;                   // pieces of the last streamed encode (0: none pending)
+    int64_t stm_piece = 0, stm_total = 0;
     static constexpr int EXPORT_SLICES = 64;
     hipEvent_t export_ev[EXPORT_SLICES] = {};   // hm_state_export_copy_async: slice k landed
     DevBuf parts_regrow_sorted;       // growth: the same, partitioned (not parts_sorted: a binned batch's slabs are there)

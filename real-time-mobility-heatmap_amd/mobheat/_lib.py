@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get("MOBHEAT_LIB") or os.path.normpath(os.path.join(_HERE,
 HM_ABI_VERSION = 11
 HM_MEM_HOST = 0
 HM_MEM_DEVICE = 1
+HM_MEM_HOST_STREAM = 2
 HM_JSON_SPLICE = 1
 HM_E_INVALID, HM_E_HIP, HM_E_NOMEM, HM_E_OVERFLOW, HM_E_STATE, HM_E_UNSUPPORTED = -1, -2, -3, -4, -5, -6
 HM_STAGE_SUMMARY_WORDS = 8200
@@ -138,6 +139,7 @@ SIGNATURES = {
     "hm_selftest_tile_statements": (c_i32, [_P(HmTileDocCfg), c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_i64, c_vp, c_i64, c_vp]),
     "hm_encode_position_updates": (c_i32, [c_vp, _P(HmPositionDocCfg), c_i32, _P(c_vp), _P(c_vp), _P(c_i64)]),
+    "hm_statements_wait": (c_i32, [c_vp, c_i64]),
     "hm_selftest_position_statements": (c_i32, [_P(HmPositionDocCfg), c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64,
                                                 c_vp]),
     "hm_last_timings": (c_i32, [c_vp, c_vp, c_i32]),

@@ -11,7 +11,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import (HM_JSON_SPLICE, HM_MEM_DEVICE, HM_MEM_HOST, STATE_REC_DTYPE, HmArrowIn, HmBatchIn, HmBatchOut, HmConfig,
+from ._lib import (HM_JSON_SPLICE, HM_MEM_DEVICE, HM_MEM_HOST, HM_MEM_HOST_STREAM, STATE_REC_DTYPE, HmArrowIn, HmBatchIn, HmBatchOut, HmConfig,
                    HmJsonIn, HmJsonOut, HmStateInfo, check, ptr)
 
 _INFO_FIELDS = [f for f, _ in HmStateInfo._fields_ if f != "reserved"]
@@ -341,6 +341,37 @@ class HeatmapEngine:
         return info
 
     # ---- tiles as MongoDB update statements, BSON-encoded on the GPU (reference heatmap_stream.py:164-196) ----
+    def encode_tile_updates_streamed(self, city, ttl_minutes):
+        """encode_tile_updates with HM_MEM_HOST_STREAM: (bytes, offsets, landed) -- the offsets are there, the bytes
+        land in pieces after the call; landed(upto) blocks until bytes[:upto] have (hm_statements_wait).  The sink
+        sends each command once its statements have landed (mobheat.stream._flush_statements)."""
+        return self._encode_tiles(city, ttl_minutes, HM_MEM_HOST_STREAM)
+
+    def encode_position_updates_streamed(self, provider_uniques, vehicle_uniques):
+        """encode_position_updates with HM_MEM_HOST_STREAM: (bytes, offsets, landed), as encode_tile_updates_streamed."""
+        bucket_ids = self.latest_buckets()
+        cfg, keep = _lib.position_doc_cfg(provider_uniques, vehicle_uniques, None, bucket_ids=bucket_ids)
+        pb, po, nd = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+        check(self._lib.hm_encode_position_updates(self._ctx, ctypes.byref(cfg), HM_MEM_HOST_STREAM, ctypes.byref(pb),
+                                                   ctypes.byref(po), ctypes.byref(nd)), self._ctx,
+              "hm_encode_position_updates")
+        return _host_statements(pb, po, nd, False) + (self._landed,)
+
+    def _landed(self, upto):
+        check(self._lib.hm_statements_wait(self._ctx, int(upto)), self._ctx, "hm_statements_wait")
+
+    def _encode_tiles(self, city, ttl_minutes, memory):
+        n = ctypes.c_int64()
+        check(self._lib.hm_last_windows(self._ctx, None, 0, ctypes.byref(n)), self._ctx, "hm_last_windows")
+        wins = np.zeros(n.value, np.int64)
+        if wins.size:
+            check(self._lib.hm_last_windows(self._ctx, ptr(wins), wins.size, ctypes.byref(n)), self._ctx, "hm_last_windows")
+        cfg, keep = _lib.tile_doc_cfg(city, ttl_minutes, wins, self.tile_us)
+        pb, po, nd = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+        check(self._lib.hm_encode_tile_updates(self._ctx, ctypes.byref(cfg), memory, ctypes.byref(pb),
+                                               ctypes.byref(po), ctypes.byref(nd)), self._ctx, "hm_encode_tile_updates")
+        return _host_statements(pb, po, nd, False) + (self._landed,)
+
     def encode_tile_updates(self, city, ttl_minutes, copy=False):
         """The last batch's tiles as the `update` statements pymongo would send for the reference's UpdateOne ops:
         (bytes uint8, offsets int64[n+1]); statement i = bytes[offsets[i]:offsets[i+1]].  Views of the library's

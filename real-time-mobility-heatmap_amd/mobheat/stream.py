@@ -228,11 +228,14 @@ class MongoSink:
     def bulk_write(self, collection, ops):
         self._pymongo_db()[collection].bulk_write(ops, ordered=False)
 
-    def update_statements(self, collection, buf, offs):
-        """Pre-encoded update statements (bytes buf, offsets[n+1]) in unordered commands of <= BULK_CHUNK."""
+    def update_statements(self, collection, buf, offs, landed=None):
+        """Pre-encoded update statements (bytes buf, offsets[n+1]) in unordered commands of <= BULK_CHUNK; landed as
+        wire.WireSink.update_statements (the wire path sends each command as its bytes land)."""
         if self._wire is not None:
-            self._wire.update_statements(collection, buf, offs)
+            self._wire.update_statements(collection, buf, offs, landed)
             return
+        if landed is not None:
+            landed(int(offs[-1]) if len(offs) else 0)
         from bson.raw_bson import RawBSONDocument
         from . import wire
         o = np.asarray(offs, dtype=np.int64)
@@ -700,18 +703,41 @@ def _flush(sink, collection, ops):
         sink.bulk_write(collection, ops[i:i + BULK_CHUNK])
 
 
-def _flush_statements(sink, collection, buf, offs):
+def _flush_statements(sink, collection, buf, offs, landed=None):
     """Pre-encoded update statements (hm_encode_tile_updates / hm_encode_position_updates) in unordered batches of
     BULK_CHUNK (:191-196, :230-235): the sink's update_statements when it has one (MongoSink), else one update_raw
-    per chunk (capture sinks in the tests)."""
+    per chunk (capture sinks in the tests).  landed (a streamed encode's hm_statements_wait): handed to a sink whose
+    update_statements takes it (it sends each command as its statements land), else waited for in full first."""
+    if landed is not None and not _takes_landed(sink):
+        landed(int(offs[-1]) if len(offs) else 0)
+        landed = None
     if hasattr(sink, "update_statements"):
-        sink.update_statements(collection, buf, offs)
+        if landed is not None:
+            sink.update_statements(collection, buf, offs, landed=landed)
+        else:
+            sink.update_statements(collection, buf, offs)
         return
     from bson.raw_bson import RawBSONDocument
     o = offs.tolist()
     for i in range(0, len(o) - 1, BULK_CHUNK):
         j = min(i + BULK_CHUNK, len(o) - 1)
         sink.update_raw(collection, [RawBSONDocument(buf[o[k]:o[k + 1]].tobytes()) for k in range(i, j)])
+
+
+def _encode(eng, name, *args):
+    """eng.<name>_streamed(*args) -> (bytes, offsets, landed); an engine without the streamed form (the tests' stand-ins):
+    eng.<name>(*args) with landed None."""
+    f = getattr(eng, name + "_streamed", None)
+    return f(*args) if f is not None else getattr(eng, name)(*args) + (None,)
+
+
+def _takes_landed(sink):
+    import inspect
+    f = getattr(sink, "update_statements", None)
+    try:
+        return f is not None and "landed" in inspect.signature(f).parameters
+    except (TypeError, ValueError):
+        return False
 
 
 # ------------------ the drop-in boundary ------------------
@@ -866,15 +892,17 @@ def foreach_batch_func(df, epoch_id: int):
     sink = SINK_FACTORY()
     try:
         # ---- 1) Upsert tiles (TTL via staleAt): the UpdateOne statements, BSON-encoded on the GPU ----
-        buf, offs = eng.encode_tile_updates(CITY, TTL_MIN)
+        # (streamed: the statements' bytes land in pieces while the sink sends the commands that have landed)
+        buf, offs, landed = _encode(eng, "encode_tile_updates", CITY, TTL_MIN)
         lap("encode")
-        _flush_statements(sink, "tiles", buf, offs)
+        _flush_statements(sink, "tiles", buf, offs, landed)
         lap("sink")
         # ---- 2) latest per (provider, vehicleId) within this micro-batch: statements encoded on the GPU ----
         if res.n_latest:
-            buf, offs = eng.encode_position_updates(*dicts)   # (local offsets of the rows' 900-s buckets)
+            # (local offsets of the rows' 900-s buckets)
+            buf, offs, landed = _encode(eng, "encode_position_updates", *dicts)
             lap("encode")
-            _flush_statements(sink, "positions_latest", buf, offs)
+            _flush_statements(sink, "positions_latest", buf, offs, landed)
             lap("sink")
     finally:
         sink.close()

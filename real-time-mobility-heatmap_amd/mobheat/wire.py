@@ -124,12 +124,15 @@ class WireMongoSink:
                 parts[0] = memoryview(parts[0])[k:]
         return self._reply(rid)
 
-    def update_statements(self, collection, buf, offsets):
+    def update_statements(self, collection, buf, offsets, landed=None):
         """All statements (buf, offsets[n+1]) in unordered commands of <= BULK_CHUNK statements; write errors raise
-        pymongo's BulkWriteError like the reference's bulk_write."""
+        pymongo's BulkWriteError like the reference's bulk_write.  landed(upto): the statements are still landing in
+        buf (a streamed encode) -- each command is sent once bytes[:its end] are there."""
         offs = np.asarray(offsets, dtype=np.int64)
         base = int(offs[0]) if offs.size else 0
         for i, j in chunks(offs, MAX_MESSAGE_BYTES - 16 * 1024):
+            if landed is not None:
+                landed(int(offs[j]))
             res = self.send_statements(collection, buf, int(offs[i]) - base, int(offs[j]) - base, j - i)
             raise_write_errors(res)
 

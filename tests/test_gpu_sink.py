@@ -89,6 +89,49 @@ def test_large_batch_statements_and_device_copy():
     del ctypes
 
 
+def test_streamed_statements_land_in_pieces_and_feed_the_wire_sink():
+    """HM_MEM_HOST_STREAM (hm_statements_wait): the offsets are there when the encode returns, the bytes land in pieces
+    (>= 32 MiB, at most 64) -- after landed(offs[k]) statements [0, k) equal the synchronous encode's; a wait past the
+    end or without a streamed encode is refused; a sink fed command by command as they land (wire.WireMongoSink, each
+    command's bytes captured as send_statements is called) sends the synchronous encode's bytes."""
+    from mobheat import HeatmapEngine
+    rng = np.random.default_rng(44)
+    n = 1_500_000
+    eng = HeatmapEngine(h3_res=9)
+    eng.process_batch(0, lat=np.degrees(np.arcsin(rng.uniform(-1, 1, n))), lon=rng.uniform(-180, 180, n),
+                      ts_us=1759572000_000_000 + rng.integers(0, 15 * 60_000_000, n), speed=rng.uniform(0, 80, n),
+                      speed_valid=rng.random(n) > 0.1, vkey=rng.integers(0, 50000, n).astype(np.uint64))
+    ref_buf, ref_offs = eng.encode_tile_updates("ath", 45, copy=True)
+    assert ref_buf.size > (64 << 20)   # (several pieces)
+    buf, offs, landed = eng.encode_tile_updates_streamed("ath", 45)
+    np.testing.assert_array_equal(offs, ref_offs)
+    seen = []
+    for k in np.linspace(0, offs.size - 1, 9).astype(int)[1:]:
+        landed(int(offs[k]))
+        seen.append(buf[: offs[k]].tobytes() == ref_buf[: ref_offs[k]].tobytes())
+    assert all(seen)
+    with pytest.raises(RuntimeError, match="bytes of"):
+        landed(int(offs[-1]) + 1)
+    # the wire sink, command by command: each command's bytes as send_statements sees them when it is called
+    from mobheat import wire
+
+    class Capture(wire.WireMongoSink):
+        def __init__(self):
+            self.sent = []
+
+        def send_statements(self, collection, buf, lo, hi, n_statements, write_concern=None):
+            self.sent.append(bytes(buf[lo:hi]))
+            return {"ok": 1.0, "n": n_statements}
+    buf, offs, landed = eng.encode_tile_updates_streamed("ath", 45)
+    sink = Capture()
+    sink.update_statements("tiles", buf, offs, landed=landed)
+    assert len(sink.sent) > 10 and b"".join(sink.sent) == ref_buf.tobytes()
+    eng.encode_tile_updates("ath", 45)   # (synchronous: nothing left to wait for)
+    with pytest.raises(RuntimeError, match="without a streamed encode"):
+        landed(1)
+    eng.close()
+
+
 def test_empty_batch_and_errors():
     from mobheat import HeatmapEngine
     eng = HeatmapEngine(h3_res=8)
