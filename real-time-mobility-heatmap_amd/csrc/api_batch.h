@@ -112,6 +112,7 @@ int hm_create(const hm_config *cfg, hm_ctx **out) {
     if (const char *m = getenv("MOBHEAT_OFFSETS_EARLY")) ctx->offsets_early = strcmp(m, "0") != 0;
     if (const char *m = getenv("MOBHEAT_STAGE_SELF")) ctx->self_hold_ok = strcmp(m, "copy") != 0;
     if (const char *m = getenv("MOBHEAT_DEDUP_DENSE")) ctx->dense_ok = strcmp(m, "0") != 0;
+    if (const char *m = getenv("MOBHEAT_COOP_PREDICT")) ctx->coop_predict = strcmp(m, "0") != 0;
     if (const char *m = getenv("MOBHEAT_SUBBINS")) ctx->subbins_mode = !strcmp(m, "0") ? 0 : !strcmp(m, "1") ? 1 : 2;
     // MOBHEAT_PIPELINE: unset / 0 never pipelines a batch (the default: slower on the bench, host_pipe.h), K >= 2
     // pipelines every binned batch in K chunks (tests, A/B), "auto": batches of >= PIPE_MIN_ROWS rows in PIPE_CHUNKS chunks

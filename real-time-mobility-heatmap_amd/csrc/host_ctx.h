@@ -114,6 +114,7 @@ struct hm_ctx {
     int merge_grid = 0;
     int64_t prev_agg_rows = 0, prev_keys = 0;   // aggregated rows and distinct keys of the last batch
     bool merge_coop = false;   // the last batch's keys were mostly existing ones: the merge's cooperative probe
+    bool coop_predict = true;  // MOBHEAT_COOP_PREDICT=0: the merge variant from the last batch (merge_coop) alone
     bool last_table = false;
     int64_t last_counts[6] = {0, 0, 0, 0, 0, 0};   // hm_last_counts [0, 6) ([6], [7]: n_allocs, n_frees)
     int64_t n_allocs = 0, n_frees = 0;             // device + pinned-host allocations / frees since create
@@ -668,6 +669,16 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t sla
     if (seg.nseg > 0) HIPCHK(ctx, hipMemcpyToSymbolAsync(HIP_SYMBOL(g_seg_bounds), &seg.bounds, sizeof(SegBounds), 0,
                                                          hipMemcpyHostToDevice, ctx->stream));
 #endif
+    // the cooperative probe (re-touched keys: old lines read) when this batch's windows already hold keys for most of
+    // its records -- known here from the census and the tables, where the last batch's ratio (merge_coop) mispredicts
+    // the batch after a window opened (all new keys, then all re-touched: 6.8-ms merges, profiles/r5/r5headprof)
+    bool coop = ctx->merge_coop;
+    if (!rehash && ctx->coop_predict) {
+        int64_t old = 0, parts = 0;
+        for (const auto &g : ctx->gens)
+            if (g.batch_parts) { parts += g.batch_parts; old += std::min(g.keys, g.batch_parts); }
+        coop = parts > 0 && 2 * old > parts;
+    }
     auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(grid), dim3(MO_THREADS), tag_bytes, ctx->stream, src ? src : (const Rec *)ctx->parts_sorted.p, slab,
                            seg.SO, seg.SP, seg.nseg,
@@ -677,7 +688,7 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t sla
     };
     if constexpr (std::is_same<Rec, EventRec>::value) {
         if (seg.nseg > 0) {   // (the multi-GPU owner)
-            if (resident && ctx->merge_coop) launch(k_merge_owned<Rec, true, true, true>);
+            if (resident && coop) launch(k_merge_owned<Rec, true, true, true>);
             else if (resident) launch(k_merge_owned<Rec, true, false, true>);
             else launch(k_merge_owned<Rec, false, false, true>);
             HIPCHK(ctx, hipGetLastError());
@@ -685,7 +696,7 @@ static int merge_sorted(hm_ctx *ctx, int64_t n_rows, int64_t ntiles, int64_t sla
         }
     }
     if constexpr (!rehash) {
-        if (resident && ctx->merge_coop) launch(k_merge_owned<Rec, true, true>);
+        if (resident && coop) launch(k_merge_owned<Rec, true, true>);
         else if (resident) launch(k_merge_owned<Rec, true>);
         else launch(k_merge_owned<Rec, false>);
     } else {
