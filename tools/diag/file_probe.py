@@ -62,35 +62,35 @@ def main():
         pn[:] = np.frombuffer(raw, np.uint8)
         bufs["pinned"] = memoryview(pn)
     for rep in range(a.reps):
-      for src, buf in bufs.items():
-        for mode, threads in (("write", 1), ("pwrite", 4), ("direct", 1), ("direct", 4)):
-            flags = os.O_WRONLY | os.O_CREAT | os.O_TRUNC
-            if mode == "direct":
-                flags |= getattr(os, "O_DIRECT", 0)
-            try:
-                fd = os.open(path, flags, 0o644)
-            except OSError as e:
-                print(json.dumps({"mode": mode, "threads": threads, "error": repr(e)}), flush=True)
-                continue
-            try:
-                t0 = time.perf_counter()
-                if mode == "write":
-                    done = 0
-                    while done < nbytes:
-                        done += os.write(fd, buf[done:])
-                else:
-                    pwrite_threads(fd, buf, threads)
-                t1 = time.perf_counter()
-                os.fsync(fd)
-                t2 = time.perf_counter()
-                print(json.dumps({"rep": rep, "src": src, "mode": mode, "threads": threads, "write_ms": round(1e3 * (t1 - t0), 1),
-                                  "fsync_ms": round(1e3 * (t2 - t1), 1), "GBps": round(nbytes / (t2 - t0) / 1e9, 2)}),
-                      flush=True)
-            except OSError as e:
-                print(json.dumps({"mode": mode, "threads": threads, "error": repr(e)}), flush=True)
-            finally:
-                os.close(fd)
-                os.remove(path)
+        for src, buf in bufs.items():
+            for mode, threads in (("write", 1), ("pwrite", 4), ("direct", 1), ("direct", 4)):
+                flags = os.O_WRONLY | os.O_CREAT | os.O_TRUNC
+                if mode == "direct":
+                    flags |= getattr(os, "O_DIRECT", 0)
+                try:
+                    fd = os.open(path, flags, 0o644)
+                except OSError as e:
+                    print(json.dumps({"mode": mode, "threads": threads, "error": repr(e)}), flush=True)
+                    continue
+                try:
+                    t0 = time.perf_counter()
+                    if mode == "write":
+                        done = 0
+                        while done < nbytes:
+                            done += os.write(fd, buf[done:])
+                    else:
+                        pwrite_threads(fd, buf, threads)
+                    t1 = time.perf_counter()
+                    os.fsync(fd)
+                    t2 = time.perf_counter()
+                    print(json.dumps({"rep": rep, "src": src, "mode": mode, "threads": threads, "write_ms": round(1e3 * (t1 - t0), 1),
+                                      "fsync_ms": round(1e3 * (t2 - t1), 1), "GBps": round(nbytes / (t2 - t0) / 1e9, 2)}),
+                          flush=True)
+                except OSError as e:
+                    print(json.dumps({"mode": mode, "threads": threads, "error": repr(e)}), flush=True)
+                finally:
+                    os.close(fd)
+                    os.remove(path)
 
 
 if __name__ == "__main__":
