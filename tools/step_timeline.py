@@ -7,9 +7,14 @@ import csv
 import sys
 
 
+def _is_ingest(name):   # (k_ingest<...> / k_ingest(...), not k_ingest_exact)
+    name = name[5:] if name.startswith("void ") else name
+    return name.startswith("k_ingest<") or name.startswith("k_ingest(")
+
+
 def main(path, k):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_ingest(")]
+    idx = [i for i, r in enumerate(rows) if _is_ingest(r["Kernel_Name"])]
     i0, i1 = idx[k], idx[k + 1]
     t0 = int(rows[i0]["Start_Timestamp"])
     prev_end = None
