@@ -70,27 +70,54 @@ __global__ __launch_bounds__(256) void k_dict_insert(const uint8_t *__restrict__
                                                      int64_t n, DictSlot *tab, unsigned long long mask, uint64_t seed,
                                                      unsigned *__restrict__ slot_of, unsigned long long *overflow) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const int32_t L = len[i];
-        if (L < 0) { slot_of[i] = ~0u; continue; }
-        const uint64_t h = str_hash(span_ptr(bytes, scratch, off[i]), L, seed);
-        unsigned long long s = mix64(h ^ seed) & mask;
+    // this lane's last string and its slot: a later row of the same string (a higher row index: its representative is
+    // already at most the earlier one's) takes the slot without touching the table
+    uint64_t last_h = DICT_EMPTY;
+    unsigned last_s = ~0u;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+        const int64_t i = base + threadIdx.x;
+        const int32_t L = i < n ? len[i] : -1;
+        const bool live = L >= 0;
+        const uint64_t h = live ? str_hash(span_ptr(bytes, scratch, off[i]), L, seed) : 0;
+        // the lanes holding the same string as the wave's first live lane take the slot that lane finds: one probe and
+        // one representative update per wave for a column of few distinct values (a batch's one provider string put
+        // every lane's CAS on one address: 4.7 ms of hm_arrow_columns per 1e7 rows, profiles/r6/r6p)
+        const unsigned long long m = __ballot(live);
+        const int leader = m ? __ffsll((long long)m) - 1 : 0;
+        const bool follower = live && lane_id() != leader && h == __shfl(h, leader, 64);
         unsigned got = ~0u;
-        for (int p = 0; p < DICT_PROBES; p++) {
-            unsigned long long k = __hip_atomic_load(&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (k == DICT_EMPTY) k = atomicCAS(&tab[s].key, DICT_EMPTY, (unsigned long long)h);
-            if (k == DICT_EMPTY || k == h) {
-                // (the representative only moves down: a row above it adds nothing -- a batch's one provider string
-                // would otherwise put every row's atomic on one address)
-                if ((unsigned)i < __hip_atomic_load(&tab[s].rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                    atomicMin(&tab[s].rep, (unsigned)i);
-                got = (unsigned)s;
-                break;
+        if (live && !follower && h == last_h) {
+            got = last_s;
+        } else if (live && !follower) {
+            unsigned long long s = mix64(h ^ seed) & mask;
+            for (int p = 0; p < DICT_PROBES; p++) {
+                // (plain loads: a slot's key never changes once set, so a key read equal to h is final and a stale
+                // EMPTY only costs the CAS that returns the real one; a stale representative only an atomicMin that
+                // changes nothing)
+                unsigned long long k = tab[s].key;
+                // (an EMPTY from the CU's cache may be stale: read the L2's before the CAS -- a CAS from every wave
+                // of the first grid pass on a single-valued column's one slot serialised there, 2.3 ms per 1e7 rows)
+                if (k == DICT_EMPTY) k = __hip_atomic_load(&tab[s].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (k == DICT_EMPTY) k = atomicCAS(&tab[s].key, DICT_EMPTY, (unsigned long long)h);
+                if (k == DICT_EMPTY || k == h) {
+                    // (the representative only moves down: a row above it adds nothing -- the leader's row is the
+                    // lowest of its followers')
+                    // (the L2's value before the atomicMin: a stale cached one sent every first-pass wave's atomicMin
+                    // to the one slot, 1.6-2.2 ms per 1e7 rows)
+                    if ((unsigned)i < tab[s].rep &&
+                        (unsigned)i < __hip_atomic_load(&tab[s].rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        atomicMin(&tab[s].rep, (unsigned)i);
+                    got = (unsigned)s;
+                    break;
+                }
+                s = (s + 1) & mask;
             }
-            s = (s + 1) & mask;
+            if (got != ~0u) { last_h = h; last_s = got; }
         }
-        slot_of[i] = got;
-        if (got == ~0u) atomicAdd(overflow, 1ull);
+        const unsigned lead_got = __shfl(got, leader, 64);
+        if (follower) got = lead_got;
+        if (i < n) slot_of[i] = got;
+        if (live && got == ~0u) atomicAdd(overflow, 1ull);
     }
 }
 // every row's bytes against its slot's representative: a mismatch is a 64-bit hash collision
