@@ -41,6 +41,12 @@ static int dict_build(hm_ctx *ctx, hm_ctx::Dict &d, const uint8_t *bytes, const 
             return rc;
         HIPCHK(ctx, hipMemsetAsync(d.tab.p, 0xff, cap * sizeof(DictSlot), ctx->stream));
         HIPCHK(ctx, hipMemsetAsync(words, 0, 16, ctx->stream));
+        // the first rows' strings first, by one workgroup: the frequent strings of a column (a batch's one provider)
+        // are then in the table, written back, when the full launch starts, so that its waves find them with plain
+        // loads -- each XCD's L2 otherwise served its waves a stale empty slot and every wave of the first grid pass
+        // re-read the slot past it (agent scope) and raced for it (1.6-2.1 ms per 1e7 rows; with this, 38 + 89 us: profiles/r6/r6p/dict_kernels.txt)
+        hipLaunchKernelGGL(k_dict_insert, dim3(1), dim3(256), 0, ctx->stream, bytes, scratch, off, len,
+                           std::min<int64_t>(n, 4096), (DictSlot *)d.tab.p, cap - 1, seed, (unsigned *)d.slot_of.p, words);
         hipLaunchKernelGGL(k_dict_insert, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, bytes, scratch, off, len, n,
                            (DictSlot *)d.tab.p, cap - 1, seed, (unsigned *)d.slot_of.p, words);
         hipLaunchKernelGGL(k_dict_verify, dim3(grid_for(n, 256)), dim3(256), 0, ctx->stream, bytes, scratch, off, len, n,
